@@ -1,0 +1,229 @@
+/*
+ * kwok_engine.h — C ABI of the MI355X Stage-lifecycle engine.
+ *
+ * This is the device boundary a Go host binds through cgo.  It replaces,
+ * for one resource kind, the per-object work the reference does between the informer event
+ * and the client-go PATCH:
+ *
+ *   reference seam (Go)                                   replaced by
+ *   ----------------------------------------------------  --------------------------------
+ *   lifecycle.NewLifecycle / NewStage                     kwk_load_stages (host-compiled
+ *     pkg/utils/lifecycle/lifecycle.go:33-46,194-267        table; explicit stage order)
+ *   PodController.preprocess -> Lifecycle.Match,          kwk_step (fused sweep kernel:
+ *     Stage.Delay, addStageJob                              match, weighted pick, delay +
+ *     pkg/kwok/controllers/pod_controller.go:196-254        jitter, schedule, fire, delta)
+ *     pkg/utils/lifecycle/lifecycle.go:125-191,313-341
+ *     pkg/utils/queue/weight_delaying_queue.go:73-174
+ *   (node: node_controller.go:262-319; generic: stage_controller.go:174-232)
+ *   playStage's state change (finalizers, delete,         applied on device as delta ops;
+ *     patches) pod_controller.go:290-360,                   the fired list (kwk_fired) is
+ *     pkg/utils/lifecycle/next.go:43-88,                    what Go renders text patches for
+ *     pkg/utils/lifecycle/finalizers.go:83-111
+ *   informer Added/Modified events -> preprocessChan      kwk_load / kwk_upsert (pre-interned
+ *     pod_controller.go:412-478                             SoA columns; marks objects dirty)
+ *   Deleted events                                        kwk_delete
+ *   server/metrics_resource_usage.go:170-224              kwk_usage (per-node segmented sums)
+ *     (podResourceUsage / nodeResourceUsage and the
+ *      *CumulativeUsage integrators :36-109)
+ *
+ * Conventions: every function returns kwk_status (0 = ok, < 0 = error; message via
+ * kwk_last_error).  No exceptions or panics cross the boundary.  Strings never cross it:
+ * the host interns labels / annotations / phases / finalizers into feature bits and
+ * pre-parses *From values.  All calls for one engine come from one thread (the reference
+ * runs all matching for a kind on a single preprocess goroutine, pod_controller.go:150).
+ * kwk_step and kwk_usage only enqueue work on the engine's HIP stream; the read functions
+ * synchronise that stream.
+ */
+#ifndef KWOK_ENGINE_H
+#define KWOK_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t kwk_status;
+#define KWK_OK 0
+#define KWK_EINVAL (-1)   /* bad argument / shape mismatch */
+#define KWK_ECAP (-2)     /* capacity exceeded */
+#define KWK_EHIP (-3)     /* HIP runtime error */
+#define KWK_ESTATE (-4)   /* call order (e.g. step before load_stages) */
+
+typedef struct kwk_engine kwk_engine;
+
+/* ------------------------------------------------------------------ object hot record */
+/* sched word layout */
+#define KWK_STAGE_NONE 0xFFu          /* bits 0..7: pending stage index */
+#define KWK_F_ALIVE (1u << 8)         /* object exists */
+#define KWK_F_DIRTY (1u << 9)         /* changed since last match: re-match this step */
+#define KWK_F_MANAGED (1u << 10)      /* pod on a managed node / node managed by this kwok */
+#define KWK_F_HASREC (1u << 11)       /* has a value record (pre-parsed *From results) */
+#define KWK_F_MATCHERR (1u << 12)     /* last match hit a Go panic path (Int63n(<0)) */
+#define KWK_GEN_SHIFT 16              /* bits 16..31: generation (bumped on re-create) */
+
+typedef struct {
+  uint32_t pred;   /* feature bits (host-compiled predicate summary) */
+  uint32_t sched;  /* pending stage | flags | generation */
+  int64_t due;     /* unix ns at which the pending stage fires */
+} kwk_hot;         /* 16 bytes, one per object slot */
+
+/* value record entry (one per value slot of a record) */
+#define KWK_V_DEFAULT 0  /* query produced no output: use the stage's default value */
+#define KWK_V_OK 1       /* value = int64 (weight) or duration ns */
+#define KWK_V_NOTOK 2    /* getter returns (0, false) */
+#define KWK_V_ABSTIME 3  /* RFC3339 time: value = unix seconds, nsec = nanoseconds; result = t - now */
+typedef struct {
+  int64_t value;
+  int32_t nsec;
+  int32_t kind;
+} kwk_value; /* 16 bytes */
+
+#define KWK_DEL_ABSENT INT64_MIN   /* deletion_s column: no deletionTimestamp */
+
+/* ------------------------------------------------------------------ stage table */
+#define KWK_MAX_STAGES 32
+#define KWK_MAX_ANY 4
+#define KWK_SLOT_NONE (-1)         /* getter has no *From query: constant default */
+#define KWK_SLOT_DELETION (-2)     /* duration getter on .metadata.deletionTimestamp (column) */
+
+#define KWK_NEXT_DELETE (1u << 0)
+#define KWK_NEXT_IMMEDIATE (1u << 1)
+#define KWK_NEXT_PATCHES (1u << 2)     /* has rendered patches: a fire always re-matches */
+#define KWK_NEXT_FIN (1u << 3)         /* has a finalizers op */
+#define KWK_NEXT_FIN_EMPTY (1u << 4)   /* finalizers.empty */
+#define KWK_NEXT_FIN_REMOVE (1u << 5)  /* finalizers.remove non-empty */
+
+typedef struct {
+  /* selector: ((pred ^ eq_val) & eq_mask) == 0  AND  for k < n_any:
+   *           ((pred & any_mask[k]) != 0) == ((any_want >> k) & 1) */
+  uint32_t eq_mask, eq_val;
+  uint32_t n_any, any_want;
+  uint32_t any_mask[KWK_MAX_ANY];
+  /* weight getter: IntFrom(&Spec.Weight, weightFrom) — always has a default */
+  int64_t weight_default;
+  int32_t weight_slot;
+  /* delay getters (Stage.Delay) */
+  int32_t has_delay;
+  int64_t delay_default;       /* durationMilliseconds (or 0) in ns; always ok when has_delay */
+  int32_t delay_slot;
+  int32_t has_jitter;
+  int64_t jitter_default;
+  int32_t jitter_default_ok;   /* jitterDurationMilliseconds present */
+  int32_t jitter_slot;
+  /* next */
+  uint32_t flags;              /* KWK_NEXT_* */
+  uint32_t fin_add, fin_remove;/* bits inside the table's fin_group_mask */
+  uint32_t pad;
+} kwk_stage_desc;
+
+typedef struct {
+  uint32_t n_stages;
+  uint32_t fin_group_mask;     /* pred bits forming the object's finalizer set */
+  uint32_t n_classes;          /* delta table is [n_classes][n_stages] */
+  uint32_t version;
+  kwk_stage_desc stages[KWK_MAX_STAGES];
+} kwk_stage_table;
+
+typedef struct {               /* next-state delta of (object class, stage) */
+  uint32_t and_mask, or_mask;  /* pred' = (pred & and_mask) | or_mask (outside fin group) */
+} kwk_delta;
+#define KWK_DELTA_UNKNOWN_AND 0u  /* and_mask 0 with or_mask 0xFFFFFFFF: not derivable -> host */
+#define KWK_DELTA_UNKNOWN_OR 0xFFFFFFFFu
+
+/* ------------------------------------------------------------------ workload harness */
+/* Optional device-side churn (simulates the user/apiserver side of a steady-state
+ * cluster; bench and parity tests only):
+ *   dead object            -> re-created: pred = pred & keep_mask, gen+1, dirty
+ *   alive, (pred & terminal_mask) != 0, deletion bit clear
+ *                          -> deletionTimestamp = now (second precision), dirty      */
+typedef struct {
+  uint32_t enable;
+  uint32_t keep_mask;
+  uint32_t terminal_mask;
+  uint32_t deletion_bit;
+} kwk_harness;
+
+/* ------------------------------------------------------------------ fired records */
+#define KWK_FIRED_DELETED (1u << 0)
+#define KWK_FIRED_REMATCH (1u << 1)
+#define KWK_FIRED_DELTA_UNKNOWN (1u << 2)
+typedef struct {
+  uint32_t slot;   /* local object slot */
+  uint16_t stage;  /* stage index in the loaded table */
+  uint16_t flags;  /* KWK_FIRED_* */
+} kwk_fired_rec;
+
+typedef struct {
+  uint64_t steps;
+  uint64_t matched;       /* objects (re)scheduled by a match */
+  uint64_t fired;         /* stage transitions */
+  uint64_t fired_per_stage[KWK_MAX_STAGES];
+} kwk_step_stats;
+
+/* ------------------------------------------------------------------ engine */
+typedef struct {
+  int32_t device;             /* HIP device ordinal */
+  uint32_t capacity;          /* object slots */
+  uint32_t value_slots;       /* kwk_value entries per value record */
+  uint32_t max_records;       /* value records */
+  uint64_t slot_base;         /* global id of local slot 0 (RNG counter; shard invariant) */
+  uint32_t kind_salt;         /* mixed into the RNG key: separate streams per kind */
+  uint32_t reserved;
+} kwk_engine_desc;
+
+const char* kwk_last_error(void);
+kwk_status kwk_engine_create(const kwk_engine_desc* desc, kwk_engine** out);
+kwk_status kwk_engine_destroy(kwk_engine* eng);
+
+/* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */
+kwk_status kwk_load_stages(kwk_engine* eng, const kwk_stage_table* table, const kwk_delta* deltas);
+kwk_status kwk_set_harness(kwk_engine* eng, const kwk_harness* h);
+
+/* bulk column load of slots [0, n) from host arrays (initial list / informer Sync) */
+kwk_status kwk_load(kwk_engine* eng, uint32_t n, const kwk_hot* hot, const int64_t* deletion_s,
+                    const uint32_t* rec_idx, const uint16_t* cls, uint32_t n_records, const kwk_value* records);
+/* per-object upsert (Added / Modified events): scatter into the given slots, marks dirty */
+kwk_status kwk_upsert(kwk_engine* eng, uint32_t n, const uint32_t* slots, const kwk_hot* hot,
+                      const int64_t* deletion_s, const uint32_t* rec_idx, const uint16_t* cls);
+kwk_status kwk_set_records(kwk_engine* eng, uint32_t first, uint32_t n, const kwk_value* records);
+/* Deleted events: clear ALIVE (cancels any pending stage) */
+kwk_status kwk_delete(kwk_engine* eng, uint32_t n, const uint32_t* slots);
+
+/* one reconciliation step at time now_ns over slots [0, n_active):
+ * harness -> match dirty objects -> fire due objects -> apply deltas.
+ * Random draws use Philox4x32-10(key = seed ^ kind_salt, ctr = (slot_base+slot, step, site)). */
+kwk_status kwk_step(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step);
+
+/* fired records of the LAST step, compacted into host memory (synchronises) */
+kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
+/* cumulative counters (synchronises) */
+kwk_status kwk_stats(kwk_engine* eng, kwk_step_stats* out);
+/* read back columns of slots [first, first+n) (synchronises) */
+kwk_status kwk_read(kwk_engine* eng, uint32_t first, uint32_t n, kwk_hot* hot, int64_t* deletion_s);
+kwk_status kwk_sync(kwk_engine* eng);
+
+/* ------------------------------------------------------------------ resource usage */
+/* Pods must be loaded node-sorted: node j owns slots [node_ptr[j], node_ptr[j+1]).
+ * usage_key per pod: bits 0..13 cpu value id, 14..27 memory value id, 28..31 containers
+ * (each container of the pod evaluates to the pod's value, as usage-from-annotation does). */
+kwk_status kwk_usage_config(kwk_engine* eng, uint32_t n_nodes, const uint32_t* node_ptr, const uint32_t* usage_key,
+                            uint32_t n_cpu, const double* cpu_values, uint32_t n_mem, const double* mem_values);
+/* per-node cpu / memory sums and cumulative integrators at now_ns (enqueue only) */
+kwk_status kwk_usage(kwk_engine* eng, int64_t now_ns);
+/* node_out: n_nodes x {cpu, mem, cpu_cumulative, mem_cumulative}; cluster_out: {cpu, mem} */
+kwk_status kwk_usage_read(kwk_engine* eng, double* node_out, double* cluster_out);
+
+/* raw device pointers for in-process consumers (RCCL aggregates, profiling) */
+kwk_status kwk_device_ptrs(kwk_engine* eng, void** hot, void** fired, void** wave_counts);
+
+/* HIP events recorded on the engine's stream (live kernel timing in bench.py) */
+kwk_status kwk_event_record(kwk_engine* eng, uint32_t idx);
+kwk_status kwk_event_elapsed(kwk_engine* eng, uint32_t a, uint32_t b, float* ms);
+uint32_t kwk_abi_version(void);
+uint32_t kwk_tile_objects(void); /* objects per sweep workgroup */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KWOK_ENGINE_H */

@@ -1,0 +1,947 @@
+// MI355X (gfx950) Stage-lifecycle engine: HIP kernels + the C ABI of include/kwok_engine.h.
+//
+// One fused, memory-bound sweep per step over the SoA object table (16-byte hot record per
+// object).  Per object it does, in this order, what the reference does
+// per informer event / per delay-queue pop:
+//   harness churn (bench/parity only)
+//   match      Lifecycle.match  pkg/utils/lifecycle/lifecycle.go:51-63, Stage.match :285-309
+//   pick       Lifecycle.Match  lifecycle.go:125-191 (Philox hook at :157,:163,:175,:180)
+//   delay      Stage.Delay      lifecycle.go:313-341 (Philox hook at :338); getters
+//              expression/value_int_from.go:53-81, value_duration_from.go:53-79
+//   schedule   addStageJob      pod_controller.go:660-671 (one pending job per object; a new
+//              match replaces it; no match leaves the old job queued, pod_controller.go:222-229)
+//   fire       delay queue pop  weight_delaying_queue.go:97-174 (due <= now)
+//   next       playStage        pod_controller.go:290-360: finalizersModify
+//              (finalizers.go:83-111) as bit-set algebra, delete, patches as a per-(class,
+//              stage) delta precompiled on the host.
+// No MFMA: nothing here is a contraction.  The stage table is wave-uniform and is read
+// through the scalar cache (s_load), the per-object record streams through VGPRs with
+// 16-byte loads; fired records are compacted per wave with a ballot into a private
+// per-wave segment (no global atomics in the sweep).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kwok_engine.h"
+
+namespace {
+
+constexpr int kBlock = 256;              // 4 waves of 64
+constexpr int kObjPerThread = 16;
+constexpr int kTile = kBlock * kObjPerThread;   // objects per workgroup
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kWaveSeg = 64 * kObjPerThread;     // fired-record capacity per wave
+constexpr int kStatWords = 2 + KWK_MAX_STAGES;   // matched, fired, fired per stage
+
+thread_local std::string g_err;
+
+kwk_status fail(kwk_status code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(x)                                                                    \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) return fail(KWK_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ Philox4x32-10
+__device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                         uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// rand.Intn / rand.Int63n replacement: floor(u64 * n / 2^64), n > 0
+__device__ __forceinline__ int64_t rng_below(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key, int64_t n) {
+  uint32_t c0 = (uint32_t)gslot, c1 = (uint32_t)step, c2 = (uint32_t)(step >> 32), c3 = site;
+  philox10(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32));
+  const uint64_t u = (uint64_t)c0 | ((uint64_t)c1 << 32);
+  return (int64_t)__umul64hi(u, (uint64_t)n);
+}
+
+constexpr uint32_t kSitePick = 1, kSiteJitter = 2;
+
+__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
+  int64_t r;
+  if (__builtin_add_overflow(a, b, &r)) return b > 0 ? INT64_MAX : INT64_MIN;
+  return r;
+}
+
+// time.Time.Sub for an RFC3339 time (sec, nsec) against now (ns), saturating like Go
+__device__ __forceinline__ int64_t abs_time_sub(int64_t sec, int32_t nsec, int64_t now) {
+  int64_t now_sec = now / 1000000000;
+  int64_t now_ns = now % 1000000000;
+  if (now_ns < 0) { now_ns += 1000000000; now_sec -= 1; }
+  int64_t ds = sec - now_sec;
+  int64_t dn = (int64_t)nsec - now_ns;  // (-1e9, 1e9)
+  if (ds == 0) return dn;
+  // move one second into dn so that ds' and dn' share a sign: overflow of ds'*1e9 then implies
+  // overflow of the total
+  if (ds > 0) { ds -= 1; dn += 1000000000; } else { ds += 1; dn -= 1000000000; }
+  int64_t p, d;
+  if (__builtin_mul_overflow(ds, (int64_t)1000000000, &p)) return ds > 0 ? INT64_MAX : INT64_MIN;
+  if (__builtin_add_overflow(p, dn, &d)) return dn > 0 ? INT64_MAX : INT64_MIN;
+  return d;
+}
+
+struct Getter {   // result of an IntFrom / DurationFrom evaluation
+  int64_t v;
+  bool ok;
+};
+
+// value of a *From getter for one object.  slot: KWK_SLOT_NONE (constant default),
+// KWK_SLOT_DELETION (deletionTimestamp column), or an index into the object's record.
+__device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool def_ok, uint32_t sched,
+                                              const kwk_value* __restrict__ rec, int64_t del_s, int64_t now,
+                                              bool is_duration) {
+  if (slot == KWK_SLOT_NONE) return {def, def_ok};
+  if (slot == KWK_SLOT_DELETION) {
+    if (del_s == KWK_DEL_ABSENT) return {def, def_ok};
+    return {abs_time_sub(del_s, 0, now), true};
+  }
+  if (!(sched & KWK_F_HASREC)) return {def, def_ok};
+  const kwk_value e = rec[slot];
+  switch (e.kind) {
+    case KWK_V_OK: return {e.value, true};
+    case KWK_V_NOTOK: return {0, false};
+    case KWK_V_ABSTIME: return {is_duration ? abs_time_sub(e.value, e.nsec, now) : 0, is_duration};
+    default: return {def, def_ok};
+  }
+}
+
+struct SweepArgs {
+  kwk_hot* __restrict__ hot;
+  int64_t* __restrict__ del_s;
+  const uint32_t* __restrict__ rec_idx;
+  const uint16_t* __restrict__ cls;
+  const kwk_value* __restrict__ values;
+  const kwk_stage_table* __restrict__ table;
+  const kwk_delta* __restrict__ deltas;
+  kwk_fired_rec* __restrict__ fired;
+  uint32_t* __restrict__ wave_counts;
+  unsigned long long* __restrict__ cum;  // [n_blocks][kStatWords]
+  uint32_t n;
+  uint32_t value_slots;
+  uint64_t slot_base;
+  uint64_t key;
+  uint64_t step;
+  int64_t now;
+  kwk_harness harness;
+};
+
+__device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
+  bool ok = ((pred ^ s.eq_val) & s.eq_mask) == 0;
+  for (uint32_t k = 0; k < s.n_any; ++k) ok &= ((pred & s.any_mask[k]) != 0) == (((s.any_want >> k) & 1u) != 0);
+  return ok;
+}
+
+// weight of matched stage s for this object (Stage.Weight)
+__device__ __forceinline__ Getter stage_weight(const kwk_stage_desc& s, uint32_t sched,
+                                               const kwk_value* __restrict__ rec) {
+  return eval_getter(s.weight_slot, s.weight_default, true, sched, rec, KWK_DEL_ABSENT, 0, false);
+}
+
+// n-th (0-based) set bit of m
+__device__ __forceinline__ int nth_bit(uint32_t m, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) m &= m - 1;
+  return __ffs(m) - 1;
+}
+
+__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+  __shared__ unsigned int s_stat[kStatWords];
+  const kwk_stage_table* __restrict__ T = a.table;
+  const uint32_t n_stages = T->n_stages;
+  const uint32_t fin_group = T->fin_group_mask;
+  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t tile_base = (uint64_t)blockIdx.x * kTile;
+  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  kwk_fired_rec* __restrict__ seg = a.fired + wave_id * kWaveSeg;
+  uint32_t seg_n = 0;         // wave-uniform
+  uint32_t n_matched = 0;     // per lane
+
+#pragma unroll 4
+  for (int k = 0; k < kObjPerThread; ++k) {
+    const uint64_t i = tile_base + (uint64_t)k * kBlock + wave * 64 + lane;
+    const bool in = i < a.n;
+    // one 16-byte load per object (global_load_dwordx4)
+    const uint4 hv = in ? reinterpret_cast<const uint4*>(a.hot)[i] : make_uint4(0, 0, 0, 0);
+    uint32_t pred = hv.x, sched = hv.y;
+    int64_t due = (int64_t)(((uint64_t)hv.w << 32) | hv.z);
+    bool dirty_rec = false;
+    bool fire = false;
+    uint32_t fire_stage = 0, fire_flags = 0;
+
+    if (in && (sched & KWK_F_MANAGED)) {
+      // ---------------- harness churn (never enabled by a production host)
+      if (a.harness.enable) {
+        if (!(sched & KWK_F_ALIVE)) {
+          const uint32_t gen = (sched >> KWK_GEN_SHIFT) + 1u;
+          pred &= a.harness.keep_mask;
+          sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
+                  (gen << KWK_GEN_SHIFT);
+          a.del_s[i] = KWK_DEL_ABSENT;
+          dirty_rec = true;
+        } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
+          pred |= a.harness.deletion_bit;
+          int64_t s = a.now / 1000000000;
+          if (a.now % 1000000000 < 0) s -= 1;
+          a.del_s[i] = s;
+          sched |= KWK_F_DIRTY;
+          dirty_rec = true;
+        }
+      }
+      if (sched & KWK_F_ALIVE) {
+        const kwk_value* __restrict__ rec =
+            (sched & KWK_F_HASREC) ? a.values + (uint64_t)a.rec_idx[i] * a.value_slots : nullptr;
+        // ---------------- match + pick + delay (preprocess)
+        if (sched & KWK_F_DIRTY) {
+          uint32_t m = 0;
+          for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+          sched &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
+          dirty_rec = true;
+          if (m != 0) {
+            const uint64_t gslot = a.slot_base + i;
+            int pick;
+            bool err = false;
+            const int cnt = __popc(m);
+            if (cnt == 1) {
+              pick = __ffs(m) - 1;
+            } else {
+              int64_t total = 0;
+              int nerr = 0, nge0 = 0;
+              for (uint32_t mm = m; mm; mm &= mm - 1) {
+                const Getter w = stage_weight(T->stages[__ffs(mm) - 1], sched, rec);
+                if (w.ok) {
+                  total = (int64_t)((uint64_t)total + (uint64_t)w.v);
+                  nge0 += w.v >= 0;
+                } else {
+                  ++nerr;
+                }
+              }
+              if (nerr == cnt || (total == 0 && nerr == 0)) {
+                pick = nth_bit(m, rng_below(gslot, a.step, kSitePick, a.key, cnt));
+              } else if (total == 0) {
+                int64_t want = rng_below(gslot, a.step, kSitePick, a.key, nge0);
+                pick = -1;
+                for (uint32_t mm = m; mm; mm &= mm - 1) {
+                  const int s = __ffs(mm) - 1;
+                  const Getter w = stage_weight(T->stages[s], sched, rec);
+                  if (w.ok && w.v >= 0) {
+                    if (want == 0) { pick = s; break; }
+                    --want;
+                  }
+                }
+              } else if (total < 0) {
+                err = true;  // rand.Int63n panics on n <= 0 in the reference
+                pick = -1;
+              } else {
+                int64_t off = rng_below(gslot, a.step, kSitePick, a.key, total);
+                pick = 31 - __clz(m);  // fallback: last matched stage
+                for (uint32_t mm = m; mm; mm &= mm - 1) {
+                  const int s = __ffs(mm) - 1;
+                  const Getter w = stage_weight(T->stages[s], sched, rec);
+                  const int64_t wv = w.ok ? w.v : -1;
+                  if (wv <= 0) continue;
+                  off -= wv;
+                  if (off < 0) { pick = s; break; }
+                }
+              }
+            }
+            if (err) {
+              sched |= KWK_F_MATCHERR;
+            } else {
+              const kwk_stage_desc& S = T->stages[pick];
+              int64_t delay = 0;
+              if (S.has_delay) {
+                const int64_t dels = (S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION)
+                                         ? a.del_s[i] : KWK_DEL_ABSENT;
+                const Getter d = eval_getter(S.delay_slot, S.delay_default, true, sched, rec, dels, a.now, true);
+                if (d.ok) {
+                  delay = d.v;
+                  if (S.has_jitter) {
+                    const Getter j = eval_getter(S.jitter_slot, S.jitter_default, S.jitter_default_ok != 0, sched,
+                                                 rec, dels, a.now, true);
+                    if (j.ok) {
+                      if (j.v < delay) {
+                        delay = j.v;
+                      } else {
+                        const int64_t jit = (int64_t)((uint64_t)j.v - (uint64_t)delay);
+                        if (jit > 0)
+                          delay = (int64_t)((uint64_t)delay +
+                                            (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));
+                      }
+                    }
+                  }
+                }
+              }
+              sched = (sched & ~0xFFu) | (uint32_t)pick;
+              due = sat_add(a.now, delay);
+              ++n_matched;
+            }
+          }
+        }
+        // ---------------- fire (delay queue pop + playStage)
+        const uint32_t st = sched & 0xFFu;
+        if (st < n_stages && due <= a.now) {
+          const kwk_stage_desc& S = T->stages[st];
+          fire = true;
+          fire_stage = st;
+          const uint32_t pre = pred;
+          bool rematch = (S.flags & KWK_NEXT_PATCHES) != 0;
+          if (S.flags & KWK_NEXT_FIN) {
+            const uint32_t F = pre & fin_group;
+            uint32_t F2;
+            if ((S.flags & KWK_NEXT_FIN_EMPTY) || ((S.flags & KWK_NEXT_FIN_REMOVE) && (F & ~S.fin_remove) == 0))
+              F2 = S.fin_add;
+            else
+              F2 = (F & ~S.fin_remove) | (S.fin_add & ~F);
+            rematch |= F2 != F;
+            pred = (pred & ~fin_group) | F2;
+          }
+          if (S.flags & KWK_NEXT_DELETE) {
+            sched &= ~KWK_F_ALIVE;
+            fire_flags |= KWK_FIRED_DELETED;
+            rematch = false;
+          } else if (S.flags & KWK_NEXT_PATCHES) {
+            const kwk_delta d = a.deltas[(uint32_t)a.cls[i] * n_stages + st];
+            if (d.and_mask == KWK_DELTA_UNKNOWN_AND && d.or_mask == KWK_DELTA_UNKNOWN_OR) {
+              fire_flags |= KWK_FIRED_DELTA_UNKNOWN;
+            } else {
+              pred = (((pred & d.and_mask) | d.or_mask) & ~fin_group) | (pred & fin_group);
+            }
+          }
+          if (rematch) {
+            sched |= KWK_F_DIRTY;
+            fire_flags |= KWK_FIRED_REMATCH;
+          }
+          sched |= KWK_STAGE_NONE;
+          dirty_rec = true;
+        }
+      }
+    }
+    if (dirty_rec)
+      reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
+
+    // ---------------- wave-ballot compaction of the fired set into the wave's segment
+    const unsigned long long bal = __ballot(fire);
+    if (fire) {
+      const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)fire_stage, (uint16_t)fire_flags};
+      atomicAdd(&s_stat[2 + fire_stage], 1u);
+    }
+    seg_n += (uint32_t)__popcll(bal);
+  }
+
+  // per-wave fired count (read by kwk_fired's scan) and block statistics
+  for (int off = 32; off > 0; off >>= 1) n_matched += __shfl_xor(n_matched, off);
+  if (lane == 0) {
+    a.wave_counts[wave_id] = seg_n;
+    atomicAdd(&s_stat[0], n_matched);
+    atomicAdd(&s_stat[1], seg_n);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 + n_stages) {
+    const unsigned int v = s_stat[threadIdx.x];
+    if (v) a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x] += v;
+  }
+}
+
+// gather the per-wave fired segments into one dense list (offsets from an exclusive scan)
+__global__ void compact_fired_kernel(const kwk_fired_rec* __restrict__ fired, const uint32_t* __restrict__ counts,
+                                     const uint32_t* __restrict__ offsets, uint32_t n_waves,
+                                     kwk_fired_rec* __restrict__ out) {
+  const uint32_t w = blockIdx.x;
+  if (w >= n_waves) return;
+  const uint32_t c = counts[w];
+  const uint32_t o = offsets[w];
+  for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) out[o + j] = fired[(uint64_t)w * kWaveSeg + j];
+}
+
+__global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, uint32_t n_blocks,
+                                    unsigned long long* __restrict__ out) {
+  const uint32_t word = blockIdx.x;  // one workgroup per statistic word
+  unsigned long long s = 0;
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) s += cum[(uint64_t)b * kStatWords + word];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  __shared__ unsigned long long part[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int i = 0; i < kBlock / 64; ++i) t += part[i];
+    out[word] = t;
+  }
+}
+
+struct ScatterArgs {
+  kwk_hot* hot;
+  int64_t* del_s;
+  uint32_t* rec_idx;
+  uint16_t* cls;
+  const uint32_t* slots;
+  const kwk_hot* s_hot;
+  const int64_t* s_del;
+  const uint32_t* s_rec;
+  const uint16_t* s_cls;
+  uint32_t n;
+  uint32_t mark_dirty;
+};
+
+__global__ void scatter_kernel(ScatterArgs a) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.n) return;
+  const uint32_t i = a.slots[j];
+  kwk_hot h = a.s_hot[j];
+  if (a.mark_dirty) h.sched |= KWK_F_DIRTY;
+  a.hot[i] = h;
+  a.del_s[i] = a.s_del[j];
+  a.rec_idx[i] = a.s_rec[j];
+  a.cls[i] = a.s_cls[j];
+}
+
+__global__ void delete_kernel(kwk_hot* hot, const uint32_t* slots, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = slots[j];
+  hot[i].sched = (hot[i].sched & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
+}
+
+// ------------------------------------------------------------------ resource usage
+// One wave per node: lanes stride over the node's (node-sorted) pods, gather the pod's
+// cpu / memory value from the interned dictionaries, multiply by its container count and
+// reduce with shuffles.  Dead pods (not in the pod cache) contribute nothing.
+// server/metrics_resource_usage.go:170-224 (sums), :36-109 (cumulative integrators).
+__global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict__ hot,
+                                                       const uint32_t* __restrict__ node_ptr,
+                                                       const uint32_t* __restrict__ ukey,
+                                                       const double* __restrict__ cpu_v,
+                                                       const double* __restrict__ mem_v, uint32_t n_nodes,
+                                                       double* __restrict__ node_out, double* __restrict__ cum,
+                                                       int64_t* __restrict__ last_t, int64_t now,
+                                                       double* __restrict__ block_part) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t node = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  double c = 0.0, m = 0.0;
+  if (node < n_nodes) {
+    const uint32_t lo = node_ptr[node], hi = node_ptr[node + 1];
+    for (uint32_t p = lo + lane; p < hi; p += 64) {
+      const uint32_t sched = hot[p].sched;
+      if (!(sched & KWK_F_ALIVE)) continue;
+      const uint32_t k = ukey[p];
+      const double nc = (double)(k >> 28);
+      c += nc * cpu_v[k & 0x3FFFu];
+      m += nc * mem_v[(k >> 14) & 0x3FFFu];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    c += __shfl_xor(c, off);
+    m += __shfl_xor(m, off);
+  }
+  __shared__ double s_c[kBlock / 64], s_m[kBlock / 64];
+  if (lane == 0) {
+    if (node < n_nodes) {
+      node_out[node * 4 + 0] = c;
+      node_out[node * 4 + 1] = m;
+      const int64_t lt = last_t[node];
+      if (lt != INT64_MIN) {
+        const double dt = (double)(now - lt) / 1e9;  // now.Sub(c.time).Seconds()
+        cum[node * 2 + 0] += dt * c;
+        cum[node * 2 + 1] += dt * m;
+      }
+      last_t[node] = now;
+      node_out[node * 4 + 2] = cum[node * 2 + 0];
+      node_out[node * 4 + 3] = cum[node * 2 + 1];
+    } else {
+      c = 0.0;
+      m = 0.0;
+    }
+    s_c[threadIdx.x >> 6] = c;
+    s_m[threadIdx.x >> 6] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tc = 0, tm = 0;
+    for (int i = 0; i < kBlock / 64; ++i) { tc += s_c[i]; tm += s_m[i]; }
+    block_part[blockIdx.x * 2 + 0] = tc;
+    block_part[blockIdx.x * 2 + 1] = tm;
+  }
+}
+
+__global__ void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks, double* __restrict__ out) {
+  double c = 0, m = 0;
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) { c += part[b * 2]; m += part[b * 2 + 1]; }
+  for (int off = 32; off > 0; off >>= 1) { c += __shfl_xor(c, off); m += __shfl_xor(m, off); }
+  __shared__ double sc[kBlock / 64], sm[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = c; sm[threadIdx.x >> 6] = m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tc = 0, tm = 0;
+    for (int i = 0; i < kBlock / 64; ++i) { tc += sc[i]; tm += sm[i]; }
+    out[0] = tc;
+    out[1] = tm;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ engine object
+struct kwk_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t capacity = 0, n_active = 0, value_slots = 0, max_records = 0;
+  uint64_t slot_base = 0;
+  uint32_t kind_salt = 0;
+  uint32_t n_blocks_cap = 0, last_blocks = 0;
+  bool loaded_table = false;
+  uint32_t n_stages = 0, n_classes = 0;
+  kwk_harness harness{};
+
+  kwk_hot* d_hot = nullptr;
+  int64_t* d_del = nullptr;
+  uint32_t* d_rec = nullptr;
+  uint16_t* d_cls = nullptr;
+  kwk_value* d_values = nullptr;
+  kwk_stage_table* d_table = nullptr;
+  kwk_delta* d_deltas = nullptr;
+  kwk_fired_rec* d_fired = nullptr;
+  kwk_fired_rec* d_compact = nullptr;
+  uint32_t* d_wave_counts = nullptr;
+  uint32_t* d_wave_offsets = nullptr;
+  unsigned long long* d_cum = nullptr;
+  unsigned long long* d_stats = nullptr;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  uint64_t steps = 0;
+
+  // usage
+  uint32_t n_nodes = 0;
+  uint32_t* d_node_ptr = nullptr;
+  uint32_t* d_ukey = nullptr;
+  double* d_cpu = nullptr;
+  double* d_mem = nullptr;
+  double* d_node_out = nullptr;
+  double* d_node_cum = nullptr;
+  int64_t* d_node_last = nullptr;
+  double* d_usage_part = nullptr;
+  double* d_cluster = nullptr;
+
+  // staging for upserts
+  void* d_stage_buf = nullptr;
+  size_t stage_bytes = 0;
+
+  std::vector<hipEvent_t> events;
+};
+
+static kwk_status set_dev(kwk_engine* e) {
+  HIP_TRY(hipSetDevice(e->device));
+  return KWK_OK;
+}
+
+static kwk_status ensure_stage_buf(kwk_engine* e, size_t bytes) {
+  if (bytes <= e->stage_bytes) return KWK_OK;
+  if (e->d_stage_buf) HIP_TRY(hipFree(e->d_stage_buf));
+  e->d_stage_buf = nullptr;
+  HIP_TRY(hipMalloc(&e->d_stage_buf, bytes));
+  e->stage_bytes = bytes;
+  return KWK_OK;
+}
+
+extern "C" {
+
+const char* kwk_last_error(void) { return g_err.c_str(); }
+
+kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
+  if (!d || !out) return fail(KWK_EINVAL, "null argument");
+  if (d->capacity == 0) return fail(KWK_EINVAL, "capacity must be > 0");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (d->device < 0 || d->device >= ndev) return fail(KWK_EINVAL, "device ordinal out of range");
+  auto* e = new kwk_engine();
+  e->device = d->device;
+  e->capacity = d->capacity;
+  e->value_slots = d->value_slots ? d->value_slots : 1;
+  e->max_records = d->max_records ? d->max_records : 1;
+  e->slot_base = d->slot_base;
+  e->kind_salt = d->kind_salt;
+  e->n_blocks_cap = (d->capacity + kTile - 1) / kTile;
+  kwk_status st = set_dev(e);
+  if (st) { delete e; return st; }
+  const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
+#define ALLOC(p, bytes)                                                          \
+  do {                                                                           \
+    hipError_t er = hipMalloc((void**)&(p), (bytes));                            \
+    if (er != hipSuccess) {                                                      \
+      kwk_engine_destroy(e);                                                     \
+      return fail(KWK_EHIP, std::string("hipMalloc: ") + hipGetErrorString(er)); \
+    }                                                                            \
+  } while (0)
+  ALLOC(e->d_hot, sizeof(kwk_hot) * (size_t)e->capacity);
+  ALLOC(e->d_del, sizeof(int64_t) * (size_t)e->capacity);
+  ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
+  ALLOC(e->d_cls, sizeof(uint16_t) * (size_t)e->capacity);
+  ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
+  ALLOC(e->d_table, sizeof(kwk_stage_table));
+  ALLOC(e->d_fired, sizeof(kwk_fired_rec) * n_waves * kWaveSeg);
+  ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
+  ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
+  ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
+  ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
+  ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
+  hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
+  hipMemsetAsync(e->d_hot, 0, sizeof(kwk_hot) * (size_t)e->capacity, e->stream);
+  hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
+  hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
+  // cub scan temp storage for the fired-list compaction
+  hipcub::DeviceScan::ExclusiveSum(nullptr, e->scan_tmp_bytes, e->d_wave_counts, e->d_wave_offsets,
+                                   (int)(n_waves + 1), e->stream);
+  ALLOC(e->d_scan_tmp, e->scan_tmp_bytes ? e->scan_tmp_bytes : 16);
+#undef ALLOC
+  er = hipStreamSynchronize(e->stream);
+  if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
+  *out = e;
+  return KWK_OK;
+}
+
+kwk_status kwk_engine_destroy(kwk_engine* e) {
+  if (!e) return KWK_OK;
+  hipSetDevice(e->device);
+  if (e->stream) hipStreamSynchronize(e->stream);
+  void* ptrs[] = {e->d_hot, e->d_del, e->d_rec, e->d_cls, e->d_values, e->d_table, e->d_deltas, e->d_fired,
+                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
+                  e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
+                  e->d_usage_part, e->d_cluster, e->d_stage_buf};
+  for (void* p : ptrs) if (p) hipFree(p);
+  for (auto ev : e->events) hipEventDestroy(ev);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+  return KWK_OK;
+}
+
+kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_delta* deltas) {
+  if (!e || !t) return fail(KWK_EINVAL, "null argument");
+  if (t->n_stages > KWK_MAX_STAGES) return fail(KWK_EINVAL, "too many stages");
+  if (t->n_classes == 0 && t->n_stages) return fail(KWK_EINVAL, "n_classes must be > 0");
+  for (uint32_t s = 0; s < t->n_stages; ++s) {
+    const kwk_stage_desc& S = t->stages[s];
+    if (S.n_any > KWK_MAX_ANY) return fail(KWK_EINVAL, "stage " + std::to_string(s) + ": n_any > KWK_MAX_ANY");
+    const int32_t slots[3] = {S.weight_slot, S.delay_slot, S.jitter_slot};
+    for (int32_t sl : slots)
+      if (sl < KWK_SLOT_DELETION || sl >= (int32_t)e->value_slots)
+        return fail(KWK_EINVAL, "stage " + std::to_string(s) + ": value slot out of range");
+    if (S.weight_slot == KWK_SLOT_DELETION) return fail(KWK_EINVAL, "weight cannot use the deletion column");
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->d_table, t, sizeof(kwk_stage_table), hipMemcpyHostToDevice));
+  if (e->d_deltas) HIP_TRY(hipFree(e->d_deltas));
+  e->d_deltas = nullptr;
+  const size_t nd = (size_t)(t->n_classes ? t->n_classes : 1) * (t->n_stages ? t->n_stages : 1);
+  HIP_TRY(hipMalloc(&e->d_deltas, sizeof(kwk_delta) * nd));
+  if (deltas && t->n_stages) HIP_TRY(hipMemcpy(e->d_deltas, deltas, sizeof(kwk_delta) * nd, hipMemcpyHostToDevice));
+  else HIP_TRY(hipMemset(e->d_deltas, 0xFF, sizeof(kwk_delta) * nd));
+  e->n_stages = t->n_stages;
+  e->n_classes = t->n_classes;
+  e->loaded_table = true;
+  return KWK_OK;
+}
+
+kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
+  if (!e || !h) return fail(KWK_EINVAL, "null argument");
+  e->harness = *h;
+  return KWK_OK;
+}
+
+kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t* del, const uint32_t* rec,
+                    const uint16_t* cls, uint32_t n_records, const kwk_value* records) {
+  if (!e || (n && (!hot || !del || !rec || !cls))) return fail(KWK_EINVAL, "null argument");
+  if (n > e->capacity) return fail(KWK_ECAP, "n exceeds capacity");
+  if (n_records > e->max_records) return fail(KWK_ECAP, "n_records exceeds max_records");
+  for (uint32_t i = 0; i < n; ++i) {
+    if ((hot[i].sched & KWK_F_HASREC) && rec[i] >= n_records)
+      return fail(KWK_EINVAL, "object " + std::to_string(i) + ": record index out of range");
+    if (e->loaded_table && cls[i] >= e->n_classes)
+      return fail(KWK_EINVAL, "object " + std::to_string(i) + ": class out of range");
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->d_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_rec, rec, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_cls, cls, sizeof(uint16_t) * n, hipMemcpyHostToDevice));
+  if (n_records)
+    HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
+                      hipMemcpyHostToDevice));
+  if (n < e->n_active)
+    HIP_TRY(hipMemset(e->d_hot + n, 0, sizeof(kwk_hot) * (size_t)(e->n_active - n)));
+  e->n_active = n;
+  return KWK_OK;
+}
+
+kwk_status kwk_set_records(kwk_engine* e, uint32_t first, uint32_t n, const kwk_value* records) {
+  if (!e || (n && !records)) return fail(KWK_EINVAL, "null argument");
+  if ((uint64_t)first + n > e->max_records) return fail(KWK_ECAP, "records exceed max_records");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->d_values + (size_t)first * e->value_slots, records, sizeof(kwk_value) * (size_t)n * e->value_slots,
+                    hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
+                      const uint32_t* rec, const uint16_t* cls) {
+  if (!e || (n && (!slots || !hot || !del || !rec || !cls))) return fail(KWK_EINVAL, "null argument");
+  if (n == 0) return KWK_OK;
+  uint32_t max_slot = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (slots[j] >= e->capacity) return fail(KWK_ECAP, "slot beyond capacity");
+    if (e->loaded_table && cls[j] >= e->n_classes) return fail(KWK_EINVAL, "class out of range");
+    if ((hot[j].sched & KWK_F_HASREC) && rec[j] >= e->max_records) return fail(KWK_EINVAL, "record out of range");
+    max_slot = slots[j] > max_slot ? slots[j] : max_slot;
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  const size_t bytes = (size_t)n * (4 + sizeof(kwk_hot) + 8 + 4 + 2) + 64;
+  if (kwk_status st = ensure_stage_buf(e, bytes)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  char* p = (char*)e->d_stage_buf;
+  kwk_hot* s_hot = (kwk_hot*)p; p += sizeof(kwk_hot) * n;
+  int64_t* s_del = (int64_t*)p; p += 8 * (size_t)n;
+  uint32_t* s_slots = (uint32_t*)p; p += 4 * (size_t)n;
+  uint32_t* s_rec = (uint32_t*)p; p += 4 * (size_t)n;
+  uint16_t* s_cls = (uint16_t*)p;
+  HIP_TRY(hipMemcpy(s_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_del, del, 8 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_rec, rec, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
+  if (max_slot + 1 > e->n_active) {
+    HIP_TRY(hipMemset(e->d_hot + e->n_active, 0, sizeof(kwk_hot) * (size_t)(max_slot + 1 - e->n_active)));
+    e->n_active = max_slot + 1;
+  }
+  ScatterArgs a{e->d_hot, e->d_del, e->d_rec, e->d_cls, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
+  hipLaunchKernelGGL(scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
+  if (!e || (n && !slots)) return fail(KWK_EINVAL, "null argument");
+  if (n == 0) return KWK_OK;
+  for (uint32_t j = 0; j < n; ++j)
+    if (slots[j] >= e->n_active) return fail(KWK_EINVAL, "slot not active");
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = ensure_stage_buf(e, 4 * (size_t)n)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->d_stage_buf, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_hot,
+                     (const uint32_t*)e->d_stage_buf, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
+  if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
+  SweepArgs a;
+  a.hot = e->d_hot;
+  a.del_s = e->d_del;
+  a.rec_idx = e->d_rec;
+  a.cls = e->d_cls;
+  a.values = e->d_values;
+  a.table = e->d_table;
+  a.deltas = e->d_deltas;
+  a.fired = e->d_fired;
+  a.wave_counts = e->d_wave_counts;
+  a.cum = e->d_cum;
+  a.n = e->n_active;
+  a.value_slots = e->value_slots;
+  a.slot_base = e->slot_base;
+  a.key = seed ^ ((uint64_t)e->kind_salt << 32);
+  a.step = step;
+  a.now = now_ns;
+  a.harness = e->harness;
+  const uint32_t blocks = (e->n_active + kTile - 1) / kTile;
+  hipLaunchKernelGGL(sweep_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+  HIP_TRY(hipGetLastError());
+  e->last_blocks = blocks;
+  ++e->steps;
+  return KWK_OK;
+}
+
+kwk_status kwk_sync(kwk_engine* e) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out) {
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (n_waves == 0) { *n_out = 0; return KWK_OK; }
+  HIP_TRY(hipMemsetAsync(e->d_wave_counts + n_waves, 0, sizeof(uint32_t), e->stream));
+  size_t tmp = e->scan_tmp_bytes;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->d_scan_tmp, tmp, e->d_wave_counts, e->d_wave_offsets,
+                                           (int)(n_waves + 1), e->stream));
+  uint32_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets + n_waves, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
+  hipLaunchKernelGGL(compact_fired_kernel, dim3(n_waves), dim3(64), 0, e->stream, e->d_fired, e->d_wave_counts,
+                     e->d_wave_offsets, n_waves, e->d_compact);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
+  if (!e || !out) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->n_blocks_cap,
+                     e->d_stats);
+  HIP_TRY(hipGetLastError());
+  unsigned long long h[kStatWords];
+  HIP_TRY(hipMemcpyAsync(h, e->d_stats, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memset(out, 0, sizeof(*out));
+  out->steps = e->steps;
+  out->matched = h[0];
+  out->fired = h[1];
+  for (int s = 0; s < KWK_MAX_STAGES; ++s) out->fired_per_stage[s] = h[2 + s];
+  return KWK_OK;
+}
+
+kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int64_t* del) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (hot) HIP_TRY(hipMemcpy(hot, e->d_hot + first, sizeof(kwk_hot) * n, hipMemcpyDeviceToHost));
+  if (del) HIP_TRY(hipMemcpy(del, e->d_del + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* node_ptr, const uint32_t* ukey,
+                            uint32_t n_cpu, const double* cpu_values, uint32_t n_mem, const double* mem_values) {
+  if (!e || !node_ptr || !ukey || !cpu_values || !mem_values) return fail(KWK_EINVAL, "null argument");
+  if (n_cpu == 0 || n_mem == 0 || n_cpu > 0x4000 || n_mem > 0x4000) return fail(KWK_EINVAL, "dictionary size");
+  if (node_ptr[0] != 0) return fail(KWK_EINVAL, "node_ptr[0] must be 0");
+  for (uint32_t j = 0; j < n_nodes; ++j)
+    if (node_ptr[j + 1] < node_ptr[j]) return fail(KWK_EINVAL, "node_ptr must be non-decreasing");
+  const uint32_t n_pods = node_ptr[n_nodes];
+  if (n_pods > e->capacity) return fail(KWK_ECAP, "node_ptr covers more pods than capacity");
+  for (uint32_t p = 0; p < n_pods; ++p)
+    if ((ukey[p] & 0x3FFFu) >= n_cpu || ((ukey[p] >> 14) & 0x3FFFu) >= n_mem)
+      return fail(KWK_EINVAL, "usage_key value id out of range");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
+                  e->d_usage_part, e->d_cluster};
+  for (void* p : olds) if (p) hipFree(p);
+  const uint32_t ublocks = (n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
+  HIP_TRY(hipMalloc(&e->d_node_ptr, 4 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMalloc(&e->d_ukey, 4 * ((size_t)n_pods + 1)));
+  HIP_TRY(hipMalloc(&e->d_cpu, 8 * (size_t)n_cpu));
+  HIP_TRY(hipMalloc(&e->d_mem, 8 * (size_t)n_mem));
+  HIP_TRY(hipMalloc(&e->d_node_out, 32 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMalloc(&e->d_node_cum, 16 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMalloc(&e->d_node_last, 8 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMalloc(&e->d_usage_part, 16 * ((size_t)ublocks + 1)));
+  HIP_TRY(hipMalloc(&e->d_cluster, 16));
+  HIP_TRY(hipMemcpy(e->d_node_ptr, node_ptr, 4 * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_ukey, ukey, 4 * (size_t)n_pods, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_cpu, cpu_values, 8 * (size_t)n_cpu, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_mem, mem_values, 8 * (size_t)n_mem, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e->d_node_cum, 0, 16 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMemset(e->d_node_last, 0x80, 8 * ((size_t)n_nodes + 1)));  // INT64_MIN-ish sentinel below
+  std::vector<int64_t> lasts((size_t)n_nodes + 1, INT64_MIN);
+  HIP_TRY(hipMemcpy(e->d_node_last, lasts.data(), 8 * lasts.size(), hipMemcpyHostToDevice));
+  e->n_nodes = n_nodes;
+  return KWK_OK;
+}
+
+kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (e->n_nodes == 0) return KWK_OK;
+  const uint32_t ublocks = (e->n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_hot, e->d_node_ptr, e->d_ukey,
+                     e->d_cpu, e->d_mem, e->n_nodes, e->d_node_out, e->d_node_cum, e->d_node_last, now_ns,
+                     e->d_usage_part);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(kBlock), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);
+  HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_read(kwk_engine* e, double* node_out, double* cluster_out) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (node_out && e->n_nodes) HIP_TRY(hipMemcpy(node_out, e->d_node_out, 32 * (size_t)e->n_nodes, hipMemcpyDeviceToHost));
+  if (cluster_out) HIP_TRY(hipMemcpy(cluster_out, e->d_cluster, 16, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_device_ptrs(kwk_engine* e, void** hot, void** fired, void** wave_counts) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (hot) *hot = e->d_hot;
+  if (fired) *fired = e->d_fired;
+  if (wave_counts) *wave_counts = e->d_wave_counts;
+  return KWK_OK;
+}
+
+// ---- timing helpers (HIP events on the engine's own stream; bench.py)
+kwk_status kwk_event_record(kwk_engine* e, uint32_t idx) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  while (e->events.size() <= idx) {
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreate(&ev));
+    e->events.push_back(ev);
+  }
+  HIP_TRY(hipEventRecord(e->events[idx], e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_event_elapsed(kwk_engine* e, uint32_t a, uint32_t b, float* ms) {
+  if (!e || !ms || a >= e->events.size() || b >= e->events.size()) return fail(KWK_EINVAL, "bad event index");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipEventSynchronize(e->events[b]));
+  HIP_TRY(hipEventElapsedTime(ms, e->events[a], e->events[b]));
+  return KWK_OK;
+}
+
+uint32_t kwk_abi_version(void) { return 1u; }
+uint32_t kwk_tile_objects(void) { return (uint32_t)kTile; }
+
+}  // extern "C"

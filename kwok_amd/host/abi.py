@@ -1,0 +1,154 @@
+"""ctypes mirror of include/kwok_engine.h and the loader for the HIP engine library.
+
+This is the Python stand-in for the cgo binding a Go host would use (INTEGRATION.md shows
+the Go side).  The library is the product: there is no CPU fallback — if it is missing or
+cannot open a GPU, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libkwok_engine.so")
+
+KWK_OK, KWK_EINVAL, KWK_ECAP, KWK_EHIP, KWK_ESTATE = 0, -1, -2, -3, -4
+STAGE_NONE = 0xFF
+F_ALIVE, F_DIRTY, F_MANAGED, F_HASREC, F_MATCHERR = 1 << 8, 1 << 9, 1 << 10, 1 << 11, 1 << 12
+GEN_SHIFT = 16
+V_DEFAULT, V_OK, V_NOTOK, V_ABSTIME = 0, 1, 2, 3
+DEL_ABSENT = -(1 << 63)
+MAX_STAGES, MAX_ANY = 32, 4
+SLOT_NONE, SLOT_DELETION = -1, -2
+NEXT_DELETE, NEXT_IMMEDIATE, NEXT_PATCHES, NEXT_FIN, NEXT_FIN_EMPTY, NEXT_FIN_REMOVE = 1, 2, 4, 8, 16, 32
+DELTA_UNKNOWN = (0, 0xFFFFFFFF)
+FIRED_DELETED, FIRED_REMATCH, FIRED_DELTA_UNKNOWN = 1, 2, 4
+
+
+class Hot(C.Structure):
+    _fields_ = [("pred", C.c_uint32), ("sched", C.c_uint32), ("due", C.c_int64)]
+
+
+class Value(C.Structure):
+    _fields_ = [("value", C.c_int64), ("nsec", C.c_int32), ("kind", C.c_int32)]
+
+
+class StageDesc(C.Structure):
+    _fields_ = [
+        ("eq_mask", C.c_uint32), ("eq_val", C.c_uint32), ("n_any", C.c_uint32), ("any_want", C.c_uint32),
+        ("any_mask", C.c_uint32 * MAX_ANY),
+        ("weight_default", C.c_int64), ("weight_slot", C.c_int32),
+        ("has_delay", C.c_int32), ("delay_default", C.c_int64), ("delay_slot", C.c_int32),
+        ("has_jitter", C.c_int32), ("jitter_default", C.c_int64), ("jitter_default_ok", C.c_int32),
+        ("jitter_slot", C.c_int32),
+        ("flags", C.c_uint32), ("fin_add", C.c_uint32), ("fin_remove", C.c_uint32), ("pad", C.c_uint32),
+    ]
+
+
+class StageTable(C.Structure):
+    _fields_ = [("n_stages", C.c_uint32), ("fin_group_mask", C.c_uint32), ("n_classes", C.c_uint32),
+                ("version", C.c_uint32), ("stages", StageDesc * MAX_STAGES)]
+
+
+class Delta(C.Structure):
+    _fields_ = [("and_mask", C.c_uint32), ("or_mask", C.c_uint32)]
+
+
+class Harness(C.Structure):
+    _fields_ = [("enable", C.c_uint32), ("keep_mask", C.c_uint32), ("terminal_mask", C.c_uint32),
+                ("deletion_bit", C.c_uint32)]
+
+
+class FiredRec(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("stage", C.c_uint16), ("flags", C.c_uint16)]
+
+
+class StepStats(C.Structure):
+    _fields_ = [("steps", C.c_uint64), ("matched", C.c_uint64), ("fired", C.c_uint64),
+                ("fired_per_stage", C.c_uint64 * MAX_STAGES)]
+
+
+class EngineDesc(C.Structure):
+    _fields_ = [("device", C.c_int32), ("capacity", C.c_uint32), ("value_slots", C.c_uint32),
+                ("max_records", C.c_uint32), ("slot_base", C.c_uint64), ("kind_salt", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+HOT_DTYPE = np.dtype([("pred", "<u4"), ("sched", "<u4"), ("due", "<i8")])
+VALUE_DTYPE = np.dtype([("value", "<i8"), ("nsec", "<i4"), ("kind", "<i4")])
+FIRED_DTYPE = np.dtype([("slot", "<u4"), ("stage", "<u2"), ("flags", "<u2")])
+
+assert C.sizeof(Hot) == 16 and C.sizeof(Value) == 16 and C.sizeof(StageDesc) == 96
+assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.itemsize == 8
+
+# every symbol include/kwok_engine.h declares (checked by the CPU test suite)
+EXPORTS = [
+    "kwk_last_error", "kwk_engine_create", "kwk_engine_destroy", "kwk_load_stages", "kwk_set_harness", "kwk_load",
+    "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
+    "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
+    "kwk_abi_version", "kwk_tile_objects",
+]
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _p(t):
+    return C.POINTER(t)
+
+
+def lib():
+    """Load libkwok_engine.so (built in-tree by __graft_entry__.build / kwok_amd.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"HIP engine library missing: {LIB_PATH} (run python -m kwok_amd.build)")
+    L = C.CDLL(LIB_PATH)
+    s = C.c_int32
+    L.kwk_last_error.restype = C.c_char_p
+    L.kwk_engine_create.argtypes = [_p(EngineDesc), _p(C.c_void_p)]
+    L.kwk_engine_destroy.argtypes = [C.c_void_p]
+    L.kwk_load_stages.argtypes = [C.c_void_p, _p(StageTable), C.c_void_p]
+    L.kwk_set_harness.argtypes = [C.c_void_p, _p(Harness)]
+    L.kwk_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                           C.c_void_p]
+    L.kwk_upsert.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
+    L.kwk_fired.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_stats.argtypes = [C.c_void_p, _p(StepStats)]
+    L.kwk_read.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.kwk_sync.argtypes = [C.c_void_p]
+    L.kwk_usage_config.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                   C.c_uint32, C.c_void_p]
+    L.kwk_usage.argtypes = [C.c_void_p, C.c_int64]
+    L.kwk_usage_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kwk_device_ptrs.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p), _p(C.c_void_p)]
+    L.kwk_event_record.argtypes = [C.c_void_p, C.c_uint32]
+    L.kwk_event_elapsed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, _p(C.c_float)]
+    L.kwk_abi_version.restype = C.c_uint32
+    L.kwk_tile_objects.restype = C.c_uint32
+    for name in EXPORTS:
+        fn = getattr(L, name)
+        if name not in ("kwk_last_error", "kwk_abi_version", "kwk_tile_objects"):
+            fn.restype = s
+    _lib = L
+    return L
+
+
+def check(status: int, what: str = ""):
+    if status != KWK_OK:
+        msg = lib().kwk_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed ({status}): {msg}")
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None

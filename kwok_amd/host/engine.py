@@ -1,0 +1,228 @@
+"""Host driver for one engine (one resource kind on one GPU).
+
+``Ingest`` turns objects into the device's SoA columns (the Go host's informer-side
+encoder); ``Engine`` owns the C-ABI handle.  Objects are interned
+by *variant*: objects that differ only in identity (name, uid, node) share one feature /
+record / class computation, which is what makes 10^8-object clusters ingestible.
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+import json
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .compiler import KindProgram, path_prefix
+from .nextstate import prune_empty
+
+
+def _variant_key(obj: dict) -> str:
+    o = copy.deepcopy(obj)
+    md = o.get("metadata") or {}
+    for k in ("name", "generateName", "uid", "resourceVersion", "creationTimestamp", "selfLink", "managedFields"):
+        md.pop(k, None)
+    if isinstance(o.get("spec"), dict):
+        o["spec"].pop("nodeName", None)
+    for r in md.get("ownerReferences") or []:
+        r.pop("uid", None)
+        r.pop("name", None)
+    return json.dumps(o, sort_keys=True, separators=(",", ":"))
+
+
+class Ingest:
+    """Objects -> (hot, deletion_s, rec_idx, cls, records) for one KindProgram."""
+
+    def __init__(self, program: KindProgram):
+        self.p = program
+        # variant memoisation is valid only if no query reads an identity field
+        self.memo_ok = not any(path_prefix(f.src)[:2] in (["metadata", "name"], ["metadata", "uid"], ["spec", "nodeName"])
+                               for f in program.features.values())
+        self._memo: Dict[str, tuple] = {}
+        self.records: List[List[tuple]] = []
+        self._rec_ids: Dict[str, int] = {}
+
+    def encode(self, obj: dict, register_class: bool = True):
+        """-> (pred, sched_flags, del_s, rec_idx, cls) for one object (sched without stage)."""
+        key = _variant_key(obj) if self.memo_ok else None
+        hit = self._memo.get(key) if key is not None else None
+        if hit is None:
+            obj = prune_empty(copy.deepcopy(obj))
+            pred = self.p.pred_of(obj)
+            rec = self.p.record_of(obj)
+            rid = 0
+            flags = abi.F_ALIVE | abi.F_MANAGED | abi.F_DIRTY
+            if rec is not None:
+                rk = json.dumps(rec)
+                rid = self._rec_ids.get(rk)
+                if rid is None:
+                    rid = self._rec_ids[rk] = len(self.records)
+                    self.records.append(rec)
+                flags |= abi.F_HASREC
+            cls = self.p.class_of(obj, register=register_class)
+            dels = self.p.deletion_s(obj)
+            hit = (pred, flags, dels, rid, cls)
+            if key is not None:
+                self._memo[key] = hit
+        return hit
+
+    def columns(self, objs: Sequence[dict]):
+        n = len(objs)
+        hot = np.zeros(n, dtype=abi.HOT_DTYPE)
+        dels = np.zeros(n, dtype=np.int64)
+        rec = np.zeros(n, dtype=np.uint32)
+        cls = np.zeros(n, dtype=np.uint16)
+        for i, o in enumerate(objs):
+            pred, flags, d, rid, c = self.encode(o)
+            hot[i] = (pred, flags | abi.STAGE_NONE, 0)
+            dels[i], rec[i], cls[i] = d, rid, c
+        return hot, dels, rec, cls
+
+    def variant_columns(self, variants: Sequence[dict], index: np.ndarray):
+        """Columns for objects given as variant ids (index[i] -> variants[index[i]])."""
+        enc = [self.encode(v) for v in variants]
+        pred = np.array([e[0] for e in enc], dtype=np.uint32)
+        flags = np.array([e[1] for e in enc], dtype=np.uint32)
+        dls = np.array([e[2] for e in enc], dtype=np.int64)
+        rid = np.array([e[3] for e in enc], dtype=np.uint32)
+        cl = np.array([e[4] for e in enc], dtype=np.uint16)
+        hot = np.empty(len(index), dtype=abi.HOT_DTYPE)
+        hot["pred"] = pred[index]
+        hot["sched"] = flags[index] | abi.STAGE_NONE
+        hot["due"] = 0
+        return hot, dls[index], rid[index], cl[index]
+
+    def record_array(self) -> np.ndarray:
+        ns = max(1, len(self.p.slots))
+        a = np.zeros((max(1, len(self.records)), ns), dtype=abi.VALUE_DTYPE)
+        for r, rec in enumerate(self.records):
+            for s, (kind, value, nsec) in enumerate(rec):
+                a[r, s] = (value, nsec, kind)
+        return a
+
+
+class Engine:
+    """One kwk_engine (C ABI) for one KindProgram."""
+
+    def __init__(self, program: KindProgram, capacity: int, device: int = 0, slot_base: int = 0, kind_salt: int = 0,
+                 max_records: int = 1 << 16):
+        self.p = program
+        L = abi.lib()
+        d = abi.EngineDesc(device=device, capacity=capacity, value_slots=max(1, len(program.slots)),
+                           max_records=max_records, slot_base=slot_base, kind_salt=kind_salt)
+        h = C.c_void_p()
+        abi.check(L.kwk_engine_create(C.byref(d), C.byref(h)), "kwk_engine_create")
+        self.h = h
+        self.capacity = capacity
+        self.n = 0
+        self.kind_salt = kind_salt
+        self.slot_base = slot_base
+
+    def close(self):
+        if getattr(self, "h", None):
+            abi.lib().kwk_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_stages(self, version: int = 1):
+        t = self.p.table(version)
+        deltas = np.ascontiguousarray(self.p.delta_array())
+        abi.check(abi.lib().kwk_load_stages(self.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
+        h = self.p.harness_struct()
+        abi.check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
+
+    def set_harness(self, enable: bool):
+        h = self.p.harness_struct()
+        h.enable = 1 if (enable and self.p.harness is not None) else 0
+        abi.check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
+
+    def load(self, hot, dels, rec, cls, records: Optional[np.ndarray] = None):
+        hot = np.ascontiguousarray(hot)
+        dels = np.ascontiguousarray(dels, dtype=np.int64)
+        rec = np.ascontiguousarray(rec, dtype=np.uint32)
+        cls = np.ascontiguousarray(cls, dtype=np.uint16)
+        n_rec = 0 if records is None else records.shape[0]
+        recs = None if records is None else np.ascontiguousarray(records)
+        abi.check(abi.lib().kwk_load(self.h, len(hot), abi.ptr(hot), abi.ptr(dels), abi.ptr(rec), abi.ptr(cls), n_rec,
+                                     abi.ptr(recs)), "kwk_load")
+        self.n = len(hot)
+
+    def upsert(self, slots, hot, dels, rec, cls):
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        hot = np.ascontiguousarray(hot)
+        abi.check(abi.lib().kwk_upsert(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
+                                       abi.ptr(np.ascontiguousarray(dels, dtype=np.int64)),
+                                       abi.ptr(np.ascontiguousarray(rec, dtype=np.uint32)),
+                                       abi.ptr(np.ascontiguousarray(cls, dtype=np.uint16))), "kwk_upsert")
+        self.n = max(self.n, int(slots.max()) + 1)
+
+    def set_records(self, records: np.ndarray, first: int = 0):
+        recs = np.ascontiguousarray(records)
+        abi.check(abi.lib().kwk_set_records(self.h, first, recs.shape[0], abi.ptr(recs)), "kwk_set_records")
+
+    def delete(self, slots):
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        abi.check(abi.lib().kwk_delete(self.h, len(slots), abi.ptr(slots)), "kwk_delete")
+
+    def step(self, now_ns: int, seed: int, step: int):
+        abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
+
+    def sync(self):
+        abi.check(abi.lib().kwk_sync(self.h), "kwk_sync")
+
+    def fired(self) -> np.ndarray:
+        n = C.c_uint32()
+        L = abi.lib()
+        abi.check(L.kwk_fired(self.h, None, 0, C.byref(n)), "kwk_fired")
+        out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
+        if n.value:
+            abi.check(L.kwk_fired(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired")
+        return out
+
+    def stats(self) -> dict:
+        s = abi.StepStats()
+        abi.check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
+        return {"steps": s.steps, "matched": s.matched, "fired": s.fired,
+                "fired_per_stage": {self.p.names[i]: s.fired_per_stage[i] for i in range(len(self.p.names))}}
+
+    def read(self, first: int = 0, n: Optional[int] = None):
+        n = self.n - first if n is None else n
+        hot = np.zeros(n, dtype=abi.HOT_DTYPE)
+        dels = np.zeros(n, dtype=np.int64)
+        abi.check(abi.lib().kwk_read(self.h, first, n, abi.ptr(hot), abi.ptr(dels)), "kwk_read")
+        return hot, dels
+
+    # usage
+    def usage_config(self, node_ptr, usage_key, cpu_values, mem_values):
+        self._uargs = [np.ascontiguousarray(node_ptr, dtype=np.uint32), np.ascontiguousarray(usage_key, dtype=np.uint32),
+                       np.ascontiguousarray(cpu_values, dtype=np.float64),
+                       np.ascontiguousarray(mem_values, dtype=np.float64)]
+        np_, uk, cv, mv = self._uargs
+        self.n_nodes = len(np_) - 1
+        abi.check(abi.lib().kwk_usage_config(self.h, self.n_nodes, abi.ptr(np_), abi.ptr(uk), len(cv), abi.ptr(cv),
+                                             len(mv), abi.ptr(mv)), "kwk_usage_config")
+
+    def usage(self, now_ns: int):
+        abi.check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")
+
+    def usage_read(self):
+        node = np.zeros((self.n_nodes, 4), dtype=np.float64)
+        cl = np.zeros(2, dtype=np.float64)
+        abi.check(abi.lib().kwk_usage_read(self.h, abi.ptr(node), abi.ptr(cl)), "kwk_usage_read")
+        return node, cl
+
+    # timing
+    def event_record(self, idx: int):
+        abi.check(abi.lib().kwk_event_record(self.h, idx), "kwk_event_record")
+
+    def event_elapsed_ms(self, a: int, b: int) -> float:
+        ms = C.c_float()
+        abi.check(abi.lib().kwk_event_elapsed(self.h, a, b, C.byref(ms)), "kwk_event_elapsed")
+        return float(ms.value)

@@ -1,0 +1,133 @@
+"""ORACLE / TEST INFRASTRUCTURE — not product code.
+
+Reference-semantics cluster simulation on JSON objects, used to check the HIP engine
+step by step.  Per object and step it does exactly what the reference controllers do
+between watch events, in the engine's documented order:
+
+  harness churn  (bench/parity workload: re-create deleted objects, delete terminal ones)
+  match + delay  refcpu (C++ restatement of lifecycle.Match / Stage.Delay, with the Philox hook)
+                 on objects that changed since their last match (informer Modified event)
+  schedule       one pending job per object; a match replaces it, no match keeps it
+                 (pod_controller.go:222-229, addStageJob :660-671)
+  fire           due <= now: playStage's effect — finalizers JSON patch, delete, rendered
+                 merge patches (next.go, finalizers.go; rendering via the gotpl mirror that
+                 tests/ pins against the reference's golden outputs); an object whose
+                 patches changed it is re-matched next step (its Modified event)
+"""
+from __future__ import annotations
+
+import copy
+import json
+from typing import List, Optional, Sequence
+
+from kwok_amd.host.compiler import exploration_funcs, strip_for_recreate
+from kwok_amd.host.gotpl import Renderer, rfc3339nano
+from kwok_amd.host.nextstate import apply_next, prune_empty
+from kwok_amd.host.stages import Stage, to_v1alpha1
+
+from . import refcpu
+
+INT64_MAX = (1 << 63) - 1
+INT64_MIN = -(1 << 63)
+
+
+def sat_add(a: int, b: int) -> int:
+    return max(INT64_MIN, min(INT64_MAX, a + b))
+
+
+class OracleSim:
+    def __init__(self, stages: Sequence[Stage], objs: Sequence[dict], harness: bool = False,
+                 terminal=("Succeeded", "Failed"), slot_base: int = 0, kind_salt: int = 0):
+        self.stages = [s for s in stages if s.selector is not None]
+        self.lc = refcpu.Lifecycle([to_v1alpha1(s) for s in stages])
+        assert self.lc.names == [s.name for s in self.stages]
+        self.objs: List[Optional[dict]] = [prune_empty(copy.deepcopy(o)) for o in objs]
+        self.orig = [copy.deepcopy(o) for o in self.objs]
+        n = len(objs)
+        self.dirty = [True] * n
+        self.pending: List[Optional[int]] = [None] * n
+        self.due = [0] * n
+        self.gen = [0] * n
+        self.matcherr = [False] * n
+        self.harness = harness
+        self.terminal = set(terminal)
+        self.slot_base = slot_base
+        self.kind_salt = kind_salt
+
+    def _is_terminal(self, o) -> bool:
+        ph = refcpu.query(".status.phase", o) or []
+        return any(p in self.terminal for p in ph if isinstance(p, str))
+
+    def step(self, now_ns: int, seed: int, step: int):
+        key = seed ^ (self.kind_salt << 32)
+        renderer = Renderer(exploration_funcs(), now_ns=now_ns)
+        renderer.funcs["Now"] = lambda: rfc3339nano(now_ns)
+        fired = []
+        for i in range(len(self.objs)):
+            o = self.objs[i]
+            if self.harness:
+                if o is None:
+                    o = self.objs[i] = strip_for_recreate(self.orig[i])
+                    self.gen[i] += 1
+                    self.dirty[i] = True
+                    self.pending[i] = None
+                elif self._is_terminal(o) and "deletionTimestamp" not in o.get("metadata", {}):
+                    sec = now_ns // 10**9
+                    o.setdefault("metadata", {})["deletionTimestamp"] = rfc3339nano(sec * 10**9)
+                    self.dirty[i] = True
+            if o is None:
+                continue
+            if self.dirty[i]:
+                self.dirty[i] = False
+                self.matcherr[i] = False
+                s, d = self.lc.match(o, now_ns, key, step, self.slot_base + i)
+                if s == -2:
+                    self.matcherr[i] = True
+                elif s is not None:
+                    self.pending[i] = s
+                    self.due[i] = sat_add(now_ns, d)
+            s = self.pending[i]
+            if s is not None and self.due[i] <= now_ns:
+                self.pending[i] = None
+                o2, changed = apply_next(self.stages[s], copy.deepcopy(o), renderer)
+                flags = 0
+                if o2 is None:
+                    flags |= 1
+                    self.objs[i] = None
+                else:
+                    self.objs[i] = o2
+                    if changed:
+                        self.dirty[i] = True
+                        flags |= 2
+                fired.append((i, s, flags))
+        return fired
+
+    def deletion_s(self, i: int) -> int:
+        o = self.objs[i]
+        if o is None:
+            return INT64_MIN
+        ts = (o.get("metadata") or {}).get("deletionTimestamp")
+        if not ts:
+            return INT64_MIN
+        return refcpu.parse_rfc3339(ts)[0]
+
+
+def oracle_pred(desc: dict, obj: dict) -> int:
+    """Feature bits of a JSON object computed with the oracle's own jq (refcpu), from the
+    compiled feature table (KindProgram.describe())."""
+    pred = 0
+    for f in desc["features"]:
+        out = refcpu.query(f["query"], obj) or []
+        if not out:
+            continue
+        if f["present_bit"] is not None:
+            pred |= 1 << f["present_bit"]
+        for v, b in f["literals"].items():
+            if any((isinstance(d, str) and d == v) or (isinstance(d, bool) and ("true" if d else "false") == v)
+                   for d in out):
+                pred |= 1 << b
+    if desc["finalizer_other_bit"] is not None:
+        for x in (obj.get("metadata") or {}).get("finalizers") or []:
+            b = desc["finalizers"].get(x)
+            pred |= 1 << (desc["finalizer_other_bit"] if b is None else b)
+    return pred

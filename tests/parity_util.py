@@ -1,0 +1,82 @@
+"""Shared driver for the GPU parity tests: run the HIP engine and the oracle simulation
+side by side on the same seeded cluster and compare every step bit for bit."""
+from __future__ import annotations
+
+import numpy as np
+
+from kwok_amd.host import abi
+from kwok_amd.host.compiler import HarnessSpec, KindProgram
+from kwok_amd.host.engine import Engine, Ingest
+from kwok_amd.host.stages import load_stage_files
+from oracle.sim import OracleSim, oracle_pred
+
+NOW0 = 1_700_000_000 * 10**9
+
+
+def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0):
+    stages = load_stage_files(*stage_files)
+    prog = KindProgram(stages, HarnessSpec() if harness else None)
+    prog.explore(objs)
+    assert not prog.delta_conflicts, prog.delta_conflicts
+    ing = Ingest(prog)
+    hot, dels, rec, cls = ing.columns(objs)
+    eng = Engine(prog, capacity=max(1, len(objs)), kind_salt=kind_salt, slot_base=slot_base)
+    eng.load_stages()
+    eng.set_harness(harness)
+    eng.load(hot, dels, rec, cls, ing.record_array())
+    sim = OracleSim(stages, objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base)
+    return prog, eng, sim
+
+
+def compare_state(prog, eng, sim, step):
+    hot, dels = eng.read()
+    desc = prog.describe()
+    bad = []
+    for i, o in enumerate(sim.objs):
+        sched = int(hot["sched"][i])
+        alive = bool(sched & abi.F_ALIVE)
+        if alive != (o is not None):
+            bad.append((i, "alive", alive))
+            continue
+        if o is None:
+            continue
+        st = sched & 0xFF
+        exp_st = 0xFF if sim.pending[i] is None else sim.pending[i]
+        if st != exp_st:
+            bad.append((i, "stage", st, exp_st))
+        elif st != 0xFF and int(hot["due"][i]) != sim.due[i]:
+            bad.append((i, "due", int(hot["due"][i]), sim.due[i]))
+        p = oracle_pred(desc, o)
+        if int(hot["pred"][i]) != p:
+            bad.append((i, "pred", hex(int(hot["pred"][i])), hex(p)))
+        if int(dels[i]) != sim.deletion_s(i):
+            bad.append((i, "deletion", int(dels[i]), sim.deletion_s(i)))
+        if bool(sched & abi.F_DIRTY) != sim.dirty[i]:
+            bad.append((i, "dirty", bool(sched & abi.F_DIRTY), sim.dirty[i]))
+    assert not bad, f"step {step}: {len(bad)} mismatches, first: {bad[:8]}"
+
+
+def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True):
+    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt)
+    total = 0
+    per_stage = np.zeros(len(prog.names), dtype=np.int64)
+    try:
+        for k in range(steps):
+            now = NOW0 + k * dt_ns
+            eng.step(now, seed, k)
+            got = eng.fired()
+            exp = sim.step(now, seed, k)
+            g = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in got)
+            assert g == sorted(exp), f"step {k}: fired differ: device-only {sorted(set(g) - set(exp))[:8]} " \
+                                     f"oracle-only {sorted(set(exp) - set(g))[:8]}"
+            total += len(exp)
+            for _, s, _ in exp:
+                per_stage[s] += 1
+            if check_state:
+                compare_state(prog, eng, sim, k)
+        st = eng.stats()
+        assert st["fired"] == total
+        assert [st["fired_per_stage"][n] for n in prog.names] == list(per_stage)
+    finally:
+        eng.close()
+    return total, dict(zip(prog.names, per_stage.tolist()))

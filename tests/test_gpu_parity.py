@@ -1,0 +1,80 @@
+"""GPU parity: the HIP sweep kernel (through the C ABI) against the oracle simulation.
+
+Matched-stage choice, stage indices, due times (delay + Philox jitter), fired sets, the
+next-state feature bits, deletion timestamps and the dirty/re-match flag must be bit-exact
+at every step (BASELINE.json north_star)."""
+import numpy as np
+import pytest
+
+from kwok_amd import workload as W
+from tests.parity_util import run
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pod_fast_c1_mini():
+    """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods."""
+    cl = W.make_cluster("C1", 40, 400, seed=11)
+    objs = cl.pods.materialize()
+    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True)
+    assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
+
+
+def test_pod_general_c2_mini():
+    """C2 shape: pod-general + chaos, init containers, override annotations (valid and
+    invalid ints / durations / RFC3339), chaos labels, deletionTimestamps; weighted picks
+    and Philox jitter."""
+    cl = W.make_cluster("C2", 50, 600, seed=12)
+    objs = cl.pods.materialize()
+    total, per = run(cl.pod_stage_files, objs, steps=40, dt_ns=500 * 10**6, harness=True)
+    assert per["pod-create"] > 0 and per["pod-ready"] > 0 and per["pod-delete"] > 0
+    assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
+
+
+def test_node_fast_heartbeat():
+    cl = W.make_cluster("C1", 64, 64, seed=13)
+    objs = cl.nodes.materialize()
+    total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1)
+    assert per["node-initialize"] == 64 and per["node-heartbeat"] > 0
+
+
+def test_node_chaos_weights():
+    """node-not-ready (weight 10000) beside node-heartbeat (weight 0): weighted pick path."""
+    objs = [W.node_object(f"node-{i}", labels={"node-not-ready.stage.kwok.x-k8s.io": "true"} if i % 3 == 0 else None,
+                          annotations={"node-not-ready.stage.kwok.x-k8s.io/weight": str(i % 5)} if i % 2 else None)
+            for i in range(90)]
+    files = W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT + W.NODE_CHAOS)
+    run(files, objs, steps=25, dt_ns=3 * 10**9, kind_salt=1)
+
+
+def test_empty_and_single():
+    files = W.stage_paths(W.POD_FAST)
+    run(files, [W.pod_object("p0", "node-0")], steps=3, dt_ns=10**9)
+
+
+def test_weight_edge_cases():
+    """All-error weights (Intn over all), zero total with errors (subset pick), negative
+    total (Go panics: no schedule, KWK_F_MATCHERR)."""
+    base = W.pod_object("p", "node-0")
+    stages_yaml = []
+    objs = []
+    for i, (w1, w2) in enumerate([("abc", "xyz"), ("0", "bad"), ("-5", "2"), ("3", "4"), ("0", "0"), ("", "7")]):
+        o = W.pod_object(f"p{i}", "node-0", annotations={"a.w": w1, "b.w": w2})
+        objs.append(o)
+    import os
+    import tempfile
+    import yaml
+    d = tempfile.mkdtemp()
+    paths = []
+    for name, key in (("a", "a.w"), ("b", "b.w")):
+        st = {"apiVersion": "kwok.x-k8s.io/v1alpha1", "kind": "Stage", "metadata": {"name": name},
+              "spec": {"resourceRef": {"apiGroup": "v1", "kind": "Pod"},
+                       "selector": {"matchExpressions": [{"key": ".metadata.deletionTimestamp",
+                                                          "operator": "DoesNotExist"}]},
+                       "weight": 1, "weightFrom": {"expressionFrom": f'.metadata.annotations["{key}"]'},
+                       "delay": {"durationMilliseconds": 1000, "jitterDurationMilliseconds": 9000},
+                       "next": {"statusTemplate": "phase: Running\n"}}}
+        p = os.path.join(d, name + ".yaml")
+        yaml.safe_dump(st, open(p, "w"))
+        paths.append(p)
+    run(paths, objs * 20, steps=6, dt_ns=2 * 10**9)
