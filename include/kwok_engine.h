@@ -89,10 +89,13 @@ typedef struct {
 
 #define KWK_NEXT_DELETE (1u << 0)
 #define KWK_NEXT_IMMEDIATE (1u << 1)
-#define KWK_NEXT_PATCHES (1u << 2)     /* has rendered patches: a fire always re-matches */
+#define KWK_NEXT_PATCHES (1u << 2)     /* has rendered patches */
 #define KWK_NEXT_FIN (1u << 3)         /* has a finalizers op */
 #define KWK_NEXT_FIN_EMPTY (1u << 4)   /* finalizers.empty */
 #define KWK_NEXT_FIN_REMOVE (1u << 5)  /* finalizers.remove non-empty */
+#define KWK_NEXT_PATCH_STATIC (1u << 6) /* patches do not depend on Now: re-applying them to an object
+                                         * whose `applied_mask` bit is set changes nothing, so (as in
+                                         * the reference: no watch event) the object is not re-matched */
 
 typedef struct {
   /* selector: ((pred ^ eq_val) & eq_mask) == 0  AND  for k < n_any:
@@ -114,7 +117,7 @@ typedef struct {
   /* next */
   uint32_t flags;              /* KWK_NEXT_* */
   uint32_t fin_add, fin_remove;/* bits inside the table's fin_group_mask */
-  uint32_t pad;
+  uint32_t applied_mask;       /* KWK_NEXT_PATCH_STATIC: feature bit "patch already applied" */
 } kwk_stage_desc;
 
 typedef struct {
@@ -158,6 +161,7 @@ typedef struct {
   uint64_t steps;
   uint64_t matched;       /* objects (re)scheduled by a match */
   uint64_t fired;         /* stage transitions */
+  uint64_t bytes;         /* algorithmic bytes moved by the sweep */
   uint64_t fired_per_stage[KWK_MAX_STAGES];
 } kwk_step_stats;
 

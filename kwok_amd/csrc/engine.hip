@@ -35,7 +35,7 @@ constexpr int kObjPerThread = 16;
 constexpr int kTile = kBlock * kObjPerThread;   // objects per workgroup
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kWaveSeg = 64 * kObjPerThread;     // fired-record capacity per wave
-constexpr int kStatWords = 2 + KWK_MAX_STAGES;   // matched, fired, fired per stage
+constexpr int kStatWords = 3 + KWK_MAX_STAGES;   // matched, fired, algorithmic bytes, fired per stage
 
 thread_local std::string g_err;
 
@@ -179,6 +179,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
   kwk_fired_rec* __restrict__ seg = a.fired + wave_id * kWaveSeg;
   uint32_t seg_n = 0;         // wave-uniform
   uint32_t n_matched = 0;     // per lane
+  uint32_t n_bytes = 0;       // per lane: algorithmic bytes moved
 
 #pragma unroll 4
   for (int k = 0; k < kObjPerThread; ++k) {
@@ -192,6 +193,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     bool fire = false;
     uint32_t fire_stage = 0, fire_flags = 0;
 
+    if (in) n_bytes += 16;
     if (in && (sched & KWK_F_MANAGED)) {
       // ---------------- harness churn (never enabled by a production host)
       if (a.harness.enable) {
@@ -201,19 +203,23 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
           sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
                   (gen << KWK_GEN_SHIFT);
           a.del_s[i] = KWK_DEL_ABSENT;
+          n_bytes += 8;
           dirty_rec = true;
         } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
           pred |= a.harness.deletion_bit;
           int64_t s = a.now / 1000000000;
           if (a.now % 1000000000 < 0) s -= 1;
           a.del_s[i] = s;
+          n_bytes += 8;
           sched |= KWK_F_DIRTY;
           dirty_rec = true;
         }
       }
       if (sched & KWK_F_ALIVE) {
         const kwk_value* __restrict__ rec =
-            (sched & KWK_F_HASREC) ? a.values + (uint64_t)a.rec_idx[i] * a.value_slots : nullptr;
+            ((sched & KWK_F_HASREC) && (sched & KWK_F_DIRTY)) ? a.values + (uint64_t)a.rec_idx[i] * a.value_slots
+                                                              : nullptr;
+        if (rec) n_bytes += 4 + 16 * 3;  // record index + (at most) the picked stage's three entries
         // ---------------- match + pick + delay (preprocess)
         if (sched & KWK_F_DIRTY) {
           uint32_t m = 0;
@@ -274,8 +280,9 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
               const kwk_stage_desc& S = T->stages[pick];
               int64_t delay = 0;
               if (S.has_delay) {
-                const int64_t dels = (S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION)
-                                         ? a.del_s[i] : KWK_DEL_ABSENT;
+                const bool need_del = S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION;
+                const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;
+                if (need_del) n_bytes += 8;
                 const Getter d = eval_getter(S.delay_slot, S.delay_default, true, sched, rec, dels, a.now, true);
                 if (d.ok) {
                   delay = d.v;
@@ -308,7 +315,10 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
           fire = true;
           fire_stage = st;
           const uint32_t pre = pred;
-          bool rematch = (S.flags & KWK_NEXT_PATCHES) != 0;
+          // re-match iff the fire changed the object (its Modified watch event): always for
+          // Now-dependent patches, for Now-independent ones only if not already applied
+          bool rematch = (S.flags & KWK_NEXT_PATCHES) &&
+                         (!(S.flags & KWK_NEXT_PATCH_STATIC) || !(pre & S.applied_mask));
           if (S.flags & KWK_NEXT_FIN) {
             const uint32_t F = pre & fin_group;
             uint32_t F2;
@@ -325,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
             rematch = false;
           } else if (S.flags & KWK_NEXT_PATCHES) {
             const kwk_delta d = a.deltas[(uint32_t)a.cls[i] * n_stages + st];
+            n_bytes += 2;
             if (d.and_mask == KWK_DELTA_UNKNOWN_AND && d.or_mask == KWK_DELTA_UNKNOWN_OR) {
               fire_flags |= KWK_FIRED_DELTA_UNKNOWN;
             } else {
@@ -340,6 +351,8 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
         }
       }
     }
+    if (dirty_rec) n_bytes += 16;
+    if (fire) n_bytes += 8;
     if (dirty_rec)
       reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
 
@@ -348,20 +361,24 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     if (fire) {
       const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)fire_stage, (uint16_t)fire_flags};
-      atomicAdd(&s_stat[2 + fire_stage], 1u);
+      atomicAdd(&s_stat[3 + fire_stage], 1u);
     }
     seg_n += (uint32_t)__popcll(bal);
   }
 
   // per-wave fired count (read by kwk_fired's scan) and block statistics
-  for (int off = 32; off > 0; off >>= 1) n_matched += __shfl_xor(n_matched, off);
+  for (int off = 32; off > 0; off >>= 1) {
+    n_matched += __shfl_xor(n_matched, off);
+    n_bytes += __shfl_xor(n_bytes, off);
+  }
   if (lane == 0) {
     a.wave_counts[wave_id] = seg_n;
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], seg_n);
+    atomicAdd(&s_stat[2], n_bytes + 4u);  // + the wave's fired count word
   }
   __syncthreads();
-  if (threadIdx.x < 2 + n_stages) {
+  if (threadIdx.x < 3 + n_stages) {
     const unsigned int v = s_stat[threadIdx.x];
     if (v) a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x] += v;
   }
@@ -835,7 +852,8 @@ kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
   out->steps = e->steps;
   out->matched = h[0];
   out->fired = h[1];
-  for (int s = 0; s < KWK_MAX_STAGES; ++s) out->fired_per_stage[s] = h[2 + s];
+  out->bytes = h[2];
+  for (int s = 0; s < KWK_MAX_STAGES; ++s) out->fired_per_stage[s] = h[3 + s];
   return KWK_OK;
 }
 

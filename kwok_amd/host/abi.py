@@ -24,6 +24,7 @@ DEL_ABSENT = -(1 << 63)
 MAX_STAGES, MAX_ANY = 32, 4
 SLOT_NONE, SLOT_DELETION = -1, -2
 NEXT_DELETE, NEXT_IMMEDIATE, NEXT_PATCHES, NEXT_FIN, NEXT_FIN_EMPTY, NEXT_FIN_REMOVE = 1, 2, 4, 8, 16, 32
+NEXT_PATCH_STATIC = 64
 DELTA_UNKNOWN = (0, 0xFFFFFFFF)
 FIRED_DELETED, FIRED_REMATCH, FIRED_DELTA_UNKNOWN = 1, 2, 4
 
@@ -44,7 +45,7 @@ class StageDesc(C.Structure):
         ("has_delay", C.c_int32), ("delay_default", C.c_int64), ("delay_slot", C.c_int32),
         ("has_jitter", C.c_int32), ("jitter_default", C.c_int64), ("jitter_default_ok", C.c_int32),
         ("jitter_slot", C.c_int32),
-        ("flags", C.c_uint32), ("fin_add", C.c_uint32), ("fin_remove", C.c_uint32), ("pad", C.c_uint32),
+        ("flags", C.c_uint32), ("fin_add", C.c_uint32), ("fin_remove", C.c_uint32), ("applied_mask", C.c_uint32),
     ]
 
 
@@ -67,7 +68,7 @@ class FiredRec(C.Structure):
 
 
 class StepStats(C.Structure):
-    _fields_ = [("steps", C.c_uint64), ("matched", C.c_uint64), ("fired", C.c_uint64),
+    _fields_ = [("steps", C.c_uint64), ("matched", C.c_uint64), ("fired", C.c_uint64), ("bytes", C.c_uint64),
                 ("fired_per_stage", C.c_uint64 * MAX_STAGES)]
 
 

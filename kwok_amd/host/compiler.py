@@ -35,7 +35,7 @@ from . import abi
 from .goparse import f64_to_i64, parse_duration, parse_int, parse_rfc3339nano
 from .gotpl import Renderer, rfc3339nano
 from .jq import Query, has_value
-from .nextstate import apply_next, prune_empty
+from .nextstate import apply_next, merge_patch, json_patch, prune_empty, render_patches
 from .stages import Stage
 
 FIN_QUERIES = {".metadata.finalizers", ".metadata.finalizers.[]", ".metadata.finalizers[]"}
@@ -158,6 +158,10 @@ class KindProgram:
         self.deltas: Dict[Tuple[int, int], Tuple[int, int]] = {}
         self.delta_conflicts: List[str] = []
         self.rematch_mismatch: List[str] = []
+        # stages whose patches can leave an object unchanged (Now-independent templates):
+        # stage index -> synthetic feature bit "this stage's patch is already applied"
+        self.applied_bits: Dict[int, int] = {}
+        self._static_renderer = Renderer(exploration_funcs(), now_ns=1_700_000_000 * 10**9)
 
     # ------------------------------------------------------------------ bits
     def _bit(self) -> int:
@@ -360,7 +364,20 @@ class KindProgram:
             for x in (obj.get("metadata") or {}).get("finalizers") or []:
                 b = self.fin_bits.get(x)
                 pred |= 1 << (self.fin_other_bit if b is None else b)
+        for s, b in self.applied_bits.items():
+            if self._patch_applied(self.stages[s], obj):
+                pred |= 1 << b
         return pred
+
+    def _patch_applied(self, st: Stage, obj: dict) -> bool:
+        """True iff rendering + applying the stage's patches leaves the object unchanged."""
+        try:
+            cur = obj
+            for ptype, data, _ in render_patches(st, obj, self._static_renderer):
+                cur = prune_empty(json_patch(cur, data) if ptype == "json" else merge_patch(cur, data))
+        except Exception:
+            return False
+        return json.dumps(cur, sort_keys=True) == json.dumps(obj, sort_keys=True)
 
     def stage_matches(self, pred: int) -> int:
         m = 0
@@ -438,7 +455,28 @@ class KindProgram:
 
         Each root is expanded by firing every matching stage (any could be picked) and, if a
         harness is configured, its churn edges; transitions (pre -> post feature bits) are
-        collected per (class, stage) and turned into and/or masks."""
+        collected per (class, stage) and turned into and/or masks.  A first pass finds stages
+        whose patches can leave the object unchanged; they get an "applied" feature bit and
+        the exploration is redone with it."""
+        roots = list(roots)
+        self._roots = getattr(self, "_roots", []) + roots
+        for _ in range(2):
+            unchanged = self._explore_pass(self._roots, max_states)
+            new = [s for s in unchanged if s not in self.applied_bits]
+            if not new:
+                break
+            for s in new:
+                self.applied_bits[s] = self._bit()
+                d = self.stage_desc[s]
+                d.flags |= abi.NEXT_PATCH_STATIC
+                d.applied_mask = 1 << self.applied_bits[s]
+        self.rematch_mismatch = []
+
+    def _explore_pass(self, roots, max_states):
+        self.class_reps = {c: [] for c in self.class_reps}
+        self.deltas = {}
+        self.delta_conflicts = []
+        unchanged = set()
         trans: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
         renderer = Renderer(exploration_funcs())
         fin = self.fin_group_mask
@@ -470,8 +508,8 @@ class KindProgram:
                         t_ns += 10**9
                         renderer.funcs["Now"] = lambda t=t_ns: rfc3339nano(t)
                         o2, changed = apply_next(st, copy.deepcopy(o), renderer)
-                        if st.next.patches and not changed:
-                            self.rematch_mismatch.append(f"class {c} stage {st.name}: patch did not change the object")
+                        if st.next.patches and not changed and not st.next.delete:
+                            unchanged.add(s)
                         if o2 is None:
                             continue
                         p2 = self.pred_of(o2)
@@ -518,6 +556,7 @@ class KindProgram:
                     ok = False
                     self.delta_conflicts.append(f"class {c} stage {self.stages[s].name}: bit {b} depends on pre-state")
             self.deltas[(c, s)] = (and_m & 0xFFFFFFFF, or_m) if ok else abi.DELTA_UNKNOWN
+        return unchanged
 
     # ------------------------------------------------------------------ device tables
     def table(self, version: int = 1) -> abi.StageTable:
@@ -558,5 +597,6 @@ class KindProgram:
         for f in self.features.values():
             feats.append({"query": f.src, "present_bit": f.present_bit, "literals": dict(f.lit_bits)})
         return {"stages": self.names, "bits": self.nbits, "features": feats,
+                "applied_bits": {self.names[s]: b for s, b in self.applied_bits.items()},
                 "finalizers": dict(self.fin_bits), "finalizer_other_bit": self.fin_other_bit,
                 "value_slots": [list(s) for s in self.slots], "classes": len(self.class_ids)}

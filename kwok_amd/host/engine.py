@@ -189,7 +189,7 @@ class Engine:
     def stats(self) -> dict:
         s = abi.StepStats()
         abi.check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
-        return {"steps": s.steps, "matched": s.matched, "fired": s.fired,
+        return {"steps": s.steps, "matched": s.matched, "fired": s.fired, "bytes": s.bytes,
                 "fired_per_stage": {self.p.names[i]: s.fired_per_stage[i] for i in range(len(self.p.names))}}
 
     def read(self, first: int = 0, n: Optional[int] = None):

@@ -126,8 +126,10 @@ def apply_next(stage: Stage, obj: dict, renderer: Renderer):
     if stage.next.finalizers is not None:
         ops = finalizers_modify((obj.get("metadata") or {}).get("finalizers"), stage.next.finalizers)
         if ops:
-            obj = prune_empty(json_patch(obj, ops))
-            changed = True
+            new = prune_empty(json_patch(obj, ops))
+            # a watch event (and so a re-match) follows only if the object really changed
+            changed = json.dumps(new, sort_keys=True) != json.dumps(obj, sort_keys=True)
+            obj = new
     if stage.next.delete:
         return None, True
     for ptype, data, _sub in render_patches(stage, obj, renderer):
