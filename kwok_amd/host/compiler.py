@@ -514,6 +514,11 @@ class KindProgram:
                             continue
                         p2 = self.pred_of(o2)
                         trans.setdefault((c, s), []).append((p, p2))
+                        # an idempotent (Now-independent) patch: firing again changes nothing
+                        if st.next.patches and s not in self.applied_bits and (self.stage_matches(p2) >> s) & 1:
+                            _, again = apply_next(st, copy.deepcopy(o2), renderer)
+                            if not again:
+                                unchanged.add(s)
                         # finalizer set algebra must reproduce the JSON-patch result
                         d = self.stage_desc[s]
                         if d.flags & abi.NEXT_FIN:
