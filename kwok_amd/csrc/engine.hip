@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -31,10 +32,9 @@
 namespace {
 
 constexpr int kBlock = 256;              // 4 waves of 64
-constexpr int kObjPerThread = 16;
-constexpr int kTile = kBlock * kObjPerThread;   // objects per workgroup
+constexpr int kMinObjPerThread = 4;      // smallest sweep variant: sizes the per-block arrays
+constexpr int kMaxObjPerThread = 16;
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kWaveSeg = 64 * kObjPerThread;     // fired-record capacity per wave
 constexpr int kStatWords = 3 + KWK_MAX_STAGES;   // matched, fired, algorithmic bytes, fired per stage
 
 thread_local std::string g_err;
@@ -164,206 +164,278 @@ __device__ __forceinline__ int nth_bit(uint32_t m, int64_t n) {
   return __ffs(m) - 1;
 }
 
+struct Fire {      // what one object's step produced
+  bool fire;
+  uint32_t stage;
+  uint32_t flags;
+  uint32_t bytes;  // algorithmic bytes beyond the 16-byte record read
+};
+
+// match + weighted pick + delay for one dirty object (preprocess, pod_controller.go:196-254).
+// Updates sched (pending stage / MATCHERR) and due; returns true if a stage was scheduled.
+__device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
+                                             uint32_t n_stages, uint64_t i, uint32_t pred, uint32_t& sched,
+                                             int64_t& due, uint32_t& bytes) {
+  uint32_t m = 0;
+  for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+  sched &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
+  if (m == 0) return false;  // no match: a queued job stays queued (pod_controller.go:222-229)
+  const kwk_value* __restrict__ rec = nullptr;
+  if (sched & KWK_F_HASREC) {
+    rec = a.values + (uint64_t)a.rec_idx[i] * a.value_slots;
+    bytes += 4 + 16 * 3;  // record index + (at most) the picked stage's three entries
+  }
+  const uint64_t gslot = a.slot_base + i;
+  int pick;
+  const int cnt = __popc(m);
+  if (cnt == 1) {
+    pick = __ffs(m) - 1;
+  } else {
+    int64_t total = 0;
+    int nerr = 0, nge0 = 0;
+    for (uint32_t mm = m; mm; mm &= mm - 1) {
+      const Getter w = stage_weight(T->stages[__ffs(mm) - 1], sched, rec);
+      if (w.ok) {
+        total = (int64_t)((uint64_t)total + (uint64_t)w.v);
+        nge0 += w.v >= 0;
+      } else {
+        ++nerr;
+      }
+    }
+    if (nerr == cnt || (total == 0 && nerr == 0)) {
+      pick = nth_bit(m, rng_below(gslot, a.step, kSitePick, a.key, cnt));          // lifecycle.go:157,163
+    } else if (total == 0) {
+      int64_t want = rng_below(gslot, a.step, kSitePick, a.key, nge0);            // lifecycle.go:175
+      pick = -1;
+      for (uint32_t mm = m; mm; mm &= mm - 1) {
+        const int s = __ffs(mm) - 1;
+        const Getter w = stage_weight(T->stages[s], sched, rec);
+        if (w.ok && w.v >= 0) {
+          if (want == 0) { pick = s; break; }
+          --want;
+        }
+      }
+    } else if (total < 0) {
+      sched |= KWK_F_MATCHERR;  // rand.Int63n panics on n <= 0 in the reference
+      return false;
+    } else {
+      int64_t off = rng_below(gslot, a.step, kSitePick, a.key, total);            // lifecycle.go:180
+      pick = 31 - __clz(m);  // fallback: last matched stage (lifecycle.go:190)
+      for (uint32_t mm = m; mm; mm &= mm - 1) {
+        const int s = __ffs(mm) - 1;
+        const Getter w = stage_weight(T->stages[s], sched, rec);
+        const int64_t wv = w.ok ? w.v : -1;
+        if (wv <= 0) continue;
+        off -= wv;
+        if (off < 0) { pick = s; break; }
+      }
+    }
+  }
+  // Stage.Delay (lifecycle.go:313-341); controllers ignore `ok` (pod_controller.go:234)
+  const kwk_stage_desc& S = T->stages[pick];
+  int64_t delay = 0;
+  if (S.has_delay) {
+    const bool need_del = S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION;
+    const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;
+    if (need_del) bytes += 8;
+    const Getter d = eval_getter(S.delay_slot, S.delay_default, true, sched, rec, dels, a.now, true);
+    if (d.ok) {
+      delay = d.v;
+      if (S.has_jitter) {
+        const Getter j = eval_getter(S.jitter_slot, S.jitter_default, S.jitter_default_ok != 0, sched, rec, dels,
+                                     a.now, true);
+        if (j.ok) {
+          if (j.v < delay) {
+            delay = j.v;
+          } else {
+            const int64_t jit = (int64_t)((uint64_t)j.v - (uint64_t)delay);
+            if (jit > 0)
+              delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));
+          }
+        }
+      }
+    }
+  }
+  sched = (sched & ~0xFFu) | (uint32_t)pick;
+  due = sat_add(a.now, delay);  // addStageJob / AddWeightAfter (weight_delaying_queue.go:73-95)
+  return true;
+}
+
+// fire the pending stage (delay queue pop + playStage, pod_controller.go:257-360)
+__device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
+                                            uint32_t n_stages, uint32_t fin_group, uint64_t i, uint32_t st,
+                                            uint32_t& pred, uint32_t& sched, Fire& f) {
+  const kwk_stage_desc& S = T->stages[st];
+  f.fire = true;
+  f.stage = st;
+  const uint32_t pre = pred;
+  // re-match iff the fire changed the object (its Modified watch event): always for
+  // Now-dependent patches, for Now-independent ones only if not already applied
+  bool rematch = (S.flags & KWK_NEXT_PATCHES) && (!(S.flags & KWK_NEXT_PATCH_STATIC) || !(pre & S.applied_mask));
+  if (S.flags & KWK_NEXT_FIN) {  // finalizersModify (finalizers.go:83-111) as set algebra
+    const uint32_t F = pre & fin_group;
+    uint32_t F2;
+    if ((S.flags & KWK_NEXT_FIN_EMPTY) || ((S.flags & KWK_NEXT_FIN_REMOVE) && (F & ~S.fin_remove) == 0))
+      F2 = S.fin_add;
+    else
+      F2 = (F & ~S.fin_remove) | (S.fin_add & ~F);
+    rematch |= F2 != F;
+    pred = (pred & ~fin_group) | F2;
+  }
+  if (S.flags & KWK_NEXT_DELETE) {
+    sched &= ~KWK_F_ALIVE;
+    f.flags |= KWK_FIRED_DELETED;
+    rematch = false;
+  } else if (S.flags & KWK_NEXT_PATCHES) {
+    const kwk_delta d = a.deltas[(uint32_t)a.cls[i] * n_stages + st];
+    f.bytes += 2;
+    if (d.and_mask == KWK_DELTA_UNKNOWN_AND && d.or_mask == KWK_DELTA_UNKNOWN_OR)
+      f.flags |= KWK_FIRED_DELTA_UNKNOWN;
+    else
+      pred = (((pred & d.and_mask) | d.or_mask) & ~fin_group) | (pred & fin_group);
+  }
+  if (rematch) {
+    sched |= KWK_F_DIRTY;
+    f.flags |= KWK_FIRED_REMATCH;
+  }
+  sched |= KWK_STAGE_NONE;
+}
+
+// harness + match + fire for one object whose record needs work; writes the record back
+template <bool kHarness>
+__device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
+                                               uint32_t n_stages, uint32_t fin_group, uint64_t i, uint32_t pred,
+                                               uint32_t sched, int64_t due, Fire& f, uint32_t& n_matched) {
+  if (kHarness) {
+    if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
+      const uint32_t gen = (sched >> KWK_GEN_SHIFT) + 1u;
+      pred &= a.harness.keep_mask;
+      sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
+              (gen << KWK_GEN_SHIFT);
+      a.del_s[i] = KWK_DEL_ABSENT;
+      f.bytes += 8;
+    } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
+      pred |= a.harness.deletion_bit;  // the user deletes a finished pod
+      int64_t sec = a.now / 1000000000;
+      if (a.now % 1000000000 < 0) sec -= 1;
+      a.del_s[i] = sec;
+      f.bytes += 8;
+      sched |= KWK_F_DIRTY;
+    }
+  }
+  if (sched & KWK_F_ALIVE) {
+    if (sched & KWK_F_DIRTY) n_matched += match_object(a, T, n_stages, i, pred, sched, due, f.bytes) ? 1 : 0;
+    const uint32_t st = sched & 0xFFu;
+    if (st < n_stages && due <= a.now) fire_object(a, T, n_stages, fin_group, i, st, pred, sched, f);
+  }
+  reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
+  f.bytes += 16;
+}
+
+// does this record need any work this step?  (the idle majority fails every test)
+template <bool kHarness>
+__device__ __forceinline__ bool needs_work(const SweepArgs& a, uint32_t n_stages, uint32_t pred, uint32_t sched,
+                                           int64_t due) {
+  return (sched & KWK_F_MANAGED) &&
+         ((sched & KWK_F_DIRTY) || ((sched & 0xFFu) < n_stages && due <= a.now) ||
+          (kHarness && (!(sched & KWK_F_ALIVE) ||
+                        ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)))));
+}
+
+// wave-ballot compaction of the fired set into the wave's private segment + per-stage counts
+__device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t lane, kwk_fired_rec* __restrict__ seg,
+                                           uint32_t& seg_n, unsigned int* s_stat, uint32_t& n_bytes) {
+  const unsigned long long bal = __ballot(f.fire);
+  if (!bal) return;
+  if (f.fire) {
+    const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
+    n_bytes += 8;
+  }
+  seg_n += (uint32_t)__popcll(bal);
+  unsigned long long rest = bal;  // one LDS add per distinct fired stage in this wave-instruction
+  while (rest) {
+    const uint32_t s = __shfl(f.stage, __ffsll((long long)rest) - 1);
+    const unsigned long long same = __ballot(f.fire && f.stage == s);
+    if (lane == 0) atomicAdd(&s_stat[3 + s], (unsigned)__popcll(same));
+    rest &= ~same;
+  }
+}
+
+// One workgroup sweeps a tile of kBlock*K consecutive objects; each lane owns K of them at a
+// stride of kBlock, so every load instruction of a wave reads 1 KiB contiguously.
+//  * single-phase (K = 4): all K 16-byte records of a lane are loaded up front (K independent
+//    global_load_dwordx4 in flight) and processed from registers;
+//  * two-phase (K = 8, 16): phase 1 streams the K records and keeps only a K-bit "needs work"
+//    mask; phase 2 re-reads the (cache-resident) records that need work and processes them in a
+//    rolled loop — more bytes in flight without holding K records across the heavy path.
+template <bool kHarness, int K>
 __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+  constexpr bool kTwoPhase = K > 4;
   __shared__ unsigned int s_stat[kStatWords];
   const kwk_stage_table* __restrict__ T = a.table;
   const uint32_t n_stages = T->n_stages;
   const uint32_t fin_group = T->fin_group_mask;
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
-  __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
-  const uint64_t tile_base = (uint64_t)blockIdx.x * kTile;
+  const uint64_t base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64 + lane;
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  kwk_fired_rec* __restrict__ seg = a.fired + wave_id * kWaveSeg;
-  uint32_t seg_n = 0;         // wave-uniform
-  uint32_t n_matched = 0;     // per lane
-  uint32_t n_bytes = 0;       // per lane: algorithmic bytes moved
+  kwk_fired_rec* __restrict__ seg = a.fired + wave_id * (64 * K);
+  const uint4* __restrict__ hot4 = reinterpret_cast<const uint4*>(a.hot);
 
-#pragma unroll 4
-  for (int k = 0; k < kObjPerThread; ++k) {
-    const uint64_t i = tile_base + (uint64_t)k * kBlock + wave * 64 + lane;
-    const bool in = i < a.n;
-    // one 16-byte load per object (global_load_dwordx4)
-    const uint4 hv = in ? reinterpret_cast<const uint4*>(a.hot)[i] : make_uint4(0, 0, 0, 0);
-    uint32_t pred = hv.x, sched = hv.y;
-    int64_t due = (int64_t)(((uint64_t)hv.w << 32) | hv.z);
-    bool dirty_rec = false;
-    bool fire = false;
-    uint32_t fire_stage = 0, fire_flags = 0;
+  uint32_t seg_n = 0;      // wave-uniform
+  uint32_t n_matched = 0;  // per lane
+  uint32_t n_bytes = 0;    // per lane: algorithmic bytes moved
 
-    if (in) n_bytes += 16;
-    if (in && (sched & KWK_F_MANAGED)) {
-      // ---------------- harness churn (never enabled by a production host)
-      if (a.harness.enable) {
-        if (!(sched & KWK_F_ALIVE)) {
-          const uint32_t gen = (sched >> KWK_GEN_SHIFT) + 1u;
-          pred &= a.harness.keep_mask;
-          sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
-                  (gen << KWK_GEN_SHIFT);
-          a.del_s[i] = KWK_DEL_ABSENT;
-          n_bytes += 8;
-          dirty_rec = true;
-        } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
-          pred |= a.harness.deletion_bit;
-          int64_t s = a.now / 1000000000;
-          if (a.now % 1000000000 < 0) s -= 1;
-          a.del_s[i] = s;
-          n_bytes += 8;
-          sched |= KWK_F_DIRTY;
-          dirty_rec = true;
-        }
-      }
-      if (sched & KWK_F_ALIVE) {
-        const kwk_value* __restrict__ rec =
-            ((sched & KWK_F_HASREC) && (sched & KWK_F_DIRTY)) ? a.values + (uint64_t)a.rec_idx[i] * a.value_slots
-                                                              : nullptr;
-        if (rec) n_bytes += 4 + 16 * 3;  // record index + (at most) the picked stage's three entries
-        // ---------------- match + pick + delay (preprocess)
-        if (sched & KWK_F_DIRTY) {
-          uint32_t m = 0;
-          for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
-          sched &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
-          dirty_rec = true;
-          if (m != 0) {
-            const uint64_t gslot = a.slot_base + i;
-            int pick;
-            bool err = false;
-            const int cnt = __popc(m);
-            if (cnt == 1) {
-              pick = __ffs(m) - 1;
-            } else {
-              int64_t total = 0;
-              int nerr = 0, nge0 = 0;
-              for (uint32_t mm = m; mm; mm &= mm - 1) {
-                const Getter w = stage_weight(T->stages[__ffs(mm) - 1], sched, rec);
-                if (w.ok) {
-                  total = (int64_t)((uint64_t)total + (uint64_t)w.v);
-                  nge0 += w.v >= 0;
-                } else {
-                  ++nerr;
-                }
-              }
-              if (nerr == cnt || (total == 0 && nerr == 0)) {
-                pick = nth_bit(m, rng_below(gslot, a.step, kSitePick, a.key, cnt));
-              } else if (total == 0) {
-                int64_t want = rng_below(gslot, a.step, kSitePick, a.key, nge0);
-                pick = -1;
-                for (uint32_t mm = m; mm; mm &= mm - 1) {
-                  const int s = __ffs(mm) - 1;
-                  const Getter w = stage_weight(T->stages[s], sched, rec);
-                  if (w.ok && w.v >= 0) {
-                    if (want == 0) { pick = s; break; }
-                    --want;
-                  }
-                }
-              } else if (total < 0) {
-                err = true;  // rand.Int63n panics on n <= 0 in the reference
-                pick = -1;
-              } else {
-                int64_t off = rng_below(gslot, a.step, kSitePick, a.key, total);
-                pick = 31 - __clz(m);  // fallback: last matched stage
-                for (uint32_t mm = m; mm; mm &= mm - 1) {
-                  const int s = __ffs(mm) - 1;
-                  const Getter w = stage_weight(T->stages[s], sched, rec);
-                  const int64_t wv = w.ok ? w.v : -1;
-                  if (wv <= 0) continue;
-                  off -= wv;
-                  if (off < 0) { pick = s; break; }
-                }
-              }
-            }
-            if (err) {
-              sched |= KWK_F_MATCHERR;
-            } else {
-              const kwk_stage_desc& S = T->stages[pick];
-              int64_t delay = 0;
-              if (S.has_delay) {
-                const bool need_del = S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION;
-                const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;
-                if (need_del) n_bytes += 8;
-                const Getter d = eval_getter(S.delay_slot, S.delay_default, true, sched, rec, dels, a.now, true);
-                if (d.ok) {
-                  delay = d.v;
-                  if (S.has_jitter) {
-                    const Getter j = eval_getter(S.jitter_slot, S.jitter_default, S.jitter_default_ok != 0, sched,
-                                                 rec, dels, a.now, true);
-                    if (j.ok) {
-                      if (j.v < delay) {
-                        delay = j.v;
-                      } else {
-                        const int64_t jit = (int64_t)((uint64_t)j.v - (uint64_t)delay);
-                        if (jit > 0)
-                          delay = (int64_t)((uint64_t)delay +
-                                            (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));
-                      }
-                    }
-                  }
-                }
-              }
-              sched = (sched & ~0xFFu) | (uint32_t)pick;
-              due = sat_add(a.now, delay);
-              ++n_matched;
-            }
-          }
-        }
-        // ---------------- fire (delay queue pop + playStage)
-        const uint32_t st = sched & 0xFFu;
-        if (st < n_stages && due <= a.now) {
-          const kwk_stage_desc& S = T->stages[st];
-          fire = true;
-          fire_stage = st;
-          const uint32_t pre = pred;
-          // re-match iff the fire changed the object (its Modified watch event): always for
-          // Now-dependent patches, for Now-independent ones only if not already applied
-          bool rematch = (S.flags & KWK_NEXT_PATCHES) &&
-                         (!(S.flags & KWK_NEXT_PATCH_STATIC) || !(pre & S.applied_mask));
-          if (S.flags & KWK_NEXT_FIN) {
-            const uint32_t F = pre & fin_group;
-            uint32_t F2;
-            if ((S.flags & KWK_NEXT_FIN_EMPTY) || ((S.flags & KWK_NEXT_FIN_REMOVE) && (F & ~S.fin_remove) == 0))
-              F2 = S.fin_add;
-            else
-              F2 = (F & ~S.fin_remove) | (S.fin_add & ~F);
-            rematch |= F2 != F;
-            pred = (pred & ~fin_group) | F2;
-          }
-          if (S.flags & KWK_NEXT_DELETE) {
-            sched &= ~KWK_F_ALIVE;
-            fire_flags |= KWK_FIRED_DELETED;
-            rematch = false;
-          } else if (S.flags & KWK_NEXT_PATCHES) {
-            const kwk_delta d = a.deltas[(uint32_t)a.cls[i] * n_stages + st];
-            n_bytes += 2;
-            if (d.and_mask == KWK_DELTA_UNKNOWN_AND && d.or_mask == KWK_DELTA_UNKNOWN_OR) {
-              fire_flags |= KWK_FIRED_DELTA_UNKNOWN;
-            } else {
-              pred = (((pred & d.and_mask) | d.or_mask) & ~fin_group) | (pred & fin_group);
-            }
-          }
-          if (rematch) {
-            sched |= KWK_F_DIRTY;
-            fire_flags |= KWK_FIRED_REMATCH;
-          }
-          sched |= KWK_STAGE_NONE;
-          dirty_rec = true;
-        }
+  if constexpr (!kTwoPhase) {
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();  // s_stat initialised
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      const bool in = i < a.n;
+      const uint32_t pred = v[k].x, sched = v[k].y;
+      const int64_t due = (int64_t)(((uint64_t)v[k].w << 32) | v[k].z);
+      if (in) n_bytes += 16;
+      Fire f{false, 0, 0, 0};
+      if (in && needs_work<kHarness>(a, n_stages, pred, sched, due))
+        process_object<kHarness>(a, T, n_stages, fin_group, i, pred, sched, due, f, n_matched);
+      n_bytes += f.bytes;
+      emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
+    }
+  } else {
+    uint32_t work = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      if (i < a.n) {
+        const uint4 v = hot4[i];
+        n_bytes += 16;
+        const int64_t due = (int64_t)(((uint64_t)v.w << 32) | v.z);
+        if (needs_work<kHarness>(a, n_stages, v.x, v.y, due)) work |= 1u << k;
       }
     }
-    if (dirty_rec) n_bytes += 16;
-    if (fire) n_bytes += 8;
-    if (dirty_rec)
-      reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
-
-    // ---------------- wave-ballot compaction of the fired set into the wave's segment
-    const unsigned long long bal = __ballot(fire);
-    if (fire) {
-      const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-      seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)fire_stage, (uint16_t)fire_flags};
-      atomicAdd(&s_stat[3 + fire_stage], 1u);
+    __syncthreads();  // s_stat initialised
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+      if (!__ballot((work >> k) & 1u)) continue;  // wave-uniform skip
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      Fire f{false, 0, 0, 0};
+      if ((work >> k) & 1u) {
+        const uint4 v = hot4[i];  // re-read: served from L2 / Infinity Cache (not counted)
+        process_object<kHarness>(a, T, n_stages, fin_group, i, v.x, v.y, (int64_t)(((uint64_t)v.w << 32) | v.z), f,
+                                 n_matched);
+      }
+      n_bytes += f.bytes;
+      emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
-    seg_n += (uint32_t)__popcll(bal);
   }
 
   // per-wave fired count (read by kwk_fired's scan) and block statistics
@@ -379,20 +451,20 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
   }
   __syncthreads();
   if (threadIdx.x < 3 + n_stages) {
-    const unsigned int v = s_stat[threadIdx.x];
-    if (v) a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x] += v;
+    const unsigned int val = s_stat[threadIdx.x];
+    if (val) a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x] += val;
   }
 }
 
 // gather the per-wave fired segments into one dense list (offsets from an exclusive scan)
 __global__ void compact_fired_kernel(const kwk_fired_rec* __restrict__ fired, const uint32_t* __restrict__ counts,
-                                     const uint32_t* __restrict__ offsets, uint32_t n_waves,
+                                     const uint32_t* __restrict__ offsets, uint32_t n_waves, uint32_t wave_seg,
                                      kwk_fired_rec* __restrict__ out) {
   const uint32_t w = blockIdx.x;
   if (w >= n_waves) return;
   const uint32_t c = counts[w];
   const uint32_t o = offsets[w];
-  for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) out[o + j] = fired[(uint64_t)w * kWaveSeg + j];
+  for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) out[o + j] = fired[(uint64_t)w * wave_seg + j];
 }
 
 __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, uint32_t n_blocks,
@@ -530,6 +602,8 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0;
+  uint32_t objs_per_thread = 4;   // sweep variant (KWOK_SWEEP_OBJS = 4 | 8 | 16)
+  uint32_t last_objs = 4;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
@@ -601,7 +675,11 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->max_records = d->max_records ? d->max_records : 1;
   e->slot_base = d->slot_base;
   e->kind_salt = d->kind_salt;
-  e->n_blocks_cap = (d->capacity + kTile - 1) / kTile;
+  e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
+  if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
+    const int k = atoi(v);
+    if (k == 4 || k == 8 || k == 16) e->objs_per_thread = (uint32_t)k;
+  }
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
   const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
@@ -619,7 +697,8 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_cls, sizeof(uint16_t) * (size_t)e->capacity);
   ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
   ALLOC(e->d_table, sizeof(kwk_stage_table));
-  ALLOC(e->d_fired, sizeof(kwk_fired_rec) * n_waves * kWaveSeg);
+  ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
+                                              (size_t)kBlock * kMaxObjPerThread));
   ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
@@ -801,8 +880,16 @@ kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step)
   a.step = step;
   a.now = now_ns;
   a.harness = e->harness;
-  const uint32_t blocks = (e->n_active + kTile - 1) / kTile;
-  hipLaunchKernelGGL(sweep_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+  const uint32_t K = e->objs_per_thread;
+  const uint32_t tile = kBlock * K;
+  const uint32_t blocks = (e->n_active + tile - 1) / tile;
+  const bool h = e->harness.enable != 0;
+#define LAUNCH(HV, KV) hipLaunchKernelGGL((sweep_kernel<HV, KV>), dim3(blocks), dim3(kBlock), 0, e->stream, a)
+  if (K == 4) { if (h) LAUNCH(true, 4); else LAUNCH(false, 4); }
+  else if (K == 8) { if (h) LAUNCH(true, 8); else LAUNCH(false, 8); }
+  else { if (h) LAUNCH(true, 16); else LAUNCH(false, 16); }
+#undef LAUNCH
+  e->last_objs = K;
   HIP_TRY(hipGetLastError());
   e->last_blocks = blocks;
   ++e->steps;
@@ -832,7 +919,7 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (!out || total == 0) return KWK_OK;
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
   hipLaunchKernelGGL(compact_fired_kernel, dim3(n_waves), dim3(64), 0, e->stream, e->d_fired, e->d_wave_counts,
-                     e->d_wave_offsets, n_waves, e->d_compact);
+                     e->d_wave_offsets, n_waves, 64u * e->last_objs, e->d_compact);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -960,6 +1047,6 @@ kwk_status kwk_event_elapsed(kwk_engine* e, uint32_t a, uint32_t b, float* ms) {
 }
 
 uint32_t kwk_abi_version(void) { return 1u; }
-uint32_t kwk_tile_objects(void) { return (uint32_t)kTile; }
+uint32_t kwk_tile_objects(void) { return (uint32_t)(kBlock * kMinObjPerThread); }
 
 }  // extern "C"
