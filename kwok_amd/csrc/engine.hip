@@ -366,9 +366,11 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 // stride of kBlock, so every load instruction of a wave reads 1 KiB contiguously.
 //  * single-phase (K = 4): all K 16-byte records of a lane are loaded up front (K independent
 //    global_load_dwordx4 in flight) and processed from registers;
-//  * two-phase (K = 8, 16): phase 1 streams the K records and keeps only a K-bit "needs work"
-//    mask; phase 2 re-reads the (cache-resident) records that need work and processes them in a
-//    rolled loop — more bytes in flight without holding K records across the heavy path.
+//  * two-phase (K = 8, 16): phase 1 streams the K records and compacts the indices of those
+//    that need work into a per-wave LDS list (ballot + popcount); phase 2 re-reads those
+//    (cache-resident) records and runs the heavy match / fire path over the dense list, so
+//    each wave-instruction of it serves 64 objects instead of the ~6 that are active in a
+//    steady-state wave.
 template <bool kHarness, int K>
 __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
   constexpr bool kTwoPhase = K > 4;
@@ -411,24 +413,39 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
   } else {
-    uint32_t work = 0;
+    // phase 1: stream the K records; compact the (local index of) records that need work
+    // into the wave's LDS list with a ballot per wave-instruction
+    __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
+    uint16_t* __restrict__ wl = s_work[wave];
+    uint32_t n_work = 0;  // wave-uniform
+    uint4 v[K];           // all K loads in flight before the first is consumed
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint64_t i = base + (uint64_t)k * kBlock;
-      if (i < a.n) {
-        const uint4 v = hot4[i];
-        n_bytes += 16;
-        const int64_t due = (int64_t)(((uint64_t)v.w << 32) | v.z);
-        if (needs_work<kHarness>(a, n_stages, v.x, v.y, due)) work |= 1u << k;
-      }
+      v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();  // s_stat initialised
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < K; ++k) {
-      if (!__ballot((work >> k) & 1u)) continue;  // wave-uniform skip
       const uint64_t i = base + (uint64_t)k * kBlock;
+      bool need = false;
+      if (i < a.n) {
+        n_bytes += 16;
+        need = needs_work<kHarness>(a, n_stages, v[k].x, v[k].y, (int64_t)(((uint64_t)v[k].w << 32) | v[k].z));
+      }
+      const unsigned long long bal = __ballot(need);
+      if (need) wl[n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(k * 64 + lane);
+      n_work += (uint32_t)__popcll(bal);
+    }
+    __syncthreads();  // s_stat initialised; work lists written (each wave reads only its own)
+    // phase 2: the heavy path over the dense work list, 64 useful lanes per wave-instruction
+    const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
+    for (uint32_t c = 0; c < n_work; c += 64) {
+      const uint32_t j = c + lane;
       Fire f{false, 0, 0, 0};
-      if ((work >> k) & 1u) {
+      uint64_t i = 0;
+      if (j < n_work) {
+        const uint32_t w = wl[j];
+        i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
         const uint4 v = hot4[i];  // re-read: served from L2 / Infinity Cache (not counted)
         process_object<kHarness>(a, T, n_stages, fin_group, i, v.x, v.y, (int64_t)(((uint64_t)v.w << 32) | v.z), f,
                                  n_matched);
