@@ -145,6 +145,8 @@ typedef struct {
   uint32_t keep_mask;
   uint32_t terminal_mask;
   uint32_t deletion_bit;
+  uint32_t track_deletion;     /* maintain the deletion_s column (only if a stage reads it) */
+  uint32_t reserved[3];
 } kwk_harness;
 
 /* ------------------------------------------------------------------ fired records */

@@ -312,14 +312,18 @@ __device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_sta
       pred &= a.harness.keep_mask;
       sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
               (gen << KWK_GEN_SHIFT);
-      a.del_s[i] = KWK_DEL_ABSENT;
-      f.bytes += 8;
+      if (a.harness.track_deletion) {
+        a.del_s[i] = KWK_DEL_ABSENT;
+        f.bytes += 8;
+      }
     } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
       pred |= a.harness.deletion_bit;  // the user deletes a finished pod
       int64_t sec = a.now / 1000000000;
       if (a.now % 1000000000 < 0) sec -= 1;
-      a.del_s[i] = sec;
-      f.bytes += 8;
+      if (a.harness.track_deletion) {
+        a.del_s[i] = sec;
+        f.bytes += 8;
+      }
       sched |= KWK_F_DIRTY;
     }
   }
@@ -619,7 +623,7 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0;
-  uint32_t objs_per_thread = 4;   // sweep variant (KWOK_SWEEP_OBJS = 4 | 8 | 16)
+  uint32_t objs_per_thread = 8;   // sweep variant (KWOK_SWEEP_OBJS = 4 | 8 | 16)
   uint32_t last_objs = 4;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;

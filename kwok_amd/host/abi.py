@@ -60,7 +60,7 @@ class Delta(C.Structure):
 
 class Harness(C.Structure):
     _fields_ = [("enable", C.c_uint32), ("keep_mask", C.c_uint32), ("terminal_mask", C.c_uint32),
-                ("deletion_bit", C.c_uint32)]
+                ("deletion_bit", C.c_uint32), ("track_deletion", C.c_uint32), ("reserved", C.c_uint32 * 3)]
 
 
 class FiredRec(C.Structure):

@@ -595,7 +595,12 @@ class KindProgram:
             h.keep_mask = self.keep_mask
             h.terminal_mask = self.terminal_mask
             h.deletion_bit = self.deletion_bit
+            h.track_deletion = 1 if self.uses_deletion_column else 0
         return h
+
+    @property
+    def uses_deletion_column(self) -> bool:
+        return any(d.delay_slot == abi.SLOT_DELETION or d.jitter_slot == abi.SLOT_DELETION for d in self.stage_desc)
 
     def describe(self) -> dict:
         feats = []
@@ -604,4 +609,5 @@ class KindProgram:
         return {"stages": self.names, "bits": self.nbits, "features": feats,
                 "applied_bits": {self.names[s]: b for s, b in self.applied_bits.items()},
                 "finalizers": dict(self.fin_bits), "finalizer_other_bit": self.fin_other_bit,
-                "value_slots": [list(s) for s in self.slots], "classes": len(self.class_ids)}
+                "value_slots": [list(s) for s in self.slots], "classes": len(self.class_ids),
+                "uses_deletion_column": self.uses_deletion_column}

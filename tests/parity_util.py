@@ -50,7 +50,7 @@ def compare_state(prog, eng, sim, step):
         applied = sum(1 << b for b in desc["applied_bits"].values())  # checked through the REMATCH flag
         if int(hot["pred"][i]) & ~applied != p:
             bad.append((i, "pred", hex(int(hot["pred"][i])), hex(p)))
-        if int(dels[i]) != sim.deletion_s(i):
+        if desc["uses_deletion_column"] and int(dels[i]) != sim.deletion_s(i):
             bad.append((i, "deletion", int(dels[i]), sim.deletion_s(i)))
         if bool(sched & abi.F_DIRTY) != sim.dirty[i]:
             bad.append((i, "dirty", bool(sched & abi.F_DIRTY), sim.dirty[i]))
