@@ -22,6 +22,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+#ifndef KWOK_NT_LOADS
+#define KWOK_NT_LOADS 0
+#endif
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -263,8 +266,9 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
 
 // fire the pending stage (delay queue pop + playStage, pod_controller.go:257-360)
 __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
-                                            uint32_t n_stages, uint32_t fin_group, uint64_t i, uint32_t st,
-                                            uint32_t& pred, uint32_t& sched, Fire& f) {
+                                            const kwk_delta* __restrict__ deltas, uint32_t n_stages,
+                                            uint32_t fin_group, uint32_t cls, uint32_t st, uint32_t& pred,
+                                            uint32_t& sched, Fire& f) {
   const kwk_stage_desc& S = T->stages[st];
   f.fire = true;
   f.stage = st;
@@ -287,7 +291,7 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
     f.flags |= KWK_FIRED_DELETED;
     rematch = false;
   } else if (S.flags & KWK_NEXT_PATCHES) {
-    const kwk_delta d = a.deltas[(uint32_t)a.cls[i] * n_stages + st];
+    const kwk_delta d = deltas[cls * n_stages + st];
     f.bytes += 2;
     if (d.and_mask == KWK_DELTA_UNKNOWN_AND && d.or_mask == KWK_DELTA_UNKNOWN_OR)
       f.flags |= KWK_FIRED_DELTA_UNKNOWN;
@@ -304,8 +308,9 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
 // harness + match + fire for one object whose record needs work; writes the record back
 template <bool kHarness>
 __device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
-                                               uint32_t n_stages, uint32_t fin_group, uint64_t i, uint32_t pred,
-                                               uint32_t sched, int64_t due, Fire& f, uint32_t& n_matched) {
+                                               const kwk_delta* __restrict__ deltas, uint32_t n_stages,
+                                               uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
+                                               int64_t due, uint32_t cls, Fire& f, uint32_t& n_matched) {
   if (kHarness) {
     if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
       const uint32_t gen = (sched >> KWK_GEN_SHIFT) + 1u;
@@ -330,7 +335,7 @@ __device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_sta
   if (sched & KWK_F_ALIVE) {
     if (sched & KWK_F_DIRTY) n_matched += match_object(a, T, n_stages, i, pred, sched, due, f.bytes) ? 1 : 0;
     const uint32_t st = sched & 0xFFu;
-    if (st < n_stages && due <= a.now) fire_object(a, T, n_stages, fin_group, i, st, pred, sched, f);
+    if (st < n_stages && due <= a.now) fire_object(a, T, deltas, n_stages, fin_group, cls, st, pred, sched, f);
   }
   reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
   f.bytes += 16;
@@ -375,14 +380,26 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 //    (cache-resident) records and runs the heavy match / fire path over the dense list, so
 //    each wave-instruction of it serves 64 objects instead of the ~6 that are active in a
 //    steady-state wave.
+#ifndef KWOK_LB_WAVES
+#define KWOK_LB_WAVES 1
+#endif
+constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
+
 template <bool kHarness, int K>
-__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
   constexpr bool kTwoPhase = K > 4;
   __shared__ unsigned int s_stat[kStatWords];
+  __shared__ kwk_delta s_delta[kLdsDeltas];
   const kwk_stage_table* __restrict__ T = a.table;
   const uint32_t n_stages = T->n_stages;
   const uint32_t fin_group = T->fin_group_mask;
+  const uint32_t n_deltas = T->n_classes * n_stages;
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  const kwk_delta* __restrict__ deltas = a.deltas;
+  if (n_deltas <= kLdsDeltas) {
+    for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
+    deltas = s_delta;
+  }
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
@@ -412,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
       if (in) n_bytes += 16;
       Fire f{false, 0, 0, 0};
       if (in && needs_work<kHarness>(a, n_stages, pred, sched, due))
-        process_object<kHarness>(a, T, n_stages, fin_group, i, pred, sched, due, f, n_matched);
+        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, a.cls[i], f, n_matched);
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
@@ -426,7 +443,13 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint64_t i = base + (uint64_t)k * kBlock;
+#if KWOK_NT_LOADS
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 t = i < a.n ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(hot4) + i) : u32x4{0, 0, 0, 0};
+      v[k] = make_uint4(t.x, t.y, t.z, t.w);
+#else
       v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
+#endif
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -450,9 +473,10 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
       if (j < n_work) {
         const uint32_t w = wl[j];
         i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
-        const uint4 v = hot4[i];  // re-read: served from L2 / Infinity Cache (not counted)
-        process_object<kHarness>(a, T, n_stages, fin_group, i, v.x, v.y, (int64_t)(((uint64_t)v.w << 32) | v.z), f,
-                                 n_matched);
+        const uint4 v = hot4[i];         // re-read: served from L2 / Infinity Cache (not counted)
+        const uint32_t cls = a.cls[i];   // issued beside the record: no dependent round trip on fire
+        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v.x, v.y,
+                                 (int64_t)(((uint64_t)v.w << 32) | v.z), cls, f, n_matched);
       }
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);

@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libkwok_engine.so")
+LIB_PATH = os.environ.get("KWOK_ENGINE_LIB") or os.path.join(PKG, "lib", "libkwok_engine.so")
 
 KWK_OK, KWK_EINVAL, KWK_ECAP, KWK_EHIP, KWK_ESTATE = 0, -1, -2, -3, -4
 STAGE_NONE = 0xFF
