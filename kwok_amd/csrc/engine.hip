@@ -384,6 +384,7 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 #define KWOK_LB_WAVES 1
 #endif
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
+constexpr int kStash = 128;      // work-item records kept in LDS per wave (the rest are re-read)
 
 template <bool kHarness, int K>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
@@ -400,6 +401,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
     deltas = s_delta;
   }
+  __syncthreads();  // s_stat / s_delta initialised
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
@@ -419,7 +421,6 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       const uint64_t i = base + (uint64_t)k * kBlock;
       v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();  // s_stat initialised
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint64_t i = base + (uint64_t)k * kBlock;
@@ -434,10 +435,12 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
   } else {
-    // phase 1: stream the K records; compact the (local index of) records that need work
-    // into the wave's LDS list with a ballot per wave-instruction
+    // phase 1: stream the K records; compact the ones that need work into the wave's LDS list
+    // (ballot + popcount): the local index always, the record itself for the first kStash
     __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
+    __shared__ uint4 s_rec[kWavesPerBlock][kStash];
     uint16_t* __restrict__ wl = s_work[wave];
+    uint4* __restrict__ wr = s_rec[wave];
     uint32_t n_work = 0;  // wave-uniform
     uint4 v[K];           // all K loads in flight before the first is consumed
 #pragma unroll
@@ -460,11 +463,17 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
         need = needs_work<kHarness>(a, n_stages, v[k].x, v[k].y, (int64_t)(((uint64_t)v[k].w << 32) | v[k].z));
       }
       const unsigned long long bal = __ballot(need);
-      if (need) wl[n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(k * 64 + lane);
+      if (need) {
+        const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        wl[pos] = (uint16_t)(k * 64 + lane);
+        if (pos < kStash) wr[pos] = v[k];
+      }
       n_work += (uint32_t)__popcll(bal);
     }
-    __syncthreads();  // s_stat initialised; work lists written (each wave reads only its own)
-    // phase 2: the heavy path over the dense work list, 64 useful lanes per wave-instruction
+    // phase 2: the heavy path over the dense work list, 64 useful lanes per wave-instruction.
+    // Only this wave wrote its list: a wavefront-scope fence (no workgroup barrier) orders the
+    // cross-lane LDS hand-off.
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
     for (uint32_t c = 0; c < n_work; c += 64) {
       const uint32_t j = c + lane;
@@ -473,10 +482,10 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (j < n_work) {
         const uint32_t w = wl[j];
         i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
-        const uint4 v = hot4[i];         // re-read: served from L2 / Infinity Cache (not counted)
-        const uint32_t cls = a.cls[i];   // issued beside the record: no dependent round trip on fire
-        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v.x, v.y,
-                                 (int64_t)(((uint64_t)v.w << 32) | v.z), cls, f, n_matched);
+        const uint32_t cls = a.cls[i];                  // issued first: overlaps the LDS read
+        const uint4 v2 = j < kStash ? wr[j] : hot4[i];  // spill-over beyond the stash: cache re-read
+        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v2.x, v2.y,
+                                 (int64_t)(((uint64_t)v2.w << 32) | v2.z), cls, f, n_matched);
       }
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
