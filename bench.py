@@ -150,6 +150,7 @@ def main():
     ap.add_argument("--dt-ms", type=int, default=1000, help="simulated time per step")
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,6 +171,8 @@ def main():
     pods, nodes, (nlo, nhi, plo, phi) = build_engines(args.nodes, args.pods_per_node, rank, world, local_rank,
                                                       args.seed, args.job_frac)
     setup_s = time.perf_counter() - t_setup
+    if args.no_harness:
+        pods.set_harness(False)
     now0 = 1_700_000_000 * 10**9
     dt = args.dt_ms * 10**6
 
