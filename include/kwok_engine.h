@@ -60,11 +60,12 @@ typedef struct kwk_engine kwk_engine;
 #define KWK_F_MANAGED (1u << 10)      /* pod on a managed node / node managed by this kwok */
 #define KWK_F_HASREC (1u << 11)       /* has a value record (pre-parsed *From results) */
 #define KWK_F_MATCHERR (1u << 12)     /* last match hit a Go panic path (Int63n(<0)) */
-#define KWK_GEN_SHIFT 16              /* bits 16..31: generation (bumped on re-create) */
+#define KWK_CLASS_SHIFT 16            /* bits 16..31: the object's delta class (spec shape) */
+#define KWK_CLASS_MASK 0xFFFF0000u
 
 typedef struct {
   uint32_t pred;   /* feature bits (host-compiled predicate summary) */
-  uint32_t sched;  /* pending stage | flags | generation */
+  uint32_t sched;  /* pending stage | flags | delta class */
   int64_t due;     /* unix ns at which the pending stage fires */
 } kwk_hot;         /* 16 bytes, one per object slot */
 
@@ -186,7 +187,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 kwk_status kwk_load_stages(kwk_engine* eng, const kwk_stage_table* table, const kwk_delta* deltas);
 kwk_status kwk_set_harness(kwk_engine* eng, const kwk_harness* h);
 
-/* bulk column load of slots [0, n) from host arrays (initial list / informer Sync) */
+/* bulk column load of slots [0, n) from host arrays (initial list / informer Sync);
+ * cls[i] is stored in the upper half of hot[i].sched */
 kwk_status kwk_load(kwk_engine* eng, uint32_t n, const kwk_hot* hot, const int64_t* deletion_s,
                     const uint32_t* rec_idx, const uint16_t* cls, uint32_t n_records, const kwk_value* records);
 /* per-object upsert (Added / Modified events): scatter into the given slots, marks dirty */

@@ -133,7 +133,6 @@ struct SweepArgs {
   kwk_hot* __restrict__ hot;
   int64_t* __restrict__ del_s;
   const uint32_t* __restrict__ rec_idx;
-  const uint16_t* __restrict__ cls;
   const kwk_value* __restrict__ values;
   const kwk_stage_table* __restrict__ table;
   const kwk_delta* __restrict__ deltas;
@@ -313,10 +312,8 @@ __device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_sta
                                                int64_t due, uint32_t cls, Fire& f, uint32_t& n_matched) {
   if (kHarness) {
     if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
-      const uint32_t gen = (sched >> KWK_GEN_SHIFT) + 1u;
-      pred &= a.harness.keep_mask;
-      sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE |
-              (gen << KWK_GEN_SHIFT);
+      pred &= a.harness.keep_mask;  // same spec: class bits and record flag stay
+      sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC | KWK_CLASS_MASK)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE;
       if (a.harness.track_deletion) {
         a.del_s[i] = KWK_DEL_ABSENT;
         f.bytes += 8;
@@ -430,7 +427,8 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (in) n_bytes += 16;
       Fire f{false, 0, 0, 0};
       if (in && needs_work<kHarness>(a, n_stages, pred, sched, due))
-        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, a.cls[i], f, n_matched);
+        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, sched >> KWK_CLASS_SHIFT, f,
+                                 n_matched);
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
@@ -482,10 +480,9 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (j < n_work) {
         const uint32_t w = wl[j];
         i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
-        const uint32_t cls = a.cls[i];                  // issued first: overlaps the LDS read
         const uint4 v2 = j < kStash ? wr[j] : hot4[i];  // spill-over beyond the stash: cache re-read
         process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v2.x, v2.y,
-                                 (int64_t)(((uint64_t)v2.w << 32) | v2.z), cls, f, n_matched);
+                                 (int64_t)(((uint64_t)v2.w << 32) | v2.z), v2.y >> KWK_CLASS_SHIFT, f, n_matched);
       }
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
@@ -541,7 +538,6 @@ struct ScatterArgs {
   kwk_hot* hot;
   int64_t* del_s;
   uint32_t* rec_idx;
-  uint16_t* cls;
   const uint32_t* slots;
   const kwk_hot* s_hot;
   const int64_t* s_del;
@@ -556,11 +552,11 @@ __global__ void scatter_kernel(ScatterArgs a) {
   if (j >= a.n) return;
   const uint32_t i = a.slots[j];
   kwk_hot h = a.s_hot[j];
+  h.sched = (h.sched & ~KWK_CLASS_MASK) | ((uint32_t)a.s_cls[j] << KWK_CLASS_SHIFT);
   if (a.mark_dirty) h.sched |= KWK_F_DIRTY;
   a.hot[i] = h;
   a.del_s[i] = a.s_del[j];
   a.rec_idx[i] = a.s_rec[j];
-  a.cls[i] = a.s_cls[j];
 }
 
 __global__ void delete_kernel(kwk_hot* hot, const uint32_t* slots, uint32_t n) {
@@ -665,7 +661,6 @@ struct kwk_engine {
   kwk_hot* d_hot = nullptr;
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
-  uint16_t* d_cls = nullptr;
   kwk_value* d_values = nullptr;
   kwk_stage_table* d_table = nullptr;
   kwk_delta* d_deltas = nullptr;
@@ -748,7 +743,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_hot, sizeof(kwk_hot) * (size_t)e->capacity);
   ALLOC(e->d_del, sizeof(int64_t) * (size_t)e->capacity);
   ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
-  ALLOC(e->d_cls, sizeof(uint16_t) * (size_t)e->capacity);
   ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
   ALLOC(e->d_table, sizeof(kwk_stage_table));
   ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
@@ -778,7 +772,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (!e) return KWK_OK;
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_hot, e->d_del, e->d_rec, e->d_cls, e->d_values, e->d_table, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_hot, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf};
@@ -836,10 +830,14 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
   }
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(e->d_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  {  // the object's delta class lives in the upper half of its sched word
+    std::vector<kwk_hot> tmp(hot, hot + n);
+    for (uint32_t i = 0; i < n; ++i)
+      tmp[i].sched = (tmp[i].sched & ~KWK_CLASS_MASK) | ((uint32_t)cls[i] << KWK_CLASS_SHIFT);
+    HIP_TRY(hipMemcpy(e->d_hot, tmp.data(), sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_rec, rec, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_cls, cls, sizeof(uint16_t) * n, hipMemcpyHostToDevice));
   if (n_records)
     HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
                       hipMemcpyHostToDevice));
@@ -889,7 +887,7 @@ kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kw
     HIP_TRY(hipMemset(e->d_hot + e->n_active, 0, sizeof(kwk_hot) * (size_t)(max_slot + 1 - e->n_active)));
     e->n_active = max_slot + 1;
   }
-  ScatterArgs a{e->d_hot, e->d_del, e->d_rec, e->d_cls, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
+  ScatterArgs a{e->d_hot, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
   hipLaunchKernelGGL(scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -920,7 +918,6 @@ kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step)
   a.hot = e->d_hot;
   a.del_s = e->d_del;
   a.rec_idx = e->d_rec;
-  a.cls = e->d_cls;
   a.values = e->d_values;
   a.table = e->d_table;
   a.deltas = e->d_deltas;

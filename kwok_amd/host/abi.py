@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("KWOK_ENGINE_LIB") or os.path.join(PKG, "lib", "libkwo
 KWK_OK, KWK_EINVAL, KWK_ECAP, KWK_EHIP, KWK_ESTATE = 0, -1, -2, -3, -4
 STAGE_NONE = 0xFF
 F_ALIVE, F_DIRTY, F_MANAGED, F_HASREC, F_MATCHERR = 1 << 8, 1 << 9, 1 << 10, 1 << 11, 1 << 12
-GEN_SHIFT = 16
+CLASS_SHIFT = 16
+CLASS_MASK = 0xFFFF0000
 V_DEFAULT, V_OK, V_NOTOK, V_ABSTIME = 0, 1, 2, 3
 DEL_ABSENT = -(1 << 63)
 MAX_STAGES, MAX_ANY = 32, 4
