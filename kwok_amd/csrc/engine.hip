@@ -22,6 +22,12 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+#ifndef KWOK_GROUP
+#define KWOK_GROUP 0
+#endif
+#ifndef KWOK_EXP_NOFIRED
+#define KWOK_EXP_NOFIRED 0
+#endif
 #ifndef KWOK_NT_LOADS
 #define KWOK_NT_LOADS 0
 #endif
@@ -306,7 +312,7 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
 
 // harness + match + fire for one object whose record needs work; writes the record back
 template <bool kHarness>
-__device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
+__device__ __forceinline__ uint4 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
                                                int64_t due, uint32_t cls, Fire& f, uint32_t& n_matched) {
@@ -334,8 +340,8 @@ __device__ __forceinline__ void process_object(const SweepArgs& a, const kwk_sta
     const uint32_t st = sched & 0xFFu;
     if (st < n_stages && due <= a.now) fire_object(a, T, deltas, n_stages, fin_group, cls, st, pred, sched, f);
   }
-  reinterpret_cast<uint4*>(a.hot)[i] = make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
-  f.bytes += 16;
+  f.bytes += 16;  // the record write-back (done by the caller)
+  return make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
 }
 
 // does this record need any work this step?  (the idle majority fails every test)
@@ -355,7 +361,9 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   if (!bal) return;
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+#if !KWOK_EXP_NOFIRED
     seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
+#endif
     n_bytes += 8;
   }
   seg_n += (uint32_t)__popcll(bal);
@@ -427,8 +435,8 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (in) n_bytes += 16;
       Fire f{false, 0, 0, 0};
       if (in && needs_work<kHarness>(a, n_stages, pred, sched, due))
-        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, sched >> KWK_CLASS_SHIFT, f,
-                                 n_matched);
+        reinterpret_cast<uint4*>(a.hot)[i] = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched,
+                                                                      due, sched >> KWK_CLASS_SHIFT, f, n_matched);
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
@@ -437,6 +445,10 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     // (ballot + popcount): the local index always, the record itself for the first kStash
     __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
     __shared__ uint4 s_rec[kWavesPerBlock][kStash];
+#if KWOK_GROUP
+    __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
+    unsigned long long rowmask[K];                      // wave-uniform: which lanes of row k changed
+#endif
     uint16_t* __restrict__ wl = s_work[wave];
     uint4* __restrict__ wr = s_rec[wave];
     uint32_t n_work = 0;  // wave-uniform
@@ -465,7 +477,13 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
         const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
         wl[pos] = (uint16_t)(k * 64 + lane);
         if (pos < kStash) wr[pos] = v[k];
+#if KWOK_GROUP
+        s_pos[wave][k * 64 + lane] = (uint16_t)pos;
+#endif
       }
+#if KWOK_GROUP
+      rowmask[k] = bal;
+#endif
       n_work += (uint32_t)__popcll(bal);
     }
     // phase 2: the heavy path over the dense work list, 64 useful lanes per wave-instruction.
@@ -481,12 +499,43 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
         const uint32_t w = wl[j];
         i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
         const uint4 v2 = j < kStash ? wr[j] : hot4[i];  // spill-over beyond the stash: cache re-read
-        process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v2.x, v2.y,
-                                 (int64_t)(((uint64_t)v2.w << 32) | v2.z), v2.y >> KWK_CLASS_SHIFT, f, n_matched);
+        const uint4 nv = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v2.x, v2.y,
+                                                  (int64_t)(((uint64_t)v2.w << 32) | v2.z), v2.y >> KWK_CLASS_SHIFT,
+                                                  f, n_matched);
+#if KWOK_GROUP
+        if (j < kStash) wr[j] = nv;  // written back in phase 3 together with its neighbours
+        else
+#endif
+          reinterpret_cast<uint4*>(a.hot)[i] = nv;
       }
       n_bytes += f.bytes;
       emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
     }
+#if KWOK_GROUP
+    // phase 3: write back whole groups of KWOK_GROUP neighbouring records (one full 16*G-byte
+    // segment per group) wherever any of them changed: full-granule writes instead of
+    // scattered 16-byte partial writes.
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    constexpr unsigned long long kGrpMask = (1ull << KWOK_GROUP) - 1ull;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const unsigned long long rm = rowmask[k];
+      if (!rm) continue;
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
+      if (i < a.n && ((rm >> g0) & kGrpMask)) {
+        uint4 val = v[k];
+        bool write = true;
+        if ((rm >> lane) & 1ull) {
+          const uint32_t p = s_pos[wave][k * 64 + lane];
+          if (p < kStash) val = wr[p]; else write = false;  // overflow items were written in phase 2
+        } else {
+          n_bytes += 16;  // an unchanged neighbour rewritten to complete the group
+        }
+        if (write) reinterpret_cast<uint4*>(a.hot)[i] = val;
+      }
+    }
+#endif
   }
 
   // per-wave fired count (read by kwk_fired's scan) and block statistics
