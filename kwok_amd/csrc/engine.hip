@@ -22,8 +22,13 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+// record write-back in groups of KWOK_GROUP neighbours (0 = per record); KEEP = keep the
+// streamed records in VGPRs for it (measured fastest on MI355X, profiles/r1/README.md)
 #ifndef KWOK_GROUP
-#define KWOK_GROUP 0
+#define KWOK_GROUP 4
+#endif
+#ifndef KWOK_GROUP_KEEP
+#define KWOK_GROUP_KEEP 1
 #endif
 #ifndef KWOK_EXP_NOFIRED
 #define KWOK_EXP_NOFIRED 0
@@ -524,12 +529,17 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       const uint64_t i = base + (uint64_t)k * kBlock;
       const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
       if (i < a.n && ((rm >> g0) & kGrpMask)) {
-        uint4 val = v[k];
+        uint4 val;
         bool write = true;
         if ((rm >> lane) & 1ull) {
           const uint32_t p = s_pos[wave][k * 64 + lane];
           if (p < kStash) val = wr[p]; else write = false;  // overflow items were written in phase 2
         } else {
+#if KWOK_GROUP_KEEP
+          val = v[k];
+#else
+          val = hot4[i];  // unchanged neighbour: re-read from cache (it was streamed in phase 1)
+#endif
           n_bytes += 16;  // an unchanged neighbour rewritten to complete the group
         }
         if (write) reinterpret_cast<uint4*>(a.hot)[i] = val;
