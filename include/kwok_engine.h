@@ -222,6 +222,10 @@ kwk_status kwk_usage(kwk_engine* eng, int64_t now_ns);
 /* node_out: n_nodes x {cpu, mem, cpu_cumulative, mem_cumulative}; cluster_out: {cpu, mem} */
 kwk_status kwk_usage_read(kwk_engine* eng, double* node_out, double* cluster_out);
 
+/* cluster aggregates: counts[k] = alive objects with (pred & masks[k]) != 0 (mask 0 = all
+ * alive objects), k < 16 — e.g. the phase histogram all-reduced across GPUs (synchronises) */
+kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);
+
 /* raw device pointers for in-process consumers (RCCL aggregates, profiling) */
 kwk_status kwk_device_ptrs(kwk_engine* eng, void** hot, void** fired, void** wave_counts);
 

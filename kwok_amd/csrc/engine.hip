@@ -663,7 +663,8 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict
       node_out[node * 4 + 1] = m;
       const int64_t lt = last_t[node];
       if (lt != INT64_MIN) {
-        const double dt = (double)(now - lt) / 1e9;  // now.Sub(c.time).Seconds()
+        const int64_t d = now - lt;  // now.Sub(c.time).Seconds() (time.Duration.Seconds)
+        const double dt = (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
         cum[node * 2 + 0] += dt * c;
         cum[node * 2 + 1] += dt * m;
       }
@@ -684,6 +685,37 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict
     block_part[blockIdx.x * 2 + 0] = tc;
     block_part[blockIdx.x * 2 + 1] = tm;
   }
+}
+
+// count alive objects with (pred & mask[k]) != 0 for each k (mask 0: every alive object):
+// phase histograms and other cluster aggregates.  One wave per 64*16 objects; per-block LDS
+// totals, one 64-bit atomic per block and mask.
+constexpr int kMaxCountMasks = 16;
+__global__ __launch_bounds__(kBlock) void count_kernel(const kwk_hot* __restrict__ hot, uint32_t n,
+                                                       const uint32_t* __restrict__ masks, uint32_t n_masks,
+                                                       unsigned long long* __restrict__ out) {
+  __shared__ unsigned int s_cnt[kMaxCountMasks];
+  if (threadIdx.x < kMaxCountMasks) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint4* __restrict__ hot4 = reinterpret_cast<const uint4*>(hot);
+  uint32_t cnt[kMaxCountMasks];
+  for (int m = 0; m < kMaxCountMasks; ++m) cnt[m] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * (kBlock * 16) + threadIdx.x;
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    if (i >= n) break;
+    const uint4 v = hot4[i];
+    if (!(v.y & KWK_F_ALIVE)) continue;
+    for (uint32_t m = 0; m < n_masks; ++m) cnt[m] += (masks[m] == 0 || (v.x & masks[m])) ? 1u : 0u;
+  }
+  for (uint32_t m = 0; m < n_masks; ++m) {
+    uint32_t c = cnt[m];
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
+  }
+  __syncthreads();
+  if (threadIdx.x < n_masks && s_cnt[threadIdx.x]) atomicAdd(&out[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
 }
 
 __global__ void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks, double* __restrict__ out) {
@@ -1124,6 +1156,27 @@ kwk_status kwk_usage_read(kwk_engine* e, double* node_out, double* cluster_out) 
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (node_out && e->n_nodes) HIP_TRY(hipMemcpy(node_out, e->d_node_out, 32 * (size_t)e->n_nodes, hipMemcpyDeviceToHost));
   if (cluster_out) HIP_TRY(hipMemcpy(cluster_out, e->d_cluster, 16, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uint64_t* counts) {
+  if (!e || (n_masks && (!masks || !counts))) return fail(KWK_EINVAL, "null argument");
+  if (n_masks > kMaxCountMasks) return fail(KWK_EINVAL, "at most 16 masks");
+  if (n_masks == 0) return KWK_OK;
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = ensure_stage_buf(e, 4 * kMaxCountMasks + 8 * kMaxCountMasks)) return st;
+  uint32_t* d_masks = (uint32_t*)e->d_stage_buf;
+  unsigned long long* d_out = (unsigned long long*)((char*)e->d_stage_buf + 4 * kMaxCountMasks);
+  HIP_TRY(hipMemcpyAsync(d_masks, masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemsetAsync(d_out, 0, 8 * kMaxCountMasks, e->stream));
+  if (e->n_active) {
+    const uint32_t blocks = (e->n_active + kBlock * 16 - 1) / (kBlock * 16);
+    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_hot, e->n_active, d_masks, n_masks,
+                       d_out);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(counts, d_out, 8 * (size_t)n_masks, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 

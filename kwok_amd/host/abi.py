@@ -91,7 +91,7 @@ EXPORTS = [
     "kwk_last_error", "kwk_engine_create", "kwk_engine_destroy", "kwk_load_stages", "kwk_set_harness", "kwk_load",
     "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
-    "kwk_abi_version", "kwk_tile_objects",
+    "kwk_abi_version", "kwk_tile_objects", "kwk_count",
 ]
 
 _lib = None
@@ -136,6 +136,7 @@ def lib():
     L.kwk_device_ptrs.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_event_record.argtypes = [C.c_void_p, C.c_uint32]
     L.kwk_event_elapsed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, _p(C.c_float)]
+    L.kwk_count.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
     L.kwk_abi_version.restype = C.c_uint32
     L.kwk_tile_objects.restype = C.c_uint32
     for name in EXPORTS:

@@ -1,0 +1,76 @@
+"""Multi-GPU layout: nodes sharded in contiguous blocks, pods colocated with their node.
+
+Every Stage decision reads one object's own columns, so a step needs no communication
+between GPUs.  Random draws are keyed by the GLOBAL object slot
+(``slot_base`` of each engine), so any sharding of a cluster reproduces the single-GPU run bit
+for bit.  The only collective is the all-reduce of the small cluster aggregates below (RCCL
+over xGMI with the "nccl" backend on ROCm; gloo in the CPU tests), once per reporting
+interval.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+
+def node_block(n_nodes: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous node block of `rank`: [n*r/W, n*(r+1)/W)."""
+    return n_nodes * rank // world, n_nodes * (rank + 1) // world
+
+
+def pod_range(node_ptr: np.ndarray, node_lo: int, node_hi: int) -> Tuple[int, int]:
+    """Node-sorted pods: node j owns [node_ptr[j], node_ptr[j+1])."""
+    return int(node_ptr[node_lo]), int(node_ptr[node_hi])
+
+
+def local_node_ptr(node_ptr: np.ndarray, node_lo: int, node_hi: int) -> np.ndarray:
+    return (node_ptr[node_lo:node_hi + 1] - node_ptr[node_lo]).astype(np.uint32)
+
+
+@dataclass
+class Aggregates:
+    """Cluster-wide counters summed over GPUs (one all-reduce of < 1 KB)."""
+    stage_names: List[str]
+    fired_per_stage: np.ndarray                 # int64 [n_stages]
+    counts: np.ndarray                          # int64 [n_counts] (phase histogram, ready nodes, ...)
+    count_names: List[str] = field(default_factory=list)
+    usage: np.ndarray = field(default_factory=lambda: np.zeros(2))  # cpu, memory (float64)
+
+    def pack(self) -> np.ndarray:
+        return np.concatenate([self.fired_per_stage.astype(np.float64), self.counts.astype(np.float64),
+                               self.usage.astype(np.float64)])
+
+    def unpack(self, v: np.ndarray) -> "Aggregates":
+        ns, nc = len(self.fired_per_stage), len(self.counts)
+        return Aggregates(self.stage_names, np.rint(v[:ns]).astype(np.int64), np.rint(v[ns:ns + nc]).astype(np.int64),
+                          self.count_names, v[ns + nc:ns + nc + 2].copy())
+
+    def allreduce(self, dist, device=None) -> "Aggregates":
+        """Sum over all ranks.  float64 carries counts exactly up to 2^53."""
+        if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+            return self
+        import torch
+        t = torch.from_numpy(self.pack())
+        if device is not None:
+            t = t.to(device)
+        dist.all_reduce(t)
+        return self.unpack(t.cpu().numpy())
+
+    def as_dict(self) -> dict:
+        return {"fired_per_stage": dict(zip(self.stage_names, self.fired_per_stage.tolist())),
+                "counts": dict(zip(self.count_names, self.counts.tolist())),
+                "usage": {"cpu": float(self.usage[0]), "memory": float(self.usage[1])}}
+
+
+def phase_masks(program, query: str = ".status.phase", values: Sequence[str] = ()) -> Dict[str, int]:
+    """pred masks for a phase histogram from the compiled feature bits (only phases some stage
+    or the harness names are interned; everything else falls into 'other')."""
+    out: Dict[str, int] = {}
+    f = program.features.get(query.replace(" ", ""))
+    lits = dict(f.lit_bits) if f is not None else {}
+    for v in values or sorted(lits):
+        if v in lits:
+            out[v] = 1 << lits[v]
+    return out

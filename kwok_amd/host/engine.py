@@ -199,6 +199,13 @@ class Engine:
         abi.check(abi.lib().kwk_read(self.h, first, n, abi.ptr(hot), abi.ptr(dels)), "kwk_read")
         return hot, dels
 
+    def count(self, masks) -> np.ndarray:
+        """kwk_count: alive objects with (pred & mask) != 0 per mask (0 = all alive)."""
+        m = np.ascontiguousarray(masks, dtype=np.uint32)
+        out = np.zeros(len(m), dtype=np.uint64)
+        abi.check(abi.lib().kwk_count(self.h, len(m), abi.ptr(m), abi.ptr(out)), "kwk_count")
+        return out
+
     # usage
     def usage_config(self, node_ptr, usage_key, cpu_values, mem_values):
         self._uargs = [np.ascontiguousarray(node_ptr, dtype=np.uint32), np.ascontiguousarray(usage_key, dtype=np.uint32),

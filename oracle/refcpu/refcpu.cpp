@@ -17,6 +17,7 @@
 // in DESIGN.md §RNG (key = seed, counter = (global slot, step lo, step hi, site)), so this
 // oracle and the HIP engine are bit-comparable.
 #include <atomic>
+#include <cmath>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -679,3 +680,131 @@ int64_t rc_match_batch(void* lcp, const char* blob, const int64_t* offsets, int6
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- resource.Quantity
+// k8s.io/apimachinery v0.30.2 api/resource/quantity.go ParseQuantity + AsApproximateFloat64
+// (dependency not vendored in the reference; restated from its published source).  Exact
+// arithmetic in __int128: inputs whose Dec-path magnitude exceeds ~1e29 are reported as
+// out of the oracle's range (-1).
+namespace refcpu {
+static double go_pow10(int n) {
+  static const double tab[32] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22, 1e23, 1e24, 1e25, 1e26, 1e27, 1e28, 1e29,
+                                 1e30, 1e31};
+  static const double pos32[10] = {1e0, 1e32, 1e64, 1e96, 1e128, 1e160, 1e192, 1e224, 1e256, 1e288};
+  static const double neg32[11] = {1e-0, 1e-32, 1e-64, 1e-96, 1e-128, 1e-160, 1e-192, 1e-224, 1e-256, 1e-288, 1e-320};
+  if (n >= 0 && n <= 308) return pos32[n / 32] * tab[n % 32];
+  if (n < 0 && n >= -323) return neg32[(-n) / 32] / tab[(-n) % 32];
+  return n > 0 ? HUGE_VAL : 0.0;
+}
+// returns 1 ok, 0 parse error, -1 outside the oracle's exact range
+static int quantity_f64(const std::string& s, double& out) {
+  out = 0;
+  if (s.empty()) return 0;
+  if (s == "0") return 1;
+  size_t pos = 0, end = s.size();
+  bool positive = true;
+  if (s[0] == '-') { positive = false; pos = 1; } else if (s[0] == '+') pos = 1;
+  const size_t sign_end = pos;
+  while (pos < end && s[pos] == '0') ++pos;
+  if (pos >= end) return 1;  // all zeros
+  size_t ns = pos;
+  while (pos < end && isdigit((unsigned char)s[pos])) ++pos;
+  std::string num = s.substr(ns, pos - ns), denom;
+  if (num.empty()) num = "0";
+  if (pos < end && s[pos] == '.') {
+    ++pos;
+    size_t ds = pos;
+    while (pos < end && isdigit((unsigned char)s[pos])) ++pos;
+    denom = s.substr(ds, pos - ds);
+  }
+  std::string suf = s.substr(pos);
+  {  // suffix grammar: [eEinumkKMGTP]* [+-]? [0-9]*
+    size_t k = 0;
+    while (k < suf.size() && strchr("eEinumkKMGTP", suf[k])) ++k;
+    if (k < suf.size() && (suf[k] == '+' || suf[k] == '-')) ++k;
+    while (k < suf.size() && isdigit((unsigned char)suf[k])) ++k;
+    if (k != suf.size()) return 0;
+  }
+  int base, exponent;
+  bool binary = false;
+  static const char* dn[] = {"n", "u", "m", "", "k", "M", "G", "T", "P", "E"};
+  static const int de[] = {-9, -6, -3, 0, 3, 6, 9, 12, 15, 18};
+  static const char* bn[] = {"Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
+  bool found = false;
+  for (int k = 0; k < 10 && !found; ++k) if (suf == dn[k]) { base = 10; exponent = de[k]; found = true; }
+  for (int k = 0; k < 6 && !found; ++k) if (suf == bn[k]) { base = 2; exponent = 10 * (k + 1); binary = true; found = true; }
+  if (!found) {
+    if (suf.size() > 1 && (suf[0] == 'e' || suf[0] == 'E')) {
+      int64_t e;
+      std::string body = suf.substr(1);
+      // strconv.ParseInt(body, 10, 64)
+      bool neg = false;
+      size_t k = 0;
+      if (!body.empty() && (body[0] == '+' || body[0] == '-')) { neg = body[0] == '-'; k = 1; }
+      if (k >= body.size()) return 0;
+      unsigned __int128 acc = 0;
+      for (; k < body.size(); ++k) { if (!isdigit((unsigned char)body[k])) return 0; acc = acc * 10 + (body[k] - '0'); if (acc > ((unsigned __int128)1 << 64)) return 0; }
+      if ((!neg && acc > (unsigned __int128)INT64_MAX) || (neg && acc > ((unsigned __int128)1 << 63))) return 0;
+      e = neg ? -(int64_t)(uint64_t)acc : (int64_t)(uint64_t)acc;
+      base = 10;
+      exponent = (int32_t)(uint32_t)(uint64_t)e;
+    } else {
+      return 0;
+    }
+  }
+  int precision, scale;
+  __int128 mantissa = 1;
+  if (!binary) {
+    scale = exponent;
+    precision = 18 - (int)(num.size() + denom.size());
+  } else {
+    scale = 0;
+    if (exponent >= 0 && denom.empty()) {
+      mantissa = (__int128)1 << exponent;
+      precision = 15 - (int)num.size() - (int)((float)exponent * 3.0f / 10.0f) - 1;
+    } else {
+      precision = -1;
+    }
+  }
+  if (precision >= 0) {
+    scale -= (int)denom.size();
+    if (scale >= -9) {
+      std::string sh = num + denom;
+      unsigned __int128 v = 0;
+      for (char c : sh) { v = v * 10 + (c - '0'); if (v > (unsigned __int128)INT64_MAX) return 0; }
+      __int128 r = (__int128)v * mantissa;
+      if (r <= (__int128)INT64_MAX) {
+        int64_t res = positive ? (int64_t)r : -(int64_t)r;
+        out = scale == 0 ? (double)res : (double)res * go_pow10(scale);
+        return 1;
+      }
+    }
+  }
+  // inf.Dec path: amount = (num.denom) * base^exponent, rounded up to 1e-9, as unscaled at scale 9.
+  // inf.Dec.SetString needs at least one digit in the text before the suffix.
+  {
+    bool digit = false;
+    for (size_t k = sign_end; k < end && (isdigit((unsigned char)s[k]) || s[k] == '.'); ++k) digit |= s[k] != '.';
+    if (!digit) return 0;
+  }
+  __int128 M = 0;  // digits of num+denom
+  for (char c : num + denom) { if (M > ((__int128)1 << 100)) return -1; M = M * 10 + (c - '0'); }
+  int dscale = (int)denom.size();  // value = M / 10^dscale
+  // value * base^exponent * 1e9, rounded up
+  __int128 numer = M, den = 1;
+  int p10 = 9 - dscale + (base == 10 ? exponent : 0);
+  if (base == 2) { if (exponent > 100) return -1; for (int k = 0; k < exponent; ++k) { numer *= 2; if (numer > ((__int128)1 << 120)) return -1; } }
+  if (p10 >= 0) { for (int k = 0; k < p10; ++k) { numer *= 10; if (numer > ((__int128)1 << 120)) return -1; } }
+  else { for (int k = 0; k < -p10; ++k) { den *= 10; if (den > ((__int128)1 << 120)) return -1; } }
+  __int128 unscaled = numer / den;
+  if (numer % den) unscaled += 1;  // RoundUp
+  if (binary && unscaled > (__int128)INT64_MAX * 1000000000) unscaled = (__int128)INT64_MAX * 1000000000;
+  double b = (double)unscaled;  // round-half-even conversion (big.Float.Float64)
+  out = b * go_pow10(-9);
+  if (!positive) out = -out;
+  return 1;
+}
+}  // namespace refcpu
+
+extern "C" int rc_quantity(const char* s, double* out) { return refcpu::quantity_f64(s, *out); }

@@ -78,3 +78,54 @@ def test_weight_edge_cases():
         yaml.safe_dump(st, open(p, "w"))
         paths.append(p)
     run(paths, objs * 20, steps=6, dt_ns=2 * 10**9)
+
+
+def test_shard_invariance_two_engines():
+    """The cluster split into two engines (slot_base = global id of each shard's first pod)
+    fires exactly what one engine over the whole cluster fires (RNG keyed by global slot),
+    and both match the oracle."""
+    from kwok_amd.host.cluster import node_block, pod_range
+    from tests.parity_util import NOW0, build
+    cl = W.make_cluster("C2", 12, 240, seed=14)
+    objs = cl.pods.materialize()
+    _, whole, sim = build(cl.pod_stage_files, objs, harness=True)
+    shards = []
+    for r in range(2):
+        lo, hi = node_block(12, 2, r)
+        plo, phi = pod_range(cl.node_ptr, lo, hi)
+        _, eng, _ = build(cl.pod_stage_files, objs[plo:phi], harness=True, slot_base=plo)
+        shards.append((plo, eng))
+    try:
+        for k in range(25):
+            now = NOW0 + k * 700 * 10**6
+            whole.step(now, 7, k)
+            for _, e in shards:
+                e.step(now, 7, k)
+            exp = sorted((i, s, f) for i, s, f in sim.step(now, 7, k))
+            w = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in whole.fired())
+            sh = sorted((plo + int(r["slot"]), int(r["stage"]), int(r["flags"])) for plo, e in shards for r in e.fired())
+            assert w == exp and sh == exp, f"step {k}"
+    finally:
+        whole.close()
+        for _, e in shards:
+            e.close()
+
+
+def test_count_phase_histogram():
+    """kwk_count (cluster aggregates for the RCCL all-reduce) against the oracle's phases."""
+    from kwok_amd.host.cluster import phase_masks
+    from oracle import refcpu
+    from tests.parity_util import NOW0, build
+    cl = W.make_cluster("C1", 20, 400, seed=15)
+    prog, eng, sim = build(cl.pod_stage_files, cl.pods.materialize(), harness=True)
+    try:
+        masks = phase_masks(prog, values=("Running", "Succeeded"))
+        for k in range(5):
+            eng.step(NOW0 + k * 10**9, 3, k)
+            sim.step(NOW0 + k * 10**9, 3, k)
+            got = eng.count([masks["Running"], masks["Succeeded"], 0])
+            alive = [o for o in sim.objs if o is not None]
+            ph = [(refcpu.query(".status.phase", o) or [None])[0] for o in alive]
+            assert got.tolist() == [ph.count("Running"), ph.count("Succeeded"), len(alive)]
+    finally:
+        eng.close()

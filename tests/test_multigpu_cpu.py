@@ -1,0 +1,89 @@
+"""Multi-GPU path on CPU: node-block sharding, shard-invariant workload generation and the
+aggregate all-reduce, with the gloo backend at world_size 2 (the GPU run uses the same code
+with RCCL).  The oracle simulation of each shard (RNG keyed by global slot) must sum to the
+single-process simulation of the whole cluster."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from kwok_amd import workload as W
+from kwok_amd.host.cluster import Aggregates, local_node_ptr, node_block, pod_range
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_node_blocks_partition_the_cluster():
+    for n, world in ((10, 3), (1_000_000, 8), (7, 8)):
+        blocks = [node_block(n, world, r) for r in range(world)]
+        assert blocks[0][0] == 0 and blocks[-1][1] == n
+        assert all(blocks[r][1] == blocks[r + 1][0] for r in range(world - 1))
+
+
+def test_bench_pod_variants_are_shard_invariant():
+    sys.path.insert(0, ROOT)
+    import bench
+    full = bench.shard_pod_variants(0, 50_000, 7, 0.1)
+    parts = [bench.shard_pod_variants(lo, hi, 7, 0.1) for lo, hi in ((0, 12_345), (12_345, 40_000), (40_000, 50_000))]
+    assert np.array_equal(full, np.concatenate(parts))
+    assert 0.08 < full.mean() < 0.12
+
+
+def _simulate(pods, slot_base, steps, files):
+    from kwok_amd.host.stages import load_stage_files
+    from oracle.sim import OracleSim
+    from oracle import refcpu
+    stages = load_stage_files(*files)
+    sim = OracleSim(stages, pods, harness=True, slot_base=slot_base)
+    fired = np.zeros(len(sim.stages), dtype=np.int64)
+    for k in range(steps):
+        for _, s, _ in sim.step(1_700_000_000 * 10**9 + k * 10**9, 99, k):
+            fired[s] += 1
+    phases = {"Running": 0, "Succeeded": 0, "alive": 0}
+    for o in sim.objs:
+        if o is None:
+            continue
+        phases["alive"] += 1
+        for p in refcpu.query(".status.phase", o) or []:
+            if p in phases:
+                phases[p] += 1
+    return [s.name for s in sim.stages], fired, np.array([phases["Running"], phases["Succeeded"], phases["alive"]])
+
+
+def _worker(rank, world, port, result_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cl = W.make_cluster("C1", 6, 60, seed=4)
+    lo, hi = node_block(6, world, rank)
+    plo, phi = pod_range(cl.node_ptr, lo, hi)
+    pods = cl.pods.materialize(plo, phi)
+    names, fired, counts = _simulate(pods, plo, 7, cl.pod_stage_files)
+    agg = Aggregates(names, fired, counts, ["Running", "Succeeded", "alive"]).allreduce(dist)
+    if rank == 0:
+        np.save(result_path, agg.pack())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_allreduce_of_sharded_oracle_equals_whole_cluster(tmp_path):
+    torch = pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "agg.npy")
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    got = np.load(out)
+    cl = W.make_cluster("C1", 6, 60, seed=4)
+    names, fired, counts = _simulate(cl.pods.materialize(), 0, 7, cl.pod_stage_files)
+    want = Aggregates(names, fired, counts).pack()
+    assert np.array_equal(got, want)
+
+
+def test_local_node_ptr():
+    ptr = np.array([0, 3, 5, 9, 12])
+    assert local_node_ptr(ptr, 1, 3).tolist() == [0, 2, 6]
+    assert pod_range(ptr, 1, 3) == (3, 9)

@@ -1,0 +1,117 @@
+"""Resource usage (BASELINE C4): per-node usage sums and cumulative integrators.
+
+CPU: the host's compiled per-pod values equal the oracle's restatement of
+evaluateContainerResourceUsage for every pod.  GPU: usage_kernel through the C ABI against
+the oracle's nodeResourceUsage / nodeResourceCumulativeUsage within 1e-6 relative
+(BASELINE.json north_star tolerance)."""
+import copy
+import os
+
+import numpy as np
+import pytest
+import yaml
+
+from kwok_amd import workload as W
+from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
+from oracle import usage_ref
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "metrics", "usage-from-annotation.yaml")
+REL_TOL = 1e-6
+
+EXTRA = """
+apiVersion: kwok.x-k8s.io/v1alpha1
+kind: ResourceUsage
+metadata:
+  name: pod-3
+  namespace: default
+spec:
+  usages:
+  - containers: [container-0]
+    usage:
+      cpu: {value: 250m}
+      memory: {value: 64Mi}
+  - usage:
+      cpu: {value: "2"}
+"""
+
+
+def _cluster(n_nodes=30, n_pods=600, seed=21):
+    cl = W.make_cluster("C4", n_nodes, n_pods, seed=seed)
+    pods = cl.pods.materialize()
+    # invalid / odd annotation values: CEL Quantity() error -> 0 (metrics_resource_usage.go:155-160)
+    for i, bad in ((5, "abc"), (6, "1.5Gi"), (7, ""), (8, "0.0000000001"), (9, "1e3")):
+        pods[i].setdefault("metadata", {}).setdefault("annotations", {})["kwok.x-k8s.io/usage-cpu"] = bad
+    return cl, pods
+
+
+def _docs():
+    return [d for d in yaml.safe_load_all(open(GOLDEN).read() + "\n---\n" + EXTRA) if d]
+
+
+def _program():
+    return UsageProgram(*load_usage_yaml(open(GOLDEN).read(), EXTRA))
+
+
+def test_host_usage_values_match_oracle():
+    cl, pods = _cluster()
+    prog = _program()
+    docs = _docs()
+    for p in pods:
+        for c in p["spec"]["containers"]:
+            for r in ("cpu", "memory"):
+                assert prog.container_value(p, c["name"], r) == usage_ref.container_usage(docs, p, c["name"], r)
+
+
+@pytest.mark.gpu
+def test_gpu_node_usage_and_cumulative():
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+
+    cl, pods = _cluster()
+    prog = _program()
+    keys, cv, mv = usage_columns(prog, pods)
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    hot, dels, rec, cls = ing.columns(pods)
+    eng = Engine(kp, capacity=len(pods))
+    try:
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        eng.usage_config(cl.node_ptr, keys, cv, mv)
+        docs = _docs()
+        ptr = cl.node_ptr
+        t0 = 1_700_000_000 * 10**9
+        eng.usage(t0)
+        node, total = eng.usage_read()
+
+        def expect(alive):
+            out = np.zeros((len(ptr) - 1, 2))
+            for j in range(len(ptr) - 1):
+                pn = [pods[k] for k in range(ptr[j], ptr[j + 1]) if alive[k]]
+                out[j] = (usage_ref.node_usage(docs, pn, "cpu"), usage_ref.node_usage(docs, pn, "memory"))
+            return out
+
+        alive = np.ones(len(pods), dtype=bool)
+        e0 = expect(alive)
+        np.testing.assert_allclose(node[:, :2], e0, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(total, e0.sum(axis=0), rtol=REL_TOL)
+        assert np.all(node[:, 2:] == 0)  # first evaluation: integrators start at 0
+        # delete every 7th pod (Deleted events) and evaluate 2.5 s later
+        gone = np.arange(0, len(pods), 7)
+        eng.delete(gone)
+        alive[gone] = False
+        t1 = t0 + 2_500_000_123
+        eng.usage(t1)
+        node, total = eng.usage_read()
+        e1 = expect(alive)
+        np.testing.assert_allclose(node[:, :2], e1, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(node[:, 2:], usage_ref.seconds(t1 - t0) * e1, rtol=REL_TOL, atol=0)
+        t2 = t1 + 10**9
+        eng.usage(t2)
+        node, _ = eng.usage_read()
+        np.testing.assert_allclose(node[:, 2:], usage_ref.seconds(t1 - t0) * e1 + usage_ref.seconds(t2 - t1) * e1,
+                                   rtol=REL_TOL, atol=0)
+    finally:
+        eng.close()
