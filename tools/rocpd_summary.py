@@ -1,0 +1,64 @@
+"""Summaries of rocprofv3 rocpd databases (ROCm 7.2 writes SQLite `run_results.db`).
+
+    python tools/rocpd_summary.py stats <db> [out.csv]        # kernel-trace --stats table
+    python tools/rocpd_summary.py pmc <db> [kernel-substring]  # per-kernel counter means per dispatch
+
+`stats` reproduces rocprofv3's kernel_stats.csv columns (Name, Calls, TotalDurationNs,
+AverageNs, Percentage, MinNs, MaxNs).  `pmc` sums each counter over its dimensions
+(SE / XCD instances) per dispatch and prints the mean over dispatches of each kernel.
+"""
+from __future__ import annotations
+
+import csv
+import sqlite3
+import statistics
+import sys
+from collections import defaultdict
+
+
+def stats(db: str, out: str | None = None):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, duration from kernels").fetchall()
+    by = defaultdict(list)
+    for name, d in rows:
+        by[name].append(int(d))
+    total = sum(sum(v) for v in by.values()) or 1
+    table = []
+    for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        table.append([name, len(v), sum(v), round(sum(v) / len(v), 3), round(100.0 * sum(v) / total, 4), min(v), max(v),
+                      round(statistics.pstdev(v), 3)])
+    hdr = ["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"]
+    f = open(out, "w", newline="") if out else sys.stdout
+    w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
+    w.writerow(hdr)
+    w.writerows(table)
+    if out:
+        f.close()
+    return table
+
+
+def pmc(db: str, kernel: str = ""):
+    c = sqlite3.connect(db)
+    rows = c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection").fetchall()
+    per = defaultdict(lambda: defaultdict(float))  # (kernel, dispatch) -> counter -> sum
+    for disp, name, cn, v in rows:
+        if kernel in name:
+            per[(name, disp)][cn] += float(v)
+    agg = defaultdict(lambda: defaultdict(list))
+    for (name, _), cs in per.items():
+        for cn, v in cs.items():
+            agg[name][cn].append(v)
+    out = {}
+    for name, cs in agg.items():
+        out[name] = {cn: (statistics.mean(v), len(v)) for cn, v in cs.items()}
+    return out
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    else:
+        for name, cs in pmc(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "").items():
+            print(name)
+            for cn, (m, n) in sorted(cs.items()):
+                print(f"  {cn:24s} mean {m:.6g} over {n} dispatches")
