@@ -8,10 +8,11 @@ kwk_fired — the PCIe-inclusive rate is reported in DESIGN.md, never here).
 
     python bench.py [--gpus N --steps K --warmup W]          # N>1 under torch.distributed.run
 
-Multi-GPU: nodes are split into contiguous blocks, each pod lives with its node (no
-data-path collective); the cluster-wide aggregates (transitions per stage, phase counts)
-are summed with one RCCL all-reduce after the timed region.  Total cluster size is fixed:
-"scaling": "strong".
+Multi-GPU (one process per GPU): every rank owns a contiguous block of nodes and the pods
+on them (no data-path collective); the cluster-wide aggregates (transitions per stage, bytes)
+are summed with one RCCL all-reduce after the timed region.  Default "scaling": "weak" — each
+rank keeps the full C5 shard (--nodes x --pods-per-node), so N GPUs simulate an N-times
+larger cluster; --scaling strong splits --nodes over the ranks instead.
 """
 from __future__ import annotations
 
@@ -54,14 +55,16 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac):
+def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, weak=True):
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
 
-    node_lo = n_nodes * rank // world
-    node_hi = n_nodes * (rank + 1) // world
+    if weak:  # rank r owns global nodes [r*n, (r+1)*n)
+        node_lo, node_hi = n_nodes * rank, n_nodes * (rank + 1)
+    else:
+        node_lo, node_hi = n_nodes * rank // world, n_nodes * (rank + 1) // world
     pod_lo, pod_hi = node_lo * pods_per_node, node_hi * pods_per_node
     # pods: pod-fast (C1 stage mix) with harness churn
     pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
@@ -141,9 +144,10 @@ def _cpu_model():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--nodes", type=int, default=1_000_000, help="nodes per GPU (weak) or in total (strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--pods-per-node", type=int, default=100)
     ap.add_argument("--job-frac", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=0x6B776F6B)
@@ -169,7 +173,7 @@ def main():
 
     t_setup = time.perf_counter()
     pods, nodes, (nlo, nhi, plo, phi) = build_engines(args.nodes, args.pods_per_node, rank, world, local_rank,
-                                                      args.seed, args.job_frac)
+                                                      args.seed, args.job_frac, weak=args.scaling == "weak")
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
@@ -226,6 +230,7 @@ def main():
     total_fired, total_bytes, max_ns = agg
     max_s = max_ns / 1e9
 
+    total_nodes = args.nodes * world if args.scaling == "weak" else args.nodes
     if rank == 0:
         value = total_fired / max_s
         pod_kernel_s = pod_ms / 1e3 / args.steps
@@ -241,11 +246,14 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_s / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32/i64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u32/i64",
             "data": "synthetic (seeded kwokctl-shaped pods/nodes; pod-fast + node-fast/heartbeat stages)",
-            "config": {"workload": "C5: 1M nodes / 100M pods, pod-fast + node-initialize/heartbeat, harness churn "
-                                   "(Succeeded -> delete -> re-create), 10% Job-owned",
-                       "nodes": args.nodes, "pods": args.nodes * args.pods_per_node, "parallelism": f"shard{world}",
+            "config": {"workload": f"C5: {args.nodes:,} nodes / {args.nodes * args.pods_per_node:,} pods "
+                                   f"{'per GPU' if args.scaling == 'weak' else 'in total'}, pod-fast + "
+                                   "node-initialize/heartbeat, harness churn (Succeeded -> delete -> re-create), "
+                                   "10% Job-owned",
+                       "nodes": total_nodes, "pods": total_nodes * args.pods_per_node,
+                       "nodes_per_gpu": nhi - nlo, "parallelism": f"node-shard{world}",
                        "sim_dt_ms": args.dt_ms},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -63,11 +63,14 @@ typedef struct kwk_engine kwk_engine;
 #define KWK_CLASS_SHIFT 16            /* bits 16..31: the object's delta class (spec shape) */
 #define KWK_CLASS_MASK 0xFFFF0000u
 
+/* Interchange row for loads / upserts / reads.  On the device the row is split:
+ * an 8-byte {pred, sched} state stream that every step reads, and a due column read only
+ * for objects with a pending stage.  due is meaningful only while a stage is pending. */
 typedef struct {
   uint32_t pred;   /* feature bits (host-compiled predicate summary) */
   uint32_t sched;  /* pending stage | flags | delta class */
   int64_t due;     /* unix ns at which the pending stage fires */
-} kwk_hot;         /* 16 bytes, one per object slot */
+} kwk_hot;         /* 16 bytes */
 
 /* value record entry (one per value slot of a record) */
 #define KWK_V_DEFAULT 0  /* query produced no output: use the stage's default value */
@@ -203,6 +206,11 @@ kwk_status kwk_delete(kwk_engine* eng, uint32_t n, const uint32_t* slots);
  * Random draws use Philox4x32-10(key = seed ^ kind_salt, ctr = (slot_base+slot, step, site)). */
 kwk_status kwk_step(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step);
 
+/* match only: Lifecycle.Match + Stage.Delay for the dirty objects (lifecycle.go:125-191,
+ * 313-341) without firing anything and without harness churn; the picked stage and its due
+ * time are then readable with kwk_read (the reference-interface mirror's Match). */
+kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step);
+
 /* fired records of the LAST step, compacted into host memory (synchronises) */
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 /* cumulative counters (synchronises) */
@@ -226,8 +234,9 @@ kwk_status kwk_usage_read(kwk_engine* eng, double* node_out, double* cluster_out
  * alive objects), k < 16 — e.g. the phase histogram all-reduced across GPUs (synchronises) */
 kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);
 
-/* raw device pointers for in-process consumers (RCCL aggregates, profiling) */
-kwk_status kwk_device_ptrs(kwk_engine* eng, void** hot, void** fired, void** wave_counts);
+/* raw device pointers for in-process consumers (RCCL aggregates, profiling): state = the
+ * {pred u32, sched u32} stream (8 bytes per slot) */
+kwk_status kwk_device_ptrs(kwk_engine* eng, void** state, void** fired, void** wave_counts);
 
 /* HIP events recorded on the engine's stream (live kernel timing in bench.py) */
 kwk_status kwk_event_record(kwk_engine* eng, uint32_t idx);

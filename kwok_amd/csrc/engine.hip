@@ -22,19 +22,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
-// record write-back in groups of KWOK_GROUP neighbours (0 = per record); KEEP = keep the
-// streamed records in VGPRs for it (measured fastest on MI355X, profiles/r1/README.md)
+// state write-back in aligned groups of KWOK_GROUP neighbours (0 = each changed state on its own)
 #ifndef KWOK_GROUP
-#define KWOK_GROUP 4
-#endif
-#ifndef KWOK_GROUP_KEEP
-#define KWOK_GROUP_KEEP 1
-#endif
-#ifndef KWOK_EXP_NOFIRED
-#define KWOK_EXP_NOFIRED 0
-#endif
-#ifndef KWOK_NT_LOADS
-#define KWOK_NT_LOADS 0
+#define KWOK_GROUP 0
 #endif
 #include <cstdlib>
 #include <cstring>
@@ -46,7 +36,7 @@
 namespace {
 
 constexpr int kBlock = 256;              // 4 waves of 64
-constexpr int kMinObjPerThread = 4;      // smallest sweep variant: sizes the per-block arrays
+constexpr int kMinObjPerThread = 8;      // smallest sweep variant: sizes the per-block arrays
 constexpr int kMaxObjPerThread = 16;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kStatWords = 3 + KWK_MAX_STAGES;   // matched, fired, algorithmic bytes, fired per stage
@@ -141,7 +131,8 @@ __device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool de
 }
 
 struct SweepArgs {
-  kwk_hot* __restrict__ hot;
+  uint2* __restrict__ st;        // per object {pred, sched} (8-byte state stream)
+  int64_t* __restrict__ due;     // per object due time (read only for objects with a pending stage)
   int64_t* __restrict__ del_s;
   const uint32_t* __restrict__ rec_idx;
   const kwk_value* __restrict__ values;
@@ -156,6 +147,7 @@ struct SweepArgs {
   uint64_t key;
   uint64_t step;
   int64_t now;
+  uint32_t fire;                 // 0: match only (kwk_match: Lifecycle.Match + Stage.Delay, no playStage)
   kwk_harness harness;
 };
 
@@ -181,7 +173,7 @@ struct Fire {      // what one object's step produced
   bool fire;
   uint32_t stage;
   uint32_t flags;
-  uint32_t bytes;  // algorithmic bytes beyond the 16-byte record read
+  uint32_t bytes;  // algorithmic bytes beyond the 8-byte state read
 };
 
 // match + weighted pick + delay for one dirty object (preprocess, pod_controller.go:196-254).
@@ -315,12 +307,14 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
   sched |= KWK_STAGE_NONE;
 }
 
-// harness + match + fire for one object whose record needs work; writes the record back
+// harness + match + fire for one object whose state needs work.  Returns the new state (the
+// caller writes it back); writes the due column itself when a newly scheduled stage stays
+// pending past this step (a stage that fires in the same step never needs its due stored).
 template <bool kHarness>
-__device__ __forceinline__ uint4 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
+__device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
-                                               int64_t due, uint32_t cls, Fire& f, uint32_t& n_matched) {
+                                               int64_t due, Fire& f, uint32_t& n_matched) {
   if (kHarness) {
     if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
       pred &= a.harness.keep_mask;  // same spec: class bits and record flag stay
@@ -340,16 +334,25 @@ __device__ __forceinline__ uint4 process_object(const SweepArgs& a, const kwk_st
       sched |= KWK_F_DIRTY;
     }
   }
+  bool scheduled = false;
   if (sched & KWK_F_ALIVE) {
-    if (sched & KWK_F_DIRTY) n_matched += match_object(a, T, n_stages, i, pred, sched, due, f.bytes) ? 1 : 0;
+    if (sched & KWK_F_DIRTY) {
+      scheduled = match_object(a, T, n_stages, i, pred, sched, due, f.bytes);
+      n_matched += scheduled ? 1 : 0;
+    }
     const uint32_t st = sched & 0xFFu;
-    if (st < n_stages && due <= a.now) fire_object(a, T, deltas, n_stages, fin_group, cls, st, pred, sched, f);
+    if (a.fire && st < n_stages && due <= a.now) fire_object(a, T, deltas, n_stages, fin_group, sched >> KWK_CLASS_SHIFT, st,
+                                                   pred, sched, f);
   }
-  f.bytes += 16;  // the record write-back (done by the caller)
-  return make_uint4(pred, sched, (uint32_t)(uint64_t)due, (uint32_t)((uint64_t)due >> 32));
+  if (scheduled && (sched & 0xFFu) < n_stages) {
+    a.due[i] = due;
+    f.bytes += 8;
+  }
+  f.bytes += 8;  // the state write-back (done by the caller)
+  return make_uint2(pred, sched);
 }
 
-// does this record need any work this step?  (the idle majority fails every test)
+// does this object need any work this step?  (the idle majority fails every test)
 template <bool kHarness>
 __device__ __forceinline__ bool needs_work(const SweepArgs& a, uint32_t n_stages, uint32_t pred, uint32_t sched,
                                            int64_t due) {
@@ -366,9 +369,7 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   if (!bal) return;
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-#if !KWOK_EXP_NOFIRED
     seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
-#endif
     n_bytes += 8;
   }
   seg_n += (uint32_t)__popcll(bal);
@@ -382,25 +383,31 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 }
 
 // One workgroup sweeps a tile of kBlock*K consecutive objects; each lane owns K of them at a
-// stride of kBlock, so every load instruction of a wave reads 1 KiB contiguously.
-//  * single-phase (K = 4): all K 16-byte records of a lane are loaded up front (K independent
-//    global_load_dwordx4 in flight) and processed from registers;
-//  * two-phase (K = 8, 16): phase 1 streams the K records and compacts the indices of those
-//    that need work into a per-wave LDS list (ballot + popcount); phase 2 re-reads those
-//    (cache-resident) records and runs the heavy match / fire path over the dense list, so
-//    each wave-instruction of it serves 64 objects instead of the ~6 that are active in a
-//    steady-state wave.
+// stride of kBlock, so every load instruction of a wave reads 512 B contiguously.
+//  phase 1  stream the K 8-byte states of each lane (all K loads in flight before the first is
+//           consumed), then the due times of those with a pending stage; compact the ones that
+//           need work into the wave's LDS work list (ballot + popcount), their state + due into
+//           the LDS stash;
+//  phase 2  the heavy path (match / pick / delay / fire / delta) over the dense work list, 64
+//           useful lanes per wave-instruction instead of the few active in a steady-state row;
+//  phase 3  write the changed states back in aligned groups of KWOK_GROUP neighbours (one full
+//           8*G-byte segment per group, unchanged neighbours from VGPRs): full-granule writes
+//           instead of scattered 8-byte partial writes.
 #ifndef KWOK_LB_WAVES
 #define KWOK_LB_WAVES 1
 #endif
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
-constexpr int kStash = 128;      // work-item records kept in LDS per wave (the rest are re-read)
+constexpr int kStash = 192;      // work items whose state + due stay in LDS per wave (the rest are re-read)
 
 template <bool kHarness, int K>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
-  constexpr bool kTwoPhase = K > 4;
   __shared__ unsigned int s_stat[kStatWords];
   __shared__ kwk_delta s_delta[kLdsDeltas];
+  __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
+  __shared__ uint4 s_rec[kWavesPerBlock][kStash];
+#if KWOK_GROUP
+  __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
+#endif
   const kwk_stage_table* __restrict__ T = a.table;
   const uint32_t n_stages = T->n_stages;
   const uint32_t fin_group = T->fin_group_mask;
@@ -418,135 +425,117 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   const uint64_t base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64 + lane;
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   kwk_fired_rec* __restrict__ seg = a.fired + wave_id * (64 * K);
-  const uint4* __restrict__ hot4 = reinterpret_cast<const uint4*>(a.hot);
+  const uint2* __restrict__ st2 = a.st;
 
   uint32_t seg_n = 0;      // wave-uniform
   uint32_t n_matched = 0;  // per lane
-  uint32_t n_bytes = 0;    // per lane: algorithmic bytes moved (DESIGN.md §Roofline)
+  uint32_t n_bytes = 0;    // per lane: algorithmic bytes moved (DESIGN.md §5)
 
-  if constexpr (!kTwoPhase) {
-    uint4 v[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint64_t i = base + (uint64_t)k * kBlock;
-      v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint64_t i = base + (uint64_t)k * kBlock;
-      const bool in = i < a.n;
-      const uint32_t pred = v[k].x, sched = v[k].y;
-      const int64_t due = (int64_t)(((uint64_t)v[k].w << 32) | v[k].z);
-      if (in) n_bytes += 16;
-      Fire f{false, 0, 0, 0};
-      if (in && needs_work<kHarness>(a, n_stages, pred, sched, due))
-        reinterpret_cast<uint4*>(a.hot)[i] = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched,
-                                                                      due, sched >> KWK_CLASS_SHIFT, f, n_matched);
-      n_bytes += f.bytes;
-      emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
-    }
-  } else {
-    // phase 1: stream the K records; compact the ones that need work into the wave's LDS list
-    // (ballot + popcount): the local index always, the record itself for the first kStash
-    __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
-    __shared__ uint4 s_rec[kWavesPerBlock][kStash];
+  // phase 1
+  uint16_t* __restrict__ wl = s_work[wave];
+  uint4* __restrict__ wr = s_rec[wave];
 #if KWOK_GROUP
-    __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
-    unsigned long long rowmask[K];                      // wave-uniform: which lanes of row k changed
+  unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
 #endif
-    uint16_t* __restrict__ wl = s_work[wave];
-    uint4* __restrict__ wr = s_rec[wave];
-    uint32_t n_work = 0;  // wave-uniform
-    uint4 v[K];           // all K loads in flight before the first is consumed
+  uint32_t n_work = 0;  // wave-uniform
+  uint2 v[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint64_t i = base + (uint64_t)k * kBlock;
-#if KWOK_NT_LOADS
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 t = i < a.n ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(hot4) + i) : u32x4{0, 0, 0, 0};
-      v[k] = make_uint4(t.x, t.y, t.z, t.w);
-#else
-      v[k] = i < a.n ? hot4[i] : make_uint4(0, 0, 0, 0);
-#endif
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint64_t i = base + (uint64_t)k * kBlock;
-      bool need = false;
-      if (i < a.n) {
-        n_bytes += 16;
-        need = needs_work<kHarness>(a, n_stages, v[k].x, v[k].y, (int64_t)(((uint64_t)v[k].w << 32) | v[k].z));
-      }
-      const unsigned long long bal = __ballot(need);
-      if (need) {
-        const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-        wl[pos] = (uint16_t)(k * 64 + lane);
-        if (pos < kStash) wr[pos] = v[k];
-#if KWOK_GROUP
-        s_pos[wave][k * 64 + lane] = (uint16_t)pos;
-#endif
-      }
-#if KWOK_GROUP
-      rowmask[k] = bal;
-#endif
-      n_work += (uint32_t)__popcll(bal);
-    }
-    // phase 2: the heavy path over the dense work list, 64 useful lanes per wave-instruction.
-    // Only this wave wrote its list: a wavefront-scope fence (no workgroup barrier) orders the
-    // cross-lane LDS hand-off.
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
-    for (uint32_t c = 0; c < n_work; c += 64) {
-      const uint32_t j = c + lane;
-      Fire f{false, 0, 0, 0};
-      uint64_t i = 0;
-      if (j < n_work) {
-        const uint32_t w = wl[j];
-        i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
-        const uint4 v2 = j < kStash ? wr[j] : hot4[i];  // spill-over beyond the stash: cache re-read
-        const uint4 nv = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, v2.x, v2.y,
-                                                  (int64_t)(((uint64_t)v2.w << 32) | v2.z), v2.y >> KWK_CLASS_SHIFT,
-                                                  f, n_matched);
-#if KWOK_GROUP
-        if (j < kStash) wr[j] = nv;  // written back in phase 3 together with its neighbours
-        else
-#endif
-          reinterpret_cast<uint4*>(a.hot)[i] = nv;
-      }
-      n_bytes += f.bytes;
-      emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
-    }
-#if KWOK_GROUP
-    // phase 3: write back whole groups of KWOK_GROUP neighbouring records (one full 16*G-byte
-    // segment per group) wherever any of them changed: full-granule writes instead of
-    // scattered 16-byte partial writes.
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    constexpr unsigned long long kGrpMask = (1ull << KWOK_GROUP) - 1ull;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const unsigned long long rm = rowmask[k];
-      if (!rm) continue;
-      const uint64_t i = base + (uint64_t)k * kBlock;
-      const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
-      if (i < a.n && ((rm >> g0) & kGrpMask)) {
-        uint4 val;
-        bool write = true;
-        if ((rm >> lane) & 1ull) {
-          const uint32_t p = s_pos[wave][k * 64 + lane];
-          if (p < kStash) val = wr[p]; else write = false;  // overflow items were written in phase 2
-        } else {
-#if KWOK_GROUP_KEEP
-          val = v[k];
-#else
-          val = hot4[i];  // unchanged neighbour: re-read from cache (it was streamed in phase 1)
-#endif
-          n_bytes += 16;  // an unchanged neighbour rewritten to complete the group
-        }
-        if (write) reinterpret_cast<uint4*>(a.hot)[i] = val;
-      }
-    }
-#endif
+  for (int k = 0; k < K; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    v[k] = i < a.n ? st2[i] : make_uint2(0, 0);
   }
+  int64_t d[K];  // due times, loaded only where a stage is pending (out-of-range lanes: MANAGED clear)
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    const bool pend = (v[k].y & KWK_F_MANAGED) && (v[k].y & 0xFFu) < n_stages;
+    d[k] = pend ? a.due[i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    bool need = false;
+    if (i < a.n) {
+      n_bytes += 8;
+      if ((v[k].y & KWK_F_MANAGED) && (v[k].y & 0xFFu) < n_stages) n_bytes += 8;
+      need = needs_work<kHarness>(a, n_stages, v[k].x, v[k].y, d[k]);
+    }
+    const unsigned long long bal = __ballot(need);
+    if (need) {
+      const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      wl[pos] = (uint16_t)(k * 64 + lane);
+      if (pos < kStash) wr[pos] = make_uint4(v[k].x, v[k].y, (uint32_t)(uint64_t)d[k], (uint32_t)((uint64_t)d[k] >> 32));
+#if KWOK_GROUP
+      s_pos[wave][k * 64 + lane] = (uint16_t)pos;
+#endif
+    }
+#if KWOK_GROUP
+    rowmask[k] = bal;
+#endif
+    n_work += (uint32_t)__popcll(bal);
+  }
+  // phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup barrier)
+  // orders the cross-lane LDS hand-off.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
+  for (uint32_t c = 0; c < n_work; c += 64) {
+    const uint32_t j = c + lane;
+    Fire f{false, 0, 0, 0};
+    uint64_t i = 0;
+    if (j < n_work) {
+      const uint32_t w = wl[j];
+      i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
+      uint32_t pred, sched;
+      int64_t due;
+      if (j < kStash) {
+        const uint4 r = wr[j];
+        pred = r.x;
+        sched = r.y;
+        due = (int64_t)(((uint64_t)r.w << 32) | r.z);
+      } else {  // spill-over beyond the stash: re-read (cache-resident, streamed in phase 1)
+        const uint2 s = st2[i];
+        pred = s.x;
+        sched = s.y;
+        due = ((sched & 0xFFu) < n_stages) ? a.due[i] : 0;
+      }
+      const uint2 nv = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, f, n_matched);
+#if KWOK_GROUP
+      if (j < kStash) wr[j] = make_uint4(nv.x, nv.y, 0, 0);  // written back in phase 3 with its group
+      else
+#endif
+        a.st[i] = nv;
+    }
+    n_bytes += f.bytes;
+    emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
+  }
+#if KWOK_GROUP
+  // phase 3: aligned groups of KWOK_GROUP lanes (8*G contiguous bytes) rewritten wherever any
+  // member changed; unchanged members come from the phase-1 registers (not algorithmic bytes:
+  // the PMC WRITE_SIZE pass shows their cost).
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  constexpr unsigned long long kGrpMask = (KWOK_GROUP >= 64) ? ~0ull : ((1ull << KWOK_GROUP) - 1ull);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long rm = rowmask[k];
+    if (!rm) continue;
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
+    if (i < a.n && ((rm >> g0) & kGrpMask)) {
+      uint2 val = v[k];
+      bool write = true;
+      if ((rm >> lane) & 1ull) {
+        const uint32_t p = s_pos[wave][k * 64 + lane];
+        if (p < kStash) {
+          const uint4 r = wr[p];
+          val = make_uint2(r.x, r.y);
+        } else {
+          write = false;  // spill-over items were written in phase 2
+        }
+      }
+      if (write) a.st[i] = val;
+    }
+  }
+#endif
 
   // per-wave fired count (read by kwk_fired's scan) and block statistics
   for (int off = 32; off > 0; off >>= 1) {
@@ -594,7 +583,8 @@ __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, 
 }
 
 struct ScatterArgs {
-  kwk_hot* hot;
+  uint2* st;
+  int64_t* due;
   int64_t* del_s;
   uint32_t* rec_idx;
   const uint32_t* slots;
@@ -613,16 +603,17 @@ __global__ void scatter_kernel(ScatterArgs a) {
   kwk_hot h = a.s_hot[j];
   h.sched = (h.sched & ~KWK_CLASS_MASK) | ((uint32_t)a.s_cls[j] << KWK_CLASS_SHIFT);
   if (a.mark_dirty) h.sched |= KWK_F_DIRTY;
-  a.hot[i] = h;
+  a.st[i] = make_uint2(h.pred, h.sched);
+  a.due[i] = h.due;
   a.del_s[i] = a.s_del[j];
   a.rec_idx[i] = a.s_rec[j];
 }
 
-__global__ void delete_kernel(kwk_hot* hot, const uint32_t* slots, uint32_t n) {
+__global__ void delete_kernel(uint2* st, const uint32_t* slots, uint32_t n) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t i = slots[j];
-  hot[i].sched = (hot[i].sched & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
+  st[i].y = (st[i].y & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
 }
 
 // ------------------------------------------------------------------ resource usage
@@ -630,7 +621,7 @@ __global__ void delete_kernel(kwk_hot* hot, const uint32_t* slots, uint32_t n) {
 // cpu / memory value from the interned dictionaries, multiply by its container count and
 // reduce with shuffles.  Dead pods (not in the pod cache) contribute nothing.
 // server/metrics_resource_usage.go:170-224 (sums), :36-109 (cumulative integrators).
-__global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict__ hot,
+__global__ __launch_bounds__(kBlock) void usage_kernel(const uint2* __restrict__ st,
                                                        const uint32_t* __restrict__ node_ptr,
                                                        const uint32_t* __restrict__ ukey,
                                                        const double* __restrict__ cpu_v,
@@ -644,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict
   if (node < n_nodes) {
     const uint32_t lo = node_ptr[node], hi = node_ptr[node + 1];
     for (uint32_t p = lo + lane; p < hi; p += 64) {
-      const uint32_t sched = hot[p].sched;
+      const uint32_t sched = st[p].y;
       if (!(sched & KWK_F_ALIVE)) continue;
       const uint32_t k = ukey[p];
       const double nc = (double)(k >> 28);
@@ -691,13 +682,12 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const kwk_hot* __restrict
 // phase histograms and other cluster aggregates.  One wave per 64*16 objects; per-block LDS
 // totals, one 64-bit atomic per block and mask.
 constexpr int kMaxCountMasks = 16;
-__global__ __launch_bounds__(kBlock) void count_kernel(const kwk_hot* __restrict__ hot, uint32_t n,
+__global__ __launch_bounds__(kBlock) void count_kernel(const uint2* __restrict__ st, uint32_t n,
                                                        const uint32_t* __restrict__ masks, uint32_t n_masks,
                                                        unsigned long long* __restrict__ out) {
   __shared__ unsigned int s_cnt[kMaxCountMasks];
   if (threadIdx.x < kMaxCountMasks) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint4* __restrict__ hot4 = reinterpret_cast<const uint4*>(hot);
   uint32_t cnt[kMaxCountMasks];
   for (int m = 0; m < kMaxCountMasks; ++m) cnt[m] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * (kBlock * 16) + threadIdx.x;
@@ -705,7 +695,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const kwk_hot* __restrict
   for (int k = 0; k < 16; ++k) {
     const uint64_t i = base + (uint64_t)k * kBlock;
     if (i >= n) break;
-    const uint4 v = hot4[i];
+    const uint2 v = st[i];
     if (!(v.y & KWK_F_ALIVE)) continue;
     for (uint32_t m = 0; m < n_masks; ++m) cnt[m] += (masks[m] == 0 || (v.x & masks[m])) ? 1u : 0u;
   }
@@ -743,13 +733,14 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0;
-  uint32_t objs_per_thread = 8;   // sweep variant (KWOK_SWEEP_OBJS = 4 | 8 | 16)
-  uint32_t last_objs = 4;
+  uint32_t objs_per_thread = 16;  // sweep variant (KWOK_SWEEP_OBJS = 8 | 16)
+  uint32_t last_objs = 16;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
 
-  kwk_hot* d_hot = nullptr;
+  uint2* d_st = nullptr;      // {pred, sched} per slot (the 8-byte state stream)
+  int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
   kwk_value* d_values = nullptr;
@@ -818,7 +809,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
   if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
     const int k = atoi(v);
-    if (k == 4 || k == 8 || k == 16) e->objs_per_thread = (uint32_t)k;
+    if (k == 8 || k == 16) e->objs_per_thread = (uint32_t)k;
   }
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
@@ -831,7 +822,8 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
       return fail(KWK_EHIP, std::string("hipMalloc: ") + hipGetErrorString(er)); \
     }                                                                            \
   } while (0)
-  ALLOC(e->d_hot, sizeof(kwk_hot) * (size_t)e->capacity);
+  ALLOC(e->d_st, sizeof(uint2) * (size_t)e->capacity);
+  ALLOC(e->d_due, sizeof(int64_t) * (size_t)e->capacity);
   ALLOC(e->d_del, sizeof(int64_t) * (size_t)e->capacity);
   ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
   ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
@@ -845,7 +837,8 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
-  hipMemsetAsync(e->d_hot, 0, sizeof(kwk_hot) * (size_t)e->capacity, e->stream);
+  hipMemsetAsync(e->d_st, 0, sizeof(uint2) * (size_t)e->capacity, e->stream);
+  hipMemsetAsync(e->d_due, 0, sizeof(int64_t) * (size_t)e->capacity, e->stream);
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
   // cub scan temp storage for the fired-list compaction
@@ -863,7 +856,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (!e) return KWK_OK;
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_hot, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf};
@@ -921,11 +914,15 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
   }
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  {  // the object's delta class lives in the upper half of its sched word
-    std::vector<kwk_hot> tmp(hot, hot + n);
-    for (uint32_t i = 0; i < n; ++i)
-      tmp[i].sched = (tmp[i].sched & ~KWK_CLASS_MASK) | ((uint32_t)cls[i] << KWK_CLASS_SHIFT);
-    HIP_TRY(hipMemcpy(e->d_hot, tmp.data(), sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  {  // AoS interchange rows -> device SoA; the delta class lives in the upper half of sched
+    std::vector<uint2> st(n);
+    std::vector<int64_t> due(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      st[i] = make_uint2(hot[i].pred, (hot[i].sched & ~KWK_CLASS_MASK) | ((uint32_t)cls[i] << KWK_CLASS_SHIFT));
+      due[i] = hot[i].due;
+    }
+    HIP_TRY(hipMemcpy(e->d_st, st.data(), sizeof(uint2) * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
   }
   HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_rec, rec, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
@@ -933,7 +930,7 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
     HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
                       hipMemcpyHostToDevice));
   if (n < e->n_active)
-    HIP_TRY(hipMemset(e->d_hot + n, 0, sizeof(kwk_hot) * (size_t)(e->n_active - n)));
+    HIP_TRY(hipMemset(e->d_st + n, 0, sizeof(uint2) * (size_t)(e->n_active - n)));
   e->n_active = n;
   return KWK_OK;
 }
@@ -975,10 +972,10 @@ kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kw
   HIP_TRY(hipMemcpy(s_rec, rec, 4 * (size_t)n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
   if (max_slot + 1 > e->n_active) {
-    HIP_TRY(hipMemset(e->d_hot + e->n_active, 0, sizeof(kwk_hot) * (size_t)(max_slot + 1 - e->n_active)));
+    HIP_TRY(hipMemset(e->d_st + e->n_active, 0, sizeof(uint2) * (size_t)(max_slot + 1 - e->n_active)));
     e->n_active = max_slot + 1;
   }
-  ScatterArgs a{e->d_hot, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
+  ScatterArgs a{e->d_st, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
   hipLaunchKernelGGL(scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -994,19 +991,20 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
   if (kwk_status st = ensure_stage_buf(e, 4 * (size_t)n)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(e->d_stage_buf, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_hot,
+  hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_st,
                      (const uint32_t*)e->d_stage_buf, n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 
-kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
   SweepArgs a;
-  a.hot = e->d_hot;
+  a.st = e->d_st;
+  a.due = e->d_due;
   a.del_s = e->d_del;
   a.rec_idx = e->d_rec;
   a.values = e->d_values;
@@ -1021,14 +1019,15 @@ kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step)
   a.key = seed ^ ((uint64_t)e->kind_salt << 32);
   a.step = step;
   a.now = now_ns;
+  a.fire = fire ? 1u : 0u;
   a.harness = e->harness;
+  if (!fire) a.harness.enable = 0;
   const uint32_t K = e->objs_per_thread;
   const uint32_t tile = kBlock * K;
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
-  const bool h = e->harness.enable != 0;
+  const bool h = a.harness.enable != 0;
 #define LAUNCH(HV, KV) hipLaunchKernelGGL((sweep_kernel<HV, KV>), dim3(blocks), dim3(kBlock), 0, e->stream, a)
-  if (K == 4) { if (h) LAUNCH(true, 4); else LAUNCH(false, 4); }
-  else if (K == 8) { if (h) LAUNCH(true, 8); else LAUNCH(false, 8); }
+  if (K == 8) { if (h) LAUNCH(true, 8); else LAUNCH(false, 8); }
   else { if (h) LAUNCH(true, 16); else LAUNCH(false, 16); }
 #undef LAUNCH
   e->last_objs = K;
@@ -1036,6 +1035,14 @@ kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step)
   e->last_blocks = blocks;
   ++e->steps;
   return KWK_OK;
+}
+
+kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  return launch_sweep(e, now_ns, seed, step, true);
+}
+
+kwk_status kwk_match(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  return launch_sweep(e, now_ns, seed, step, false);
 }
 
 kwk_status kwk_sync(kwk_engine* e) {
@@ -1091,7 +1098,13 @@ kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int
   if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  if (hot) HIP_TRY(hipMemcpy(hot, e->d_hot + first, sizeof(kwk_hot) * n, hipMemcpyDeviceToHost));
+  if (hot) {  // device SoA -> AoS interchange rows
+    std::vector<uint2> st(n);
+    std::vector<int64_t> due(n);
+    HIP_TRY(hipMemcpy(st.data(), e->d_st + first, sizeof(uint2) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(due.data(), e->d_due + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) hot[i] = kwk_hot{st[i].x, st[i].y, due[i]};
+  }
   if (del) HIP_TRY(hipMemcpy(del, e->d_del + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
   return KWK_OK;
 }
@@ -1140,7 +1153,7 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
   const uint32_t ublocks = (e->n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_hot, e->d_node_ptr, e->d_ukey,
+  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_st, e->d_node_ptr, e->d_ukey,
                      e->d_cpu, e->d_mem, e->n_nodes, e->d_node_out, e->d_node_cum, e->d_node_last, now_ns,
                      e->d_usage_part);
   HIP_TRY(hipGetLastError());
@@ -1171,7 +1184,7 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
   HIP_TRY(hipMemsetAsync(d_out, 0, 8 * kMaxCountMasks, e->stream));
   if (e->n_active) {
     const uint32_t blocks = (e->n_active + kBlock * 16 - 1) / (kBlock * 16);
-    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_hot, e->n_active, d_masks, n_masks,
+    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_st, e->n_active, d_masks, n_masks,
                        d_out);
     HIP_TRY(hipGetLastError());
   }
@@ -1182,7 +1195,7 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
 
 kwk_status kwk_device_ptrs(kwk_engine* e, void** hot, void** fired, void** wave_counts) {
   if (!e) return fail(KWK_EINVAL, "null engine");
-  if (hot) *hot = e->d_hot;
+  if (hot) *hot = e->d_st;
   if (fired) *fired = e->d_fired;
   if (wave_counts) *wave_counts = e->d_wave_counts;
   return KWK_OK;

@@ -89,7 +89,7 @@ assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.i
 # every symbol include/kwok_engine.h declares (checked by the CPU test suite)
 EXPORTS = [
     "kwk_last_error", "kwk_engine_create", "kwk_engine_destroy", "kwk_load_stages", "kwk_set_harness", "kwk_load",
-    "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
+    "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_match", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count",
 ]
@@ -125,6 +125,7 @@ def lib():
     L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
+    L.kwk_match.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_fired.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
     L.kwk_stats.argtypes = [C.c_void_p, _p(StepStats)]
     L.kwk_read.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]

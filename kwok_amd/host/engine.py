@@ -174,6 +174,10 @@ class Engine:
     def step(self, now_ns: int, seed: int, step: int):
         abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
+    def match(self, now_ns: int, seed: int, step: int):
+        """kwk_match: pick + delay for dirty objects, nothing fires."""
+        abi.check(abi.lib().kwk_match(self.h, now_ns, seed, step), "kwk_match")
+
     def sync(self):
         abi.check(abi.lib().kwk_sync(self.h), "kwk_sync")
 

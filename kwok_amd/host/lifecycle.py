@@ -5,9 +5,9 @@ The Go controllers consume ``lifecycle.Lifecycle`` (lifecycle.go:49) through
 ``Stage.Delay / Next / Name / ImmediateNextStage``.  This module keeps those names and
 meanings so code (and tests) written against the reference read the same:
 
-* ``Lifecycle.match(...)`` / ``match_batch(...)`` run the HIP sweep kernel (one step of a
-  scratch engine over the given objects): matching, weighted pick and delay are computed on
-  the GPU exactly as in ``kwk_step``;
+* ``Lifecycle.match(...)`` / ``match_batch(...)`` run the HIP sweep kernel in match-only
+  mode (``kwk_match`` on a scratch engine over the given objects): matching, weighted pick
+  and delay are computed on the GPU exactly as in ``kwk_step``, nothing fires;
 * ``list_all_possible``, ``Stage.weight`` and ``Stage.delay`` are the deterministic helpers
   the stage tester uses (pkg/tools/stage/stage.go:37-85); they evaluate the compiled table on
   the host from the interned feature bits / pre-parsed records;
@@ -197,14 +197,12 @@ class Lifecycle:
         eng = self._engine
         eng.load_stages()
         eng.load(hot, dels, rec, cls, ing.record_array())
-        eng.step(now_ns, seed, step)
-        fired = eng.fired()
+        eng.match(now_ns, seed, step)
         out_hot, _ = eng.read(0, n)
-        picked = {int(r["slot"]): int(r["stage"]) for r in fired}
         res = []
         for i in range(n):
             st = int(out_hot["sched"][i]) & 0xFF
-            s = picked.get(i, None if st == abi.STAGE_NONE else st)
+            s = None if st == abi.STAGE_NONE else st
             if s is None:
                 res.append((None, 0))
             else:
