@@ -55,7 +55,7 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, weak=True):
+def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, weak=True, wide_state=False):
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
     from kwok_amd.host.engine import Engine, Ingest
@@ -76,7 +76,7 @@ def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, w
     phot, pdel, prec, pcls = ping.variant_columns(pvars, pidx)
     log(f"rank {rank}: loading {pod_hi - pod_lo} pods onto device {device}")
     del pidx
-    pods = Engine(pprog, capacity=pod_hi - pod_lo, device=device, slot_base=pod_lo, kind_salt=0)
+    pods = Engine(pprog, capacity=pod_hi - pod_lo, device=device, slot_base=pod_lo, kind_salt=0, wide_state=wide_state)
     pods.load_stages()
     pods.load(phot, pdel, prec, pcls, ping.record_array())
     del phot, pdel, prec, pcls
@@ -87,7 +87,8 @@ def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, w
     ning = Ingest(nprog)
     nidx = np.zeros(node_hi - node_lo, dtype=np.int32)
     nhot, ndel, nrec, ncls = ning.variant_columns(nvars, nidx)
-    nodes = Engine(nprog, capacity=node_hi - node_lo, device=device, slot_base=node_lo, kind_salt=1)
+    nodes = Engine(nprog, capacity=node_hi - node_lo, device=device, slot_base=node_lo, kind_salt=1,
+                   wide_state=wide_state)
     nodes.load_stages()
     nodes.load(nhot, ndel, nrec, ncls, ning.record_array())
     return pods, nodes, (node_lo, node_hi, pod_lo, pod_hi)
@@ -155,6 +156,8 @@ def main():
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
+    ap.add_argument("--wide-state", action="store_true", default=os.environ.get("KWOK_BENCH_WIDE") == "1",
+                    help="diagnostic: force the 8-byte device state format")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,7 +176,8 @@ def main():
 
     t_setup = time.perf_counter()
     pods, nodes, (nlo, nhi, plo, phi) = build_engines(args.nodes, args.pods_per_node, rank, world, local_rank,
-                                                      args.seed, args.job_frac, weak=args.scaling == "weak")
+                                                      args.seed, args.job_frac, weak=args.scaling == "weak",
+                                                      wide_state=args.wide_state)
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
@@ -238,6 +242,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
                 "kernel": "sweep_kernel (pods)", "bytes_per_launch": int(pbytes / args.steps),
+                "state_bytes_per_object": int(s1p["state_bytes"]),
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2)}
         cpu = None
         log(f"timed {args.steps} steps in {max_s:.3f} s; cpu baseline next")

@@ -129,6 +129,9 @@ typedef struct {
   uint32_t fin_group_mask;     /* pred bits forming the object's finalizer set */
   uint32_t n_classes;          /* delta table is [n_classes][n_stages] */
   uint32_t version;
+  uint32_t pred_bits;          /* feature bits in use: pred < 2^pred_bits (0 = all 32).  With the class
+                                * and stage counts this picks the device state format */
+  uint32_t reserved[3];
   kwk_stage_desc stages[KWK_MAX_STAGES];
 } kwk_stage_table;
 
@@ -167,8 +170,9 @@ typedef struct {
   uint64_t steps;
   uint64_t matched;       /* objects (re)scheduled by a match */
   uint64_t fired;         /* stage transitions */
-  uint64_t bytes;         /* algorithmic bytes moved by the sweep (DESIGN.md §Roofline) */
+  uint64_t bytes;         /* algorithmic bytes moved by the sweep (DESIGN.md §5) */
   uint64_t fired_per_stage[KWK_MAX_STAGES];
+  uint64_t state_bytes;   /* bytes per object of the device state stream: 4 (narrow) or 8 (wide) */
 } kwk_step_stats;
 
 /* ------------------------------------------------------------------ engine */
@@ -179,8 +183,9 @@ typedef struct {
   uint32_t max_records;       /* value records */
   uint64_t slot_base;         /* global id of local slot 0 (RNG counter; shard invariant) */
   uint32_t kind_salt;         /* mixed into the RNG key: separate streams per kind */
-  uint32_t reserved;
+  uint32_t flags;             /* KWK_ENGINE_* */
 } kwk_engine_desc;
+#define KWK_ENGINE_WIDE_STATE (1u << 0) /* always use the 8-byte state format (never the packed 4-byte one) */
 
 const char* kwk_last_error(void);
 kwk_status kwk_engine_create(const kwk_engine_desc* desc, kwk_engine** out);

@@ -22,10 +22,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
-// state write-back in aligned groups of KWOK_GROUP neighbours (0 = each changed state on its own)
-#ifndef KWOK_GROUP
-#define KWOK_GROUP 0
-#endif
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -37,7 +33,7 @@ namespace {
 
 constexpr int kBlock = 256;              // 4 waves of 64
 constexpr int kMinObjPerThread = 8;      // smallest sweep variant: sizes the per-block arrays
-constexpr int kMaxObjPerThread = 16;
+constexpr int kMaxObjPerThread = 32;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kStatWords = 3 + KWK_MAX_STAGES;   // matched, fired, algorithmic bytes, fired per stage
 
@@ -130,8 +126,53 @@ __device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool de
   }
 }
 
+// ------------------------------------------------------------------ object state formats
+// wide   : uint2 {pred, sched} per slot (any compiled program);
+// narrow : one u32 per slot when the program fits 32 bits:
+//          [pred: pred_bits][class: cbits][stage code: sbits][flags: 5]
+//          flags = sched bits 8..12 (ALIVE DIRTY MANAGED HASREC MATCHERR); stage code n_stages = none.
+struct StateFmt {
+  uint32_t narrow;
+  uint32_t pmask;
+  uint32_t cshift, cmask;
+  uint32_t sshift, smask, none_code;
+  uint32_t fshift;
+};
+
+__host__ __device__ __forceinline__ uint2 fmt_unpack(uint32_t w, const StateFmt& f) {
+  const uint32_t cls = (w >> f.cshift) & f.cmask;
+  const uint32_t sc = (w >> f.sshift) & f.smask;
+  const uint32_t stage = sc == f.none_code ? KWK_STAGE_NONE : sc;
+  const uint32_t fl = (w >> f.fshift) & 0x1Fu;
+  return make_uint2(w & f.pmask, stage | (fl << 8) | (cls << KWK_CLASS_SHIFT));
+}
+
+__host__ __device__ __forceinline__ uint32_t fmt_pack(uint32_t pred, uint32_t sched, const StateFmt& f) {
+  const uint32_t stage = sched & 0xFFu;
+  const uint32_t sc = stage == KWK_STAGE_NONE ? f.none_code : stage;
+  return (pred & f.pmask) | (((sched >> KWK_CLASS_SHIFT) & f.cmask) << f.cshift) | ((sc & f.smask) << f.sshift) |
+         (((sched >> 8) & 0x1Fu) << f.fshift);
+}
+
+// small kernels (scatter / delete / usage / count) branch on the format at run time
+__device__ __forceinline__ uint2 load_state(const void* st, uint64_t i, const StateFmt& f) {
+  return f.narrow ? fmt_unpack(reinterpret_cast<const uint32_t*>(st)[i], f) : reinterpret_cast<const uint2*>(st)[i];
+}
+__device__ __forceinline__ void store_state(void* st, uint64_t i, uint2 v, const StateFmt& f) {
+  if (f.narrow) reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
+  else reinterpret_cast<uint2*>(st)[i] = v;
+}
+
+// the sweep is specialised per format
+template <bool kNarrow> struct StateWord { typedef uint2 T; };
+template <> struct StateWord<true> { typedef uint32_t T; };
+__device__ __forceinline__ uint2 sw_decode(uint2 w, const StateFmt&) { return w; }
+__device__ __forceinline__ uint2 sw_decode(uint32_t w, const StateFmt& f) { return fmt_unpack(w, f); }
+__device__ __forceinline__ void sw_encode(uint2& out, uint2 v, const StateFmt&) { out = v; }
+__device__ __forceinline__ void sw_encode(uint32_t& out, uint2 v, const StateFmt& f) { out = fmt_pack(v.x, v.y, f); }
+
 struct SweepArgs {
-  uint2* __restrict__ st;        // per object {pred, sched} (8-byte state stream)
+  void* __restrict__ st;         // per object state word (StateFmt: uint2 {pred, sched} or packed u32)
   int64_t* __restrict__ due;     // per object due time (read only for objects with a pending stage)
   int64_t* __restrict__ del_s;
   const uint32_t* __restrict__ rec_idx;
@@ -148,6 +189,7 @@ struct SweepArgs {
   uint64_t step;
   int64_t now;
   uint32_t fire;                 // 0: match only (kwk_match: Lifecycle.Match + Stage.Delay, no playStage)
+  StateFmt fmt;
   kwk_harness harness;
 };
 
@@ -310,7 +352,7 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
 // harness + match + fire for one object whose state needs work.  Returns the new state (the
 // caller writes it back); writes the due column itself when a newly scheduled stage stays
 // pending past this step (a stage that fires in the same step never needs its due stored).
-template <bool kHarness>
+template <bool kHarness, uint32_t kWordBytes>
 __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
@@ -348,7 +390,7 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
     a.due[i] = due;
     f.bytes += 8;
   }
-  f.bytes += 8;  // the state write-back (done by the caller)
+  f.bytes += kWordBytes;  // the state write-back (done by the caller)
   return make_uint2(pred, sched);
 }
 
@@ -383,31 +425,29 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 }
 
 // One workgroup sweeps a tile of kBlock*K consecutive objects; each lane owns K of them at a
-// stride of kBlock, so every load instruction of a wave reads 512 B contiguously.
-//  phase 1  stream the K 8-byte states of each lane (all K loads in flight before the first is
+// stride of kBlock, so every load instruction of a wave reads 64 consecutive state words.
+//  phase 1  stream the K state words of each lane (all K loads in flight before the first is
 //           consumed), then the due times of those with a pending stage; compact the ones that
-//           need work into the wave's LDS work list (ballot + popcount), their state + due into
-//           the LDS stash;
+//           need work into the wave's LDS work list (ballot + popcount), their decoded state +
+//           due into the LDS stash;
 //  phase 2  the heavy path (match / pick / delay / fire / delta) over the dense work list, 64
 //           useful lanes per wave-instruction instead of the few active in a steady-state row;
-//  phase 3  write the changed states back in aligned groups of KWOK_GROUP neighbours (one full
-//           8*G-byte segment per group, unchanged neighbours from VGPRs): full-granule writes
-//           instead of scattered 8-byte partial writes.
+//           each changed state word is written straight back (measured faster on MI355X than
+//           rewriting aligned groups of neighbours, profiles/r1/README.md).
 #ifndef KWOK_LB_WAVES
 #define KWOK_LB_WAVES 1
 #endif
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
 constexpr int kStash = 192;      // work items whose state + due stay in LDS per wave (the rest are re-read)
 
-template <bool kHarness, int K>
+template <bool kHarness, int K, bool kNarrow>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
+  typedef typename StateWord<kNarrow>::T W;
+  constexpr uint32_t kWordBytes = sizeof(W);
   __shared__ unsigned int s_stat[kStatWords];
   __shared__ kwk_delta s_delta[kLdsDeltas];
   __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
   __shared__ uint4 s_rec[kWavesPerBlock][kStash];
-#if KWOK_GROUP
-  __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
-#endif
   const kwk_stage_table* __restrict__ T = a.table;
   const uint32_t n_stages = T->n_stages;
   const uint32_t fin_group = T->fin_group_mask;
@@ -425,7 +465,8 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   const uint64_t base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64 + lane;
   const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   kwk_fired_rec* __restrict__ seg = a.fired + wave_id * (64 * K);
-  const uint2* __restrict__ st2 = a.st;
+  W* __restrict__ stw = reinterpret_cast<W*>(a.st);
+  const StateFmt fmt = a.fmt;
 
   uint32_t seg_n = 0;      // wave-uniform
   uint32_t n_matched = 0;  // per lane
@@ -434,44 +475,38 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   // phase 1
   uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ wr = s_rec[wave];
-#if KWOK_GROUP
-  unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
-#endif
   uint32_t n_work = 0;  // wave-uniform
-  uint2 v[K];
+  W v[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint64_t i = base + (uint64_t)k * kBlock;
-    v[k] = i < a.n ? st2[i] : make_uint2(0, 0);
+    if (i < a.n) v[k] = stw[i];
+    else v[k] = W{};  // MANAGED clear: never work
   }
-  int64_t d[K];  // due times, loaded only where a stage is pending (out-of-range lanes: MANAGED clear)
+  int64_t d[K];  // due times, loaded only where a stage is pending
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint64_t i = base + (uint64_t)k * kBlock;
-    const bool pend = (v[k].y & KWK_F_MANAGED) && (v[k].y & 0xFFu) < n_stages;
+    const uint2 s = sw_decode(v[k], fmt);
+    const bool pend = (s.y & KWK_F_MANAGED) && (s.y & 0xFFu) < n_stages;
     d[k] = pend ? a.due[i] : 0;
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint64_t i = base + (uint64_t)k * kBlock;
+    const uint2 s = sw_decode(v[k], fmt);
     bool need = false;
     if (i < a.n) {
-      n_bytes += 8;
-      if ((v[k].y & KWK_F_MANAGED) && (v[k].y & 0xFFu) < n_stages) n_bytes += 8;
-      need = needs_work<kHarness>(a, n_stages, v[k].x, v[k].y, d[k]);
+      n_bytes += kWordBytes;
+      if ((s.y & KWK_F_MANAGED) && (s.y & 0xFFu) < n_stages) n_bytes += 8;
+      need = needs_work<kHarness>(a, n_stages, s.x, s.y, d[k]);
     }
     const unsigned long long bal = __ballot(need);
     if (need) {
       const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       wl[pos] = (uint16_t)(k * 64 + lane);
-      if (pos < kStash) wr[pos] = make_uint4(v[k].x, v[k].y, (uint32_t)(uint64_t)d[k], (uint32_t)((uint64_t)d[k] >> 32));
-#if KWOK_GROUP
-      s_pos[wave][k * 64 + lane] = (uint16_t)pos;
-#endif
+      if (pos < kStash) wr[pos] = make_uint4(s.x, s.y, (uint32_t)(uint64_t)d[k], (uint32_t)((uint64_t)d[k] >> 32));
     }
-#if KWOK_GROUP
-    rowmask[k] = bal;
-#endif
     n_work += (uint32_t)__popcll(bal);
   }
   // phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup barrier)
@@ -493,49 +528,20 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
         sched = r.y;
         due = (int64_t)(((uint64_t)r.w << 32) | r.z);
       } else {  // spill-over beyond the stash: re-read (cache-resident, streamed in phase 1)
-        const uint2 s = st2[i];
+        const uint2 s = sw_decode(stw[i], fmt);
         pred = s.x;
         sched = s.y;
         due = ((sched & 0xFFu) < n_stages) ? a.due[i] : 0;
       }
-      const uint2 nv = process_object<kHarness>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, f, n_matched);
-#if KWOK_GROUP
-      if (j < kStash) wr[j] = make_uint4(nv.x, nv.y, 0, 0);  // written back in phase 3 with its group
-      else
-#endif
-        a.st[i] = nv;
+      const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, f,
+                                                            n_matched);
+      W out;
+      sw_encode(out, nv, fmt);
+      stw[i] = out;
     }
     n_bytes += f.bytes;
     emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
   }
-#if KWOK_GROUP
-  // phase 3: aligned groups of KWOK_GROUP lanes (8*G contiguous bytes) rewritten wherever any
-  // member changed; unchanged members come from the phase-1 registers (not algorithmic bytes:
-  // the PMC WRITE_SIZE pass shows their cost).
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  constexpr unsigned long long kGrpMask = (KWOK_GROUP >= 64) ? ~0ull : ((1ull << KWOK_GROUP) - 1ull);
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const unsigned long long rm = rowmask[k];
-    if (!rm) continue;
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
-    if (i < a.n && ((rm >> g0) & kGrpMask)) {
-      uint2 val = v[k];
-      bool write = true;
-      if ((rm >> lane) & 1ull) {
-        const uint32_t p = s_pos[wave][k * 64 + lane];
-        if (p < kStash) {
-          const uint4 r = wr[p];
-          val = make_uint2(r.x, r.y);
-        } else {
-          write = false;  // spill-over items were written in phase 2
-        }
-      }
-      if (write) a.st[i] = val;
-    }
-  }
-#endif
 
   // per-wave fired count (read by kwk_fired's scan) and block statistics
   for (int off = 32; off > 0; off >>= 1) {
@@ -583,7 +589,8 @@ __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, 
 }
 
 struct ScatterArgs {
-  uint2* st;
+  void* st;
+  StateFmt fmt;
   int64_t* due;
   int64_t* del_s;
   uint32_t* rec_idx;
@@ -603,17 +610,19 @@ __global__ void scatter_kernel(ScatterArgs a) {
   kwk_hot h = a.s_hot[j];
   h.sched = (h.sched & ~KWK_CLASS_MASK) | ((uint32_t)a.s_cls[j] << KWK_CLASS_SHIFT);
   if (a.mark_dirty) h.sched |= KWK_F_DIRTY;
-  a.st[i] = make_uint2(h.pred, h.sched);
+  store_state(a.st, i, make_uint2(h.pred, h.sched), a.fmt);
   a.due[i] = h.due;
   a.del_s[i] = a.s_del[j];
   a.rec_idx[i] = a.s_rec[j];
 }
 
-__global__ void delete_kernel(uint2* st, const uint32_t* slots, uint32_t n) {
+__global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uint32_t n) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t i = slots[j];
-  st[i].y = (st[i].y & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
+  uint2 v = load_state(st, i, fmt);
+  v.y = (v.y & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
+  store_state(st, i, v, fmt);
 }
 
 // ------------------------------------------------------------------ resource usage
@@ -621,7 +630,7 @@ __global__ void delete_kernel(uint2* st, const uint32_t* slots, uint32_t n) {
 // cpu / memory value from the interned dictionaries, multiply by its container count and
 // reduce with shuffles.  Dead pods (not in the pod cache) contribute nothing.
 // server/metrics_resource_usage.go:170-224 (sums), :36-109 (cumulative integrators).
-__global__ __launch_bounds__(kBlock) void usage_kernel(const uint2* __restrict__ st,
+__global__ __launch_bounds__(kBlock) void usage_kernel(const void* __restrict__ st, StateFmt fmt,
                                                        const uint32_t* __restrict__ node_ptr,
                                                        const uint32_t* __restrict__ ukey,
                                                        const double* __restrict__ cpu_v,
@@ -635,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const uint2* __restrict__
   if (node < n_nodes) {
     const uint32_t lo = node_ptr[node], hi = node_ptr[node + 1];
     for (uint32_t p = lo + lane; p < hi; p += 64) {
-      const uint32_t sched = st[p].y;
+      const uint32_t sched = load_state(st, p, fmt).y;
       if (!(sched & KWK_F_ALIVE)) continue;
       const uint32_t k = ukey[p];
       const double nc = (double)(k >> 28);
@@ -682,7 +691,7 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const uint2* __restrict__
 // phase histograms and other cluster aggregates.  One wave per 64*16 objects; per-block LDS
 // totals, one 64-bit atomic per block and mask.
 constexpr int kMaxCountMasks = 16;
-__global__ __launch_bounds__(kBlock) void count_kernel(const uint2* __restrict__ st, uint32_t n,
+__global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, StateFmt fmt, uint32_t n,
                                                        const uint32_t* __restrict__ masks, uint32_t n_masks,
                                                        unsigned long long* __restrict__ out) {
   __shared__ unsigned int s_cnt[kMaxCountMasks];
@@ -695,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const uint2* __restrict__
   for (int k = 0; k < 16; ++k) {
     const uint64_t i = base + (uint64_t)k * kBlock;
     if (i >= n) break;
-    const uint2 v = st[i];
+    const uint2 v = load_state(st, i, fmt);
     if (!(v.y & KWK_F_ALIVE)) continue;
     for (uint32_t m = 0; m < n_masks; ++m) cnt[m] += (masks[m] == 0 || (v.x & masks[m])) ? 1u : 0u;
   }
@@ -733,13 +742,16 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0;
-  uint32_t objs_per_thread = 16;  // sweep variant (KWOK_SWEEP_OBJS = 8 | 16)
+  uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 16 | 32)
+  uint32_t objs_narrow = 16;
   uint32_t last_objs = 16;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
 
-  uint2* d_st = nullptr;      // {pred, sched} per slot (the 8-byte state stream)
+  void* d_st = nullptr;       // state word per slot (8-byte capacity; format in fmt)
+  StateFmt fmt{};             // current state format (wide until a table allows narrow)
+  bool force_wide = false;
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -775,6 +787,63 @@ struct kwk_engine {
   std::vector<hipEvent_t> events;
 };
 
+// narrow iff pred + class + stage code + 5 flag bits fit 32 bits
+static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stages, bool allow_narrow) {
+  auto bitlen = [](uint32_t x) {
+    uint32_t b = 0;
+    while (x) { ++b; x >>= 1; }
+    return b;
+  };
+  const uint32_t pb = pred_bits == 0 ? 32u : pred_bits;
+  const uint32_t cb = bitlen(n_classes ? n_classes - 1 : 0);
+  const uint32_t sb = bitlen(n_stages);  // codes 0..n_stages, n_stages = none
+  StateFmt f{};
+  if (!allow_narrow || pb + cb + sb + 5 > 32) return f;
+  f.narrow = 1;
+  f.pmask = (1u << pb) - 1u;
+  f.cshift = pb;
+  f.cmask = cb ? ((1u << cb) - 1u) : 0u;
+  f.sshift = pb + cb;
+  f.smask = sb ? ((1u << sb) - 1u) : 0u;
+  f.none_code = n_stages;
+  f.fshift = pb + cb + sb;
+  return f;
+}
+
+static size_t word_bytes(const StateFmt& f) { return f.narrow ? 4 : 8; }
+
+static bool same_fmt(const StateFmt& a, const StateFmt& b) { return memcmp(&a, &b, sizeof(StateFmt)) == 0; }
+
+// host-side conversion of device state words <-> (pred, sched)
+static std::vector<uint2> unpack_words(const std::vector<uint8_t>& raw, const StateFmt& f, uint32_t n) {
+  std::vector<uint2> out(n);
+  if (f.narrow) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(raw.data());
+    for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
+  } else {
+    memcpy(out.data(), raw.data(), sizeof(uint2) * (size_t)n);
+  }
+  return out;
+}
+
+static std::vector<uint8_t> pack_words(const std::vector<uint2>& v, const StateFmt& f) {
+  std::vector<uint8_t> raw(word_bytes(f) * v.size());
+  if (f.narrow) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(raw.data());
+    for (size_t i = 0; i < v.size(); ++i) w[i] = fmt_pack(v[i].x, v[i].y, f);
+  } else {
+    memcpy(raw.data(), v.data(), sizeof(uint2) * v.size());
+  }
+  return raw;
+}
+
+// the narrow format holds only pred bits < pred_bits and stage indices < n_stages
+static bool fits_fmt(const StateFmt& f, uint32_t n_stages, uint32_t pred, uint32_t sched) {
+  if (!f.narrow) return true;
+  const uint32_t st = sched & 0xFFu;
+  return (pred & ~f.pmask) == 0 && (st == KWK_STAGE_NONE || st < n_stages);
+}
+
 static kwk_status set_dev(kwk_engine* e) {
   HIP_TRY(hipSetDevice(e->device));
   return KWK_OK;
@@ -807,9 +876,11 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->slot_base = d->slot_base;
   e->kind_salt = d->kind_salt;
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
+  e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
   if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
     const int k = atoi(v);
-    if (k == 8 || k == 16) e->objs_per_thread = (uint32_t)k;
+    if (k == 8 || k == 16) e->objs_wide = (uint32_t)k;
+    if (k == 16 || k == 32) e->objs_narrow = (uint32_t)k;
   }
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
@@ -880,8 +951,24 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
         return fail(KWK_EINVAL, "stage " + std::to_string(s) + ": value slot out of range");
     if (S.weight_slot == KWK_SLOT_DELETION) return fail(KWK_EINVAL, "weight cannot use the deletion column");
   }
+  if (t->pred_bits > 32) return fail(KWK_EINVAL, "pred_bits > 32");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
+  const StateFmt nf = make_fmt(t->pred_bits, t->n_classes, t->n_stages, !e->force_wide);
+  if (!same_fmt(nf, e->fmt)) {
+    if (e->n_active) {  // repack the resident objects into the new format
+      const uint32_t n = e->n_active;
+      std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
+      HIP_TRY(hipMemcpy(raw.data(), e->d_st, raw.size(), hipMemcpyDeviceToHost));
+      std::vector<uint2> v = unpack_words(raw, e->fmt, n);
+      for (uint32_t i = 0; i < n; ++i)
+        if (!fits_fmt(nf, t->n_stages, v[i].x, v[i].y) || (v[i].y >> KWK_CLASS_SHIFT) >= (t->n_classes ? t->n_classes : 1))
+          return fail(KWK_EINVAL, "resident object " + std::to_string(i) + " does not fit the new stage table");
+      std::vector<uint8_t> out = pack_words(v, nf);
+      HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
+    }
+    e->fmt = nf;
+  }
   HIP_TRY(hipMemcpy(e->d_table, t, sizeof(kwk_stage_table), hipMemcpyHostToDevice));
   if (e->d_deltas) HIP_TRY(hipFree(e->d_deltas));
   e->d_deltas = nullptr;
@@ -919,9 +1006,12 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
     std::vector<int64_t> due(n);
     for (uint32_t i = 0; i < n; ++i) {
       st[i] = make_uint2(hot[i].pred, (hot[i].sched & ~KWK_CLASS_MASK) | ((uint32_t)cls[i] << KWK_CLASS_SHIFT));
+      if (!fits_fmt(e->fmt, e->n_stages, st[i].x, st[i].y))
+        return fail(KWK_EINVAL, "object " + std::to_string(i) + ": pred bits / stage beyond the loaded stage table");
       due[i] = hot[i].due;
     }
-    HIP_TRY(hipMemcpy(e->d_st, st.data(), sizeof(uint2) * n, hipMemcpyHostToDevice));
+    const std::vector<uint8_t> raw = pack_words(st, e->fmt);
+    HIP_TRY(hipMemcpy(e->d_st, raw.data(), raw.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
   }
   HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
@@ -930,7 +1020,7 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
     HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
                       hipMemcpyHostToDevice));
   if (n < e->n_active)
-    HIP_TRY(hipMemset(e->d_st + n, 0, sizeof(uint2) * (size_t)(e->n_active - n)));
+    HIP_TRY(hipMemset((char*)e->d_st + word_bytes(e->fmt) * n, 0, word_bytes(e->fmt) * (size_t)(e->n_active - n)));
   e->n_active = n;
   return KWK_OK;
 }
@@ -954,6 +1044,8 @@ kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kw
     if (slots[j] >= e->capacity) return fail(KWK_ECAP, "slot beyond capacity");
     if (e->loaded_table && cls[j] >= e->n_classes) return fail(KWK_EINVAL, "class out of range");
     if ((hot[j].sched & KWK_F_HASREC) && rec[j] >= e->max_records) return fail(KWK_EINVAL, "record out of range");
+    if (!fits_fmt(e->fmt, e->n_stages, hot[j].pred, hot[j].sched))
+      return fail(KWK_EINVAL, "pred bits / stage beyond the loaded stage table");
     max_slot = slots[j] > max_slot ? slots[j] : max_slot;
   }
   if (kwk_status st = set_dev(e)) return st;
@@ -972,10 +1064,11 @@ kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kw
   HIP_TRY(hipMemcpy(s_rec, rec, 4 * (size_t)n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
   if (max_slot + 1 > e->n_active) {
-    HIP_TRY(hipMemset(e->d_st + e->n_active, 0, sizeof(uint2) * (size_t)(max_slot + 1 - e->n_active)));
+    HIP_TRY(hipMemset((char*)e->d_st + word_bytes(e->fmt) * e->n_active, 0,
+                      word_bytes(e->fmt) * (size_t)(max_slot + 1 - e->n_active)));
     e->n_active = max_slot + 1;
   }
-  ScatterArgs a{e->d_st, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
+  ScatterArgs a{e->d_st, e->fmt, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
   hipLaunchKernelGGL(scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -992,7 +1085,7 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(e->d_stage_buf, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_st,
-                     (const uint32_t*)e->d_stage_buf, n);
+                     e->fmt, (const uint32_t*)e->d_stage_buf, n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
@@ -1020,15 +1113,22 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   a.step = step;
   a.now = now_ns;
   a.fire = fire ? 1u : 0u;
+  a.fmt = e->fmt;
   a.harness = e->harness;
   if (!fire) a.harness.enable = 0;
-  const uint32_t K = e->objs_per_thread;
+  const bool nar = e->fmt.narrow != 0;
+  const uint32_t K = nar ? e->objs_narrow : e->objs_wide;
   const uint32_t tile = kBlock * K;
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
   const bool h = a.harness.enable != 0;
-#define LAUNCH(HV, KV) hipLaunchKernelGGL((sweep_kernel<HV, KV>), dim3(blocks), dim3(kBlock), 0, e->stream, a)
-  if (K == 8) { if (h) LAUNCH(true, 8); else LAUNCH(false, 8); }
-  else { if (h) LAUNCH(true, 16); else LAUNCH(false, 16); }
+#define LAUNCH(HV, KV, NV) hipLaunchKernelGGL((sweep_kernel<HV, KV, NV>), dim3(blocks), dim3(kBlock), 0, e->stream, a)
+  if (!nar) {
+    if (K == 8) { if (h) LAUNCH(true, 8, false); else LAUNCH(false, 8, false); }
+    else { if (h) LAUNCH(true, 16, false); else LAUNCH(false, 16, false); }
+  } else {
+    if (K == 32) { if (h) LAUNCH(true, 32, true); else LAUNCH(false, 32, true); }
+    else { if (h) LAUNCH(true, 16, true); else LAUNCH(false, 16, true); }
+  }
 #undef LAUNCH
   e->last_objs = K;
   HIP_TRY(hipGetLastError());
@@ -1090,6 +1190,7 @@ kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
   out->fired = h[1];
   out->bytes = h[2];
   for (int s = 0; s < KWK_MAX_STAGES; ++s) out->fired_per_stage[s] = h[3 + s];
+  out->state_bytes = word_bytes(e->fmt);
   return KWK_OK;
 }
 
@@ -1099,10 +1200,11 @@ kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (hot) {  // device SoA -> AoS interchange rows
-    std::vector<uint2> st(n);
+    std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
     std::vector<int64_t> due(n);
-    HIP_TRY(hipMemcpy(st.data(), e->d_st + first, sizeof(uint2) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(raw.data(), (const char*)e->d_st + word_bytes(e->fmt) * first, raw.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(due.data(), e->d_due + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    const std::vector<uint2> st = unpack_words(raw, e->fmt, n);
     for (uint32_t i = 0; i < n; ++i) hot[i] = kwk_hot{st[i].x, st[i].y, due[i]};
   }
   if (del) HIP_TRY(hipMemcpy(del, e->d_del + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
@@ -1153,7 +1255,7 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
   const uint32_t ublocks = (e->n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_st, e->d_node_ptr, e->d_ukey,
+  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->d_node_ptr, e->d_ukey,
                      e->d_cpu, e->d_mem, e->n_nodes, e->d_node_out, e->d_node_cum, e->d_node_last, now_ns,
                      e->d_usage_part);
   HIP_TRY(hipGetLastError());
@@ -1184,7 +1286,7 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
   HIP_TRY(hipMemsetAsync(d_out, 0, 8 * kMaxCountMasks, e->stream));
   if (e->n_active) {
     const uint32_t blocks = (e->n_active + kBlock * 16 - 1) / (kBlock * 16);
-    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_st, e->n_active, d_masks, n_masks,
+    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->n_active, d_masks, n_masks,
                        d_out);
     HIP_TRY(hipGetLastError());
   }

@@ -52,7 +52,8 @@ class StageDesc(C.Structure):
 
 class StageTable(C.Structure):
     _fields_ = [("n_stages", C.c_uint32), ("fin_group_mask", C.c_uint32), ("n_classes", C.c_uint32),
-                ("version", C.c_uint32), ("stages", StageDesc * MAX_STAGES)]
+                ("version", C.c_uint32), ("pred_bits", C.c_uint32), ("reserved", C.c_uint32 * 3),
+                ("stages", StageDesc * MAX_STAGES)]
 
 
 class Delta(C.Structure):
@@ -70,13 +71,16 @@ class FiredRec(C.Structure):
 
 class StepStats(C.Structure):
     _fields_ = [("steps", C.c_uint64), ("matched", C.c_uint64), ("fired", C.c_uint64), ("bytes", C.c_uint64),
-                ("fired_per_stage", C.c_uint64 * MAX_STAGES)]
+                ("fired_per_stage", C.c_uint64 * MAX_STAGES), ("state_bytes", C.c_uint64)]
 
 
 class EngineDesc(C.Structure):
     _fields_ = [("device", C.c_int32), ("capacity", C.c_uint32), ("value_slots", C.c_uint32),
                 ("max_records", C.c_uint32), ("slot_base", C.c_uint64), ("kind_salt", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("flags", C.c_uint32)]
+
+
+ENGINE_WIDE_STATE = 1
 
 
 HOT_DTYPE = np.dtype([("pred", "<u4"), ("sched", "<u4"), ("due", "<i8")])

@@ -570,6 +570,7 @@ class KindProgram:
         t.fin_group_mask = self.fin_group_mask
         t.n_classes = max(1, len(self.class_ids))
         t.version = version
+        t.pred_bits = self.nbits
         for i, d in enumerate(self.stage_desc):
             t.stages[i] = d
         return t

@@ -107,11 +107,12 @@ class Engine:
     """One kwk_engine (C ABI) for one KindProgram."""
 
     def __init__(self, program: KindProgram, capacity: int, device: int = 0, slot_base: int = 0, kind_salt: int = 0,
-                 max_records: int = 1 << 16):
+                 max_records: int = 1 << 16, wide_state: bool = False):
         self.p = program
         L = abi.lib()
         d = abi.EngineDesc(device=device, capacity=capacity, value_slots=max(1, len(program.slots)),
-                           max_records=max_records, slot_base=slot_base, kind_salt=kind_salt)
+                           max_records=max_records, slot_base=slot_base, kind_salt=kind_salt,
+                           flags=abi.ENGINE_WIDE_STATE if wide_state else 0)
         h = C.c_void_p()
         abi.check(L.kwk_engine_create(C.byref(d), C.byref(h)), "kwk_engine_create")
         self.h = h
@@ -194,6 +195,7 @@ class Engine:
         s = abi.StepStats()
         abi.check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
         return {"steps": s.steps, "matched": s.matched, "fired": s.fired, "bytes": s.bytes,
+                "state_bytes": s.state_bytes,
                 "fired_per_stage": {self.p.names[i]: s.fired_per_stage[i] for i in range(len(self.p.names))}}
 
     def read(self, first: int = 0, n: Optional[int] = None):

@@ -12,21 +12,24 @@ from tests.parity_util import run
 pytestmark = pytest.mark.gpu
 
 
-def test_pod_fast_c1_mini():
-    """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods."""
+@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
+def test_pod_fast_c1_mini(wide):
+    """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in both
+    device state formats."""
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True)
+    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, wide_state=wide)
     assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
 
 
-def test_pod_general_c2_mini():
+@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
+def test_pod_general_c2_mini(wide):
     """C2 shape: pod-general + chaos, init containers, override annotations (valid and
     invalid ints / durations / RFC3339), chaos labels, deletionTimestamps; weighted picks
     and Philox jitter."""
     cl = W.make_cluster("C2", 50, 600, seed=12)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=40, dt_ns=500 * 10**6, harness=True)
+    total, per = run(cl.pod_stage_files, objs, steps=40, dt_ns=500 * 10**6, harness=True, wide_state=wide)
     assert per["pod-create"] > 0 and per["pod-ready"] > 0 and per["pod-delete"] > 0
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
@@ -127,5 +130,32 @@ def test_count_phase_histogram():
             alive = [o for o in sim.objs if o is not None]
             ph = [(refcpu.query(".status.phase", o) or [None])[0] for o in alive]
             assert got.tolist() == [ph.count("Running"), ph.count("Succeeded"), len(alive)]
+    finally:
+        eng.close()
+
+
+def test_state_format_repack_on_table_reload():
+    """kwk_load_stages with objects resident and a table that needs the other state format
+    (pred_bits = 0 -> 32 bits -> wide, then back to packed) repacks them in place; the run
+    stays bit-exact with the oracle."""
+    import ctypes as C
+    from kwok_amd.host import abi
+    from tests.parity_util import NOW0, build, compare_state
+    cl = W.make_cluster("C1", 10, 200, seed=16)
+    prog, eng, sim = build(cl.pod_stage_files, cl.pods.materialize(), harness=True)
+    try:
+        for k in range(8):
+            if k in (3, 6):
+                t = prog.table(version=k)
+                if k == 3:
+                    t.pred_bits = 0
+                deltas = np.ascontiguousarray(prog.delta_array())
+                abi.check(abi.lib().kwk_load_stages(eng.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
+                assert eng.stats()["state_bytes"] == (8 if k == 3 else 4)
+            now = NOW0 + k * 10**9
+            eng.step(now, 9, k)
+            got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
+            assert got == sorted(sim.step(now, 9, k)), f"step {k}"
+            compare_state(prog, eng, sim, k)
     finally:
         eng.close()

@@ -47,7 +47,8 @@ def test_abi_struct_layout_matches_header():
     # sizes the device code relies on (16-byte hot record / value entry, 96-byte stage desc)
     assert ctypes.sizeof(abi.Hot) == 16 and ctypes.sizeof(abi.Value) == 16
     assert ctypes.sizeof(abi.StageDesc) == 96 and ctypes.sizeof(abi.FiredRec) == 8
-    assert ctypes.sizeof(abi.StageTable) == 16 + 32 * 96
+    assert ctypes.sizeof(abi.StageTable) == 32 + 32 * 96
+    assert ctypes.sizeof(abi.StepStats) == 8 * (4 + 32 + 1) and ctypes.sizeof(abi.EngineDesc) == 32
 
 
 def test_engine_fails_loudly_without_gpu():

@@ -4,10 +4,11 @@ R=$GRAFT_REPO_ROOT; T=${1:-var}; O=$R/gpurun_out/$T
 mkdir -p $O && cd $R
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
-for lib in kwok_amd/lib/variants/*.so; do
-  for k in 8 16; do
-    n=$(basename $lib .so)_k$k
-    KWOK_ENGINE_LIB=$R/$lib KWOK_SWEEP_OBJS=$k timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 40 > $O/bench_$n.json 2> $O/bench_$n.err || { cat $O/bench_$n.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('$O/bench_$n.json')); r=d['roofline']; print('$n', '%.3g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'])"
-  done
-done
+run() {  # name, env assignments...
+  n=$1; shift
+  env "$@" timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 40 > $O/bench_$n.json 2> $O/bench_$n.err || { cat $O/bench_$n.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/bench_$n.json')); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'))"
+}
+run narrow_k16 KWOK_SWEEP_OBJS=16
+run narrow_k32 KWOK_SWEEP_OBJS=32
+run wide_k16 KWOK_SWEEP_OBJS=16 KWOK_BENCH_WIDE=1
