@@ -171,6 +171,15 @@ __device__ __forceinline__ uint2 sw_decode(uint32_t w, const StateFmt& f) { retu
 __device__ __forceinline__ void sw_encode(uint2& out, uint2 v, const StateFmt&) { out = v; }
 __device__ __forceinline__ void sw_encode(uint32_t& out, uint2 v, const StateFmt& f) { out = fmt_pack(v.x, v.y, f); }
 
+// the phase-1 idle test on raw state words: bit masks of the word holding flags + stage
+// (fw: sched in the wide format, the packed word in the narrow one) and of the word holding
+// pred (pw), computed on the host per launch
+struct RawTest {
+  uint32_t managed, dirty, alive;
+  uint32_t sshift, smask, none_code;
+  uint32_t term, del;  // harness: terminal phase bits / deletionTimestamp bit (pred)
+};
+
 struct SweepArgs {
   void* __restrict__ st;         // per object state word (StateFmt: uint2 {pred, sched} or packed u32)
   int64_t* __restrict__ due;     // per object due time (read only for objects with a pending stage)
@@ -190,6 +199,7 @@ struct SweepArgs {
   int64_t now;
   uint32_t fire;                 // 0: match only (kwk_match: Lifecycle.Match + Stage.Delay, no playStage)
   StateFmt fmt;
+  RawTest raw;
   kwk_harness harness;
 };
 
@@ -394,16 +404,6 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
   return make_uint2(pred, sched);
 }
 
-// does this object need any work this step?  (the idle majority fails every test)
-template <bool kHarness>
-__device__ __forceinline__ bool needs_work(const SweepArgs& a, uint32_t n_stages, uint32_t pred, uint32_t sched,
-                                           int64_t due) {
-  return (sched & KWK_F_MANAGED) &&
-         ((sched & KWK_F_DIRTY) || ((sched & 0xFFu) < n_stages && due <= a.now) ||
-          (kHarness && (!(sched & KWK_F_ALIVE) ||
-                        ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)))));
-}
-
 // wave-ballot compaction of the fired set into the wave's private segment + per-stage counts
 __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t lane, kwk_fired_rec* __restrict__ seg,
                                            uint32_t& seg_n, unsigned int* s_stat, uint32_t& n_bytes) {
@@ -427,18 +427,37 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 // One workgroup sweeps a tile of kBlock*K consecutive objects; each lane owns K of them at a
 // stride of kBlock, so every load instruction of a wave reads 64 consecutive state words.
 //  phase 1  stream the K state words of each lane (all K loads in flight before the first is
-//           consumed), then the due times of those with a pending stage; compact the ones that
-//           need work into the wave's LDS work list (ballot + popcount), their decoded state +
-//           due into the LDS stash;
-//  phase 2  the heavy path (match / pick / delay / fire / delta) over the dense work list, 64
-//           useful lanes per wave-instruction instead of the few active in a steady-state row;
-//           each changed state word is written straight back (measured faster on MI355X than
-//           rewriting aligned groups of neighbours, profiles/r1/README.md).
+//           consumed), then the due times of those with a pending stage.  The idle test runs
+//           on the raw words with precomputed masks (RawTest): no unpacking, a handful of
+//           VALU ops per object.  Objects that need work go to the wave's LDS work list
+//           (ballot + mbcnt), their raw word + due into the LDS stash;
+//  phase 2  the heavy path (decode, match / pick / delay / fire / delta, encode) over the dense
+//           work list, 64 useful lanes per wave-instruction instead of the few active in a
+//           steady-state row; each changed word is written back (KWOK_GROUP = 0) or parked in
+//           the stash for phase 3;
+//  phase 3  (KWOK_GROUP = G > 0) aligned groups of G neighbouring words rewritten whole
+//           wherever any member changed: full-segment writes instead of scattered partial ones.
 #ifndef KWOK_LB_WAVES
 #define KWOK_LB_WAVES 1
 #endif
+#ifndef KWOK_GROUP
+#define KWOK_GROUP 0
+#endif
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
-constexpr int kStash = 192;      // work items whose state + due stay in LDS per wave (the rest are re-read)
+constexpr int kStash = 192;      // work items whose word + due stay in LDS per wave (the rest are re-read)
+
+__device__ __forceinline__ uint32_t fw_of(uint2 w) { return w.y; }      // word holding flags + stage
+__device__ __forceinline__ uint32_t pw_of(uint2 w) { return w.x; }      // word holding pred
+__device__ __forceinline__ uint32_t fw_of(uint32_t w) { return w; }
+__device__ __forceinline__ uint32_t pw_of(uint32_t w) { return w; }
+__device__ __forceinline__ uint4 stash_of(uint2 w, int64_t d) {
+  return make_uint4(w.x, w.y, (uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32));
+}
+__device__ __forceinline__ uint4 stash_of(uint32_t w, int64_t d) {
+  return make_uint4(w, 0u, (uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32));
+}
+__device__ __forceinline__ void unstash(const uint4& r, uint2& w) { w = make_uint2(r.x, r.y); }
+__device__ __forceinline__ void unstash(const uint4& r, uint32_t& w) { w = r.x; }
 
 template <bool kHarness, int K, bool kNarrow>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
@@ -448,6 +467,9 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   __shared__ kwk_delta s_delta[kLdsDeltas];
   __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
   __shared__ uint4 s_rec[kWavesPerBlock][kStash];
+#if KWOK_GROUP
+  __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
+#endif
   const kwk_stage_table* __restrict__ T = a.table;
   const uint32_t n_stages = T->n_stages;
   const uint32_t fin_group = T->fin_group_mask;
@@ -467,50 +489,68 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   kwk_fired_rec* __restrict__ seg = a.fired + wave_id * (64 * K);
   W* __restrict__ stw = reinterpret_cast<W*>(a.st);
   const StateFmt fmt = a.fmt;
+  const RawTest R = a.raw;
+  const bool full = (uint64_t)(blockIdx.x + 1) * (kBlock * K) <= a.n;
 
-  uint32_t seg_n = 0;      // wave-uniform
-  uint32_t n_matched = 0;  // per lane
-  uint32_t n_bytes = 0;    // per lane: algorithmic bytes moved
+  uint32_t seg_n = 0;       // wave-uniform
+  uint32_t n_matched = 0;   // per lane
+  uint32_t n_bytes = 0;     // per lane: algorithmic bytes of the heavy path
+  uint32_t wave_bytes = 0;  // wave-uniform: streamed words + due reads
 
-  // phase 1
+  // ---- phase 1
   uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ wr = s_rec[wave];
+#if KWOK_GROUP
+  unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
+#endif
   uint32_t n_work = 0;  // wave-uniform
   W v[K];
+  if (full) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    if (i < a.n) v[k] = stw[i];
-    else v[k] = W{};  // MANAGED clear: never work
+    for (int k = 0; k < K; ++k) v[k] = stw[base + (uint64_t)k * kBlock];
+    wave_bytes += 64u * K * kWordBytes;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + (uint64_t)k * kBlock;
+      const bool in = i < a.n;
+      v[k] = in ? stw[i] : W{};  // MANAGED clear out of range: never work
+      wave_bytes += kWordBytes * (uint32_t)__popcll(__ballot(in));
+    }
   }
   int64_t d[K];  // due times, loaded only where a stage is pending
+  uint32_t pend_bits = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    const uint2 s = sw_decode(v[k], fmt);
-    const bool pend = (s.y & KWK_F_MANAGED) && (s.y & 0xFFu) < n_stages;
-    d[k] = pend ? a.due[i] : 0;
+    const uint32_t fw = fw_of(v[k]);
+    const bool pend = (fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code;
+    pend_bits |= (pend ? 1u : 0u) << k;
+    d[k] = pend ? a.due[base + (uint64_t)k * kBlock] : 0;
+    wave_bytes += 8u * (uint32_t)__popcll(__ballot(pend));
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    const uint2 s = sw_decode(v[k], fmt);
-    bool need = false;
-    if (i < a.n) {
-      n_bytes += kWordBytes;
-      if ((s.y & KWK_F_MANAGED) && (s.y & 0xFFu) < n_stages) n_bytes += 8;
-      need = needs_work<kHarness>(a, n_stages, s.x, s.y, d[k]);
-    }
+    const uint32_t fw = fw_of(v[k]);
+    const uint32_t pw = pw_of(v[k]);
+    bool need = (fw & R.dirty) || (((pend_bits >> k) & 1u) && d[k] <= a.now);
+    if (kHarness) need = need || !(fw & R.alive) || ((pw & R.term) && !(pw & R.del));
+    need = need && (fw & R.managed);
     const unsigned long long bal = __ballot(need);
     if (need) {
       const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       wl[pos] = (uint16_t)(k * 64 + lane);
-      if (pos < kStash) wr[pos] = make_uint4(s.x, s.y, (uint32_t)(uint64_t)d[k], (uint32_t)((uint64_t)d[k] >> 32));
+      if (pos < kStash) wr[pos] = stash_of(v[k], d[k]);
+#if KWOK_GROUP
+      s_pos[wave][k * 64 + lane] = (uint16_t)pos;
+#endif
     }
+#if KWOK_GROUP
+    rowmask[k] = bal;
+#endif
     n_work += (uint32_t)__popcll(bal);
   }
-  // phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup barrier)
-  // orders the cross-lane LDS hand-off.
+  // ---- phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup
+  // barrier) orders the cross-lane LDS hand-off.
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
   for (uint32_t c = 0; c < n_work; c += 64) {
@@ -520,30 +560,57 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     if (j < n_work) {
       const uint32_t w = wl[j];
       i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
-      uint32_t pred, sched;
+      W raw;
       int64_t due;
       if (j < kStash) {
         const uint4 r = wr[j];
-        pred = r.x;
-        sched = r.y;
+        unstash(r, raw);
         due = (int64_t)(((uint64_t)r.w << 32) | r.z);
       } else {  // spill-over beyond the stash: re-read (cache-resident, streamed in phase 1)
-        const uint2 s = sw_decode(stw[i], fmt);
-        pred = s.x;
-        sched = s.y;
-        due = ((sched & 0xFFu) < n_stages) ? a.due[i] : 0;
+        raw = stw[i];
+        const uint32_t fw = fw_of(raw);
+        due = ((fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code) ? a.due[i] : 0;
       }
-      const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, pred, sched, due, f,
+      const uint2 s = sw_decode(raw, fmt);
+      const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
                                                             n_matched);
       W out;
       sw_encode(out, nv, fmt);
-      stw[i] = out;
+#if KWOK_GROUP
+      if (j < kStash) wr[j] = stash_of(out, 0);  // written back in phase 3 with its group
+      else
+#endif
+        stw[i] = out;
     }
     n_bytes += f.bytes;
     emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
   }
+#if KWOK_GROUP
+  // ---- phase 3: aligned groups of KWOK_GROUP lanes rewritten whole wherever any member
+  // changed; unchanged members come from the phase-1 registers (not algorithmic bytes: the
+  // PMC WRITE_SIZE pass shows their cost)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  constexpr unsigned long long kGrpMask = (KWOK_GROUP >= 64) ? ~0ull : ((1ull << KWOK_GROUP) - 1ull);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long rm = rowmask[k];
+    if (!rm) continue;
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
+    if ((full || i < a.n) && ((rm >> g0) & kGrpMask)) {
+      W val = v[k];
+      bool write = true;
+      if ((rm >> lane) & 1ull) {
+        const uint32_t p = s_pos[wave][k * 64 + lane];
+        if (p < kStash) unstash(wr[p], val);
+        else write = false;  // spill-over items were written in phase 2
+      }
+      if (write) stw[i] = val;
+    }
+  }
+#endif
 
-  // per-wave fired count (read by kwk_fired's scan) and block statistics
+  // ---- per-wave fired count (read by kwk_fired's scan) and block statistics
   for (int off = 32; off > 0; off >>= 1) {
     n_matched += __shfl_xor(n_matched, off);
     n_bytes += __shfl_xor(n_bytes, off);
@@ -552,7 +619,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     a.wave_counts[wave_id] = seg_n;
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], seg_n);
-    atomicAdd(&s_stat[2], n_bytes + 4u);  // + the wave's fired count word
+    atomicAdd(&s_stat[2], n_bytes + wave_bytes + 4u);  // + the wave's fired count word
   }
   __syncthreads();
   if (threadIdx.x < 3 + n_stages) {
@@ -1114,6 +1181,15 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   a.now = now_ns;
   a.fire = fire ? 1u : 0u;
   a.fmt = e->fmt;
+  if (e->fmt.narrow) {  // flag bits sit at fshift in the packed word (sched bits 8..12 there)
+    const uint32_t fs = e->fmt.fshift;
+    a.raw = RawTest{(KWK_F_MANAGED >> 8) << fs, (KWK_F_DIRTY >> 8) << fs, (KWK_F_ALIVE >> 8) << fs, e->fmt.sshift,
+                    e->fmt.smask, e->fmt.none_code, e->harness.terminal_mask & e->fmt.pmask,
+                    e->harness.deletion_bit & e->fmt.pmask};
+  } else {
+    a.raw = RawTest{KWK_F_MANAGED, KWK_F_DIRTY, KWK_F_ALIVE, 0, 0xFFu, KWK_STAGE_NONE, e->harness.terminal_mask,
+                    e->harness.deletion_bit};
+  }
   a.harness = e->harness;
   if (!fire) a.harness.enable = 0;
   const bool nar = e->fmt.narrow != 0;
