@@ -22,6 +22,13 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+// cost-isolation experiments only (wrong results): skip the state write-back / fired records
+#ifndef KWOK_EXP_NOWRITE
+#define KWOK_EXP_NOWRITE 0
+#endif
+#ifndef KWOK_EXP_NOFIRED
+#define KWOK_EXP_NOFIRED 0
+#endif
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -411,7 +418,7 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   if (!bal) return;
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
+    if (!KWOK_EXP_NOFIRED) seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
     n_bytes += 8;
   }
   seg_n += (uint32_t)__popcll(bal);
@@ -444,7 +451,30 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 #define KWOK_GROUP 0
 #endif
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
-constexpr int kStash = 192;      // work items whose word + due stay in LDS per wave (the rest are re-read)
+#ifndef KWOK_STASH
+#define KWOK_STASH 192
+#endif
+constexpr int kStash = KWOK_STASH;      // work items whose word + due stay in LDS per wave (the rest are re-read)
+
+// Streamed loads go through buffer resources (T8 in cdna_hip_programming.md): a load past the
+// resource's byte size returns 0, so the tile tail and "load due only where a stage is
+// pending" need no exec-mask branches (0 = MANAGED clear = never work).  Offsets are 32-bit:
+// kwk_engine_create caps capacity so that capacity * 8 bytes fit.
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void buf_load(uint32_t& w, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  w = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_load(uint2& w, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  w = make_uint2(t[0], t[1]);
+}
+__device__ __forceinline__ int64_t buf_load_i64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return (int64_t)(((uint64_t)t[1] << 32) | t[0]);
+}
 
 __device__ __forceinline__ uint32_t fw_of(uint2 w) { return w.y; }      // word holding flags + stage
 __device__ __forceinline__ uint32_t pw_of(uint2 w) { return w.x; }      // word holding pred
@@ -484,49 +514,50 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
-  const uint64_t base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64 + lane;
-  const uint64_t wave_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  kwk_fired_rec* __restrict__ seg = a.fired + wave_id * (64 * K);
   W* __restrict__ stw = reinterpret_cast<W*>(a.st);
   const StateFmt fmt = a.fmt;
   const RawTest R = a.raw;
-  const bool full = (uint64_t)(blockIdx.x + 1) * (kBlock * K) <= a.n;
-
-  uint32_t seg_n = 0;       // wave-uniform
-  uint32_t n_matched = 0;   // per lane
-  uint32_t n_bytes = 0;     // per lane: algorithmic bytes of the heavy path (DESIGN.md §5)
-  uint32_t wave_bytes = 0;  // wave-uniform: streamed words + due reads
-
-  // ---- phase 1
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n * kWordBytes);
+  const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ wr = s_rec[wave];
+
+  uint32_t n_matched = 0;   // per lane
+  uint32_t n_bytes = 0;     // per lane: algorithmic bytes of the heavy path (DESIGN.md §5)
+  uint32_t wave_bytes = 0;  // wave-uniform: fired count words
+  uint32_t wave_fired = 0;  // wave-uniform
+
+  // Persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ... so the per-block
+  // set-up (stage deltas into LDS, statistics) is paid once per CU slot, not once per tile.
+  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kBlock * K - 1) / (kBlock * K));
+  for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  const uint32_t ibase = tile * (uint32_t)(kBlock * K) + wave * 64 + lane;
+  const uint64_t base = ibase;
+  const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;  // fired segment of (tile, wave)
+  kwk_fired_rec* __restrict__ seg = a.fired + seg_id * (64 * K);
+  const bool full = (uint64_t)(tile + 1) * (kBlock * K) <= a.n;
+  uint32_t seg_n = 0;  // wave-uniform
+
+  // ---- phase 1
 #if KWOK_GROUP
   unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
 #endif
   uint32_t n_work = 0;  // wave-uniform
   W v[K];
-  if (full) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = stw[base + (uint64_t)k * kBlock];
-    wave_bytes += 64u * K * kWordBytes;
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint64_t i = base + (uint64_t)k * kBlock;
-      const bool in = i < a.n;
-      v[k] = in ? stw[i] : W{};  // MANAGED clear out of range: never work
-      wave_bytes += kWordBytes * (uint32_t)__popcll(__ballot(in));
-    }
-  }
-  int64_t d[K];  // due times, loaded only where a stage is pending
+  for (int k = 0; k < K; ++k) buf_load(v[k], st_rs, (ibase + (uint32_t)k * kBlock) * kWordBytes);
+  int64_t d[K];  // due times, loaded only where a stage is pending (else an out-of-range 0)
   uint32_t pend_bits = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t fw = fw_of(v[k]);
     const bool pend = (fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code;
     pend_bits |= (pend ? 1u : 0u) << k;
-    d[k] = pend ? a.due[base + (uint64_t)k * kBlock] : 0;
-    wave_bytes += 8u * (uint32_t)__popcll(__ballot(pend));
+    d[k] = buf_load_i64(due_rs, pend ? (ibase + (uint32_t)k * kBlock) * 8u : kOOB);
+  }
+  {  // streamed words of this lane + its due reads
+    const uint32_t in_k = full ? (uint32_t)K : (ibase >= a.n ? 0u : min((uint32_t)K, (a.n - ibase + kBlock - 1) / kBlock));
+    n_bytes += kWordBytes * in_k + 8u * (uint32_t)__popc(pend_bits);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -552,7 +583,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   // ---- phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup
   // barrier) orders the cross-lane LDS hand-off.
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const uint64_t wave_base = (uint64_t)blockIdx.x * (kBlock * K) + wave * 64;
+  const uint64_t wave_base = (uint64_t)tile * (kBlock * K) + wave * 64;
   for (uint32_t c = 0; c < n_work; c += 64) {
     const uint32_t j = c + lane;
     Fire f{false, 0, 0, 0};
@@ -580,7 +611,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (j < kStash) wr[j] = stash_of(out, 0);  // written back in phase 3 with its group
       else
 #endif
-        stw[i] = out;
+      if (!KWOK_EXP_NOWRITE) stw[i] = out;
     }
     n_bytes += f.bytes;
     emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
@@ -610,16 +641,23 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   }
 #endif
 
-  // ---- per-wave fired count (read by kwk_fired's scan) and block statistics
+  // per-(tile, wave) fired count, read by kwk_fired's scan
+  if (lane == 0) a.wave_counts[seg_id] = seg_n;
+  wave_fired += seg_n;
+  wave_bytes += 4u;  // the fired count word
+  // the next tile reuses this wave's LDS lists: keep its phase-1 writes after these reads
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }  // tile loop
+
+  // ---- block statistics
   for (int off = 32; off > 0; off >>= 1) {
     n_matched += __shfl_xor(n_matched, off);
     n_bytes += __shfl_xor(n_bytes, off);
   }
   if (lane == 0) {
-    a.wave_counts[wave_id] = seg_n;
     atomicAdd(&s_stat[0], n_matched);
-    atomicAdd(&s_stat[1], seg_n);
-    atomicAdd(&s_stat[2], n_bytes + wave_bytes + 4u);  // + the wave's fired count word
+    atomicAdd(&s_stat[1], wave_fired);
+    atomicAdd(&s_stat[2], n_bytes + wave_bytes);
   }
   __syncthreads();
   if (threadIdx.x < 3 + n_stages) {
@@ -809,7 +847,7 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0;
-  uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 16 | 32)
+  uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 8 | 16 | 32)
   uint32_t objs_narrow = 16;
   uint32_t last_objs = 16;
   bool loaded_table = false;
@@ -819,6 +857,8 @@ struct kwk_engine {
   void* d_st = nullptr;       // state word per slot (8-byte capacity; format in fmt)
   StateFmt fmt{};             // current state format (wide until a table allows narrow)
   bool force_wide = false;
+  int n_cus = 256;
+  bool grid_per_tile = false;
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -932,6 +972,8 @@ const char* kwk_last_error(void) { return g_err.c_str(); }
 kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   if (!d || !out) return fail(KWK_EINVAL, "null argument");
   if (d->capacity == 0) return fail(KWK_EINVAL, "capacity must be > 0");
+  if ((uint64_t)d->capacity * 8u >= kOOB)  // 32-bit buffer offsets of the due column (sweep phase 1)
+    return fail(KWK_ECAP, "capacity above 536870909 slots per engine: shard the kind over more engines");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (d->device < 0 || d->device >= ndev) return fail(KWK_EINVAL, "device ordinal out of range");
@@ -944,13 +986,17 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->kind_salt = d->kind_salt;
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
   e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
+  e->grid_per_tile = true;  // one block per tile: measured faster than the persistent grid with churn
+  if (const char* v = getenv("KWOK_SWEEP_GRID")) e->grid_per_tile = strcmp(v, "persist") != 0;
   if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
     const int k = atoi(v);
     if (k == 8 || k == 16) e->objs_wide = (uint32_t)k;
-    if (k == 16 || k == 32) e->objs_narrow = (uint32_t)k;
+    if (k == 8 || k == 16 || k == 32) e->objs_narrow = (uint32_t)k;
   }
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
+  if (hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || e->n_cus <= 0)
+    e->n_cus = 256;
   const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
 #define ALLOC(p, bytes)                                                          \
   do {                                                                           \
@@ -1158,6 +1204,22 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
   return KWK_OK;
 }
 
+// sweep grid: one block per tile (default), or KWOK_SWEEP_GRID=persist: every CU slot the
+// occupancy allows, each block walking tiles (faster on idle sweeps, slower with churn on
+// MI355X, profiles/r1/README.md)
+extern "C++" template <bool H, int K, bool N>
+static uint32_t sweep_grid(kwk_engine* e, uint32_t tiles) {
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<H, K, N>, kBlock, 0) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 1;
+  }
+  if (e->grid_per_tile) return tiles;
+  const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
+  return tiles < g ? tiles : g;
+}
+
 static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
@@ -1197,12 +1259,14 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   const uint32_t tile = kBlock * K;
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
   const bool h = a.harness.enable != 0;
-#define LAUNCH(HV, KV, NV) hipLaunchKernelGGL((sweep_kernel<HV, KV, NV>), dim3(blocks), dim3(kBlock), 0, e->stream, a)
+#define LAUNCH(HV, KV, NV) \
+  hipLaunchKernelGGL((sweep_kernel<HV, KV, NV>), dim3(sweep_grid<HV, KV, NV>(e, blocks)), dim3(kBlock), 0, e->stream, a)
   if (!nar) {
     if (K == 8) { if (h) LAUNCH(true, 8, false); else LAUNCH(false, 8, false); }
     else { if (h) LAUNCH(true, 16, false); else LAUNCH(false, 16, false); }
   } else {
     if (K == 32) { if (h) LAUNCH(true, 32, true); else LAUNCH(false, 32, true); }
+    else if (K == 8) { if (h) LAUNCH(true, 8, true); else LAUNCH(false, 8, true); }
     else { if (h) LAUNCH(true, 16, true); else LAUNCH(false, 16, true); }
   }
 #undef LAUNCH
