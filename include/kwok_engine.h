@@ -235,6 +235,59 @@ kwk_status kwk_usage(kwk_engine* eng, int64_t now_ns);
 /* node_out: n_nodes x {cpu, mem, cpu_cumulative, mem_cumulative}; cluster_out: {cpu, mem} */
 kwk_status kwk_usage_read(kwk_engine* eng, double* node_out, double* cluster_out);
 
+/* ------------------------------------------------------------------ node leases */
+/* NodeLeaseController (pkg/kwok/controllers/node_lease_controller.go) on a NODE engine: one
+ * lease record per node slot — the informer's cached coordination/v1 Lease plus the
+ * controller's queue entry — advanced on the device by kwk_lease_step. */
+#define KWK_LEASE_EXISTS (1u << 0)    /* the Lease object exists (getLease ok) */
+#define KWK_LEASE_HOLDER (1u << 1)    /* spec.holderIdentity != nil */
+#define KWK_LEASE_DURATION (1u << 2)  /* spec.leaseDurationSeconds != nil */
+#define KWK_LEASE_RENEW (1u << 3)     /* spec.renewTime != nil */
+#define KWK_LEASE_HOLD (1u << 4)      /* node in holdLeaseSet (TryHold; ReleaseHold clears it) */
+#define KWK_LEASE_QUEUED (1u << 5)    /* a sync is queued at next_try_ns (TryHold queues one at once) */
+typedef struct {
+  int64_t renew_ns;      /* spec.renewTime, unix ns (a MicroTime: microsecond precision) */
+  int64_t next_try_ns;   /* delay-queue due time of the node's next sync */
+  uint32_t holder;       /* spec.holderIdentity, interned by the host */
+  int32_t duration_s;    /* spec.leaseDurationSeconds */
+  int32_t transitions;   /* spec.leaseTransitions */
+  uint32_t flags;        /* KWK_LEASE_* */
+} kwk_lease;             /* 32 bytes */
+
+typedef struct {
+  uint32_t holder_id;          /* this kwok's HolderIdentity (controller.go:275), interned */
+  int32_t lease_duration_s;    /* NodeLeaseDurationSeconds */
+  int64_t renew_interval_ns;   /* leaseDuration / 4 (controller.go:247) */
+  double renew_jitter;         /* RenewIntervalJitter: 0.04 (controller.go:249) */
+  uint32_t manage_nodes;       /* 1: the node's MANAGED bit follows Held() (readOnlyFunc,
+                                * controller.go:285-288) and a successful sync re-matches it */
+  uint32_t reserved;
+} kwk_lease_params;
+
+/* API writes of the last kwk_lease_step, as kwk_fired_rec {slot, op, 0} (unordered) */
+#define KWK_LEASE_OP_CREATE 1   /* ensureLease (node_lease_controller.go:225-249) */
+#define KWK_LEASE_OP_RENEW 2    /* renewLease by the holder (:252-275) */
+#define KWK_LEASE_OP_ACQUIRE 3  /* renewLease taking over an absent or expired holder (transitions + 1) */
+#define KWK_LEASE_OP_BUSY 4     /* held by another holder: no write, retried after interval() */
+
+typedef struct {
+  uint64_t steps, creates, renews, acquires, busy;
+} kwk_lease_counters;
+
+kwk_status kwk_lease_config(kwk_engine* nodes, const kwk_lease_params* cfg);
+/* lease informer events / TryHold / ReleaseHold: overwrite records [first, first+n) */
+kwk_status kwk_lease_set(kwk_engine* nodes, uint32_t first, uint32_t n, const kwk_lease* leases);
+/* one pass of syncWorker over every held node whose sync is due (enqueue only).
+ * interval() jitter uses Philox (key = seed ^ kind_salt, ctr = (slot_base+slot, step, 3)) */
+kwk_status kwk_lease_step(kwk_engine* nodes, int64_t now_ns, uint64_t seed, uint64_t step);
+kwk_status kwk_lease_ops(kwk_engine* nodes, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
+kwk_status kwk_lease_read(kwk_engine* nodes, uint32_t first, uint32_t n, kwk_lease* out);
+kwk_status kwk_lease_stats(kwk_engine* nodes, kwk_lease_counters* out);
+/* pods of the nodes synced by the last lease step (node j owns pod slots [node_ptr[j],
+ * node_ptr[j+1])): MANAGED follows Held(), a successful sync re-matches pods with no queued
+ * stage (podsOnNodeSyncWorker, controller.go:559-573) */
+kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr);
+
 /* cluster aggregates: counts[k] = alive objects with (pred & masks[k]) != 0 (mask 0 = all
  * alive objects), k < 16 — e.g. the phase histogram all-reduced across GPUs (synchronises) */
 kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);

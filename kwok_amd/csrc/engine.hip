@@ -75,15 +75,23 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
   }
 }
 
-// rand.Intn / rand.Int63n replacement (DESIGN.md §RNG): floor(u64 * n / 2^64), n > 0
-__device__ __forceinline__ int64_t rng_below(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key, int64_t n) {
+__device__ __forceinline__ uint64_t philox_u64(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key) {
   uint32_t c0 = (uint32_t)gslot, c1 = (uint32_t)step, c2 = (uint32_t)(step >> 32), c3 = site;
   philox10(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32));
-  const uint64_t u = (uint64_t)c0 | ((uint64_t)c1 << 32);
-  return (int64_t)__umul64hi(u, (uint64_t)n);
+  return (uint64_t)c0 | ((uint64_t)c1 << 32);
 }
 
-constexpr uint32_t kSitePick = 1, kSiteJitter = 2;
+// rand.Intn / rand.Int63n replacement (DESIGN.md §RNG): floor(u64 * n / 2^64), n > 0
+__device__ __forceinline__ int64_t rng_below(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key, int64_t n) {
+  return (int64_t)__umul64hi(philox_u64(gslot, step, site, key), (uint64_t)n);
+}
+
+// rand.Float64 replacement: (u64 >> 11) * 2^-53, in [0, 1)
+__device__ __forceinline__ double rng_float64(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key) {
+  return (double)(philox_u64(gslot, step, site, key) >> 11) * 0x1.0p-53;
+}
+
+constexpr uint32_t kSitePick = 1, kSiteJitter = 2, kSiteLeaseJitter = 3;
 
 __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
   int64_t r;
@@ -837,6 +845,149 @@ __global__ void usage_total_kernel(const double* __restrict__ part, uint32_t n_b
   }
 }
 
+// ------------------------------------------------------------------ node leases
+// NodeLeaseController.syncWorker (pkg/kwok/controllers/node_lease_controller.go:108-143) for
+// every held node whose queued sync is due, one lane per lease:
+//   dur  = interval() = wait.Jitter(renewInterval, jitter)          :145-147 (Philox site 3)
+//   sync: lease exists ? (tryAcquireOrRenew ? renewLease : "held by another")
+//                      : ensureLease                                :174-275
+//   next = lease ok ? nextTryDuration(dur, expireTime - now, hold) : dur   :131-141, 309-338
+//   AddWeightAfter(node, next)                                       (<= 0: runnable now)
+// The API writes are applied to the device copy of the lease (what the informer cache shows
+// the next Held()); renewTime is a MicroTime, so it keeps microseconds.  With manage_nodes,
+// the node's MANAGED bit follows Held() (readOnlyFunc, controller.go:285-288) and a
+// successful sync re-matches a node with no queued stage (onNodeManaged -> ManageNode,
+// controller.go:276-279, 307-329; preprocess skips nodes whose queued job is current).
+struct LeaseArgs {
+  kwk_lease* __restrict__ lease;
+  uint8_t* __restrict__ op;          // per node: KWK_LEASE_OP_* of this step (0 = no sync)
+  void* __restrict__ st;             // node engine state words
+  kwk_fired_rec* __restrict__ ops;   // API writes (slot, op) of this step
+  uint32_t* __restrict__ n_ops;
+  unsigned long long* __restrict__ stats;  // [5]: steps, creates, renews, acquires, busy
+  StateFmt fmt;
+  uint32_t n;
+  uint64_t slot_base;
+  uint64_t key;
+  uint64_t step;
+  int64_t now;
+  kwk_lease_params cfg;
+};
+
+__device__ __forceinline__ bool lease_try_acquire_or_renew(const kwk_lease& L, uint32_t me, int64_t now) {
+  if (!(L.flags & KWK_LEASE_HOLDER) || L.holder == me) return true;
+  if (!(L.flags & KWK_LEASE_RENEW) || !(L.flags & KWK_LEASE_DURATION)) return true;
+  return sat_add(L.renew_ns, (int64_t)L.duration_s * 1000000000) < now;  // expireTime.Before(now)
+}
+
+__device__ __forceinline__ int64_t lease_next_try(int64_t renew_interval, int64_t expire, bool hold) {
+  if (!hold) return renew_interval;
+  if (renew_interval < expire) return renew_interval;
+  if (expire < 1000000000) return 1000000000;
+  return expire;
+}
+
+__global__ __launch_bounds__(kBlock) void lease_kernel(LeaseArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t op = 0;
+  if (i < a.n) {
+    kwk_lease L = a.lease[i];
+    if ((L.flags & (KWK_LEASE_HOLD | KWK_LEASE_QUEUED)) == (KWK_LEASE_HOLD | KWK_LEASE_QUEUED) &&
+        L.next_try_ns <= a.now) {
+      const uint32_t me = a.cfg.holder_id;
+      const double factor = a.cfg.renew_jitter <= 0.0 ? 1.0 : a.cfg.renew_jitter;
+      const double u = rng_float64(a.slot_base + i, a.step, kSiteLeaseJitter, a.key);
+      const int64_t dur = a.cfg.renew_interval_ns + (int64_t)(u * factor * (double)a.cfg.renew_interval_ns);
+      const int64_t now_us = a.now - a.now % 1000;  // metav1.MicroTime
+      bool ok = false;
+      if (L.flags & KWK_LEASE_EXISTS) {
+        if (lease_try_acquire_or_renew(L, me, a.now)) {
+          op = KWK_LEASE_OP_RENEW;
+          if (!(L.flags & KWK_LEASE_HOLDER) || L.holder != me) {  // renewLease transitions (:255-260)
+            L.holder = me;
+            L.duration_s = a.cfg.lease_duration_s;
+            L.transitions += 1;
+            L.flags |= KWK_LEASE_HOLDER | KWK_LEASE_DURATION;
+            op = KWK_LEASE_OP_ACQUIRE;
+          }
+          L.renew_ns = now_us;
+          L.flags |= KWK_LEASE_RENEW;
+          ok = true;
+        } else {
+          op = KWK_LEASE_OP_BUSY;  // sync returns (nil, nil): expireTime not ok
+        }
+      } else {  // ensureLease
+        L.flags |= KWK_LEASE_EXISTS | KWK_LEASE_HOLDER | KWK_LEASE_DURATION | KWK_LEASE_RENEW;
+        L.holder = me;
+        L.duration_s = a.cfg.lease_duration_s;
+        L.renew_ns = now_us;
+        L.transitions = 0;
+        op = KWK_LEASE_OP_CREATE;
+        ok = true;
+      }
+      int64_t next = dur;
+      if (ok) {
+        const int64_t expire = sat_add(L.renew_ns, (int64_t)L.duration_s * 1000000000);
+        next = lease_next_try(dur, expire - a.now, lease_try_acquire_or_renew(L, me, a.now));
+      }
+      L.next_try_ns = next <= 0 ? a.now : sat_add(a.now, next);
+      a.lease[i] = L;
+      if (a.cfg.manage_nodes) {
+        uint2 s = load_state(a.st, i, a.fmt);
+        const bool held = (L.flags & KWK_LEASE_EXISTS) && (L.flags & KWK_LEASE_HOLDER) && L.holder == me;
+        if (held) {
+          s.y |= KWK_F_MANAGED;
+          if (ok && (s.y & KWK_F_ALIVE) && (s.y & 0xFFu) == KWK_STAGE_NONE) s.y |= KWK_F_DIRTY;
+        } else {
+          s.y &= ~KWK_F_MANAGED;
+        }
+        store_state(a.st, i, s, a.fmt);
+      }
+    }
+    a.op[i] = (uint8_t)op;
+  }
+  // API writes of this step, compacted per wave (one atomic per wave), and counters
+  const unsigned long long bal = __ballot(op != 0);
+  if (bal) {
+    uint32_t base = 0;
+    if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(a.n_ops, (uint32_t)__popcll(bal));
+    base = __shfl(base, __ffsll((long long)bal) - 1);
+    if (op) a.ops[base + __popcll(bal & ((1ull << lane) - 1ull))] = kwk_fired_rec{i, (uint16_t)op, 0};
+    for (uint32_t k = 1; k <= 4; ++k) {
+      const unsigned long long m = __ballot(op == k);
+      if (m && lane == 0) atomicAdd(&a.stats[k], (unsigned long long)__popcll(m));
+    }
+  }
+}
+
+// pods on nodes whose lease sync ran this step: MANAGED follows Held(); a successful sync
+// re-matches the pods with no queued stage (podsOnNodeSyncWorker, controller.go:559-573).
+// One wave per node over its node-sorted pods.
+__global__ __launch_bounds__(kBlock) void lease_pods_kernel(void* __restrict__ st, StateFmt fmt,
+                                                            const uint32_t* __restrict__ node_ptr,
+                                                            const uint8_t* __restrict__ op,
+                                                            const kwk_lease* __restrict__ lease, uint32_t me,
+                                                            uint32_t n_nodes) {
+  const uint32_t node = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (node >= n_nodes) return;
+  const uint32_t o = op[node];
+  if (o == 0) return;
+  const kwk_lease L = lease[node];
+  const bool held = (L.flags & KWK_LEASE_EXISTS) && (L.flags & KWK_LEASE_HOLDER) && L.holder == me;
+  const bool ok = o != KWK_LEASE_OP_BUSY;
+  for (uint32_t p = node_ptr[node] + (threadIdx.x & 63); p < node_ptr[node + 1]; p += 64) {
+    uint2 s = load_state(st, p, fmt);
+    if (held) {
+      s.y |= KWK_F_MANAGED;
+      if (ok && (s.y & KWK_F_ALIVE) && (s.y & 0xFFu) == KWK_STAGE_NONE) s.y |= KWK_F_DIRTY;
+    } else {
+      s.y &= ~KWK_F_MANAGED;
+    }
+    store_state(st, p, s, fmt);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ engine object
@@ -890,6 +1041,16 @@ struct kwk_engine {
   // staging for upserts
   void* d_stage_buf = nullptr;
   size_t stage_bytes = 0;
+
+  // node leases (node engines only)
+  bool lease_on = false;
+  kwk_lease_params lease_cfg{};
+  kwk_lease* d_lease = nullptr;
+  uint8_t* d_lease_op = nullptr;
+  kwk_fired_rec* d_lease_ops = nullptr;
+  uint32_t* d_lease_nops = nullptr;
+  unsigned long long* d_lease_stats = nullptr;
+  uint64_t lease_steps = 0;
 
   std::vector<hipEvent_t> events;
 };
@@ -1043,7 +1204,8 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
-                  e->d_usage_part, e->d_cluster, e->d_stage_buf};
+                  e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_lease, e->d_lease_op, e->d_lease_ops,
+                  e->d_lease_nops, e->d_lease_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
@@ -1432,6 +1594,125 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
   }
   HIP_TRY(hipMemcpyAsync(counts, d_out, 8 * (size_t)n_masks, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+// ---- node leases
+kwk_status kwk_lease_config(kwk_engine* e, const kwk_lease_params* cfg) {
+  if (!e || !cfg) return fail(KWK_EINVAL, "null argument");
+  if (cfg->renew_interval_ns <= 0) return fail(KWK_EINVAL, "renew_interval_ns must be > 0");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (!e->d_lease) {
+    HIP_TRY(hipMalloc(&e->d_lease, sizeof(kwk_lease) * (size_t)e->capacity));
+    HIP_TRY(hipMalloc(&e->d_lease_op, (size_t)e->capacity));
+    HIP_TRY(hipMalloc(&e->d_lease_ops, sizeof(kwk_fired_rec) * (size_t)e->capacity));
+    HIP_TRY(hipMalloc(&e->d_lease_nops, sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&e->d_lease_stats, sizeof(unsigned long long) * 5));
+    HIP_TRY(hipMemset(e->d_lease, 0, sizeof(kwk_lease) * (size_t)e->capacity));
+    HIP_TRY(hipMemset(e->d_lease_op, 0, (size_t)e->capacity));
+    HIP_TRY(hipMemset(e->d_lease_nops, 0, sizeof(uint32_t)));
+    HIP_TRY(hipMemset(e->d_lease_stats, 0, sizeof(unsigned long long) * 5));
+  }
+  e->lease_cfg = *cfg;
+  e->lease_on = true;
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_set(kwk_engine* e, uint32_t first, uint32_t n, const kwk_lease* leases) {
+  if (!e || (n && !leases)) return fail(KWK_EINVAL, "null argument");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if ((uint64_t)first + n > e->capacity) return fail(KWK_ECAP, "lease range beyond capacity");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (n) HIP_TRY(hipMemcpy(e->d_lease + first, leases, sizeof(kwk_lease) * n, hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipMemsetAsync(e->d_lease_nops, 0, sizeof(uint32_t), e->stream));
+  ++e->lease_steps;
+  if (e->n_active == 0) return KWK_OK;
+  LeaseArgs a;
+  a.lease = e->d_lease;
+  a.op = e->d_lease_op;
+  a.st = e->d_st;
+  a.ops = e->d_lease_ops;
+  a.n_ops = e->d_lease_nops;
+  a.stats = e->d_lease_stats;
+  a.fmt = e->fmt;
+  a.n = e->n_active;
+  a.slot_base = e->slot_base;
+  a.key = seed ^ ((uint64_t)e->kind_salt << 32);
+  a.step = step;
+  a.now = now_ns;
+  a.cfg = e->lease_cfg;
+  hipLaunchKernelGGL(lease_kernel, dim3((e->n_active + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
+  HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_ops(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out) {
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  uint32_t n = 0;
+  HIP_TRY(hipMemcpyAsync(&n, e->d_lease_nops, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_out = n;
+  if (!out || n == 0) return KWK_OK;
+  if (n > cap) return fail(KWK_ECAP, "lease ops buffer too small: need " + std::to_string(n));
+  HIP_TRY(hipMemcpy(out, e->d_lease_ops, sizeof(kwk_fired_rec) * n, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_lease* out) {
+  if (!e || (n && !out)) return fail(KWK_EINVAL, "null argument");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (n) HIP_TRY(hipMemcpy(out, e->d_lease + first, sizeof(kwk_lease) * n, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_stats(kwk_engine* e, kwk_lease_counters* out) {
+  if (!e || !out) return fail(KWK_EINVAL, "null argument");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  unsigned long long h[5];
+  HIP_TRY(hipMemcpyAsync(h, e->d_lease_stats, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  out->steps = e->lease_steps;
+  out->creates = h[1];
+  out->renews = h[2];
+  out->acquires = h[3];
+  out->busy = h[4];
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr) {
+  if (!pods || !nodes || !node_ptr) return fail(KWK_EINVAL, "null argument");
+  if (!nodes->lease_on) return fail(KWK_ESTATE, "node engine has no lease configuration");
+  if (n_nodes > nodes->n_active) return fail(KWK_EINVAL, "n_nodes beyond the node engine's objects");
+  if (pods->device != nodes->device) return fail(KWK_EINVAL, "pod and node engines on different devices");
+  if (node_ptr[0] != 0 || node_ptr[n_nodes] > pods->n_active) return fail(KWK_EINVAL, "node_ptr out of range");
+  for (uint32_t j = 0; j < n_nodes; ++j)
+    if (node_ptr[j + 1] < node_ptr[j]) return fail(KWK_EINVAL, "node_ptr must be non-decreasing");
+  if (kwk_status st = set_dev(pods)) return st;
+  if (n_nodes == 0) return KWK_OK;
+  if (kwk_status st = ensure_stage_buf(pods, 4 * ((size_t)n_nodes + 1))) return st;
+  // the node engine's lease step must be complete before the pods read its results
+  HIP_TRY(hipStreamSynchronize(nodes->stream));
+  HIP_TRY(hipMemcpyAsync(pods->d_stage_buf, node_ptr, 4 * ((size_t)n_nodes + 1), hipMemcpyHostToDevice, pods->stream));
+  hipLaunchKernelGGL(lease_pods_kernel, dim3((n_nodes + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0,
+                     pods->stream, pods->d_st, pods->fmt, (const uint32_t*)pods->d_stage_buf, nodes->d_lease_op,
+                     nodes->d_lease, nodes->lease_cfg.holder_id, n_nodes);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(pods->stream));
   return KWK_OK;
 }
 

@@ -83,11 +83,32 @@ class EngineDesc(C.Structure):
 ENGINE_WIDE_STATE = 1
 
 
+class Lease(C.Structure):
+    _fields_ = [("renew_ns", C.c_int64), ("next_try_ns", C.c_int64), ("holder", C.c_uint32), ("duration_s", C.c_int32),
+                ("transitions", C.c_int32), ("flags", C.c_uint32)]
+
+
+class LeaseParams(C.Structure):
+    _fields_ = [("holder_id", C.c_uint32), ("lease_duration_s", C.c_int32), ("renew_interval_ns", C.c_int64),
+                ("renew_jitter", C.c_double), ("manage_nodes", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class LeaseCounters(C.Structure):
+    _fields_ = [("steps", C.c_uint64), ("creates", C.c_uint64), ("renews", C.c_uint64), ("acquires", C.c_uint64),
+                ("busy", C.c_uint64)]
+
+
+LEASE_EXISTS, LEASE_HOLDER, LEASE_DURATION, LEASE_RENEW, LEASE_HOLD, LEASE_QUEUED = 1, 2, 4, 8, 16, 32
+LEASE_OP_CREATE, LEASE_OP_RENEW, LEASE_OP_ACQUIRE, LEASE_OP_BUSY = 1, 2, 3, 4
+LEASE_DTYPE = np.dtype([("renew_ns", "<i8"), ("next_try_ns", "<i8"), ("holder", "<u4"), ("duration_s", "<i4"),
+                        ("transitions", "<i4"), ("flags", "<u4")])
+
 HOT_DTYPE = np.dtype([("pred", "<u4"), ("sched", "<u4"), ("due", "<i8")])
 VALUE_DTYPE = np.dtype([("value", "<i8"), ("nsec", "<i4"), ("kind", "<i4")])
 FIRED_DTYPE = np.dtype([("slot", "<u4"), ("stage", "<u2"), ("flags", "<u2")])
 
 assert C.sizeof(Hot) == 16 and C.sizeof(Value) == 16 and C.sizeof(StageDesc) == 96
+assert C.sizeof(Lease) == 32 == LEASE_DTYPE.itemsize and C.sizeof(LeaseParams) == 32
 assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.itemsize == 8
 
 # every symbol include/kwok_engine.h declares (checked by the CPU test suite)
@@ -95,7 +116,8 @@ EXPORTS = [
     "kwk_last_error", "kwk_engine_create", "kwk_engine_destroy", "kwk_load_stages", "kwk_set_harness", "kwk_load",
     "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_match", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
-    "kwk_abi_version", "kwk_tile_objects", "kwk_count",
+    "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
+    "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods",
 ]
 
 _lib = None
@@ -142,6 +164,13 @@ def lib():
     L.kwk_event_record.argtypes = [C.c_void_p, C.c_uint32]
     L.kwk_event_elapsed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, _p(C.c_float)]
     L.kwk_count.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.kwk_lease_config.argtypes = [C.c_void_p, _p(LeaseParams)]
+    L.kwk_lease_set.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.kwk_lease_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
+    L.kwk_lease_ops.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_lease_read.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.kwk_lease_stats.argtypes = [C.c_void_p, _p(LeaseCounters)]
+    L.kwk_lease_sync_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_abi_version.restype = C.c_uint32
     L.kwk_tile_objects.restype = C.c_uint32
     for name in EXPORTS:

@@ -231,6 +231,49 @@ class Engine:
         abi.check(abi.lib().kwk_usage_read(self.h, abi.ptr(node), abi.ptr(cl)), "kwk_usage_read")
         return node, cl
 
+    # node leases (NodeLeaseController, node_lease_controller.go)
+    def lease_config(self, holder_id: int, lease_duration_s: int, renew_interval_ns: int = None,
+                     renew_jitter: float = 0.04, manage_nodes: bool = True):
+        """renew interval defaults to leaseDuration / 4 and jitter to 0.04 (controller.go:245-249)."""
+        if renew_interval_ns is None:
+            renew_interval_ns = lease_duration_s * 10**9 // 4
+        p = abi.LeaseParams(holder_id=holder_id, lease_duration_s=lease_duration_s,
+                            renew_interval_ns=renew_interval_ns, renew_jitter=renew_jitter,
+                            manage_nodes=1 if manage_nodes else 0)
+        abi.check(abi.lib().kwk_lease_config(self.h, C.byref(p)), "kwk_lease_config")
+
+    def lease_set(self, leases: np.ndarray, first: int = 0):
+        a = np.ascontiguousarray(leases, dtype=abi.LEASE_DTYPE)
+        abi.check(abi.lib().kwk_lease_set(self.h, first, len(a), abi.ptr(a)), "kwk_lease_set")
+
+    def lease_step(self, now_ns: int, seed: int, step: int):
+        abi.check(abi.lib().kwk_lease_step(self.h, now_ns, seed, step), "kwk_lease_step")
+
+    def lease_ops(self) -> np.ndarray:
+        n = C.c_uint32()
+        L = abi.lib()
+        abi.check(L.kwk_lease_ops(self.h, None, 0, C.byref(n)), "kwk_lease_ops")
+        out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
+        if n.value:
+            abi.check(L.kwk_lease_ops(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_lease_ops")
+        return out
+
+    def lease_read(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.n - first if n is None else n
+        out = np.zeros(n, dtype=abi.LEASE_DTYPE)
+        abi.check(abi.lib().kwk_lease_read(self.h, first, n, abi.ptr(out)), "kwk_lease_read")
+        return out
+
+    def lease_stats(self) -> dict:
+        c = abi.LeaseCounters()
+        abi.check(abi.lib().kwk_lease_stats(self.h, C.byref(c)), "kwk_lease_stats")
+        return {k: getattr(c, k) for k, _ in abi.LeaseCounters._fields_}
+
+    def lease_sync_pods(self, pods: "Engine", node_ptr):
+        """Pods on the nodes synced by this engine's last lease step (podsOnNodeSyncWorker)."""
+        ptr = np.ascontiguousarray(node_ptr, dtype=np.uint32)
+        abi.check(abi.lib().kwk_lease_sync_pods(pods.h, self.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_lease_sync_pods")
+
     # timing
     def event_record(self, idx: int):
         abi.check(abi.lib().kwk_event_record(self.h, idx), "kwk_event_record")

@@ -49,6 +49,7 @@ class OracleSim:
         self.due = [0] * n
         self.gen = [0] * n
         self.matcherr = [False] * n
+        self.managed = [True] * n   # readOnlyFunc: objects on nodes whose lease is not held are skipped
         self.harness = harness
         self.terminal = set(terminal)
         self.slot_base = slot_base
@@ -64,6 +65,8 @@ class OracleSim:
         renderer.funcs["Now"] = lambda: rfc3339nano(now_ns)
         fired = []
         for i in range(len(self.objs)):
+            if not self.managed[i]:  # read-only (watchResources skips it, controller.go:285-288)
+                continue
             o = self.objs[i]
             if self.harness:
                 if o is None:
@@ -101,6 +104,14 @@ class OracleSim:
                         flags |= 2
                 fired.append((i, s, flags))
         return fired
+
+    def set_managed(self, i: int, held: bool, resync: bool):
+        """Lease sync outcome for object i: MANAGED = Held(); a successful sync re-sends the
+        object to preprocess (ManageNode / podsOnNodeSyncWorker), which re-matches it unless a
+        job for its current version is queued (pod_controller.go:205-214)."""
+        self.managed[i] = held
+        if held and resync and self.pending[i] is None and self.objs[i] is not None:
+            self.dirty[i] = True
 
     def deletion_s(self, i: int) -> int:
         o = self.objs[i]

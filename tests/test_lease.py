@@ -1,0 +1,223 @@
+"""Node leases (NodeLeaseController, BASELINE C3): the oracle pinned by the reference's unit
+vectors and its controller scenario test; the device lease step (kwk_lease_step) bit-exact
+against the oracle, coupled to the node sweep (readOnlyFunc / ManageNode) and to the pods on
+those nodes (podsOnNodeSyncWorker)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from kwok_amd import workload as W
+from oracle import lease_ref as LR
+
+VEC = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "lease_vectors.json")))
+NOW = 1_700_000_000 * 10**9
+IDS = {"test": 1, "test-new": 2, "lease1": 11, "lease2": 12, "lease3": 13}
+
+
+def _lease(holder, duration_s, renew_rel_s, exists=True):
+    f = LR.EXISTS if exists else 0
+    L = LR.Lease(flags=f)
+    if holder is not None:
+        L.holder, L.flags = IDS[holder], L.flags | LR.HOLDER
+    if duration_s is not None:
+        L.duration_s, L.flags = duration_s, L.flags | LR.DURATION
+    if renew_rel_s is not None:
+        L.renew_ns, L.flags = NOW + renew_rel_s * 10**9, L.flags | LR.RENEW
+    return L
+
+
+@pytest.mark.parametrize("c", VEC["try_acquire_or_renew"], ids=lambda c: c["ref"])
+def test_try_acquire_or_renew(c):
+    L = _lease(c["holder"], c["duration_s"], c["renew_rel_s"])
+    assert LR.try_acquire_or_renew(L, IDS[c["self"]], NOW) is c["want"]
+
+
+@pytest.mark.parametrize("c", VEC["next_try_duration"], ids=lambda c: c["ref"])
+def test_next_try_duration(c):
+    ms = 10**6
+    assert LR.next_try_duration(c["renew_interval_ms"] * ms, c["expire_ms"] * ms, c["hold"]) == c["want_ms"] * ms
+
+
+@pytest.mark.parametrize("c", VEC["expire_time"], ids=lambda c: c["ref"])
+def test_expire_time(c):
+    L = _lease(c["holder"], c["duration_s"], c["renew_rel_s"])
+    t, ok = LR.expire_time(L)
+    assert ok is c["want_ok"]
+    if ok:
+        assert t == NOW + c["want_rel_s"] * 10**9
+
+
+def test_jitter_hook_range():
+    """wait.Jitter(10 s, 0.04) stays in [10 s, 10.4 s); maxFactor <= 0 means 1."""
+    for slot in range(200):
+        u = LR.float64_hook(7, slot, 3)
+        assert 0.0 <= u < 1.0
+        d = LR.jitter(10 * 10**9, 0.04, u)
+        assert 10 * 10**9 <= d < 10.4 * 10**9
+    assert LR.jitter(10, 0.0, 0.5) == 15
+
+
+def _scenario_leases():
+    sc = VEC["controller_scenario"]
+    names = ["lease0", "lease1", "lease2", "lease3", "lease4"]
+    leases = []
+    for n in names:
+        spec = sc["leases"].get(n)
+        L = _lease(spec["holder"], spec["duration_s"], spec["renew_rel_s"]) if spec else LR.Lease()
+        if n in sc["try_hold"]:  # TryHold: into holdLeaseSet, queued at once
+            L.flags |= LR.HOLD | LR.QUEUED
+            L.next_try_ns = NOW
+        leases.append(L)
+    return sc, names, leases
+
+
+def test_controller_scenario_oracle():
+    """TestNodeLeaseController (node_lease_controller_test.go:37-156) on the oracle."""
+    sc, names, leases = _scenario_leases()
+    sim = LR.LeaseSim(leases, IDS[sc["self"]], sc["lease_duration_s"], sc["renew_interval_s"] * 10**9, sc["jitter"])
+    sim.step(NOW, 1, 0)
+    for n, want in sc["after_1s_held"].items():
+        assert LR.held(sim.leases[names.index(n)], IDS[sc["self"]]) is want, n
+    # the apiserver deletes lease1: the informer cache no longer has it
+    sim.leases[names.index(sc["delete"])].flags &= ~(LR.EXISTS | LR.HOLDER | LR.DURATION | LR.RENEW)
+    sim.step(NOW + 2 * 10**9, 1, 1)
+    for n, want in sc["after_delete_held"].items():
+        assert LR.held(sim.leases[names.index(n)], IDS[sc["self"]]) is want, n
+
+
+def to_array(leases):
+    a = np.zeros(len(leases), dtype=[("renew_ns", "<i8"), ("next_try_ns", "<i8"), ("holder", "<u4"),
+                                     ("duration_s", "<i4"), ("transitions", "<i4"), ("flags", "<u4")])
+    for i, L in enumerate(leases):
+        a[i] = (L.renew_ns, L.next_try_ns, L.holder, L.duration_s, L.transitions, L.flags)
+    return a
+
+
+def assert_leases_equal(got, sim_leases, step):
+    want = to_array(sim_leases)
+    for f in want.dtype.names:
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert bad.size == 0, f"step {step}: lease field {f} differs at {bad[:8].tolist()}: " \
+                              f"{got[f][bad[:4]].tolist()} vs {want[f][bad[:4]].tolist()}"
+
+
+def c3_leases(n, now, rng):
+    """C3 lease mix: 50% absent (created), 20% our own stale lease, 20% foreign and expiring
+    during the run, 5% foreign and fresh, 5% not in the hold set."""
+    leases = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.5:
+            L = LR.Lease()
+        elif r < 0.7:
+            L = LR.Lease(flags=LR.EXISTS | LR.HOLDER | LR.DURATION | LR.RENEW, holder=1, duration_s=40,
+                         renew_ns=now - int(rng.integers(0, 60)) * 10**9, transitions=int(rng.integers(0, 3)))
+        elif r < 0.95:
+            L = LR.Lease(flags=LR.EXISTS | LR.HOLDER | LR.DURATION | LR.RENEW, holder=7, duration_s=40,
+                         renew_ns=now - (40 - int(rng.integers(0, 30))) * 10**9 if r < 0.9 else now)
+        else:
+            L = LR.Lease(flags=LR.EXISTS | LR.HOLDER | LR.DURATION | LR.RENEW, holder=7, duration_s=40,
+                         renew_ns=now - 100 * 10**9)
+        if r < 0.95 or i % 2:
+            L.flags |= LR.HOLD | LR.QUEUED
+            L.next_try_ns = now
+        leases.append(L)
+    return leases
+
+
+@pytest.mark.gpu
+def test_controller_scenario_gpu():
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    sc, names, leases = _scenario_leases()
+    objs = [W.node_object(n) for n in names]
+    prog = KindProgram(load_stage_files(*W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT)))
+    prog.explore(objs)
+    ing = Ingest(prog)
+    eng = Engine(prog, capacity=len(objs), kind_salt=1)
+    try:
+        eng.load_stages()
+        eng.load(*ing.columns(objs), ing.record_array())
+        eng.lease_config(IDS[sc["self"]], sc["lease_duration_s"], sc["renew_interval_s"] * 10**9, sc["jitter"])
+        eng.lease_set(to_array(leases))
+        sim = LR.LeaseSim(leases, IDS[sc["self"]], sc["lease_duration_s"], sc["renew_interval_s"] * 10**9, sc["jitter"])
+        eng.lease_step(NOW, 1, 0)
+        want_ops = sorted(sim.step(NOW, 1, 0))
+        assert sorted((int(r["slot"]), int(r["stage"])) for r in eng.lease_ops()) == want_ops
+        got = eng.lease_read()
+        assert_leases_equal(got, sim.leases, 0)
+        me = IDS[sc["self"]]
+        for n, want in sc["after_1s_held"].items():
+            i = names.index(n)
+            assert bool(got["flags"][i] & LR.EXISTS and got["flags"][i] & LR.HOLDER and got["holder"][i] == me) is want
+        assert eng.lease_stats()["creates"] == 1 and eng.lease_stats()["acquires"] == 1
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
+def test_c3_nodes_leases_pods_parity(wide):
+    """C3 shape at 96 nodes (node-initialize + node-heartbeat 20 s / 25 s, leases 40 s with a
+    10 s +- 4% renew, 250 ms tick for 50 s) with 4 pod-fast pods per node: lease step ->
+    node MANAGED / resync -> node sweep -> pod resync -> pod sweep, every step bit-exact
+    (lease records, lease API writes, fired sets, object states) against the oracle."""
+    from tests.parity_util import NOW0, build, compare_state
+    rng = np.random.default_rng(33)
+    n_nodes, ppn = 96, 4
+    nodes = [W.node_object(f"node-{i}") for i in range(n_nodes)]
+    pods = [W.pod_object(f"pod-{i}", f"node-{i // ppn}", job=(i % 10 == 0)) for i in range(n_nodes * ppn)]
+    node_ptr = np.arange(0, n_nodes * ppn + 1, ppn, dtype=np.uint32)
+    leases = c3_leases(n_nodes, NOW0, rng)
+    me = 1
+    nprog, neng, nsim = build(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), nodes, kind_salt=1, wide_state=wide)
+    pprog, peng, psim = build(W.stage_paths(W.POD_FAST), pods, harness=True, wide_state=wide)
+    try:
+        # initial readOnly: only nodes whose cached lease is ours are managed (and their pods)
+        init_held = [LR.held(L, me) for L in leases]
+        hot, dels = neng.read()
+        from kwok_amd.host import abi
+        for i in range(n_nodes):
+            if not init_held[i]:
+                hot["sched"][i] &= ~np.uint32(abi.F_MANAGED)
+                nsim.managed[i] = False
+        neng.upsert(np.arange(n_nodes), hot, dels, np.zeros(n_nodes, np.uint32),
+                    (hot["sched"] >> 16).astype(np.uint16))
+        phot, pdels = peng.read()
+        for i in range(len(pods)):
+            if not init_held[i // ppn]:
+                phot["sched"][i] &= ~np.uint32(abi.F_MANAGED)
+                psim.managed[i] = False
+        peng.upsert(np.arange(len(pods)), phot, pdels, np.zeros(len(pods), np.uint32),
+                    (phot["sched"] >> 16).astype(np.uint16))
+        neng.lease_config(me, 40, 10 * 10**9, 0.04)
+        neng.lease_set(to_array(leases))
+        lsim = LR.LeaseSim(leases, me, 40, 10 * 10**9, 0.04, kind_salt=1)
+        seed = 0x77
+        for k in range(200):
+            now = NOW0 + k * 250 * 10**6
+            neng.lease_step(now, seed, k)
+            ops = lsim.step(now, seed, k)
+            assert sorted((int(r["slot"]), int(r["stage"])) for r in neng.lease_ops()) == sorted(ops), f"step {k}"
+            assert_leases_equal(neng.lease_read(), lsim.leases, k)
+            for i, op in ops:
+                h = LR.held(lsim.leases[i], me)
+                nsim.set_managed(i, h, op != LR.OP_BUSY)
+                for p in range(node_ptr[i], node_ptr[i + 1]):
+                    psim.set_managed(p, h, op != LR.OP_BUSY)
+            neng.lease_sync_pods(peng, node_ptr)
+            for eng, sim, prog in ((neng, nsim, nprog), (peng, psim, pprog)):
+                eng.step(now, seed, k)
+                got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
+                assert got == sorted(sim.step(now, seed, k)), f"step {k}"
+                compare_state(prog, eng, sim, k)
+                hot, _ = eng.read()
+                assert [bool(x & abi.F_MANAGED) for x in hot["sched"]] == sim.managed, f"step {k}: managed"
+        st = neng.lease_stats()
+        assert st["creates"] > 0 and st["renews"] > 0 and st["acquires"] > 0 and st["busy"] > 0, st
+    finally:
+        neng.close()
+        peng.close()
