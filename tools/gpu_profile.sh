@@ -11,4 +11,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 6 --warmup 4 > $O/pmc_fetch.log 2>&1 || { tail -20 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --steps 6 --warmup 4 > $O/pmc_write.log 2>&1 || { tail -20 $O/pmc_write.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d $O/pmc_sq -o run -- python3 $R/bench.py --no-cpu-baseline --steps 6 --warmup 4 > $O/pmc_sq.log 2>&1 || { tail -20 $O/pmc_sq.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_idle -o run -- python3 $R/bench.py --no-cpu-baseline --no-harness --steps 6 --warmup 4 > $O/pmc_fetch_idle.log 2>&1 || { tail -20 $O/pmc_fetch_idle.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_idle -o run -- python3 $R/bench.py --no-cpu-baseline --no-harness --steps 6 --warmup 4 > $O/pmc_write_idle.log 2>&1 || { tail -20 $O/pmc_write_idle.log; exit 1; }
 echo profile done
