@@ -29,6 +29,10 @@
 #ifndef KWOK_EXP_NOFIRED
 #define KWOK_EXP_NOFIRED 0
 #endif
+// phase-2 state write-back with nontemporal stores (experiment)
+#ifndef KWOK_NT_STORE
+#define KWOK_NT_STORE 0
+#endif
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -484,6 +488,15 @@ __device__ __forceinline__ int64_t buf_load_i64(__amdgpu_buffer_rsrc_t r, uint32
   return (int64_t)(((uint64_t)t[1] << 32) | t[0]);
 }
 
+__device__ __forceinline__ void store_word(uint32_t* p, uint32_t w) {
+  if (KWOK_NT_STORE) __builtin_nontemporal_store(w, p);
+  else *p = w;
+}
+__device__ __forceinline__ void store_word(uint2* p, uint2 w) {
+  if (KWOK_NT_STORE) __builtin_nontemporal_store(((uint64_t)w.y << 32) | w.x, reinterpret_cast<uint64_t*>(p));
+  else *p = w;
+}
+
 __device__ __forceinline__ uint32_t fw_of(uint2 w) { return w.y; }      // word holding flags + stage
 __device__ __forceinline__ uint32_t pw_of(uint2 w) { return w.x; }      // word holding pred
 __device__ __forceinline__ uint32_t fw_of(uint32_t w) { return w; }
@@ -619,7 +632,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (j < kStash) wr[j] = stash_of(out, 0);  // written back in phase 3 with its group
       else
 #endif
-      if (!KWOK_EXP_NOWRITE) stw[i] = out;
+      if (!KWOK_EXP_NOWRITE) store_word(&stw[i], out);
     }
     n_bytes += f.bytes;
     emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);

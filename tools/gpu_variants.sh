@@ -11,10 +11,7 @@ run() {  # name, env assignments...   (BARGS: extra bench args)
   python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'))"
 }
 run narrow_k16 KWOK_SWEEP_OBJS=16
-run narrow_k8 KWOK_SWEEP_OBJS=8
-run narrow_k16_tiles KWOK_SWEEP_OBJS=16 KWOK_SWEEP_GRID=tiles
-run narrow_k8_tiles KWOK_SWEEP_OBJS=8 KWOK_SWEEP_GRID=tiles
-run wide_k16 KWOK_SWEEP_OBJS=16 KWOK_BENCH_WIDE=1
-run wide_k8 KWOK_SWEEP_OBJS=8 KWOK_BENCH_WIDE=1
-BARGS=--no-harness run idle_narrow_k16 KWOK_SWEEP_OBJS=16
-BARGS=--no-harness run idle_narrow_k8 KWOK_SWEEP_OBJS=8
+for lib in kwok_amd/lib/variants/*.so; do
+  [ -e "$lib" ] && run $(basename $lib .so) KWOK_SWEEP_OBJS=16 KWOK_ENGINE_LIB=$R/$lib
+done
+run narrow_k16_again KWOK_SWEEP_OBJS=16
