@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--nodes", type=int, default=1_000_000, help="nodes per GPU (weak) or in total (strong)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C5",
+                    help="BASELINE.json configuration; C5 is the headline line, C1-C4 run on one GPU")
     ap.add_argument("--pods-per-node", type=int, default=100)
     ap.add_argument("--job-frac", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=0x6B776F6B)
@@ -159,6 +161,20 @@ def main():
     ap.add_argument("--wide-state", action="store_true", default=os.environ.get("KWOK_BENCH_WIDE") == "1",
                     help="diagnostic: force the 8-byte device state format")
     args = ap.parse_args()
+
+    if args.config != "C5":
+        from kwok_amd import build as kbuild
+        from kwok_amd import configs
+        if not os.path.exists(kbuild.OUT):
+            kbuild.build()
+        r = configs.run(args.config, args.steps, args.warmup, args.seed)
+        line = {"metric": r.pop("metric"), "value": round(r.pop("value"), 1), "n_gpus": 1, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(r.pop("ms_per_step"), 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u32/i64" if args.config != "C4" else "f64",
+                "data": "synthetic (seeded kwokctl-shaped objects), cache-resident working set",
+                "config": {"workload": r.pop("workload")}, "detail": r}
+        print(json.dumps(line), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
