@@ -257,12 +257,13 @@ def main():
         achieved = (pbytes / args.steps) / pod_kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
+                "traffic_GBps": (round(_pmc_traffic() / pod_kernel_s / 1e9, 1) if _pmc_traffic() else None),
                 "kernel": "sweep_kernel (pods)", "bytes_per_launch": int(pbytes / args.steps),
                 "state_bytes_per_object": int(s1p["state_bytes"]),
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2)}
         cpu = None
         log(f"timed {args.steps} steps in {max_s:.3f} s; cpu baseline next")
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             cpu = cpu_baseline(args.cpu_sample_s, args.seed)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
