@@ -510,7 +510,7 @@ __device__ __forceinline__ uint4 stash_of(uint32_t w, int64_t d) {
 __device__ __forceinline__ void unstash(const uint4& r, uint2& w) { w = make_uint2(r.x, r.y); }
 __device__ __forceinline__ void unstash(const uint4& r, uint32_t& w) { w = r.x; }
 
-template <bool kHarness, int K, bool kNarrow>
+template <bool kHarness, int K, bool kNarrow, bool kPersist>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
   typedef typename StateWord<kNarrow>::T W;
   constexpr uint32_t kWordBytes = sizeof(W);
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   // Persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ... so the per-block
   // set-up (stage deltas into LDS, statistics) is paid once per CU slot, not once per tile.
   const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kBlock * K - 1) / (kBlock * K));
-  for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  auto tile_body = [&](const uint32_t tile) {
   const uint32_t ibase = tile * (uint32_t)(kBlock * K) + wave * 64 + lane;
   const uint64_t base = ibase;
   const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;  // fired segment of (tile, wave)
@@ -668,7 +668,12 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   wave_bytes += 4u;  // the fired count word
   // the next tile reuses this wave's LDS lists: keep its phase-1 writes after these reads
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }  // tile loop
+  };  // tile_body
+  if constexpr (kPersist) {
+    for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) tile_body(tile);
+  } else if (blockIdx.x < n_tiles) {  // one block per tile: straight-line code, shorter live ranges
+    tile_body(blockIdx.x);
+  }
 
   // ---- block statistics
   for (int off = 32; off > 0; off >>= 1) {
@@ -1382,15 +1387,15 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
 // sweep grid: one block per tile (default), or KWOK_SWEEP_GRID=persist: every CU slot the
 // occupancy allows, each block walking tiles (faster on idle sweeps, slower with churn on
 // MI355X, profiles/r1/README.md)
-extern "C++" template <bool H, int K, bool N>
+extern "C++" template <bool H, int K, bool N, bool P>
 static uint32_t sweep_grid(kwk_engine* e, uint32_t tiles) {
   static int per_cu = 0;
   if (per_cu == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<H, K, N>, kBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<H, K, N, P>, kBlock, 0) != hipSuccess ||
         per_cu <= 0)
       per_cu = 1;
   }
-  if (e->grid_per_tile) return tiles;
+  if (!P) return tiles;
   const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
   return tiles < g ? tiles : g;
 }
@@ -1435,7 +1440,13 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
   const bool h = a.harness.enable != 0;
 #define LAUNCH(HV, KV, NV) \
-  hipLaunchKernelGGL((sweep_kernel<HV, KV, NV>), dim3(sweep_grid<HV, KV, NV>(e, blocks)), dim3(kBlock), 0, e->stream, a)
+  do {                                                                                                           \
+    if (e->grid_per_tile)                                                                                       \
+      hipLaunchKernelGGL((sweep_kernel<HV, KV, NV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);      \
+    else                                                                                                         \
+      hipLaunchKernelGGL((sweep_kernel<HV, KV, NV, true>), dim3(sweep_grid<HV, KV, NV, true>(e, blocks)),      \
+                         dim3(kBlock), 0, e->stream, a);                                                         \
+  } while (0)
   if (!nar) {
     if (K == 8) { if (h) LAUNCH(true, 8, false); else LAUNCH(false, 8, false); }
     else { if (h) LAUNCH(true, 16, false); else LAUNCH(false, 16, false); }

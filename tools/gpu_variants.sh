@@ -11,7 +11,12 @@ run() {  # name, env assignments...   (BARGS: extra bench args)
   python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'))"
 }
 run narrow_k16 KWOK_SWEEP_OBJS=16
+run narrow_k8 KWOK_SWEEP_OBJS=8
+run narrow_k16_persist KWOK_SWEEP_OBJS=16 KWOK_SWEEP_GRID=persist
+run wide_k16 KWOK_SWEEP_OBJS=16 KWOK_BENCH_WIDE=1
 for lib in kwok_amd/lib/variants/*.so; do
   [ -e "$lib" ] && run $(basename $lib .so) KWOK_SWEEP_OBJS=16 KWOK_ENGINE_LIB=$R/$lib
 done
+BARGS=--no-harness run idle_narrow_k16 KWOK_SWEEP_OBJS=16
+BARGS=--no-harness run idle_narrow_k16_persist KWOK_SWEEP_OBJS=16 KWOK_SWEEP_GRID=persist
 run narrow_k16_again KWOK_SWEEP_OBJS=16
