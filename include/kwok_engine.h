@@ -234,6 +234,11 @@ kwk_status kwk_usage_config(kwk_engine* eng, uint32_t n_nodes, const uint32_t* n
 kwk_status kwk_usage(kwk_engine* eng, int64_t now_ns);
 /* node_out: n_nodes x {cpu, mem, cpu_cumulative, mem_cumulative}; cluster_out: {cpu, mem} */
 kwk_status kwk_usage_read(kwk_engine* eng, double* node_out, double* cluster_out);
+/* per-pod outputs of kwk_usage (podResourceUsage / podResourceCumulativeUsage,
+ * metrics_resource_usage.go:36-65,170-193): enable allocates 56 bytes per slot */
+kwk_status kwk_usage_pods(kwk_engine* eng, uint32_t enable);
+/* pod_out: n x {cpu, mem, cpu_cumulative, mem_cumulative} for slots [first, first+n) */
+kwk_status kwk_usage_read_pods(kwk_engine* eng, uint32_t first, uint32_t n, double* pod_out);
 
 /* ------------------------------------------------------------------ node leases */
 /* NodeLeaseController (pkg/kwok/controllers/node_lease_controller.go) on a NODE engine: one

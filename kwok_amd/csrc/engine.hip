@@ -761,6 +761,10 @@ __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uin
 // cpu / memory value from the interned dictionaries, multiply by its container count and
 // reduce with shuffles.  Dead pods (not in the pod cache) contribute nothing.
 // server/metrics_resource_usage.go:170-224 (sums), :36-109 (cumulative integrators).
+// With per-pod outputs enabled (kwk_usage_pods) every pod also gets its Usage (podResourceUsage,
+// :170-193) and its cumulative usage (podResourceCumulativeUsage, :54-65: the sum of its
+// containers' integrators, each advanced by (now - last) * value, :36-52); a dead pod reads 0
+// and keeps its integrators (Go keys them by name, so a re-created pod continues them).
 __global__ __launch_bounds__(kBlock) void usage_kernel(const void* __restrict__ st, StateFmt fmt,
                                                        const uint32_t* __restrict__ node_ptr,
                                                        const uint32_t* __restrict__ ukey,
@@ -768,7 +772,8 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const void* __restrict__ 
                                                        const double* __restrict__ mem_v, uint32_t n_nodes,
                                                        double* __restrict__ node_out, double* __restrict__ cum,
                                                        int64_t* __restrict__ last_t, int64_t now,
-                                                       double* __restrict__ block_part) {
+                                                       double* __restrict__ block_part, double* __restrict__ pod_out,
+                                                       double* __restrict__ pod_cum, int64_t* __restrict__ pod_last) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t node = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   double c = 0.0, m = 0.0;
@@ -776,11 +781,29 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(const void* __restrict__ 
     const uint32_t lo = node_ptr[node], hi = node_ptr[node + 1];
     for (uint32_t p = lo + lane; p < hi; p += 64) {
       const uint32_t sched = load_state(st, p, fmt).y;
-      if (!(sched & KWK_F_ALIVE)) continue;
+      if (!(sched & KWK_F_ALIVE)) {
+        if (pod_out) reinterpret_cast<double4*>(pod_out)[p] = make_double4(0.0, 0.0, 0.0, 0.0);
+        continue;
+      }
       const uint32_t k = ukey[p];
       const double nc = (double)(k >> 28);
-      c += nc * cpu_v[k & 0x3FFFu];
-      m += nc * mem_v[(k >> 14) & 0x3FFFu];
+      const double pc = nc * cpu_v[k & 0x3FFFu];
+      const double pm = nc * mem_v[(k >> 14) & 0x3FFFu];
+      c += pc;
+      m += pm;
+      if (pod_out) {
+        double2 pcum = reinterpret_cast<double2*>(pod_cum)[p];
+        const int64_t lt = pod_last[p];
+        if (lt != INT64_MIN) {
+          const int64_t d = now - lt;
+          const double dt = (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
+          pcum.x += dt * pc;
+          pcum.y += dt * pm;
+          reinterpret_cast<double2*>(pod_cum)[p] = pcum;
+        }
+        pod_last[p] = now;
+        reinterpret_cast<double4*>(pod_out)[p] = make_double4(pc, pm, pcum.x, pcum.y);
+      }
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -1053,6 +1076,9 @@ struct kwk_engine {
   double* d_node_out = nullptr;
   double* d_node_cum = nullptr;
   int64_t* d_node_last = nullptr;
+  double* d_pod_out = nullptr;   // per pod {cpu, mem, cpu_cumulative, mem_cumulative} (kwk_usage_pods)
+  double* d_pod_cum = nullptr;
+  int64_t* d_pod_last = nullptr;
   double* d_usage_part = nullptr;
   double* d_cluster = nullptr;
 
@@ -1222,7 +1248,8 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
-                  e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_lease, e->d_lease_op, e->d_lease_ops,
+                  e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
+                  e->d_lease, e->d_lease_op, e->d_lease_ops,
                   e->d_lease_nops, e->d_lease_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
@@ -1583,10 +1610,41 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   const uint32_t ublocks = (e->n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->d_node_ptr, e->d_ukey,
                      e->d_cpu, e->d_mem, e->n_nodes, e->d_node_out, e->d_node_cum, e->d_node_last, now_ns,
-                     e->d_usage_part);
+                     e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(kBlock), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);
   HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_pods(kwk_engine* e, uint32_t enable) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  void* olds[] = {e->d_pod_out, e->d_pod_cum, e->d_pod_last};
+  for (void* p : olds) if (p) HIP_TRY(hipFree(p));
+  e->d_pod_out = nullptr;
+  e->d_pod_cum = nullptr;
+  e->d_pod_last = nullptr;
+  if (!enable) return KWK_OK;
+  const size_t n = e->capacity;
+  HIP_TRY(hipMalloc(&e->d_pod_out, 32 * n));
+  HIP_TRY(hipMalloc(&e->d_pod_cum, 16 * n));
+  HIP_TRY(hipMalloc(&e->d_pod_last, 8 * n));
+  HIP_TRY(hipMemset(e->d_pod_out, 0, 32 * n));
+  HIP_TRY(hipMemset(e->d_pod_cum, 0, 16 * n));
+  std::vector<int64_t> lasts(n, INT64_MIN);
+  HIP_TRY(hipMemcpy(e->d_pod_last, lasts.data(), 8 * n, hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_read_pods(kwk_engine* e, uint32_t first, uint32_t n, double* pod_out) {
+  if (!e || (n && !pod_out)) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
+  if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (n) HIP_TRY(hipMemcpy(pod_out, e->d_pod_out + 4 * (size_t)first, 32 * (size_t)n, hipMemcpyDeviceToHost));
   return KWK_OK;
 }
 

@@ -117,7 +117,8 @@ EXPORTS = [
     "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_match", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
-    "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods",
+    "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
+    "kwk_usage_read_pods",
 ]
 
 _lib = None
@@ -160,6 +161,8 @@ def lib():
                                    C.c_uint32, C.c_void_p]
     L.kwk_usage.argtypes = [C.c_void_p, C.c_int64]
     L.kwk_usage_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kwk_usage_pods.argtypes = [C.c_void_p, C.c_uint32]
+    L.kwk_usage_read_pods.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_device_ptrs.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_event_record.argtypes = [C.c_void_p, C.c_uint32]
     L.kwk_event_elapsed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, _p(C.c_float)]

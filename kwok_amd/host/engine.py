@@ -225,6 +225,16 @@ class Engine:
     def usage(self, now_ns: int):
         abi.check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")
 
+    def usage_pods(self, enable: bool = True):
+        abi.check(abi.lib().kwk_usage_pods(self.h, 1 if enable else 0), "kwk_usage_pods")
+
+    def usage_read_pods(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        """n x {cpu, mem, cpu_cumulative, mem_cumulative} per pod slot."""
+        n = self.n - first if n is None else n
+        out = np.zeros((n, 4), dtype=np.float64)
+        abi.check(abi.lib().kwk_usage_read_pods(self.h, first, n, abi.ptr(out)), "kwk_usage_read_pods")
+        return out
+
     def usage_read(self):
         node = np.zeros((self.n_nodes, 4), dtype=np.float64)
         cl = np.zeros(2, dtype=np.float64)

@@ -96,3 +96,35 @@ def seconds(d_ns: int) -> float:
     """time.Duration.Seconds()"""
     sec, nsec = int(d_ns / 10**9), d_ns - int(d_ns / 10**9) * 10**9
     return float(sec) + float(nsec) / 1e9
+
+
+def pod_usage(docs, pod, resource):
+    """podResourceUsage (metrics_resource_usage.go:170-193): the sum over the pod's containers."""
+    return node_usage(docs, [pod], resource)
+
+
+class Cumulative:
+    """The cumulative-usage integrators of metrics_resource_usage.go:36-109, keyed like the
+    reference's (one per container x resource, one per node): each evaluation adds
+    seconds(now - last) * value to the key's total and moves last to now; the first
+    evaluation of a key only records the time."""
+
+    def __init__(self):
+        self.total = {}
+        self.last = {}
+
+    def advance(self, key, value, now_ns):
+        t = self.total.get(key, 0.0)
+        if key in self.last:
+            t += seconds(now_ns - self.last[key]) * value
+        self.total[key], self.last[key] = t, now_ns
+        return t
+
+    def pod(self, docs, pod, resource, now_ns):
+        """podResourceCumulativeUsage (:54-65): the pod's containers' integrators, summed."""
+        s = 0.0
+        name = (pod.get("metadata") or {}).get("name", "")
+        for c in (pod.get("spec") or {}).get("containers") or []:
+            cn = c.get("name", "")
+            s += self.advance((name, cn, resource), container_usage(docs, pod, cn, resource), now_ns)
+        return s

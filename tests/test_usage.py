@@ -115,3 +115,65 @@ def test_gpu_node_usage_and_cumulative():
                                    rtol=REL_TOL, atol=0)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pod_usage_and_cumulative():
+    """Per-pod Usage / CumulativeUsage (the pod and container series of metrics-resource.yaml)
+    against the oracle's per-container integrators, across deletions and re-creation."""
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+
+    cl, pods = _cluster(n_nodes=12, n_pods=300, seed=5)
+    prog = _program()
+    keys, cv, mv = usage_columns(prog, pods)
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    cols = ing.columns(pods)
+    eng = Engine(kp, capacity=len(pods))
+    try:
+        eng.load_stages()
+        eng.load(*cols, ing.record_array())
+        eng.usage_config(cl.node_ptr, keys, cv, mv)
+        eng.usage_pods(True)
+        docs = _docs()
+        cum = usage_ref.Cumulative()
+        alive = np.ones(len(pods), dtype=bool)
+        gone = np.arange(0, len(pods), 5)
+        t = 1_700_000_000 * 10**9
+        for k in range(6):
+            if k == 2:
+                eng.delete(gone)
+                alive[gone] = False
+            if k == 4:  # re-created under the same names: the integrators continue
+                hot, dels, rec, cls = cols
+                eng.upsert(gone, hot[gone], dels[gone], rec[gone], cls[gone])
+                alive[gone] = True
+            eng.usage(t)
+            got = eng.usage_read_pods()
+            want = np.zeros((len(pods), 4))
+            for i, p in enumerate(pods):
+                if alive[i]:
+                    want[i] = (usage_ref.pod_usage(docs, p, "cpu"), usage_ref.pod_usage(docs, p, "memory"),
+                               cum.pod(docs, p, "cpu", t), cum.pod(docs, p, "memory", t))
+            np.testing.assert_allclose(got, want, rtol=REL_TOL, atol=1e-9, err_msg=f"evaluation {k}")
+            t += 1_000_000_000 + 37_000_001 * k
+        assert np.any(got[:, 2] > 0) and np.any(got[:, 3] > 0)
+    finally:
+        eng.close()
+
+
+def test_oracle_cumulative_integrator():
+    """The first evaluation of a key records the time only; later ones add seconds(dt) * value
+    (metrics_resource_usage.go:36-52); pods sum their containers' integrators."""
+    c = usage_ref.Cumulative()
+    assert c.advance("k", 3.0, 10**9) == 0.0
+    assert c.advance("k", 3.0, 3_500_000_000) == pytest.approx(7.5)
+    assert c.advance("k", 1.0, 4_500_000_000) == pytest.approx(8.5)
+    docs = _docs()
+    _, pods = _cluster(n_nodes=2, n_pods=20, seed=3)
+    p = max(pods, key=lambda q: len(q["spec"]["containers"]))
+    assert c.pod(docs, p, "cpu", 0) == 0.0
+    assert c.pod(docs, p, "cpu", 2 * 10**9) == pytest.approx(2 * usage_ref.pod_usage(docs, p, "cpu"))
