@@ -207,10 +207,12 @@ struct SweepArgs {
   const kwk_value* __restrict__ values;
   const kwk_stage_table* __restrict__ table;
   const kwk_delta* __restrict__ deltas;
+  const uint32_t* __restrict__ lut;  // pred -> matched-stage mask, lut_n entries (0: no table)
   kwk_fired_rec* __restrict__ fired;
   uint32_t* __restrict__ wave_counts;
   unsigned long long* __restrict__ cum;  // [n_blocks][kStatWords]
   uint32_t n;
+  uint32_t lut_n;
   uint32_t value_slots;
   uint64_t slot_base;
   uint64_t key;
@@ -222,7 +224,7 @@ struct SweepArgs {
   kwk_harness harness;
 };
 
-__device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
+__host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
   bool ok = ((pred ^ s.eq_val) & s.eq_mask) == 0;
   for (uint32_t k = 0; k < s.n_any; ++k) ok &= ((pred & s.any_mask[k]) != 0) == (((s.any_want >> k) & 1u) != 0);
   return ok;
@@ -251,9 +253,13 @@ struct Fire {      // what one object's step produced
 // Updates sched (pending stage / MATCHERR) and due; returns true if a stage was scheduled.
 __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                              uint32_t n_stages, uint64_t i, uint32_t pred, uint32_t& sched,
-                                             int64_t& due, uint32_t& bytes) {
+                                             int64_t& due, uint32_t& bytes, const uint32_t* lut, uint32_t lut_n) {
   uint32_t m = 0;
-  for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+  if (pred < lut_n) {
+    m = lut[pred];
+  } else {
+    for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+  }
   sched &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
   if (m == 0) return false;  // no match: a queued job stays queued (pod_controller.go:222-229)
   const kwk_value* __restrict__ rec = nullptr;
@@ -385,7 +391,8 @@ template <bool kHarness, uint32_t kWordBytes>
 __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
-                                               int64_t due, Fire& f, uint32_t& n_matched) {
+                                               int64_t due, Fire& f, uint32_t& n_matched, const uint32_t* lut,
+                                               uint32_t lut_n) {
   if (kHarness) {
     if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
       pred &= a.harness.keep_mask;  // same spec: class bits and record flag stay
@@ -408,7 +415,7 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
   bool scheduled = false;
   if (sched & KWK_F_ALIVE) {
     if (sched & KWK_F_DIRTY) {
-      scheduled = match_object(a, T, n_stages, i, pred, sched, due, f.bytes);
+      scheduled = match_object(a, T, n_stages, i, pred, sched, due, f.bytes, lut, lut_n);
       n_matched += scheduled ? 1 : 0;
     }
     const uint32_t st = sched & 0xFFu;
@@ -462,6 +469,18 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
 #ifndef KWOK_GROUP
 #define KWOK_GROUP 0
 #endif
+#ifndef KWOK_VEC
+#define KWOK_VEC 1
+#endif
+// slot of a lane's k-th word relative to its wave's first slot.  V = 1: row k of the tile is
+// kBlock consecutive words, 64 per wave (one 4-byte load per word); V = 4: each lane holds 4
+// consecutive words per 16-byte load, a wave covers 256 consecutive words per load
+template <int V>
+__device__ __forceinline__ uint32_t rel_slot(uint32_t k, uint32_t lane) {
+  if constexpr (V == 1) return k * kBlock + lane;
+  else return (k / 4) * (kBlock * 4) + lane * 4 + (k % 4);
+}
+constexpr uint32_t kLutMax = 256;  // pred -> match-mask table for programs with pred_bits <= 8
 constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
 #ifndef KWOK_STASH
 #define KWOK_STASH 192
@@ -514,31 +533,69 @@ template <bool kHarness, int K, bool kNarrow, bool kPersist>
 __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
   typedef typename StateWord<kNarrow>::T W;
   constexpr uint32_t kWordBytes = sizeof(W);
+  constexpr int V = kNarrow ? KWOK_VEC : 1;  // consecutive words per lane per load
+  static_assert(V == 1 || (V == 4 && K % 4 == 0 && !KWOK_GROUP), "KWOK_VEC: 1, or 4 with K % 4 == 0");
   __shared__ unsigned int s_stat[kStatWords];
   __shared__ kwk_delta s_delta[kLdsDeltas];
   __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
   __shared__ uint4 s_rec[kWavesPerBlock][kStash];
+  __shared__ uint32_t s_lut[kLutMax];
+  __shared__ kwk_stage_table s_tab;
 #if KWOK_GROUP
   __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
 #endif
-  const kwk_stage_table* __restrict__ T = a.table;
-  const uint32_t n_stages = T->n_stages;
-  const uint32_t fin_group = T->fin_group_mask;
-  const uint32_t n_deltas = T->n_classes * n_stages;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kBlock * K - 1) / (kBlock * K));
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n * kWordBytes);
+  // The state stream of the block's first tile is issued before the LDS set-up below, so its
+  // HBM latency overlaps the table / LUT / delta copies and the barrier; in the persistent
+  // grid the next tile's words are issued as soon as phase 1 of the current one is done
+  // (register double-buffering: the words are dead during phase 2).
+  W v[K];
+  auto issue_tile = [&](const uint32_t tile) {
+    const uint32_t wb = tile * (uint32_t)(kBlock * K) + wave * 64 * V;
+    if constexpr (V == 4) {
+      if ((uint64_t)(tile + 1) * (kBlock * K) <= a.n) {  // one 16-byte load per 4 words
+#pragma unroll
+        for (int q = 0; q < K / 4; ++q) {
+          const auto t = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wb + (uint32_t)q * kBlock * 4 + lane * 4) * 4u, 0, 0);
+          v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) buf_load(v[k], st_rs, (wb + rel_slot<V>(k, lane)) * kWordBytes);
+  };
+  if (blockIdx.x < n_tiles) issue_tile(blockIdx.x);
+  // Phase 2 reads the stage table per lane with divergent indices: staged in LDS they are
+  // ds_reads instead of global loads (header + the loaded stages only).  For programs with
+  // pred_bits <= 8 the match set is one LDS lookup (table built by kwk_load_stages).
+  {
+    const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&s_tab);
+    for (uint32_t j = threadIdx.x; j < nw; j += kBlock) dst[j] = src[j];
+  }
+  const kwk_stage_table* __restrict__ T = &s_tab;
+  const uint32_t n_stages = a.table->n_stages;
+  const uint32_t fin_group = a.table->fin_group_mask;
+  const uint32_t n_deltas = a.table->n_classes * n_stages;
+  const uint32_t lut_n = a.lut_n;
+  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
+  const uint32_t* lut = s_lut;
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   const kwk_delta* __restrict__ deltas = a.deltas;
   if (n_deltas <= kLdsDeltas) {
     for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
     deltas = s_delta;
   }
-  __syncthreads();  // s_stat / s_delta initialised
+  __syncthreads();  // s_stat / s_delta / s_tab / s_lut initialised
 
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = threadIdx.x >> 6;
   W* __restrict__ stw = reinterpret_cast<W*>(a.st);
   const StateFmt fmt = a.fmt;
   const RawTest R = a.raw;
-  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n * kWordBytes);
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ wr = s_rec[wave];
@@ -550,10 +607,9 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
 
   // Persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ... so the per-block
   // set-up (stage deltas into LDS, statistics) is paid once per CU slot, not once per tile.
-  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kBlock * K - 1) / (kBlock * K));
   auto tile_body = [&](const uint32_t tile) {
-  const uint32_t ibase = tile * (uint32_t)(kBlock * K) + wave * 64 + lane;
-  const uint64_t base = ibase;
+  const uint32_t wbase = tile * (uint32_t)(kBlock * K) + wave * 64 * V;  // the wave's first slot
+  const uint64_t base = wbase + lane;
   const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;  // fired segment of (tile, wave)
   kwk_fired_rec* __restrict__ seg = a.fired + seg_id * (64 * K);
   const bool full = (uint64_t)(tile + 1) * (kBlock * K) <= a.n;
@@ -564,9 +620,6 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
 #endif
   uint32_t n_work = 0;  // wave-uniform
-  W v[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) buf_load(v[k], st_rs, (ibase + (uint32_t)k * kBlock) * kWordBytes);
   int64_t d[K];  // due times, loaded only where a stage is pending (else an out-of-range 0)
   uint32_t pend_bits = 0;
 #pragma unroll
@@ -574,19 +627,24 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     const uint32_t fw = fw_of(v[k]);
     const bool pend = (fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code;
     pend_bits |= (pend ? 1u : 0u) << k;
-    d[k] = buf_load_i64(due_rs, pend ? (ibase + (uint32_t)k * kBlock) * 8u : kOOB);
+    d[k] = buf_load_i64(due_rs, pend ? (wbase + rel_slot<V>(k, lane)) * 8u : kOOB);
   }
   {  // streamed words of this lane + its due reads
-    const uint32_t in_k = full ? (uint32_t)K : (ibase >= a.n ? 0u : min((uint32_t)K, (a.n - ibase + kBlock - 1) / kBlock));
+    uint32_t in_k = K;
+    if (!full) {
+      in_k = 0;
+      for (int k = 0; k < K; ++k) in_k += (wbase + rel_slot<V>(k, lane) < a.n) ? 1u : 0u;
+    }
     n_bytes += kWordBytes * in_k + 8u * (uint32_t)__popc(pend_bits);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t fw = fw_of(v[k]);
     const uint32_t pw = pw_of(v[k]);
-    bool need = (fw & R.dirty) || (((pend_bits >> k) & 1u) && d[k] <= a.now);
-    if (kHarness) need = need || !(fw & R.alive) || ((pw & R.term) && !(pw & R.del));
-    need = need && (fw & R.managed);
+    // straight bit arithmetic, no short-circuit branches
+    uint32_t nb = (fw & R.dirty) | (((pend_bits >> k) & 1u) & (uint32_t)(d[k] <= a.now));
+    if (kHarness) nb |= (~fw & R.alive) | ((uint32_t)((pw & R.term) != 0) & (uint32_t)((pw & R.del) == 0));
+    const bool need = (nb != 0) & ((fw & R.managed) != 0);
     const unsigned long long bal = __ballot(need);
     if (need) {
       const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
@@ -601,17 +659,22 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
 #endif
     n_work += (uint32_t)__popcll(bal);
   }
+#if !KWOK_GROUP
+  if constexpr (kPersist) {  // prefetch the next tile's words (phase 3 of KWOK_GROUP still reads v)
+    if (tile + gridDim.x < n_tiles) issue_tile(tile + gridDim.x);
+  }
+#endif
   // ---- phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup
   // barrier) orders the cross-lane LDS hand-off.
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const uint64_t wave_base = (uint64_t)tile * (kBlock * K) + wave * 64;
+  const uint64_t wave_base = wbase;
   for (uint32_t c = 0; c < n_work; c += 64) {
     const uint32_t j = c + lane;
     Fire f{false, 0, 0, 0};
     uint64_t i = 0;
     if (j < n_work) {
       const uint32_t w = wl[j];
-      i = wave_base + (uint64_t)(w >> 6) * kBlock + (w & 63u);
+      i = wave_base + rel_slot<V>(w >> 6, w & 63u);
       W raw;
       int64_t due;
       if (j < kStash) {
@@ -625,7 +688,7 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       }
       const uint2 s = sw_decode(raw, fmt);
       const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                            n_matched);
+                                                            n_matched, lut, lut_n);
       W out;
       sw_encode(out, nv, fmt);
 #if KWOK_GROUP
@@ -660,6 +723,9 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
       if (write) stw[i] = val;
     }
   }
+  if constexpr (kPersist) {
+    if (tile + gridDim.x < n_tiles) issue_tile(tile + gridDim.x);
+  }
 #endif
 
   // per-(tile, wave) fired count, read by kwk_fired's scan
@@ -688,7 +754,8 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   __syncthreads();
   if (threadIdx.x < 3 + n_stages) {
     const unsigned int val = s_stat[threadIdx.x];
-    if (val) a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x] += val;
+    // no-return atomic: the block does not wait for a read-modify-write round trip
+    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
   }
 }
 
@@ -1056,6 +1123,8 @@ struct kwk_engine {
   uint32_t* d_rec = nullptr;
   kwk_value* d_values = nullptr;
   kwk_stage_table* d_table = nullptr;
+  uint32_t* d_lut = nullptr;  // kLutMax match masks (valid for lut_n entries)
+  uint32_t lut_n = 0;
   kwk_delta* d_deltas = nullptr;
   kwk_fired_rec* d_fired = nullptr;
   kwk_fired_rec* d_compact = nullptr;
@@ -1217,6 +1286,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
   ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
   ALLOC(e->d_table, sizeof(kwk_stage_table));
+  ALLOC(e->d_lut, sizeof(uint32_t) * kLutMax);
   ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
                                               (size_t)kBlock * kMaxObjPerThread));
   ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
@@ -1245,7 +1315,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (!e) return KWK_OK;
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -1290,6 +1360,14 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
     e->fmt = nf;
   }
   HIP_TRY(hipMemcpy(e->d_table, t, sizeof(kwk_stage_table), hipMemcpyHostToDevice));
+  // the match set of every pred value, when pred_bits is small (Lifecycle.match, lifecycle.go:51-63)
+  e->lut_n = (t->pred_bits != 0 && t->pred_bits <= 8) ? (1u << t->pred_bits) : 0u;
+  if (e->lut_n) {
+    std::vector<uint32_t> lut(e->lut_n, 0u);
+    for (uint32_t p = 0; p < e->lut_n; ++p)
+      for (uint32_t s = 0; s < t->n_stages; ++s) lut[p] |= (stage_matches(t->stages[s], p) ? 1u : 0u) << s;
+    HIP_TRY(hipMemcpy(e->d_lut, lut.data(), sizeof(uint32_t) * e->lut_n, hipMemcpyHostToDevice));
+  }
   if (e->d_deltas) HIP_TRY(hipFree(e->d_deltas));
   e->d_deltas = nullptr;
   const size_t nd = (size_t)(t->n_classes ? t->n_classes : 1) * (t->n_stages ? t->n_stages : 1);
@@ -1439,6 +1517,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   a.values = e->d_values;
   a.table = e->d_table;
   a.deltas = e->d_deltas;
+  a.lut = e->d_lut;
+  a.lut_n = e->lut_n;
   a.fired = e->d_fired;
   a.wave_counts = e->d_wave_counts;
   a.cum = e->d_cum;
