@@ -255,11 +255,13 @@ def main():
         value = total_fired / max_s
         pod_kernel_s = pod_ms / 1e3 / args.steps
         achieved = (pbytes / args.steps) / pod_kernel_s / 1e9
+        sb = int(s1p["state_bytes"])
+        traffic = _pmc_traffic(sb)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
-                "traffic_GBps": (round(_pmc_traffic() / pod_kernel_s / 1e9, 1) if _pmc_traffic() else None),
-                "kernel": "sweep_kernel (pods)", "bytes_per_launch": int(pbytes / args.steps),
-                "state_bytes_per_object": int(s1p["state_bytes"]),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_GBps": (round(traffic / pod_kernel_s / 1e9, 1) if traffic else None),
+                "kernel": ("sweep16_kernel" if sb == 2 else "sweep_kernel") + " (pods)",
+                "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2)}
         cpu = None
         log(f"timed {args.steps} steps in {max_s:.3f} s; cpu baseline next")
@@ -268,7 +270,8 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_s / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u32/i64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+            "dtype": {2: "u16", 4: "u32", 8: "u32x2"}[sb] + "/i64",
             "data": "synthetic (seeded kwokctl-shaped pods/nodes; pod-fast + node-fast/heartbeat stages)",
             "config": {"workload": f"C5: {args.nodes:,} nodes / {args.nodes * args.pods_per_node:,} pods "
                                    f"{'per GPU' if args.scaling == 'weak' else 'in total'}, pod-fast + "
@@ -290,13 +293,18 @@ def main():
         dist.destroy_process_group()
 
 
-def _pmc_traffic():
-    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+def _pmc_traffic(state_bytes):
+    """HBM bytes per pod-sweep launch from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None when they were taken on
+    another state format (a different kernel)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(p)).get("hbm_bytes_per_launch")
+        d = json.load(open(p))
     except (OSError, ValueError):
         return None
+    if d.get("state_bytes_per_object") != state_bytes:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 if __name__ == "__main__":

@@ -172,7 +172,7 @@ typedef struct {
   uint64_t fired;         /* stage transitions */
   uint64_t bytes;         /* algorithmic bytes moved by the sweep */
   uint64_t fired_per_stage[KWK_MAX_STAGES];
-  uint64_t state_bytes;   /* bytes per object of the device state stream: 4 (narrow) or 8 (wide) */
+  uint64_t state_bytes;   /* bytes per object of the device state stream: 2 or 4 (packed) or 8 (wide) */
 } kwk_step_stats;
 
 /* ------------------------------------------------------------------ engine */
@@ -185,7 +185,8 @@ typedef struct {
   uint32_t kind_salt;         /* mixed into the RNG key: separate streams per kind */
   uint32_t flags;             /* KWK_ENGINE_* */
 } kwk_engine_desc;
-#define KWK_ENGINE_WIDE_STATE (1u << 0) /* always use the 8-byte state format (never the packed 4-byte one) */
+#define KWK_ENGINE_WIDE_STATE (1u << 0) /* always use the 8-byte state format (never a packed one) */
+#define KWK_ENGINE_STATE32 (1u << 1)    /* never the 2-byte packed format (4-byte packed or wide only) */
 
 const char* kwk_last_error(void);
 kwk_status kwk_engine_create(const kwk_engine_desc* desc, kwk_engine** out);

@@ -150,8 +150,10 @@ __device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool de
 // narrow : one u32 per slot when the program fits 32 bits:
 //          [pred: pred_bits][class: cbits][stage code: sbits][flags: 5]
 //          flags = sched bits 8..12 (ALIVE DIRTY MANAGED HASREC MATCHERR); stage code n_stages = none.
+// half   : the same packing in one u16 per slot when it fits 16 bits (narrow = half = 1).
 struct StateFmt {
   uint32_t narrow;
+  uint32_t half;
   uint32_t pmask;
   uint32_t cshift, cmask;
   uint32_t sshift, smask, none_code;
@@ -175,10 +177,12 @@ __host__ __device__ __forceinline__ uint32_t fmt_pack(uint32_t pred, uint32_t sc
 
 // small kernels (scatter / delete / usage / count) branch on the format at run time
 __device__ __forceinline__ uint2 load_state(const void* st, uint64_t i, const StateFmt& f) {
+  if (f.half) return fmt_unpack(reinterpret_cast<const uint16_t*>(st)[i], f);
   return f.narrow ? fmt_unpack(reinterpret_cast<const uint32_t*>(st)[i], f) : reinterpret_cast<const uint2*>(st)[i];
 }
 __device__ __forceinline__ void store_state(void* st, uint64_t i, uint2 v, const StateFmt& f) {
-  if (f.narrow) reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
+  if (f.half) reinterpret_cast<uint16_t*>(st)[i] = (uint16_t)fmt_pack(v.x, v.y, f);
+  else if (f.narrow) reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
   else reinterpret_cast<uint2*>(st)[i] = v;
 }
 
@@ -759,6 +763,229 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
   }
 }
 
+// ------------------------------------------------------------------ 2-byte state sweep
+// Sweep over the 2-byte packed format (StateFmt.half: every shipped pod-fast / node stage set
+// fits 16 bits).  At the steady-state churn of the C5 workload (~10 % of objects change per
+// step) nearly every 128-byte line of the state column holds a changed word, so writing the
+// changed words one by one costs a line fill plus a partial write per line once the line has
+// left L2 (profiles/r1/README.md).  This kernel instead keeps the tile on chip and rewrites
+// it as whole 128-byte lines:
+//  phase 1  each lane streams Q 16-byte chunks (8 words each) of its wave's region (row q of
+//           a wave = 1 KiB contiguous); due times only for lanes with a pending stage; the
+//           idle test on the raw words; objects needing work are ballot-compacted into the
+//           wave's LDS work list.  A wave with no work is done (no LDS, no stores);
+//  phase 2  the chunks go to the wave's LDS tile; the heavy path runs over the dense work
+//           list, reads and writes the word in LDS, emits fired records;
+//  phase 3  every lane re-reads its chunks; each aligned group of 8 lanes (one 128-byte line)
+//           with any changed word is stored whole from LDS (16 bytes per lane).
+// Words past n are never work; chunks past n hold what was loaded (0 past the buffer range),
+// so rewriting them is harmless inside the (tile-padded) allocation.
+#ifndef KWOK_Q16
+#define KWOK_Q16 2
+#endif
+
+#ifndef KWOK_WPE16
+#define KWOK_WPE16 6  // waves per SIMD the register allocation must allow (LDS allows 6 at Q = 2)
+#endif
+template <bool kHarness, int Q, bool kPersist>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
+  constexpr int K = 8 * Q;                 // words per lane
+  constexpr uint32_t kWave = 64u * K;      // words per wave region
+  constexpr uint32_t kTile = kBlock * K;   // words per block
+  __shared__ unsigned int s_stat[kStatWords];
+  __shared__ kwk_delta s_delta[kLdsDeltas];
+  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
+  __shared__ uint32_t s_lut[kLutMax];
+  __shared__ kwk_stage_table s_tab;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
+  // load range rounded to 16 bytes (the allocation is tile-padded): a chunk holding the last
+  // words comes back whole
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * 2u) + 15u) & ~15u);
+  uint4 v[Q];
+  auto issue_tile = [&](const uint32_t t) {
+    const uint32_t wb = t * kTile + wave * kWave;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wb + (uint32_t)q * 512u + lane * 8u) * 2u, 0, 0);
+      v[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  uint32_t tile = blockIdx.x;
+  if (tile < n_tiles) issue_tile(tile);
+  {  // LDS set-up overlaps the stream's latency (see sweep_kernel)
+    const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&s_tab);
+    for (uint32_t j = threadIdx.x; j < nw; j += kBlock) dst[j] = src[j];
+  }
+  const kwk_stage_table* __restrict__ T = &s_tab;
+  const uint32_t n_stages = a.table->n_stages;
+  const uint32_t fin_group = a.table->fin_group_mask;
+  const uint32_t n_deltas = a.table->n_classes * n_stages;
+  const uint32_t lut_n = a.lut_n;
+  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
+  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  const kwk_delta* __restrict__ deltas = a.deltas;
+  if (n_deltas <= kLdsDeltas) {
+    for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
+    deltas = s_delta;
+  }
+  __syncthreads();
+
+  const StateFmt fmt = a.fmt;
+  const RawTest R = a.raw;
+  // the idle test's masks doubled for both halves of a dword, and the shifts that move each
+  // single-bit flag to bit 15 of its half (a zero mask yields a zero flag whatever the shift)
+  struct {
+    uint32_t m2, d2, a2, t2, l2, s2, n2;
+    uint32_t sm, sd, sa, sl;
+  } X;
+  X.m2 = R.managed * 0x10001u; X.d2 = R.dirty * 0x10001u; X.a2 = R.alive * 0x10001u;
+  X.t2 = R.term * 0x10001u; X.l2 = R.del * 0x10001u;
+  X.s2 = R.smask * 0x10001u; X.n2 = R.none_code * 0x10001u;
+  X.sm = (uint32_t)(16 - __ffs(R.managed)) & 31u; X.sd = (uint32_t)(16 - __ffs(R.dirty)) & 31u;
+  X.sa = (uint32_t)(16 - __ffs(R.alive)) & 31u; X.sl = (uint32_t)(16 - __ffs(R.del)) & 31u;
+  uint32_t n_matched = 0, n_bytes = 0;  // per lane
+  uint32_t wave_fired = 0;              // wave-uniform
+  uint16_t* __restrict__ wl = s_work[wave];
+  uint4* __restrict__ tq = s_tile[wave];
+  uint16_t* __restrict__ tw = reinterpret_cast<uint16_t*>(tq);
+  uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+
+  // one tile per block, or (kPersist) tiles blockIdx.x, +gridDim.x, ... with the next tile's
+  // chunks in flight while this one runs phases 2 and 3
+  while (tile < n_tiles) {
+    const uint32_t wbase = tile * kTile + wave * kWave;  // the wave's first slot
+    const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
+    uint32_t seg_n = 0;  // wave-uniform
+    const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
+    kwk_fired_rec* __restrict__ seg = a.fired + seg_id * kWave;
+
+    // ---- phase 1: idle test on the raw words.  bit k = q * 8 + h of a lane's masks
+    uint32_t in_range = 0xFFFFFFFFu >> (32 - K);
+    if (!full) {
+      in_range = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        in_range |= (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8) < a.n ? 1u : 0u) << k;
+    }
+    // two words per dword (SWAR): each test leaves its per-word flag at bit 15 / bit 31
+    uint32_t pend = 0, need = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t dw[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d = dw[j];
+        const uint32_t mg = (d & X.m2) << X.sm;
+        const uint32_t pe = ((((d >> R.sshift) & X.s2) ^ X.n2) + 0x7FFF7FFFu) & 0x80008000u;
+        uint32_t nb = (d & X.d2) << X.sd;
+        if (kHarness) {
+          nb |= (~d & X.a2) << X.sa;
+          nb |= (((d & X.t2) + 0x7FFF7FFFu) & 0x80008000u) & ~((d & X.l2) << X.sl);
+        }
+        const uint32_t n2 = mg & nb, p2 = mg & pe;
+        const int k = q * 8 + 2 * j;
+        need |= ((n2 >> 15) & 1u) << k | (n2 >> 31) << (k + 1);
+        pend |= ((p2 >> 15) & 1u) << k | (p2 >> 31) << (k + 1);
+      }
+    }
+    pend &= in_range;
+    need &= in_range;
+    if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
+      const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+#pragma unroll 8
+      for (int k = 0; k < K; ++k) {
+        const uint32_t p = (pend >> k) & 1u;
+        const int64_t d =
+            buf_load_i64(due_rs, p ? (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8)) * 8u : kOOB);
+        need |= (p & (uint32_t)(d <= a.now)) << k;
+      }
+    }
+    n_bytes += 2u * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
+    // work list in slot order: exclusive prefix of the per-lane counts (6 ballots, counts
+    // <= 32), then each lane writes its own entries
+    uint32_t n_work = 0, pos = 0;  // n_work wave-uniform
+    {
+      const uint32_t cnt = (uint32_t)__popc(need);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const unsigned long long bal = __ballot((cnt >> b) & 1u);
+        pos += (uint32_t)__popcll(bal & lt) << b;
+        n_work += (uint32_t)__popcll(bal) << b;
+      }
+      for (uint32_t m = need; m; m &= m - 1u) {
+        const uint32_t k = (uint32_t)__ffs(m) - 1u;
+        wl[pos++] = (uint16_t)((k >> 3) * 512u + lane * 8u + (k & 7u));
+      }
+    }
+    uint4 cur[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[q] = v[q];
+    const uint32_t next = kPersist ? tile + gridDim.x : n_tiles;
+    if (kPersist && next < n_tiles) issue_tile(next);
+
+    if (n_work) {
+      // ---- phase 2
+#pragma unroll
+      for (int q = 0; q < Q; ++q) tq[q * 64 + lane] = cur[q];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (uint32_t c = 0; c < n_work; c += 64) {
+        const uint32_t j = c + lane;
+        Fire f{false, 0, 0, 0};
+        uint64_t i = 0;
+        if (j < n_work) {
+          const uint32_t w = wl[j];
+          i = wbase + w;
+          const uint2 s = fmt_unpack(tw[w], fmt);
+          const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;  // counted in phase 1
+          const uint2 nv = process_object<kHarness, 2>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
+                                                       n_matched, s_lut, lut_n);
+          tw[w] = (uint16_t)fmt_pack(nv.x, nv.y, fmt);
+        }
+        n_bytes += f.bytes;
+        emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // ---- phase 3: whole 128-byte lines wherever a word changed
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint4 nv = tq[q * 64 + lane];
+        const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
+        const unsigned long long bal = __ballot(ch);
+        if (!KWOK_EXP_NOWRITE && ((bal >> (lane & ~7u)) & 0xFFull))
+          gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u] = nv;
+      }
+      // the next tile reuses this wave's LDS lists and tile
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (lane == 0) a.wave_counts[seg_id] = seg_n;
+    wave_fired += seg_n;
+    n_bytes += lane == 0 ? 4u : 0u;  // the fired count word
+    tile = next;
+  }
+
+  // ---- block statistics
+  for (int off = 32; off > 0; off >>= 1) {
+    n_matched += __shfl_xor(n_matched, off);
+    n_bytes += __shfl_xor(n_bytes, off);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_stat[0], n_matched);
+    atomicAdd(&s_stat[1], wave_fired);
+    atomicAdd(&s_stat[2], n_bytes);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 + n_stages) {
+    const unsigned int val = s_stat[threadIdx.x];
+    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
+  }
+}
+
 // gather the per-wave fired segments into one dense list (offsets from an exclusive scan)
 __global__ void compact_fired_kernel(const kwk_fired_rec* __restrict__ fired, const uint32_t* __restrict__ counts,
                                      const uint32_t* __restrict__ offsets, uint32_t n_waves, uint32_t wave_seg,
@@ -1105,7 +1332,7 @@ struct kwk_engine {
   uint32_t capacity = 0, n_active = 0, value_slots = 0, max_records = 0;
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
-  uint32_t n_blocks_cap = 0, last_blocks = 0;
+  uint32_t n_blocks_cap = 0, last_blocks = 0, last_grid = 0;
   uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 8 | 16 | 32)
   uint32_t objs_narrow = 16;
   uint32_t last_objs = 16;
@@ -1116,8 +1343,11 @@ struct kwk_engine {
   void* d_st = nullptr;       // state word per slot (8-byte capacity; format in fmt)
   StateFmt fmt{};             // current state format (wide until a table allows narrow)
   bool force_wide = false;
+  bool allow_half = true;     // KWK_ENGINE_STATE32 / KWOK_STATE_BYTES=4: never the 2-byte format
+  uint32_t q16 = KWOK_Q16;    // 2-byte sweep: 16-byte chunks per lane (KWOK_SWEEP_Q16: 2 | 4)
   int n_cus = 256;
   bool grid_per_tile = false;
+  bool persist16 = true;      // 2-byte sweep grid (KWOK_SWEEP16_GRID=tile: one block per tile)
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -1168,8 +1398,9 @@ struct kwk_engine {
   std::vector<hipEvent_t> events;
 };
 
-// narrow iff pred + class + stage code + 5 flag bits fit 32 bits
-static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stages, bool allow_narrow) {
+// narrow iff pred + class + stage code + 5 flag bits fit 32 bits, half iff they fit 16
+// 
+static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stages, bool allow_narrow, bool allow_half) {
   auto bitlen = [](uint32_t x) {
     uint32_t b = 0;
     while (x) { ++b; x >>= 1; }
@@ -1181,6 +1412,7 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
   StateFmt f{};
   if (!allow_narrow || pb + cb + sb + 5 > 32) return f;
   f.narrow = 1;
+  f.half = (allow_half && pb + cb + sb + 5 <= 16) ? 1u : 0u;
   f.pmask = (1u << pb) - 1u;
   f.cshift = pb;
   f.cmask = cb ? ((1u << cb) - 1u) : 0u;
@@ -1191,14 +1423,17 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
   return f;
 }
 
-static size_t word_bytes(const StateFmt& f) { return f.narrow ? 4 : 8; }
+static size_t word_bytes(const StateFmt& f) { return f.half ? 2 : f.narrow ? 4 : 8; }
 
 static bool same_fmt(const StateFmt& a, const StateFmt& b) { return memcmp(&a, &b, sizeof(StateFmt)) == 0; }
 
 // host-side conversion of device state words <-> (pred, sched)
 static std::vector<uint2> unpack_words(const std::vector<uint8_t>& raw, const StateFmt& f, uint32_t n) {
   std::vector<uint2> out(n);
-  if (f.narrow) {
+  if (f.half) {
+    const uint16_t* w = reinterpret_cast<const uint16_t*>(raw.data());
+    for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
+  } else if (f.narrow) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(raw.data());
     for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
   } else {
@@ -1209,7 +1444,10 @@ static std::vector<uint2> unpack_words(const std::vector<uint8_t>& raw, const St
 
 static std::vector<uint8_t> pack_words(const std::vector<uint2>& v, const StateFmt& f) {
   std::vector<uint8_t> raw(word_bytes(f) * v.size());
-  if (f.narrow) {
+  if (f.half) {
+    uint16_t* w = reinterpret_cast<uint16_t*>(raw.data());
+    for (size_t i = 0; i < v.size(); ++i) w[i] = (uint16_t)fmt_pack(v[i].x, v[i].y, f);
+  } else if (f.narrow) {
     uint32_t* w = reinterpret_cast<uint32_t*>(raw.data());
     for (size_t i = 0; i < v.size(); ++i) w[i] = fmt_pack(v[i].x, v[i].y, f);
   } else {
@@ -1260,8 +1498,15 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->kind_salt = d->kind_salt;
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
   e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
+  e->allow_half = (d->flags & KWK_ENGINE_STATE32) == 0;
+  if (const char* v = getenv("KWOK_STATE_BYTES")) e->allow_half = e->allow_half && atoi(v) != 4;
+  if (const char* v = getenv("KWOK_SWEEP_Q16")) {
+    const int q = atoi(v);
+    if (q == 2 || q == 4) e->q16 = (uint32_t)q;
+  }
   e->grid_per_tile = true;  // one block per tile: measured faster than the persistent grid with churn
   if (const char* v = getenv("KWOK_SWEEP_GRID")) e->grid_per_tile = strcmp(v, "persist") != 0;
+  if (const char* v = getenv("KWOK_SWEEP16_GRID")) e->persist16 = strcmp(v, "tile") != 0;
   if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
     const int k = atoi(v);
     if (k == 8 || k == 16) e->objs_wide = (uint32_t)k;
@@ -1280,7 +1525,11 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
       return fail(KWK_EHIP, std::string("hipMalloc: ") + hipGetErrorString(er)); \
     }                                                                            \
   } while (0)
-  ALLOC(e->d_st, sizeof(uint2) * (size_t)e->capacity);
+  // state words: 8 bytes per slot (wide), slots padded to the largest sweep tile so that whole
+  // chunks / lines of the last tile stay inside the allocation
+  const size_t st_slots = ((size_t)e->capacity + kBlock * kMaxObjPerThread - 1) / (kBlock * kMaxObjPerThread) *
+                          (kBlock * kMaxObjPerThread);
+  ALLOC(e->d_st, sizeof(uint2) * st_slots);
   ALLOC(e->d_due, sizeof(int64_t) * (size_t)e->capacity);
   ALLOC(e->d_del, sizeof(int64_t) * (size_t)e->capacity);
   ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
@@ -1296,7 +1545,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
-  hipMemsetAsync(e->d_st, 0, sizeof(uint2) * (size_t)e->capacity, e->stream);
+  hipMemsetAsync(e->d_st, 0, sizeof(uint2) * st_slots, e->stream);
   hipMemsetAsync(e->d_due, 0, sizeof(int64_t) * (size_t)e->capacity, e->stream);
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
@@ -1344,7 +1593,7 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   if (t->pred_bits > 32) return fail(KWK_EINVAL, "pred_bits > 32");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  const StateFmt nf = make_fmt(t->pred_bits, t->n_classes, t->n_stages, !e->force_wide);
+  const StateFmt nf = make_fmt(t->pred_bits, t->n_classes, t->n_stages, !e->force_wide, e->allow_half);
   if (!same_fmt(nf, e->fmt)) {
     if (e->n_active) {  // repack the resident objects into the new format
       const uint32_t n = e->n_active;
@@ -1505,6 +1754,14 @@ static uint32_t sweep_grid(kwk_engine* e, uint32_t tiles) {
   return tiles < g ? tiles : g;
 }
 
+// persistent grid of the 2-byte sweep: every block slot the occupancy allows on every CU
+static uint32_t persist_grid(kwk_engine* e, const void* kernel, uint32_t tiles) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
+  return tiles < g ? tiles : g;
+}
+
 static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
@@ -1542,10 +1799,36 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   a.harness = e->harness;
   if (!fire) a.harness.enable = 0;
   const bool nar = e->fmt.narrow != 0;
+  const bool h = a.harness.enable != 0;
+  if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
+    const uint32_t K = 8 * e->q16, tile = kBlock * K;
+    const uint32_t tiles = (e->n_active + tile - 1) / tile;
+    uint32_t blocks = tiles;
+#define LAUNCH16(HV, QV)                                                                                        \
+  do {                                                                                                          \
+    if (!e->persist16) {                                                                                       \
+      hipLaunchKernelGGL((sweep16_kernel<HV, QV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);       \
+    } else {                                                                                                    \
+      blocks = persist_grid(e, (const void*)sweep16_kernel<HV, QV, true>, tiles);                              \
+      hipLaunchKernelGGL((sweep16_kernel<HV, QV, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);        \
+    }                                                                                                           \
+  } while (0)
+    if (e->q16 == 4) {
+      if (h) LAUNCH16(true, 4); else LAUNCH16(false, 4);
+    } else {
+      if (h) LAUNCH16(true, 2); else LAUNCH16(false, 2);
+    }
+#undef LAUNCH16
+    e->last_objs = K;
+    HIP_TRY(hipGetLastError());
+    e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
+    e->last_grid = blocks;
+    ++e->steps;
+    return KWK_OK;
+  }
   const uint32_t K = nar ? e->objs_narrow : e->objs_wide;
   const uint32_t tile = kBlock * K;
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
-  const bool h = a.harness.enable != 0;
 #define LAUNCH(HV, KV, NV) \
   do {                                                                                                           \
     if (e->grid_per_tile)                                                                                       \

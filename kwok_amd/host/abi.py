@@ -81,6 +81,7 @@ class EngineDesc(C.Structure):
 
 
 ENGINE_WIDE_STATE = 1
+ENGINE_STATE32 = 2
 
 
 class Lease(C.Structure):

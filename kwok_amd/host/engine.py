@@ -107,12 +107,16 @@ class Engine:
     """One kwk_engine (C ABI) for one KindProgram."""
 
     def __init__(self, program: KindProgram, capacity: int, device: int = 0, slot_base: int = 0, kind_salt: int = 0,
-                 max_records: int = 1 << 16, wide_state: bool = False):
+                 max_records: int = 1 << 16, wide_state: bool = False, state: str = "auto"):
+        """state: "auto" (the narrowest packed format the stage table fits: 2 or 4 bytes, else
+        8), "u32" (never the 2-byte format) or "wide" (always 8 bytes; = wide_state)."""
         self.p = program
         L = abi.lib()
+        if wide_state:
+            state = "wide"
+        flags = {"auto": 0, "u32": abi.ENGINE_STATE32, "wide": abi.ENGINE_WIDE_STATE}[state]
         d = abi.EngineDesc(device=device, capacity=capacity, value_slots=max(1, len(program.slots)),
-                           max_records=max_records, slot_base=slot_base, kind_salt=kind_salt,
-                           flags=abi.ENGINE_WIDE_STATE if wide_state else 0)
+                           max_records=max_records, slot_base=slot_base, kind_salt=kind_salt, flags=flags)
         h = C.c_void_p()
         abi.check(L.kwk_engine_create(C.byref(d), C.byref(h)), "kwk_engine_create")
         self.h = h

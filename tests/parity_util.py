@@ -13,14 +13,27 @@ from oracle.sim import OracleSim, oracle_pred
 NOW0 = 1_700_000_000 * 10**9
 
 
-def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False):
+def expected_state_bytes(prog, state="auto"):
+    """Mirror of make_fmt (engine.hip): packed word = pred | class | stage code | 5 flags."""
+    if state == "wide":
+        return 8
+    t = prog.table()
+    pb = t.pred_bits or 32
+    bits = pb + max(0, t.n_classes - 1).bit_length() + t.n_stages.bit_length() + 5
+    if bits <= 16 and state == "auto":
+        return 2
+    return 4 if bits <= 32 else 8
+
+
+def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto"):
     stages = load_stage_files(*stage_files)
     prog = KindProgram(stages, HarnessSpec() if harness else None)
     prog.explore(objs)
     assert not prog.delta_conflicts, prog.delta_conflicts
     ing = Ingest(prog)
     hot, dels, rec, cls = ing.columns(objs)
-    eng = Engine(prog, capacity=max(1, len(objs)), kind_salt=kind_salt, slot_base=slot_base, wide_state=wide_state)
+    eng = Engine(prog, capacity=max(1, len(objs)), kind_salt=kind_salt, slot_base=slot_base, wide_state=wide_state,
+                 state=state)
     eng.load_stages()
     eng.set_harness(harness)
     eng.load(hot, dels, rec, cls, ing.record_array())
@@ -57,8 +70,11 @@ def compare_state(prog, eng, sim, step):
     assert not bad, f"step {step}: {len(bad)} mismatches, first: {bad[:8]}"
 
 
-def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False):
-    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, wide_state=wide_state)
+def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False,
+        state="auto"):
+    if wide_state:
+        state = "wide"
+    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state)
     total = 0
     per_stage = np.zeros(len(prog.names), dtype=np.int64)
     try:
@@ -76,7 +92,7 @@ def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0
             if check_state:
                 compare_state(prog, eng, sim, k)
         st = eng.stats()
-        assert st["state_bytes"] == (8 if wide_state else 4)  # every shipped stage set fits the packed format
+        assert st["state_bytes"] == expected_state_bytes(prog, state)
         assert st["fired"] == total
         assert [st["fired_per_stage"][n] for n in prog.names] == list(per_stage)
     finally:

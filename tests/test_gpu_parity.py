@@ -12,13 +12,16 @@ from tests.parity_util import run
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
-def test_pod_fast_c1_mini(wide):
-    """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in both
-    device state formats."""
+FORMATS = ["auto", "u32", "wide"]
+
+
+@pytest.mark.parametrize("state", FORMATS)
+def test_pod_fast_c1_mini(state):
+    """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in every
+    device state format (auto = the 2-byte words of the whole-line sweep)."""
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, wide_state=wide)
+    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state)
     assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
 
 
@@ -34,10 +37,11 @@ def test_pod_general_c2_mini(wide):
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
 
-def test_node_fast_heartbeat():
+@pytest.mark.parametrize("state", ["auto", "u32"])
+def test_node_fast_heartbeat(state):
     cl = W.make_cluster("C1", 64, 64, seed=13)
     objs = cl.nodes.materialize()
-    total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1)
+    total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1, state=state)
     assert per["node-initialize"] == 64 and per["node-heartbeat"] > 0
 
 
@@ -136,7 +140,7 @@ def test_count_phase_histogram():
 
 def test_state_format_repack_on_table_reload():
     """kwk_load_stages with objects resident and a table that needs the other state format
-    (pred_bits = 0 -> 32 bits -> wide, then back to packed) repacks them in place; the run
+    (pred_bits = 0 -> 32 bits -> wide, then back to the 2-byte packed words) repacks them in place; the run
     stays bit-exact with the oracle."""
     import ctypes as C
     from kwok_amd.host import abi
@@ -151,7 +155,7 @@ def test_state_format_repack_on_table_reload():
                     t.pred_bits = 0
                 deltas = np.ascontiguousarray(prog.delta_array())
                 abi.check(abi.lib().kwk_load_stages(eng.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
-                assert eng.stats()["state_bytes"] == (8 if k == 3 else 4)
+                assert eng.stats()["state_bytes"] == (8 if k == 3 else 2)
             now = NOW0 + k * 10**9
             eng.step(now, 9, k)
             got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())

@@ -159,8 +159,8 @@ def test_controller_scenario_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
-def test_c3_nodes_leases_pods_parity(wide):
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_c3_nodes_leases_pods_parity(state):
     """C3 shape at 96 nodes (node-initialize + node-heartbeat 20 s / 25 s, leases 40 s with a
     10 s +- 4% renew, 250 ms tick for 50 s) with 4 pod-fast pods per node: lease step ->
     node MANAGED / resync -> node sweep -> pod resync -> pod sweep, every step bit-exact
@@ -173,8 +173,8 @@ def test_c3_nodes_leases_pods_parity(wide):
     node_ptr = np.arange(0, n_nodes * ppn + 1, ppn, dtype=np.uint32)
     leases = c3_leases(n_nodes, NOW0, rng)
     me = 1
-    nprog, neng, nsim = build(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), nodes, kind_salt=1, wide_state=wide)
-    pprog, peng, psim = build(W.stage_paths(W.POD_FAST), pods, harness=True, wide_state=wide)
+    nprog, neng, nsim = build(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), nodes, kind_salt=1, state=state)
+    pprog, peng, psim = build(W.stage_paths(W.POD_FAST), pods, harness=True, state=state)
     try:
         # initial readOnly: only nodes whose cached lease is ours are managed (and their pods)
         init_held = [LR.held(L, me) for L in leases]
