@@ -226,6 +226,9 @@ struct SweepArgs {
   StateFmt fmt;
   RawTest raw;
   kwk_harness harness;
+  const uint32_t* __restrict__ fsm;  // 2-byte sweep: per-(due ready, word) transition entries (or null)
+  const int64_t* __restrict__ fsm_due;
+  uint32_t fsm_bits;
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -255,9 +258,13 @@ struct Fire {      // what one object's step produced
 
 // match + weighted pick + delay for one dirty object (preprocess, pod_controller.go:196-254).
 // Updates sched (pending stage / MATCHERR) and due; returns true if a stage was scheduled.
+// kProbe (fsm_build_kernel): evaluate for a state word alone; every step that needs more than
+// the word (a value record, the deletion column, a Philox draw) sets `gen` instead.
+template <bool kProbe = false>
 __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                              uint32_t n_stages, uint64_t i, uint32_t pred, uint32_t& sched,
-                                             int64_t& due, uint32_t& bytes, const uint32_t* lut, uint32_t lut_n) {
+                                             int64_t& due, uint32_t& bytes, const uint32_t* lut, uint32_t lut_n,
+                                             uint32_t& gen) {
   uint32_t m = 0;
   if (pred < lut_n) {
     m = lut[pred];
@@ -268,6 +275,7 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
   if (m == 0) return false;  // no match: a queued job stays queued (pod_controller.go:222-229)
   const kwk_value* __restrict__ rec = nullptr;
   if (sched & KWK_F_HASREC) {
+    if constexpr (kProbe) { gen = 1; return false; }
     rec = a.values + (uint64_t)a.rec_idx[i] * a.value_slots;
     bytes += 4 + 16 * 3;  // record index + (at most) the picked stage's three entries
   }
@@ -277,6 +285,7 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
   if (cnt == 1) {
     pick = __ffs(m) - 1;
   } else {
+    if constexpr (kProbe) { gen = 1; return false; }  // weighted pick: a Philox draw (or a panic path)
     int64_t total = 0;
     int nerr = 0, nge0 = 0;
     for (uint32_t mm = m; mm; mm &= mm - 1) {
@@ -322,6 +331,9 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
   int64_t delay = 0;
   if (S.has_delay) {
     const bool need_del = S.delay_slot == KWK_SLOT_DELETION || S.jitter_slot == KWK_SLOT_DELETION;
+    if constexpr (kProbe) {
+      if (need_del) { gen = 1; return false; }
+    }
     const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;
     if (need_del) bytes += 8;
     const Getter d = eval_getter(S.delay_slot, S.delay_default, true, sched, rec, dels, a.now, true);
@@ -335,6 +347,9 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
             delay = j.v;
           } else {
             const int64_t jit = (int64_t)((uint64_t)j.v - (uint64_t)delay);
+            if constexpr (kProbe) {
+              if (jit > 0) { gen = 1; return false; }
+            }
             if (jit > 0)
               delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));
           }
@@ -391,18 +406,21 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
 // harness + match + fire for one object whose state needs work.  Returns the new state (the
 // caller writes it back); writes the due column itself when a newly scheduled stage stays
 // pending past this step (a stage that fires in the same step never needs its due stored).
-template <bool kHarness, uint32_t kWordBytes>
+// kProbe: see match_object; the due time a scheduled stage would store goes to due_w (gen and
+// due_w are unused otherwise)
+template <bool kHarness, uint32_t kWordBytes, bool kProbe = false>
 __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
                                                int64_t due, Fire& f, uint32_t& n_matched, const uint32_t* lut,
-                                               uint32_t lut_n) {
+                                               uint32_t lut_n, uint32_t& gen, int64_t& due_w) {
   if (kHarness) {
     if (!(sched & KWK_F_ALIVE)) {  // re-create a deleted object from its spec
       pred &= a.harness.keep_mask;  // same spec: class bits and record flag stay
       sched = (sched & (KWK_F_MANAGED | KWK_F_HASREC | KWK_CLASS_MASK)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE;
       if (a.harness.track_deletion) {
-        a.del_s[i] = KWK_DEL_ABSENT;
+        if constexpr (kProbe) gen = 1;
+        else a.del_s[i] = KWK_DEL_ABSENT;
         f.bytes += 8;
       }
     } else if ((pred & a.harness.terminal_mask) && !(pred & a.harness.deletion_bit)) {
@@ -410,7 +428,8 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
       int64_t sec = a.now / 1000000000;
       if (a.now % 1000000000 < 0) sec -= 1;
       if (a.harness.track_deletion) {
-        a.del_s[i] = sec;
+        if constexpr (kProbe) gen = 1;
+        else a.del_s[i] = sec;
         f.bytes += 8;
       }
       sched |= KWK_F_DIRTY;
@@ -419,7 +438,7 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
   bool scheduled = false;
   if (sched & KWK_F_ALIVE) {
     if (sched & KWK_F_DIRTY) {
-      scheduled = match_object(a, T, n_stages, i, pred, sched, due, f.bytes, lut, lut_n);
+      scheduled = match_object<kProbe>(a, T, n_stages, i, pred, sched, due, f.bytes, lut, lut_n, gen);
       n_matched += scheduled ? 1 : 0;
     }
     const uint32_t st = sched & 0xFFu;
@@ -427,7 +446,8 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
                                                    pred, sched, f);
   }
   if (scheduled && (sched & 0xFFu) < n_stages) {
-    a.due[i] = due;
+    if constexpr (kProbe) due_w = due;
+    else a.due[i] = due;
     f.bytes += 8;
   }
   f.bytes += kWordBytes;  // the state write-back (done by the caller)
@@ -691,8 +711,10 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
         due = ((fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code) ? a.due[i] : 0;
       }
       const uint2 s = sw_decode(raw, fmt);
+      uint32_t gen_unused = 0;
+      int64_t due_unused = 0;
       const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                            n_matched, lut, lut_n);
+                                                            n_matched, lut, lut_n, gen_unused, due_unused);
       W out;
       sw_encode(out, nv, fmt);
 #if KWOK_GROUP
@@ -761,6 +783,41 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     // no-return atomic: the block does not wait for a read-modify-write round trip
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
   }
+}
+
+// ------------------------------------------------------------------ 2-byte state transition table
+// With 2-byte state words the compiled stage program is a finite state machine over at most
+// 2^16 words: for every word (and whether its queued stage is due) fsm_build_kernel runs the
+// same process_object as the sweep, in probe mode, once per stage-table / harness load.  An
+// entry is marked general whenever the outcome needs more than the word (a Philox draw for a
+// weighted pick or jitter, a value record, the deletion column); the sweep runs process_object
+// for those and one table lookup for the rest.  Entry: [15:0] new word, [20:16] fired stage,
+// [21] fired, [24:22] fired flags, [25] matched, [29:26] algorithmic bytes / 2, [30] writes
+// due = now + fsm_due[entry], [31] general.
+constexpr uint32_t kFsmDue = 1u << 30, kFsmGeneral = 1u << 31;
+
+template <bool kHarness>
+__global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_t* __restrict__ dtab) {
+  const uint32_t bits = a.fsm_bits;
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (2u << bits)) return;
+  const uint32_t w = idx & ((1u << bits) - 1u), rdy = idx >> bits;
+  const uint2 s = fmt_unpack(w, a.fmt);
+  const kwk_stage_table* __restrict__ T = a.table;
+  // probe clock: now = 0, a queued stage is due (0) or not yet (1)
+  const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? (rdy ? 0 : 1) : 0;
+  Fire f{false, 0, 0, 0};
+  uint32_t nm = 0, gen = 0;
+  int64_t dw = INT64_MIN;  // set iff process_object stores a due time
+  const uint2 nv = process_object<kHarness, 2, true>(a, T, a.deltas, T->n_stages, T->fin_group_mask, 0, s.x, s.y, due,
+                                                     f, nm, a.lut, a.lut_n, gen, dw);
+  uint32_t e = fmt_pack(nv.x, nv.y, a.fmt) & 0xFFFFu;
+  e |= (f.stage & 31u) << 16 | (f.fire ? 1u : 0u) << 21 | (f.flags & 7u) << 22 | (nm & 1u) << 25;
+  e |= ((f.bytes >> 1) & 15u) << 26;
+  if (dw != INT64_MIN) e |= kFsmDue;
+  if (gen || f.bytes > 30 || (f.bytes & 1u)) e = kFsmGeneral;
+  tab[idx] = e;
+  dtab[idx] = dw;
 }
 
 // ------------------------------------------------------------------ 2-byte state sweep
@@ -873,7 +930,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
         in_range |= (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8) < a.n ? 1u : 0u) << k;
     }
     // two words per dword (SWAR): each test leaves its per-word flag at bit 15 / bit 31
-    uint32_t pend = 0, need = 0;
+    uint32_t pend = 0, need = 0, ready = 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t dw[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -902,8 +959,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
         const uint32_t p = (pend >> k) & 1u;
         const int64_t d =
             buf_load_i64(due_rs, p ? (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8)) * 8u : kOOB);
-        need |= (p & (uint32_t)(d <= a.now)) << k;
+        ready |= (p & (uint32_t)(d <= a.now)) << k;
       }
+      need |= ready;
     }
     n_bytes += 2u * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
     // work list in slot order: exclusive prefix of the per-lane counts (6 ballots, counts
@@ -920,7 +978,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
       }
       for (uint32_t m = need; m; m &= m - 1u) {
         const uint32_t k = (uint32_t)__ffs(m) - 1u;
-        wl[pos++] = (uint16_t)((k >> 3) * 512u + lane * 8u + (k & 7u));
+        wl[pos++] = (uint16_t)((k >> 3) * 512u + lane * 8u + (k & 7u) + (((ready >> k) & 1u) << 15));
       }
     }
     uint4 cur[Q];
@@ -939,13 +997,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
         Fire f{false, 0, 0, 0};
         uint64_t i = 0;
         if (j < n_work) {
-          const uint32_t w = wl[j];
+          const uint32_t we = wl[j];
+          const uint32_t w = we & 0x7FFFu, rdy = we >> 15;  // slot in the wave region, due ready
           i = wbase + w;
-          const uint2 s = fmt_unpack(tw[w], fmt);
-          const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;  // counted in phase 1
-          const uint2 nv = process_object<kHarness, 2>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                       n_matched, s_lut, lut_n);
-          tw[w] = (uint16_t)fmt_pack(nv.x, nv.y, fmt);
+          const uint32_t raw = tw[w];
+          const uint32_t e = a.fsm ? a.fsm[(rdy << a.fsm_bits) | raw] : kFsmGeneral;
+          if (!(e & kFsmGeneral)) {  // the word's transition, precomputed by fsm_build_kernel
+            tw[w] = (uint16_t)e;
+            if (e & kFsmDue) a.due[i] = sat_add(a.now, a.fsm_due[(rdy << a.fsm_bits) | raw]);
+            f.fire = (e >> 21) & 1u;
+            f.stage = (e >> 16) & 31u;
+            f.flags = (e >> 22) & 7u;
+            f.bytes = ((e >> 26) & 15u) * 2u;
+            n_matched += (e >> 25) & 1u;
+          } else {
+            const uint2 s = fmt_unpack(raw, fmt);
+            const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;  // counted in phase 1
+            uint32_t gen_unused = 0;
+            int64_t due_unused = 0;
+            const uint2 nv = process_object<kHarness, 2>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
+                                                         n_matched, s_lut, lut_n, gen_unused, due_unused);
+            tw[w] = (uint16_t)fmt_pack(nv.x, nv.y, fmt);
+          }
         }
         n_bytes += f.bytes;
         emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
@@ -1347,7 +1420,12 @@ struct kwk_engine {
   uint32_t q16 = KWOK_Q16;    // 2-byte sweep: 16-byte chunks per lane (KWOK_SWEEP_Q16: 2 | 4)
   int n_cus = 256;
   bool grid_per_tile = false;
-  bool persist16 = true;      // 2-byte sweep grid (KWOK_SWEEP16_GRID=tile: one block per tile)
+  bool persist16 = true;
+  bool use_fsm = true;        // KWOK_FSM=0: 2-byte sweep without the transition table
+  uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
+  int64_t* d_fsm_due = nullptr;
+  uint32_t fsm_bits = 0;
+  int fsm_harness = -1;       // harness enable the table was built for (-1: no table)      // 2-byte sweep grid (KWOK_SWEEP16_GRID=tile: one block per tile)
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -1422,6 +1500,8 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
   f.fshift = pb + cb + sb;
   return f;
 }
+
+static kwk_status build_fsm(kwk_engine* e);
 
 static size_t word_bytes(const StateFmt& f) { return f.half ? 2 : f.narrow ? 4 : 8; }
 
@@ -1507,6 +1587,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->grid_per_tile = true;  // one block per tile: measured faster than the persistent grid with churn
   if (const char* v = getenv("KWOK_SWEEP_GRID")) e->grid_per_tile = strcmp(v, "persist") != 0;
   if (const char* v = getenv("KWOK_SWEEP16_GRID")) e->persist16 = strcmp(v, "tile") != 0;
+  if (const char* v = getenv("KWOK_FSM")) e->use_fsm = atoi(v) != 0;
   if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
     const int k = atoi(v);
     if (k == 8 || k == 16) e->objs_wide = (uint32_t)k;
@@ -1568,7 +1649,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
-                  e->d_lease, e->d_lease_op, e->d_lease_ops,
+                  e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due,
                   e->d_lease_nops, e->d_lease_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
@@ -1626,13 +1707,14 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   e->n_stages = t->n_stages;
   e->n_classes = t->n_classes;
   e->loaded_table = true;
-  return KWK_OK;
+  return build_fsm(e);
 }
 
 kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
   if (!e || !h) return fail(KWK_EINVAL, "null argument");
   e->harness = *h;
-  return KWK_OK;
+  if (kwk_status st = set_dev(e)) return st;
+  return build_fsm(e);
 }
 
 kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t* del, const uint32_t* rec,
@@ -1762,10 +1844,7 @@ static uint32_t persist_grid(kwk_engine* e, const void* kernel, uint32_t tiles) 
   return tiles < g ? tiles : g;
 }
 
-static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
-  if (!e) return fail(KWK_EINVAL, "null engine");
-  if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
-  if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
+static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
   SweepArgs a;
   a.st = e->d_st;
   a.due = e->d_due;
@@ -1798,8 +1877,55 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   }
   a.harness = e->harness;
   if (!fire) a.harness.enable = 0;
+  a.fsm = nullptr;
+  a.fsm_due = nullptr;
+  a.fsm_bits = 0;
+  return a;
+}
+
+// (re)build the 2-byte format's transition table for the loaded stage table and harness
+static kwk_status build_fsm(kwk_engine* e) {
+  e->fsm_harness = -1;
+  if (!e->fmt.half || !e->loaded_table || !e->use_fsm) return KWK_OK;
+  const uint32_t bits = e->fmt.fshift + 5;
+  if (bits > 16) return KWK_OK;
+  if (e->fsm_bits != bits || !e->d_fsm) {
+    if (e->d_fsm) HIP_TRY(hipFree(e->d_fsm));
+    if (e->d_fsm_due) HIP_TRY(hipFree(e->d_fsm_due));
+    e->d_fsm = nullptr;
+    e->d_fsm_due = nullptr;
+    HIP_TRY(hipMalloc(&e->d_fsm, sizeof(uint32_t) * (2u << bits)));
+    HIP_TRY(hipMalloc(&e->d_fsm_due, sizeof(int64_t) * (2u << bits)));
+    e->fsm_bits = bits;
+  }
+  SweepArgs a = sweep_args(e, 0, 0, 0, true);
+  a.fsm_bits = bits;
+  const uint32_t n = 2u << bits;
+  if (a.harness.enable)
+    hipLaunchKernelGGL(fsm_build_kernel<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, e->d_fsm,
+                       e->d_fsm_due);
+  else
+    hipLaunchKernelGGL(fsm_build_kernel<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, e->d_fsm,
+                       e->d_fsm_due);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->fsm_harness = a.harness.enable ? 1 : 0;
+  return KWK_OK;
+}
+
+static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
+  if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
+  SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
   const bool h = a.harness.enable != 0;
+  if (e->fmt.half && fire && e->fsm_harness == (h ? 1 : 0)) {
+    a.fsm = e->d_fsm;
+    a.fsm_due = e->d_fsm_due;
+    a.fsm_bits = e->fsm_bits;
+  }
+
   if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
     const uint32_t K = 8 * e->q16, tile = kBlock * K;
     const uint32_t tiles = (e->n_active + tile - 1) / tile;

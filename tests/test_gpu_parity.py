@@ -15,10 +15,14 @@ pytestmark = pytest.mark.gpu
 FORMATS = ["auto", "u32", "wide"]
 
 
-@pytest.mark.parametrize("state", FORMATS)
-def test_pod_fast_c1_mini(state):
+@pytest.mark.parametrize("state", FORMATS + ["auto-nofsm"])
+def test_pod_fast_c1_mini(state, monkeypatch):
     """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in every
-    device state format (auto = the 2-byte words of the whole-line sweep)."""
+    device state format (auto = the 2-byte words of the whole-line sweep, with and without
+    its precomputed transition table)."""
+    if state == "auto-nofsm":
+        monkeypatch.setenv("KWOK_FSM", "0")
+        state = "auto"
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
     total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state)
@@ -37,8 +41,11 @@ def test_pod_general_c2_mini(wide):
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
 
-@pytest.mark.parametrize("state", ["auto", "u32"])
-def test_node_fast_heartbeat(state):
+@pytest.mark.parametrize("state", ["auto", "auto-nofsm", "u32"])
+def test_node_fast_heartbeat(state, monkeypatch):
+    if state == "auto-nofsm":
+        monkeypatch.setenv("KWOK_FSM", "0")
+        state = "auto"
     cl = W.make_cluster("C1", 64, 64, seed=13)
     objs = cl.nodes.materialize()
     total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1, state=state)

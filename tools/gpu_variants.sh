@@ -10,16 +10,13 @@ run() {  # name, env assignments...   (BARGS: extra bench args)
   env "$@" timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 40 $BARGS > $O/bench_$n.json 2> $O/bench_$n.err || { cat $O/bench_$n.err; exit 1; }
   python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'))"
 }
-run half_q2_persist KWOK_SWEEP_Q16=2
-run half_q2_tile KWOK_SWEEP_Q16=2 KWOK_SWEEP16_GRID=tile
-run half_q4_persist KWOK_SWEEP_Q16=4
+run fsm_q2_persist KWOK_SWEEP_Q16=2
+run nofsm_q2_persist KWOK_SWEEP_Q16=2 KWOK_FSM=0
+run fsm_q2_tile KWOK_SWEEP_Q16=2 KWOK_SWEEP16_GRID=tile
+run fsm_q4_persist KWOK_SWEEP_Q16=4
 for lib in kwok_amd/lib/variants/*.so; do
   [ -e "$lib" ] && run $(basename $lib .so) KWOK_ENGINE_LIB=$R/$lib
 done
-BARGS=--no-harness run idle_half_q2_persist KWOK_SWEEP_Q16=2
-BARGS=--no-harness run idle_half_q2_tile KWOK_SWEEP_Q16=2 KWOK_SWEEP16_GRID=tile
-BARGS=--no-harness run idle_half_q4_persist KWOK_SWEEP_Q16=4
-BARGS=--no-harness run idle_u32_k16 KWOK_STATE_BYTES=4 KWOK_SWEEP_OBJS=16
-run u32_k16 KWOK_STATE_BYTES=4 KWOK_SWEEP_OBJS=16
-run half_q2_persist_again KWOK_SWEEP_Q16=2
+BARGS=--no-harness run idle_q2_persist KWOK_SWEEP_Q16=2
+run fsm_q2_persist_again KWOK_SWEEP_Q16=2
 echo variants done
