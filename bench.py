@@ -236,6 +236,7 @@ def main():
 
     fired = (s1p["fired"] - s0p["fired"]) + (s1n["fired"] - s0n["fired"])
     pbytes = s1p["bytes"] - s0p["bytes"]
+    plines = s1p["line_bytes"] - s0p["line_bytes"]
     per_stage = {k: s1p["fired_per_stage"][k] - s0p["fired_per_stage"][k] for k in s1p["fired_per_stage"]}
     per_stage.update({k: s1n["fired_per_stage"][k] - s0n["fired_per_stage"][k] for k in s1n["fired_per_stage"]})
 
@@ -262,6 +263,11 @@ def main():
                 "traffic_GBps": (round(traffic / pod_kernel_s / 1e9, 1) if traffic else None),
                 "kernel": ("sweep16_kernel" if sb == 2 else "sweep_kernel") + " (pods)",
                 "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
+                # the same count with state writes as the whole 128-byte lines the sweep stores
+                # (at ~10 % churn nearly every line of the 2-byte column holds a changed word)
+                "line_bytes_per_launch": int(plines / args.steps),
+                "line_achieved": round(plines / args.steps / pod_kernel_s / 1e9, 1),
+                "line_frac": round(plines / args.steps / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2)}
         cpu = None
         log(f"timed {args.steps} steps in {max_s:.3f} s; cpu baseline next")

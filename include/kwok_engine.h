@@ -173,6 +173,8 @@ typedef struct {
   uint64_t bytes;         /* algorithmic bytes moved by the sweep */
   uint64_t fired_per_stage[KWK_MAX_STAGES];
   uint64_t state_bytes;   /* bytes per object of the device state stream: 2 or 4 (packed) or 8 (wide) */
+  uint64_t line_bytes;    /* `bytes` with state writes counted as the whole 128-byte lines the 2-byte
+                           * sweep stores (= bytes for the word-granular 4/8-byte sweeps) */
 } kwk_step_stats;
 
 /* ------------------------------------------------------------------ engine */

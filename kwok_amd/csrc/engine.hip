@@ -46,7 +46,10 @@ constexpr int kBlock = 256;              // 4 waves of 64
 constexpr int kMinObjPerThread = 8;      // smallest sweep variant: sizes the per-block arrays
 constexpr int kMaxObjPerThread = 32;
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kStatWords = 3 + KWK_MAX_STAGES;   // matched, fired, algorithmic bytes, fired per stage
+// matched, fired, algorithmic bytes, fired per stage, line bytes (algorithmic with state writes
+// counted as the whole lines / chunks the sweep stores)
+constexpr int kStatWords = 4 + KWK_MAX_STAGES;
+constexpr int kStatLine = 3 + KWK_MAX_STAGES;
 
 thread_local std::string g_err;
 
@@ -776,9 +779,10 @@ __global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs 
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], wave_fired);
     atomicAdd(&s_stat[2], n_bytes + wave_bytes);
+    atomicAdd(&s_stat[kStatLine], n_bytes + wave_bytes);  // word-granular stores
   }
   __syncthreads();
-  if (threadIdx.x < 3 + n_stages) {
+  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
     const unsigned int val = s_stat[threadIdx.x];
     // no-return atomic: the block does not wait for a read-modify-write round trip
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
@@ -844,7 +848,13 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 #ifndef KWOK_WPE16
 #define KWOK_WPE16 6  // waves per SIMD the register allocation must allow (LDS allows 6 at Q = 2)
 #endif
-template <bool kHarness, int Q, bool kPersist>
+#ifndef KWOK_NT16
+#define KWOK_NT16 1  // phase-3 line stores with the nontemporal hint (r1y: 122 -> 119 us)
+#endif
+#ifndef KWOK_PF16
+#define KWOK_PF16 1  // tiles in flight per wave in the persistent grid (1 or 2)
+#endif
+template <bool kHarness, int Q, bool kPersist, int kDepth = KWOK_PF16>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
   constexpr int K = 8 * Q;                 // words per lane
   constexpr uint32_t kWave = 64u * K;      // words per wave region
@@ -861,17 +871,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
   // load range rounded to 16 bytes (the allocation is tile-padded): a chunk holding the last
   // words comes back whole
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * 2u) + 15u) & ~15u);
-  uint4 v[Q];
-  auto issue_tile = [&](const uint32_t t) {
+  // kDepth tiles in flight per wave (persistent grid): register buffers va (and vb)
+  uint4 va[Q], vb[Q];
+  auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) {
+    if (t >= n_tiles) return;
     const uint32_t wb = t * kTile + wave * kWave;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wb + (uint32_t)q * 512u + lane * 8u) * 2u, 0, 0);
-      v[q] = make_uint4(c[0], c[1], c[2], c[3]);
+      dst[q] = make_uint4(c[0], c[1], c[2], c[3]);
     }
   };
   uint32_t tile = blockIdx.x;
-  if (tile < n_tiles) issue_tile(tile);
+  issue_tile(va, tile);
+  if (kPersist && kDepth == 2) issue_tile(vb, tile + gridDim.x);
   {  // LDS set-up overlaps the stream's latency (see sweep_kernel)
     const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
@@ -906,6 +919,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
   X.sm = (uint32_t)(16 - __ffs(R.managed)) & 31u; X.sd = (uint32_t)(16 - __ffs(R.dirty)) & 31u;
   X.sa = (uint32_t)(16 - __ffs(R.alive)) & 31u; X.sl = (uint32_t)(16 - __ffs(R.del)) & 31u;
   uint32_t n_matched = 0, n_bytes = 0;  // per lane
+  uint32_t n_line = 0;                  // per lane: line bytes - algorithmic bytes (mod 2^32)
   uint32_t wave_fired = 0;              // wave-uniform
   uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ tq = s_tile[wave];
@@ -914,7 +928,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
 
   // one tile per block, or (kPersist) tiles blockIdx.x, +gridDim.x, ... with the next tile's
   // chunks in flight while this one runs phases 2 and 3
-  while (tile < n_tiles) {
+  auto tile_body = [&](uint4 (&v)[Q], const uint32_t tile) {
     const uint32_t wbase = tile * kTile + wave * kWave;  // the wave's first slot
     const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
     uint32_t seg_n = 0;  // wave-uniform
@@ -984,8 +998,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
     uint4 cur[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) cur[q] = v[q];
-    const uint32_t next = kPersist ? tile + gridDim.x : n_tiles;
-    if (kPersist && next < n_tiles) issue_tile(next);
+    if (kPersist) issue_tile(v, tile + kDepth * gridDim.x);  // refill this buffer
 
     if (n_work) {
       // ---- phase 2
@@ -1021,6 +1034,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
           }
         }
         n_bytes += f.bytes;
+        n_line -= j < n_work ? 2u : 0u;  // the word's own write is replaced by the line stores below
         emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1030,8 +1044,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
         const uint4 nv = tq[q * 64 + lane];
         const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
         const unsigned long long bal = __ballot(ch);
-        if (!KWOK_EXP_NOWRITE && ((bal >> (lane & ~7u)) & 0xFFull))
-          gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u] = nv;
+        if ((bal >> (lane & ~7u)) & 0xFFull) {
+          if (!KWOK_EXP_NOWRITE) {
+            if (KWOK_NT16) {
+              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+              __builtin_nontemporal_store(u32x4{nv.x, nv.y, nv.z, nv.w},
+                                          reinterpret_cast<u32x4*>(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u]));
+            }
+            else gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u] = nv;
+          }
+          n_line += 16u;
+        }
       }
       // the next tile reuses this wave's LDS lists and tile
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1039,21 +1062,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
     if (lane == 0) a.wave_counts[seg_id] = seg_n;
     wave_fired += seg_n;
     n_bytes += lane == 0 ? 4u : 0u;  // the fired count word
-    tile = next;
+  };
+  if constexpr (!kPersist) {
+    if (tile < n_tiles) tile_body(va, tile);
+  } else if constexpr (kDepth == 1) {
+    for (; tile < n_tiles; tile += gridDim.x) tile_body(va, tile);
+  } else {
+    for (; tile < n_tiles; tile += 2 * gridDim.x) {
+      tile_body(va, tile);
+      if (tile + gridDim.x < n_tiles) tile_body(vb, tile + gridDim.x);
+    }
   }
 
   // ---- block statistics
   for (int off = 32; off > 0; off >>= 1) {
     n_matched += __shfl_xor(n_matched, off);
     n_bytes += __shfl_xor(n_bytes, off);
+    n_line += __shfl_xor(n_line, off);
   }
   if (lane == 0) {
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], wave_fired);
     atomicAdd(&s_stat[2], n_bytes);
+    atomicAdd(&s_stat[kStatLine], n_bytes + n_line);
   }
   __syncthreads();
-  if (threadIdx.x < 3 + n_stages) {
+  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
     const unsigned int val = s_stat[threadIdx.x];
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
   }
@@ -1582,7 +1616,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   if (const char* v = getenv("KWOK_STATE_BYTES")) e->allow_half = e->allow_half && atoi(v) != 4;
   if (const char* v = getenv("KWOK_SWEEP_Q16")) {
     const int q = atoi(v);
-    if (q == 2 || q == 4) e->q16 = (uint32_t)q;
+    if (q == 1 || q == 2 || q == 4) e->q16 = (uint32_t)q;
   }
   e->grid_per_tile = true;  // one block per tile: measured faster than the persistent grid with churn
   if (const char* v = getenv("KWOK_SWEEP_GRID")) e->grid_per_tile = strcmp(v, "persist") != 0;
@@ -1838,8 +1872,16 @@ static uint32_t sweep_grid(kwk_engine* e, uint32_t tiles) {
 
 // persistent grid of the 2-byte sweep: every block slot the occupancy allows on every CU
 static uint32_t persist_grid(kwk_engine* e, const void* kernel, uint32_t tiles) {
+  static const void* keys[16];
+  static int vals[16];
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  for (int j = 0; j < 16 && keys[j]; ++j)
+    if (keys[j] == kernel) per_cu = vals[j];
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+    for (int j = 0; j < 16; ++j)
+      if (!keys[j]) { keys[j] = kernel; vals[j] = per_cu; break; }
+  }
   const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
   return tiles < g ? tiles : g;
 }
@@ -1927,20 +1969,27 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   }
 
   if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
-    const uint32_t K = 8 * e->q16, tile = kBlock * K;
+    // small engines (a node kind, the cache-resident configs) take 2048-word tiles so that
+    // the grid still spreads over every CU
+    uint32_t q16 = e->q16;
+    if (q16 > 1 && (e->n_active + kBlock * 8 * q16 - 1) / (kBlock * 8 * q16) < 4u * (uint32_t)e->n_cus) q16 = 1;
+    const uint32_t K = 8 * q16, tile = kBlock * K;
     const uint32_t tiles = (e->n_active + tile - 1) / tile;
     uint32_t blocks = tiles;
 #define LAUNCH16(HV, QV)                                                                                        \
   do {                                                                                                          \
-    if (!e->persist16) {                                                                                       \
+    const uint32_t pg = e->persist16 ? persist_grid(e, (const void*)sweep16_kernel<HV, QV, true>, tiles) : tiles; \
+    if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
       hipLaunchKernelGGL((sweep16_kernel<HV, QV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);       \
     } else {                                                                                                    \
-      blocks = persist_grid(e, (const void*)sweep16_kernel<HV, QV, true>, tiles);                              \
+      blocks = pg;                                                                                              \
       hipLaunchKernelGGL((sweep16_kernel<HV, QV, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);        \
     }                                                                                                           \
   } while (0)
-    if (e->q16 == 4) {
+    if (q16 == 4) {
       if (h) LAUNCH16(true, 4); else LAUNCH16(false, 4);
+    } else if (q16 == 1) {
+      if (h) LAUNCH16(true, 1); else LAUNCH16(false, 1);
     } else {
       if (h) LAUNCH16(true, 2); else LAUNCH16(false, 2);
     }
@@ -2032,6 +2081,7 @@ kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
   out->fired = h[1];
   out->bytes = h[2];
   for (int s = 0; s < KWK_MAX_STAGES; ++s) out->fired_per_stage[s] = h[3 + s];
+  out->line_bytes = h[kStatLine];
   out->state_bytes = word_bytes(e->fmt);
   return KWK_OK;
 }

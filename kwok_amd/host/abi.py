@@ -71,7 +71,8 @@ class FiredRec(C.Structure):
 
 class StepStats(C.Structure):
     _fields_ = [("steps", C.c_uint64), ("matched", C.c_uint64), ("fired", C.c_uint64), ("bytes", C.c_uint64),
-                ("fired_per_stage", C.c_uint64 * MAX_STAGES), ("state_bytes", C.c_uint64)]
+                ("fired_per_stage", C.c_uint64 * MAX_STAGES), ("state_bytes", C.c_uint64),
+                ("line_bytes", C.c_uint64)]
 
 
 class EngineDesc(C.Structure):

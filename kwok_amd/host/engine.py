@@ -199,7 +199,7 @@ class Engine:
         s = abi.StepStats()
         abi.check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
         return {"steps": s.steps, "matched": s.matched, "fired": s.fired, "bytes": s.bytes,
-                "state_bytes": s.state_bytes,
+                "state_bytes": s.state_bytes, "line_bytes": s.line_bytes,
                 "fired_per_stage": {self.p.names[i]: s.fired_per_stage[i] for i in range(len(self.p.names))}}
 
     def read(self, first: int = 0, n: Optional[int] = None):

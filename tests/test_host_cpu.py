@@ -48,7 +48,7 @@ def test_abi_struct_layout_matches_header():
     assert ctypes.sizeof(abi.Hot) == 16 and ctypes.sizeof(abi.Value) == 16
     assert ctypes.sizeof(abi.StageDesc) == 96 and ctypes.sizeof(abi.FiredRec) == 8
     assert ctypes.sizeof(abi.StageTable) == 32 + 32 * 96
-    assert ctypes.sizeof(abi.StepStats) == 8 * (4 + 32 + 1) and ctypes.sizeof(abi.EngineDesc) == 32
+    assert ctypes.sizeof(abi.StepStats) == 8 * (4 + 32 + 2) and ctypes.sizeof(abi.EngineDesc) == 32
 
 
 def test_engine_fails_loudly_without_gpu():

@@ -8,15 +8,14 @@ tail -2 $O/pytest_gpu.log
 run() {  # name, env assignments...   (BARGS: extra bench args)
   n=$1; shift
   env "$@" timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 40 $BARGS > $O/bench_$n.json 2> $O/bench_$n.err || { cat $O/bench_$n.err; exit 1; }
-  python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'))"
+  python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'), 'node_ms', d['detail']['node_kernel_ms_per_step'])"
 }
-run fsm_q2_persist KWOK_SWEEP_Q16=2
-run nofsm_q2_persist KWOK_SWEEP_Q16=2 KWOK_FSM=0
-run fsm_q2_tile KWOK_SWEEP_Q16=2 KWOK_SWEEP16_GRID=tile
-run fsm_q4_persist KWOK_SWEEP_Q16=4
+run q2_persist KWOK_SWEEP_Q16=2
+run q2_tile KWOK_SWEEP_Q16=2 KWOK_SWEEP16_GRID=tile
 for lib in kwok_amd/lib/variants/*.so; do
   [ -e "$lib" ] && run $(basename $lib .so) KWOK_ENGINE_LIB=$R/$lib
 done
 BARGS=--no-harness run idle_q2_persist KWOK_SWEEP_Q16=2
-run fsm_q2_persist_again KWOK_SWEEP_Q16=2
+BARGS="--config C3" run c3 KWOK_SWEEP_Q16=2 || true
+run q2_persist_again KWOK_SWEEP_Q16=2
 echo variants done

@@ -3,9 +3,9 @@
 FETCH_SIZE / WRITE_SIZE (KiB per dispatch) are summed over the PMC dimensions per dispatch.
 Only the pod engine's sweep launches count: in the churn run they are the harness
 instantiation (`<true`); in the no-harness run pods and nodes share one instantiation, so
-the pod launches are the large ones (>= 30 % of the largest dispatch; the node sweep moves
-~1 % of the pod sweep's bytes).  The first `skip` pod launches (warm-up transients: the
-initial pod-ready of every pod) are dropped.
+the pod launches are the large ones (>= 30 % of the largest steady-state dispatch; the node
+sweep moves ~1 % of the pod sweep's bytes).  The first `skip` launches (warm-up transients:
+the initial pod-ready of every pod) are dropped.
 
 The guide's x2 FETCH_SIZE correction is stated for 16-B-per-lane reads; it is checked here
 on the no-harness run, whose pod launches read exactly the state stream (bytes_per_launch of
@@ -25,7 +25,7 @@ CHURN = "<true"    # harness instantiation: pods only
 IDLE = "<false"    # pods and nodes
 
 
-def pod_dispatches(db, counter, tag, skip=3):
+def pod_dispatches(db, counter, tag, skip=3, shared=False):
     c = sqlite3.connect(db)
     per = defaultdict(float)
     for disp, name, cn, v in c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection"):
@@ -34,8 +34,11 @@ def pod_dispatches(db, counter, tag, skip=3):
     vals = [per[d] for d in sorted(per)]
     if not vals:
         raise SystemExit(f"{db}: no {counter} for sweep kernels {tag}")
-    big = max(vals)
-    vals = [v for v in vals if v >= 0.3 * big][skip:]
+    if shared:  # pods and nodes in one instantiation: the pod launches are the large ones
+        big = max(vals[skip:] or vals)
+        vals = [v for v in vals[skip:] if v >= 0.3 * big]
+    else:
+        vals = vals[skip:]
     return statistics.mean(vals), len(vals)
 
 
@@ -43,7 +46,7 @@ def main(d, out):
     bench_idle = json.loads(open(os.path.join(d, "bench_noharness.json")).read().strip().splitlines()[-1])
     bench = json.loads(open(os.path.join(d, "bench.json")).read().strip().splitlines()[-1])
     idle_bytes = bench_idle["roofline"]["bytes_per_launch"]
-    fi, ni = pod_dispatches(os.path.join(d, "pmc_fetch_idle", "run_results.db"), "FETCH_SIZE", IDLE)
+    fi, ni = pod_dispatches(os.path.join(d, "pmc_fetch_idle", "run_results.db"), "FETCH_SIZE", IDLE, shared=True)
     fh, nf = pod_dispatches(os.path.join(d, "pmc_fetch", "run_results.db"), "FETCH_SIZE", CHURN)
     wh, nw = pod_dispatches(os.path.join(d, "pmc_write", "run_results.db"), "WRITE_SIZE", CHURN)
     factor = idle_bytes / (fi * 1024.0)
