@@ -301,7 +301,8 @@ kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32
 kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);
 
 /* raw device pointers for in-process consumers (RCCL aggregates, profiling): state = the
- * {pred u32, sched u32} stream (8 bytes per slot) */
+ * state stream (kwk_step_stats.state_bytes per slot); fired / wave_counts = the sweep's
+ * internal fired segments and per-segment counts (valid after kwk_fired) */
 kwk_status kwk_device_ptrs(kwk_engine* eng, void** state, void** fired, void** wave_counts);
 
 /* HIP events recorded on the engine's stream (live kernel timing in bench.py) */

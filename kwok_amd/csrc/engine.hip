@@ -29,6 +29,9 @@
 #ifndef KWOK_EXP_NOFIRED
 #define KWOK_EXP_NOFIRED 0
 #endif
+#ifndef KWOK_EXP_NOSTAGECNT
+#define KWOK_EXP_NOSTAGECNT 0
+#endif
 // phase-2 state write-back with nontemporal stores (experiment)
 #ifndef KWOK_NT_STORE
 #define KWOK_NT_STORE 0
@@ -458,17 +461,26 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
 }
 
 // wave-ballot compaction of the fired set into the wave's private segment + per-stage counts
+// kPacked (2-byte sweep): 4-byte records {slot within the wave region: 11 bits, stage: 5,
+// flags: 3}, expanded to kwk_fired_rec by compact_fired_kernel (slot = segment * segment size
+// + index)
+template <bool kPacked = false>
 __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t lane, kwk_fired_rec* __restrict__ seg,
                                            uint32_t& seg_n, unsigned int* s_stat, uint32_t& n_bytes) {
   const unsigned long long bal = __ballot(f.fire);
   if (!bal) return;
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (!KWOK_EXP_NOFIRED) seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
-    n_bytes += 8;
+    if constexpr (kPacked) {
+      if (!KWOK_EXP_NOFIRED) reinterpret_cast<uint32_t*>(seg)[pos] = (uint32_t)i | f.stage << 11 | f.flags << 16;
+      n_bytes += 4;
+    } else {
+      if (!KWOK_EXP_NOFIRED) seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
+      n_bytes += 8;
+    }
   }
   seg_n += (uint32_t)__popcll(bal);
-  unsigned long long rest = bal;  // one LDS add per distinct fired stage in this wave-instruction
+  unsigned long long rest = KWOK_EXP_NOSTAGECNT ? 0ull : bal;  // one LDS add per distinct fired stage
   while (rest) {
     const uint32_t s = __shfl(f.stage, __ffsll((long long)rest) - 1);
     const unsigned long long same = __ballot(f.fire && f.stage == s);
@@ -851,9 +863,15 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 #ifndef KWOK_NT16
 #define KWOK_NT16 1  // phase-3 line stores with the nontemporal hint (r1y: 122 -> 119 us)
 #endif
+#ifndef KWOK_PF_LATE
+#define KWOK_PF_LATE 0
+#endif
 #ifndef KWOK_PF16
 #define KWOK_PF16 1  // tiles in flight per wave in the persistent grid (1 or 2)
 #endif
+template <int Q>
+constexpr uint32_t seg16_words() { return 64u * 8u * Q + 32u; }  // count + records + padding line
+#define kSeg16 seg16_words<Q>()
 template <bool kHarness, int Q, bool kPersist, int kDepth = KWOK_PF16>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
   constexpr int K = 8 * Q;                 // words per lane
@@ -933,7 +951,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
     const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
     uint32_t seg_n = 0;  // wave-uniform
     const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
-    kwk_fired_rec* __restrict__ seg = a.fired + seg_id * kWave;
+    // the (tile, wave) segment: [count][packed 4-byte records ...], kSeg16 words apart; its
+    // used part is padded to whole 128-byte lines (HBM3E has no write mask: a partial line
+    // costs a read-modify-write), the count lives in the segment's first line
+    uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * kSeg16;
+    kwk_fired_rec* __restrict__ seg = reinterpret_cast<kwk_fired_rec*>(seg32 + 1);
 
     // ---- phase 1: idle test on the raw words.  bit k = q * 8 + h of a lane's masks
     uint32_t in_range = 0xFFFFFFFFu >> (32 - K);
@@ -998,33 +1020,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
     uint4 cur[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) cur[q] = v[q];
-    if (kPersist) issue_tile(v, tile + kDepth * gridDim.x);  // refill this buffer
+    // refill this buffer.  KWOK_PF_LATE: only after phase 2, whose table lookups would
+    // otherwise wait for it (vmcnt retires in issue order)
+    if (kPersist && (!KWOK_PF_LATE || !n_work)) issue_tile(v, tile + kDepth * gridDim.x);
 
     if (n_work) {
       // ---- phase 2
 #pragma unroll
       for (int q = 0; q < Q; ++q) tq[q * 64 + lane] = cur[q];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      for (uint32_t c = 0; c < n_work; c += 64) {
-        const uint32_t j = c + lane;
+      // Software-pipelined passes of 64 work items: the next pass's work-list / tile reads and
+      // table lookup are issued before this pass's stores (fired records, due), so waiting
+      // for the lookup does not wait for those stores (vmcnt counts loads and stores in issue
+      // order).
+      auto fetch = [&](const uint32_t c, uint32_t& we, uint32_t& raw, uint32_t& ent) {
+        we = (c + lane < n_work) ? (uint32_t)wl[c + lane] : 0xFFFFFFFFu;
+        raw = we != 0xFFFFFFFFu ? (uint32_t)tw[we & 0x7FFFu] : 0u;
+        ent = (we != 0xFFFFFFFFu && a.fsm) ? a.fsm[((we >> 15) << a.fsm_bits) | raw] : kFsmGeneral;
+      };
+      uint32_t we, raw, ent;
+      fetch(0, we, raw, ent);
+      for (uint32_t c = 0; c < n_work; c += 64u) {
+        const uint32_t cwe = we, craw = raw, e = ent;
+        if (c + 64u < n_work) fetch(c + 64u, we, raw, ent);  // wave-uniform
         Fire f{false, 0, 0, 0};
         uint64_t i = 0;
-        if (j < n_work) {
-          const uint32_t we = wl[j];
-          const uint32_t w = we & 0x7FFFu, rdy = we >> 15;  // slot in the wave region, due ready
+        if (cwe != 0xFFFFFFFFu) {
+          const uint32_t w = cwe & 0x7FFFu, rdy = cwe >> 15;  // slot in the wave region, due ready
           i = wbase + w;
-          const uint32_t raw = tw[w];
-          const uint32_t e = a.fsm ? a.fsm[(rdy << a.fsm_bits) | raw] : kFsmGeneral;
           if (!(e & kFsmGeneral)) {  // the word's transition, precomputed by fsm_build_kernel
             tw[w] = (uint16_t)e;
-            if (e & kFsmDue) a.due[i] = sat_add(a.now, a.fsm_due[(rdy << a.fsm_bits) | raw]);
+            if (e & kFsmDue) a.due[i] = sat_add(a.now, a.fsm_due[(rdy << a.fsm_bits) | craw]);
             f.fire = (e >> 21) & 1u;
             f.stage = (e >> 16) & 31u;
             f.flags = (e >> 22) & 7u;
             f.bytes = ((e >> 26) & 15u) * 2u;
             n_matched += (e >> 25) & 1u;
           } else {
-            const uint2 s = fmt_unpack(raw, fmt);
+            const uint2 s = fmt_unpack(craw, fmt);
             const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;  // counted in phase 1
             uint32_t gen_unused = 0;
             int64_t due_unused = 0;
@@ -1032,11 +1065,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
                                                          n_matched, s_lut, lut_n, gen_unused, due_unused);
             tw[w] = (uint16_t)fmt_pack(nv.x, nv.y, fmt);
           }
+          n_line -= 2u;  // the word's own write is replaced by the line stores below
         }
         n_bytes += f.bytes;
-        n_line -= j < n_work ? 2u : 0u;  // the word's own write is replaced by the line stores below
-        emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
+        emit_fired<true>(f, i - wbase, lane, seg, seg_n, s_stat, n_bytes);
       }
+      if (kPersist && KWOK_PF_LATE) issue_tile(v, tile + kDepth * gridDim.x);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       // ---- phase 3: whole 128-byte lines wherever a word changed
 #pragma unroll
@@ -1059,7 +1093,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
       // the next tile reuses this wave's LDS lists and tile
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (lane == 0) a.wave_counts[seg_id] = seg_n;
+    {
+      const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
+      for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
+      if (lane == 0) seg32[0] = seg_n;
+      n_line += 4u * (uint32_t)__popc((uint32_t)(lane < end - used));  // padding: line bytes only
+    }
     wave_fired += seg_n;
     n_bytes += lane == 0 ? 4u : 0u;  // the fired count word
   };
@@ -1093,14 +1132,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
   }
 }
 
+// per-wave fired counts of the 2-byte sweep (the first word of each segment) for the scan
+__global__ void seg_counts_kernel(const uint32_t* __restrict__ fired32, uint32_t n_waves, uint32_t stride,
+                                  uint32_t* __restrict__ counts) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < n_waves) counts[w] = fired32[(uint64_t)w * stride];
+}
+
 // gather the per-wave fired segments into one dense list (offsets from an exclusive scan)
 __global__ void compact_fired_kernel(const kwk_fired_rec* __restrict__ fired, const uint32_t* __restrict__ counts,
                                      const uint32_t* __restrict__ offsets, uint32_t n_waves, uint32_t wave_seg,
-                                     kwk_fired_rec* __restrict__ out) {
+                                     uint32_t packed, kwk_fired_rec* __restrict__ out) {
   const uint32_t w = blockIdx.x;
   if (w >= n_waves) return;
   const uint32_t c = counts[w];
   const uint32_t o = offsets[w];
+  if (packed) {  // 2-byte sweep: segment w = [count][emit_fired<true> records] at w * (wave_seg + 32)
+                 // words, covering slots w * wave_seg + [0, wave_seg)
+    const uint32_t* f32 = reinterpret_cast<const uint32_t*>(fired) + (uint64_t)w * (wave_seg + 32u) + 1u;
+    for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) {
+      const uint32_t r = f32[j];
+      out[o + j] = kwk_fired_rec{w * wave_seg + (r & 0x7FFu), (uint16_t)((r >> 11) & 31u), (uint16_t)((r >> 16) & 7u)};
+    }
+    return;
+  }
   for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) out[o + j] = fired[(uint64_t)w * wave_seg + j];
 }
 
@@ -1443,6 +1498,7 @@ struct kwk_engine {
   uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 8 | 16 | 32)
   uint32_t objs_narrow = 16;
   uint32_t last_objs = 16;
+  bool last_packed = false;   // fired segments hold 4-byte records (2-byte sweep)
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
@@ -1995,6 +2051,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     }
 #undef LAUNCH16
     e->last_objs = K;
+    e->last_packed = true;
     HIP_TRY(hipGetLastError());
     e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
     e->last_grid = blocks;
@@ -2022,6 +2079,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   }
 #undef LAUNCH
   e->last_objs = K;
+  e->last_packed = false;
   HIP_TRY(hipGetLastError());
   e->last_blocks = blocks;
   ++e->steps;
@@ -2049,6 +2107,12 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
   HIP_TRY(hipMemsetAsync(e->d_wave_counts + n_waves, 0, sizeof(uint32_t), e->stream));
+  if (e->last_packed) {
+    hipLaunchKernelGGL(seg_counts_kernel, dim3((n_waves + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
+                       reinterpret_cast<const uint32_t*>(e->d_fired), n_waves, 64u * e->last_objs + 32u,
+                       e->d_wave_counts);
+    HIP_TRY(hipGetLastError());
+  }
   size_t tmp = e->scan_tmp_bytes;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->d_scan_tmp, tmp, e->d_wave_counts, e->d_wave_offsets,
                                            (int)(n_waves + 1), e->stream));
@@ -2059,7 +2123,7 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (!out || total == 0) return KWK_OK;
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
   hipLaunchKernelGGL(compact_fired_kernel, dim3(n_waves), dim3(64), 0, e->stream, e->d_fired, e->d_wave_counts,
-                     e->d_wave_offsets, n_waves, 64u * e->last_objs, e->d_compact);
+                     e->d_wave_offsets, n_waves, 64u * e->last_objs, e->last_packed ? 1u : 0u, e->d_compact);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
