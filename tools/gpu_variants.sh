@@ -13,13 +13,12 @@ run() {  # name, env assignments...   (BARGS: extra bench args)
   python -c "import json; d=json.loads(open('$O/bench_$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', '%.4g'%d['value'], r['avg_launch_us'], r['achieved'], r['bytes_per_launch'], r.get('state_bytes_per_object'), 'node_ms', d['detail']['node_kernel_ms_per_step'])"
 }
 run q2_persist KWOK_SWEEP_Q16=2
-run q1_persist KWOK_SWEEP_Q16=1
-run q1_tile KWOK_SWEEP_Q16=1 KWOK_SWEEP16_GRID=tile
 for lib in kwok_amd/lib/variants/*.so; do
   [ -e "$lib" ] && run $(basename $lib .so) KWOK_ENGINE_LIB=$R/$lib
 done
+for lib in kwok_amd/lib/variants/*.so; do
+  [ -e "$lib" ] && BARGS=--no-harness run idle_$(basename $lib .so) KWOK_ENGINE_LIB=$R/$lib
+done
 BARGS=--no-harness run idle_q2_persist KWOK_SWEEP_Q16=2
-BARGS=--no-harness run idle_q1_persist KWOK_SWEEP_Q16=1
-BARGS=--no-harness run idle_q1_tile KWOK_SWEEP_Q16=1 KWOK_SWEEP16_GRID=tile
 run q2_persist_again KWOK_SWEEP_Q16=2
 echo variants done
