@@ -209,6 +209,26 @@ kwk_status kwk_set_records(kwk_engine* eng, uint32_t first, uint32_t n, const kw
 /* Deleted events: clear ALIVE (cancels any pending stage) */
 kwk_status kwk_delete(kwk_engine* eng, uint32_t n, const uint32_t* slots);
 
+/* Failed playStage with a retryable error (shouldRetry, pkg/kwok/controllers/utils.go:146-160):
+ * the object did not change in the apiserver, so the device state the fire produced is replaced
+ * by the host's unchanged row (`hot`, `cls`: what kwk_upsert would take, without a re-match) and
+ * the same stage is queued again after backoffDelayByStep(retry_count, backoff)
+ * (utils.go:138-143: min(duration * factor^steps, cap), then wait.Jitter(d, jitter) with
+ * rand.Float64 from the Philox hook, site 4), as playStageWorker does
+ * (pod_controller.go:257-285, node_controller.go / stage_controller.go alike; the retry's
+ * queue weight 1 only orders jobs due at the same instant, which one device step fires
+ * together).  retry_count[j] = the job's RetryCount before the increment (0 on the first
+ * retry).  Go's math.Pow is restated for integer exponents (exact). */
+typedef struct {
+  int64_t duration_ns;   /* wait.Backoff.Duration (defaultBackoff, utils.go:133-135: 1 s) */
+  double factor;         /* Factor (2.0) */
+  double jitter;         /* Jitter (0.2; <= 0 means 1.0, as wait.Jitter) */
+  int64_t cap_ns;        /* Cap (32 min) */
+} kwk_backoff;
+kwk_status kwk_retry(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n, const uint32_t* slots,
+                     const kwk_hot* hot, const uint16_t* cls, const uint16_t* stages, const uint32_t* retry_count,
+                     const kwk_backoff* backoff);
+
 /* one reconciliation step at time now_ns over slots [0, n_active):
  * harness -> match dirty objects -> fire due objects -> apply deltas.
  * Random draws use Philox4x32-10(key = seed ^ kind_salt, ctr = (slot_base+slot, step, site)). */

@@ -101,7 +101,7 @@ __device__ __forceinline__ double rng_float64(uint64_t gslot, uint64_t step, uin
   return (double)(philox_u64(gslot, step, site, key) >> 11) * 0x1.0p-53;
 }
 
-constexpr uint32_t kSitePick = 1, kSiteJitter = 2, kSiteLeaseJitter = 3;
+constexpr uint32_t kSitePick = 1, kSiteJitter = 2, kSiteLeaseJitter = 3, kSiteRetryJitter = 4;
 
 __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
   int64_t r;
@@ -1203,6 +1203,78 @@ __global__ void scatter_kernel(ScatterArgs a) {
   a.rec_idx[i] = a.s_rec[j];
 }
 
+// Go's math.Pow(x, y) for a non-negative integer y (src/math/pow.go: frexp, then repeated
+// squaring of the mantissa with a separate binary exponent, Ldexp at the end), so the
+// backoff matches the reference bit for bit
+__device__ __forceinline__ double go_pow_int(double x, uint64_t n) {
+  if (n == 0 || x == 1.0) return 1.0;
+  if (n == 1) return x;
+  if (x == 0.0 || isinf(x) || isnan(x)) return pow(x, (double)n);
+  double a1 = 1.0;
+  int ae = 0;
+  int xe;
+  double x1 = frexp(x, &xe);
+  for (uint64_t i = n; i != 0; i >>= 1) {
+    if (xe < -(1 << 12) || (1 << 12) < xe) {  // catastrophic overflow: let Ldexp handle it
+      ae += xe;
+      break;
+    }
+    if (i & 1) {
+      a1 *= x1;
+      ae += xe;
+    }
+    x1 *= x1;
+    xe <<= 1;
+    if (x1 < 0.5) {
+      x1 += x1;
+      xe--;
+    }
+  }
+  return ldexp(a1, ae);
+}
+
+// float64 -> time.Duration (int64) as Go converts it on amd64: truncation, out of range ->
+// INT64_MIN
+__device__ __forceinline__ int64_t go_duration(double d) {
+  if (!(d > -9223372036854775808.0 && d < 9223372036854775808.0)) return INT64_MIN;
+  return (int64_t)d;
+}
+
+struct RetryArgs {
+  void* st;
+  StateFmt fmt;
+  int64_t* due;
+  const uint32_t* slots;
+  const kwk_hot* hot;
+  const uint16_t* cls;
+  const uint16_t* stages;
+  const uint32_t* retry_count;
+  kwk_backoff b;
+  uint32_t n;
+  uint64_t slot_base;
+  uint64_t key;
+  uint64_t step;
+  int64_t now;
+};
+
+// kwk_retry: playStageWorker's retry branch (pod_controller.go:273-284) for each failed job
+__global__ void retry_kernel(RetryArgs a) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.n) return;
+  const uint32_t i = a.slots[j];
+  // backoffDelayByStep (utils.go:138-143)
+  const double d = fmin((double)a.b.duration_ns * go_pow_int(a.b.factor, a.retry_count[j]), (double)a.b.cap_ns);
+  const int64_t base = go_duration(d);
+  const double mf = a.b.jitter <= 0.0 ? 1.0 : a.b.jitter;
+  const double u = rng_float64(a.slot_base + i, a.step, kSiteRetryJitter, a.key);
+  const int64_t delay = base + go_duration(u * mf * (double)base);
+  // the unchanged object, its job queued again (no event: not dirty)
+  const uint32_t sched = (a.hot[j].sched & ~(KWK_CLASS_MASK | 0xFFu | KWK_F_DIRTY)) |
+                         ((uint32_t)a.cls[j] << KWK_CLASS_SHIFT) | (uint32_t)a.stages[j];
+  store_state(a.st, i, make_uint2(a.hot[j].pred, sched), a.fmt);
+  a.due[i] = sat_add(a.now, delay);  // addStageJob -> AddWeightAfter(job, 1, retryDelay)
+}
+
 __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uint32_t n) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
@@ -1905,6 +1977,42 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
   HIP_TRY(hipMemcpy(e->d_stage_buf, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_st,
                      e->fmt, (const uint32_t*)e->d_stage_buf, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_retry(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n, const uint32_t* slots,
+                     const kwk_hot* hot, const uint16_t* cls, const uint16_t* stages, const uint32_t* retry_count,
+                     const kwk_backoff* backoff) {
+  if (!e || !backoff || (n && (!slots || !hot || !cls || !stages || !retry_count)))
+    return fail(KWK_EINVAL, "null argument");
+  if (n == 0) return KWK_OK;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (slots[j] >= e->n_active) return fail(KWK_EINVAL, "slot not active");
+    if (stages[j] >= e->n_stages) return fail(KWK_EINVAL, "stage out of range");
+    if (e->loaded_table && cls[j] >= e->n_classes) return fail(KWK_EINVAL, "class out of range");
+    if (!(hot[j].sched & KWK_F_ALIVE)) return fail(KWK_EINVAL, "retried object must be alive");
+    if (!fits_fmt(e->fmt, e->n_stages, hot[j].pred, stages[j])) return fail(KWK_EINVAL, "pred bits beyond the stage table");
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  const size_t bytes = (size_t)n * (4 + sizeof(kwk_hot) + 2 + 2 + 4) + 64;
+  if (kwk_status st = ensure_stage_buf(e, bytes)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  char* p = (char*)e->d_stage_buf;
+  kwk_hot* s_hot = (kwk_hot*)p; p += sizeof(kwk_hot) * n;
+  uint32_t* s_slots = (uint32_t*)p; p += 4 * (size_t)n;
+  uint32_t* s_rc = (uint32_t*)p; p += 4 * (size_t)n;
+  uint16_t* s_cls = (uint16_t*)p; p += 2 * (size_t)n;
+  uint16_t* s_stg = (uint16_t*)p;
+  HIP_TRY(hipMemcpy(s_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_rc, retry_count, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_stg, stages, 2 * (size_t)n, hipMemcpyHostToDevice));
+  RetryArgs a{e->d_st, e->fmt, e->d_due, s_slots, s_hot, s_cls, s_stg, s_rc, *backoff, n, e->slot_base,
+              seed ^ ((uint64_t)e->kind_salt << 32), step, now_ns};
+  hipLaunchKernelGGL(retry_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;

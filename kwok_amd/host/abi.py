@@ -109,6 +109,14 @@ HOT_DTYPE = np.dtype([("pred", "<u4"), ("sched", "<u4"), ("due", "<i8")])
 VALUE_DTYPE = np.dtype([("value", "<i8"), ("nsec", "<i4"), ("kind", "<i4")])
 FIRED_DTYPE = np.dtype([("slot", "<u4"), ("stage", "<u2"), ("flags", "<u2")])
 
+
+class Backoff(C.Structure):
+    """kwk_backoff = wait.Backoff; default = defaultBackoff (controllers/utils.go:133-135)."""
+    _fields_ = [("duration_ns", C.c_int64), ("factor", C.c_double), ("jitter", C.c_double), ("cap_ns", C.c_int64)]
+
+
+DEFAULT_BACKOFF = dict(duration_ns=10**9, factor=2.0, jitter=0.2, cap_ns=32 * 60 * 10**9)
+
 assert C.sizeof(Hot) == 16 and C.sizeof(Value) == 16 and C.sizeof(StageDesc) == 96
 assert C.sizeof(Lease) == 32 == LEASE_DTYPE.itemsize and C.sizeof(LeaseParams) == 32
 assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.itemsize == 8
@@ -120,7 +128,7 @@ EXPORTS = [
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
-    "kwk_usage_read_pods",
+    "kwk_usage_read_pods", "kwk_retry",
 ]
 
 _lib = None
@@ -153,6 +161,8 @@ def lib():
     L.kwk_upsert.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_retry.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
+                            C.c_void_p, C.c_void_p, C.c_void_p, _p(Backoff)]
     L.kwk_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_match.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_fired.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]

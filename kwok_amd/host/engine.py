@@ -176,6 +176,18 @@ class Engine:
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
         abi.check(abi.lib().kwk_delete(self.h, len(slots), abi.ptr(slots)), "kwk_delete")
 
+    def retry(self, now_ns: int, seed: int, step: int, slots, hot, cls, stages, retry_count, backoff=None):
+        """kwk_retry: re-queue failed playStage jobs (pod_controller.go:273-284) with the
+        host's unchanged rows (`hot` / `cls` as Ingest.columns gives them)."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        hot = np.ascontiguousarray(hot, dtype=abi.HOT_DTYPE)
+        cls = np.ascontiguousarray(cls, dtype=np.uint16)
+        stages = np.ascontiguousarray(stages, dtype=np.uint16)
+        rc = np.ascontiguousarray(retry_count, dtype=np.uint32)
+        b = abi.Backoff(**(backoff or abi.DEFAULT_BACKOFF))
+        abi.check(abi.lib().kwk_retry(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(hot), abi.ptr(cls),
+                                      abi.ptr(stages), abi.ptr(rc), C.byref(b)), "kwk_retry")
+
     def step(self, now_ns: int, seed: int, step: int):
         abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
