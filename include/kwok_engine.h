@@ -297,6 +297,7 @@ typedef struct {
 #define KWK_LEASE_OP_RENEW 2    /* renewLease by the holder (:252-275) */
 #define KWK_LEASE_OP_ACQUIRE 3  /* renewLease taking over an absent or expired holder (transitions + 1) */
 #define KWK_LEASE_OP_BUSY 4     /* held by another holder: no write, retried after interval() */
+#define KWK_LEASE_OP_FAILED 5   /* set by kwk_lease_fail: the write was rejected, retried after interval() */
 
 typedef struct {
   uint64_t steps, creates, renews, acquires, busy;
@@ -310,6 +311,14 @@ kwk_status kwk_lease_set(kwk_engine* nodes, uint32_t first, uint32_t n, const kw
 kwk_status kwk_lease_step(kwk_engine* nodes, int64_t now_ns, uint64_t seed, uint64_t step);
 kwk_status kwk_lease_ops(kwk_engine* nodes, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 kwk_status kwk_lease_read(kwk_engine* nodes, uint32_t first, uint32_t n, kwk_lease* out);
+/* Lease writes of the last kwk_lease_step that the apiserver rejected (syncWorker's err
+ * branch, node_lease_controller.go:121-128): `old` = the lease the informer still holds; the
+ * device restores it (keeping HOLD / QUEUED), queues the retry after the same interval() draw
+ * (AddWeightAfter(node, 1, dur)), sets the node's MANAGED bit from Held() of the restored lease
+ * and drops the re-match the write would have caused; kwk_lease_sync_pods then applies
+ * MANAGED to the node's pods without a resync.  Call before kwk_lease_sync_pods / kwk_step. */
+kwk_status kwk_lease_fail(kwk_engine* nodes, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n,
+                          const uint32_t* slots, const kwk_lease* old);
 kwk_status kwk_lease_stats(kwk_engine* nodes, kwk_lease_counters* out);
 /* pods of the nodes synced by the last lease step (node j owns pod slots [node_ptr[j],
  * node_ptr[j+1])): MANAGED follows Held(), a successful sync re-matches pods with no queued

@@ -1427,6 +1427,8 @@ __global__ void usage_total_kernel(const double* __restrict__ part, uint32_t n_b
 // the node's MANAGED bit follows Held() (readOnlyFunc, controller.go:285-288) and a
 // successful sync re-matches a node with no queued stage (onNodeManaged -> ManageNode,
 // controller.go:276-279, 307-329; preprocess skips nodes whose queued job is current).
+constexpr uint32_t kLeaseOpSetDirty = 0x80u;  // per-node op byte: this sync set the node's DIRTY bit
+
 struct LeaseArgs {
   kwk_lease* __restrict__ lease;
   uint8_t* __restrict__ op;          // per node: KWK_LEASE_OP_* of this step (0 = no sync)
@@ -1502,19 +1504,25 @@ __global__ __launch_bounds__(kBlock) void lease_kernel(LeaseArgs a) {
       }
       L.next_try_ns = next <= 0 ? a.now : sat_add(a.now, next);
       a.lease[i] = L;
+      uint32_t set_dirty = 0;  // kwk_lease_fail undoes exactly this re-match
       if (a.cfg.manage_nodes) {
         uint2 s = load_state(a.st, i, a.fmt);
         const bool held = (L.flags & KWK_LEASE_EXISTS) && (L.flags & KWK_LEASE_HOLDER) && L.holder == me;
         if (held) {
           s.y |= KWK_F_MANAGED;
-          if (ok && (s.y & KWK_F_ALIVE) && (s.y & 0xFFu) == KWK_STAGE_NONE) s.y |= KWK_F_DIRTY;
+          if (ok && (s.y & KWK_F_ALIVE) && (s.y & 0xFFu) == KWK_STAGE_NONE && !(s.y & KWK_F_DIRTY)) {
+            s.y |= KWK_F_DIRTY;
+            set_dirty = kLeaseOpSetDirty;
+          }
         } else {
           s.y &= ~KWK_F_MANAGED;
         }
         store_state(a.st, i, s, a.fmt);
       }
+      a.op[i] = (uint8_t)(op | set_dirty);
+    } else {
+      a.op[i] = 0;
     }
-    a.op[i] = (uint8_t)op;
   }
   // API writes of this step, compacted per wave (one atomic per wave), and counters
   const unsigned long long bal = __ballot(op != 0);
@@ -1540,11 +1548,11 @@ __global__ __launch_bounds__(kBlock) void lease_pods_kernel(void* __restrict__ s
                                                             uint32_t n_nodes) {
   const uint32_t node = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (node >= n_nodes) return;
-  const uint32_t o = op[node];
+  const uint32_t o = op[node] & 0x7Fu;
   if (o == 0) return;
   const kwk_lease L = lease[node];
   const bool held = (L.flags & KWK_LEASE_EXISTS) && (L.flags & KWK_LEASE_HOLDER) && L.holder == me;
-  const bool ok = o != KWK_LEASE_OP_BUSY;
+  const bool ok = o != KWK_LEASE_OP_BUSY && o != KWK_LEASE_OP_FAILED;
   for (uint32_t p = node_ptr[node] + (threadIdx.x & 63); p < node_ptr[node + 1]; p += 64) {
     uint2 s = load_state(st, p, fmt);
     if (held) {
@@ -1554,6 +1562,34 @@ __global__ __launch_bounds__(kBlock) void lease_pods_kernel(void* __restrict__ s
       s.y &= ~KWK_F_MANAGED;
     }
     store_state(st, p, s, fmt);
+  }
+}
+
+// kwk_lease_fail: syncWorker's error branch (node_lease_controller.go:121-128) for lease writes
+// the apiserver rejected: the informer still shows the old lease (the controller flags HOLD /
+// QUEUED stay), the sync is retried after the same interval() draw, and the node's MANAGED bit
+// follows Held() of the restored lease without the re-match the write would have caused.
+__global__ void lease_fail_kernel(LeaseArgs a, const uint32_t* __restrict__ slots, const kwk_lease* __restrict__ old,
+                                  uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = slots[j];
+  const uint32_t ctl = a.lease[i].flags & (KWK_LEASE_HOLD | KWK_LEASE_QUEUED);
+  kwk_lease L = old[j];
+  L.flags = (L.flags & ~(KWK_LEASE_HOLD | KWK_LEASE_QUEUED)) | ctl;
+  const double factor = a.cfg.renew_jitter <= 0.0 ? 1.0 : a.cfg.renew_jitter;
+  const double u = rng_float64(a.slot_base + i, a.step, kSiteLeaseJitter, a.key);
+  const int64_t dur = a.cfg.renew_interval_ns + (int64_t)(u * factor * (double)a.cfg.renew_interval_ns);
+  L.next_try_ns = sat_add(a.now, dur);  // AddWeightAfter(nodeName, 1, dur)
+  a.lease[i] = L;
+  const uint32_t prev = a.op[i];
+  a.op[i] = (uint8_t)KWK_LEASE_OP_FAILED;
+  if (a.cfg.manage_nodes) {
+    uint2 s = load_state(a.st, i, a.fmt);
+    if (prev & kLeaseOpSetDirty) s.y &= ~KWK_F_DIRTY;
+    const bool held = (L.flags & KWK_LEASE_EXISTS) && (L.flags & KWK_LEASE_HOLDER) && L.holder == a.cfg.holder_id;
+    s.y = held ? (s.y | KWK_F_MANAGED) : (s.y & ~KWK_F_MANAGED);
+    store_state(a.st, i, s, a.fmt);
   }
 }
 
@@ -2445,6 +2481,40 @@ kwk_status kwk_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t
   a.cfg = e->lease_cfg;
   hipLaunchKernelGGL(lease_kernel, dim3((e->n_active + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
+kwk_status kwk_lease_fail(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n, const uint32_t* slots,
+                          const kwk_lease* old) {
+  if (!e || (n && (!slots || !old))) return fail(KWK_EINVAL, "null argument");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if (n == 0) return KWK_OK;
+  for (uint32_t j = 0; j < n; ++j)
+    if (slots[j] >= e->n_active) return fail(KWK_EINVAL, "slot not active");
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = ensure_stage_buf(e, (size_t)n * (4 + sizeof(kwk_lease)) + 64)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  kwk_lease* s_old = (kwk_lease*)e->d_stage_buf;
+  uint32_t* s_slots = (uint32_t*)((char*)e->d_stage_buf + sizeof(kwk_lease) * n);
+  HIP_TRY(hipMemcpy(s_old, old, sizeof(kwk_lease) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  LeaseArgs a;
+  a.lease = e->d_lease;
+  a.op = e->d_lease_op;
+  a.st = e->d_st;
+  a.ops = e->d_lease_ops;
+  a.n_ops = e->d_lease_nops;
+  a.stats = e->d_lease_stats;
+  a.fmt = e->fmt;
+  a.n = e->n_active;
+  a.slot_base = e->slot_base;
+  a.key = seed ^ ((uint64_t)e->kind_salt << 32);
+  a.step = step;
+  a.now = now_ns;
+  a.cfg = e->lease_cfg;
+  hipLaunchKernelGGL(lease_fail_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, s_slots, s_old, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 

@@ -128,7 +128,7 @@ EXPORTS = [
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
-    "kwk_usage_read_pods", "kwk_retry",
+    "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail",
 ]
 
 _lib = None
@@ -184,6 +184,7 @@ def lib():
     L.kwk_lease_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_lease_ops.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
     L.kwk_lease_read.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.kwk_lease_fail.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
     L.kwk_lease_stats.argtypes = [C.c_void_p, _p(LeaseCounters)]
     L.kwk_lease_sync_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_abi_version.restype = C.c_uint32

@@ -290,6 +290,14 @@ class Engine:
         abi.check(abi.lib().kwk_lease_read(self.h, first, n, abi.ptr(out)), "kwk_lease_read")
         return out
 
+    def lease_fail(self, now_ns: int, seed: int, step: int, slots, old: np.ndarray):
+        """kwk_lease_fail: the apiserver rejected these nodes' lease writes of the last lease
+        step; `old` = the leases the informer still holds."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        old = np.ascontiguousarray(old, dtype=abi.LEASE_DTYPE)
+        abi.check(abi.lib().kwk_lease_fail(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(old)),
+                  "kwk_lease_fail")
+
     def lease_stats(self) -> dict:
         c = abi.LeaseCounters()
         abi.check(abi.lib().kwk_lease_stats(self.h, C.byref(c)), "kwk_lease_stats")

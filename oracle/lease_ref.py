@@ -13,7 +13,8 @@ CPU restatement of KWOK's node-lease controller, the checker for the device's le
 
 rand.Float64 is replaced by the same Philox hook as the device (site 3, (u64 >> 11) * 2^-53).
 The apiserver round trip returns renewTime as a metav1.MicroTime, i.e. truncated to
-microseconds.  API writes always succeed here (retry paths are out of scope).
+microseconds.  A rejected write (LeaseSim.fail) is syncWorker's err branch (:121-128):
+the informer keeps the old lease and the sync is retried after the same interval() draw.
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ from typing import List, Optional, Tuple
 from . import refcpu
 
 EXISTS, HOLDER, DURATION, RENEW, HOLD, QUEUED = 1, 2, 4, 8, 16, 32
-OP_CREATE, OP_RENEW, OP_ACQUIRE, OP_BUSY = 1, 2, 3, 4
+OP_CREATE, OP_RENEW, OP_ACQUIRE, OP_BUSY, OP_FAILED = 1, 2, 3, 4, 5
 SITE_LEASE_JITTER = 3
 SEC = 10**9
 INT64_MAX = (1 << 63) - 1
@@ -141,3 +142,15 @@ class LeaseSim:
             L.next_try_ns = now_ns if nxt <= 0 else sat_add(now_ns, nxt)
             out.append((i, op))
         return out
+
+    def fail(self, i: int, old: Lease, now_ns: int, seed: int, step: int):
+        """syncWorker's err branch (node_lease_controller.go:121-128): the write of the sync
+        that ran at (now_ns, step) was rejected; the cached lease stays `old`, the controller's
+        hold / queue flags stay, AddWeightAfter(node, 1, dur) with the same dur."""
+        key = seed ^ (self.kind_salt << 32)
+        dur = jitter(self.renew_interval, self.jitter, float64_hook(key, self.slot_base + i, step))
+        ctl = self.leases[i].flags & (HOLD | QUEUED)
+        L = replace(old)
+        L.flags = (L.flags & ~(HOLD | QUEUED)) | ctl
+        L.next_try_ns = sat_add(now_ns, dur)
+        self.leases[i] = L

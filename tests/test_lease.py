@@ -221,3 +221,61 @@ def test_c3_nodes_leases_pods_parity(state):
     finally:
         neng.close()
         peng.close()
+
+
+@pytest.mark.gpu
+def test_c3_lease_write_failures_parity():
+    """The C3 loop with every fourth lease write rejected by the apiserver (kwk_lease_fail,
+    syncWorker's err branch node_lease_controller.go:121-128): restored lease, retry after the
+    same interval() draw, MANAGED from Held() of the old lease, no re-match; bit-exact with
+    the oracle at every step."""
+    from dataclasses import replace
+    from kwok_amd.host import abi
+    from tests.parity_util import NOW0, build, compare_state
+    rng = np.random.default_rng(34)
+    n_nodes, ppn = 64, 3
+    nodes = [W.node_object(f"node-{i}") for i in range(n_nodes)]
+    pods = [W.pod_object(f"pod-{i}", f"node-{i // ppn}", job=(i % 10 == 0)) for i in range(n_nodes * ppn)]
+    node_ptr = np.arange(0, n_nodes * ppn + 1, ppn, dtype=np.uint32)
+    leases = c3_leases(n_nodes, NOW0, rng)
+    me = 1
+    nprog, neng, nsim = build(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), nodes, kind_salt=1)
+    pprog, peng, psim = build(W.stage_paths(W.POD_FAST), pods, harness=True)
+    try:
+        neng.lease_config(me, 40, 10 * 10**9, 0.04)
+        neng.lease_set(to_array(leases))
+        lsim = LR.LeaseSim(leases, me, 40, 10 * 10**9, 0.04, kind_salt=1)
+        seed = 0x78
+        n_failed = 0
+        for k in range(160):
+            now = NOW0 + k * 250 * 10**6
+            before = [replace(L) for L in lsim.leases]
+            neng.lease_step(now, seed, k)
+            ops = lsim.step(now, seed, k)
+            assert sorted((int(r["slot"]), int(r["stage"])) for r in neng.lease_ops()) == sorted(ops), f"step {k}"
+            writes = sorted(i for i, op in ops if op != LR.OP_BUSY)
+            failed = writes[k % 4::4]
+            if failed:
+                neng.lease_fail(now, seed, k, failed, to_array([before[i] for i in failed]))
+                for i in failed:
+                    lsim.fail(i, before[i], now, seed, k)
+                n_failed += len(failed)
+            assert_leases_equal(neng.lease_read(), lsim.leases, k)
+            for i, op in ops:
+                h = LR.held(lsim.leases[i], me)
+                resync = op != LR.OP_BUSY and i not in failed
+                nsim.set_managed(i, h, resync)
+                for p in range(node_ptr[i], node_ptr[i + 1]):
+                    psim.set_managed(p, h, resync)
+            neng.lease_sync_pods(peng, node_ptr)
+            for eng, sim, prog in ((neng, nsim, nprog), (peng, psim, pprog)):
+                eng.step(now, seed, k)
+                got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
+                assert got == sorted(sim.step(now, seed, k)), f"step {k}"
+                compare_state(prog, eng, sim, k)
+                hot, _ = eng.read()
+                assert [bool(x & abi.F_MANAGED) for x in hot["sched"]] == sim.managed, f"step {k}: managed"
+        assert n_failed > 10
+    finally:
+        neng.close()
+        peng.close()
