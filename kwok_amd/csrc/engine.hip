@@ -866,6 +866,9 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 #ifndef KWOK_PF_LATE
 #define KWOK_PF_LATE 0
 #endif
+#ifndef KWOK_STORE_LANES
+#define KWOK_STORE_LANES 8  // phase-3 store group: 8 lanes = one 128-byte line (2 = 32-byte sectors)
+#endif
 #ifndef KWOK_PF16
 #define KWOK_PF16 1  // tiles in flight per wave in the persistent grid (1 or 2)
 #endif
@@ -1078,7 +1081,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
         const uint4 nv = tq[q * 64 + lane];
         const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
         const unsigned long long bal = __ballot(ch);
-        if ((bal >> (lane & ~7u)) & 0xFFull) {
+        if ((bal >> (lane & ~(KWOK_STORE_LANES - 1u))) & ((1ull << KWOK_STORE_LANES) - 1ull)) {
           if (!KWOK_EXP_NOWRITE) {
             if (KWOK_NT16) {
               typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
