@@ -520,7 +520,10 @@ __device__ __forceinline__ uint32_t rel_slot(uint32_t k, uint32_t lane) {
   else return (k / 4) * (kBlock * 4) + lane * 4 + (k % 4);
 }
 constexpr uint32_t kLutMax = 256;  // pred -> match-mask table for programs with pred_bits <= 8
-constexpr int kLdsDeltas = 512;  // (class, stage) deltas staged in LDS when the table is this small
+#ifndef KWOK_LDS_DELTAS
+#define KWOK_LDS_DELTAS 512
+#endif
+constexpr int kLdsDeltas = KWOK_LDS_DELTAS;  // (class, stage) deltas staged in LDS when the table is this small
 #ifndef KWOK_STASH
 #define KWOK_STASH 192
 #endif
@@ -854,11 +857,17 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 // Words past n are never work; chunks past n hold what was loaded (0 past the buffer range),
 // so rewriting them is harmless inside the (tile-padded) allocation.
 #ifndef KWOK_Q16
-#define KWOK_Q16 2
+#define KWOK_Q16 4  // r1ao: Q = 4 at 4 blocks per CU 113.9 us / idle 42.8 us vs Q = 2 at 6: 116.6 / 47.8
 #endif
 
 #ifndef KWOK_WPE16
 #define KWOK_WPE16 6  // waves per SIMD the register allocation must allow (LDS allows 6 at Q = 2)
+#endif
+#ifndef KWOK_WPE16_Q4
+#define KWOK_WPE16_Q4 4  // Q = 4: the LDS tile + work list allow 4 blocks per CU, so 128 VGPRs
+#endif
+#ifndef KWOK_LDS_DELTAS16
+#define KWOK_LDS_DELTAS16 64  // (class, stage) deltas staged in LDS by the 2-byte sweep (<= 11-bit programs)
 #endif
 #ifndef KWOK_NT16
 #define KWOK_NT16 1  // phase-3 line stores with the nontemporal hint (r1y: 122 -> 119 us)
@@ -876,12 +885,12 @@ template <int Q>
 constexpr uint32_t seg16_words() { return 64u * 8u * Q + 32u; }  // count + records + padding line
 #define kSeg16 seg16_words<Q>()
 template <bool kHarness, int Q, bool kPersist, int kDepth = KWOK_PF16>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ? KWOK_WPE16_Q4 : KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
   constexpr int K = 8 * Q;                 // words per lane
   constexpr uint32_t kWave = 64u * K;      // words per wave region
   constexpr uint32_t kTile = kBlock * K;   // words per block
   __shared__ unsigned int s_stat[kStatWords];
-  __shared__ kwk_delta s_delta[kLdsDeltas];
+  __shared__ kwk_delta s_delta[KWOK_LDS_DELTAS16];
   __shared__ uint16_t s_work[kWavesPerBlock][kWave];
   __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
   __shared__ uint32_t s_lut[kLutMax];
@@ -920,7 +929,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KWOK_WPE
   for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   const kwk_delta* __restrict__ deltas = a.deltas;
-  if (n_deltas <= kLdsDeltas) {
+  if (n_deltas <= KWOK_LDS_DELTAS16) {
     for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
     deltas = s_delta;
   }

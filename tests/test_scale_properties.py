@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 N_NODES, PPN, STEPS = 40_000, 100, 20
 
 
-def _pods(state):
+def _pods(state, n_nodes=N_NODES):
     from bench import shard_pod_variants
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
@@ -23,9 +23,9 @@ def _pods(state):
     prog = KindProgram(load_stage_files(*W.stage_paths(W.POD_FAST)), HarnessSpec())
     prog.explore(pvars)
     ing = Ingest(prog)
-    idx = shard_pod_variants(0, N_NODES * PPN, 0x6B776F6B, 0.1)
+    idx = shard_pod_variants(0, n_nodes * PPN, 0x6B776F6B, 0.1)
     hot, dels, rec, cls = ing.variant_columns(pvars, idx)
-    eng = Engine(prog, capacity=N_NODES * PPN, state=state)
+    eng = Engine(prog, capacity=n_nodes * PPN, state=state)
     eng.load_stages()
     eng.set_harness(True)
     eng.load(hot, dels, rec, cls, ing.record_array())
@@ -62,6 +62,36 @@ def test_three_sweeps_agree_at_4m_pods():
         for s in ("u32", "wide"):
             assert st[s]["fired"] == st["auto"]["fired"] and st[s]["fired_per_stage"] == st["auto"]["fired_per_stage"]
         assert sum(st["auto"]["fired_per_stage"].values()) == st["auto"]["fired"]
+    finally:
+        for _, e in engines.values():
+            e.close()
+
+
+def test_sweep16_tile_shapes_agree_at_17m_pods(monkeypatch):
+    """The 2-byte sweep's tile shapes: Q = 4 (8192-word tiles, persistent grid: at 17M pods
+    the tiles outnumber twice the resident blocks), Q = 2 and Q = 1 (one block per tile) must
+    fire the same sets and leave the same words.  KWOK_SWEEP_Q16 is read at engine creation."""
+    engines = {}
+    try:
+        for q in ("4", "2", "1"):
+            monkeypatch.setenv("KWOK_SWEEP_Q16", q)
+            engines[q] = _pods("auto", n_nodes=170_000)
+        monkeypatch.delenv("KWOK_SWEEP_Q16")
+        assert all(e.stats()["state_bytes"] == 2 for _, e in engines.values())
+        now0 = 1_700_000_000 * 10**9
+        for k in range(10):
+            keys = {}
+            for q, (_, e) in engines.items():
+                e.step(now0 + k * 10**9, 0x6B776F6B, k)
+                keys[q] = _fired_key(e.fired())
+            assert len(keys["4"]) > 0
+            assert np.array_equal(keys["4"], keys["2"]) and np.array_equal(keys["4"], keys["1"]), f"step {k}"
+        states = {q: e.read()[0] for q, (_, e) in engines.items()}
+        for q in ("2", "1"):
+            for col in ("pred", "sched"):
+                assert np.array_equal(states["4"][col], states[q][col]), (q, col)
+        st = {q: e.stats() for q, (_, e) in engines.items()}
+        assert st["4"]["fired_per_stage"] == st["2"]["fired_per_stage"] == st["1"]["fired_per_stage"]
     finally:
         for _, e in engines.values():
             e.close()
