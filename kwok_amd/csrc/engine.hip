@@ -875,6 +875,9 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 #ifndef KWOK_PF_LATE
 #define KWOK_PF_LATE 0
 #endif
+#ifndef KWOK_PF_EARLY
+#define KWOK_PF_EARLY 1  // issue the next tile's loads before phase 1 of this one
+#endif
 #ifndef KWOK_STORE_LANES
 #define KWOK_STORE_LANES 8  // phase-3 store group: 8 lanes = one 128-byte line (2 = 32-byte sectors)
 #endif
@@ -969,6 +972,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * kSeg16;
     kwk_fired_rec* __restrict__ seg = reinterpret_cast<kwk_fired_rec*>(seg32 + 1);
 
+    // the tile's words leave the prefetch buffer; the next tile's loads are issued before
+    // phase 1 (KWOK_PF_EARLY), so they overlap this tile's idle test as well as phases 2-3
+    uint4 cur[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[q] = v[q];
+    if (kPersist && KWOK_PF_EARLY) issue_tile(v, tile + kDepth * gridDim.x);
     // ---- phase 1: idle test on the raw words.  bit k = q * 8 + h of a lane's masks
     uint32_t in_range = 0xFFFFFFFFu >> (32 - K);
     if (!full) {
@@ -981,7 +990,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     uint32_t pend = 0, need = 0, ready = 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const uint32_t dw[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+      const uint32_t dw[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t d = dw[j];
@@ -1029,12 +1038,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         wl[pos++] = (uint16_t)((k >> 3) * 512u + lane * 8u + (k & 7u) + (((ready >> k) & 1u) << 15));
       }
     }
-    uint4 cur[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) cur[q] = v[q];
-    // refill this buffer.  KWOK_PF_LATE: only after phase 2, whose table lookups would
-    // otherwise wait for it (vmcnt retires in issue order)
-    if (kPersist && (!KWOK_PF_LATE || !n_work)) issue_tile(v, tile + kDepth * gridDim.x);
+    // refill this buffer here instead (KWOK_PF_EARLY=0).  KWOK_PF_LATE: only after phase 2,
+    // whose table lookups would otherwise wait for it (vmcnt retires in issue order)
+    if (kPersist && !KWOK_PF_EARLY && (!KWOK_PF_LATE || !n_work)) issue_tile(v, tile + kDepth * gridDim.x);
 
     if (n_work) {
       // ---- phase 2
@@ -1082,7 +1088,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         n_bytes += f.bytes;
         emit_fired<true>(f, i - wbase, lane, seg, seg_n, s_stat, n_bytes);
       }
-      if (kPersist && KWOK_PF_LATE) issue_tile(v, tile + kDepth * gridDim.x);
+      if (kPersist && !KWOK_PF_EARLY && KWOK_PF_LATE) issue_tile(v, tile + kDepth * gridDim.x);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       // ---- phase 3: whole 128-byte lines wherever a word changed
 #pragma unroll
