@@ -884,6 +884,10 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 #ifndef KWOK_PF16
 #define KWOK_PF16 1  // tiles in flight per wave in the persistent grid (1 or 2)
 #endif
+// word offset (minus lane * 8) of bit b of a lane's phase-1 masks in the 2-byte sweep
+__device__ __forceinline__ constexpr uint32_t bit_word(const uint32_t b) {
+  return ((b & 15u) >> 2) * 512u + 2u * (b & 3u) + (b >> 4);
+}
 template <int Q>
 constexpr uint32_t seg16_words() { return 64u * 8u * Q + 32u; }  // count + records + padding line
 #define kSeg16 seg16_words<Q>()
@@ -979,12 +983,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     for (int q = 0; q < Q; ++q) cur[q] = v[q];
     if (kPersist && KWOK_PF_EARLY) issue_tile(v, tile + kDepth * gridDim.x);
     // ---- phase 1: idle test on the raw words.  bit k = q * 8 + h of a lane's masks
-    uint32_t in_range = 0xFFFFFFFFu >> (32 - K);
+    // bit b of a lane's masks: dword (b & 15) of the lane's 4Q dwords (row (b & 15) / 4),
+    // its low word for b < 16, its high word for b >= 16 (so the SWAR flags at bits 15 / 31
+    // of each dword pack with one shift); word offset in the wave region: bit_word(b) + lane * 8
+    constexpr uint32_t kHalfMask = (1u << (4 * Q)) - 1u;
+    uint32_t in_range = kHalfMask | kHalfMask << 16;
     if (!full) {
       in_range = 0;
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        in_range |= (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8) < a.n ? 1u : 0u) << k;
+      for (int t = 0; t < K; ++t) {
+        const int b = t < 4 * Q ? t : 16 + t - 4 * Q;
+        in_range |= (wbase + bit_word((uint32_t)b) + lane * 8u < a.n ? 1u : 0u) << b;
+      }
     }
     // two words per dword (SWAR): each test leaves its per-word flag at bit 15 / bit 31
     uint32_t pend = 0, need = 0, ready = 0;
@@ -1002,9 +1012,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
           nb |= (((d & X.t2) + 0x7FFF7FFFu) & 0x80008000u) & ~((d & X.l2) << X.sl);
         }
         const uint32_t n2 = mg & nb, p2 = mg & pe;
-        const int k = q * 8 + 2 * j;
-        need |= ((n2 >> 15) & 1u) << k | (n2 >> 31) << (k + 1);
-        pend |= ((p2 >> 15) & 1u) << k | (p2 >> 31) << (k + 1);
+        const int jj = q * 4 + j;  // flags at bits 15 / 31 -> bits jj / 16 + jj
+        need |= n2 >> (15 - jj);
+        pend |= p2 >> (15 - jj);
       }
     }
     pend &= in_range;
@@ -1012,10 +1022,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
       const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
 #pragma unroll 8
-      for (int k = 0; k < K; ++k) {
+      for (int t = 0; t < K; ++t) {
+        const int k = t < 4 * Q ? t : 16 + t - 4 * Q;
         const uint32_t p = (pend >> k) & 1u;
-        const int64_t d =
-            buf_load_i64(due_rs, p ? (wbase + (uint32_t)(k / 8) * 512u + lane * 8u + (uint32_t)(k % 8)) * 8u : kOOB);
+        const int64_t d = buf_load_i64(due_rs, p ? (wbase + bit_word((uint32_t)k) + lane * 8u) * 8u : kOOB);
         ready |= (p & (uint32_t)(d <= a.now)) << k;
       }
       need |= ready;
@@ -1035,7 +1045,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
       }
       for (uint32_t m = need; m; m &= m - 1u) {
         const uint32_t k = (uint32_t)__ffs(m) - 1u;
-        wl[pos++] = (uint16_t)((k >> 3) * 512u + lane * 8u + (k & 7u) + (((ready >> k) & 1u) << 15));
+        wl[pos++] = (uint16_t)(bit_word(k) + lane * 8u + (((ready >> k) & 1u) << 15));
       }
     }
     // refill this buffer here instead (KWOK_PF_EARLY=0).  KWOK_PF_LATE: only after phase 2,
