@@ -952,7 +952,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   } X;
   X.m2 = R.managed * 0x10001u; X.d2 = R.dirty * 0x10001u; X.a2 = R.alive * 0x10001u;
   X.t2 = R.term * 0x10001u; X.l2 = R.del * 0x10001u;
-  X.s2 = R.smask * 0x10001u; X.n2 = R.none_code * 0x10001u;
+  // the stage field sits below the flags, so it never reaches bit 15: tested in place
+  X.s2 = (R.smask << R.sshift) * 0x10001u; X.n2 = (R.none_code << R.sshift) * 0x10001u;
   X.sm = (uint32_t)(16 - __ffs(R.managed)) & 31u; X.sd = (uint32_t)(16 - __ffs(R.dirty)) & 31u;
   X.sa = (uint32_t)(16 - __ffs(R.alive)) & 31u; X.sl = (uint32_t)(16 - __ffs(R.del)) & 31u;
   uint32_t n_matched = 0, n_bytes = 0;  // per lane
@@ -1005,7 +1006,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
       for (int j = 0; j < 4; ++j) {
         const uint32_t d = dw[j];
         const uint32_t mg = (d & X.m2) << X.sm;
-        const uint32_t pe = ((((d >> R.sshift) & X.s2) ^ X.n2) + 0x7FFF7FFFu) & 0x80008000u;
+        const uint32_t pe = (((d & X.s2) ^ X.n2) + 0x7FFF7FFFu) & 0x80008000u;
         uint32_t nb = (d & X.d2) << X.sd;
         if (kHarness) {
           nb |= (~d & X.a2) << X.sa;
