@@ -1,25 +1,39 @@
-"""Headline benchmark: stage transitions/sec at 1M nodes / 100M pods (BASELINE.json).
+"""Headline benchmark: stage transitions/sec at 1M nodes / 100M pods (BASELINE.json, config C5).
 
 One *step* = one reconciliation pass of the HIP engines over the whole resident cluster
 (pods + nodes): harness churn, match of changed objects, weighted pick + delay/jitter,
-firing of due objects and their next-state deltas.  Inputs are resident in HBM before the
-timed region; the fired lists stay on the device (the Go host would pull them with
-kwk_fired — the PCIe-inclusive rate is reported in DESIGN.md, never here).
+firing of due objects, their next-state deltas, and the fired hand-back — each engine's
+fired list compacted into one dense device list every step (kwk_fired_compact; the Go host
+would DMA it from there).  Every `--report-every` steps (the reporting interval) the cluster
+aggregates are computed on the device and summed over all GPUs with one RCCL all-reduce:
+per-stage transition counts, the pod / node phase histograms (kwk_count) and the cluster
+CPU / memory usage (kwk_usage over the default usage-from-annotation ClusterResourceUsage).
+All of it is inside the timed region.  Inputs are resident in HBM before it starts.
 
     python bench.py [--gpus N --steps K --warmup W]          # N>1 under torch.distributed.run
 
-Multi-GPU (one process per GPU): every rank owns a contiguous block of nodes and the pods
-on them (no data-path collective); the cluster-wide aggregates (transitions per stage, bytes)
-are summed with one RCCL all-reduce after the timed region.  Default "scaling": "weak" — each
-rank keeps the full C5 shard (--nodes x --pods-per-node), so N GPUs simulate an N-times
-larger cluster; --scaling strong splits --nodes over the ranks instead.
+Multi-GPU (one process per GPU): rank r owns the contiguous node block [r*n/N, (r+1)*n/N) and
+every pod on those nodes (no data-path collective).  Default "scaling": "strong" — the C5
+cluster (--nodes total) is split over the ranks; --scaling weak keeps --nodes per rank.
+
+The JSON line carries `roofline` for the pod sweep kernel (algorithmic bytes per launch /
+its HIP-event duration on the engine's stream; `traffic` = HBM bytes per launch from two
+rocprofv3 PMC passes of this same workload run as child processes at N=1, FETCH_SIZE x 2 —
+the gfx950 correction of MI355X_MICROARCH.md — + WRITE_SIZE, or null when they cannot run),
+`cpu_baseline` (the oracle timed on this host), `pcie_inclusive` (the rate when every step's
+fired list is also copied to pinned host memory) and `hbm_working_set` (the C2 stage mix at
+100M pods: 4-byte words, 0.4 GB of state, beyond the 256 MiB Infinity Cache).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import sqlite3
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -29,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "stage transitions/sec (whole node), 1M nodes/100M pods; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NOW0 = 1_700_000_000 * 10**9
 
 
 def splitmix64(x: np.ndarray) -> np.ndarray:
@@ -55,28 +70,35 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, weak=True, wide_state=False):
+def node_range(n_nodes, rank, world, weak):
+    if weak:  # rank r owns global nodes [r*n, (r+1)*n)
+        return n_nodes * rank, n_nodes * (rank + 1)
+    from kwok_amd.host.cluster import node_block
+    return node_block(n_nodes, world, rank)
+
+
+def build_engines(node_lo, node_hi, pods_per_node, device, seed, job_frac, wide_state=False, mix="fast"):
+    """Pod and node engines of one shard.  mix "fast": pod-fast (C1/C5 stage mix, 2-byte words);
+    "general": pod-general + pod-chaos (C2 stage mix, 4-byte words)."""
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
 
-    if weak:  # rank r owns global nodes [r*n, (r+1)*n)
-        node_lo, node_hi = n_nodes * rank, n_nodes * (rank + 1)
-    else:
-        node_lo, node_hi = n_nodes * rank // world, n_nodes * (rank + 1) // world
     pod_lo, pod_hi = node_lo * pods_per_node, node_hi * pods_per_node
-    # pods: pod-fast (C1 stage mix) with harness churn
-    pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
-    pprog = KindProgram(load_stage_files(*W.stage_paths(W.POD_FAST)), HarnessSpec())
+    if mix == "fast":
+        pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+        pidx = shard_pod_variants(pod_lo, pod_hi, seed, job_frac)
+        files = W.POD_FAST
+    else:
+        pvars, pidx = W.c2_pod_variants(pod_lo, pod_hi, seed=seed, job_frac=job_frac)
+        files = W.POD_GENERAL + W.POD_CHAOS
+    pprog = KindProgram(load_stage_files(*W.stage_paths(files)), HarnessSpec())
     pprog.explore(pvars)
     ping = Ingest(pprog)
-    log(f"rank {rank}: generating pods [{pod_lo}, {pod_hi})")
-    pidx = shard_pod_variants(pod_lo, pod_hi, seed, job_frac)
     phot, pdel, prec, pcls = ping.variant_columns(pvars, pidx)
-    log(f"rank {rank}: loading {pod_hi - pod_lo} pods onto device {device}")
-    del pidx
-    pods = Engine(pprog, capacity=pod_hi - pod_lo, device=device, slot_base=pod_lo, kind_salt=0, wide_state=wide_state)
+    pods = Engine(pprog, capacity=pod_hi - pod_lo, device=device, slot_base=pod_lo, kind_salt=0, wide_state=wide_state,
+                  max_records=max(1, len(ping.records)) + 16)
     pods.load_stages()
     pods.load(phot, pdel, prec, pcls, ping.record_array())
     del phot, pdel, prec, pcls
@@ -91,19 +113,154 @@ def build_engines(n_nodes, pods_per_node, rank, world, device, seed, job_frac, w
                    wide_state=wide_state)
     nodes.load_stages()
     nodes.load(nhot, ndel, nrec, ncls, ning.record_array())
-    return pods, nodes, (node_lo, node_hi, pod_lo, pod_hi)
+    return pods, nodes, (pvars, pidx)
 
 
+def configure_usage(pods, pvars, pidx, n_nodes_local, pods_per_node):
+    """kwk_usage_config for the shard: the default usage-from-annotation ClusterResourceUsage
+    (kustomize/metrics/usage/usage-from-annotation.yaml) evaluated once per variant."""
+    from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
+    path = os.path.join(ROOT, "tests", "golden", "metrics", "usage-from-annotation.yaml")
+    up = UsageProgram(*load_usage_yaml(open(path).read()))
+    vkeys, cv, mv = usage_columns(up, pvars)
+    node_ptr = np.arange(n_nodes_local + 1, dtype=np.uint32) * np.uint32(pods_per_node)
+    pods.usage_config(node_ptr, vkeys[pidx], cv, mv)
+
+
+class Reporter:
+    """One reporting interval: device aggregates of this shard, summed over all GPUs (RCCL)."""
+
+    def __init__(self, pods, nodes, dist, device):
+        from kwok_amd.host.cluster import phase_masks
+        self.pods, self.nodes, self.dist, self.device = pods, nodes, dist, device
+        pm = phase_masks(pods.p, values=("Running", "Succeeded", "Failed"))
+        nm = phase_masks(nodes.p, values=("Running",))
+        self.masks = [[0] + list(pm.values()), [0] + list(nm.values())]
+        self.names = [["pods"] + [f"pods_{k}" for k in pm], ["nodes"] + [f"nodes_{k}" for k in nm]]
+
+    def collect(self, now_ns):
+        from kwok_amd.host.cluster import engine_aggregates
+        agg = engine_aggregates([self.pods, self.nodes], self.masks, self.names, now_ns, usage_engine=self.pods)
+        return agg.allreduce(self.dist, device=self.device)
+
+
+def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None):
+    """Steps k0..k1-1; ev_base: record HIP events (pod stream) around each pod sweep."""
+    last = None
+    n_fired_host = 0
+    for k in range(k0, k1):
+        now = NOW0 + k * dt
+        j = k - k0
+        if ev_base is not None:
+            pods.event_record(ev_base + 3 * j)
+        pods.step(now, seed, k)
+        if ev_base is not None:
+            pods.event_record(ev_base + 3 * j + 1)
+        pods.fired_compact()
+        if ev_base is not None:
+            pods.event_record(ev_base + 3 * j + 2)
+        nodes.step(now, seed, k)
+        nodes.fired_compact()
+        if pinned is not None:  # PCIe-inclusive: every fired record copied to pinned host memory
+            n_fired_host += len(pods.fired(pinned[0])) + len(nodes.fired(pinned[1]))
+        if reporter is not None and report_every and (j + 1) % report_every == 0:
+            last = reporter.collect(now)
+    return last, n_fired_host
+
+
+def sweep_bytes(s0, s1):
+    return s1["bytes"] - s0["bytes"], s1["line_bytes"] - s0["line_bytes"]
+
+
+def measure_hbm_working_set(args, device):
+    """The C2 stage mix (pod-general + chaos: weighted picks, jitter, value records) at 100M
+    pods on one GPU: 4-byte words = 0.4 GB of state + 0.8 GB of due times, beyond the 256 MiB
+    Infinity Cache, so the roofline fraction is an HBM claim."""
+    n_nodes = args.hbm_nodes
+    pods, nodes, _ = build_engines(0, n_nodes, args.pods_per_node, device, args.seed, args.job_frac, mix="general")
+    try:
+        dt = 500 * 10**6
+        steps, warm = args.hbm_steps, args.hbm_warmup
+        run_steps(pods, nodes, args.seed, dt, 0, warm)
+        pods.sync()
+        nodes.sync()
+        s0 = pods.stats()
+        t0 = time.perf_counter()
+        run_steps(pods, nodes, args.seed, dt, warm, warm + steps, ev_base=0)
+        pods.sync()
+        nodes.sync()
+        wall = time.perf_counter() - t0
+        s1 = pods.stats()
+        sweep_ms = sum(pods.event_elapsed_ms(3 * j, 3 * j + 1) for j in range(steps))
+        b, lb = sweep_bytes(s0, s1)
+        us = sweep_ms / steps * 1e3
+        ach = b / steps / (us * 1e-6) / 1e9
+        return {"workload": f"C2 stage mix at {n_nodes * args.pods_per_node:,} pods ({n_nodes:,} nodes): pod-general + "
+                            "pod-chaos, harness churn, 0.5 s per step",
+                "kernel": ("sweepw_kernel<4-byte>" if s1["state_bytes"] == 4 else "sweepw_kernel<8-byte>") + " (pods)",
+                "state_bytes_per_object": int(s1["state_bytes"]),
+                "state_column_GB": round(n_nodes * args.pods_per_node * int(s1["state_bytes"]) / 1e9, 3),
+                "transitions_per_s": round((s1["fired"] - s0["fired"]) / wall, 1),
+                "transitions_per_step": (s1["fired"] - s0["fired"]) / steps,
+                "avg_launch_us": round(us, 2), "bytes_per_launch": int(b / steps),
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "line_bytes_per_launch": int(lb / steps),
+                "line_frac": round(lb / steps / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "steps": steps}
+    finally:
+        pods.close()
+        nodes.close()
+
+
+# ------------------------------------------------------------------ PMC traffic (child passes)
+def _pmc_pass(counter, args, outdir):
+    """One rocprofv3 --pmc pass over a short run of this workload (a child process: this
+    process has not touched the GPU).  -> mean counter value per pod-sweep launch (KiB)."""
+    d = os.path.join(outdir, counter.lower())
+    cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
+           "--pmc-child", "--steps", "6", "--warmup", "4", "--nodes", str(args.nodes),
+           "--pods-per-node", str(args.pods_per_node), "--seed", str(args.seed)]
+    env = dict(os.environ, TMPDIR=outdir)
+    r = subprocess.run(cmd, cwd=outdir, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150)
+    if r.returncode != 0:
+        raise RuntimeError(f"rocprofv3 {counter}: rc {r.returncode}: {r.stderr.decode(errors='replace')[-400:]}")
+    dbs = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs if f.endswith(".db")]
+    if not dbs:
+        raise RuntimeError(f"rocprofv3 {counter}: no results database")
+    per = {}
+    c = sqlite3.connect(dbs[0])
+    for disp, name, cn, v in c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection"):
+        if "sweep" in name and "<true" in name and cn == counter:  # the pod engine (harness) only
+            per[disp] = per.get(disp, 0.0) + float(v)
+    vals = [per[k] for k in sorted(per)][4:]  # past the warm-up launches
+    if not vals:
+        raise RuntimeError(f"rocprofv3 {counter}: no pod sweep dispatches")
+    return statistics.mean(vals), len(vals)
+
+
+def pmc_traffic(args):
+    """HBM bytes per pod-sweep launch: FETCH_SIZE x 2 (gfx950: 128-B requests tallied at 64 B,
+    MI355X_MICROARCH.md HBM) + WRITE_SIZE, from two separate PMC passes (FETCH_SIZE and
+    WRITE_SIZE do not fit one pass).  Infinity-Cache hits are counted, not excluded."""
+    outdir = tempfile.mkdtemp(prefix="kwok_pmc_", dir="/tmp")
+    try:
+        fetch_kib, nf = _pmc_pass("FETCH_SIZE", args, outdir)
+        write_kib, nw = _pmc_pass("WRITE_SIZE", args, outdir)
+    except Exception as e:  # noqa: BLE001 - the bench line still prints, with traffic null
+        log(f"PMC passes failed: {e}")
+        return None, str(e)[:200]
+    return {"read": int(fetch_kib * 1024 * 2), "write": int(write_kib * 1024), "launches": [nf, nw]}, None
+
+
+# ------------------------------------------------------------------ CPU baseline
 def cpu_baseline(sample_s: float, seed: int):
     """The oracle (refcpu, C++ restatement of the Go path) timed on this host: per object a
     JSON re-parse (ToJSONStandard), Lifecycle.Match and Stage.Delay, on one thread (the
     reference's single preprocess goroutine, pod_controller.go:150).  Each stage transition
     costs the reference at least one such match, so objects/sec bounds its transitions/sec."""
+    import yaml
     from kwok_amd import workload as W
-    from kwok_amd.host.stages import load_stage_files, to_v1alpha1
     from oracle import refcpu
-    stages = load_stage_files(*W.stage_paths(W.POD_FAST))
-    lc = refcpu.Lifecycle([to_v1alpha1(s) for s in stages])
+    lc = refcpu.Lifecycle([yaml.safe_load(open(p)) for p in W.stage_paths(W.POD_FAST)])
     # a sample in the steady-state mix: Pending (fresh / re-created), Running, Succeeded+deleting
     base = W.make_cluster("C1", 100, 20000, seed=seed).pods.materialize()
     objs = []
@@ -115,7 +272,7 @@ def cpu_baseline(sample_s: float, seed: int):
             o["status"] = {"phase": "Succeeded", "podIP": "10.0.0.2"}
             o["metadata"]["deletionTimestamp"] = "2023-11-14T22:13:20Z"
         objs.append(json.dumps(o, separators=(",", ":")).encode())
-    now = 1_700_000_000 * 10**9
+    now = NOW0
     lc.match_batch(objs[:2000], now, seed, 0)  # warm-up
     t0 = time.perf_counter()
     n = 0
@@ -125,7 +282,7 @@ def cpu_baseline(sample_s: float, seed: int):
         n += len(objs)
         reps += 1
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "stage transitions/sec (upper bound: matches/sec)", "cores": 1,
+    return {"value": round(n / dt, 1), "unit": "stage transitions/sec (upper bound: matches/sec)", "cores": 1,
             "kind": "port",
             "sample": f"{len(objs)} pod JSON objects x {reps} passes ({dt:.1f} s): JSON re-parse + Match + Delay "
                       f"(pod-fast stages), 1 thread = the reference's preprocess goroutine; CPU "
@@ -147,19 +304,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--nodes", type=int, default=1_000_000, help="nodes per GPU (weak) or in total (strong)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--nodes", type=int, default=1_000_000, help="nodes in total (strong) or per GPU (weak)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong")
     ap.add_argument("--config", choices=("C1", "C2", "C3", "C4", "C5"), default="C5",
                     help="BASELINE.json configuration; C5 is the headline line, C1-C4 run on one GPU")
     ap.add_argument("--pods-per-node", type=int, default=100)
     ap.add_argument("--job-frac", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=0x6B776F6B)
     ap.add_argument("--dt-ms", type=int, default=1000, help="simulated time per step")
+    ap.add_argument("--report-every", type=int, default=10, help="steps per reporting interval (aggregates + RCCL)")
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child passes (traffic null)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--hbm-nodes", type=int, default=1_000_000, help="nodes of the C2-mix HBM working-set run (0: off)")
+    ap.add_argument("--hbm-steps", type=int, default=10)
+    ap.add_argument("--hbm-warmup", type=int, default=12)
+    ap.add_argument("--pcie-steps", type=int, default=5)
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
-    ap.add_argument("--wide-state", action="store_true", default=os.environ.get("KWOK_BENCH_WIDE") == "1",
-                    help="diagnostic: force the 8-byte device state format")
+    ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
     args = ap.parse_args()
 
     if args.config != "C5":
@@ -179,6 +342,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    weak = args.scaling == "weak"
+
+    # PMC child passes first, while this process has not touched the GPU (N=1 only)
+    traffic, pmc_err = None, "not collected (N>1, --no-pmc or --no-harness)"
+    if world == 1 and not args.pmc_child and not args.no_pmc and not args.no_harness:
+        log("PMC passes (FETCH_SIZE, WRITE_SIZE) as child processes")
+        traffic, pmc_err = pmc_traffic(args)
+
     dist = None
     if world > 1:
         import torch
@@ -191,23 +362,21 @@ def main():
         kbuild.build()
 
     t_setup = time.perf_counter()
-    pods, nodes, (nlo, nhi, plo, phi) = build_engines(args.nodes, args.pods_per_node, rank, world, local_rank,
-                                                      args.seed, args.job_frac, weak=args.scaling == "weak",
-                                                      wide_state=args.wide_state)
+    nlo, nhi = node_range(args.nodes, rank, world, weak)
+    log(f"rank {rank}: nodes [{nlo}, {nhi}), pods [{nlo * args.pods_per_node}, {nhi * args.pods_per_node})")
+    pods, nodes, (pvars, pidx) = build_engines(nlo, nhi, args.pods_per_node, local_rank, args.seed, args.job_frac,
+                                               wide_state=args.wide_state)
+    configure_usage(pods, pvars, pidx, nhi - nlo, args.pods_per_node)
+    del pidx
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
-    now0 = 1_700_000_000 * 10**9
     dt = args.dt_ms * 10**6
-
-    def step(k):
-        now = now0 + k * dt
-        pods.step(now, args.seed, k)
-        nodes.step(now, args.seed, k)
+    reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None)
+    report_every = 0 if args.pmc_child else args.report_every
 
     log(f"setup {setup_s:.1f} s; warmup {args.warmup} steps")
-    for k in range(args.warmup):
-        step(k)
+    run_steps(pods, nodes, args.seed, dt, 0, args.warmup)
     pods.sync()
     nodes.sync()
     s0p, s0n = pods.stats(), nodes.stats()
@@ -220,97 +389,112 @@ def main():
     pods.sync()
     nodes.sync()
     t0 = time.perf_counter()
-    pods.event_record(0)
-    nodes.event_record(0)
-    for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
-    pods.event_record(1)
-    nodes.event_record(1)
+    agg, _ = run_steps(pods, nodes, args.seed, dt, args.warmup, args.warmup + args.steps, ev_base=0,
+                       reporter=reporter, report_every=report_every)
     pods.sync()
     nodes.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    pod_ms = pods.event_elapsed_ms(0, 1)
-    node_ms = nodes.event_elapsed_ms(0, 1)
     s1p, s1n = pods.stats(), nodes.stats()
+    sweep_ms = [pods.event_elapsed_ms(3 * j, 3 * j + 1) for j in range(args.steps)]
+    compact_ms = [pods.event_elapsed_ms(3 * j + 1, 3 * j + 2) for j in range(args.steps)]
 
     fired = (s1p["fired"] - s0p["fired"]) + (s1n["fired"] - s0n["fired"])
-    pbytes = s1p["bytes"] - s0p["bytes"]
-    plines = s1p["line_bytes"] - s0p["line_bytes"]
+    pbytes, plines = sweep_bytes(s0p, s1p)
     per_stage = {k: s1p["fired_per_stage"][k] - s0p["fired_per_stage"][k] for k in s1p["fired_per_stage"]}
     per_stage.update({k: s1n["fired_per_stage"][k] - s0n["fired_per_stage"][k] for k in s1n["fired_per_stage"]})
 
-    agg = np.array([fired, pbytes, elapsed * 1e9], dtype=np.float64)
+    total_fired, max_s = float(fired), elapsed
     if dist is not None:
         import torch
-        t = torch.tensor([float(fired), float(pbytes)], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t)  # cluster-wide aggregates over RCCL (xGMI)
+        t = torch.tensor([float(fired)], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t)  # RCCL over xGMI
         tm = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        agg = np.array([t[0].item(), t[1].item(), tm.item() * 1e9])
-    total_fired, total_bytes, max_ns = agg
-    max_s = max_ns / 1e9
+        total_fired, max_s = t.item(), tm.item()
 
-    total_nodes = args.nodes * world if args.scaling == "weak" else args.nodes
+    if args.pmc_child:
+        pods.close()
+        nodes.close()
+        return
+
+    # PCIe-inclusive rate: the same steps with every fired record copied to pinned host memory
+    pcie = None
+    if args.pcie_steps > 0 and world == 1:
+        from kwok_amd.host.engine import PinnedBuffer
+        pin = (PinnedBuffer(8 * pods.capacity), PinnedBuffer(8 * nodes.capacity))
+        k0 = args.warmup + args.steps
+        s2p, s2n = pods.stats(), nodes.stats()
+        t1 = time.perf_counter()
+        _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin)
+        wall = time.perf_counter() - t1
+        s3p, s3n = pods.stats(), nodes.stats()
+        nf = (s3p["fired"] - s2p["fired"]) + (s3n["fired"] - s2n["fired"])
+        assert n_host == nf, (n_host, nf)
+        pcie = {"value": round(nf / wall, 1), "unit": "stage transitions/sec", "steps": args.pcie_steps,
+                "fired_records_to_host_per_step": nf / args.pcie_steps, "ms_per_step": round(wall / args.pcie_steps * 1e3, 4),
+                "note": "each step's fired lists copied (kwk_fired, 8 B per transition) into kwk_alloc_host buffers"}
+        for p in pin:
+            p.close()
+    pods.close()
+    nodes.close()
+
+    hbm = None
+    if rank == 0 and world == 1 and args.hbm_nodes > 0 and not args.no_harness:
+        log("HBM working-set run: C2 stage mix at 100M pods")
+        hbm = measure_hbm_working_set(args, local_rank)
+
     if rank == 0:
         value = total_fired / max_s
-        pod_kernel_s = pod_ms / 1e3 / args.steps
+        pod_kernel_s = statistics.mean(sweep_ms) / 1e3
         achieved = (pbytes / args.steps) / pod_kernel_s / 1e9
         sb = int(s1p["state_bytes"])
-        traffic = _pmc_traffic(sb)
+        tr = None if traffic is None else traffic["read"] + traffic["write"]
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_GBps": (round(traffic / pod_kernel_s / 1e9, 1) if traffic else None),
-                "kernel": ("sweep16_kernel" if sb == 2 else "sweep_kernel") + " (pods)",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
+                "traffic_note": (f"rocprofv3 PMC child passes of this workload ({traffic['launches']} pod-sweep launches): "
+                                 f"FETCH_SIZE x 2 = {traffic['read']} B read + WRITE_SIZE = {traffic['write']} B written "
+                                 "per launch" if traffic else f"null: {pmc_err}"),
+                "kernel": ("sweep16_kernel" if sb == 2 else "sweepw_kernel") + " (pods)",
                 "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
+                "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
-                # (at ~10 % churn nearly every line of the 2-byte column holds a changed word)
                 "line_bytes_per_launch": int(plines / args.steps),
-                "line_achieved": round(plines / args.steps / pod_kernel_s / 1e9, 1),
-                "line_frac": round(plines / args.steps / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(pod_kernel_s * 1e6, 2)}
+                "line_frac": round(plines / args.steps / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
+        if tr:
+            roof["traffic_GBps"] = round(tr / pod_kernel_s / 1e9, 1)
         cpu = None
-        log(f"timed {args.steps} steps in {max_s:.3f} s; cpu baseline next")
+        log(f"timed {args.steps} steps in {max_s:.3f} s")
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             cpu = cpu_baseline(args.cpu_sample_s, args.seed)
+        total_nodes = args.nodes * world if weak else args.nodes
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_s / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": {2: "u16", 4: "u32", 8: "u32x2"}[sb] + "/i64",
             "data": "synthetic (seeded kwokctl-shaped pods/nodes; pod-fast + node-fast/heartbeat stages)",
-            "config": {"workload": f"C5: {args.nodes:,} nodes / {args.nodes * args.pods_per_node:,} pods "
-                                   f"{'per GPU' if args.scaling == 'weak' else 'in total'}, pod-fast + "
-                                   "node-initialize/heartbeat, harness churn (Succeeded -> delete -> re-create), "
-                                   "10% Job-owned",
+            "config": {"workload": f"C5: {total_nodes:,} nodes / {total_nodes * args.pods_per_node:,} pods in total "
+                                   f"over {world} GPU(s), pod-fast + node-initialize/heartbeat, harness churn "
+                                   "(Succeeded -> delete -> re-create), 10% Job-owned; per step: sweep + fired "
+                                   f"hand-back (device compaction); every {args.report_every} steps: phase "
+                                   "histograms + cluster usage + per-stage counts all-reduced over RCCL",
                        "nodes": total_nodes, "pods": total_nodes * args.pods_per_node,
-                       "nodes_per_gpu": nhi - nlo, "parallelism": f"node-shard{world}",
-                       "sim_dt_ms": args.dt_ms},
+                       "nodes_per_gpu": nhi - nlo, "parallelism": f"node-shard{world}", "sim_dt_ms": args.dt_ms},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
+            "hbm_working_set": hbm,
+            "aggregates": agg.as_dict() if agg is not None else None,
             "detail": {"transitions_per_step": total_fired / args.steps, "per_stage_rank0": per_stage,
-                       "pod_kernel_ms_per_step": round(pod_ms / args.steps, 4),
-                       "node_kernel_ms_per_step": round(node_ms / args.steps, 4), "setup_s": round(setup_s, 1)},
+                       "pod_sweep_us_mean": round(statistics.mean(sweep_ms) * 1e3, 2),
+                       "pod_sweep_us_median": round(statistics.median(sweep_ms) * 1e3, 2),
+                       "pod_handback_us_mean": round(statistics.mean(compact_ms) * 1e3, 2),
+                       "setup_s": round(setup_s, 1)},
         }
         print(json.dumps(line), flush=True)
-    pods.close()
-    nodes.close()
     if dist is not None:
         dist.destroy_process_group()
-
-
-def _pmc_traffic(state_bytes):
-    """HBM bytes per pod-sweep launch from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None when they were taken on
-    another state format (a different kernel)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        d = json.load(open(p))
-    except (OSError, ValueError):
-        return None
-    if d.get("state_bytes_per_object") != state_bytes:
-        return None
-    return d.get("hbm_bytes_per_launch")
 
 
 if __name__ == "__main__":

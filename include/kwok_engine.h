@@ -194,6 +194,13 @@ const char* kwk_last_error(void);
 kwk_status kwk_engine_create(const kwk_engine_desc* desc, kwk_engine** out);
 kwk_status kwk_engine_destroy(kwk_engine* eng);
 
+/* Explicit kernel choices (defaults = the measured best; tests use them to check
+ * that every kernel shape gives the same results).  Nothing is read from the environment. */
+#define KWK_TUNE_FSM 1        /* 2-byte sweep: precomputed transition table, 1 (default) or 0 */
+#define KWK_TUNE_Q16 2        /* 2-byte sweep: 16-byte chunks per lane, 4 (default), 2 or 1 */
+#define KWK_TUNE_PERSIST16 3  /* 2-byte sweep: persistent grid for large engines, 1 (default) or 0 */
+kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
+
 /* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */
 kwk_status kwk_load_stages(kwk_engine* eng, const kwk_stage_table* table, const kwk_delta* deltas);
 kwk_status kwk_set_harness(kwk_engine* eng, const kwk_harness* h);
@@ -231,7 +238,8 @@ kwk_status kwk_retry(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t st
 
 /* one reconciliation step at time now_ns over slots [0, n_active):
  * harness -> match dirty objects -> fire due objects -> apply deltas.
- * Random draws use Philox4x32-10(key = seed ^ kind_salt, ctr = (slot_base+slot, step, site)). */
+ * Random draws use Philox4x32-10(key = seed ^ ((uint64_t)kind_salt << 32),
+ * ctr = (slot_base+slot, step lo, step hi, site)).  Enqueue only. */
 kwk_status kwk_step(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step);
 
 /* match only: Lifecycle.Match + Stage.Delay for the dirty objects (lifecycle.go:125-191,
@@ -239,8 +247,19 @@ kwk_status kwk_step(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t ste
  * time are then readable with kwk_read (the reference-interface mirror's Match). */
 kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t step);
 
-/* fired records of the LAST step, compacted into host memory (synchronises) */
+/* Fired hand-back (the objects Go renders patches for, pod_controller.go:290-360).  The sweep
+ * leaves per-(tile, wave) segments; kwk_fired_compact enqueues their scan + compaction into one
+ * dense device list (enqueue only: call it after kwk_step to keep the list on the device, e.g.
+ * for an in-process consumer through kwk_fired_device).  kwk_fired copies the LAST step's list
+ * (compacting first if needed) into host memory — a kwk_alloc_host buffer makes the copy a
+ * direct DMA — and synchronises.  Record order: slot order. */
+kwk_status kwk_fired_compact(kwk_engine* eng);
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
+/* device pointers of the compacted list and of its u32 count (valid until the next kwk_step) */
+kwk_status kwk_fired_device(kwk_engine* eng, const kwk_fired_rec** recs, const uint32_t** count);
+/* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */
+kwk_status kwk_alloc_host(uint64_t bytes, void** out);
+kwk_status kwk_free_host(void* p);
 /* cumulative counters (synchronises) */
 kwk_status kwk_stats(kwk_engine* eng, kwk_step_stats* out);
 /* read back columns of slots [first, first+n) (synchronises) */
@@ -307,7 +326,7 @@ kwk_status kwk_lease_config(kwk_engine* nodes, const kwk_lease_params* cfg);
 /* lease informer events / TryHold / ReleaseHold: overwrite records [first, first+n) */
 kwk_status kwk_lease_set(kwk_engine* nodes, uint32_t first, uint32_t n, const kwk_lease* leases);
 /* one pass of syncWorker over every held node whose sync is due (enqueue only).
- * interval() jitter uses Philox (key = seed ^ kind_salt, ctr = (slot_base+slot, step, 3)) */
+ * interval() jitter uses Philox (key = seed ^ ((uint64_t)kind_salt << 32), ctr = (slot_base+slot, step, 3)) */
 kwk_status kwk_lease_step(kwk_engine* nodes, int64_t now_ns, uint64_t seed, uint64_t step);
 kwk_status kwk_lease_ops(kwk_engine* nodes, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 kwk_status kwk_lease_read(kwk_engine* nodes, uint32_t first, uint32_t n, kwk_lease* out);

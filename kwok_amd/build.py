@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 SRC = [os.path.join(PKG, "csrc", "engine.hip")]
 HDR = [os.path.join(ROOT, "include", "kwok_engine.h")]
 OUT = os.path.join(PKG, "lib", "libkwok_engine.so")
-ARCH = os.environ.get("KWOK_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X only
 
 
 def _stale() -> bool:

@@ -19,26 +19,14 @@
 // 16-byte loads; fired records are compacted per wave with a ballot into a private
 // per-wave segment (no global atomics in the sweep).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstdio>
-// cost-isolation experiments only (wrong results): skip the state write-back / fired records
-#ifndef KWOK_EXP_NOWRITE
-#define KWOK_EXP_NOWRITE 0
-#endif
-#ifndef KWOK_EXP_NOFIRED
-#define KWOK_EXP_NOFIRED 0
-#endif
-#ifndef KWOK_EXP_NOSTAGECNT
-#define KWOK_EXP_NOSTAGECNT 0
-#endif
-// phase-2 state write-back with nontemporal stores (experiment)
-#ifndef KWOK_NT_STORE
-#define KWOK_NT_STORE 0
-#endif
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/kwok_engine.h"
@@ -46,8 +34,8 @@
 namespace {
 
 constexpr int kBlock = 256;              // 4 waves of 64
-constexpr int kMinObjPerThread = 8;      // smallest sweep variant: sizes the per-block arrays
-constexpr int kMaxObjPerThread = 32;
+constexpr int kMinObjPerThread = 8;      // smallest sweep tile (2048 objects): sizes the per-tile arrays
+constexpr int kMaxObjPerThread = 32;     // largest sweep tile (8192 objects): pads the state allocation
 constexpr int kWavesPerBlock = kBlock / 64;
 // matched, fired, algorithmic bytes, fired per stage, line bytes (algorithmic with state writes
 // counted as the whole lines / chunks the sweep stores)
@@ -192,9 +180,7 @@ __device__ __forceinline__ void store_state(void* st, uint64_t i, uint2 v, const
   else reinterpret_cast<uint2*>(st)[i] = v;
 }
 
-// the sweep is specialised per format
-template <bool kNarrow> struct StateWord { typedef uint2 T; };
-template <> struct StateWord<true> { typedef uint32_t T; };
+// the word sweep is specialised per format
 __device__ __forceinline__ uint2 sw_decode(uint2 w, const StateFmt&) { return w; }
 __device__ __forceinline__ uint2 sw_decode(uint32_t w, const StateFmt& f) { return fmt_unpack(w, f); }
 __device__ __forceinline__ void sw_encode(uint2& out, uint2 v, const StateFmt&) { out = v; }
@@ -462,7 +448,7 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
 
 // wave-ballot compaction of the fired set into the wave's private segment + per-stage counts
 // kPacked (2-byte sweep): 4-byte records {slot within the wave region: 11 bits, stage: 5,
-// flags: 3}, expanded to kwk_fired_rec by compact_fired_kernel (slot = segment * segment size
+// flags: 3}, expanded to kwk_fired_rec by compact_kernel (slot = segment * segment size
 // + index)
 template <bool kPacked = false>
 __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t lane, kwk_fired_rec* __restrict__ seg,
@@ -472,15 +458,15 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
     if constexpr (kPacked) {
-      if (!KWOK_EXP_NOFIRED) reinterpret_cast<uint32_t*>(seg)[pos] = (uint32_t)i | f.stage << 11 | f.flags << 16;
+      reinterpret_cast<uint32_t*>(seg)[pos] = (uint32_t)i | f.stage << 11 | f.flags << 16;
       n_bytes += 4;
     } else {
-      if (!KWOK_EXP_NOFIRED) seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
+      seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
       n_bytes += 8;
     }
   }
   seg_n += (uint32_t)__popcll(bal);
-  unsigned long long rest = KWOK_EXP_NOSTAGECNT ? 0ull : bal;  // one LDS add per distinct fired stage
+  unsigned long long rest = bal;  // one LDS add per distinct fired stage
   while (rest) {
     const uint32_t s = __shfl(f.stage, __ffsll((long long)rest) - 1);
     const unsigned long long same = __ballot(f.fire && f.stage == s);
@@ -489,45 +475,7 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   }
 }
 
-// One workgroup sweeps a tile of kBlock*K consecutive objects; each lane owns K of them at a
-// stride of kBlock, so every load instruction of a wave reads 64 consecutive state words.
-//  phase 1  stream the K state words of each lane (all K loads in flight before the first is
-//           consumed), then the due times of those with a pending stage.  The idle test runs
-//           on the raw words with precomputed masks (RawTest): no unpacking, a handful of
-//           VALU ops per object.  Objects that need work go to the wave's LDS work list
-//           (ballot + mbcnt), their raw word + due into the LDS stash;
-//  phase 2  the heavy path (decode, match / pick / delay / fire / delta, encode) over the dense
-//           work list, 64 useful lanes per wave-instruction instead of the few active in a
-//           steady-state row; each changed word is written back (KWOK_GROUP = 0) or parked in
-//           the stash for phase 3;
-//  phase 3  (KWOK_GROUP = G > 0) aligned groups of G neighbouring words rewritten whole
-//           wherever any member changed: full-segment writes instead of scattered partial ones.
-#ifndef KWOK_LB_WAVES
-#define KWOK_LB_WAVES 1
-#endif
-#ifndef KWOK_GROUP
-#define KWOK_GROUP 0
-#endif
-#ifndef KWOK_VEC
-#define KWOK_VEC 1
-#endif
-// slot of a lane's k-th word relative to its wave's first slot.  V = 1: row k of the tile is
-// kBlock consecutive words, 64 per wave (one 4-byte load per word); V = 4: each lane holds 4
-// consecutive words per 16-byte load, a wave covers 256 consecutive words per load
-template <int V>
-__device__ __forceinline__ uint32_t rel_slot(uint32_t k, uint32_t lane) {
-  if constexpr (V == 1) return k * kBlock + lane;
-  else return (k / 4) * (kBlock * 4) + lane * 4 + (k % 4);
-}
 constexpr uint32_t kLutMax = 256;  // pred -> match-mask table for programs with pred_bits <= 8
-#ifndef KWOK_LDS_DELTAS
-#define KWOK_LDS_DELTAS 512
-#endif
-constexpr int kLdsDeltas = KWOK_LDS_DELTAS;  // (class, stage) deltas staged in LDS when the table is this small
-#ifndef KWOK_STASH
-#define KWOK_STASH 192
-#endif
-constexpr int kStash = KWOK_STASH;      // work items whose word + due stay in LDS per wave (the rest are re-read)
 
 // Streamed loads go through buffer resources (T8 in cdna_hip_programming.md): a load past the
 // resource's byte size returns 0, so the tile tail and "load due only where a stage is
@@ -537,271 +485,17 @@ constexpr uint32_t kOOB = 0xFFFFFFF0u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ void buf_load(uint32_t& w, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-  w = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
-}
-__device__ __forceinline__ void buf_load(uint2& w, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-  const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-  w = make_uint2(t[0], t[1]);
-}
 __device__ __forceinline__ int64_t buf_load_i64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
   return (int64_t)(((uint64_t)t[1] << 32) | t[0]);
 }
 
-__device__ __forceinline__ void store_word(uint32_t* p, uint32_t w) {
-  if (KWOK_NT_STORE) __builtin_nontemporal_store(w, p);
-  else *p = w;
-}
-__device__ __forceinline__ void store_word(uint2* p, uint2 w) {
-  if (KWOK_NT_STORE) __builtin_nontemporal_store(((uint64_t)w.y << 32) | w.x, reinterpret_cast<uint64_t*>(p));
-  else *p = w;
-}
-
-__device__ __forceinline__ uint32_t fw_of(uint2 w) { return w.y; }      // word holding flags + stage
-__device__ __forceinline__ uint32_t pw_of(uint2 w) { return w.x; }      // word holding pred
-__device__ __forceinline__ uint32_t fw_of(uint32_t w) { return w; }
-__device__ __forceinline__ uint32_t pw_of(uint32_t w) { return w; }
-__device__ __forceinline__ uint4 stash_of(uint2 w, int64_t d) {
-  return make_uint4(w.x, w.y, (uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32));
-}
-__device__ __forceinline__ uint4 stash_of(uint32_t w, int64_t d) {
-  return make_uint4(w, 0u, (uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32));
-}
-__device__ __forceinline__ void unstash(const uint4& r, uint2& w) { w = make_uint2(r.x, r.y); }
-__device__ __forceinline__ void unstash(const uint4& r, uint32_t& w) { w = r.x; }
-
-template <bool kHarness, int K, bool kNarrow, bool kPersist>
-__global__ __launch_bounds__(kBlock, KWOK_LB_WAVES) void sweep_kernel(SweepArgs a) {
-  typedef typename StateWord<kNarrow>::T W;
-  constexpr uint32_t kWordBytes = sizeof(W);
-  constexpr int V = kNarrow ? KWOK_VEC : 1;  // consecutive words per lane per load
-  static_assert(V == 1 || (V == 4 && K % 4 == 0 && !KWOK_GROUP), "KWOK_VEC: 1, or 4 with K % 4 == 0");
-  __shared__ unsigned int s_stat[kStatWords];
-  __shared__ kwk_delta s_delta[kLdsDeltas];
-  __shared__ uint16_t s_work[kWavesPerBlock][64 * K];
-  __shared__ uint4 s_rec[kWavesPerBlock][kStash];
-  __shared__ uint32_t s_lut[kLutMax];
-  __shared__ kwk_stage_table s_tab;
-#if KWOK_GROUP
-  __shared__ uint16_t s_pos[kWavesPerBlock][64 * K];  // (k, lane) -> work-list position
-#endif
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kBlock * K - 1) / (kBlock * K));
-  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n * kWordBytes);
-  // The state stream of the block's first tile is issued before the LDS set-up below, so its
-  // HBM latency overlaps the table / LUT / delta copies and the barrier; in the persistent
-  // grid the next tile's words are issued as soon as phase 1 of the current one is done
-  // (register double-buffering: the words are dead during phase 2).
-  W v[K];
-  auto issue_tile = [&](const uint32_t tile) {
-    const uint32_t wb = tile * (uint32_t)(kBlock * K) + wave * 64 * V;
-    if constexpr (V == 4) {
-      if ((uint64_t)(tile + 1) * (kBlock * K) <= a.n) {  // one 16-byte load per 4 words
-#pragma unroll
-        for (int q = 0; q < K / 4; ++q) {
-          const auto t = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wb + (uint32_t)q * kBlock * 4 + lane * 4) * 4u, 0, 0);
-          v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-        }
-        return;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) buf_load(v[k], st_rs, (wb + rel_slot<V>(k, lane)) * kWordBytes);
-  };
-  if (blockIdx.x < n_tiles) issue_tile(blockIdx.x);
-  // Phase 2 reads the stage table per lane with divergent indices: staged in LDS they are
-  // ds_reads instead of global loads (header + the loaded stages only).  For programs with
-  // pred_bits <= 8 the match set is one LDS lookup (table built by kwk_load_stages).
-  {
-    const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&s_tab);
-    for (uint32_t j = threadIdx.x; j < nw; j += kBlock) dst[j] = src[j];
-  }
-  const kwk_stage_table* __restrict__ T = &s_tab;
-  const uint32_t n_stages = a.table->n_stages;
-  const uint32_t fin_group = a.table->fin_group_mask;
-  const uint32_t n_deltas = a.table->n_classes * n_stages;
-  const uint32_t lut_n = a.lut_n;
-  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
-  const uint32_t* lut = s_lut;
-  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
-  const kwk_delta* __restrict__ deltas = a.deltas;
-  if (n_deltas <= kLdsDeltas) {
-    for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
-    deltas = s_delta;
-  }
-  __syncthreads();  // s_stat / s_delta / s_tab / s_lut initialised
-
-  W* __restrict__ stw = reinterpret_cast<W*>(a.st);
-  const StateFmt fmt = a.fmt;
-  const RawTest R = a.raw;
-  const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
-  uint16_t* __restrict__ wl = s_work[wave];
-  uint4* __restrict__ wr = s_rec[wave];
-
-  uint32_t n_matched = 0;   // per lane
-  uint32_t n_bytes = 0;     // per lane: algorithmic bytes of the heavy path
-  uint32_t wave_bytes = 0;  // wave-uniform: fired count words
-  uint32_t wave_fired = 0;  // wave-uniform
-
-  // Persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ... so the per-block
-  // set-up (stage deltas into LDS, statistics) is paid once per CU slot, not once per tile.
-  auto tile_body = [&](const uint32_t tile) {
-  const uint32_t wbase = tile * (uint32_t)(kBlock * K) + wave * 64 * V;  // the wave's first slot
-  const uint64_t base = wbase + lane;
-  const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;  // fired segment of (tile, wave)
-  kwk_fired_rec* __restrict__ seg = a.fired + seg_id * (64 * K);
-  const bool full = (uint64_t)(tile + 1) * (kBlock * K) <= a.n;
-  uint32_t seg_n = 0;  // wave-uniform
-
-  // ---- phase 1
-#if KWOK_GROUP
-  unsigned long long rowmask[K];  // wave-uniform: which lanes of row k changed
-#endif
-  uint32_t n_work = 0;  // wave-uniform
-  int64_t d[K];  // due times, loaded only where a stage is pending (else an out-of-range 0)
-  uint32_t pend_bits = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint32_t fw = fw_of(v[k]);
-    const bool pend = (fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code;
-    pend_bits |= (pend ? 1u : 0u) << k;
-    d[k] = buf_load_i64(due_rs, pend ? (wbase + rel_slot<V>(k, lane)) * 8u : kOOB);
-  }
-  {  // streamed words of this lane + its due reads
-    uint32_t in_k = K;
-    if (!full) {
-      in_k = 0;
-      for (int k = 0; k < K; ++k) in_k += (wbase + rel_slot<V>(k, lane) < a.n) ? 1u : 0u;
-    }
-    n_bytes += kWordBytes * in_k + 8u * (uint32_t)__popc(pend_bits);
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint32_t fw = fw_of(v[k]);
-    const uint32_t pw = pw_of(v[k]);
-    // straight bit arithmetic, no short-circuit branches
-    uint32_t nb = (fw & R.dirty) | (((pend_bits >> k) & 1u) & (uint32_t)(d[k] <= a.now));
-    if (kHarness) nb |= (~fw & R.alive) | ((uint32_t)((pw & R.term) != 0) & (uint32_t)((pw & R.del) == 0));
-    const bool need = (nb != 0) & ((fw & R.managed) != 0);
-    const unsigned long long bal = __ballot(need);
-    if (need) {
-      const uint32_t pos = n_work + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-      wl[pos] = (uint16_t)(k * 64 + lane);
-      if (pos < kStash) wr[pos] = stash_of(v[k], d[k]);
-#if KWOK_GROUP
-      s_pos[wave][k * 64 + lane] = (uint16_t)pos;
-#endif
-    }
-#if KWOK_GROUP
-    rowmask[k] = bal;
-#endif
-    n_work += (uint32_t)__popcll(bal);
-  }
-#if !KWOK_GROUP
-  if constexpr (kPersist) {  // prefetch the next tile's words (phase 3 of KWOK_GROUP still reads v)
-    if (tile + gridDim.x < n_tiles) issue_tile(tile + gridDim.x);
-  }
-#endif
-  // ---- phase 2.  Only this wave wrote its list: a wavefront-scope fence (no workgroup
-  // barrier) orders the cross-lane LDS hand-off.
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const uint64_t wave_base = wbase;
-  for (uint32_t c = 0; c < n_work; c += 64) {
-    const uint32_t j = c + lane;
-    Fire f{false, 0, 0, 0};
-    uint64_t i = 0;
-    if (j < n_work) {
-      const uint32_t w = wl[j];
-      i = wave_base + rel_slot<V>(w >> 6, w & 63u);
-      W raw;
-      int64_t due;
-      if (j < kStash) {
-        const uint4 r = wr[j];
-        unstash(r, raw);
-        due = (int64_t)(((uint64_t)r.w << 32) | r.z);
-      } else {  // spill-over beyond the stash: re-read (cache-resident, streamed in phase 1)
-        raw = stw[i];
-        const uint32_t fw = fw_of(raw);
-        due = ((fw & R.managed) && ((fw >> R.sshift) & R.smask) != R.none_code) ? a.due[i] : 0;
-      }
-      const uint2 s = sw_decode(raw, fmt);
-      uint32_t gen_unused = 0;
-      int64_t due_unused = 0;
-      const uint2 nv = process_object<kHarness, kWordBytes>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                            n_matched, lut, lut_n, gen_unused, due_unused);
-      W out;
-      sw_encode(out, nv, fmt);
-#if KWOK_GROUP
-      if (j < kStash) wr[j] = stash_of(out, 0);  // written back in phase 3 with its group
-      else
-#endif
-      if (!KWOK_EXP_NOWRITE) store_word(&stw[i], out);
-    }
-    n_bytes += f.bytes;
-    emit_fired(f, i, lane, seg, seg_n, s_stat, n_bytes);
-  }
-#if KWOK_GROUP
-  // ---- phase 3: aligned groups of KWOK_GROUP lanes rewritten whole wherever any member
-  // changed; unchanged members come from the phase-1 registers (not algorithmic bytes: the
-  // PMC WRITE_SIZE pass shows their cost)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  constexpr unsigned long long kGrpMask = (KWOK_GROUP >= 64) ? ~0ull : ((1ull << KWOK_GROUP) - 1ull);
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const unsigned long long rm = rowmask[k];
-    if (!rm) continue;
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    const uint32_t g0 = lane & ~(uint32_t)(KWOK_GROUP - 1);
-    if ((full || i < a.n) && ((rm >> g0) & kGrpMask)) {
-      W val = v[k];
-      bool write = true;
-      if ((rm >> lane) & 1ull) {
-        const uint32_t p = s_pos[wave][k * 64 + lane];
-        if (p < kStash) unstash(wr[p], val);
-        else write = false;  // spill-over items were written in phase 2
-      }
-      if (write) stw[i] = val;
-    }
-  }
-  if constexpr (kPersist) {
-    if (tile + gridDim.x < n_tiles) issue_tile(tile + gridDim.x);
-  }
-#endif
-
-  // per-(tile, wave) fired count, read by kwk_fired's scan
-  if (lane == 0) a.wave_counts[seg_id] = seg_n;
-  wave_fired += seg_n;
-  wave_bytes += 4u;  // the fired count word
-  // the next tile reuses this wave's LDS lists: keep its phase-1 writes after these reads
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  };  // tile_body
-  if constexpr (kPersist) {
-    for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) tile_body(tile);
-  } else if (blockIdx.x < n_tiles) {  // one block per tile: straight-line code, shorter live ranges
-    tile_body(blockIdx.x);
-  }
-
-  // ---- block statistics
-  for (int off = 32; off > 0; off >>= 1) {
-    n_matched += __shfl_xor(n_matched, off);
-    n_bytes += __shfl_xor(n_bytes, off);
-  }
-  if (lane == 0) {
-    atomicAdd(&s_stat[0], n_matched);
-    atomicAdd(&s_stat[1], wave_fired);
-    atomicAdd(&s_stat[2], n_bytes + wave_bytes);
-    atomicAdd(&s_stat[kStatLine], n_bytes + wave_bytes);  // word-granular stores
-  }
-  __syncthreads();
-  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
-    const unsigned int val = s_stat[threadIdx.x];
-    // no-return atomic: the block does not wait for a read-modify-write round trip
-    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
-  }
+// whole 128-byte line store of one lane's 16-byte chunk (8 lanes = one line), nontemporal:
+// the state column is streamed once per step, keeping it out of L2 leaves room for the
+// due / fired traffic (r1y: 122 -> 119 us)
+__device__ __forceinline__ void store_chunk_nt(void* p, const uint4& v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
 }
 
 // ------------------------------------------------------------------ 2-byte state transition table
@@ -856,34 +550,11 @@ __global__ void fsm_build_kernel(SweepArgs a, uint32_t* __restrict__ tab, int64_
 //           with any changed word is stored whole from LDS (16 bytes per lane).
 // Words past n are never work; chunks past n hold what was loaded (0 past the buffer range),
 // so rewriting them is harmless inside the (tile-padded) allocation.
-#ifndef KWOK_Q16
-#define KWOK_Q16 4  // r1ao: Q = 4 at 4 blocks per CU 113.9 us / idle 42.8 us vs Q = 2 at 6: 116.6 / 47.8
-#endif
-
-#ifndef KWOK_WPE16
-#define KWOK_WPE16 6  // waves per SIMD the register allocation must allow (LDS allows 6 at Q = 2)
-#endif
-#ifndef KWOK_WPE16_Q4
-#define KWOK_WPE16_Q4 4  // Q = 4: the LDS tile + work list allow 4 blocks per CU, so 128 VGPRs
-#endif
-#ifndef KWOK_LDS_DELTAS16
-#define KWOK_LDS_DELTAS16 64  // (class, stage) deltas staged in LDS by the 2-byte sweep (<= 11-bit programs)
-#endif
-#ifndef KWOK_NT16
-#define KWOK_NT16 1  // phase-3 line stores with the nontemporal hint (r1y: 122 -> 119 us)
-#endif
-#ifndef KWOK_PF_LATE
-#define KWOK_PF_LATE 0
-#endif
-#ifndef KWOK_PF_EARLY
-#define KWOK_PF_EARLY 1  // issue the next tile's loads before phase 1 of this one
-#endif
-#ifndef KWOK_STORE_LANES
-#define KWOK_STORE_LANES 8  // phase-3 store group: 8 lanes = one 128-byte line (2 = 32-byte sectors)
-#endif
-#ifndef KWOK_PF16
-#define KWOK_PF16 1  // tiles in flight per wave in the persistent grid (1 or 2)
-#endif
+constexpr uint32_t kQ16 = 4;  // r1ao: Q = 4 at 4 blocks per CU 113.9 us / idle 42.8 us vs Q = 2 at 6: 116.6 / 47.8
+constexpr int kWpe16 = 6;     // waves per SIMD the register allocation must allow (LDS allows 6 at Q = 2)
+constexpr int kWpe16Q4 = 4;   // Q = 4: the LDS tile + work list allow 4 blocks per CU, so 128 VGPRs
+constexpr int kLdsDeltas16 = 64;  // (class, stage) deltas staged in LDS by the 2-byte sweep (<= 11-bit programs)
+constexpr uint32_t kStoreLanes = 8;  // phase-3 store group: 8 lanes x 16 bytes = one 128-byte line
 // word offset (minus lane * 8) of bit b of a lane's phase-1 masks in the 2-byte sweep
 __device__ __forceinline__ constexpr uint32_t bit_word(const uint32_t b) {
   return ((b & 15u) >> 2) * 512u + 2u * (b & 3u) + (b >> 4);
@@ -891,13 +562,13 @@ __device__ __forceinline__ constexpr uint32_t bit_word(const uint32_t b) {
 template <int Q>
 constexpr uint32_t seg16_words() { return 64u * 8u * Q + 32u; }  // count + records + padding line
 #define kSeg16 seg16_words<Q>()
-template <bool kHarness, int Q, bool kPersist, int kDepth = KWOK_PF16>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ? KWOK_WPE16_Q4 : KWOK_WPE16))) void sweep16_kernel(SweepArgs a) {
+template <bool kHarness, int Q, bool kPersist>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ? kWpe16Q4 : kWpe16))) void sweep16_kernel(SweepArgs a) {
   constexpr int K = 8 * Q;                 // words per lane
   constexpr uint32_t kWave = 64u * K;      // words per wave region
   constexpr uint32_t kTile = kBlock * K;   // words per block
   __shared__ unsigned int s_stat[kStatWords];
-  __shared__ kwk_delta s_delta[KWOK_LDS_DELTAS16];
+  __shared__ kwk_delta s_delta[kLdsDeltas16];
   __shared__ uint16_t s_work[kWavesPerBlock][kWave];
   __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
   __shared__ uint32_t s_lut[kLutMax];
@@ -908,8 +579,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   // load range rounded to 16 bytes (the allocation is tile-padded): a chunk holding the last
   // words comes back whole
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * 2u) + 15u) & ~15u);
-  // kDepth tiles in flight per wave (persistent grid): register buffers va (and vb)
-  uint4 va[Q], vb[Q];
+  // one tile in flight per wave while the previous one is worked on (persistent grid): register
+  // buffer va (a second buffer spilled VGPRs: 125-149 us, r1al)
+  uint4 va[Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) {
     if (t >= n_tiles) return;
     const uint32_t wb = t * kTile + wave * kWave;
@@ -921,8 +593,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   };
   uint32_t tile = blockIdx.x;
   issue_tile(va, tile);
-  if (kPersist && kDepth == 2) issue_tile(vb, tile + gridDim.x);
-  {  // LDS set-up overlaps the stream's latency (see sweep_kernel)
+  {  // LDS set-up overlaps the stream's latency
     const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&s_tab);
@@ -936,7 +607,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   const kwk_delta* __restrict__ deltas = a.deltas;
-  if (n_deltas <= KWOK_LDS_DELTAS16) {
+  if (n_deltas <= kLdsDeltas16) {
     for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
     deltas = s_delta;
   }
@@ -978,11 +649,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     kwk_fired_rec* __restrict__ seg = reinterpret_cast<kwk_fired_rec*>(seg32 + 1);
 
     // the tile's words leave the prefetch buffer; the next tile's loads are issued before
-    // phase 1 (KWOK_PF_EARLY), so they overlap this tile's idle test as well as phases 2-3
+    // phase 1, so they overlap this tile's idle test as well as phases 2-3 (r1as: 114.8 ->
+    // 112.4 us against issuing them after phase 1)
     uint4 cur[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) cur[q] = v[q];
-    if (kPersist && KWOK_PF_EARLY) issue_tile(v, tile + kDepth * gridDim.x);
+    if (kPersist) issue_tile(v, tile + gridDim.x);
     // ---- phase 1: idle test on the raw words.  bit k = q * 8 + h of a lane's masks
     // bit b of a lane's masks: dword (b & 15) of the lane's 4Q dwords (row (b & 15) / 4),
     // its low word for b < 16, its high word for b >= 16 (so the SWAR flags at bits 15 / 31
@@ -1049,9 +721,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         wl[pos++] = (uint16_t)(bit_word(k) + lane * 8u + (((ready >> k) & 1u) << 15));
       }
     }
-    // refill this buffer here instead (KWOK_PF_EARLY=0).  KWOK_PF_LATE: only after phase 2,
-    // whose table lookups would otherwise wait for it (vmcnt retires in issue order)
-    if (kPersist && !KWOK_PF_EARLY && (!KWOK_PF_LATE || !n_work)) issue_tile(v, tile + kDepth * gridDim.x);
 
     if (n_work) {
       // ---- phase 2
@@ -1099,7 +768,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         n_bytes += f.bytes;
         emit_fired<true>(f, i - wbase, lane, seg, seg_n, s_stat, n_bytes);
       }
-      if (kPersist && !KWOK_PF_EARLY && KWOK_PF_LATE) issue_tile(v, tile + kDepth * gridDim.x);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       // ---- phase 3: whole 128-byte lines wherever a word changed
 #pragma unroll
@@ -1107,15 +775,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         const uint4 nv = tq[q * 64 + lane];
         const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
         const unsigned long long bal = __ballot(ch);
-        if ((bal >> (lane & ~(KWOK_STORE_LANES - 1u))) & ((1ull << KWOK_STORE_LANES) - 1ull)) {
-          if (!KWOK_EXP_NOWRITE) {
-            if (KWOK_NT16) {
-              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-              __builtin_nontemporal_store(u32x4{nv.x, nv.y, nv.z, nv.w},
-                                          reinterpret_cast<u32x4*>(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u]));
-            }
-            else gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u] = nv;
-          }
+        if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
+          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);
           n_line += 16u;
         }
       }
@@ -1125,7 +786,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     {
       const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
       for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
-      if (lane == 0) seg32[0] = seg_n;
+      if (lane == 0) {
+        seg32[0] = seg_n;
+        a.wave_counts[seg_id] = seg_n;  // the hand-back's scan input
+      }
       n_line += 4u * (uint32_t)__popc((uint32_t)(lane < end - used));  // padding: line bytes only
     }
     wave_fired += seg_n;
@@ -1133,13 +797,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   };
   if constexpr (!kPersist) {
     if (tile < n_tiles) tile_body(va, tile);
-  } else if constexpr (kDepth == 1) {
-    for (; tile < n_tiles; tile += gridDim.x) tile_body(va, tile);
   } else {
-    for (; tile < n_tiles; tile += 2 * gridDim.x) {
-      tile_body(va, tile);
-      if (tile + gridDim.x < n_tiles) tile_body(vb, tile + gridDim.x);
-    }
+    for (; tile < n_tiles; tile += gridDim.x) tile_body(va, tile);
   }
 
   // ---- block statistics
@@ -1161,33 +820,286 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   }
 }
 
-// per-wave fired counts of the 2-byte sweep (the first word of each segment) for the scan
-__global__ void seg_counts_kernel(const uint32_t* __restrict__ fired32, uint32_t n_waves, uint32_t stride,
-                                  uint32_t* __restrict__ counts) {
-  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < n_waves) counts[w] = fired32[(uint64_t)w * stride];
-}
+// ------------------------------------------------------------------ 4- and 8-byte state sweep
+// Sweep over the 4-byte packed and the 8-byte wide formats (pod-general / chaos and any
+// program wider than 16 bits: no transition table, every work item runs process_object).
+// Same three phases and the same whole-line write-back as sweep16_kernel — the word-granular
+// write-back it replaces cost a line fill plus a partial-line write per scattered store
+// (r1o: 1.09 GB of HBM traffic against 0.534 GB algorithmic at 100M pods):
+//  phase 1  each lane streams Q 16-byte chunks (kC = 16 / word bytes words each) of its
+//           wave's region, row q of a wave = 1 KiB contiguous; due times only for words with
+//           a pending stage (and only if the wave has one); the idle test on the raw words;
+//           the per-lane need masks become the wave's LDS work list in slot order, each entry
+//           carrying "the queued stage is due" so phase 2 never re-reads the due column;
+//  phase 2  the chunks go to the wave's LDS tile; process_object runs over the dense work
+//           list, reading and writing the word in LDS (a due time is written only when a
+//           newly scheduled stage stays pending), and emits packed fired records into the
+//           (tile, wave) segment;
+//  phase 3  aligned 8-lane groups (one 128-byte line) holding a changed word are stored whole.
+constexpr int kQW = 4;                 // 16-byte chunks per lane: 16 (4-byte) / 8 (8-byte) words per lane
+constexpr int kLdsDeltasW = 256;       // (class, stage) deltas staged in LDS by the word sweep
 
-// gather the per-wave fired segments into one dense list (offsets from an exclusive scan)
-__global__ void compact_fired_kernel(const kwk_fired_rec* __restrict__ fired, const uint32_t* __restrict__ counts,
-                                     const uint32_t* __restrict__ offsets, uint32_t n_waves, uint32_t wave_seg,
-                                     uint32_t packed, kwk_fired_rec* __restrict__ out) {
-  const uint32_t w = blockIdx.x;
-  if (w >= n_waves) return;
-  const uint32_t c = counts[w];
-  const uint32_t o = offsets[w];
-  if (packed) {  // 2-byte sweep: segment w = [count][emit_fired<true> records] at w * (wave_seg + 32)
-                 // words, covering slots w * wave_seg + [0, wave_seg)
-    const uint32_t* f32 = reinterpret_cast<const uint32_t*>(fired) + (uint64_t)w * (wave_seg + 32u) + 1u;
-    for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) {
-      const uint32_t r = f32[j];
-      out[o + j] = kwk_fired_rec{w * wave_seg + (r & 0x7FFu), (uint16_t)((r >> 11) & 31u), (uint16_t)((r >> 16) & 7u)};
-    }
-    return;
+template <uint32_t kWB> struct WordOf { typedef uint32_t T; };
+template <> struct WordOf<8> { typedef uint2 T; };
+
+// word j of a 16-byte chunk
+__device__ __forceinline__ uint32_t chunk_word(const uint4& c, int j, uint32_t*) {
+  return j == 0 ? c.x : j == 1 ? c.y : j == 2 ? c.z : c.w;
+}
+__device__ __forceinline__ uint2 chunk_word(const uint4& c, int j, uint2*) {
+  return j == 0 ? make_uint2(c.x, c.y) : make_uint2(c.z, c.w);
+}
+__device__ __forceinline__ uint32_t flag_word(uint32_t w) { return w; }  // word holding flags + stage
+__device__ __forceinline__ uint32_t flag_word(uint2 w) { return w.y; }
+__device__ __forceinline__ uint32_t pred_word(uint32_t w) { return w; }  // word holding pred
+__device__ __forceinline__ uint32_t pred_word(uint2 w) { return w.x; }
+
+template <bool kHarness, uint32_t kWB>
+__global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
+  typedef typename WordOf<kWB>::T W;
+  constexpr int kC = 16 / (int)kWB;        // words per chunk
+  constexpr int K = kC * kQW;              // words per lane
+  constexpr uint32_t kWave = 64u * K;      // words per wave region (<= 1024: 10-bit work entries)
+  constexpr uint32_t kTile = kBlock * K;
+  static_assert(kWave <= 2048, "fired records carry an 11-bit slot within the wave region");
+  __shared__ unsigned int s_stat[kStatWords];
+  __shared__ kwk_delta s_delta[kLdsDeltasW];
+  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint4 s_tile[kWavesPerBlock][64 * kQW];
+  __shared__ uint32_t s_lut[kLutMax];
+  __shared__ kwk_stage_table s_tab;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t tile = blockIdx.x;        // one block per tile
+  const uint32_t wbase = tile * kTile + wave * kWave;
+  // the tile's stream is issued before the LDS set-up so its latency overlaps it
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * kWB) + 15u) & ~15u);
+  uint4 cur[kQW];
+#pragma unroll
+  for (int q = 0; q < kQW; ++q) {
+    const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wbase + (uint32_t)q * 64u * kC + lane * kC) * kWB, 0, 0);
+    cur[q] = make_uint4(c[0], c[1], c[2], c[3]);
   }
-  for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) out[o + j] = fired[(uint64_t)w * wave_seg + j];
+  {
+    const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&s_tab);
+    for (uint32_t j = threadIdx.x; j < nw; j += kBlock) dst[j] = src[j];
+  }
+  const kwk_stage_table* __restrict__ T = &s_tab;
+  const uint32_t n_stages = a.table->n_stages;
+  const uint32_t fin_group = a.table->fin_group_mask;
+  const uint32_t n_deltas = a.table->n_classes * n_stages;
+  const uint32_t lut_n = a.lut_n;
+  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
+  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  const kwk_delta* __restrict__ deltas = a.deltas;
+  if (n_deltas <= (uint32_t)kLdsDeltasW) {
+    for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
+    deltas = s_delta;
+  }
+  __syncthreads();
+
+  const StateFmt fmt = a.fmt;
+  const RawTest R = a.raw;
+  uint32_t n_matched = 0, n_bytes = 0, n_line = 0;  // per lane
+  uint16_t* __restrict__ wl = s_work[wave];
+  uint4* __restrict__ tq = s_tile[wave];
+  W* __restrict__ tw = reinterpret_cast<W*>(tq);
+  const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
+  const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
+  uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * (kWave + 32u);
+  kwk_fired_rec* __restrict__ seg = reinterpret_cast<kwk_fired_rec*>(seg32 + 1);
+  uint32_t seg_n = 0;  // wave-uniform
+
+  // ---- phase 1: bit k = q * kC + j of a lane's masks <-> word q * 64 * kC + lane * kC + j
+  uint32_t need = 0, pend = 0, in_range = 0;
+#pragma unroll
+  for (int q = 0; q < kQW; ++q) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      const W w = chunk_word(cur[q], j, (W*)nullptr);
+      const uint32_t fw = flag_word(w), pw = pred_word(w);
+      const uint32_t off = (uint32_t)q * 64u * kC + lane * kC + (uint32_t)j;
+      const uint32_t in = (full || wbase + off < a.n) ? 1u : 0u;
+      const uint32_t mg = (fw & R.managed) ? in : 0u;
+      const uint32_t pe = ((fw >> R.sshift) & R.smask) != R.none_code ? 1u : 0u;
+      uint32_t nb = (fw & R.dirty) ? 1u : 0u;
+      if (kHarness) nb |= ((~fw & R.alive) ? 1u : 0u) | (((pw & R.term) != 0 && (pw & R.del) == 0) ? 1u : 0u);
+      const int k = q * kC + j;
+      need |= (mg & nb) << k;
+      pend |= (mg & pe) << k;
+      in_range |= in << k;
+    }
+  }
+  uint32_t ready = 0;
+  if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
+    const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t p = (pend >> k) & 1u;
+      const uint32_t off = (uint32_t)(k / kC) * 64u * kC + lane * kC + (uint32_t)(k % kC);
+      const int64_t d = buf_load_i64(due_rs, p ? (wbase + off) * 8u : kOOB);
+      ready |= (p & (uint32_t)(d <= a.now)) << k;
+    }
+    need |= ready;
+  }
+  n_bytes += kWB * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
+  // work list in slot order: exclusive prefix of the per-lane counts (counts <= 16)
+  uint32_t n_work = 0, pos = 0;  // n_work wave-uniform
+  {
+    const uint32_t cnt = (uint32_t)__popc(need);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const unsigned long long bal = __ballot((cnt >> b) & 1u);
+      pos += (uint32_t)__popcll(bal & lt) << b;
+      n_work += (uint32_t)__popcll(bal) << b;
+    }
+    for (uint32_t m = need; m; m &= m - 1u) {
+      const uint32_t k = (uint32_t)__ffs(m) - 1u;
+      const uint32_t off = (k / kC) * 64u * kC + lane * kC + (k % kC);
+      wl[pos++] = (uint16_t)(off | (((ready >> k) & 1u) << 15));
+    }
+  }
+
+  if (n_work) {
+    // ---- phase 2
+#pragma unroll
+    for (int q = 0; q < kQW; ++q) tq[q * 64 + lane] = cur[q];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t c = 0; c < n_work; c += 64u) {
+      const uint32_t jw = c + lane;
+      Fire f{false, 0, 0, 0};
+      uint32_t off = 0;
+      if (jw < n_work) {
+        const uint32_t we = wl[jw];
+        off = we & 0x7FFFu;
+        const uint64_t i = wbase + off;
+        const uint2 s = sw_decode(tw[off], fmt);
+        // the queued stage's due time matters only as "due <= now" (a new match overwrites
+        // it), which phase 1 already decided
+        const int64_t due = (we >> 15) ? INT64_MIN : INT64_MAX;
+        uint32_t gen_unused = 0;
+        int64_t due_unused = 0;
+        const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
+                                                       n_matched, s_lut, lut_n, gen_unused, due_unused);
+        W out;
+        sw_encode(out, nv, fmt);
+        tw[off] = out;
+        n_line -= kWB;  // the word's own write is replaced by the line stores below
+      }
+      n_bytes += f.bytes;
+      emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- phase 3: whole 128-byte lines wherever a word changed
+    uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+#pragma unroll
+    for (int q = 0; q < kQW; ++q) {
+      const uint4 nv = tq[q * 64 + lane];
+      const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
+      const unsigned long long bal = __ballot(ch);
+      if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
+        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);
+        n_line += 16u;
+      }
+    }
+  }
+  {  // segment: [count][records], padded to whole 128-byte lines
+    const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
+    for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
+    if (lane == 0) {
+      seg32[0] = seg_n;
+      a.wave_counts[seg_id] = seg_n;  // the hand-back's scan input
+    }
+    n_line += 4u * (uint32_t)__popc((uint32_t)(lane < end - used));
+  }
+  n_bytes += lane == 0 ? 4u : 0u;  // the fired count word
+
+  for (int o = 32; o > 0; o >>= 1) {
+    n_matched += __shfl_xor(n_matched, o);
+    n_bytes += __shfl_xor(n_bytes, o);
+    n_line += __shfl_xor(n_line, o);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_stat[0], n_matched);
+    atomicAdd(&s_stat[1], seg_n);
+    atomicAdd(&s_stat[2], n_bytes);
+    atomicAdd(&s_stat[kStatLine], n_bytes + n_line);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
+    const unsigned int val = s_stat[threadIdx.x];
+    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
+  }
 }
 
+// ------------------------------------------------------------------ fired hand-back
+// One pass over the sweep's per-(tile, wave) segments: a single-pass scan with decoupled
+// look-back over the per-segment counts (which the sweep writes into `counts`), then each wave
+// expands its segment's 4-byte records {slot within the wave region: 11, stage: 5, flags: 3}
+// into kwk_fired_rec at its offset of one dense list, in slot order.  A block's place in the
+// scan is a ticket drawn on arrival (so every predecessor it waits on is already running);
+// status words are 8-byte agent-scope atomics {epoch: 30, flag: 2 | value: 32}, the epoch
+// distinguishes this launch's entries from earlier ones (no reset between launches).
+constexpr uint32_t kSegsPerBlock = kWavesPerBlock;  // one wave per segment
+struct CompactArgs {
+  const uint32_t* __restrict__ fired32;   // segments, `stride` words apart: [count][records]
+  const uint32_t* __restrict__ counts;    // records per segment
+  kwk_fired_rec* __restrict__ out;
+  uint32_t* __restrict__ total;           // number of records (written by the last block)
+  unsigned long long* __restrict__ status;  // per block
+  unsigned long long* __restrict__ ticket;  // monotone arrival counter (never reset)
+  unsigned long long ticket_base;           // its value before this launch
+  uint32_t n_segs;
+  uint32_t seg_slots;                     // object slots per segment (wave region)
+  uint32_t stride;
+  uint32_t epoch;                         // 30 bits
+};
+
+__global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
+  __shared__ uint32_t s_blk, s_prefix, s_cnt[kSegsPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0)
+    s_blk = (uint32_t)(__hip_atomic_fetch_add(a.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket_base);
+  __syncthreads();
+  const uint32_t blk = s_blk;
+  const uint32_t seg = blk * kSegsPerBlock + wave;
+  const uint32_t c = seg < a.n_segs ? a.counts[seg] : 0u;
+  if (lane == 0) s_cnt[wave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t agg = 0;
+    for (uint32_t w = 0; w < kSegsPerBlock; ++w) agg += s_cnt[w];
+    const unsigned long long tag = (unsigned long long)(a.epoch & 0x3FFFFFFFu) << 34;
+    uint32_t prefix = 0;
+    if (blk > 0) {
+      __hip_atomic_store(&a.status[blk], tag | (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t j = blk - 1;;) {
+        const unsigned long long st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((st >> 34) != (tag >> 34)) continue;  // not yet published in this launch: its block is running
+        prefix += (uint32_t)st;
+        if (((st >> 32) & 3u) == 2u) break;       // an inclusive prefix: done
+        --j;                                      // an aggregate: keep looking back
+      }
+    }
+    __hip_atomic_store(&a.status[blk], tag | (2ull << 32) | (uint32_t)(prefix + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    s_prefix = prefix;
+    if ((blk + 1) * kSegsPerBlock >= a.n_segs) *a.total = prefix + agg;
+  }
+  __syncthreads();
+  uint32_t off = s_prefix;
+  for (uint32_t w = 0; w < wave; ++w) off += s_cnt[w];
+  const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
+  for (uint32_t j = lane; j < c; j += 64) {
+    const uint32_t r = f32[j];
+    a.out[off + j] = kwk_fired_rec{seg * a.seg_slots + (r & 0x7FFu), (uint16_t)((r >> 11) & 31u), (uint16_t)((r >> 16) & 7u)};
+  }
+}
+
+// sums the per-block statistics rows [0, n_blocks) (the rows any sweep grid has used)
 __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, uint32_t n_blocks,
                                     unsigned long long* __restrict__ out) {
   const uint32_t word = blockIdx.x;  // one workgroup per statistic word
@@ -1314,133 +1226,223 @@ __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uin
 }
 
 // ------------------------------------------------------------------ resource usage
-// One wave per node: lanes stride over the node's (node-sorted) pods, gather the pod's
-// cpu / memory value from the interned dictionaries, multiply by its container count and
-// reduce with shuffles.  Dead pods (not in the pod cache) contribute nothing.
-// server/metrics_resource_usage.go:170-224 (sums), :36-109 (cumulative integrators).
+// server/metrics_resource_usage.go:170-224 (pod / node sums), :36-109 (cumulative integrators).
+// One wave per group of kUG consecutive nodes: the group's node-sorted pods form one contiguous
+// range that the wave streams kUU passes of 64 pods at a time (all loads of a batch in flight
+// before any is used: enough bytes in flight per CU to stream instead of waiting on each
+// node's latency chain).  A pod contributes containers x its interned cpu / memory value (dead
+// pods — not in the pod cache — nothing); each pass is reduced per node with a segmented scan
+// across the lanes (pods of one node are contiguous), whose segment tails add into the node's
+// LDS accumulator: a fixed order, so results are reproducible run to run.  The reference adds
+// pods in SyncMap order (unordered, utils/maps/sync.go:93-100), so sums agree with it to
+// floating-point reassociation: the tests hold them to 1e-6 relative (north_star).
 // With per-pod outputs enabled (kwk_usage_pods) every pod also gets its Usage (podResourceUsage,
 // :170-193) and its cumulative usage (podResourceCumulativeUsage, :54-65: the sum of its
 // containers' integrators, each advanced by (now - last) * value, :36-52); a dead pod reads 0
 // and keeps its integrators (Go keys them by name, so a re-created pod continues them).
-__global__ __launch_bounds__(kBlock) void usage_kernel(const void* __restrict__ st, StateFmt fmt,
-                                                       const uint32_t* __restrict__ node_ptr,
-                                                       const uint32_t* __restrict__ ukey,
-                                                       const double* __restrict__ cpu_v,
-                                                       const double* __restrict__ mem_v, uint32_t n_nodes,
-                                                       double* __restrict__ node_out, double* __restrict__ cum,
-                                                       int64_t* __restrict__ last_t, int64_t now,
-                                                       double* __restrict__ block_part, double* __restrict__ pod_out,
-                                                       double* __restrict__ pod_cum, int64_t* __restrict__ pod_last) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t node = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  double c = 0.0, m = 0.0;
-  if (node < n_nodes) {
-    const uint32_t lo = node_ptr[node], hi = node_ptr[node + 1];
-    for (uint32_t p = lo + lane; p < hi; p += 64) {
-      const uint32_t sched = load_state(st, p, fmt).y;
-      if (!(sched & KWK_F_ALIVE)) {
-        if (pod_out) reinterpret_cast<double4*>(pod_out)[p] = make_double4(0.0, 0.0, 0.0, 0.0);
-        continue;
-      }
-      const uint32_t k = ukey[p];
-      const double nc = (double)(k >> 28);
-      const double pc = nc * cpu_v[k & 0x3FFFu];
-      const double pm = nc * mem_v[(k >> 14) & 0x3FFFu];
-      c += pc;
-      m += pm;
-      if (pod_out) {
-        double2 pcum = reinterpret_cast<double2*>(pod_cum)[p];
-        const int64_t lt = pod_last[p];
-        if (lt != INT64_MIN) {
-          const int64_t d = now - lt;
-          const double dt = (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
-          pcum.x += dt * pc;
-          pcum.y += dt * pm;
-          reinterpret_cast<double2*>(pod_cum)[p] = pcum;
+constexpr uint32_t kUG = 16;  // nodes per wave
+constexpr int kUU = 4;        // passes of 64 pods with loads in flight together
+struct UsageArgs {
+  const void* __restrict__ st;
+  StateFmt fmt;
+  const uint32_t* __restrict__ node_ptr;
+  const uint32_t* __restrict__ ukey;
+  const double* __restrict__ cpu_v;
+  const double* __restrict__ mem_v;
+  uint32_t n_nodes;
+  uint32_t n_pods;
+  double* __restrict__ node_out;   // n_nodes x {cpu, mem, cpu_cum, mem_cum}
+  double* __restrict__ cum;        // n_nodes x {cpu, mem}
+  int64_t* __restrict__ last_t;
+  int64_t now;
+  double* __restrict__ block_part;  // per block {cpu, mem}
+  double* __restrict__ pod_out;     // optional per pod outputs
+  double* __restrict__ pod_cum;
+  int64_t* __restrict__ pod_last;
+};
+
+// time.Duration.Seconds() of now - last
+__device__ __forceinline__ double dur_seconds(int64_t d) {
+  return (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
+}
+
+__global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
+  __shared__ double s_acc[kWavesPerBlock][kUG][2];
+  __shared__ uint32_t s_bnd[kWavesPerBlock][kUG + 1];
+  __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t j0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kUG;
+  const uint32_t jn = j0 < a.n_nodes ? (uint32_t)min((uint64_t)kUG, a.n_nodes - j0) : 0u;
+  if (lane < kUG) { s_acc[wave][lane][0] = 0.0; s_acc[wave][lane][1] = 0.0; }
+  if (lane <= jn && jn) s_bnd[wave][lane] = a.node_ptr[j0 + lane];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t lo = jn ? s_bnd[wave][0] : 0u, hi = jn ? s_bnd[wave][jn] : 0u;
+  uint32_t nl = 0;  // the lane's current node within the group (pods only move forward)
+  for (uint32_t base = lo; base < hi; base += 64u * kUU) {
+    uint32_t sched[kUU], key[kUU];
+#pragma unroll
+    for (int u = 0; u < kUU; ++u) {  // all loads of the batch first
+      const uint32_t p = base + (uint32_t)u * 64u + lane;
+      sched[u] = p < hi ? load_state(a.st, p, a.fmt).y : 0u;
+      key[u] = p < hi ? a.ukey[p] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kUU; ++u) {
+      const uint32_t p = base + (uint32_t)u * 64u + lane;
+      if (base + (uint32_t)u * 64u >= hi) break;  // wave-uniform
+      const bool valid = p < hi;
+      double vc = 0.0, vm = 0.0;
+      if (valid) {
+        while (nl + 1 < jn && p >= s_bnd[wave][nl + 1]) ++nl;
+        if (sched[u] & KWK_F_ALIVE) {
+          const double nc = (double)(key[u] >> 28);
+          vc = nc * a.cpu_v[key[u] & 0x3FFFu];
+          vm = nc * a.mem_v[(key[u] >> 14) & 0x3FFFu];
         }
-        pod_last[p] = now;
-        reinterpret_cast<double4*>(pod_out)[p] = make_double4(pc, pm, pcum.x, pcum.y);
+        if (a.pod_out) {
+          if (sched[u] & KWK_F_ALIVE) {
+            double2 pcum = reinterpret_cast<double2*>(a.pod_cum)[p];
+            const int64_t lt = a.pod_last[p];
+            if (lt != INT64_MIN) {
+              const double dt = dur_seconds(a.now - lt);
+              pcum.x += dt * vc;
+              pcum.y += dt * vm;
+              reinterpret_cast<double2*>(a.pod_cum)[p] = pcum;
+            }
+            a.pod_last[p] = a.now;
+            reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(vc, vm, pcum.x, pcum.y);
+          } else {
+            reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(0.0, 0.0, 0.0, 0.0);
+          }
+        }
+      }
+      // segmented inclusive scan over the lanes, keyed by node (contiguous segments)
+      const uint32_t seg = valid ? nl : 0xFFFFu;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double uc = __shfl_up(vc, o), um = __shfl_up(vm, o);
+        const uint32_t us = __shfl_up(seg, o);
+        if (lane >= (uint32_t)o && us == seg) { vc += uc; vm += um; }
+      }
+      const uint32_t next = __shfl_down(seg, 1);
+      if (valid && (lane == 63 || next != seg)) {  // segment tail: one lane per node and pass
+        s_acc[wave][seg][0] += vc;
+        s_acc[wave][seg][1] += vm;
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    c += __shfl_xor(c, off);
-    m += __shfl_xor(m, off);
-  }
-  __shared__ double s_c[kBlock / 64], s_m[kBlock / 64];
-  if (lane == 0) {
-    if (node < n_nodes) {
-      node_out[node * 4 + 0] = c;
-      node_out[node * 4 + 1] = m;
-      const int64_t lt = last_t[node];
-      if (lt != INT64_MIN) {
-        const int64_t d = now - lt;  // now.Sub(c.time).Seconds() (time.Duration.Seconds)
-        const double dt = (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
-        cum[node * 2 + 0] += dt * c;
-        cum[node * 2 + 1] += dt * m;
-      }
-      last_t[node] = now;
-      node_out[node * 4 + 2] = cum[node * 2 + 0];
-      node_out[node * 4 + 3] = cum[node * 2 + 1];
-    } else {
-      c = 0.0;
-      m = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  double c = 0.0, m = 0.0;
+  if (lane < jn) {
+    const uint64_t node = j0 + lane;
+    c = s_acc[wave][lane][0];
+    m = s_acc[wave][lane][1];
+    double2 cm = reinterpret_cast<double2*>(a.cum)[node];
+    const int64_t lt = a.last_t[node];
+    if (lt != INT64_MIN) {  // now.Sub(c.time).Seconds()
+      const double dt = dur_seconds(a.now - lt);
+      cm.x += dt * c;
+      cm.y += dt * m;
+      reinterpret_cast<double2*>(a.cum)[node] = cm;
     }
-    s_c[threadIdx.x >> 6] = c;
-    s_m[threadIdx.x >> 6] = m;
+    a.last_t[node] = a.now;
+    reinterpret_cast<double4*>(a.node_out)[node] = make_double4(c, m, cm.x, cm.y);
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    m += __shfl_xor(m, o);
+  }
+  if (lane == 0) { s_c[wave] = c; s_m[wave] = m; }
   __syncthreads();
   if (threadIdx.x == 0) {
     double tc = 0, tm = 0;
-    for (int i = 0; i < kBlock / 64; ++i) { tc += s_c[i]; tm += s_m[i]; }
-    block_part[blockIdx.x * 2 + 0] = tc;
-    block_part[blockIdx.x * 2 + 1] = tm;
+    for (int i = 0; i < kWavesPerBlock; ++i) { tc += s_c[i]; tm += s_m[i]; }
+    a.block_part[blockIdx.x * 2 + 0] = tc;
+    a.block_part[blockIdx.x * 2 + 1] = tm;
+  }
+}
+
+// cluster totals: the per-block partials summed in a fixed order (1024 threads)
+__global__ __launch_bounds__(1024) void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks,
+                                                           double* __restrict__ out) {
+  double c = 0, m = 0;
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) { c += part[b * 2]; m += part[b * 2 + 1]; }
+  for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o); m += __shfl_xor(m, o); }
+  __shared__ double sc[16], sm[16];
+  if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = c; sm[threadIdx.x >> 6] = m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tc = 0, tm = 0;
+    for (uint32_t i = 0; i < blockDim.x / 64; ++i) { tc += sc[i]; tm += sm[i]; }
+    out[0] = tc;
+    out[1] = tm;
   }
 }
 
 // count alive objects with (pred & mask[k]) != 0 for each k (mask 0: every alive object):
-// phase histograms and other cluster aggregates.  One wave per 64*16 objects; per-block LDS
-// totals, one 64-bit atomic per block and mask.
+// phase histograms and other cluster aggregates.  Each lane streams 16-byte chunks of the
+// state column (8, 4 or 2 words), per-lane counters in registers, one 64-bit atomic per block
+// and mask.
 constexpr int kMaxCountMasks = 16;
 __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, StateFmt fmt, uint32_t n,
                                                        const uint32_t* __restrict__ masks, uint32_t n_masks,
                                                        unsigned long long* __restrict__ out) {
   __shared__ unsigned int s_cnt[kMaxCountMasks];
-  if (threadIdx.x < kMaxCountMasks) s_cnt[threadIdx.x] = 0;
+  __shared__ uint32_t s_masks[kMaxCountMasks];
+  if (threadIdx.x < kMaxCountMasks) {
+    s_cnt[threadIdx.x] = 0;
+    s_masks[threadIdx.x] = threadIdx.x < n_masks ? masks[threadIdx.x] : 0u;
+  }
   __syncthreads();
   uint32_t cnt[kMaxCountMasks];
-  for (int m = 0; m < kMaxCountMasks; ++m) cnt[m] = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * (kBlock * 16) + threadIdx.x;
-#pragma unroll 4
-  for (int k = 0; k < 16; ++k) {
-    const uint64_t i = base + (uint64_t)k * kBlock;
-    if (i >= n) break;
-    const uint2 v = load_state(st, i, fmt);
-    if (!(v.y & KWK_F_ALIVE)) continue;
-    for (uint32_t m = 0; m < n_masks; ++m) cnt[m] += (masks[m] == 0 || (v.x & masks[m])) ? 1u : 0u;
+  uint32_t mk[kMaxCountMasks];
+#pragma unroll
+  for (int m = 0; m < kMaxCountMasks; ++m) { cnt[m] = 0; mk[m] = s_masks[m]; }
+  const uint32_t wb = fmt.half ? 2u : fmt.narrow ? 4u : 8u;
+  const uint32_t wpc = 16u / wb;  // words per chunk
+  const uint64_t n_chunks = ((uint64_t)n * wb + 15u) / 16u;
+  const uint4* __restrict__ q = reinterpret_cast<const uint4*>(st);
+  auto tally = [&](uint32_t pred, uint32_t sched) {
+    if (!(sched & KWK_F_ALIVE)) return;
+#pragma unroll
+    for (int m = 0; m < kMaxCountMasks; ++m)
+      cnt[m] += ((uint32_t)m < n_masks && (mk[m] == 0u || (pred & mk[m]) != 0u)) ? 1u : 0u;
+  };
+  for (uint64_t ch = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ch < n_chunks; ch += (uint64_t)gridDim.x * kBlock) {
+    const uint4 v = q[ch];
+    const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+    const uint64_t i0 = ch * wpc;
+    if (fmt.half) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (i0 + j < n) {
+          const uint2 u = fmt_unpack((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, fmt);
+          tally(u.x, u.y);
+        }
+      }
+    } else if (fmt.narrow) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (i0 + j < n) {
+          const uint2 u = fmt_unpack(dw[j], fmt);
+          tally(u.x, u.y);
+        }
+      }
+    } else {
+      tally(v.x, v.y);
+      if (i0 + 1 < n) tally(v.z, v.w);
+    }
   }
-  for (uint32_t m = 0; m < n_masks; ++m) {
-    uint32_t c = cnt[m];
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
+#pragma unroll
+  for (int m = 0; m < kMaxCountMasks; ++m) {
+    if ((uint32_t)m < n_masks) {  // wave-uniform
+      uint32_t c = cnt[m];
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
+    }
   }
   __syncthreads();
   if (threadIdx.x < n_masks && s_cnt[threadIdx.x]) atomicAdd(&out[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
-}
-
-__global__ void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks, double* __restrict__ out) {
-  double c = 0, m = 0;
-  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) { c += part[b * 2]; m += part[b * 2 + 1]; }
-  for (int off = 32; off > 0; off >>= 1) { c += __shfl_xor(c, off); m += __shfl_xor(m, off); }
-  __shared__ double sc[kBlock / 64], sm[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = c; sm[threadIdx.x >> 6] = m; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tc = 0, tm = 0;
-    for (int i = 0; i < kBlock / 64; ++i) { tc += sc[i]; tm += sm[i]; }
-    out[0] = tc;
-    out[1] = tm;
-  }
 }
 
 // ------------------------------------------------------------------ node leases
@@ -1632,10 +1634,13 @@ struct kwk_engine {
   uint64_t slot_base = 0;
   uint32_t kind_salt = 0;
   uint32_t n_blocks_cap = 0, last_blocks = 0, last_grid = 0;
-  uint32_t objs_wide = 16;    // sweep variants (KWOK_SWEEP_OBJS: wide 8 | 16, narrow 8 | 16 | 32)
-  uint32_t objs_narrow = 16;
-  uint32_t last_objs = 16;
-  bool last_packed = false;   // fired segments hold 4-byte records (2-byte sweep)
+  uint32_t cum_rows = 0;      // statistics rows any sweep grid has written (<= n_blocks_cap)
+  uint32_t last_objs = 16;    // words per lane of the last sweep (fired segment stride = 64 * last_objs + 32)
+  bool compacted = false;     // the last sweep's fired list is compacted on the device
+  unsigned long long* d_compact_status = nullptr;  // compact_kernel look-back status per block
+  unsigned long long* d_compact_ticket = nullptr;  // compact_kernel arrival counter (never reset)
+  unsigned long long compact_tickets = 0;          // its value before the next launch
+  uint32_t compact_epoch = 0;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
@@ -1643,16 +1648,17 @@ struct kwk_engine {
   void* d_st = nullptr;       // state word per slot (8-byte capacity; format in fmt)
   StateFmt fmt{};             // current state format (wide until a table allows narrow)
   bool force_wide = false;
-  bool allow_half = true;     // KWK_ENGINE_STATE32 / KWOK_STATE_BYTES=4: never the 2-byte format
-  uint32_t q16 = KWOK_Q16;    // 2-byte sweep: 16-byte chunks per lane (KWOK_SWEEP_Q16: 2 | 4)
+  bool allow_half = true;     // KWK_ENGINE_STATE32: never the 2-byte format
+  // kernel choices (kwk_set_tuning; defaults = the measured best)
+  uint32_t q16 = kQ16;        // 2-byte sweep: 16-byte chunks per lane (1 | 2 | 4)
+  bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
+  bool use_fsm = true;        // 2-byte sweep: transition table
   int n_cus = 256;
-  bool grid_per_tile = false;
-  bool persist16 = true;
-  bool use_fsm = true;        // KWOK_FSM=0: 2-byte sweep without the transition table
+  std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
   uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
   int64_t* d_fsm_due = nullptr;
   uint32_t fsm_bits = 0;
-  int fsm_harness = -1;       // harness enable the table was built for (-1: no table)      // 2-byte sweep grid (KWOK_SWEEP16_GRID=tile: one block per tile)
+  int fsm_harness = -1;       // harness enable the table was built for (-1: no table)
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -1667,12 +1673,10 @@ struct kwk_engine {
   uint32_t* d_wave_offsets = nullptr;
   unsigned long long* d_cum = nullptr;
   unsigned long long* d_stats = nullptr;
-  void* d_scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
   uint64_t steps = 0;
 
   // usage
-  uint32_t n_nodes = 0;
+  uint32_t n_nodes = 0, n_usage_pods = 0;
   uint32_t* d_node_ptr = nullptr;
   uint32_t* d_ukey = nullptr;
   double* d_cpu = nullptr;
@@ -1806,20 +1810,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
   e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
   e->allow_half = (d->flags & KWK_ENGINE_STATE32) == 0;
-  if (const char* v = getenv("KWOK_STATE_BYTES")) e->allow_half = e->allow_half && atoi(v) != 4;
-  if (const char* v = getenv("KWOK_SWEEP_Q16")) {
-    const int q = atoi(v);
-    if (q == 1 || q == 2 || q == 4) e->q16 = (uint32_t)q;
-  }
-  e->grid_per_tile = true;  // one block per tile: measured faster than the persistent grid with churn
-  if (const char* v = getenv("KWOK_SWEEP_GRID")) e->grid_per_tile = strcmp(v, "persist") != 0;
-  if (const char* v = getenv("KWOK_SWEEP16_GRID")) e->persist16 = strcmp(v, "tile") != 0;
-  if (const char* v = getenv("KWOK_FSM")) e->use_fsm = atoi(v) != 0;
-  if (const char* v = getenv("KWOK_SWEEP_OBJS")) {
-    const int k = atoi(v);
-    if (k == 8 || k == 16) e->objs_wide = (uint32_t)k;
-    if (k == 8 || k == 16 || k == 32) e->objs_narrow = (uint32_t)k;
-  }
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
   if (hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || e->n_cus <= 0)
@@ -1851,16 +1841,18 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
+  ALLOC(e->d_compact_status, sizeof(unsigned long long) * ((n_waves + kSegsPerBlock - 1) / kSegsPerBlock + 1));
+  ALLOC(e->d_compact_ticket, sizeof(unsigned long long));
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
   hipMemsetAsync(e->d_st, 0, sizeof(uint2) * st_slots, e->stream);
   hipMemsetAsync(e->d_due, 0, sizeof(int64_t) * (size_t)e->capacity, e->stream);
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
-  // cub scan temp storage for the fired-list compaction
-  hipcub::DeviceScan::ExclusiveSum(nullptr, e->scan_tmp_bytes, e->d_wave_counts, e->d_wave_offsets,
-                                   (int)(n_waves + 1), e->stream);
-  ALLOC(e->d_scan_tmp, e->scan_tmp_bytes ? e->scan_tmp_bytes : 16);
+  hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
+  hipMemsetAsync(e->d_compact_status, 0, sizeof(unsigned long long) * ((n_waves + kSegsPerBlock - 1) / kSegsPerBlock + 1),
+                 e->stream);
+  hipMemsetAsync(e->d_compact_ticket, 0, sizeof(unsigned long long), e->stream);
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
@@ -1873,7 +1865,8 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_scan_tmp,
+                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_compact_status,
+                  e->d_compact_ticket,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due,
@@ -1935,6 +1928,28 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   e->n_classes = t->n_classes;
   e->loaded_table = true;
   return build_fsm(e);
+}
+
+kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  switch (key) {
+    case KWK_TUNE_FSM:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FSM: 0 or 1");
+      e->use_fsm = value != 0;
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      return build_fsm(e);
+    case KWK_TUNE_Q16:
+      if (value != 1 && value != 2 && value != 4) return fail(KWK_EINVAL, "KWK_TUNE_Q16: 1, 2 or 4");
+      e->q16 = value;
+      return KWK_OK;
+    case KWK_TUNE_PERSIST16:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_PERSIST16: 0 or 1");
+      e->persist16 = value != 0;
+      return KWK_OK;
+    default:
+      return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
+  }
 }
 
 kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
@@ -2083,33 +2098,15 @@ kwk_status kwk_retry(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step
   return KWK_OK;
 }
 
-// sweep grid: one block per tile (default), or KWOK_SWEEP_GRID=persist: every CU slot the
-// occupancy allows, each block walking tiles (faster on idle sweeps, slower with churn on
-// MI355X, profiles/r1/README.md)
-extern "C++" template <bool H, int K, bool N, bool P>
-static uint32_t sweep_grid(kwk_engine* e, uint32_t tiles) {
-  static int per_cu = 0;
-  if (per_cu == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<H, K, N, P>, kBlock, 0) != hipSuccess ||
-        per_cu <= 0)
-      per_cu = 1;
-  }
-  if (!P) return tiles;
-  const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
-  return tiles < g ? tiles : g;
-}
-
 // persistent grid of the 2-byte sweep: every block slot the occupancy allows on every CU
+// (occupancy cached per engine and kernel: engines on different devices or threads never share it)
 static uint32_t persist_grid(kwk_engine* e, const void* kernel, uint32_t tiles) {
-  static const void* keys[16];
-  static int vals[16];
   int per_cu = 0;
-  for (int j = 0; j < 16 && keys[j]; ++j)
-    if (keys[j] == kernel) per_cu = vals[j];
+  for (const auto& kv : e->occupancy)
+    if (kv.first == kernel) per_cu = kv.second;
   if (per_cu == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
-    for (int j = 0; j < 16; ++j)
-      if (!keys[j]) { keys[j] = kernel; vals[j] = per_cu; break; }
+    e->occupancy.emplace_back(kernel, per_cu);
   }
   const uint32_t g = (uint32_t)e->n_cus * (uint32_t)per_cu;
   return tiles < g ? tiles : g;
@@ -2187,10 +2184,13 @@ static kwk_status build_fsm(kwk_engine* e) {
 static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
+  e->compacted = false;
   if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
   const bool h = a.harness.enable != 0;
+  // every sweep emits packed fired segments of 64 * K + 32 words per (tile, wave) and counts one
+  // statistics row per block: the per-tile arrays are sized for the smallest tile
   if (e->fmt.half && fire && e->fsm_harness == (h ? 1 : 0)) {
     a.fsm = e->d_fsm;
     a.fsm_due = e->d_fsm_due;
@@ -2224,37 +2224,29 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     }
 #undef LAUNCH16
     e->last_objs = K;
-    e->last_packed = true;
     HIP_TRY(hipGetLastError());
     e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
     e->last_grid = blocks;
+    e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
     ++e->steps;
     return KWK_OK;
   }
-  const uint32_t K = nar ? e->objs_narrow : e->objs_wide;
+  // 4- / 8-byte words: whole-line write-back word sweep, one block per tile
+  const uint32_t K = (uint32_t)kQW * (nar ? 4u : 2u);
   const uint32_t tile = kBlock * K;
   const uint32_t blocks = (e->n_active + tile - 1) / tile;
-#define LAUNCH(HV, KV, NV) \
-  do {                                                                                                           \
-    if (e->grid_per_tile)                                                                                       \
-      hipLaunchKernelGGL((sweep_kernel<HV, KV, NV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);      \
-    else                                                                                                         \
-      hipLaunchKernelGGL((sweep_kernel<HV, KV, NV, true>), dim3(sweep_grid<HV, KV, NV, true>(e, blocks)),      \
-                         dim3(kBlock), 0, e->stream, a);                                                         \
-  } while (0)
-  if (!nar) {
-    if (K == 8) { if (h) LAUNCH(true, 8, false); else LAUNCH(false, 8, false); }
-    else { if (h) LAUNCH(true, 16, false); else LAUNCH(false, 16, false); }
+  if (nar) {
+    if (h) hipLaunchKernelGGL((sweepw_kernel<true, 4>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    else hipLaunchKernelGGL((sweepw_kernel<false, 4>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   } else {
-    if (K == 32) { if (h) LAUNCH(true, 32, true); else LAUNCH(false, 32, true); }
-    else if (K == 8) { if (h) LAUNCH(true, 8, true); else LAUNCH(false, 8, true); }
-    else { if (h) LAUNCH(true, 16, true); else LAUNCH(false, 16, true); }
+    if (h) hipLaunchKernelGGL((sweepw_kernel<true, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    else hipLaunchKernelGGL((sweepw_kernel<false, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   }
-#undef LAUNCH
   e->last_objs = K;
-  e->last_packed = false;
   HIP_TRY(hipGetLastError());
   e->last_blocks = blocks;
+  e->last_grid = blocks;
+  e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
   ++e->steps;
   return KWK_OK;
 }
@@ -2274,39 +2266,80 @@ kwk_status kwk_sync(kwk_engine* e) {
   return KWK_OK;
 }
 
+// fired hand-back on the device: per-(tile, wave) counts -> exclusive scan -> dense list in
+// d_compact, total at d_wave_offsets[n_waves] (enqueue only)
+static kwk_status enqueue_compact(kwk_engine* e) {
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  e->compacted = true;
+  if (n_waves == 0) return KWK_OK;
+  const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
+  CompactArgs a;
+  a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
+  a.counts = e->d_wave_counts;
+  a.out = e->d_compact;
+  a.total = e->d_wave_offsets;  // word 0: the list's length
+  a.status = e->d_compact_status;
+  a.ticket = e->d_compact_ticket;
+  a.ticket_base = e->compact_tickets;
+  a.n_segs = n_waves;
+  a.seg_slots = 64u * e->last_objs;
+  a.stride = 64u * e->last_objs + 32u;
+  a.epoch = ++e->compact_epoch & 0x3FFFFFFFu;
+  hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+  HIP_TRY(hipGetLastError());
+  e->compact_tickets += blocks;
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_compact(kwk_engine* e) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  return enqueue_compact(e);
+}
+
+kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
+  if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
+  if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
+  *recs = e->d_compact;
+  *count = e->d_wave_offsets;
+  return KWK_OK;
+}
+
 kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out) {
   if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = set_dev(e)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
-  HIP_TRY(hipMemsetAsync(e->d_wave_counts + n_waves, 0, sizeof(uint32_t), e->stream));
-  if (e->last_packed) {
-    hipLaunchKernelGGL(seg_counts_kernel, dim3((n_waves + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
-                       reinterpret_cast<const uint32_t*>(e->d_fired), n_waves, 64u * e->last_objs + 32u,
-                       e->d_wave_counts);
-    HIP_TRY(hipGetLastError());
-  }
-  size_t tmp = e->scan_tmp_bytes;
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->d_scan_tmp, tmp, e->d_wave_counts, e->d_wave_offsets,
-                                           (int)(n_waves + 1), e->stream));
+  if (!e->compacted)
+    if (kwk_status st = enqueue_compact(e)) return st;
   uint32_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets + n_waves, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   *n_out = total;
   if (!out || total == 0) return KWK_OK;
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
-  hipLaunchKernelGGL(compact_fired_kernel, dim3(n_waves), dim3(64), 0, e->stream, e->d_fired, e->d_wave_counts,
-                     e->d_wave_offsets, n_waves, 64u * e->last_objs, e->last_packed ? 1u : 0u, e->d_compact);
-  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_alloc_host(uint64_t bytes, void** out) {
+  if (!out) return fail(KWK_EINVAL, "null argument");
+  *out = nullptr;
+  if (bytes == 0) return KWK_OK;
+  HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return KWK_OK;
+}
+
+kwk_status kwk_free_host(void* p) {
+  if (p) HIP_TRY(hipHostFree(p));
   return KWK_OK;
 }
 
 kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
   if (!e || !out) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = set_dev(e)) return st;
-  hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->n_blocks_cap,
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->cum_rows,
                      e->d_stats);
   HIP_TRY(hipGetLastError());
   unsigned long long h[kStatWords];
@@ -2357,7 +2390,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster};
   for (void* p : olds) if (p) hipFree(p);
-  const uint32_t ublocks = (n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t ublocks = (n_nodes + kWavesPerBlock * kUG - 1) / (kWavesPerBlock * kUG);
   HIP_TRY(hipMalloc(&e->d_node_ptr, 4 * ((size_t)n_nodes + 1)));
   HIP_TRY(hipMalloc(&e->d_ukey, 4 * ((size_t)n_pods + 1)));
   HIP_TRY(hipMalloc(&e->d_cpu, 8 * (size_t)n_cpu));
@@ -2376,6 +2409,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   std::vector<int64_t> lasts((size_t)n_nodes + 1, INT64_MIN);
   HIP_TRY(hipMemcpy(e->d_node_last, lasts.data(), 8 * lasts.size(), hipMemcpyHostToDevice));
   e->n_nodes = n_nodes;
+  e->n_usage_pods = n_pods;
   return KWK_OK;
 }
 
@@ -2383,12 +2417,12 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
-  const uint32_t ublocks = (e->n_nodes + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->d_node_ptr, e->d_ukey,
-                     e->d_cpu, e->d_mem, e->n_nodes, e->d_node_out, e->d_node_cum, e->d_node_last, now_ns,
-                     e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last);
+  const uint32_t ublocks = (e->n_nodes + kWavesPerBlock * kUG - 1) / (kWavesPerBlock * kUG);
+  UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->n_nodes, e->n_usage_pods, e->d_node_out,
+               e->d_node_cum, e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last};
+  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, ua);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(kBlock), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);
+  hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
@@ -2445,9 +2479,11 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
   HIP_TRY(hipMemcpyAsync(d_masks, masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemsetAsync(d_out, 0, 8 * kMaxCountMasks, e->stream));
   if (e->n_active) {
-    const uint32_t blocks = (e->n_active + kBlock * 16 - 1) / (kBlock * 16);
-    hipLaunchKernelGGL(count_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->n_active, d_masks, n_masks,
-                       d_out);
+    const uint64_t chunks = ((uint64_t)e->n_active * word_bytes(e->fmt) + 15u) / 16u;
+    uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);  // ~4 chunks per lane
+    blocks = blocks < (uint64_t)e->n_cus * 8u ? blocks : (uint64_t)e->n_cus * 8u;
+    hipLaunchKernelGGL(count_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->n_active,
+                       d_masks, n_masks, d_out);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(counts, d_out, 8 * (size_t)n_masks, hipMemcpyDeviceToHost, e->stream));

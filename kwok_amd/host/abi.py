@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(_HERE)
-LIB_PATH = os.environ.get("KWOK_ENGINE_LIB") or os.path.join(PKG, "lib", "libkwok_engine.so")
+LIB_PATH = os.path.join(PKG, "lib", "libkwok_engine.so")
 
 KWK_OK, KWK_EINVAL, KWK_ECAP, KWK_EHIP, KWK_ESTATE = 0, -1, -2, -3, -4
 STAGE_NONE = 0xFF
@@ -83,6 +83,7 @@ class EngineDesc(C.Structure):
 
 ENGINE_WIDE_STATE = 1
 ENGINE_STATE32 = 2
+TUNE_FSM, TUNE_Q16, TUNE_PERSIST16 = 1, 2, 3
 
 
 class Lease(C.Structure):
@@ -128,7 +129,8 @@ EXPORTS = [
     "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
-    "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail",
+    "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
+    "kwk_alloc_host", "kwk_free_host",
 ]
 
 _lib = None
@@ -166,6 +168,11 @@ def lib():
     L.kwk_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_match.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]
     L.kwk_fired.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_fired_compact.argtypes = [C.c_void_p]
+    L.kwk_fired_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
+    L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
+    L.kwk_free_host.argtypes = [C.c_void_p]
+    L.kwk_set_tuning.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
     L.kwk_stats.argtypes = [C.c_void_p, _p(StepStats)]
     L.kwk_read.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     L.kwk_sync.argtypes = [C.c_void_p]

@@ -74,3 +74,23 @@ def phase_masks(program, query: str = ".status.phase", values: Sequence[str] = (
         if v in lits:
             out[v] = 1 << lits[v]
     return out
+
+
+def engine_aggregates(engines, count_masks, count_names, now_ns: int = None, usage_engine=None) -> Aggregates:
+    """This shard's aggregates straight from its engines (device work, C ABI): per-stage
+    transition counts (kwk_stats) of every engine in order, kwk_count of each engine's masks,
+    and — when `usage_engine` is given — the cluster usage of its pods at now_ns (kwk_usage,
+    metrics_resource_usage.go:195-224).  `count_masks` / `count_names` are one list per engine."""
+    names, fired, counts, cnames = [], [], [], []
+    for e, masks, mnames in zip(engines, count_masks, count_names):
+        st = e.stats()
+        names += list(st["fired_per_stage"])
+        fired += list(st["fired_per_stage"].values())
+        counts += [int(c) for c in e.count(masks)] if len(masks) else []
+        cnames += list(mnames)
+    usage = np.zeros(2)
+    if usage_engine is not None:
+        usage_engine.usage(now_ns)
+        _, usage = usage_engine.usage_read(node_out=False)
+    return Aggregates(names, np.asarray(fired, dtype=np.int64), np.asarray(counts, dtype=np.int64), cnames,
+                      np.asarray(usage, dtype=np.float64))

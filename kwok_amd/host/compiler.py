@@ -458,8 +458,22 @@ class KindProgram:
         collected per (class, stage) and turned into and/or masks.  A first pass finds stages
         whose patches can leave the object unchanged; they get an "applied" feature bit and
         the exploration is redone with it."""
-        roots = list(roots)
-        self._roots = getattr(self, "_roots", []) + roots
+        # roots are deduplicated by (class, start features) as they arrive: matching the same
+        # objects again (Lifecycle.match_batch explores every batch) re-runs nothing
+        if not hasattr(self, "_roots"):
+            self._roots, self._root_keys, self._explored = [], set(), False
+        added = 0
+        for r in roots:
+            r = prune_empty(copy.deepcopy(r))
+            k = (class_key(r), self.pred_of(r))
+            if k in self._root_keys:
+                continue
+            self._root_keys.add(k)
+            self._roots.append(r)
+            added += 1
+        if self._explored and not added:
+            return
+        self._explored = True
         for _ in range(2):
             unchanged = self._explore_pass(self._roots, max_states)
             new = [s for s in unchanged if s not in self.applied_bits]

@@ -103,6 +103,35 @@ class Ingest:
         return a
 
 
+class PinnedBuffer:
+    """kwk_alloc_host / kwk_free_host: a page-locked host buffer reused across steps."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.p = C.c_void_p()
+        abi.check(abi.lib().kwk_alloc_host(self.nbytes, C.byref(self.p)), "kwk_alloc_host")
+
+    def array(self, dtype, n: int) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        if n * dtype.itemsize > self.nbytes:
+            raise abi.EngineError(f"pinned buffer of {self.nbytes} bytes too small for {n} x {dtype}")
+        if n == 0:
+            return np.zeros(0, dtype=dtype)
+        buf = (C.c_char * (n * dtype.itemsize)).from_address(self.p.value)
+        return np.frombuffer(buf, dtype=dtype, count=n)
+
+    def close(self):
+        if self.p:
+            abi.lib().kwk_free_host(self.p)
+            self.p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One kwk_engine (C ABI) for one KindProgram."""
 
@@ -191,6 +220,14 @@ class Engine:
     def step(self, now_ns: int, seed: int, step: int):
         abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
+    def fired_compact(self):
+        """kwk_fired_compact: the last step's fired list compacted on the device (enqueue only)."""
+        abi.check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
+
+    def set_tuning(self, key: int, value: int):
+        """kwk_set_tuning: an explicit kernel choice (abi.TUNE_*)."""
+        abi.check(abi.lib().kwk_set_tuning(self.h, key, value), "kwk_set_tuning")
+
     def match(self, now_ns: int, seed: int, step: int):
         """kwk_match: pick + delay for dirty objects, nothing fires."""
         abi.check(abi.lib().kwk_match(self.h, now_ns, seed, step), "kwk_match")
@@ -198,11 +235,16 @@ class Engine:
     def sync(self):
         abi.check(abi.lib().kwk_sync(self.h), "kwk_sync")
 
-    def fired(self) -> np.ndarray:
+    def fired(self, pinned: Optional["PinnedBuffer"] = None) -> np.ndarray:
+        """The last step's fired records (kwk_fired).  With `pinned` (a PinnedBuffer) the copy
+        lands in page-locked memory and the returned array is a view of it."""
         n = C.c_uint32()
         L = abi.lib()
         abi.check(L.kwk_fired(self.h, None, 0, C.byref(n)), "kwk_fired")
-        out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
+        if pinned is not None:
+            out = pinned.array(abi.FIRED_DTYPE, n.value)
+        else:
+            out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
         if n.value:
             abi.check(L.kwk_fired(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired")
         return out
@@ -251,8 +293,9 @@ class Engine:
         abi.check(abi.lib().kwk_usage_read_pods(self.h, first, n, abi.ptr(out)), "kwk_usage_read_pods")
         return out
 
-    def usage_read(self):
-        node = np.zeros((self.n_nodes, 4), dtype=np.float64)
+    def usage_read(self, node_out: bool = True):
+        """(per-node {cpu, mem, cpu_cumulative, mem_cumulative} or None, cluster {cpu, mem})."""
+        node = np.zeros((self.n_nodes, 4), dtype=np.float64) if node_out else None
         cl = np.zeros(2, dtype=np.float64)
         abi.check(abi.lib().kwk_usage_read(self.h, abi.ptr(node), abi.ptr(cl)), "kwk_usage_read")
         return node, cl

@@ -121,6 +121,74 @@ def _pods_per_node(n_nodes: int, n_pods: int) -> np.ndarray:
     return base
 
 
+def _c2_override_sets(rng, n_over: int = 32) -> List[dict]:
+    """C2's override-annotation sets: 3 stages x {weight, delay, jitter-delay} per set."""
+    out = []
+    for _ in range(n_over):
+        ann = {}
+        for st in rng.choice(GENERAL_NAMES, size=3, replace=False):
+            kind = rng.choice(["weight", "delay", "jitter-delay"])
+            ann[f"{st}.stage.kwok.x-k8s.io/{kind}"] = str(rng.choice(OVERRIDE_VALUES))
+        out.append(ann)
+    return out
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)).astype(np.uint64)
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)).astype(np.uint64)
+    return x ^ (x >> np.uint64(31))
+
+
+def _unit(ids: np.ndarray, seed: int, salt: int) -> np.ndarray:
+    h = _splitmix64(ids ^ np.uint64((seed ^ (salt * 0x2545F4914F6CDD1D)) & 0xFFFFFFFFFFFFFFFF))
+    return (h >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53)), h
+
+
+def c2_pod_variants(pod_lo: int, pod_hi: int, seed: int = CLUSTER_SEED, now_s: int = 1_700_000_000,
+                    job_frac: float = 0.1) -> Tuple[List[dict], np.ndarray]:
+    """The C2 pod mix (pod-general + chaos: 20 % with 1-2 init containers, 10 % override
+    annotations, 5 % chaos label, 10 % deletionTimestamp, job_frac Job-owned) for global pods
+    [pod_lo, pod_hi) at any scale: every attribute is a hash of the GLOBAL pod id, so every
+    sharding of the cluster sees the same objects (vectorised; make_cluster's per-pod draw is
+    the small-cluster form of the same mix)."""
+    over_sets = _c2_override_sets(np.random.default_rng(seed))
+    del_ts = np.datetime_as_string(np.datetime64(now_s + 30, "s")) + "Z"
+    n = pod_hi - pod_lo
+    code = np.empty(n, dtype=np.int32)
+    chunk = 1 << 24
+    for a in range(pod_lo, pod_hi, chunk):
+        b = min(pod_hi, a + chunk)
+        ids = np.arange(a, b, dtype=np.uint64)
+        job = _unit(ids, seed, 1)[0] < job_frac
+        u2, h2 = _unit(ids, seed, 2)
+        init = np.where(u2 < 0.2, 1 + (h2 & np.uint64(1)).astype(np.int64), 0)
+        u4, h4 = _unit(ids, seed, 4)
+        over = np.where(u4 < 0.1, (h4 % np.uint64(len(over_sets))).astype(np.int64), -1)
+        chaos = np.where(_unit(ids, seed, 6)[0] < 0.05, np.where(init > 0, 2, 1), 0)
+        dele = _unit(ids, seed, 7)[0] < 0.1
+        code[a - pod_lo:b - pod_lo] = job + 2 * (init + 3 * ((over + 1) + 33 * (chaos + 3 * dele)))
+    present = np.zeros(2 * 3 * 33 * 3 * 2, dtype=bool)
+    present[code] = True
+    ids_of = np.cumsum(present) - 1
+    variants = []
+    for c in np.flatnonzero(present):
+        c = int(c)
+        job, r = c % 2, c // 2
+        init, r = r % 3, r // 3
+        over, r = r % 33 - 1, r // 33
+        chaos, dele = r % 3, r // 3
+        labels = None
+        if chaos == 1:
+            labels = {"pod-container-running-failed.stage.kwok.x-k8s.io": "true"}
+        elif chaos == 2:
+            labels = {"pod-init-container-running-failed.stage.kwok.x-k8s.io": "true"}
+        variants.append(pod_object("p", "n", job=bool(job), init=init, labels=labels,
+                                   annotations=over_sets[over] if over >= 0 else None,
+                                   deletion=del_ts if dele else None))
+    return variants, ids_of[code].astype(np.int32)
+
+
 def make_cluster(config: str, n_nodes: int, n_pods: int, seed: int = CLUSTER_SEED, now_s: int = 1_700_000_000,
                  job_frac: float = 0.1) -> Cluster:
     """Configs C1..C5 (BASELINE.json `configs`)."""
@@ -142,13 +210,7 @@ def make_cluster(config: str, n_nodes: int, n_pods: int, seed: int = CLUSTER_SEE
         # 5% chaos label, 10% deletionTimestamp = now + 30 s (second precision)
         del_ts = np.datetime_as_string(np.datetime64(now_s + 30, "s")) + "Z"
         n_over = 32
-        over_sets = []
-        for _ in range(n_over):
-            ann = {}
-            for st in rng.choice(GENERAL_NAMES, size=3, replace=False):
-                kind = rng.choice(["weight", "delay", "jitter-delay"])
-                ann[f"{st}.stage.kwok.x-k8s.io/{kind}"] = str(rng.choice(OVERRIDE_VALUES))
-            over_sets.append(ann)
+        over_sets = _c2_override_sets(rng, n_over)
         key_to_var: Dict[Tuple, int] = {}
         pod_vars = []
         job = rng.random(n_pods) < job_frac

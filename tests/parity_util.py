@@ -25,7 +25,7 @@ def expected_state_bytes(prog, state="auto"):
     return 4 if bits <= 32 else 8
 
 
-def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto"):
+def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto", tuning=None):
     stages = load_stage_files(*stage_files)
     prog = KindProgram(stages, HarnessSpec() if harness else None)
     prog.explore(objs)
@@ -34,6 +34,8 @@ def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state
     hot, dels, rec, cls = ing.columns(objs)
     eng = Engine(prog, capacity=max(1, len(objs)), kind_salt=kind_salt, slot_base=slot_base, wide_state=wide_state,
                  state=state)
+    for k, v in (tuning or {}).items():
+        eng.set_tuning(k, v)
     eng.load_stages()
     eng.set_harness(harness)
     eng.load(hot, dels, rec, cls, ing.record_array())
@@ -71,10 +73,10 @@ def compare_state(prog, eng, sim, step):
 
 
 def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False,
-        state="auto"):
+        state="auto", tuning=None):
     if wide_state:
         state = "wide"
-    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state)
+    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state, tuning=tuning)
     total = 0
     per_stage = np.zeros(len(prog.names), dtype=np.int64)
     try:

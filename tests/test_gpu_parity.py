@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from kwok_amd import workload as W
+from kwok_amd.host import abi
 from tests.parity_util import run
 
 pytestmark = pytest.mark.gpu
@@ -16,16 +17,17 @@ FORMATS = ["auto", "u32", "wide"]
 
 
 @pytest.mark.parametrize("state", FORMATS + ["auto-nofsm"])
-def test_pod_fast_c1_mini(state, monkeypatch):
+def test_pod_fast_c1_mini(state):
     """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in every
     device state format (auto = the 2-byte words of the whole-line sweep, with and without
     its precomputed transition table)."""
+    tuning = {}
     if state == "auto-nofsm":
-        monkeypatch.setenv("KWOK_FSM", "0")
+        tuning = {abi.TUNE_FSM: 0}
         state = "auto"
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state)
+    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state, tuning=tuning)
     assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
 
 
@@ -42,13 +44,14 @@ def test_pod_general_c2_mini(wide):
 
 
 @pytest.mark.parametrize("state", ["auto", "auto-nofsm", "u32"])
-def test_node_fast_heartbeat(state, monkeypatch):
+def test_node_fast_heartbeat(state):
+    tuning = {}
     if state == "auto-nofsm":
-        monkeypatch.setenv("KWOK_FSM", "0")
+        tuning = {abi.TUNE_FSM: 0}
         state = "auto"
     cl = W.make_cluster("C1", 64, 64, seed=13)
     objs = cl.nodes.materialize()
-    total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1, state=state)
+    total, per = run(cl.node_stage_files, objs, steps=30, dt_ns=2 * 10**9, kind_salt=1, state=state, tuning=tuning)
     assert per["node-initialize"] == 64 and per["node-heartbeat"] > 0
 
 

@@ -31,44 +31,48 @@ def test_bench_pod_variants_are_shard_invariant():
     assert 0.08 < full.mean() < 0.12
 
 
-def _simulate(pods, slot_base, steps, files):
+GOLDEN_USAGE = os.path.join(ROOT, "tests", "golden", "metrics", "usage-from-annotation.yaml")
+
+
+def _shard_aggregates(pods, slot_base, steps, files):
+    """A shard's aggregates in the engine's shape (bench.py Reporter / cluster.engine_aggregates):
+    per-stage transitions, [alive, Running, Succeeded] counts and the cluster usage, computed
+    by the oracle simulation of the shard (RNG keyed by global slot)."""
+    import yaml
     from kwok_amd.host.stages import load_stage_files
     from oracle.sim import OracleSim
-    from oracle import refcpu
+    from oracle import refcpu, usage_ref
     stages = load_stage_files(*files)
     sim = OracleSim(stages, pods, harness=True, slot_base=slot_base)
     fired = np.zeros(len(sim.stages), dtype=np.int64)
     for k in range(steps):
         for _, s, _ in sim.step(1_700_000_000 * 10**9 + k * 10**9, 99, k):
             fired[s] += 1
-    phases = {"Running": 0, "Succeeded": 0, "alive": 0}
-    for o in sim.objs:
-        if o is None:
-            continue
-        phases["alive"] += 1
-        for p in refcpu.query(".status.phase", o) or []:
-            if p in phases:
-                phases[p] += 1
-    return [s.name for s in sim.stages], fired, np.array([phases["Running"], phases["Succeeded"], phases["alive"]])
+    alive = [o for o in sim.objs if o is not None]
+    ph = [(refcpu.query(".status.phase", o) or [None])[0] for o in alive]
+    docs = [d for d in yaml.safe_load_all(open(GOLDEN_USAGE).read()) if d]
+    usage = np.array([sum(usage_ref.pod_usage(docs, o, r) for o in alive) for r in ("cpu", "memory")])
+    return Aggregates([s.name for s in sim.stages], fired, np.array([len(alive), ph.count("Running"),
+                                                                      ph.count("Succeeded")]),
+                      ["pods", "pods_Running", "pods_Succeeded"], usage)
 
 
 def _worker(rank, world, port, result_path):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cl = W.make_cluster("C1", 6, 60, seed=4)
+    cl = W.make_cluster("C4", 6, 60, seed=4)
     lo, hi = node_block(6, world, rank)
     plo, phi = pod_range(cl.node_ptr, lo, hi)
     pods = cl.pods.materialize(plo, phi)
-    names, fired, counts = _simulate(pods, plo, 7, cl.pod_stage_files)
-    agg = Aggregates(names, fired, counts, ["Running", "Succeeded", "alive"]).allreduce(dist)
+    agg = _shard_aggregates(pods, plo, 7, cl.pod_stage_files).allreduce(dist)
     if rank == 0:
         np.save(result_path, agg.pack())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_allreduce_of_sharded_oracle_equals_whole_cluster(tmp_path):
+def test_gloo_allreduce_of_sharded_aggregates_equals_whole_cluster(tmp_path):
     torch = pytest.importorskip("torch")
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -77,10 +81,13 @@ def test_gloo_allreduce_of_sharded_oracle_equals_whole_cluster(tmp_path):
     out = str(tmp_path / "agg.npy")
     mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
     got = np.load(out)
-    cl = W.make_cluster("C1", 6, 60, seed=4)
-    names, fired, counts = _simulate(cl.pods.materialize(), 0, 7, cl.pod_stage_files)
-    want = Aggregates(names, fired, counts).pack()
-    assert np.array_equal(got, want)
+    cl = W.make_cluster("C4", 6, 60, seed=4)
+    whole = _shard_aggregates(cl.pods.materialize(), 0, 7, cl.pod_stage_files)
+    want = whole.pack()
+    n_exact = len(whole.fired_per_stage) + len(whole.counts)
+    assert np.array_equal(got[:n_exact], want[:n_exact])  # transitions and phase counts: exact
+    np.testing.assert_allclose(got[n_exact:], want[n_exact:], rtol=1e-12)  # usage: reassociated sums
+    assert whole.counts[0] > 0 and whole.usage[0] > 0
 
 
 def test_local_node_ptr():

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 N_NODES, PPN, STEPS = 40_000, 100, 20
 
 
-def _pods(state, n_nodes=N_NODES):
+def _pods(state, n_nodes=N_NODES, tuning=None):
     from bench import shard_pod_variants
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
@@ -26,6 +26,8 @@ def _pods(state, n_nodes=N_NODES):
     idx = shard_pod_variants(0, n_nodes * PPN, 0x6B776F6B, 0.1)
     hot, dels, rec, cls = ing.variant_columns(pvars, idx)
     eng = Engine(prog, capacity=n_nodes * PPN, state=state)
+    for k, v in (tuning or {}).items():
+        eng.set_tuning(k, v)
     eng.load_stages()
     eng.set_harness(True)
     eng.load(hot, dels, rec, cls, ing.record_array())
@@ -67,16 +69,15 @@ def test_three_sweeps_agree_at_4m_pods():
             e.close()
 
 
-def test_sweep16_tile_shapes_agree_at_17m_pods(monkeypatch):
+def test_sweep16_tile_shapes_agree_at_17m_pods():
     """The 2-byte sweep's tile shapes: Q = 4 (8192-word tiles, persistent grid: at 17M pods
     the tiles outnumber twice the resident blocks), Q = 2 and Q = 1 (one block per tile) must
-    fire the same sets and leave the same words.  KWOK_SWEEP_Q16 is read at engine creation."""
+    fire the same sets and leave the same words (kwk_set_tuning KWK_TUNE_Q16)."""
+    from kwok_amd.host import abi
     engines = {}
     try:
         for q in ("4", "2", "1"):
-            monkeypatch.setenv("KWOK_SWEEP_Q16", q)
-            engines[q] = _pods("auto", n_nodes=170_000)
-        monkeypatch.delenv("KWOK_SWEEP_Q16")
+            engines[q] = _pods("auto", n_nodes=170_000, tuning={abi.TUNE_Q16: int(q)})
         assert all(e.stats()["state_bytes"] == 2 for _, e in engines.values())
         now0 = 1_700_000_000 * 10**9
         for k in range(10):
@@ -95,3 +96,55 @@ def test_sweep16_tile_shapes_agree_at_17m_pods(monkeypatch):
     finally:
         for _, e in engines.values():
             e.close()
+
+
+def test_aggregates_and_handback_at_17m_pods():
+    """At 17M pods (the 2-byte sweep's persistent grid): kwk_count and kwk_usage against the
+    state read back through kwk_read (numpy), and the device-compacted fired list (one
+    look-back pass) in strict slot order with the step's transition count."""
+    from kwok_amd.host import abi
+    from kwok_amd.host.cluster import phase_masks
+    n_nodes = 170_000
+    prog, eng = _pods("auto", n_nodes=n_nodes)
+    try:
+        n = n_nodes * PPN
+        rng = np.random.default_rng(5)
+        cpu = rng.random(37) * 4
+        mem = rng.random(41) * 2**32
+        ci, mi, nc = rng.integers(0, 37, n), rng.integers(0, 41, n), rng.integers(1, 5, n)
+        keys = (ci | (mi << 14) | (nc << 28)).astype(np.uint32)
+        ptr = np.concatenate([[0], np.cumsum(rng.integers(0, 2 * PPN, n_nodes))]).astype(np.int64)
+        ptr = (ptr * (n / ptr[-1])).astype(np.uint32)
+        ptr[-1] = n
+        eng.usage_config(ptr, keys, cpu, mem)
+        pm = phase_masks(prog, values=("Running", "Succeeded"))
+        masks = [0, pm["Running"], pm["Succeeded"], pm["Running"] | pm["Succeeded"]]
+        now0 = 1_700_000_000 * 10**9
+        prev = eng.stats()["fired"]
+        for k in range(6):
+            eng.step(now0 + k * 10**9, 0x6B776F6B, k)
+            eng.fired_compact()
+            f = eng.fired()
+            st = eng.stats()["fired"]
+            assert len(f) == st - prev and len(f) > 0
+            prev = st
+            assert np.all(np.diff(f["slot"].astype(np.int64)) > 0), f"step {k}: fired list not in slot order"
+            got = eng.count(masks)
+            hot, _ = eng.read()
+            alive = (hot["sched"] & abi.F_ALIVE) != 0
+            want = [int(alive.sum())] + [int((alive & ((hot["pred"] & m) != 0)).sum()) for m in masks[1:]]
+            assert got.tolist() == want, f"step {k}"
+            eng.usage(now0 + k * 10**9)
+            node, total = eng.usage_read()
+            vc = np.where(alive, nc * cpu[ci], 0.0)
+            vm = np.where(alive, nc * mem[mi], 0.0)
+            seg_c = np.add.reduceat(np.append(vc, 0.0), ptr[:-1].astype(np.int64))
+            seg_m = np.add.reduceat(np.append(vm, 0.0), ptr[:-1].astype(np.int64))
+            empty = ptr[1:] == ptr[:-1]
+            seg_c[empty] = 0.0
+            seg_m[empty] = 0.0
+            np.testing.assert_allclose(node[:, 0], seg_c, rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(node[:, 1], seg_m, rtol=1e-9, atol=1e-3)
+            np.testing.assert_allclose(total, [vc.sum(), vm.sum()], rtol=1e-9)
+    finally:
+        eng.close()
