@@ -9,23 +9,20 @@ between watch events, in the engine's documented order:
                  on objects that changed since their last match (informer Modified event)
   schedule       one pending job per object; a match replaces it, no match keeps it
                  (pod_controller.go:222-229, addStageJob :660-671)
-  fire           due <= now: playStage's effect — finalizers JSON patch, delete, rendered
-                 merge patches (next.go, finalizers.go; rendering via the gotpl mirror that
-                 tests/ pins against the reference's golden outputs); an object whose
+  fire           due <= now: playStage's effect — finalizers JSON patch, delete, the status
+                 merge patch (oracle/next_ref.py: the oracle's own restatement of the shipped
+                 templates, pinned on the reference's golden outputs); an object whose
                  patches changed it is re-matched next step (its Modified event)
+
+Stages are v1alpha1 Stage documents (the YAML kwok loads); nothing here imports the product.
 """
 from __future__ import annotations
 
 import copy
-import json
 from typing import List, Optional, Sequence
 
-from kwok_amd.host.compiler import exploration_funcs, strip_for_recreate
-from kwok_amd.host.gotpl import Renderer, rfc3339nano
-from kwok_amd.host.nextstate import apply_next, prune_empty
-from kwok_amd.host.stages import Stage, to_v1alpha1
-
 from . import refcpu
+from .next_ref import Funcs, StageNext, format_rfc3339nano, omitempty, strip_for_recreate
 
 INT64_MAX = (1 << 63) - 1
 INT64_MIN = -(1 << 63)
@@ -36,12 +33,15 @@ def sat_add(a: int, b: int) -> int:
 
 
 class OracleSim:
-    def __init__(self, stages: Sequence[Stage], objs: Sequence[dict], harness: bool = False,
+    def __init__(self, stage_docs: Sequence[dict], objs: Sequence[dict], harness: bool = False,
                  terminal=("Succeeded", "Failed"), slot_base: int = 0, kind_salt: int = 0):
-        self.stages = [s for s in stages if s.selector is not None]
-        self.lc = refcpu.Lifecycle([to_v1alpha1(s) for s in stages])
-        assert self.lc.names == [s.name for s in self.stages]
-        self.objs: List[Optional[dict]] = [prune_empty(copy.deepcopy(o)) for o in objs]
+        # NewLifecycle drops stages with a nil selector (lifecycle.go:199-201)
+        docs = [d for d in stage_docs if (d.get("spec") or {}).get("selector") is not None]
+        self.lc = refcpu.Lifecycle(list(stage_docs))
+        assert self.lc.names == [d["metadata"]["name"] for d in docs]
+        self.stages = [StageNext(d, self.lc, i) for i, d in enumerate(docs)]
+        self.names = self.lc.names
+        self.objs: List[Optional[dict]] = [omitempty(copy.deepcopy(o)) for o in objs]
         self.orig = [copy.deepcopy(o) for o in self.objs]
         n = len(objs)
         self.dirty = [True] * n
@@ -61,8 +61,7 @@ class OracleSim:
 
     def step(self, now_ns: int, seed: int, step: int):
         key = seed ^ (self.kind_salt << 32)
-        renderer = Renderer(exploration_funcs(), now_ns=now_ns)
-        renderer.funcs["Now"] = lambda: rfc3339nano(now_ns)
+        F = Funcs(now_ns)
         fired = []
         for i in range(len(self.objs)):
             if not self.managed[i]:  # read-only (watchResources skips it, controller.go:285-288)
@@ -76,7 +75,7 @@ class OracleSim:
                     self.pending[i] = None
                 elif self._is_terminal(o) and "deletionTimestamp" not in o.get("metadata", {}):
                     sec = now_ns // 10**9
-                    o.setdefault("metadata", {})["deletionTimestamp"] = rfc3339nano(sec * 10**9)
+                    o.setdefault("metadata", {})["deletionTimestamp"] = format_rfc3339nano(sec * 10**9)
                     self.dirty[i] = True
             if o is None:
                 continue
@@ -92,7 +91,7 @@ class OracleSim:
             s = self.pending[i]
             if s is not None and self.due[i] <= now_ns:
                 self.pending[i] = None
-                o2, changed = apply_next(self.stages[s], copy.deepcopy(o), renderer)
+                o2, changed = self.stages[s].apply(o, F)
                 flags = 0
                 if o2 is None:
                     flags |= 1
@@ -125,7 +124,8 @@ class OracleSim:
 
 def oracle_pred(desc: dict, obj: dict) -> int:
     """Feature bits of a JSON object computed with the oracle's own jq (refcpu), from the
-    compiled feature table (KindProgram.describe())."""
+    compiled feature table (KindProgram.describe(): data, the query text and bit of each
+    feature)."""
     pred = 0
     for f in desc["features"]:
         out = refcpu.query(f["query"], obj) or []

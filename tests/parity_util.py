@@ -8,6 +8,7 @@ from kwok_amd.host import abi
 from kwok_amd.host.compiler import HarnessSpec, KindProgram
 from kwok_amd.host.engine import Engine, Ingest
 from kwok_amd.host.stages import load_stage_files
+from oracle.next_ref import load_stage_docs
 from oracle.sim import OracleSim, oracle_pred
 
 NOW0 = 1_700_000_000 * 10**9
@@ -39,7 +40,7 @@ def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state
     eng.load_stages()
     eng.set_harness(harness)
     eng.load(hot, dels, rec, cls, ing.record_array())
-    sim = OracleSim(stages, objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base)
+    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base)
     return prog, eng, sim
 
 

@@ -39,11 +39,10 @@ def _shard_aggregates(pods, slot_base, steps, files):
     per-stage transitions, [alive, Running, Succeeded] counts and the cluster usage, computed
     by the oracle simulation of the shard (RNG keyed by global slot)."""
     import yaml
-    from kwok_amd.host.stages import load_stage_files
+    from oracle.next_ref import load_stage_docs
     from oracle.sim import OracleSim
     from oracle import refcpu, usage_ref
-    stages = load_stage_files(*files)
-    sim = OracleSim(stages, pods, harness=True, slot_base=slot_base)
+    sim = OracleSim(load_stage_docs(*files), pods, harness=True, slot_base=slot_base)
     fired = np.zeros(len(sim.stages), dtype=np.int64)
     for k in range(steps):
         for _, s, _ in sim.step(1_700_000_000 * 10**9 + k * 10**9, 99, k):
