@@ -212,6 +212,12 @@ kwk_status kwk_load(kwk_engine* eng, uint32_t n, const kwk_hot* hot, const int64
 /* per-object upsert (Added / Modified events): scatter into the given slots, marks dirty */
 kwk_status kwk_upsert(kwk_engine* eng, uint32_t n, const uint32_t* slots, const kwk_hot* hot,
                       const int64_t* deletion_s, const uint32_t* rec_idx, const uint16_t* cls);
+/* the same scatter with the rows taken as given (DIRTY only if the row carries it): the host's
+ * re-encoded object after a fire whose next state the device could not derive
+ * (KWK_FIRED_DELTA_UNKNOWN) — the watch event the reference would receive
+ * (pod_controller.go:336-351, 412-478) re-matches it only if the object changed */
+kwk_status kwk_replace(kwk_engine* eng, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* deletion_s,
+                       const uint32_t* rec_idx, const uint16_t* cls);
 kwk_status kwk_set_records(kwk_engine* eng, uint32_t first, uint32_t n, const kwk_value* records);
 /* Deleted events: clear ALIVE (cancels any pending stage) */
 kwk_status kwk_delete(kwk_engine* eng, uint32_t n, const uint32_t* slots);
@@ -252,7 +258,8 @@ kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t st
  * dense device list (enqueue only: call it after kwk_step to keep the list on the device, e.g.
  * for an in-process consumer through kwk_fired_device).  kwk_fired copies the LAST step's list
  * (compacting first if needed) into host memory — a kwk_alloc_host buffer makes the copy a
- * direct DMA — and synchronises.  Record order: slot order. */
+ * direct DMA — and synchronises.  Records are grouped by sweep region (ascending regions of
+ * 512-2048 slots), unordered within a region; each fired slot appears once. */
 kwk_status kwk_fired_compact(kwk_engine* eng);
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 /* device pointers of the compacted list and of its u32 count (valid until the next kwk_step) */

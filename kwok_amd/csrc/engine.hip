@@ -2006,8 +2006,21 @@ kwk_status kwk_set_records(kwk_engine* e, uint32_t first, uint32_t n, const kwk_
   return KWK_OK;
 }
 
+static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
+                               const uint32_t* rec, const uint16_t* cls, uint32_t mark_dirty);
+
 kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
                       const uint32_t* rec, const uint16_t* cls) {
+  return scatter_rows(e, n, slots, hot, del, rec, cls, 1u);
+}
+
+kwk_status kwk_replace(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
+                       const uint32_t* rec, const uint16_t* cls) {
+  return scatter_rows(e, n, slots, hot, del, rec, cls, 0u);
+}
+
+static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
+                               const uint32_t* rec, const uint16_t* cls, uint32_t mark_dirty) {
   if (!e || (n && (!slots || !hot || !del || !rec || !cls))) return fail(KWK_EINVAL, "null argument");
   if (n == 0) return KWK_OK;
   uint32_t max_slot = 0;
@@ -2039,7 +2052,7 @@ kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kw
                       word_bytes(e->fmt) * (size_t)(max_slot + 1 - e->n_active)));
     e->n_active = max_slot + 1;
   }
-  ScatterArgs a{e->d_st, e->fmt, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, 1u};
+  ScatterArgs a{e->d_st, e->fmt, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, mark_dirty};
   hipLaunchKernelGGL(scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));

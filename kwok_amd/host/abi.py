@@ -130,7 +130,7 @@ EXPORTS = [
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
-    "kwk_alloc_host", "kwk_free_host",
+    "kwk_alloc_host", "kwk_free_host", "kwk_replace",
 ]
 
 _lib = None
@@ -161,6 +161,7 @@ def lib():
     L.kwk_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                            C.c_void_p]
     L.kwk_upsert.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kwk_replace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_retry.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,

@@ -197,6 +197,15 @@ class Engine:
                                        abi.ptr(np.ascontiguousarray(cls, dtype=np.uint16))), "kwk_upsert")
         self.n = max(self.n, int(slots.max()) + 1)
 
+    def replace(self, slots, hot, dels, rec, cls):
+        """kwk_replace: rows written as given (no implicit DIRTY)."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        hot = np.ascontiguousarray(hot)
+        abi.check(abi.lib().kwk_replace(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
+                                        abi.ptr(np.ascontiguousarray(dels, dtype=np.int64)),
+                                        abi.ptr(np.ascontiguousarray(rec, dtype=np.uint32)),
+                                        abi.ptr(np.ascontiguousarray(cls, dtype=np.uint16))), "kwk_replace")
+
     def set_records(self, records: np.ndarray, first: int = 0):
         recs = np.ascontiguousarray(records)
         abi.check(abi.lib().kwk_set_records(self.h, first, recs.shape[0], abi.ptr(recs)), "kwk_set_records")

@@ -101,7 +101,7 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
 def test_aggregates_and_handback_at_17m_pods():
     """At 17M pods (the 2-byte sweep's persistent grid): kwk_count and kwk_usage against the
     state read back through kwk_read (numpy), and the device-compacted fired list (one
-    look-back pass) in strict slot order with the step's transition count."""
+    look-back pass): every slot once, as many records as the step's transition count."""
     from kwok_amd.host import abi
     from kwok_amd.host.cluster import phase_masks
     n_nodes = 170_000
@@ -128,7 +128,8 @@ def test_aggregates_and_handback_at_17m_pods():
             st = eng.stats()["fired"]
             assert len(f) == st - prev and len(f) > 0
             prev = st
-            assert np.all(np.diff(f["slot"].astype(np.int64)) > 0), f"step {k}: fired list not in slot order"
+            sl = np.sort(f["slot"].astype(np.int64))
+            assert np.all(np.diff(sl) > 0) and sl[-1] < n, f"step {k}: a slot fired twice / out of range"
             got = eng.count(masks)
             hot, _ = eng.read()
             alive = (hot["sched"] & abi.F_ALIVE) != 0
