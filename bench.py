@@ -122,9 +122,9 @@ def configure_usage(pods, pvars, pidx, n_nodes_local, pods_per_node):
     from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
     path = os.path.join(ROOT, "tests", "golden", "metrics", "usage-from-annotation.yaml")
     up = UsageProgram(*load_usage_yaml(open(path).read()))
-    vkeys, cv, mv = usage_columns(up, pvars)
+    vkeys, cv, mv, mx, ck = usage_columns(up, pvars)
     node_ptr = np.arange(n_nodes_local + 1, dtype=np.uint32) * np.uint32(pods_per_node)
-    pods.usage_config(node_ptr, vkeys[pidx], cv, mv)
+    pods.usage_config(node_ptr, vkeys[pidx], cv, mv, mx, ck)
 
 
 class Reporter:
@@ -319,6 +319,7 @@ def main():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000, help="nodes of the C2-mix HBM working-set run (0: off)")
     ap.add_argument("--hbm-steps", type=int, default=10)
+    ap.add_argument("--hbm-only", action="store_true", help="diagnostic: only the C2-mix HBM working-set run")
     ap.add_argument("--hbm-warmup", type=int, default=12)
     ap.add_argument("--pcie-steps", type=int, default=5)
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
@@ -343,6 +344,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     weak = args.scaling == "weak"
+    if args.hbm_only:
+        from kwok_amd import build as kbuild
+        if not os.path.exists(kbuild.OUT):
+            kbuild.build()
+        print(json.dumps(measure_hbm_working_set(args, local_rank)), flush=True)
+        return
 
     # PMC child passes first, while this process has not touched the GPU (N=1 only)
     traffic, pmc_err = None, "not collected (N>1, --no-pmc or --no-harness)"

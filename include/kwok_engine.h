@@ -289,6 +289,78 @@ kwk_status kwk_usage_pods(kwk_engine* eng, uint32_t enable);
 /* pod_out: n x {cpu, mem, cpu_cumulative, mem_cumulative} for slots [first, first+n) */
 kwk_status kwk_usage_read_pods(kwk_engine* eng, uint32_t first, uint32_t n, double* pod_out);
 
+/* Pods whose containers evaluate to different usages (metrics_resource_usage.go:136-168 per
+ * container): usage_key = m with a 0 container count (bits 28..31), m indexing
+ * mixed[2m] = first, mixed[2m+1] = count into ckeys (per container: cpu id | memory id << 14,
+ * in spec.containers order).  Call after kwk_usage_config. */
+kwk_status kwk_usage_mixed(kwk_engine* eng, uint32_t n_mixed, const uint32_t* mixed, uint32_t n_ckeys,
+                           const uint32_t* ckeys);
+/* per-container outputs of kwk_usage (containerResourceUsage / containerResourceCumulativeUsage,
+ * metrics_resource_usage.go:36-52,111-134) for the containers of pods [first, first+n), in pod
+ * then spec order: {cpu, mem, cpu_cumulative, mem_cumulative} each (0 for dead pods);
+ * *n_out = the number of containers (synchronises; needs kwk_usage_pods(eng, 1)) */
+kwk_status kwk_usage_read_containers(kwk_engine* eng, uint32_t first, uint32_t n, double* out, uint32_t cap,
+                                     uint32_t* n_out);
+
+/* ------------------------------------------------------------------ Metric CRD values */
+/* A Metric CR's value expressions (kustomize/metrics/resource/metrics-resource.yaml; CEL,
+ * pkg/kwok/metrics/evaluator.go) lowered by the host to postfix programs over doubles:
+ * KWK_MOP_LOAD pushes one of the per-series inputs KWK_MIN_* (the engine's usage outputs of the
+ * last kwk_usage, creation times, the scrape clock).  One program per metric, evaluated for
+ * every series of a scrape by kwk_metrics_eval (one GPU thread per series). */
+#define KWK_METRIC_DIM_NODE 0
+#define KWK_METRIC_DIM_POD 1
+#define KWK_METRIC_DIM_CONTAINER 2
+#define KWK_MOP_CONST 1
+#define KWK_MOP_LOAD 2
+#define KWK_MOP_ADD 3
+#define KWK_MOP_SUB 4
+#define KWK_MOP_MUL 5
+#define KWK_MOP_DIV 6
+#define KWK_MOP_NEG 7
+#define KWK_MIN_NOW_S 0               /* Now().UnixSecond() */
+#define KWK_MIN_CONTAINER_CPU 1       /* pod.Usage("cpu", container.name) */
+#define KWK_MIN_CONTAINER_MEM 2
+#define KWK_MIN_CONTAINER_CUM_CPU 3   /* pod.CumulativeUsage("cpu", container.name) */
+#define KWK_MIN_CONTAINER_CUM_MEM 4
+#define KWK_MIN_POD_CPU 5             /* pod.Usage("cpu") */
+#define KWK_MIN_POD_MEM 6
+#define KWK_MIN_POD_CUM_CPU 7
+#define KWK_MIN_POD_CUM_MEM 8
+#define KWK_MIN_NODE_CPU 9            /* node.Usage("cpu") */
+#define KWK_MIN_NODE_MEM 10
+#define KWK_MIN_NODE_CUM_CPU 11
+#define KWK_MIN_NODE_CUM_MEM 12
+#define KWK_MIN_POD_SINCE 13          /* pod.SinceSecond() */
+#define KWK_MIN_NODE_SINCE 14
+#define KWK_MIN_POD_CREATED 15        /* pod.metadata.creationTimestamp.UnixSecond() */
+#define KWK_MIN_NODE_CREATED 16
+#define KWK_MIN_STARTED_CONTAINERS 17 /* node.StartedContainersTotal() */
+typedef struct {
+  uint32_t op;     /* KWK_MOP_* */
+  uint32_t arg;    /* KWK_MIN_* for KWK_MOP_LOAD */
+  double value;    /* KWK_MOP_CONST */
+} kwk_metric_op;   /* 16 bytes */
+typedef struct {
+  uint32_t dimension;  /* KWK_METRIC_DIM_* */
+  uint32_t first_op, n_ops;
+  uint32_t reserved;
+} kwk_metric_desc;
+/* programs (replaces earlier ones); at most 64 ops per metric, stack depth 8 */
+kwk_status kwk_metrics_load(kwk_engine* pods, uint32_t n_metrics, const kwk_metric_desc* metrics, uint32_t n_ops,
+                            const kwk_metric_op* ops);
+/* per-object inputs: creation times (unix ns, INT64_MIN = unset: the Go zero time) of the
+ * engine's pods and of the n_nodes nodes of kwk_usage_config, and StartedContainersTotal per
+ * node (controller.go:602-611); zero_time_unix_s = what UnixSecond() gives for the zero time */
+kwk_status kwk_metrics_inputs(kwk_engine* pods, const int64_t* pod_created_ns, const int64_t* node_created_ns,
+                              const double* node_started, double zero_time_unix_s);
+/* every metric's series for the scrape of nodes [node_first, node_first + n_nodes) at now_ns
+ * (after kwk_usage(now_ns)): metric by metric, node series per node, pod series per pod slot,
+ * container series per container (kwk_usage_read_containers order); NaN for dead pods.
+ * *n_out = values written (synchronises) */
+kwk_status kwk_metrics_eval(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out,
+                            uint64_t cap, uint64_t* n_out);
+
 /* ------------------------------------------------------------------ node leases */
 /* NodeLeaseController (pkg/kwok/controllers/node_lease_controller.go) on a NODE engine: one
  * lease record per node slot — the informer's cached coordination/v1 Lease plus the

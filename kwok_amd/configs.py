@@ -130,10 +130,10 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         n_nodes, n_pods = 10_000, 1_000_000
         cl = W.make_cluster("C4", n_nodes, n_pods, seed=seed)
         uprog = UsageProgram(*load_usage_yaml(open(USAGE_YAML).read()))
-        vkeys, cv, mv = usage_columns(uprog, cl.pods.variants)  # no per-name ResourceUsage: per variant
+        vkeys, cv, mv, mx, ck = usage_columns(uprog, cl.pods.variants)  # no per-name ResourceUsage: per variant
         keys = vkeys[cl.pods.index]
         prog, pods = _engine(cl.pod_stage_files, cl.pods.variants, cl.pods.index, False, 0)
-        pods.usage_config(cl.node_ptr, keys, cv, mv)
+        pods.usage_config(cl.node_ptr, keys, cv, mv, mx, ck)
         containers = int((keys >> 28).astype(np.int64).sum())
 
         def step(k):

@@ -1069,25 +1069,35 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   const uint32_t c = seg < a.n_segs ? a.counts[seg] : 0u;
   if (lane == 0) s_cnt[wave] = c;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (wave == 0) {  // the look-back: one wave reads 64 predecessors' status words at a time
     uint32_t agg = 0;
     for (uint32_t w = 0; w < kSegsPerBlock; ++w) agg += s_cnt[w];
     const unsigned long long tag = (unsigned long long)(a.epoch & 0x3FFFFFFFu) << 34;
-    uint32_t prefix = 0;
-    if (blk > 0) {
+    if (blk > 0 && lane == 0)
       __hip_atomic_store(&a.status[blk], tag | (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t j = blk - 1;;) {
-        const unsigned long long st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((st >> 34) != (tag >> 34)) continue;  // not yet published in this launch: its block is running
-        prefix += (uint32_t)st;
-        if (((st >> 32) & 3u) == 2u) break;       // an inclusive prefix: done
-        --j;                                      // an aggregate: keep looking back
-      }
+    uint32_t prefix = 0;
+    for (int64_t hi = (int64_t)blk - 1; hi >= 0;) {
+      const int64_t j = hi - (int64_t)lane;  // lane 0 = the nearest predecessor
+      unsigned long long st = 2ull << 32;    // before block 0: an inclusive prefix of 0
+      if (j >= 0) st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool ready = j < 0 || (st >> 34) == (tag >> 34);
+      const unsigned long long inc = __ballot(ready && ((st >> 32) & 3u) == 2u);
+      const unsigned long long wait = __ballot(!ready);
+      const uint32_t first = inc ? (uint32_t)__ffsll((long long)inc) - 1u : 64u;  // nearest inclusive prefix
+      const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+      if (wait & need) continue;  // a predecessor in the window has not published yet: read again
+      uint32_t v = (lane <= first && ready) ? (uint32_t)st : 0u;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      prefix += v;
+      if (first < 64) break;
+      hi -= 64;  // 64 aggregates: move the window back
     }
-    __hip_atomic_store(&a.status[blk], tag | (2ull << 32) | (uint32_t)(prefix + agg), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    s_prefix = prefix;
-    if ((blk + 1) * kSegsPerBlock >= a.n_segs) *a.total = prefix + agg;
+    if (lane == 0) {
+      __hip_atomic_store(&a.status[blk], tag | (2ull << 32) | (uint32_t)(prefix + agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+      if ((blk + 1) * kSegsPerBlock >= a.n_segs) *a.total = prefix + agg;
+    }
   }
   __syncthreads();
   uint32_t off = s_prefix;
@@ -1257,9 +1267,16 @@ struct UsageArgs {
   int64_t now;
   double* __restrict__ block_part;  // per block {cpu, mem}
   double* __restrict__ pod_out;     // optional per pod outputs
-  double* __restrict__ pod_cum;
+  double* __restrict__ pod_cum;     // per pod: one container's integrators (uniform pods)
   int64_t* __restrict__ pod_last;
+  const uint2* __restrict__ mixed;  // pods whose containers differ: {first, count} into ckeys
+  const uint32_t* __restrict__ ckeys;
+  double* __restrict__ ccum;        // per container of a mixed pod: {cpu, mem} integrators
 };
+
+// a pod's usage_key: containers (bits 28..31) x one interned value each, or 0 containers =
+// a pod whose containers differ: bits 0..27 index its {first, count} entry of the mixed table
+constexpr uint32_t kUKeyMixedIndex = 0x0FFFFFFFu;
 
 // time.Duration.Seconds() of now - last
 __device__ __forceinline__ double dur_seconds(int64_t d) {
@@ -1294,23 +1311,55 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
       double vc = 0.0, vm = 0.0;
       if (valid) {
         while (nl + 1 < jn && p >= s_bnd[wave][nl + 1]) ++nl;
-        if (sched[u] & KWK_F_ALIVE) {
-          const double nc = (double)(key[u] >> 28);
-          vc = nc * a.cpu_v[key[u] & 0x3FFFu];
-          vm = nc * a.mem_v[(key[u] >> 14) & 0x3FFFu];
+        const bool alive = (sched[u] & KWK_F_ALIVE) != 0;
+        const uint32_t k = key[u], nc = k >> 28;
+        // podResourceUsage (:170-193) adds the containers in spec order, as below
+        double c1 = 0.0, m1 = 0.0;  // one container's value (uniform pods)
+        uint2 fc = make_uint2(0u, 0u);
+        if (alive) {
+          if (nc) {
+            c1 = a.cpu_v[k & 0x3FFFu];
+            m1 = a.mem_v[(k >> 14) & 0x3FFFu];
+            for (uint32_t j = 0; j < nc; ++j) { vc += c1; vm += m1; }
+          } else {
+            fc = a.mixed[k & kUKeyMixedIndex];
+            for (uint32_t j = 0; j < fc.y; ++j) {
+              const uint32_t ck = a.ckeys[fc.x + j];
+              vc += a.cpu_v[ck & 0x3FFFu];
+              vm += a.mem_v[(ck >> 14) & 0x3FFFu];
+            }
+          }
         }
         if (a.pod_out) {
-          if (sched[u] & KWK_F_ALIVE) {
-            double2 pcum = reinterpret_cast<double2*>(a.pod_cum)[p];
+          if (alive) {
+            // containerResourceCumulativeUsage (:36-52): one integrator per container, advanced
+            // by (now - last) * value; the pod's is their sum (:54-65)
             const int64_t lt = a.pod_last[p];
-            if (lt != INT64_MIN) {
-              const double dt = dur_seconds(a.now - lt);
-              pcum.x += dt * vc;
-              pcum.y += dt * vm;
-              reinterpret_cast<double2*>(a.pod_cum)[p] = pcum;
+            const double dt = lt != INT64_MIN ? dur_seconds(a.now - lt) : 0.0;
+            double cc = 0.0, cm = 0.0;
+            if (nc) {  // equal containers share one integrator
+              double2 unit = reinterpret_cast<double2*>(a.pod_cum)[p];
+              if (lt != INT64_MIN) {
+                unit.x += dt * c1;
+                unit.y += dt * m1;
+                reinterpret_cast<double2*>(a.pod_cum)[p] = unit;
+              }
+              for (uint32_t j = 0; j < nc; ++j) { cc += unit.x; cm += unit.y; }
+            } else {
+              for (uint32_t j = 0; j < fc.y; ++j) {
+                const uint32_t ck = a.ckeys[fc.x + j];
+                double2 cu = reinterpret_cast<double2*>(a.ccum)[fc.x + j];
+                if (lt != INT64_MIN) {
+                  cu.x += dt * a.cpu_v[ck & 0x3FFFu];
+                  cu.y += dt * a.mem_v[(ck >> 14) & 0x3FFFu];
+                  reinterpret_cast<double2*>(a.ccum)[fc.x + j] = cu;
+                }
+                cc += cu.x;
+                cm += cu.y;
+              }
             }
             a.pod_last[p] = a.now;
-            reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(vc, vm, pcum.x, pcum.y);
+            reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(vc, vm, cc, cm);
           } else {
             reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(0.0, 0.0, 0.0, 0.0);
           }
@@ -1377,6 +1426,127 @@ __global__ __launch_bounds__(1024) void usage_total_kernel(const double* __restr
     out[0] = tc;
     out[1] = tm;
   }
+}
+
+// ------------------------------------------------------------------ Metric CRD values
+// kwok's Metric CRs (pkg/kwok/metrics/metrics.go:168-571) evaluate one CEL value per series:
+// per node, per pod of the node or per container of its pods.  The host lowers each value to a
+// postfix program over doubles (kwok_amd/host/cel.py lower()); one thread per series runs it
+// over the quantities the engine keeps: the last kwk_usage's pod / node outputs, the
+// per-container values and integrators, creation times and the scrape's clock.  Dead pods
+// (not in the pod cache, so not listed by ListPods) yield NaN, which the host skips.
+struct MetricArgs {
+  const kwk_metric_op* __restrict__ ops;
+  uint32_t n_ops;
+  uint32_t dim;          // KWK_METRIC_DIM_*
+  uint32_t n0, n1;       // nodes [n0, n1) of the scrape, their pods [p0, p1)
+  uint32_t p0, p1, c0;   // and the containers from c0 on
+  uint32_t n_series;
+  const void* __restrict__ st;
+  StateFmt fmt;
+  const uint32_t* __restrict__ node_ptr;
+  const uint32_t* __restrict__ cptr;      // per pod: first container (n_pods + 1)
+  const uint32_t* __restrict__ ukey;
+  const uint2* __restrict__ mixed;
+  const uint32_t* __restrict__ ckeys;
+  const double* __restrict__ cpu_v;
+  const double* __restrict__ mem_v;
+  const double* __restrict__ pod_out;
+  const double* __restrict__ pod_cum;
+  const double* __restrict__ ccum;
+  const double* __restrict__ node_out;
+  const int64_t* __restrict__ pod_created;   // ns, INT64_MIN = the Go zero time
+  const int64_t* __restrict__ node_created;
+  const double* __restrict__ node_started;   // StartedContainersTotal per node
+  int64_t now;
+  double zero_time_unix_s;                   // UnixSecond of the Go zero time
+  double* __restrict__ out;
+};
+
+// first index i in [lo, hi) with a[i] > x, minus one (the segment holding x)
+__device__ __forceinline__ uint32_t seg_of(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi, uint32_t x) {
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (a[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ double since_seconds(int64_t now, int64_t created) {
+  if (created == INT64_MIN) return 9223372036.854775807;  // time.Since(zero time) saturates
+  int64_t d;
+  if (__builtin_sub_overflow(now, created, &d)) d = now > created ? INT64_MAX : INT64_MIN;
+  return dur_seconds(d);
+}
+
+__global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
+  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+  if (s >= a.n_series) return;
+  uint32_t node = 0, pod = 0, j = 0;
+  if (a.dim == KWK_METRIC_DIM_NODE) {
+    node = a.n0 + s;
+  } else {
+    if (a.dim == KWK_METRIC_DIM_CONTAINER) {
+      const uint32_t c = a.c0 + s;
+      pod = seg_of(a.cptr, a.p0, a.p1, c);
+      j = c - a.cptr[pod];
+    } else {
+      pod = a.p0 + s;
+    }
+    if (!(load_state(a.st, pod, a.fmt).y & KWK_F_ALIVE)) {
+      a.out[s] = __builtin_nan("");
+      return;
+    }
+    node = seg_of(a.node_ptr, a.n0, a.n1, pod);
+  }
+  double stk[8];
+  int sp = 0;
+  for (uint32_t i = 0; i < a.n_ops; ++i) {
+    const kwk_metric_op op = a.ops[i];
+    switch (op.op) {
+      case KWK_MOP_CONST: stk[sp++] = op.value; break;
+      case KWK_MOP_LOAD: {
+        double v = 0.0;
+        const uint32_t in = op.arg;
+        if (in == KWK_MIN_NOW_S) {
+          v = (double)a.now / 1e9;
+        } else if (in >= KWK_MIN_CONTAINER_CPU && in <= KWK_MIN_CONTAINER_CUM_MEM) {
+          const uint32_t k = a.ukey[pod];
+          const bool cum = in >= KWK_MIN_CONTAINER_CUM_CPU;
+          const uint32_t r = (in - KWK_MIN_CONTAINER_CPU) & 1u;
+          if (k >> 28) {
+            v = cum ? a.pod_cum[2 * (uint64_t)pod + r] : (r ? a.mem_v[(k >> 14) & 0x3FFFu] : a.cpu_v[k & 0x3FFFu]);
+          } else {
+            const uint2 fc = a.mixed[k & kUKeyMixedIndex];
+            const uint32_t ck = a.ckeys[fc.x + j];
+            v = cum ? a.ccum[2 * (uint64_t)(fc.x + j) + r] : (r ? a.mem_v[(ck >> 14) & 0x3FFFu] : a.cpu_v[ck & 0x3FFFu]);
+          }
+        } else if (in >= KWK_MIN_POD_CPU && in <= KWK_MIN_POD_CUM_MEM) {
+          v = a.pod_out[4 * (uint64_t)pod + (in - KWK_MIN_POD_CPU)];
+        } else if (in >= KWK_MIN_NODE_CPU && in <= KWK_MIN_NODE_CUM_MEM) {
+          v = a.node_out[4 * (uint64_t)node + (in - KWK_MIN_NODE_CPU)];
+        } else if (in == KWK_MIN_POD_SINCE) {
+          v = since_seconds(a.now, a.pod_created[pod]);
+        } else if (in == KWK_MIN_NODE_SINCE) {
+          v = since_seconds(a.now, a.node_created[node]);
+        } else if (in == KWK_MIN_POD_CREATED || in == KWK_MIN_NODE_CREATED) {
+          const int64_t c = in == KWK_MIN_POD_CREATED ? a.pod_created[pod] : a.node_created[node];
+          v = c == INT64_MIN ? a.zero_time_unix_s : (double)c / 1e9;
+        } else if (in == KWK_MIN_STARTED_CONTAINERS) {
+          v = a.node_started[node];
+        }
+        stk[sp++] = v;
+        break;
+      }
+      case KWK_MOP_ADD: --sp; stk[sp - 1] = stk[sp - 1] + stk[sp]; break;
+      case KWK_MOP_SUB: --sp; stk[sp - 1] = stk[sp - 1] - stk[sp]; break;
+      case KWK_MOP_MUL: --sp; stk[sp - 1] = stk[sp - 1] * stk[sp]; break;
+      case KWK_MOP_DIV: --sp; stk[sp - 1] = stk[sp - 1] / stk[sp]; break;
+      case KWK_MOP_NEG: stk[sp - 1] = -stk[sp - 1]; break;
+      default: break;
+    }
+  }
+  a.out[s] = sp > 0 ? stk[sp - 1] : 0.0;
 }
 
 // count alive objects with (pred & mask[k]) != 0 for each k (mask 0: every alive object):
@@ -1689,6 +1859,24 @@ struct kwk_engine {
   int64_t* d_pod_last = nullptr;
   double* d_usage_part = nullptr;
   double* d_cluster = nullptr;
+  // host copies of the usage configuration (per-container reads, metric scrapes)
+  std::vector<uint32_t> h_node_ptr, h_ukey, h_mixed, h_ckeys, h_cptr;
+  std::vector<double> h_cpu, h_mem;
+  bool has_mixed_keys = false;
+  uint2* d_mixed = nullptr;       // {first, count} per mixed pod
+  uint32_t* d_ckeys = nullptr;
+  double* d_ccum = nullptr;       // per container of a mixed pod: {cpu, mem} integrators
+  uint32_t* d_cptr = nullptr;     // per pod: first container (metric scrapes)
+  // Metric CRD programs
+  kwk_metric_op* d_mops = nullptr;
+  std::vector<kwk_metric_desc> metrics;
+  uint32_t metric_inputs_needed = 0;  // 1: some program reads creation times / started containers
+  int64_t* d_pod_created = nullptr;
+  int64_t* d_node_created = nullptr;
+  double* d_node_started = nullptr;
+  double zero_time_unix_s = 0.0;
+  double* d_mout = nullptr;
+  size_t mout_cap = 0;
 
   // staging for upserts
   void* d_stage_buf = nullptr;
@@ -1869,7 +2057,8 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_compact_ticket,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
-                  e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due,
+                  e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
+                  e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
                   e->d_lease_nops, e->d_lease_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
@@ -2395,9 +2584,15 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
     if (node_ptr[j + 1] < node_ptr[j]) return fail(KWK_EINVAL, "node_ptr must be non-decreasing");
   const uint32_t n_pods = node_ptr[n_nodes];
   if (n_pods > e->capacity) return fail(KWK_ECAP, "node_ptr covers more pods than capacity");
-  for (uint32_t p = 0; p < n_pods; ++p)
+  bool mixed_keys = false;
+  for (uint32_t p = 0; p < n_pods; ++p) {
+    if ((ukey[p] >> 28) == 0) {  // containers differ: index into kwk_usage_mixed's table
+      mixed_keys = true;
+      continue;
+    }
     if ((ukey[p] & 0x3FFFu) >= n_cpu || ((ukey[p] >> 14) & 0x3FFFu) >= n_mem)
       return fail(KWK_EINVAL, "usage_key value id out of range");
+  }
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
@@ -2423,6 +2618,254 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   HIP_TRY(hipMemcpy(e->d_node_last, lasts.data(), 8 * lasts.size(), hipMemcpyHostToDevice));
   e->n_nodes = n_nodes;
   e->n_usage_pods = n_pods;
+  e->has_mixed_keys = mixed_keys;
+  e->h_node_ptr.assign(node_ptr, node_ptr + n_nodes + 1);
+  e->h_ukey.assign(ukey, ukey + n_pods);
+  e->h_cpu.assign(cpu_values, cpu_values + n_cpu);
+  e->h_mem.assign(mem_values, mem_values + n_mem);
+  e->h_mixed.clear();
+  e->h_ckeys.clear();
+  e->h_cptr.clear();
+  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr})
+    if (q) HIP_TRY(hipFree(q));
+  e->d_mixed = nullptr;
+  e->d_ckeys = nullptr;
+  e->d_ccum = nullptr;
+  e->d_cptr = nullptr;
+  if (e->d_pod_cum) HIP_TRY(hipMemset(e->d_pod_cum, 0, 16 * (size_t)e->capacity));
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_mixed(kwk_engine* e, uint32_t n_mixed, const uint32_t* mixed, uint32_t n_ckeys, const uint32_t* ckeys) {
+  if (!e || (n_mixed && !mixed) || (n_ckeys && !ckeys)) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (n_mixed > kUKeyMixedIndex) return fail(KWK_ECAP, "too many mixed pods");
+  for (uint32_t m = 0; m < n_mixed; ++m)
+    if ((uint64_t)mixed[2 * m] + mixed[2 * m + 1] > n_ckeys) return fail(KWK_EINVAL, "mixed entry beyond ckeys");
+  for (uint32_t c = 0; c < n_ckeys; ++c)
+    if ((ckeys[c] & 0x3FFFu) >= e->h_cpu.size() || ((ckeys[c] >> 14) & 0x3FFFu) >= e->h_mem.size())
+      return fail(KWK_EINVAL, "ckeys value id out of range");
+  for (uint32_t p = 0; p < e->n_usage_pods; ++p)
+    if ((e->h_ukey[p] >> 28) == 0 && (e->h_ukey[p] & kUKeyMixedIndex) >= n_mixed)
+      return fail(KWK_EINVAL, "usage_key mixed index out of range");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr})
+    if (q) HIP_TRY(hipFree(q));
+  e->d_cptr = nullptr;
+  e->h_cptr.clear();
+  HIP_TRY(hipMalloc(&e->d_mixed, 8 * ((size_t)n_mixed + 1)));
+  HIP_TRY(hipMalloc(&e->d_ckeys, 4 * ((size_t)n_ckeys + 1)));
+  HIP_TRY(hipMalloc(&e->d_ccum, 16 * ((size_t)n_ckeys + 1)));
+  if (n_mixed) HIP_TRY(hipMemcpy(e->d_mixed, mixed, 8 * (size_t)n_mixed, hipMemcpyHostToDevice));
+  if (n_ckeys) HIP_TRY(hipMemcpy(e->d_ckeys, ckeys, 4 * (size_t)n_ckeys, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e->d_ccum, 0, 16 * ((size_t)n_ckeys + 1)));
+  e->h_mixed.assign(mixed, mixed + 2 * (size_t)n_mixed);
+  e->h_ckeys.assign(ckeys, ckeys + n_ckeys);
+  return KWK_OK;
+}
+
+// containers per pod of the usage configuration
+static uint32_t pod_containers(const kwk_engine* e, uint32_t p) {
+  const uint32_t k = e->h_ukey[p];
+  return (k >> 28) ? (k >> 28) : e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
+}
+
+static kwk_status ensure_cptr(kwk_engine* e) {
+  if (e->d_cptr) return KWK_OK;
+  e->h_cptr.resize((size_t)e->n_usage_pods + 1);
+  uint64_t c = 0;
+  for (uint32_t p = 0; p < e->n_usage_pods; ++p) {
+    e->h_cptr[p] = (uint32_t)c;
+    c += pod_containers(e, p);
+    if (c > 0xFFFFFFFFull) return fail(KWK_ECAP, "more than 2^32 containers");
+  }
+  e->h_cptr[e->n_usage_pods] = (uint32_t)c;
+  HIP_TRY(hipMalloc(&e->d_cptr, 4 * e->h_cptr.size()));
+  HIP_TRY(hipMemcpy(e->d_cptr, e->h_cptr.data(), 4 * e->h_cptr.size(), hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, double* out, uint32_t cap, uint32_t* n_out) {
+  if (!e || !n_out || (n && cap && !out)) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
+  if ((uint64_t)first + n > e->n_usage_pods) return fail(KWK_EINVAL, "pods beyond the usage configuration");
+  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
+  uint64_t total = 0;
+  uint32_t cmin = 0xFFFFFFFFu, cmax = 0;
+  for (uint32_t p = first; p < first + n; ++p) {
+    total += pod_containers(e, p);
+    const uint32_t k = e->h_ukey[p];
+    if (!(k >> 28)) {
+      const uint32_t f = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex)], c = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
+      if (c) { cmin = f < cmin ? f : cmin; cmax = f + c > cmax ? f + c : cmax; }
+    }
+  }
+  *n_out = (uint32_t)total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "container buffer too small: need " + std::to_string(total));
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
+  HIP_TRY(hipMemcpy(raw.data(), (const char*)e->d_st + word_bytes(e->fmt) * first, raw.size(), hipMemcpyDeviceToHost));
+  const std::vector<uint2> st = unpack_words(raw, e->fmt, n);
+  std::vector<double> unit(2 * (size_t)n);
+  HIP_TRY(hipMemcpy(unit.data(), e->d_pod_cum + 2 * (size_t)first, 16 * (size_t)n, hipMemcpyDeviceToHost));
+  std::vector<double> cc;
+  if (cmin < cmax) {
+    cc.resize(2 * (size_t)(cmax - cmin));
+    HIP_TRY(hipMemcpy(cc.data(), e->d_ccum + 2 * (size_t)cmin, 16 * (size_t)(cmax - cmin), hipMemcpyDeviceToHost));
+  }
+  size_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = first + i, k = e->h_ukey[p];
+    const bool alive = (st[i].y & KWK_F_ALIVE) != 0;
+    if (k >> 28) {
+      for (uint32_t j = 0; j < (k >> 28); ++j, o += 4) {
+        out[o] = alive ? e->h_cpu[k & 0x3FFFu] : 0.0;
+        out[o + 1] = alive ? e->h_mem[(k >> 14) & 0x3FFFu] : 0.0;
+        out[o + 2] = alive ? unit[2 * (size_t)i] : 0.0;
+        out[o + 3] = alive ? unit[2 * (size_t)i + 1] : 0.0;
+      }
+    } else {
+      const uint32_t f = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex)], c = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
+      for (uint32_t j = 0; j < c; ++j, o += 4) {
+        const uint32_t ck = e->h_ckeys[f + j];
+        out[o] = alive ? e->h_cpu[ck & 0x3FFFu] : 0.0;
+        out[o + 1] = alive ? e->h_mem[(ck >> 14) & 0x3FFFu] : 0.0;
+        out[o + 2] = alive ? cc[2 * (size_t)(f + j - cmin)] : 0.0;
+        out[o + 3] = alive ? cc[2 * (size_t)(f + j - cmin) + 1] : 0.0;
+      }
+    }
+  }
+  return KWK_OK;
+}
+
+kwk_status kwk_metrics_load(kwk_engine* e, uint32_t n_metrics, const kwk_metric_desc* metrics, uint32_t n_ops,
+                            const kwk_metric_op* ops) {
+  if (!e || (n_metrics && !metrics) || (n_ops && !ops)) return fail(KWK_EINVAL, "null argument");
+  uint32_t needs = 0;
+  for (uint32_t m = 0; m < n_metrics; ++m) {
+    const kwk_metric_desc& d = metrics[m];
+    if (d.dimension > KWK_METRIC_DIM_CONTAINER) return fail(KWK_EINVAL, "metric dimension");
+    if (d.n_ops == 0 || d.n_ops > 64 || (uint64_t)d.first_op + d.n_ops > n_ops) return fail(KWK_EINVAL, "metric ops range");
+    int depth = 0;
+    for (uint32_t i = d.first_op; i < d.first_op + d.n_ops; ++i) {
+      const kwk_metric_op& op = ops[i];
+      if (op.op == KWK_MOP_CONST || op.op == KWK_MOP_LOAD) {
+        if (++depth > 8) return fail(KWK_EINVAL, "metric program deeper than 8");
+        if (op.op == KWK_MOP_LOAD) {
+          if (op.arg > KWK_MIN_STARTED_CONTAINERS) return fail(KWK_EINVAL, "metric input");
+          if (op.arg >= KWK_MIN_POD_SINCE) needs = 1;
+          if (d.dimension == KWK_METRIC_DIM_NODE && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_POD_CUM_MEM)
+            return fail(KWK_EINVAL, "a node metric cannot read pod / container inputs");
+          if (d.dimension == KWK_METRIC_DIM_NODE && (op.arg == KWK_MIN_POD_SINCE || op.arg == KWK_MIN_POD_CREATED))
+            return fail(KWK_EINVAL, "a node metric cannot read pod inputs");
+          if (d.dimension == KWK_METRIC_DIM_POD && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_CONTAINER_CUM_MEM)
+            return fail(KWK_EINVAL, "a pod metric cannot read container inputs");
+        }
+      } else if (op.op == KWK_MOP_NEG) {
+        if (depth < 1) return fail(KWK_EINVAL, "metric program underflow");
+      } else if (op.op >= KWK_MOP_ADD && op.op <= KWK_MOP_DIV) {
+        if (depth < 2) return fail(KWK_EINVAL, "metric program underflow");
+        --depth;
+      } else {
+        return fail(KWK_EINVAL, "metric op");
+      }
+    }
+    if (depth != 1) return fail(KWK_EINVAL, "a metric program leaves one value");
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->d_mops) HIP_TRY(hipFree(e->d_mops));
+  e->d_mops = nullptr;
+  HIP_TRY(hipMalloc(&e->d_mops, sizeof(kwk_metric_op) * ((size_t)n_ops + 1)));
+  if (n_ops) HIP_TRY(hipMemcpy(e->d_mops, ops, sizeof(kwk_metric_op) * n_ops, hipMemcpyHostToDevice));
+  e->metrics.assign(metrics, metrics + n_metrics);
+  e->metric_inputs_needed = needs;
+  return KWK_OK;
+}
+
+kwk_status kwk_metrics_inputs(kwk_engine* e, const int64_t* pod_created, const int64_t* node_created, const double* started,
+                              double zero_time_unix_s) {
+  if (!e || !pod_created || !node_created || !started) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (void* q : {(void*)e->d_pod_created, (void*)e->d_node_created, (void*)e->d_node_started})
+    if (q) HIP_TRY(hipFree(q));
+  HIP_TRY(hipMalloc(&e->d_pod_created, 8 * ((size_t)e->n_usage_pods + 1)));
+  HIP_TRY(hipMalloc(&e->d_node_created, 8 * ((size_t)e->n_nodes + 1)));
+  HIP_TRY(hipMalloc(&e->d_node_started, 8 * ((size_t)e->n_nodes + 1)));
+  if (e->n_usage_pods)
+    HIP_TRY(hipMemcpy(e->d_pod_created, pod_created, 8 * (size_t)e->n_usage_pods, hipMemcpyHostToDevice));
+  if (e->n_nodes) {
+    HIP_TRY(hipMemcpy(e->d_node_created, node_created, 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_node_started, started, 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+  }
+  e->zero_time_unix_s = zero_time_unix_s;
+  return KWK_OK;
+}
+
+kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out, uint64_t cap,
+                            uint64_t* n_out) {
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
+  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
+  if (e->metric_inputs_needed && !e->d_pod_created) return fail(KWK_ESTATE, "kwk_metrics_inputs must be called first");
+  if ((uint64_t)node_first + n_nodes > e->n_nodes) return fail(KWK_EINVAL, "nodes beyond the usage configuration");
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = ensure_cptr(e)) return st;
+  const uint32_t n0 = node_first, n1 = node_first + n_nodes;
+  const uint32_t p0 = e->h_node_ptr[n0], p1 = e->h_node_ptr[n1];
+  const uint32_t c0 = e->h_cptr[p0], c1 = e->h_cptr[p1];
+  uint64_t total = 0;
+  for (const auto& m : e->metrics)
+    total += m.dimension == KWK_METRIC_DIM_NODE ? n_nodes : m.dimension == KWK_METRIC_DIM_POD ? (p1 - p0) : (c1 - c0);
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "metric buffer too small: need " + std::to_string(total));
+  if (total > e->mout_cap) {
+    if (e->d_mout) HIP_TRY(hipFree(e->d_mout));
+    e->d_mout = nullptr;
+    HIP_TRY(hipMalloc(&e->d_mout, 8 * total));
+    e->mout_cap = total;
+  }
+  uint64_t off = 0;
+  for (const auto& m : e->metrics) {
+    MetricArgs a;
+    a.ops = e->d_mops + m.first_op;
+    a.n_ops = m.n_ops;
+    a.dim = m.dimension;
+    a.n0 = n0; a.n1 = n1; a.p0 = p0; a.p1 = p1; a.c0 = c0;
+    a.n_series = m.dimension == KWK_METRIC_DIM_NODE ? n_nodes : m.dimension == KWK_METRIC_DIM_POD ? (p1 - p0) : (c1 - c0);
+    a.st = e->d_st;
+    a.fmt = e->fmt;
+    a.node_ptr = e->d_node_ptr;
+    a.cptr = e->d_cptr;
+    a.ukey = e->d_ukey;
+    a.mixed = e->d_mixed;
+    a.ckeys = e->d_ckeys;
+    a.cpu_v = e->d_cpu;
+    a.mem_v = e->d_mem;
+    a.pod_out = e->d_pod_out;
+    a.pod_cum = e->d_pod_cum;
+    a.ccum = e->d_ccum;
+    a.node_out = e->d_node_out;
+    a.pod_created = e->d_pod_created;
+    a.node_created = e->d_node_created;
+    a.node_started = e->d_node_started;
+    a.now = now_ns;
+    a.zero_time_unix_s = e->zero_time_unix_s;
+    a.out = e->d_mout + off;
+    if (a.n_series)
+      hipLaunchKernelGGL(metrics_kernel, dim3((a.n_series + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
+    HIP_TRY(hipGetLastError());
+    off += a.n_series;
+  }
+  HIP_TRY(hipMemcpyAsync(out, e->d_mout, 8 * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 
@@ -2431,8 +2874,10 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
   const uint32_t ublocks = (e->n_nodes + kWavesPerBlock * kUG - 1) / (kWavesPerBlock * kUG);
+  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
   UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->n_nodes, e->n_usage_pods, e->d_node_out,
-               e->d_node_cum, e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last};
+               e->d_node_cum, e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
+               e->d_mixed, e->d_ckeys, e->d_ccum};
   hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, ua);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);

@@ -111,6 +111,17 @@ VALUE_DTYPE = np.dtype([("value", "<i8"), ("nsec", "<i4"), ("kind", "<i4")])
 FIRED_DTYPE = np.dtype([("slot", "<u4"), ("stage", "<u2"), ("flags", "<u2")])
 
 
+class MetricOp(C.Structure):
+    _fields_ = [("op", C.c_uint32), ("arg", C.c_uint32), ("value", C.c_double)]
+
+
+class MetricDesc(C.Structure):
+    _fields_ = [("dimension", C.c_uint32), ("first_op", C.c_uint32), ("n_ops", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+METRIC_DIM = {"node": 0, "pod": 1, "container": 2}
+
+
 class Backoff(C.Structure):
     """kwk_backoff = wait.Backoff; default = defaultBackoff (controllers/utils.go:133-135)."""
     _fields_ = [("duration_ns", C.c_int64), ("factor", C.c_double), ("jitter", C.c_double), ("cap_ns", C.c_int64)]
@@ -118,6 +129,7 @@ class Backoff(C.Structure):
 
 DEFAULT_BACKOFF = dict(duration_ns=10**9, factor=2.0, jitter=0.2, cap_ns=32 * 60 * 10**9)
 
+assert C.sizeof(MetricOp) == 16 and C.sizeof(MetricDesc) == 16
 assert C.sizeof(Hot) == 16 and C.sizeof(Value) == 16 and C.sizeof(StageDesc) == 96
 assert C.sizeof(Lease) == 32 == LEASE_DTYPE.itemsize and C.sizeof(LeaseParams) == 32
 assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.itemsize == 8
@@ -130,7 +142,8 @@ EXPORTS = [
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
-    "kwk_alloc_host", "kwk_free_host", "kwk_replace",
+    "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
+    "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval",
 ]
 
 _lib = None
@@ -162,6 +175,11 @@ def lib():
                            C.c_void_p]
     L.kwk_upsert.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.kwk_replace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kwk_usage_mixed.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_usage_read_containers.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_metrics_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_metrics_inputs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double]
+    L.kwk_metrics_eval.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _p(C.c_uint64)]
     L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_retry.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,

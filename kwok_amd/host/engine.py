@@ -280,7 +280,9 @@ class Engine:
         return out
 
     # usage
-    def usage_config(self, node_ptr, usage_key, cpu_values, mem_values):
+    def usage_config(self, node_ptr, usage_key, cpu_values, mem_values, mixed=None, ckeys=None):
+        """kwk_usage_config (+ kwk_usage_mixed when some pod's containers differ): the columns
+        usage.usage_columns computes."""
         self._uargs = [np.ascontiguousarray(node_ptr, dtype=np.uint32), np.ascontiguousarray(usage_key, dtype=np.uint32),
                        np.ascontiguousarray(cpu_values, dtype=np.float64),
                        np.ascontiguousarray(mem_values, dtype=np.float64)]
@@ -288,6 +290,60 @@ class Engine:
         self.n_nodes = len(np_) - 1
         abi.check(abi.lib().kwk_usage_config(self.h, self.n_nodes, abi.ptr(np_), abi.ptr(uk), len(cv), abi.ptr(cv),
                                              len(mv), abi.ptr(mv)), "kwk_usage_config")
+        mixed = np.zeros(0, dtype=np.uint32) if mixed is None else np.ascontiguousarray(mixed, dtype=np.uint32)
+        ckeys = np.zeros(0, dtype=np.uint32) if ckeys is None else np.ascontiguousarray(ckeys, dtype=np.uint32)
+        if len(mixed) or np.any((uk >> 28) == 0):
+            abi.check(abi.lib().kwk_usage_mixed(self.h, len(mixed) // 2, abi.ptr(mixed), len(ckeys), abi.ptr(ckeys)),
+                      "kwk_usage_mixed")
+        # containers per pod (series of a container metric)
+        nc = (uk >> 28).astype(np.int64)
+        if len(mixed):
+            nc = np.where(nc == 0, mixed[1::2].astype(np.int64)[uk & 0x0FFFFFFF] if len(mixed) else 0, nc)
+        self.usage_containers = nc
+
+    def usage_read_containers(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        """containers x {cpu, mem, cpu_cumulative, mem_cumulative} of pods [first, first+n)."""
+        n = self.n - first if n is None else n
+        cnt = C.c_uint32()
+        L = abi.lib()
+        abi.check(L.kwk_usage_read_containers(self.h, first, n, None, 0, C.byref(cnt)), "kwk_usage_read_containers")
+        out = np.zeros((cnt.value, 4), dtype=np.float64)
+        if cnt.value:
+            abi.check(L.kwk_usage_read_containers(self.h, first, n, abi.ptr(out), cnt.value, C.byref(cnt)),
+                      "kwk_usage_read_containers")
+        return out
+
+    # Metric CRD values (kwok_amd/host/metrics.py)
+    def metrics_load(self, programs):
+        """programs: [(dimension name, [(op, arg), ...])] from cel.lower()."""
+        from . import cel
+        descs = (abi.MetricDesc * max(1, len(programs)))()
+        flat = []
+        for i, (dim, prog) in enumerate(programs):
+            descs[i] = abi.MetricDesc(abi.METRIC_DIM[dim], len(flat), len(prog), 0)
+            flat += prog
+        ops = (abi.MetricOp * max(1, len(flat)))()
+        for i, (op, x) in enumerate(flat):
+            ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
+        abi.check(abi.lib().kwk_metrics_load(self.h, len(programs), descs, len(flat), ops), "kwk_metrics_load")
+
+    def metrics_inputs(self, pod_created_ns, node_created_ns, node_started, zero_time_unix_s: float):
+        self._minputs = [np.ascontiguousarray(pod_created_ns, dtype=np.int64),
+                         np.ascontiguousarray(node_created_ns, dtype=np.int64),
+                         np.ascontiguousarray(node_started, dtype=np.float64)]
+        a, b, c = self._minputs
+        abi.check(abi.lib().kwk_metrics_inputs(self.h, abi.ptr(a), abi.ptr(b), abi.ptr(c), zero_time_unix_s),
+                  "kwk_metrics_inputs")
+
+    def metrics_eval(self, now_ns: int, node_first: int, n_nodes: int) -> np.ndarray:
+        cnt = C.c_uint64()
+        L = abi.lib()
+        abi.check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, None, 0, C.byref(cnt)), "kwk_metrics_eval")
+        out = np.zeros(cnt.value, dtype=np.float64)
+        if cnt.value:
+            abi.check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, abi.ptr(out), cnt.value, C.byref(cnt)),
+                      "kwk_metrics_eval")
+        return out
 
     def usage(self, now_ns: int):
         abi.check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")

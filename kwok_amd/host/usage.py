@@ -5,25 +5,25 @@ Restates the per-container resolution of pkg/kwok/server/metrics_resource_usage.
 first ClusterResourceUsage whose ObjectSelector matches *and* has an entry for the
 container), ``findUsageInUsages`` (:252-264: the entry listing the container, else the first
 entry with no containers) and ``evaluateContainerResourceUsage`` (:136-168: a static
-``value`` via AsApproximateFloat64, or a CEL ``expression``; any error -> 0).
+``value`` via AsApproximateFloat64, or a CEL ``expression`` evaluated with the pod, its node
+and the container bound — kwok_amd/host/cel.py; any error -> 0).
 
-CEL expressions are compiled for the forms KWOK ships (kustomize/metrics/usage/
-usage-from-annotation.yaml): ``"<key>" in pod.metadata.annotations ?
-Quantity(pod.metadata.annotations["<key>"]) : Quantity("<default>")`` and
-``Quantity("<q>")``; anything else is rejected at compile time.
-
-The device gets, per pod, an interned cpu / memory value and the number of containers that
-carry it (``usage_key``); per-node sums and cumulative integrators run in ``usage_kernel``.
+Usage expressions are evaluated once per pod variant at ingest, so they must not depend on
+the clock or on other usages (``Now``, ``Rand``, ``SinceSecond``, ``Usage``, ...): such an
+expression is rejected at compile time rather than frozen.  The device gets, per pod, either
+one interned cpu / memory value and the number of containers that carry it, or — when the
+pod's containers differ — a {first, count} entry into a per-container key table
+(``kwk_usage_mixed``); per-node sums and all cumulative integrators run in ``usage_kernel``.
 """
 from __future__ import annotations
 
-import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import yaml
 
+from . import cel
 from .quantity import parse_quantity_or_none
 
 
@@ -31,11 +31,22 @@ class UsageCompileError(ValueError):
     pass
 
 
-_ANNOT_FORM = re.compile(
-    r'^"(?P<k1>[^"]*)"\s+in\s+pod\.metadata\.annotations\s*\?\s*'
-    r'Quantity\(\s*pod\.metadata\.annotations\[\s*"(?P<k2>[^"]*)"\s*\]\s*\)\s*:\s*'
-    r'Quantity\(\s*"(?P<d>[^"]*)"\s*\)$')
-_CONST_FORM = re.compile(r'^Quantity\(\s*"(?P<q>[^"]*)"\s*\)$')
+_CLOCKED = ("Now", "now", "Rand", "SinceSecond", "Usage", "CumulativeUsage", "StartedContainersTotal",
+            "startedContainersTotal")
+
+
+def _reads_clock(ast) -> bool:
+    if not isinstance(ast, tuple):
+        return False
+    if ast[0] in ("call", "method") and ast[1 if ast[0] == "call" else 2] in _CLOCKED:
+        return True
+    for x in ast[1:]:
+        if isinstance(x, tuple) and _reads_clock(x):
+            return True
+        if isinstance(x, list) and any(_reads_clock(y) if isinstance(y, tuple) and isinstance(y[0], str)
+                                       else any(_reads_clock(z) for z in y) for y in x):
+            return True
+    return False
 
 
 @dataclass
@@ -50,16 +61,13 @@ class UsageValue:
                 raise UsageCompileError(f"invalid quantity {self.value!r}")
             return ("const", q)
         if self.expression is not None:
-            e = " ".join(self.expression.split())
-            m = _ANNOT_FORM.match(e)
-            if m and m.group("k1") == m.group("k2"):
-                d = parse_quantity_or_none(m.group("d"))
-                return ("annot", m.group("k1"), 0.0 if d is None else d)  # CEL error -> 0
-            m = _CONST_FORM.match(e)
-            if m:
-                q = parse_quantity_or_none(m.group("q"))
-                return ("const", 0.0 if q is None else q)
-            raise UsageCompileError(f"unsupported usage expression: {self.expression!r}")
+            try:
+                ast = cel.compile(self.expression)
+            except cel.CELSyntaxError:
+                return ("const", 0.0)  # Compile fails -> 0 (metrics_resource_usage.go:150-155)
+            if _reads_clock(ast):
+                raise UsageCompileError(f"usage expression depends on the clock / other usages: {self.expression!r}")
+            return ("cel", self.expression)
         return ("const", 0.0)
 
 
@@ -161,8 +169,9 @@ class UsageProgram:
                 return u
         return None
 
-    def container_value(self, pod: dict, container: str, resource: str) -> float:
-        """evaluateContainerResourceUsage (:136-168)."""
+    def container_value(self, pod: dict, container: str, resource: str, node: Optional[dict] = None) -> float:
+        """evaluateContainerResourceUsage (:136-168) for the container named `container` (the
+        first with that name, as containerResourceUsage's slices.Find, :111-134)."""
         md = pod.get("metadata") or {}
         u = self._entry(md.get("name", ""), md.get("namespace", ""), container)
         if u is None or u.usage is None:
@@ -173,47 +182,50 @@ class UsageProgram:
         c = self._compiled[id(v)]
         if c[0] == "const":
             return c[1]
-        key, default = c[1], c[2]
-        ann = md.get("annotations") or {}
-        if key in ann:
-            q = parse_quantity_or_none(str(ann[key]))
-            return 0.0 if q is None else q
-        return default
+        cobj = next((x for x in (pod.get("spec") or {}).get("containers") or [] if x.get("name", "") == container), {})
+        try:
+            return cel.evaluate_float64(c[1], node=node or {}, pod=pod, container=cobj)
+        except cel.CELError:
+            return 0.0
 
-    def pod_values(self, pod: dict) -> Tuple[float, float, int]:
-        """(cpu, memory, containers): per-container value and the container count when every
-        container evaluates the same (the common case); else the exact Go-order sum with count 1."""
+    def pod_container_values(self, pod: dict, node: Optional[dict] = None) -> List[Tuple[float, float]]:
+        """(cpu, memory) of each of the pod's containers, in spec order."""
         names = [c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []]
-        out = []
-        for r in self.RESOURCES:
-            vals = [self.container_value(pod, n, r) for n in names]
-            out.append(vals)
-        if not names:
-            return 0.0, 0.0, 0
-        if all(v == out[0][0] for v in out[0]) and all(v == out[1][0] for v in out[1]) and len(names) < 16:
-            return out[0][0], out[1][0], len(names)
-        s0 = 0.0
-        for v in out[0]:
-            s0 += v
-        s1 = 0.0
-        for v in out[1]:
-            s1 += v
-        return s0, s1, 1
+        return [(self.container_value(pod, n, "cpu", node), self.container_value(pod, n, "memory", node)) for n in names]
 
 
-def usage_columns(program: UsageProgram, pods: Sequence[dict]):
-    """-> usage_key u32[n], cpu_values f64[], mem_values f64[] (interned)."""
+def usage_columns(program: UsageProgram, pods: Sequence[dict], nodes: Optional[Dict[str, dict]] = None):
+    """-> usage_key u32[n], cpu_values f64[], mem_values f64[] (interned), and the mixed tables
+    (kwk_usage_mixed): mixed u32[2 * n_mixed] = {first, count}, ckeys u32[n_containers].
+    A pod whose containers all evaluate alike (1..15 of them) is one key x its container count;
+    any other pod (containers differ, none, or more than 15) gets a mixed entry."""
     cpu_ids: Dict[float, int] = {}
     mem_ids: Dict[float, int] = {}
     keys = np.zeros(len(pods), dtype=np.uint32)
-    memo: Dict[int, int] = {}
-    for i, p in enumerate(pods):
-        c, m, n = program.pod_values(p)
+    mixed: List[int] = []
+    ckeys: List[int] = []
+    memo: Dict[tuple, int] = {}
+
+    def vid(c, m):
         ci = cpu_ids.setdefault(c, len(cpu_ids))
         mi = mem_ids.setdefault(m, len(mem_ids))
         if ci >= 1 << 14 or mi >= 1 << 14:
             raise UsageCompileError("more than 16384 distinct usage values")
-        keys[i] = ci | (mi << 14) | (n << 28)
+        return ci | (mi << 14)
+
+    for i, p in enumerate(pods):
+        node = (nodes or {}).get((p.get("spec") or {}).get("nodeName", ""))
+        vals = program.pod_container_values(p, node)
+        if 1 <= len(vals) <= 15 and all(v == vals[0] for v in vals):
+            keys[i] = vid(*vals[0]) | (len(vals) << 28)
+            continue
+        t = tuple(vals)
+        m = memo.get(t)
+        if m is None:
+            m = memo[t] = len(mixed) // 2
+            mixed += [len(ckeys), len(vals)]
+            ckeys += [vid(c, mm) for c, mm in vals]
+        keys[i] = m
     cv = np.array(sorted(cpu_ids, key=cpu_ids.get), dtype=np.float64) if cpu_ids else np.zeros(1)
     mv = np.array(sorted(mem_ids, key=mem_ids.get), dtype=np.float64) if mem_ids else np.zeros(1)
-    return keys, cv, mv
+    return keys, cv, mv, np.array(mixed, dtype=np.uint32), np.array(ckeys, dtype=np.uint32)

@@ -39,15 +39,15 @@ def test_shard_engine_aggregates_equal_whole_engine_and_oracle():
     up = UsageProgram(*load_usage_yaml(text))
     docs = [d for d in yaml.safe_load_all(text) if d]
     prog, whole, sim = build(cl.pod_stage_files, objs, harness=True)
-    keys, cv, mv = usage_columns(up, objs)
-    whole.usage_config(cl.node_ptr, keys, cv, mv)
+    keys, cv, mv, mx, ck = usage_columns(up, objs)
+    whole.usage_config(cl.node_ptr, keys, cv, mv, mx, ck)
     shards = []
     for r in range(world):
         lo, hi = node_block(n_nodes, world, r)
         plo, phi = pod_range(cl.node_ptr, lo, hi)
         _, eng, _ = build(cl.pod_stage_files, objs[plo:phi], harness=True, slot_base=plo)
-        k2, c2, m2 = usage_columns(up, objs[plo:phi])
-        eng.usage_config(local_node_ptr(cl.node_ptr, lo, hi), k2, c2, m2)
+        k2, c2, m2, x2, q2 = usage_columns(up, objs[plo:phi])
+        eng.usage_config(local_node_ptr(cl.node_ptr, lo, hi), k2, c2, m2, x2, q2)
         shards.append(eng)
     pm = phase_masks(prog, values=("Running", "Succeeded"))
     masks, names = [[0, pm["Running"], pm["Succeeded"]]], [["pods", "Running", "Succeeded"]]

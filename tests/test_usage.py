@@ -70,7 +70,7 @@ def test_gpu_node_usage_and_cumulative():
 
     cl, pods = _cluster()
     prog = _program()
-    keys, cv, mv = usage_columns(prog, pods)
+    keys, cv, mv, mx, ck = usage_columns(prog, pods)
     kp = KindProgram(load_stage_files(*cl.pod_stage_files))
     kp.explore(pods)
     ing = Ingest(kp)
@@ -79,7 +79,7 @@ def test_gpu_node_usage_and_cumulative():
     try:
         eng.load_stages()
         eng.load(hot, dels, rec, cls, ing.record_array())
-        eng.usage_config(cl.node_ptr, keys, cv, mv)
+        eng.usage_config(cl.node_ptr, keys, cv, mv, mx, ck)
         docs = _docs()
         ptr = cl.node_ptr
         t0 = 1_700_000_000 * 10**9
@@ -127,7 +127,7 @@ def test_gpu_pod_usage_and_cumulative():
 
     cl, pods = _cluster(n_nodes=12, n_pods=300, seed=5)
     prog = _program()
-    keys, cv, mv = usage_columns(prog, pods)
+    keys, cv, mv, mx, ck = usage_columns(prog, pods)
     kp = KindProgram(load_stage_files(*cl.pod_stage_files))
     kp.explore(pods)
     ing = Ingest(kp)
@@ -136,7 +136,7 @@ def test_gpu_pod_usage_and_cumulative():
     try:
         eng.load_stages()
         eng.load(*cols, ing.record_array())
-        eng.usage_config(cl.node_ptr, keys, cv, mv)
+        eng.usage_config(cl.node_ptr, keys, cv, mv, mx, ck)
         eng.usage_pods(True)
         docs = _docs()
         cum = usage_ref.Cumulative()
