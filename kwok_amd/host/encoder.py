@@ -1,0 +1,162 @@
+"""Native ingestion encoder: the stage compiler's feature table as a
+spec for libkwok_encoder.so (kwok_amd/csrc/encoder.cpp, include/kwok_encoder.h), and
+``NativeIngest``, a drop-in for ``engine.Ingest`` that encodes JSON bytes without per-object
+Python (a Go host hands the informer's bytes straight to kwk_encode).
+
+Feature and *From queries compile to step programs the encoder interprets: ``field`` (.k,
+.["k"]), ``iter`` (.[]) and ``select_eq`` (select(.a.b == literal)) joined by ``|`` — the forms
+kwok's Stage CRs use (kustomize/stage/**).  A program using any other jq construct, or
+"patch already applied" features (which need the template renderer), is rejected at
+``encoder_spec`` time with an explicit error; such a kind keeps the Python Ingest.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import re
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .compiler import _IDENTITY_META, KindProgram
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libkwok_encoder.so")
+CLASS_UNKNOWN = 0xFFFF
+
+
+class EncoderUnsupported(ValueError):
+    pass
+
+
+_SEG = re.compile(r'\.?\[\s*"((?:[^"\\]|\\.)*)"\s*\]|\.([A-Za-z_][A-Za-z0-9_]*)|\.?\[\s*\]|\.(?=\s*$)')
+_SELECT = re.compile(r'^select\s*\(\s*(?P<path>[^=]+?)\s*==\s*(?P<lit>"(?:[^"\\]|\\.)*"|true|false|null|-?\d+(?:\.\d+)?)\s*\)$')
+
+
+def _path(src: str) -> List[list]:
+    steps, i, s = [], 0, src.strip()
+    if s == ".":
+        return steps
+    while i < len(s):
+        m = _SEG.match(s, i)
+        if not m or m.end() == i:
+            raise EncoderUnsupported(f"jq construct not supported natively: {src!r}")
+        if m.group(1) is not None:
+            steps.append(["field", json.loads('"%s"' % m.group(1))])
+        elif m.group(2) is not None:
+            steps.append(["field", m.group(2)])
+        elif m.group(0).strip().endswith("]"):
+            steps.append(["iter"])
+        i = m.end()
+        while i < len(s) and s[i] == " ":
+            i += 1
+    return steps
+
+
+def query_steps(src: str) -> List[list]:
+    """jq query -> step program (field / iter / select_eq), or EncoderUnsupported."""
+    steps: List[list] = []
+    for part in (p.strip() for p in src.split("|")):
+        m = _SELECT.match(part)
+        if m:
+            sub = _path(m.group("path"))
+            if any(s[0] != "field" for s in sub):
+                raise EncoderUnsupported(f"select over a non-path: {src!r}")
+            steps.append(["select_eq", [s[1] for s in sub], json.loads(m.group("lit"))])
+        elif part.startswith("."):
+            steps += _path(part)
+        else:
+            raise EncoderUnsupported(f"jq construct not supported natively: {src!r}")
+    return steps
+
+
+def encoder_spec(program: KindProgram) -> str:
+    if program.applied_bits:
+        raise EncoderUnsupported("'patch already applied' features need the host renderer")
+    feats = [{"steps": query_steps(f.src), "present_bit": f.present_bit, "literals": dict(f.lit_bits)}
+             for f in program.features.values()]
+    slots = [{"type": typ, "steps": query_steps(src)} for typ, src in program.slots]
+    return json.dumps({"features": feats, "finalizers": dict(program.fin_bits),
+                       "finalizer_other_bit": program.fin_other_bit, "slots": slots,
+                       "classes": dict(program.class_ids), "identity_meta": list(_IDENTITY_META)})
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise abi.EngineError(f"native encoder library missing: {LIB_PATH} (run python -m kwok_amd.build)")
+        L = C.CDLL(LIB_PATH)
+        L.kwk_encoder_last_error.restype = C.c_char_p
+        L.kwk_encoder_create.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+        L.kwk_encoder_destroy.argtypes = [C.c_void_p]
+        L.kwk_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
+        L.kwk_encoder_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        for n in ("kwk_encoder_create", "kwk_encoder_destroy", "kwk_encode", "kwk_encoder_records"):
+            getattr(L, n).restype = C.c_int32
+        _lib = L
+    return _lib
+
+
+def _check(st, what):
+    if st != 0:
+        raise abi.EngineError(f"{what} failed ({st}): {lib().kwk_encoder_last_error().decode(errors='replace')}")
+
+
+def pack_json(objs: Sequence) -> tuple:
+    """Objects (dicts or JSON bytes) -> (contiguous buffer, n + 1 offsets)."""
+    parts = [o if isinstance(o, (bytes, bytearray)) else json.dumps(o, separators=(",", ":")).encode() for o in objs]
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    np.cumsum([len(p) for p in parts], out=offs[1:])
+    return b"".join(parts), offs
+
+
+class NativeIngest:
+    """engine.Ingest through libkwok_encoder: columns() of JSON objects / bytes."""
+
+    def __init__(self, program: KindProgram, n_threads: int = 1):
+        self.p = program
+        self.n_threads = n_threads
+        self.h = C.c_void_p()
+        _check(lib().kwk_encoder_create(encoder_spec(program).encode(), C.byref(self.h)), "kwk_encoder_create")
+
+    def close(self):
+        if self.h:
+            lib().kwk_encoder_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode_buffer(self, buf: bytes, offsets: np.ndarray):
+        n = len(offsets) - 1
+        hot = np.zeros(n, dtype=abi.HOT_DTYPE)
+        dels = np.zeros(n, dtype=np.int64)
+        rec = np.zeros(n, dtype=np.uint32)
+        cls = np.zeros(n, dtype=np.uint16)
+        unknown = C.c_uint32()
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _check(lib().kwk_encode(self.h, n, buf, abi.ptr(offsets), self.n_threads, abi.ptr(hot), abi.ptr(dels),
+                                abi.ptr(rec), abi.ptr(cls), C.byref(unknown)), "kwk_encode")
+        self.unknown_classes = unknown.value
+        return hot, dels, rec, cls
+
+    def columns(self, objs: Sequence):
+        return self.encode_buffer(*pack_json(objs))
+
+    def record_array(self) -> np.ndarray:
+        ns = max(1, len(self.p.slots))
+        n = C.c_uint32()
+        _check(lib().kwk_encoder_records(self.h, None, 0, C.byref(n)), "kwk_encoder_records")
+        a = np.zeros((max(1, n.value), ns), dtype=abi.VALUE_DTYPE)
+        if n.value and self.p.slots:
+            _check(lib().kwk_encoder_records(self.h, abi.ptr(a), n.value, C.byref(n)), "kwk_encoder_records")
+        return a

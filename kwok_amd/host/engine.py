@@ -297,8 +297,9 @@ class Engine:
                       "kwk_usage_mixed")
         # containers per pod (series of a container metric)
         nc = (uk >> 28).astype(np.int64)
-        if len(mixed):
-            nc = np.where(nc == 0, mixed[1::2].astype(np.int64)[uk & 0x0FFFFFFF] if len(mixed) else 0, nc)
+        mx = nc == 0
+        if np.any(mx):
+            nc[mx] = mixed[1::2].astype(np.int64)[(uk[mx] & 0x0FFFFFFF).astype(np.int64)]
         self.usage_containers = nc
 
     def usage_read_containers(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
