@@ -289,6 +289,36 @@ def cpu_baseline(sample_s: float, seed: int):
                       f"{_cpu_model()} ({os.cpu_count()} logical CPUs visible)"}
 
 
+def cpu_baseline_soa(sample_s: float, seed: int, n_pods: int = 20_000_000):
+    """All-cores SoA mode: the compiled pod-fast program stepped over
+    integer columns by every host thread this job may use (oracle/refcpu rc_soa_steps), on a
+    C5-shaped sample with the bench's churn; transitions per second."""
+    from kwok_amd import workload as W
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Ingest
+    from kwok_amd.host.stages import load_stage_files
+    from oracle import refcpu
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+    prog = KindProgram(load_stage_files(*W.stage_paths(W.POD_FAST)), HarnessSpec())
+    prog.explore(pvars)
+    hot, _, _, cls = Ingest(prog).variant_columns(pvars, shard_pod_variants(0, n_pods, seed, 0.1))
+    pred = np.ascontiguousarray(hot["pred"])
+    sched = np.ascontiguousarray((hot["sched"] & ~np.uint32(0xFFFF0000)) | (cls.astype(np.uint32) << np.uint32(16)))
+    due = np.zeros(n_pods, dtype=np.int64)
+    table, deltas, harness = prog.table(), prog.delta_array(), prog.harness_struct()
+    refcpu.soa_steps(table, deltas, harness, pred, sched, due, NOW0, 10**9, 3, seed, cores)  # warm-up: first matches
+    steps, fired, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < sample_s:
+        fired += refcpu.soa_steps(table, deltas, harness, pred, sched, due, NOW0 + (3 + steps) * 10**9, 10**9, 4, seed,
+                                  cores)
+        steps += 4
+    dt = time.perf_counter() - t0
+    return {"value": round(fired / dt, 1), "unit": "stage transitions/sec", "cores": cores, "kind": "port",
+            "sample": f"{n_pods:,} C5-shaped pods x {steps} steps ({dt:.1f} s): the compiled pod-fast program over SoA "
+                      f"columns (harness churn, match, pick, delay, fire, delta), {cores} threads; CPU {_cpu_model()}"}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -472,8 +502,10 @@ def main():
             roof["traffic_GBps"] = round(tr / pod_kernel_s / 1e9, 1)
         cpu = None
         log(f"timed {args.steps} steps in {max_s:.3f} s")
+        cpu_soa = None
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             cpu = cpu_baseline(args.cpu_sample_s, args.seed)
+            cpu_soa = cpu_baseline_soa(args.cpu_sample_s / 2, args.seed)
         total_nodes = args.nodes * world if weak else args.nodes
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
@@ -490,6 +522,7 @@ def main():
                        "nodes_per_gpu": nhi - nlo, "parallelism": f"node-shard{world}", "sim_dt_ms": args.dt_ms},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "cpu_baseline_soa": cpu_soa,
             "pcie_inclusive": pcie,
             "hbm_working_set": hbm,
             "aggregates": agg.as_dict() if agg is not None else None,

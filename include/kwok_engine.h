@@ -292,7 +292,8 @@ kwk_status kwk_usage_read_pods(kwk_engine* eng, uint32_t first, uint32_t n, doub
 /* Pods whose containers evaluate to different usages (metrics_resource_usage.go:136-168 per
  * container): usage_key = m with a 0 container count (bits 28..31), m indexing
  * mixed[2m] = first, mixed[2m+1] = count into ckeys (per container: cpu id | memory id << 14,
- * in spec.containers order).  Call after kwk_usage_config. */
+ * in spec.containers order).  Pods may share a mixed entry (their containers evaluate alike);
+ * the cumulative integrators are still per pod and container.  Call after kwk_usage_config. */
 kwk_status kwk_usage_mixed(kwk_engine* eng, uint32_t n_mixed, const uint32_t* mixed, uint32_t n_ckeys,
                            const uint32_t* ckeys);
 /* per-container outputs of kwk_usage (containerResourceUsage / containerResourceCumulativeUsage,

@@ -1271,6 +1271,7 @@ struct UsageArgs {
   int64_t* __restrict__ pod_last;
   const uint2* __restrict__ mixed;  // pods whose containers differ: {first, count} into ckeys
   const uint32_t* __restrict__ ckeys;
+  const uint32_t* __restrict__ mbase;  // per pod: its containers' first integrator in ccum (mixed pods)
   double* __restrict__ ccum;        // per container of a mixed pod: {cpu, mem} integrators
 };
 
@@ -1346,13 +1347,14 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
               }
               for (uint32_t j = 0; j < nc; ++j) { cc += unit.x; cm += unit.y; }
             } else {
+              const uint32_t mb = a.mbase[p];
               for (uint32_t j = 0; j < fc.y; ++j) {
                 const uint32_t ck = a.ckeys[fc.x + j];
-                double2 cu = reinterpret_cast<double2*>(a.ccum)[fc.x + j];
+                double2 cu = reinterpret_cast<double2*>(a.ccum)[mb + j];
                 if (lt != INT64_MIN) {
                   cu.x += dt * a.cpu_v[ck & 0x3FFFu];
                   cu.y += dt * a.mem_v[(ck >> 14) & 0x3FFFu];
-                  reinterpret_cast<double2*>(a.ccum)[fc.x + j] = cu;
+                  reinterpret_cast<double2*>(a.ccum)[mb + j] = cu;
                 }
                 cc += cu.x;
                 cm += cu.y;
@@ -1449,6 +1451,7 @@ struct MetricArgs {
   const uint32_t* __restrict__ ukey;
   const uint2* __restrict__ mixed;
   const uint32_t* __restrict__ ckeys;
+  const uint32_t* __restrict__ mbase;
   const double* __restrict__ cpu_v;
   const double* __restrict__ mem_v;
   const double* __restrict__ pod_out;
@@ -1519,7 +1522,7 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
           } else {
             const uint2 fc = a.mixed[k & kUKeyMixedIndex];
             const uint32_t ck = a.ckeys[fc.x + j];
-            v = cum ? a.ccum[2 * (uint64_t)(fc.x + j) + r] : (r ? a.mem_v[(ck >> 14) & 0x3FFFu] : a.cpu_v[ck & 0x3FFFu]);
+            v = cum ? a.ccum[2 * (uint64_t)(a.mbase[pod] + j) + r] : (r ? a.mem_v[(ck >> 14) & 0x3FFFu] : a.cpu_v[ck & 0x3FFFu]);
           }
         } else if (in >= KWK_MIN_POD_CPU && in <= KWK_MIN_POD_CUM_MEM) {
           v = a.pod_out[4 * (uint64_t)pod + (in - KWK_MIN_POD_CPU)];
@@ -1866,6 +1869,8 @@ struct kwk_engine {
   uint2* d_mixed = nullptr;       // {first, count} per mixed pod
   uint32_t* d_ckeys = nullptr;
   double* d_ccum = nullptr;       // per container of a mixed pod: {cpu, mem} integrators
+  uint32_t* d_mbase = nullptr;    // per pod: first integrator of its containers in d_ccum (mixed pods)
+  std::vector<uint32_t> h_mbase;
   uint32_t* d_cptr = nullptr;     // per pod: first container (metric scrapes)
   // Metric CRD programs
   kwk_metric_op* d_mops = nullptr;
@@ -2058,7 +2063,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
-                  e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
+                  e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
                   e->d_lease_nops, e->d_lease_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
@@ -2626,12 +2631,14 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   e->h_mixed.clear();
   e->h_ckeys.clear();
   e->h_cptr.clear();
-  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr})
+  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr, (void*)e->d_mbase})
     if (q) HIP_TRY(hipFree(q));
   e->d_mixed = nullptr;
   e->d_ckeys = nullptr;
   e->d_ccum = nullptr;
   e->d_cptr = nullptr;
+  e->d_mbase = nullptr;
+  e->h_mbase.clear();
   if (e->d_pod_cum) HIP_TRY(hipMemset(e->d_pod_cum, 0, 16 * (size_t)e->capacity));
   return KWK_OK;
 }
@@ -2650,16 +2657,28 @@ kwk_status kwk_usage_mixed(kwk_engine* e, uint32_t n_mixed, const uint32_t* mixe
       return fail(KWK_EINVAL, "usage_key mixed index out of range");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr})
+  for (void* q : {(void*)e->d_mixed, (void*)e->d_ckeys, (void*)e->d_ccum, (void*)e->d_cptr, (void*)e->d_mbase})
     if (q) HIP_TRY(hipFree(q));
   e->d_cptr = nullptr;
   e->h_cptr.clear();
+  // integrators are per pod and container (mixed entries may be shared by pods whose containers
+  // evaluate alike): each mixed pod's containers get their own range of ccum
+  e->h_mbase.assign(e->n_usage_pods, 0u);
+  uint64_t nint = 0;
+  for (uint32_t p = 0; p < e->n_usage_pods; ++p)
+    if ((e->h_ukey[p] >> 28) == 0) {
+      e->h_mbase[p] = (uint32_t)nint;
+      nint += mixed[2 * (size_t)(e->h_ukey[p] & kUKeyMixedIndex) + 1];
+      if (nint > 0xFFFFFFFFull) return fail(KWK_ECAP, "more than 2^32 containers of mixed pods");
+    }
   HIP_TRY(hipMalloc(&e->d_mixed, 8 * ((size_t)n_mixed + 1)));
   HIP_TRY(hipMalloc(&e->d_ckeys, 4 * ((size_t)n_ckeys + 1)));
-  HIP_TRY(hipMalloc(&e->d_ccum, 16 * ((size_t)n_ckeys + 1)));
+  HIP_TRY(hipMalloc(&e->d_ccum, 16 * ((size_t)nint + 1)));
+  HIP_TRY(hipMalloc(&e->d_mbase, 4 * ((size_t)e->n_usage_pods + 1)));
   if (n_mixed) HIP_TRY(hipMemcpy(e->d_mixed, mixed, 8 * (size_t)n_mixed, hipMemcpyHostToDevice));
   if (n_ckeys) HIP_TRY(hipMemcpy(e->d_ckeys, ckeys, 4 * (size_t)n_ckeys, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(e->d_ccum, 0, 16 * ((size_t)n_ckeys + 1)));
+  if (e->n_usage_pods) HIP_TRY(hipMemcpy(e->d_mbase, e->h_mbase.data(), 4 * (size_t)e->n_usage_pods, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e->d_ccum, 0, 16 * ((size_t)nint + 1)));
   e->h_mixed.assign(mixed, mixed + 2 * (size_t)n_mixed);
   e->h_ckeys.assign(ckeys, ckeys + n_ckeys);
   return KWK_OK;
@@ -2697,7 +2716,7 @@ kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, 
     total += pod_containers(e, p);
     const uint32_t k = e->h_ukey[p];
     if (!(k >> 28)) {
-      const uint32_t f = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex)], c = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
+      const uint32_t f = e->h_mbase[p], c = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
       if (c) { cmin = f < cmin ? f : cmin; cmax = f + c > cmax ? f + c : cmax; }
     }
   }
@@ -2729,12 +2748,13 @@ kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, 
       }
     } else {
       const uint32_t f = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex)], c = e->h_mixed[2 * (size_t)(k & kUKeyMixedIndex) + 1];
+      const uint32_t mb = e->h_mbase[p];
       for (uint32_t j = 0; j < c; ++j, o += 4) {
         const uint32_t ck = e->h_ckeys[f + j];
         out[o] = alive ? e->h_cpu[ck & 0x3FFFu] : 0.0;
         out[o + 1] = alive ? e->h_mem[(ck >> 14) & 0x3FFFu] : 0.0;
-        out[o + 2] = alive ? cc[2 * (size_t)(f + j - cmin)] : 0.0;
-        out[o + 3] = alive ? cc[2 * (size_t)(f + j - cmin) + 1] : 0.0;
+        out[o + 2] = alive ? cc[2 * (size_t)(mb + j - cmin)] : 0.0;
+        out[o + 3] = alive ? cc[2 * (size_t)(mb + j - cmin) + 1] : 0.0;
       }
     }
   }
@@ -2847,6 +2867,7 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
     a.ukey = e->d_ukey;
     a.mixed = e->d_mixed;
     a.ckeys = e->d_ckeys;
+    a.mbase = e->d_mbase;
     a.cpu_v = e->d_cpu;
     a.mem_v = e->d_mem;
     a.pod_out = e->d_pod_out;
@@ -2877,7 +2898,7 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
   UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->n_nodes, e->n_usage_pods, e->d_node_out,
                e->d_node_cum, e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
-               e->d_mixed, e->d_ckeys, e->d_ccum};
+               e->d_mixed, e->d_ckeys, e->d_mbase, e->d_ccum};
   hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, ua);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);

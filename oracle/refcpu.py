@@ -205,3 +205,17 @@ class Lifecycle:
                                  seed, step, slot_base, st.ctypes.data_as(C.POINTER(C.c_int32)),
                                  de.ctypes.data_as(C.POINTER(C.c_int64)), nthreads)
         return st, de, n
+
+
+def soa_steps(table, deltas, harness, pred, sched, due, now0_ns: int, dt_ns: int, steps: int, seed: int,
+              nthreads: int) -> int:
+    """TIMING BASELINE ONLY: the compiled stage program stepped over SoA columns on nthreads
+    host threads (rc_soa_steps); the columns are updated in place.  -> transitions fired."""
+    import numpy as np
+    L = lib()
+    L.rc_soa_steps.restype = C.c_int64
+    L.rc_soa_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                               C.c_int64, C.c_int64, C.c_int, C.c_uint64, C.c_int]
+    d = np.ascontiguousarray(deltas, dtype=np.uint32)
+    return L.rc_soa_steps(C.addressof(table), d.ctypes.data, C.addressof(harness), pred.ctypes.data, sched.ctypes.data,
+                          due.ctypes.data, len(pred), now0_ns, dt_ns, steps, seed, nthreads)

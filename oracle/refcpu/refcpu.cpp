@@ -808,3 +808,119 @@ static int quantity_f64(const std::string& s, double& out) {
 }  // namespace refcpu
 
 extern "C" int rc_quantity(const char* s, double* out) { return refcpu::quantity_f64(s, *out); }
+
+// ---------------------------------------------------------------- SoA step (CPU baseline)
+// TIMING BASELINE ONLY (bench.py cpu_baseline leg, SURVEY.md §8(d)(2) "SoA scalar mode on all
+// host cores"): the compiled stage program (include/kwok_engine.h layouts, filled by the host
+// stage compiler) stepped over integer columns by N threads, the per-object order of the step
+// model (harness -> match -> pick -> delay -> fire -> delta) with the Philox hook.  Supports
+// programs without value records (every shipped pod-fast / node program); parity is not claimed
+// for it — the GPU is checked against the JSON-level oracle above.
+#include "../../include/kwok_engine.h"
+
+namespace {
+inline bool soa_matches(const kwk_stage_desc& s, uint32_t pred) {
+  bool ok = ((pred ^ s.eq_val) & s.eq_mask) == 0;
+  for (uint32_t k = 0; k < s.n_any; ++k) ok &= ((pred & s.any_mask[k]) != 0) == (((s.any_want >> k) & 1u) != 0);
+  return ok;
+}
+}  // namespace
+
+extern "C" int64_t rc_soa_steps(const kwk_stage_table* T, const kwk_delta* deltas, const kwk_harness* H, uint32_t* pred,
+                                uint32_t* sched, int64_t* due, uint64_t n, int64_t now0, int64_t dt, int steps,
+                                uint64_t seed, int nthreads) {
+  std::atomic<int64_t> fired{0};
+  const uint32_t ns = T->n_stages, fin = T->fin_group_mask;
+  auto body = [&](uint64_t lo, uint64_t hi) {
+    int64_t f = 0;
+    for (int k = 0; k < steps; ++k) {
+      const int64_t now = now0 + k * dt;
+      Rng rng{seed, 0, (uint64_t)k};
+      for (uint64_t i = lo; i < hi; ++i) {
+        uint32_t p = pred[i], s = sched[i];
+        if (!(s & KWK_F_MANAGED)) continue;
+        if (H->enable) {
+          if (!(s & KWK_F_ALIVE)) {
+            p &= H->keep_mask;
+            s = (s & (KWK_F_MANAGED | KWK_F_HASREC | KWK_CLASS_MASK)) | KWK_F_ALIVE | KWK_F_DIRTY | KWK_STAGE_NONE;
+          } else if ((p & H->terminal_mask) && !(p & H->deletion_bit)) {
+            p |= H->deletion_bit;
+            s |= KWK_F_DIRTY;
+          }
+        }
+        if (s & KWK_F_ALIVE) {
+          if (s & KWK_F_DIRTY) {
+            s &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
+            uint32_t m = 0;
+            for (uint32_t j = 0; j < ns; ++j) m |= (soa_matches(T->stages[j], p) ? 1u : 0u) << j;
+            if (m) {
+              rng.slot = i;
+              int pick = __builtin_ctz(m);
+              const int cnt = __builtin_popcount(m);
+              if (cnt > 1) {
+                int64_t total = 0;
+                for (uint32_t mm = m; mm; mm &= mm - 1) total += T->stages[__builtin_ctz(mm)].weight_default;
+                if (total <= 0) {
+                  int64_t want = rng.below(SITE_PICK, cnt);
+                  uint32_t mm = m;
+                  while (want-- > 0) mm &= mm - 1;
+                  pick = __builtin_ctz(mm);
+                } else {
+                  int64_t off = rng.below(SITE_PICK, total);
+                  for (uint32_t mm = m; mm; mm &= mm - 1) {
+                    const int j = __builtin_ctz(mm);
+                    const int64_t w = T->stages[j].weight_default;
+                    if (w <= 0) continue;
+                    off -= w;
+                    if (off < 0) { pick = j; break; }
+                  }
+                }
+              }
+              const kwk_stage_desc& S = T->stages[pick];
+              int64_t delay = S.has_delay ? S.delay_default : 0;
+              if (S.has_delay && S.has_jitter && S.jitter_default_ok) {
+                if (S.jitter_default < delay) delay = S.jitter_default;
+                else if (S.jitter_default > delay) delay += rng.below(SITE_JITTER, S.jitter_default - delay);
+              }
+              s = (s & ~0xFFu) | (uint32_t)pick;
+              due[i] = now + delay;
+            }
+          }
+          const uint32_t st = s & 0xFFu;
+          if (st < ns && due[i] <= now) {
+            const kwk_stage_desc& S = T->stages[st];
+            bool rematch = (S.flags & KWK_NEXT_PATCHES) && (!(S.flags & KWK_NEXT_PATCH_STATIC) || !(p & S.applied_mask));
+            if (S.flags & KWK_NEXT_FIN) {
+              const uint32_t F = p & fin;
+              const uint32_t F2 = ((S.flags & KWK_NEXT_FIN_EMPTY) || ((S.flags & KWK_NEXT_FIN_REMOVE) && (F & ~S.fin_remove) == 0))
+                                      ? S.fin_add : ((F & ~S.fin_remove) | (S.fin_add & ~F));
+              rematch |= F2 != F;
+              p = (p & ~fin) | F2;
+            }
+            if (S.flags & KWK_NEXT_DELETE) {
+              s &= ~KWK_F_ALIVE;
+              rematch = false;
+            } else if (S.flags & KWK_NEXT_PATCHES) {
+              const kwk_delta d = deltas[(s >> KWK_CLASS_SHIFT) * ns + st];
+              p = (((p & d.and_mask) | d.or_mask) & ~fin) | (p & fin);
+            }
+            if (rematch) s |= KWK_F_DIRTY;
+            s |= KWK_STAGE_NONE;
+            ++f;
+          }
+        }
+        pred[i] = p;
+        sched[i] = s;
+      }
+    }
+    fired += f;
+  };
+  const int T_ = nthreads > 0 ? nthreads : 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < T_; ++t) {
+    const uint64_t lo = n * (uint64_t)t / (uint64_t)T_, hi = n * (uint64_t)(t + 1) / (uint64_t)T_;
+    th.emplace_back(body, lo, hi);
+  }
+  for (auto& t : th) t.join();
+  return fired.load();
+}
