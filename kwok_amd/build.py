@@ -13,9 +13,13 @@ ROOT = os.path.dirname(PKG)
 SRC = [os.path.join(PKG, "csrc", "engine.hip")]
 HDR = [os.path.join(ROOT, "include", "kwok_engine.h")]
 OUT = os.path.join(PKG, "lib", "libkwok_engine.so")
+DOM_HDR = os.path.join(PKG, "csrc", "json_dom.hpp")
 ENC_SRC = [os.path.join(PKG, "csrc", "encoder.cpp")]
-ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "include", "kwok_engine.h")]
+ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
 ENC_OUT = os.path.join(PKG, "lib", "libkwok_encoder.so")
+PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
+PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
+PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
 ARCH = "gfx950"  # MI355X only
 
 
@@ -26,22 +30,34 @@ def _stale(out, srcs) -> bool:
     return any(os.path.getmtime(p) > t for p in srcs)
 
 
-def build_encoder(force: bool = False, verbose: bool = False) -> str:
-    """The native ingestion encoder: host C++ (no device code)."""
-    if not force and not _stale(ENC_OUT, ENC_SRC + ENC_HDR):
-        return ENC_OUT
-    os.makedirs(os.path.dirname(ENC_OUT), exist_ok=True)
+def _host_lib(out, srcs, hdrs, force, verbose) -> str:
+    """A host-only C++ library (no device code)."""
+    if not force and not _stale(out, srcs + hdrs):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", os.path.join(ROOT, "include"),
-           "-o", ENC_OUT + ".tmp"] + ENC_SRC
+           "-o", out + ".tmp"] + srcs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(ENC_OUT + ".tmp", ENC_OUT)
-    return ENC_OUT
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_encoder(force: bool = False, verbose: bool = False) -> str:
+    """The native ingestion encoder."""
+    return _host_lib(ENC_OUT, ENC_SRC, ENC_HDR, force, verbose)
+
+
+def build_patch(force: bool = False, verbose: bool = False) -> str:
+    """The native patch renderer (precompiled merge-patch byte templates)."""
+    return _host_lib(PATCH_OUT, PATCH_SRC, PATCH_HDR, force, verbose)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     build_encoder(force, verbose)
+    if os.path.exists(PATCH_SRC[0]):
+        build_patch(force, verbose)
     if not force and not _stale(OUT, SRC + HDR):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)

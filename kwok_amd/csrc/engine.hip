@@ -447,9 +447,9 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
 }
 
 // wave-ballot compaction of the fired set into the wave's private segment + per-stage counts
-// kPacked (2-byte sweep): 4-byte records {slot within the wave region: 11 bits, stage: 5,
-// flags: 3}, expanded to kwk_fired_rec by compact_kernel (slot = segment * segment size
-// + index)
+// kPacked: 4-byte records {slot within the sweep region: 13 bits, stage: 5, flags: 3},
+// expanded to kwk_fired_rec by compact_kernel (slot = region * region size + index; a region
+// is a wave's words in sweep16_kernel, a tile's in sweepw_kernel)
 template <bool kPacked = false>
 __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t lane, kwk_fired_rec* __restrict__ seg,
                                            uint32_t& seg_n, unsigned int* s_stat, uint32_t& n_bytes) {
@@ -458,7 +458,7 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   if (f.fire) {
     const uint32_t pos = seg_n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
     if constexpr (kPacked) {
-      reinterpret_cast<uint32_t*>(seg)[pos] = (uint32_t)i | f.stage << 11 | f.flags << 16;
+      reinterpret_cast<uint32_t*>(seg)[pos] = (uint32_t)i | f.stage << 13 | f.flags << 18;
       n_bytes += 4;
     } else {
       seg[pos] = kwk_fired_rec{(uint32_t)i, (uint16_t)f.stage, (uint16_t)f.flags};
@@ -859,19 +859,21 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   typedef typename WordOf<kWB>::T W;
   constexpr int kC = 16 / (int)kWB;        // words per chunk
   constexpr int K = kC * kQW;              // words per lane
-  constexpr uint32_t kWave = 64u * K;      // words per wave region (<= 1024: 10-bit work entries)
-  constexpr uint32_t kTile = kBlock * K;
-  static_assert(kWave <= 2048, "fired records carry an 11-bit slot within the wave region");
+  constexpr uint32_t kWave = 64u * K;      // words per wave region
+  constexpr uint32_t kTile = kBlock * K;   // words per tile (one block)
+  static_assert(kTile <= 8192, "fired records carry a 13-bit slot within the tile");
   __shared__ unsigned int s_stat[kStatWords];
   __shared__ kwk_delta s_delta[kLdsDeltasW];
-  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint16_t s_work[kTile];
   __shared__ uint4 s_tile[kWavesPerBlock][64 * kQW];
   __shared__ uint32_t s_lut[kLutMax];
+  __shared__ uint32_t s_cnt[kWavesPerBlock][2];
   __shared__ kwk_stage_table s_tab;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t tile = blockIdx.x;        // one block per tile
-  const uint32_t wbase = tile * kTile + wave * kWave;
+  const uint32_t tbase = tile * kTile;
+  const uint32_t wbase = tbase + wave * kWave;
   // the tile's stream is issued before the LDS set-up so its latency overlaps it
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * kWB) + 15u) & ~15u);
   uint4 cur[kQW];
@@ -898,14 +900,12 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
     for (uint32_t j = threadIdx.x; j < n_deltas; j += kBlock) s_delta[j] = a.deltas[j];
     deltas = s_delta;
   }
-  __syncthreads();
 
   const StateFmt fmt = a.fmt;
   const RawTest R = a.raw;
   uint32_t n_matched = 0, n_bytes = 0, n_line = 0;  // per lane
-  uint16_t* __restrict__ wl = s_work[wave];
   uint4* __restrict__ tq = s_tile[wave];
-  W* __restrict__ tw = reinterpret_cast<W*>(tq);
+  W* __restrict__ tw = reinterpret_cast<W*>(&s_tile[0][0]);  // the whole tile: slot t = wave * kWave + offset
   const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
   const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
   uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * (kWave + 32u);
@@ -913,7 +913,7 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   uint32_t seg_n = 0;  // wave-uniform
 
   // ---- phase 1: bit k = q * kC + j of a lane's masks <-> word q * 64 * kC + lane * kC + j
-  uint32_t need = 0, pend = 0, in_range = 0;
+  uint32_t need = 0, heavy = 0, pend = 0, in_range = 0;
 #pragma unroll
   for (int q = 0; q < kQW; ++q) {
 #pragma unroll
@@ -927,11 +927,12 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
       uint32_t nb = (fw & R.dirty) ? 1u : 0u;
       if (kHarness) nb |= ((~fw & R.alive) ? 1u : 0u) | (((pw & R.term) != 0 && (pw & R.del) == 0) ? 1u : 0u);
       const int k = q * kC + j;
-      need |= (mg & nb) << k;
+      heavy |= (mg & nb) << k;
       pend |= (mg & pe) << k;
       in_range |= in << k;
     }
   }
+  need = heavy;
   uint32_t ready = 0;
   if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
     const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
@@ -945,37 +946,59 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
     need |= ready;
   }
   n_bytes += kWB * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
-  // work list in slot order: exclusive prefix of the per-lane counts (counts <= 16)
-  uint32_t n_work = 0, pos = 0;  // n_work wave-uniform
+  // One work list per tile, sorted by kind: the fire-only items (a due stage, nothing to
+  // match) of all four waves first, then the items that match (dirty / harness).  The waves
+  // then take 64 consecutive items at a time: passes are full, and a pass runs the matcher
+  // (weighted pick, jitter draws, getters) only if one of its items needs it.
+  const uint32_t light = need & ~heavy;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t pos_l = 0, pos_h = 0, n_l = 0, n_h = 0;  // n_* wave-uniform
   {
-    const uint32_t cnt = (uint32_t)__popc(need);
-    const unsigned long long lt = (1ull << lane) - 1ull;
+    const uint32_t cl = (uint32_t)__popc(light), ch = (uint32_t)__popc(heavy);
 #pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const unsigned long long bal = __ballot((cnt >> b) & 1u);
-      pos += (uint32_t)__popcll(bal & lt) << b;
-      n_work += (uint32_t)__popcll(bal) << b;
-    }
-    for (uint32_t m = need; m; m &= m - 1u) {
-      const uint32_t k = (uint32_t)__ffs(m) - 1u;
-      const uint32_t off = (k / kC) * 64u * kC + lane * kC + (k % kC);
-      wl[pos++] = (uint16_t)(off | (((ready >> k) & 1u) << 15));
+    for (int b = 0; b < 5; ++b) {  // counts <= 16 (4-byte) / 8 (8-byte)
+      const unsigned long long bl = __ballot((cl >> b) & 1u), bh = __ballot((ch >> b) & 1u);
+      pos_l += (uint32_t)__popcll(bl & lt) << b;
+      n_l += (uint32_t)__popcll(bl) << b;
+      pos_h += (uint32_t)__popcll(bh & lt) << b;
+      n_h += (uint32_t)__popcll(bh) << b;
     }
   }
+  if (lane == 0) {
+    s_cnt[wave][0] = n_l;
+    s_cnt[wave][1] = n_h;
+  }
+#pragma unroll
+  for (int q = 0; q < kQW; ++q) tq[q * 64 + lane] = cur[q];
+  __syncthreads();
+  uint32_t tot_l = 0, n_work = 0;  // block-uniform
+#pragma unroll
+  for (uint32_t w = 0; w < kWavesPerBlock; ++w) {
+    const uint32_t xl = s_cnt[w][0], xh = s_cnt[w][1];
+    if (w < wave) { pos_l += xl; pos_h += xh; }
+    tot_l += xl;
+    n_work += xl + xh;
+  }
+  pos_h += tot_l;
+  for (uint32_t m = need; m; m &= m - 1u) {
+    const uint32_t k = (uint32_t)__ffs(m) - 1u;
+    const uint32_t off = wave * kWave + (k / kC) * 64u * kC + lane * kC + (k % kC);
+    const uint16_t ent = (uint16_t)(off | (((ready >> k) & 1u) << 15));
+    if ((heavy >> k) & 1u) s_work[pos_h++] = ent;
+    else s_work[pos_l++] = ent;
+  }
+  __syncthreads();
 
   if (n_work) {
-    // ---- phase 2
-#pragma unroll
-    for (int q = 0; q < kQW; ++q) tq[q * 64 + lane] = cur[q];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t c = 0; c < n_work; c += 64u) {
+    // ---- phase 2: the tile's list, 64 items per wave pass
+    for (uint32_t c = wave * 64u; c < n_work; c += kBlock) {
       const uint32_t jw = c + lane;
       Fire f{false, 0, 0, 0};
       uint32_t off = 0;
       if (jw < n_work) {
-        const uint32_t we = wl[jw];
+        const uint32_t we = s_work[jw];
         off = we & 0x7FFFu;
-        const uint64_t i = wbase + off;
+        const uint64_t i = tbase + off;
         const uint2 s = sw_decode(tw[off], fmt);
         // the queued stage's due time matters only as "due <= now" (a new match overwrites
         // it), which phase 1 already decided
@@ -992,8 +1015,8 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
       n_bytes += f.bytes;
       emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // ---- phase 3: whole 128-byte lines wherever a word changed
+    __syncthreads();
+    // ---- phase 3: whole 128-byte lines of the wave's region wherever a word changed
     uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
 #pragma unroll
     for (int q = 0; q < kQW; ++q) {
@@ -1036,76 +1059,64 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
 }
 
 // ------------------------------------------------------------------ fired hand-back
-// One pass over the sweep's per-(tile, wave) segments: a single-pass scan with decoupled
-// look-back over the per-segment counts (which the sweep writes into `counts`), then each wave
-// expands its segment's 4-byte records {slot within the wave region: 11, stage: 5, flags: 3}
-// into kwk_fired_rec at its offset of one dense list, in slot order.  A block's place in the
-// scan is a ticket drawn on arrival (so every predecessor it waits on is already running);
-// status words are 8-byte agent-scope atomics {epoch: 30, flag: 2 | value: 32}, the epoch
-// distinguishes this launch's entries from earlier ones (no reset between launches).
+// Two launches over the sweep's per-(tile, wave) segments: one workgroup scans the segment
+// counts (which the sweep writes into `counts`) into exclusive offsets — a few hundred KB,
+// read once per step — then one wave per segment expands its 4-byte records {slot within the
+// wave region: 11, stage: 5, flags: 3} into kwk_fired_rec at its offset of one dense list.
+// (A single-pass decoupled look-back was measured slower here: with ~12k tiny blocks the
+// look-back chains, not the bytes, set the time — 165 us vs the ~30 us the bytes need.)
+constexpr uint32_t kScanThreads = 1024;
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;  // one wave per segment
+
+// offsets[0] = total, offsets[1 + i] = records before segment i
+__global__ __launch_bounds__(kScanThreads) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
+                                                                uint32_t* __restrict__ offsets) {
+  __shared__ uint32_t s_wave[kScanThreads / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
+  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
+  uint32_t sum = 0;
+#pragma unroll 8
+  for (uint32_t i = lo; i < hi; ++i) sum += counts[i];
+  uint32_t incl = sum;  // inclusive scan over the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += s_wave[w];
+  uint32_t run = base + incl - sum;
+#pragma unroll 8
+  for (uint32_t i = lo; i < hi; ++i) {
+    offsets[1 + i] = run;
+    run += counts[i];
+  }
+  if (t == kScanThreads - 1) offsets[0] = run;
+}
+
 struct CompactArgs {
   const uint32_t* __restrict__ fired32;   // segments, `stride` words apart: [count][records]
   const uint32_t* __restrict__ counts;    // records per segment
+  const uint32_t* __restrict__ offsets;   // seg_scan_kernel's output
   kwk_fired_rec* __restrict__ out;
-  uint32_t* __restrict__ total;           // number of records (written by the last block)
-  unsigned long long* __restrict__ status;  // per block
-  unsigned long long* __restrict__ ticket;  // monotone arrival counter (never reset)
-  unsigned long long ticket_base;           // its value before this launch
   uint32_t n_segs;
-  uint32_t seg_slots;                     // object slots per segment (wave region)
+  uint32_t seg_region_shift;              // segments per sweep region = 1 << shift
+  uint32_t region_slots;                  // object slots per region (wave / tile)
   uint32_t stride;
-  uint32_t epoch;                         // 30 bits
 };
 
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
-  __shared__ uint32_t s_blk, s_prefix, s_cnt[kSegsPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0)
-    s_blk = (uint32_t)(__hip_atomic_fetch_add(a.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket_base);
-  __syncthreads();
-  const uint32_t blk = s_blk;
-  const uint32_t seg = blk * kSegsPerBlock + wave;
-  const uint32_t c = seg < a.n_segs ? a.counts[seg] : 0u;
-  if (lane == 0) s_cnt[wave] = c;
-  __syncthreads();
-  if (wave == 0) {  // the look-back: one wave reads 64 predecessors' status words at a time
-    uint32_t agg = 0;
-    for (uint32_t w = 0; w < kSegsPerBlock; ++w) agg += s_cnt[w];
-    const unsigned long long tag = (unsigned long long)(a.epoch & 0x3FFFFFFFu) << 34;
-    if (blk > 0 && lane == 0)
-      __hip_atomic_store(&a.status[blk], tag | (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t prefix = 0;
-    for (int64_t hi = (int64_t)blk - 1; hi >= 0;) {
-      const int64_t j = hi - (int64_t)lane;  // lane 0 = the nearest predecessor
-      unsigned long long st = 2ull << 32;    // before block 0: an inclusive prefix of 0
-      if (j >= 0) st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool ready = j < 0 || (st >> 34) == (tag >> 34);
-      const unsigned long long inc = __ballot(ready && ((st >> 32) & 3u) == 2u);
-      const unsigned long long wait = __ballot(!ready);
-      const uint32_t first = inc ? (uint32_t)__ffsll((long long)inc) - 1u : 64u;  // nearest inclusive prefix
-      const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
-      if (wait & need) continue;  // a predecessor in the window has not published yet: read again
-      uint32_t v = (lane <= first && ready) ? (uint32_t)st : 0u;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      prefix += v;
-      if (first < 64) break;
-      hi -= 64;  // 64 aggregates: move the window back
-    }
-    if (lane == 0) {
-      __hip_atomic_store(&a.status[blk], tag | (2ull << 32) | (uint32_t)(prefix + agg), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      s_prefix = prefix;
-      if ((blk + 1) * kSegsPerBlock >= a.n_segs) *a.total = prefix + agg;
-    }
-  }
-  __syncthreads();
-  uint32_t off = s_prefix;
-  for (uint32_t w = 0; w < wave; ++w) off += s_cnt[w];
+  const uint32_t seg = blockIdx.x * kSegsPerBlock + wave;
+  if (seg >= a.n_segs) return;
+  const uint32_t c = a.counts[seg], off = a.offsets[1 + seg];
   const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
   for (uint32_t j = lane; j < c; j += 64) {
     const uint32_t r = f32[j];
-    a.out[off + j] = kwk_fired_rec{seg * a.seg_slots + (r & 0x7FFu), (uint16_t)((r >> 11) & 31u), (uint16_t)((r >> 16) & 7u)};
+    a.out[off + j] = kwk_fired_rec{(seg >> a.seg_region_shift) * a.region_slots + (r & 0x1FFFu),
+                                   (uint16_t)((r >> 13) & 31u), (uint16_t)((r >> 18) & 7u)};
   }
 }
 
@@ -1809,11 +1820,8 @@ struct kwk_engine {
   uint32_t n_blocks_cap = 0, last_blocks = 0, last_grid = 0;
   uint32_t cum_rows = 0;      // statistics rows any sweep grid has written (<= n_blocks_cap)
   uint32_t last_objs = 16;    // words per lane of the last sweep (fired segment stride = 64 * last_objs + 32)
+  uint32_t last_region_shift = 0;  // fired segments per record region = 1 << shift (wave: 0, tile: 2)
   bool compacted = false;     // the last sweep's fired list is compacted on the device
-  unsigned long long* d_compact_status = nullptr;  // compact_kernel look-back status per block
-  unsigned long long* d_compact_ticket = nullptr;  // compact_kernel arrival counter (never reset)
-  unsigned long long compact_tickets = 0;          // its value before the next launch
-  uint32_t compact_epoch = 0;
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
@@ -2034,8 +2042,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
-  ALLOC(e->d_compact_status, sizeof(unsigned long long) * ((n_waves + kSegsPerBlock - 1) / kSegsPerBlock + 1));
-  ALLOC(e->d_compact_ticket, sizeof(unsigned long long));
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
   hipMemsetAsync(e->d_st, 0, sizeof(uint2) * st_slots, e->stream);
@@ -2043,9 +2049,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
   hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
-  hipMemsetAsync(e->d_compact_status, 0, sizeof(unsigned long long) * ((n_waves + kSegsPerBlock - 1) / kSegsPerBlock + 1),
-                 e->stream);
-  hipMemsetAsync(e->d_compact_ticket, 0, sizeof(unsigned long long), e->stream);
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
@@ -2058,8 +2061,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats, e->d_compact_status,
-                  e->d_compact_ticket,
+                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
@@ -2431,6 +2433,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     }
 #undef LAUNCH16
     e->last_objs = K;
+    e->last_region_shift = 0;
     HIP_TRY(hipGetLastError());
     e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
     e->last_grid = blocks;
@@ -2450,6 +2453,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     else hipLaunchKernelGGL((sweepw_kernel<false, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   }
   e->last_objs = K;
+  e->last_region_shift = 2;  // log2(kWavesPerBlock): records carry tile-relative slots
+  static_assert(kWavesPerBlock == 4, "region shift");
   HIP_TRY(hipGetLastError());
   e->last_blocks = blocks;
   e->last_grid = blocks;
@@ -2480,21 +2485,19 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   e->compacted = true;
   if (n_waves == 0) return KWK_OK;
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_wave_counts, n_waves,
+                     e->d_wave_offsets);
   CompactArgs a;
   a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
   a.counts = e->d_wave_counts;
+  a.offsets = e->d_wave_offsets;
   a.out = e->d_compact;
-  a.total = e->d_wave_offsets;  // word 0: the list's length
-  a.status = e->d_compact_status;
-  a.ticket = e->d_compact_ticket;
-  a.ticket_base = e->compact_tickets;
   a.n_segs = n_waves;
-  a.seg_slots = 64u * e->last_objs;
+  a.seg_region_shift = e->last_region_shift;
+  a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
-  a.epoch = ++e->compact_epoch & 0x3FFFFFFFu;
   hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
-  e->compact_tickets += blocks;
   return KWK_OK;
 }
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import json
+import math
 import re
 
 import yaml
@@ -109,11 +110,90 @@ def _go_gostring(v) -> str:
     return go_sprint(v)
 
 
+def go_json_string(s: str) -> str:
+    """encoding/json string encoding with escapeHTML (encode.go appendString, Go 1.22)."""
+    out = ['"']
+    for ch in s:
+        o = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\b":
+            out.append("\\b")
+        elif ch == "\f":
+            out.append("\\f")
+        elif o < 0x20 or ch in "<>&" or o in (0x2028, 0x2029):
+            out.append("\\u%04x" % o)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+_REPR = re.compile(r"^(\d+)(?:\.(\d+))?(?:e([-+]\d+))?$")
+
+
+def go_json_float(f: float) -> str:
+    """encoding/json float64 (encode.go floatEncoder): shortest digits, 'f' format unless the
+    magnitude is < 1e-6 or >= 1e21, then 'e' with "e-07" cleaned to "e-7"."""
+    if math.isnan(f) or math.isinf(f):
+        raise ValueError("json: unsupported value")
+    if f == 0:
+        return "-0" if math.copysign(1.0, f) < 0 else "0"
+    a = abs(f)
+    m = _REPR.match(repr(a))
+    ip, fp, ex = m.group(1), m.group(2) or "", int(m.group(3) or 0)
+    s, point = ip + fp, len(ip) + ex
+    while s.startswith("0"):
+        s, point = s[1:], point - 1
+    s = s.rstrip("0") or "0"
+    if a < 1e-6 or a >= 1e21:
+        e = point - 1
+        out = s[0] + ("." + s[1:] if len(s) > 1 else "") + "e" + ("-" if e < 0 else "+") + "%02d" % abs(e)
+        if e < 0 and out[-2] == "0":
+            out = out[:-2] + out[-1]
+    elif point <= 0:
+        out = "0." + "0" * (-point) + s
+    elif point >= len(s):
+        out = s + "0" * (point - len(s))
+    else:
+        out = s[:point] + "." + s[point:]
+    return ("-" if f < 0 else "") + out
+
+
+def go_json_bytes(v) -> str:
+    """json.Marshal of a decoded YAML / JSON value: map keys sorted, Go string / float form."""
+    if v is None or v is MISSING:
+        return "null"
+    if v is True:
+        return "true"
+    if v is False:
+        return "false"
+    if isinstance(v, Num):
+        return str(v)
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return go_json_float(v)
+    if isinstance(v, str):
+        return go_json_string(v)
+    if isinstance(v, list):
+        return "[" + ",".join(go_json_bytes(x) for x in v) + "]"
+    if isinstance(v, dict):
+        return "{" + ",".join(go_json_string(str(k)) + ":" + go_json_bytes(v[k]) for k in sorted(v, key=str)) + "}"
+    raise TypeError(f"json: unsupported type {type(v).__name__}")
+
+
 def go_json_marshal(v) -> str:
-    v = _from_go_data(v)
-    s = json.dumps(v, separators=(",", ":"), ensure_ascii=False)
-    # encoding/json escapes <, > and & for HTML safety
-    return s.replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+    """encoding/json Marshal of a template value (json.Number keeps its text, maps sorted)."""
+    return go_json_bytes(v)
 
 
 def quote(s) -> str:
