@@ -203,12 +203,14 @@ struct SweepArgs {
   const kwk_value* __restrict__ values;
   const kwk_stage_table* __restrict__ table;
   const kwk_delta* __restrict__ deltas;
-  const uint32_t* __restrict__ lut;  // pred -> matched-stage mask, lut_n entries (0: no table)
+  const uint32_t* __restrict__ lut;  // match-mask tables (lut_bytes x 256 entries, or 2^pred_bits), see match_mask
   kwk_fired_rec* __restrict__ fired;
   uint32_t* __restrict__ wave_counts;
   unsigned long long* __restrict__ cum;  // [n_blocks][kStatWords]
   uint32_t n;
-  uint32_t lut_n;
+  uint32_t lut_n;                    // table entries (0: no table)
+  uint32_t lut_bytes;                // pred bytes with a table (1..4)
+  uint32_t lut_rest;                 // stages the tables do not decide (clause loop)
   uint32_t value_slots;
   uint64_t slot_base;
   uint64_t key;
@@ -252,17 +254,36 @@ struct Fire {      // what one object's step produced
 // Updates sched (pending stage / MATCHERR) and due; returns true if a stage was scheduled.
 // kProbe (fsm_build_kernel): evaluate for a state word alone; every step that needs more than
 // the word (a value record, the deletion column, a Philox draw) sets `gen` instead.
+// Matched-stage mask: the selector of a stage is a conjunction of per-bit tests (eq) and
+// any-of clauses; when each clause lies within one byte of pred the stage is decided byte by
+// byte, so the mask is the AND of one 256-entry table per pred byte (kwk_load_stages builds
+// them; a program with <= 8 pred bits has one exact table).  Stages with a clause spanning
+// bytes (lut_rest) run the clause loop.
+__device__ __forceinline__ uint32_t match_mask(const kwk_stage_table* __restrict__ T, uint32_t n_stages,
+                                               uint32_t pred, const uint32_t* lut, uint32_t lut_n,
+                                               uint32_t lut_bytes, uint32_t lut_rest) {
+  uint32_t m = 0;
+  if (lut_n) {
+    m = lut[pred & 0xFFu];
+    if (lut_bytes > 1) m &= lut[256u | ((pred >> 8) & 0xFFu)];
+    if (lut_bytes > 2) m &= lut[512u | ((pred >> 16) & 0xFFu)];
+    if (lut_bytes > 3) m &= lut[768u | (pred >> 24)];
+    for (uint32_t r = lut_rest; r; r &= r - 1) {
+      const uint32_t s = (uint32_t)__ffs(r) - 1u;
+      m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+    }
+  } else {
+    for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
+  }
+  return m;
+}
+
 template <bool kProbe = false>
 __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                              uint32_t n_stages, uint64_t i, uint32_t pred, uint32_t& sched,
                                              int64_t& due, uint32_t& bytes, const uint32_t* lut, uint32_t lut_n,
                                              uint32_t& gen) {
-  uint32_t m = 0;
-  if (pred < lut_n) {
-    m = lut[pred];
-  } else {
-    for (uint32_t s = 0; s < n_stages; ++s) m |= (stage_matches(T->stages[s], pred) ? 1u : 0u) << s;
-  }
+  const uint32_t m = match_mask(T, n_stages, pred, lut, lut_n, a.lut_bytes, a.lut_rest);
   sched &= ~(KWK_F_DIRTY | KWK_F_MATCHERR);
   if (m == 0) return false;  // no match: a queued job stays queued (pod_controller.go:222-229)
   const kwk_value* __restrict__ rec = nullptr;
@@ -475,7 +496,9 @@ __device__ __forceinline__ void emit_fired(const Fire& f, uint64_t i, uint32_t l
   }
 }
 
-constexpr uint32_t kLutMax = 256;  // pred -> match-mask table for programs with pred_bits <= 8
+constexpr uint32_t kLutMax = 256;      // one match-mask table (programs with pred_bits <= 8)
+constexpr uint32_t kLutTables = 1024;  // four byte tables (any pred width)
+constexpr uint32_t kLutLdsW = 512;     // tables the word sweep stages in LDS (pred <= 16 bits)
 
 // Streamed loads go through buffer resources (T8 in cdna_hip_programming.md): a load past the
 // resource's byte size returns 0, so the tile tail and "load due only where a stage is
@@ -604,7 +627,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   const uint32_t fin_group = a.table->fin_group_mask;
   const uint32_t n_deltas = a.table->n_classes * n_stages;
   const uint32_t lut_n = a.lut_n;
-  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
+  const uint32_t* __restrict__ lutp = lut_n <= kLutMax ? s_lut : a.lut;  // byte tables: read through L1
+  if (lut_n <= kLutMax)
+    for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   const kwk_delta* __restrict__ deltas = a.deltas;
   if (n_deltas <= kLdsDeltas16) {
@@ -760,7 +785,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
             uint32_t gen_unused = 0;
             int64_t due_unused = 0;
             const uint2 nv = process_object<kHarness, 2>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                         n_matched, s_lut, lut_n, gen_unused, due_unused);
+                                                         n_matched, lutp, lut_n, gen_unused, due_unused);
             tw[w] = (uint16_t)fmt_pack(nv.x, nv.y, fmt);
           }
           n_line -= 2u;  // the word's own write is replaced by the line stores below
@@ -837,7 +862,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
 //           (tile, wave) segment;
 //  phase 3  aligned 8-lane groups (one 128-byte line) holding a changed word are stored whole.
 constexpr int kQW = 4;                 // 16-byte chunks per lane: 16 (4-byte) / 8 (8-byte) words per lane
-constexpr int kLdsDeltasW = 256;       // (class, stage) deltas staged in LDS by the word sweep
+constexpr int kLdsDeltasW = 128;       // (class, stage) deltas staged in LDS by the word sweep
 
 template <uint32_t kWB> struct WordOf { typedef uint32_t T; };
 template <> struct WordOf<8> { typedef uint2 T; };
@@ -866,7 +891,7 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   __shared__ kwk_delta s_delta[kLdsDeltasW];
   __shared__ uint16_t s_work[kTile];
   __shared__ uint4 s_tile[kWavesPerBlock][64 * kQW];
-  __shared__ uint32_t s_lut[kLutMax];
+  __shared__ uint32_t s_lut[kLutLdsW];
   __shared__ uint32_t s_cnt[kWavesPerBlock][2];
   __shared__ kwk_stage_table s_tab;
   const uint32_t lane = threadIdx.x & 63;
@@ -893,7 +918,9 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   const uint32_t fin_group = a.table->fin_group_mask;
   const uint32_t n_deltas = a.table->n_classes * n_stages;
   const uint32_t lut_n = a.lut_n;
-  for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
+  const uint32_t* __restrict__ lutp = lut_n <= kLutLdsW ? s_lut : a.lut;  // wider programs: through L1
+  if (lut_n <= kLutLdsW)
+    for (uint32_t j = threadIdx.x; j < lut_n; j += kBlock) s_lut[j] = a.lut[j];
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   const kwk_delta* __restrict__ deltas = a.deltas;
   if (n_deltas <= (uint32_t)kLdsDeltasW) {
@@ -1006,7 +1033,7 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
         uint32_t gen_unused = 0;
         int64_t due_unused = 0;
         const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                       n_matched, s_lut, lut_n, gen_unused, due_unused);
+                                                       n_matched, lutp, lut_n, gen_unused, due_unused);
         W out;
         sw_encode(out, nv, fmt);
         tw[off] = out;
@@ -1068,32 +1095,58 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
 constexpr uint32_t kScanThreads = 1024;
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;  // one wave per segment
 
-// offsets[0] = total, offsets[1 + i] = records before segment i
+// offsets[0] = total, offsets[1 + i] = records before segment i.  Rounds of 4096 counts: each
+// thread loads 4 consecutive counts (coalesced 16-byte loads, the next round's issued before
+// this round's scan), the block scans the round's 1024 partial sums, a carry joins the rounds.
 __global__ __launch_bounds__(kScanThreads) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
                                                                 uint32_t* __restrict__ offsets) {
+  constexpr uint32_t kRound = kScanThreads * 4;
   __shared__ uint32_t s_wave[kScanThreads / 64];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
-  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
-  uint32_t sum = 0;
-#pragma unroll 8
-  for (uint32_t i = lo; i < hi; ++i) sum += counts[i];
-  uint32_t incl = sum;  // inclusive scan over the wave
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o);
-    if (lane >= (uint32_t)o) incl += y;
+  auto load4 = [&](uint32_t i0) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (i0 + 3 < n) {
+      v = *reinterpret_cast<const uint4*>(counts + i0);  // counts is 16-byte aligned
+    } else {
+      if (i0 < n) v.x = counts[i0];
+      if (i0 + 1 < n) v.y = counts[i0 + 1];
+      if (i0 + 2 < n) v.z = counts[i0 + 2];
+    }
+    return v;
+  };
+  uint32_t carry = 0;
+  uint4 nxt = load4(t * 4);
+  for (uint32_t base = 0; base < n; base += kRound) {
+    const uint32_t i0 = base + t * 4;
+    const uint4 v = nxt;
+    if (base + kRound < n) nxt = load4(i0 + kRound);
+    const uint32_t sum = v.x + v.y + v.z + v.w;
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, round = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kScanThreads / 64; ++w) {
+      const uint32_t x = s_wave[w];
+      before += w < wave ? x : 0u;
+      round += x;
+    }
+    uint32_t run = carry + before + incl - sum;
+    if (i0 < n) offsets[1 + i0] = run;
+    run += v.x;
+    if (i0 + 1 < n) offsets[2 + i0] = run;
+    run += v.y;
+    if (i0 + 2 < n) offsets[3 + i0] = run;
+    run += v.z;
+    if (i0 + 3 < n) offsets[4 + i0] = run;
+    carry += round;
+    __syncthreads();  // s_wave is rewritten by the next round
   }
-  if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint32_t base = 0;
-  for (uint32_t w = 0; w < wave; ++w) base += s_wave[w];
-  uint32_t run = base + incl - sum;
-#pragma unroll 8
-  for (uint32_t i = lo; i < hi; ++i) {
-    offsets[1 + i] = run;
-    run += counts[i];
-  }
-  if (t == kScanThreads - 1) offsets[0] = run;
+  if (t == 0) offsets[0] = carry;
 }
 
 struct CompactArgs {
@@ -1107,16 +1160,28 @@ struct CompactArgs {
   uint32_t stride;
 };
 
+// one wave per segment; the first 256 records are loaded together with the segment's count and
+// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it)
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
+  constexpr int kPre = 4;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t seg = blockIdx.x * kSegsPerBlock + wave;
   if (seg >= a.n_segs) return;
-  const uint32_t c = a.counts[seg], off = a.offsets[1 + seg];
   const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
-  for (uint32_t j = lane; j < c; j += 64) {
-    const uint32_t r = f32[j];
-    a.out[off + j] = kwk_fired_rec{(seg >> a.seg_region_shift) * a.region_slots + (r & 0x1FFFu),
-                                   (uint16_t)((r >> 13) & 31u), (uint16_t)((r >> 18) & 7u)};
+  uint32_t r[kPre];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) r[k] = f32[lane + 64u * k];
+  const uint32_t c = a.counts[seg], off = a.offsets[1 + seg];
+  const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const uint32_t j = lane + 64u * k;
+    if (j < c)
+      a.out[off + j] = kwk_fired_rec{base + (r[k] & 0x1FFFu), (uint16_t)((r[k] >> 13) & 31u), (uint16_t)((r[k] >> 18) & 7u)};
+  }
+  for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
+    const uint32_t x = f32[j];
+    a.out[off + j] = kwk_fired_rec{base + (x & 0x1FFFu), (uint16_t)((x >> 13) & 31u), (uint16_t)((x >> 18) & 7u)};
   }
 }
 
@@ -1845,8 +1910,8 @@ struct kwk_engine {
   uint32_t* d_rec = nullptr;
   kwk_value* d_values = nullptr;
   kwk_stage_table* d_table = nullptr;
-  uint32_t* d_lut = nullptr;  // kLutMax match masks (valid for lut_n entries)
-  uint32_t lut_n = 0;
+  uint32_t* d_lut = nullptr;  // kLutTables match masks (valid for lut_n entries)
+  uint32_t lut_n = 0, lut_bytes = 0, lut_rest = 0;
   kwk_delta* d_deltas = nullptr;
   kwk_fired_rec* d_fired = nullptr;
   kwk_fired_rec* d_compact = nullptr;
@@ -2034,7 +2099,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_rec, sizeof(uint32_t) * (size_t)e->capacity);
   ALLOC(e->d_values, sizeof(kwk_value) * (size_t)e->max_records * e->value_slots);
   ALLOC(e->d_table, sizeof(kwk_stage_table));
-  ALLOC(e->d_lut, sizeof(uint32_t) * kLutMax);
+  ALLOC(e->d_lut, sizeof(uint32_t) * kLutTables);
   ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
                                               (size_t)kBlock * kMaxObjPerThread));
   ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
@@ -2107,11 +2172,45 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   }
   HIP_TRY(hipMemcpy(e->d_table, t, sizeof(kwk_stage_table), hipMemcpyHostToDevice));
   // the match set of every pred value, when pred_bits is small (Lifecycle.match, lifecycle.go:51-63)
-  e->lut_n = (t->pred_bits != 0 && t->pred_bits <= 8) ? (1u << t->pred_bits) : 0u;
+  // match-mask tables (match_mask): one exact table up to 8 pred bits, else one per pred byte
+  // for the stages whose clauses each lie within one byte
+  e->lut_n = e->lut_bytes = e->lut_rest = 0;
+  if (t->pred_bits != 0 && t->pred_bits <= 8) {
+    e->lut_n = 1u << t->pred_bits;
+    e->lut_bytes = 1;
+  } else if (t->pred_bits > 8) {
+    e->lut_bytes = (t->pred_bits + 7) / 8;
+    e->lut_n = 256u * e->lut_bytes;
+  }
   if (e->lut_n) {
     std::vector<uint32_t> lut(e->lut_n, 0u);
-    for (uint32_t p = 0; p < e->lut_n; ++p)
-      for (uint32_t s = 0; s < t->n_stages; ++s) lut[p] |= (stage_matches(t->stages[s], p) ? 1u : 0u) << s;
+    if (e->lut_bytes == 1 && e->lut_n <= 256) {
+      for (uint32_t p = 0; p < e->lut_n; ++p)
+        for (uint32_t s = 0; s < t->n_stages; ++s) lut[p] |= (stage_matches(t->stages[s], p) ? 1u : 0u) << s;
+    } else {
+      for (uint32_t s = 0; s < t->n_stages; ++s) {
+        const kwk_stage_desc& S = t->stages[s];
+        bool sep = true;
+        for (uint32_t k = 0; k < S.n_any; ++k) {
+          const uint32_t am = S.any_mask[k];
+          bool one = false;
+          for (uint32_t b = 0; b < 4; ++b) one |= am != 0 && (am & ~(0xFFu << (8 * b))) == 0;
+          sep &= one || am == 0;
+        }
+        if (!sep) { e->lut_rest |= 1u << s; continue; }
+        for (uint32_t b = 0; b < e->lut_bytes; ++b)
+          for (uint32_t v = 0; v < 256; ++v) {
+            const uint32_t x = v << (8 * b), bm = 0xFFu << (8 * b);
+            bool ok = ((x ^ S.eq_val) & S.eq_mask & bm) == 0;
+            for (uint32_t k = 0; k < S.n_any; ++k)
+              if ((S.any_mask[k] & ~bm) == 0 && S.any_mask[k])
+                ok &= ((x & S.any_mask[k]) != 0) == (((S.any_want >> k) & 1u) != 0);
+              else if (S.any_mask[k] == 0 && b == 0)
+                ok &= ((S.any_want >> k) & 1u) == 0;  // an empty clause is never satisfied
+            lut[256 * b + v] |= (ok ? 1u : 0u) << s;
+          }
+      }
+    }
     HIP_TRY(hipMemcpy(e->d_lut, lut.data(), sizeof(uint32_t) * e->lut_n, hipMemcpyHostToDevice));
   }
   if (e->d_deltas) HIP_TRY(hipFree(e->d_deltas));
@@ -2332,6 +2431,8 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
   a.deltas = e->d_deltas;
   a.lut = e->d_lut;
   a.lut_n = e->lut_n;
+  a.lut_bytes = e->lut_bytes;
+  a.lut_rest = e->lut_rest;
   a.fired = e->d_fired;
   a.wave_counts = e->d_wave_counts;
   a.cum = e->d_cum;

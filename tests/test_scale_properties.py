@@ -149,3 +149,72 @@ def test_aggregates_and_handback_at_17m_pods():
             np.testing.assert_allclose(total, [vc.sum(), vm.sum()], rtol=1e-9)
     finally:
         eng.close()
+
+
+def _c2_program(n):
+    from kwok_amd import workload as W
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.stages import load_stage_files
+    pvars, _ = W.c2_pod_variants(0, n, seed=0x6B776F6B, job_frac=0.1)
+    prog = KindProgram(load_stage_files(*W.stage_paths(W.POD_GENERAL + W.POD_CHAOS)), HarnessSpec())
+    prog.explore(pvars)  # one program for every shard (same classes / features)
+    return prog
+
+
+def _c2_pods(prog, lo, hi, state):
+    """Pods [lo, hi) of the C2 mix (pod-general + pod-chaos: weighted picks, jitter draws, value
+    records, deletion-timestamp getters) as one engine with slot_base = lo."""
+    from kwok_amd import workload as W
+    from kwok_amd.host.engine import Engine, Ingest
+    pvars, pidx = W.c2_pod_variants(lo, hi, seed=0x6B776F6B, job_frac=0.1)
+    ing = Ingest(prog)
+    hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+    eng = Engine(prog, capacity=hi - lo, state=state, slot_base=lo, max_records=max(1, len(ing.records)) + 16)
+    eng.load_stages()
+    eng.set_harness(True)
+    eng.load(hot, dels, rec, cls, ing.record_array())
+    return prog, eng
+
+
+def test_c2_mix_formats_and_shards_agree_at_4m_pods():
+    """The word sweep on the C2 stage mix at 4M pods: the 4-byte and 8-byte formats and two
+    half-cluster shards (global-slot RNG keys) fire the same (slot, stage, flags) sets and leave
+    the same objects, step after step; the weighted-pick / jitter / record paths all run."""
+    n = 4_000_000
+    prog = _c2_program(n)
+    eng = {"u32": _c2_pods(prog, 0, n, "u32"), "wide": _c2_pods(prog, 0, n, "wide"),
+           "s0": _c2_pods(prog, 0, n // 2, "u32"), "s1": _c2_pods(prog, n // 2, n, "u32")}
+    try:
+        assert eng["u32"][1].stats()["state_bytes"] == 4 and eng["wide"][1].stats()["state_bytes"] == 8
+        now0 = 1_700_000_000 * 10**9
+        total = 0
+        for k in range(24):
+            keys = {}
+            for s, (_, e) in eng.items():
+                e.step(now0 + k * 500 * 10**6, 0x6B776F6B, k)
+                f = e.fired()
+                assert len(np.unique(f["slot"])) == len(f), f"{s} step {k}: a slot fired twice"
+                if s == "s1":
+                    f = f.copy()
+                    f["slot"] += n // 2
+                keys[s] = _fired_key(f)
+            shards = np.sort(np.concatenate([keys["s0"], keys["s1"]]))
+            assert np.array_equal(keys["u32"], keys["wide"]), f"step {k}: formats differ"
+            assert np.array_equal(keys["u32"], shards), f"step {k}: shards differ"
+            total += len(keys["u32"])
+        assert total > n // 2
+        a = eng["u32"][1].read()[0]
+        w = eng["wide"][1].read()[0]
+        s0, s1 = eng["s0"][1].read()[0], eng["s1"][1].read()[0]
+        for col in ("pred", "sched"):
+            assert np.array_equal(a[col], w[col]), col
+            assert np.array_equal(a[col], np.concatenate([s0[col], s1[col]])), col
+        pend = (a["sched"] & 0xFF) != 0xFF
+        assert np.array_equal(a["due"][pend], w["due"][pend])
+        st = eng["u32"][1].stats()
+        fired = {name: c for name, c in st["fired_per_stage"].items() if c}
+        assert {"pod-create", "pod-ready", "pod-complete", "pod-delete"} <= set(fired), fired
+        assert any("failed" in name for name in fired), fired  # the chaos stages (weighted picks)
+    finally:
+        for _, e in eng.values():
+            e.close()

@@ -1,0 +1,93 @@
+"""Cost-isolation builds of the engine (tools only: never loaded by the package, the tests or
+bench.py).  Each variant is engine.hip with a few source replacements — most of them give
+WRONG results on purpose (a phase skipped, a draw replaced) and exist only to time what the
+removed work costs on the C2-mix HBM working set.
+
+    python tools/variants.py build [names...]      # -> tools/build/libkwok_engine_<name>.so
+    python tools/variants.py run [names...]        # one child process per variant, JSON lines
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "kwok_amd", "csrc", "engine.hip")
+OUT = os.path.join(ROOT, "tools", "build")
+
+_P2 = ("const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,\n"
+       "                                                       n_matched, lutp, lut_n, gen_unused, due_unused);")
+
+VARIANTS = {
+    "base": [],
+    # phase 2 of the word sweep does nothing (no state change, no fires)
+    "w_nophase2": [(_P2, "const uint2 nv = s; (void)due; (void)i; (void)gen_unused; (void)due_unused;")],
+    # jitter without its Philox draw
+    "nojitter": [("delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));",
+                  "delay = (int64_t)((uint64_t)delay + (uint64_t)(jit >> 1));")],
+    # the word sweep's fired records / per-stage counts are not written
+    "w_noemit": [("      emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);\n", "      (void)f;\n")],
+}
+
+
+def build(names):
+    os.makedirs(OUT, exist_ok=True)
+    src = open(SRC).read()
+
+    def one(name):
+        s = src
+        for old, new in VARIANTS[name]:
+            if old not in s:
+                raise SystemExit(f"variant {name}: pattern not found: {old[:60]!r}")
+            s = s.replace(old, new)
+        path = os.path.join(OUT, f"engine_{name}.hip")
+        open(path, "w").write(s)
+        so = os.path.join(OUT, f"libkwok_engine_{name}.so")
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+               "-Wno-unused-value", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "kwok_amd", "csrc"),
+               "-o", so, path]
+        subprocess.run(cmd, check=True)
+        return so
+
+    with ThreadPoolExecutor(4) as ex:
+        for so in ex.map(one, names):
+            print(so, flush=True)
+
+
+def child(name, hbm_nodes, steps):
+    sys.path.insert(0, ROOT)
+    from kwok_amd.host import abi
+    abi.LIB_PATH = os.path.join(OUT, f"libkwok_engine_{name}.so")
+    import bench
+    args = argparse.Namespace(hbm_nodes=hbm_nodes, pods_per_node=100, seed=0x6B776F6B, job_frac=0.1,
+                              hbm_steps=steps, hbm_warmup=12)
+    r = bench.measure_hbm_working_set(args, 0)
+    print(json.dumps({"variant": name, **r}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=("build", "run", "child"))
+    ap.add_argument("names", nargs="*")
+    ap.add_argument("--hbm-nodes", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    names = a.names or list(VARIANTS)
+    if a.cmd == "build":
+        build(names)
+    elif a.cmd == "child":
+        child(names[0], a.hbm_nodes, a.steps)
+    else:
+        for n in names:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "child", n, "--hbm-nodes", str(a.hbm_nodes),
+                                "--steps", str(a.steps)], timeout=300)
+            if r.returncode != 0:
+                raise SystemExit(f"variant {n}: rc {r.returncode}")
+
+
+if __name__ == "__main__":
+    main()
