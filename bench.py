@@ -128,37 +128,41 @@ def configure_usage(pods, pvars, pidx, n_nodes_local, pods_per_node):
 
 
 class Reporter:
-    """One reporting interval: device aggregates of this shard, summed over all GPUs (RCCL)."""
+    """One reporting interval: this shard's aggregates computed on the device (kwk_aggregate:
+    per-stage transitions, phase histograms, cluster usage) and, with several GPUs, summed in
+    place by one RCCL all-reduce — no host round trip except the wait before the collective."""
 
     def __init__(self, pods, nodes, dist, device):
-        from kwok_amd.host.cluster import phase_masks
-        self.pods, self.nodes, self.dist, self.device = pods, nodes, dist, device
+        from kwok_amd.host.cluster import DeviceReport, phase_masks
         pm = phase_masks(pods.p, values=("Running", "Succeeded", "Failed"))
         nm = phase_masks(nodes.p, values=("Running",))
-        self.masks = [[0] + list(pm.values()), [0] + list(nm.values())]
-        self.names = [["pods"] + [f"pods_{k}" for k in pm], ["nodes"] + [f"nodes_{k}" for k in nm]]
+        masks = [[0] + list(pm.values()), [0] + list(nm.values())]
+        names = [["pods"] + [f"pods_{k}" for k in pm], ["nodes"] + [f"nodes_{k}" for k in nm]]
+        self.report = DeviceReport([pods, nodes], masks, names, usage_engine=pods, dist=dist, device=device)
 
     def collect(self, now_ns):
-        from kwok_amd.host.cluster import engine_aggregates
-        agg = engine_aggregates([self.pods, self.nodes], self.masks, self.names, now_ns, usage_engine=self.pods)
-        return agg.allreduce(self.dist, device=self.device)
+        self.report.collect(now_ns)
+        return self.report
+
+
+EV_EVERY = 2  # HIP events bracket the pod sweep of every 2nd step: each marker idles the stream ~5 us (r2b)
 
 
 def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None):
-    """Steps k0..k1-1; ev_base: record HIP events (pod stream) around each pod sweep."""
+    """Steps k0..k1-1; ev_base: record HIP events (pod stream) around the pod sweep of every
+    EV_EVERY-th step (events 2i, 2i+1 of sample i)."""
     last = None
     n_fired_host = 0
     for k in range(k0, k1):
         now = NOW0 + k * dt
         j = k - k0
-        if ev_base is not None:
-            pods.event_record(ev_base + 3 * j)
+        timed = ev_base is not None and j % EV_EVERY == 0
+        if timed:
+            pods.event_record(ev_base + 2 * (j // EV_EVERY))
         pods.step(now, seed, k)
-        if ev_base is not None:
-            pods.event_record(ev_base + 3 * j + 1)
+        if timed:
+            pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
         pods.fired_compact()
-        if ev_base is not None:
-            pods.event_record(ev_base + 3 * j + 2)
         nodes.step(now, seed, k)
         nodes.fired_compact()
         if pinned is not None:  # PCIe-inclusive: every fired record copied to pinned host memory
@@ -191,9 +195,10 @@ def measure_hbm_working_set(args, device):
         nodes.sync()
         wall = time.perf_counter() - t0
         s1 = pods.stats()
-        sweep_ms = sum(pods.event_elapsed_ms(3 * j, 3 * j + 1) for j in range(steps))
+        n_ev = (steps + EV_EVERY - 1) // EV_EVERY
+        sweep_ms = statistics.mean(pods.event_elapsed_ms(2 * i, 2 * i + 1) for i in range(n_ev))
         b, lb = sweep_bytes(s0, s1)
-        us = sweep_ms / steps * 1e3
+        us = sweep_ms * 1e3
         ach = b / steps / (us * 1e-6) / 1e9
         return {"workload": f"C2 stage mix at {n_nodes * args.pods_per_node:,} pods ({n_nodes:,} nodes): pod-general + "
                             "pod-chaos, harness churn, 0.5 s per step",
@@ -432,9 +437,9 @@ def main():
     nodes.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    agg_dict = agg.result().as_dict() if agg is not None else None  # the last interval's all-reduced aggregates
     s1p, s1n = pods.stats(), nodes.stats()
-    sweep_ms = [pods.event_elapsed_ms(3 * j, 3 * j + 1) for j in range(args.steps)]
-    compact_ms = [pods.event_elapsed_ms(3 * j + 1, 3 * j + 2) for j in range(args.steps)]
+    sweep_ms = [pods.event_elapsed_ms(2 * i, 2 * i + 1) for i in range((args.steps + EV_EVERY - 1) // EV_EVERY)]
 
     fired = (s1p["fired"] - s0p["fired"]) + (s1n["fired"] - s0n["fired"])
     pbytes, plines = sweep_bytes(s0p, s1p)
@@ -525,11 +530,11 @@ def main():
             "cpu_baseline_soa": cpu_soa,
             "pcie_inclusive": pcie,
             "hbm_working_set": hbm,
-            "aggregates": agg.as_dict() if agg is not None else None,
+            "aggregates": agg_dict,
             "detail": {"transitions_per_step": total_fired / args.steps, "per_stage_rank0": per_stage,
                        "pod_sweep_us_mean": round(statistics.mean(sweep_ms) * 1e3, 2),
                        "pod_sweep_us_median": round(statistics.median(sweep_ms) * 1e3, 2),
-                       "pod_handback_us_mean": round(statistics.mean(compact_ms) * 1e3, 2),
+                       "pod_sweep_launches_timed": len(sweep_ms),
                        "setup_s": round(setup_s, 1)},
         }
         print(json.dumps(line), flush=True)

@@ -428,6 +428,24 @@ kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32
  * alive objects), k < 16 — e.g. the phase histogram all-reduced across GPUs (synchronises) */
 kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);
 
+/* The whole reporting-interval aggregate of one engine, computed on the device without a host
+ * round trip (SURVEY §8(b) kwk_aggregates; the C5 all-reduce reads it in place): enqueues the
+ * per-stage transition totals (as kwk_stats), kwk_count of `masks` and, with KWK_AGG_USAGE, a
+ * kwk_usage evaluation at now_ns, and writes float64
+ *   out[0 .. n_stages)                       cumulative transitions per stage
+ *   out[n_stages .. n_stages + n_masks)      counts per mask
+ *   out[n_stages + n_masks + {0, 1}]         cluster cpu / memory usage (KWK_AGG_USAGE only)
+ * `out` is DEVICE memory on the engine's device (e.g. the RCCL buffer; counts stay exact up to
+ * 2^53), or NULL for the engine's own buffer, read back with kwk_aggregate_read.  Stream-ordered:
+ * kwk_sync (or kwk_aggregate_read) before another stream reads `out`.  Returns the number of
+ * doubles written in *n_out.  Reference: metrics_resource_usage.go:195-224 (cluster usage). */
+#define KWK_AGG_USAGE (1u << 0)
+kwk_status kwk_aggregate(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, int64_t now_ns, uint32_t flags,
+                         double* out, uint32_t* n_out);
+/* copies the engine-owned aggregate buffer (the last kwk_aggregate with out = NULL) to host memory
+ * (synchronises): n doubles */
+kwk_status kwk_aggregate_read(kwk_engine* eng, double* host_out, uint32_t n);
+
 /* raw device pointers for in-process consumers (RCCL aggregates, profiling): state = the
  * state stream (kwk_step_stats.state_bytes per slot); fired / wave_counts = the sweep's
  * internal fired segments and per-segment counts (valid after kwk_fired) */

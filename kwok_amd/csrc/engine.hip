@@ -1086,73 +1086,68 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
 }
 
 // ------------------------------------------------------------------ fired hand-back
-// Two launches over the sweep's per-(tile, wave) segments: one workgroup scans the segment
-// counts (which the sweep writes into `counts`) into exclusive offsets — a few hundred KB,
-// read once per step — then one wave per segment expands its 4-byte records {slot within the
-// wave region: 11, stage: 5, flags: 3} into kwk_fired_rec at its offset of one dense list.
-// (A single-pass decoupled look-back was measured slower here: with ~12k tiny blocks the
-// look-back chains, not the bytes, set the time — 165 us vs the ~30 us the bytes need.)
-constexpr uint32_t kScanThreads = 1024;
-constexpr uint32_t kSegsPerBlock = kWavesPerBlock;  // one wave per segment
+// Two launches over the sweep's per-(tile, wave) segments: seg_scan_kernel turns the segment
+// counts (which the sweep writes into `counts`) into exclusive offsets within groups of
+// kScanGroup segments plus one total per group (all groups in parallel: a single-workgroup scan
+// over the ~50k counts of a 100M-object sweep was latency-bound, 18.5 us, r2b), then one wave
+// per segment adds the totals of the groups before its own and expands its 4-byte records
+// {slot within the wave region: 11, stage: 5, flags: 3} into kwk_fired_rec at its offset of one
+// dense list; the last segment's wave writes the list length.  (A single-pass decoupled
+// look-back was measured slower here: with ~12k tiny blocks the look-back chains, not the bytes,
+// set the time — 165 us vs the ~30 us the bytes need.)
+constexpr uint32_t kScanPer = 16;                         // counts per thread
+constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 4096 counts per group (one workgroup)
+constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
 
-// offsets[0] = total, offsets[1 + i] = records before segment i.  Rounds of 4096 counts: each
-// thread loads 4 consecutive counts (coalesced 16-byte loads, the next round's issued before
-// this round's scan), the block scans the round's 1024 partial sums, a carry joins the rounds.
-__global__ __launch_bounds__(kScanThreads) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
-                                                                uint32_t* __restrict__ offsets) {
-  constexpr uint32_t kRound = kScanThreads * 4;
-  __shared__ uint32_t s_wave[kScanThreads / 64];
+// offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records
+__global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
+                                                         uint32_t* __restrict__ offsets,
+                                                         uint32_t* __restrict__ group_tot) {
+  __shared__ uint32_t s_wave[kWavesPerBlock];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  auto load4 = [&](uint32_t i0) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (i0 + 3 < n) {
-      v = *reinterpret_cast<const uint4*>(counts + i0);  // counts is 16-byte aligned
-    } else {
-      if (i0 < n) v.x = counts[i0];
-      if (i0 + 1 < n) v.y = counts[i0 + 1];
-      if (i0 + 2 < n) v.z = counts[i0 + 2];
-    }
-    return v;
-  };
-  uint32_t carry = 0;
-  uint4 nxt = load4(t * 4);
-  for (uint32_t base = 0; base < n; base += kRound) {
-    const uint32_t i0 = base + t * 4;
-    const uint4 v = nxt;
-    if (base + kRound < n) nxt = load4(i0 + kRound);
-    const uint32_t sum = v.x + v.y + v.z + v.w;
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o);
-      if (lane >= (uint32_t)o) incl += y;
-    }
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0, round = 0;
+  const uint32_t i0 = blockIdx.x * kScanGroup + t * kScanPer;
+  uint32_t v[kScanPer];
 #pragma unroll
-    for (uint32_t w = 0; w < kScanThreads / 64; ++w) {
-      const uint32_t x = s_wave[w];
-      before += w < wave ? x : 0u;
-      round += x;
+  for (uint32_t q = 0; q < kScanPer / 4; ++q) {
+    const uint32_t i = i0 + 4u * q;
+    uint4 c = make_uint4(0u, 0u, 0u, 0u);
+    if (i + 3 < n) {
+      c = *reinterpret_cast<const uint4*>(counts + i);  // counts is 16-byte aligned
+    } else {
+      if (i < n) c.x = counts[i];
+      if (i + 1 < n) c.y = counts[i + 1];
+      if (i + 2 < n) c.z = counts[i + 2];
     }
-    uint32_t run = carry + before + incl - sum;
-    if (i0 < n) offsets[1 + i0] = run;
-    run += v.x;
-    if (i0 + 1 < n) offsets[2 + i0] = run;
-    run += v.y;
-    if (i0 + 2 < n) offsets[3 + i0] = run;
-    run += v.z;
-    if (i0 + 3 < n) offsets[4 + i0] = run;
-    carry += round;
-    __syncthreads();  // s_wave is rewritten by the next round
+    v[4 * q] = c.x; v[4 * q + 1] = c.y; v[4 * q + 2] = c.z; v[4 * q + 3] = c.w;
   }
-  if (t == 0) offsets[0] = carry;
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) sum += v[j];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kWavesPerBlock; ++w) before += w < wave ? s_wave[w] : 0u;
+  uint32_t run = before + incl - sum;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    if (i0 + j < n) offsets[1 + i0 + j] = run;
+    run += v[j];
+  }
+  if (t == kBlock - 1) group_tot[blockIdx.x] = run;
 }
 
 struct CompactArgs {
   const uint32_t* __restrict__ fired32;   // segments, `stride` words apart: [count][records]
   const uint32_t* __restrict__ counts;    // records per segment
-  const uint32_t* __restrict__ offsets;   // seg_scan_kernel's output
+  uint32_t* __restrict__ offsets;         // seg_scan_kernel's output; [0] <- the list length
+  const uint32_t* __restrict__ group_tot;
   kwk_fired_rec* __restrict__ out;
   uint32_t n_segs;
   uint32_t seg_region_shift;              // segments per sweep region = 1 << shift
@@ -1171,7 +1166,12 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   uint32_t r[kPre];
 #pragma unroll
   for (int k = 0; k < kPre; ++k) r[k] = f32[lane + 64u * k];
-  const uint32_t c = a.counts[seg], off = a.offsets[1 + seg];
+  const uint32_t c = a.counts[seg];
+  uint32_t gp = 0;  // records of the groups before this segment's
+  for (uint32_t g = lane; g < seg / kScanGroup; g += 64) gp += a.group_tot[g];
+  for (int o = 32; o > 0; o >>= 1) gp += __shfl_xor(gp, o);
+  const uint32_t off = gp + a.offsets[1 + seg];
+  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
   const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
@@ -1313,21 +1313,31 @@ __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uin
 
 // ------------------------------------------------------------------ resource usage
 // server/metrics_resource_usage.go:170-224 (pod / node sums), :36-109 (cumulative integrators).
-// One wave per group of kUG consecutive nodes: the group's node-sorted pods form one contiguous
-// range that the wave streams kUU passes of 64 pods at a time (all loads of a batch in flight
-// before any is used: enough bytes in flight per CU to stream instead of waiting on each
-// node's latency chain).  A pod contributes containers x its interned cpu / memory value (dead
-// pods — not in the pod cache — nothing); each pass is reduced per node with a segmented scan
-// across the lanes (pods of one node are contiguous), whose segment tails add into the node's
-// LDS accumulator: a fixed order, so results are reproducible run to run.  The reference adds
-// pods in SyncMap order (unordered, utils/maps/sync.go:93-100), so sums agree with it to
-// floating-point reassociation: the tests hold them to 1e-6 relative (north_star).
+// The pods are node-sorted (node_ptr CSR).  kwk_usage_config cuts the node list into chunks of
+// whole nodes holding at most kUChunkPods pods (and kUChunkNodes nodes); one wave per chunk.
+// Each lane owns kURun consecutive pods (the wave's row of 64 x kURun slots starts at the
+// chunk's first pod rounded down to 8, so every lane's state / usage-key bytes are whole
+// 16-byte loads) and adds them up in order, closing a node where its pods end:
+//  * a node whose first pod lies in the lane is complete in the lane: finalised there;
+//  * the lane's first node may have started in earlier lanes (its "head"), its last may go on
+//    in later lanes (its open "tail"): one segmented scan over the lanes' tails (keyed by node,
+//    pods of a node are contiguous) gives the earlier lanes' share, which the lane that closes
+//    the node adds to its head.  Nodes larger than a row carry their sum into the next row.
+// So a node sum costs one cross-lane scan per 64 x kURun pods instead of one per 64, and the
+// stream is read with wide loads.  A pod contributes containers x its interned cpu / memory
+// value (dead pods — not in the pod cache — nothing), containers added in spec order (:170-193).
+// The reference adds pods in SyncMap order (unordered, utils/maps/sync.go:93-100), so sums agree
+// with it to floating-point reassociation: the tests hold them to 1e-6 relative (north_star);
+// the order here is fixed, so results are reproducible run to run.
 // With per-pod outputs enabled (kwk_usage_pods) every pod also gets its Usage (podResourceUsage,
 // :170-193) and its cumulative usage (podResourceCumulativeUsage, :54-65: the sum of its
 // containers' integrators, each advanced by (now - last) * value, :36-52); a dead pod reads 0
 // and keeps its integrators (Go keys them by name, so a re-created pod continues them).
-constexpr uint32_t kUG = 16;  // nodes per wave
-constexpr int kUU = 4;        // passes of 64 pods with loads in flight together
+constexpr uint32_t kURun = 16;                  // consecutive pods per lane
+constexpr uint32_t kURow = 64u * kURun;         // slots per wave row
+constexpr uint32_t kUChunkPods = kURow - 8u;    // a chunk fits one row even after rounding its start down to 8
+constexpr uint32_t kUChunkNodes = 128;          // nodes per chunk: the wave's LDS copy of node_ptr
+constexpr uint32_t kULdsValues = 512;           // cpu + mem dictionary entries staged in LDS (else read via L1)
 struct UsageArgs {
   const void* __restrict__ st;
   StateFmt fmt;
@@ -1335,7 +1345,9 @@ struct UsageArgs {
   const uint32_t* __restrict__ ukey;
   const double* __restrict__ cpu_v;
   const double* __restrict__ mem_v;
-  uint32_t n_nodes;
+  uint32_t n_cpu, n_mem;
+  const uint4* __restrict__ chunks;  // {first pod, end pod, first node, end node}
+  uint32_t n_chunks;
   uint32_t n_pods;
   double* __restrict__ node_out;   // n_nodes x {cpu, mem, cpu_cum, mem_cum}
   double* __restrict__ cum;        // n_nodes x {cpu, mem}
@@ -1349,6 +1361,8 @@ struct UsageArgs {
   const uint32_t* __restrict__ ckeys;
   const uint32_t* __restrict__ mbase;  // per pod: its containers' first integrator in ccum (mixed pods)
   double* __restrict__ ccum;        // per container of a mixed pod: {cpu, mem} integrators
+  const double* __restrict__ podv;  // usage_fast_kernel: pod values per (containers, value id), see kwk_usage_config
+  uint32_t podv_n;                  // entries of podv
 };
 
 // a pod's usage_key: containers (bits 28..31) x one interned value each, or 0 containers =
@@ -1360,50 +1374,158 @@ __device__ __forceinline__ double dur_seconds(int64_t d) {
   return (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
 }
 
+// alive flag of pod j of a lane's run (kURun words of WB bytes in WB 16-byte chunks)
+template <uint32_t WB>
+__device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t abit) {
+  if constexpr (WB == 2) {
+    const uint4 c = sv[j >> 3];
+    const int d = (j >> 1) & 3;
+    const uint32_t w = d == 0 ? c.x : d == 1 ? c.y : d == 2 ? c.z : c.w;
+    return ((w >> (16 * (j & 1))) & abit) != 0;
+  } else if constexpr (WB == 4) {
+    const uint4 c = sv[j >> 2];
+    const int d = j & 3;
+    return ((d == 0 ? c.x : d == 1 ? c.y : d == 2 ? c.z : c.w) & abit) != 0;
+  } else {
+    const uint4 c = sv[j >> 1];
+    return (((j & 1) ? c.w : c.y) & abit) != 0;  // the sched word of {pred, sched}
+  }
+}
+
+// persistent grid: wave w takes chunks w, w + W, ... (W = waves in the grid); the next chunk's
+// descriptor and first row are requested before the current chunk is worked on, so each
+// wave keeps one chunk's loads in flight (one block per chunk paid 3 memory latencies per
+// chunk back to back: 236-255 us for 100M pods, r2c-r2e)
+template <uint32_t WB>
 __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
-  __shared__ double s_acc[kWavesPerBlock][kUG][2];
-  __shared__ uint32_t s_bnd[kWavesPerBlock][kUG + 1];
+  __shared__ uint32_t s_ptr[kWavesPerBlock][kUChunkNodes + 1];
+  __shared__ double2 s_sum[kWavesPerBlock][kUChunkNodes];  // node sums, each written once where the node closes
+  __shared__ double s_val[kULdsValues];
   __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t j0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kUG;
-  const uint32_t jn = j0 < a.n_nodes ? (uint32_t)min((uint64_t)kUG, a.n_nodes - j0) : 0u;
-  if (lane < kUG) { s_acc[wave][lane][0] = 0.0; s_acc[wave][lane][1] = 0.0; }
-  if (lane <= jn && jn) s_bnd[wave][lane] = a.node_ptr[j0 + lane];
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const uint32_t lo = jn ? s_bnd[wave][0] : 0u, hi = jn ? s_bnd[wave][jn] : 0u;
-  uint32_t nl = 0;  // the lane's current node within the group (pods only move forward)
-  for (uint32_t base = lo; base < hi; base += 64u * kUU) {
-    uint32_t sched[kUU], key[kUU];
+  const uint32_t n_waves = gridDim.x * kWavesPerBlock;
+  uint32_t chunk = blockIdx.x * kWavesPerBlock + wave;
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods * WB);
+  const __amdgpu_buffer_rsrc_t uk_rs = make_rsrc(a.ukey, a.n_pods * 4u);
+  // the next chunk: descriptor and first row in flight
+  uint4 nch = make_uint4(0u, 0u, 0u, 0u);
+  uint4 nsv[WB], nkv[4];
+  auto load_row = [&](uint4 (&dsv)[WB], uint4 (&dkv)[4], uint32_t r0, uint32_t c0, uint32_t c1) {
+    const uint32_t lf = r0 + lane * kURun;
+    const bool has = max(lf, c0) < min(lf + kURun, c1);
 #pragma unroll
-    for (int u = 0; u < kUU; ++u) {  // all loads of the batch first
-      const uint32_t p = base + (uint32_t)u * 64u + lane;
-      sched[u] = p < hi ? load_state(a.st, p, a.fmt).y : 0u;
-      key[u] = p < hi ? a.ukey[p] : 0u;
+    for (uint32_t q = 0; q < WB; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, has ? lf * WB + q * 16u : kOOB, 0, 0);
+      dsv[q] = make_uint4(c[0], c[1], c[2], c[3]);
     }
 #pragma unroll
-    for (int u = 0; u < kUU; ++u) {
-      const uint32_t p = base + (uint32_t)u * 64u + lane;
-      if (base + (uint32_t)u * 64u >= hi) break;  // wave-uniform
-      const bool valid = p < hi;
-      double vc = 0.0, vm = 0.0;
-      if (valid) {
-        while (nl + 1 < jn && p >= s_bnd[wave][nl + 1]) ++nl;
-        const bool alive = (sched[u] & KWK_F_ALIVE) != 0;
-        const uint32_t k = key[u], nc = k >> 28;
-        // podResourceUsage (:170-193) adds the containers in spec order, as below
-        double c1 = 0.0, m1 = 0.0;  // one container's value (uniform pods)
+    for (uint32_t q = 0; q < 4; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(uk_rs, has ? lf * 4u + q * 16u : kOOB, 0, 0);
+      dkv[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  if (chunk < a.n_chunks) {
+    nch = a.chunks[chunk];
+    load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+  }
+  const bool lds_vals = a.n_cpu + a.n_mem <= kULdsValues;
+  if (lds_vals) {
+    for (uint32_t j = threadIdx.x; j < a.n_cpu + a.n_mem; j += kBlock)
+      s_val[j] = j < a.n_cpu ? a.cpu_v[j] : a.mem_v[j - a.n_cpu];
+  }
+  __syncthreads();
+  const double* __restrict__ cpu_v = lds_vals ? s_val : a.cpu_v;
+  const double* __restrict__ mem_v = lds_vals ? s_val + a.n_cpu : a.mem_v;
+  // the alive flag in the raw word (packed: at fshift; wide: in sched)
+  const uint32_t abit = WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  double tot_c = 0.0, tot_m = 0.0;  // per lane: the nodes it finalised
+  uint32_t* __restrict__ sp = s_ptr[wave];
+  double2* __restrict__ ss = s_sum[wave];
+  for (; chunk < a.n_chunks; chunk += n_waves) {  // wave-uniform
+    const uint4 ch = nch;
+    const uint32_t c0 = ch.x, c1 = ch.y, na = ch.z, nk = ch.w - ch.z;  // pods [c0, c1), nodes na + [0, nk)
+    const uint32_t r_first = c0 & ~7u;
+    uint4 sv[WB], kv[4];
+#pragma unroll
+    for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) kv[q] = nkv[q];
+    const uint32_t nxt = chunk + n_waves;
+    if (nxt < a.n_chunks) nch = a.chunks[nxt];
+    // the first 64 nodes' integrators and the node boundaries
+    double2 pre_cum = make_double2(0.0, 0.0);
+    int64_t pre_last = INT64_MIN;
+    if (lane < nk) {
+      pre_cum = reinterpret_cast<const double2*>(a.cum)[na + lane];
+      pre_last = a.last_t[na + lane];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the previous chunk is done with sp / ss
+    for (uint32_t j = lane; j <= nk; j += 64) sp[j] = a.node_ptr[na + j];
+    if (nxt < a.n_chunks) load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // a node's sum is final where it closes (in LDS); the integrators and outputs are written
+    // after the rows, all lanes at once
+    auto finalize = [&](uint32_t k, double c, double m) { ss[k] = make_double2(c, m); };
+    if (c0 == c1) {  // nodes without pods
+      for (uint32_t k = lane; k < nk; k += 64) finalize(k, 0.0, 0.0);
+    }
+    double carry_c = 0.0, carry_m = 0.0;  // the open node's sum from earlier rows
+    uint32_t carry_k = 0xFFFFFFFFu;
+    for (uint32_t r0 = r_first; r0 < c1; r0 += kURow) {  // wave-uniform
+      if (r0 != r_first) load_row(sv, kv, r0, c0, c1);  // nodes larger than a row
+      const uint32_t lf = r0 + lane * kURun;
+      const uint32_t p_lo = max(lf, c0), p_hi = min(lf + kURun, c1);
+      const bool has = p_lo < p_hi;
+      // the node holding the lane's pod before its first (the chunk's first lane: node 0)
+      uint32_t k = 0;
+      if (has && p_lo > c0) {
+        uint32_t lo = 0, hi = nk;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sp[mid] <= p_lo - 1u) lo = mid; else hi = mid;
+        }
+        k = lo;
+      }
+      double acc_c = 0.0, acc_m = 0.0, head_c = 0.0, head_m = 0.0;
+      bool head = false;
+      uint32_t head_k = 0;
+      uint32_t bnd = sp[k + 1];  // end of node k
+      auto close = [&]() {
+        if (!head && sp[k] < p_lo) {  // started in an earlier lane: the head
+          head = true;
+          head_k = k;
+          head_c = acc_c;
+          head_m = acc_m;
+        } else {
+          finalize(k, acc_c, acc_m);
+        }
+        acc_c = 0.0;
+        acc_m = 0.0;
+        ++k;
+        bnd = k < nk ? sp[k + 1] : 0xFFFFFFFFu;
+      };
+#pragma unroll
+      for (int j = 0; j < (int)kURun; ++j) {
+        const uint32_t p = lf + (uint32_t)j;
+        if (p < p_lo || p >= p_hi) continue;
+        while (p >= bnd) close();
+        const uint4 kq = kv[j >> 2];
+        const uint32_t key = (j & 3) == 0 ? kq.x : (j & 3) == 1 ? kq.y : (j & 3) == 2 ? kq.z : kq.w;
+        const bool alive = run_alive<WB>(sv, j, abit);
+        const uint32_t nc = key >> 28;
+        double vc = 0.0, vm = 0.0, c1v = 0.0, m1v = 0.0;
         uint2 fc = make_uint2(0u, 0u);
         if (alive) {
           if (nc) {
-            c1 = a.cpu_v[k & 0x3FFFu];
-            m1 = a.mem_v[(k >> 14) & 0x3FFFu];
-            for (uint32_t j = 0; j < nc; ++j) { vc += c1; vm += m1; }
+            c1v = cpu_v[key & 0x3FFFu];
+            m1v = mem_v[(key >> 14) & 0x3FFFu];
+            for (uint32_t c = 0; c < nc; ++c) { vc += c1v; vm += m1v; }
           } else {
-            fc = a.mixed[k & kUKeyMixedIndex];
-            for (uint32_t j = 0; j < fc.y; ++j) {
-              const uint32_t ck = a.ckeys[fc.x + j];
-              vc += a.cpu_v[ck & 0x3FFFu];
-              vm += a.mem_v[(ck >> 14) & 0x3FFFu];
+            fc = a.mixed[key & kUKeyMixedIndex];
+            for (uint32_t c = 0; c < fc.y; ++c) {
+              const uint32_t ck = a.ckeys[fc.x + c];
+              vc += cpu_v[ck & 0x3FFFu];
+              vm += mem_v[(ck >> 14) & 0x3FFFu];
             }
           }
         }
@@ -1417,20 +1539,20 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
             if (nc) {  // equal containers share one integrator
               double2 unit = reinterpret_cast<double2*>(a.pod_cum)[p];
               if (lt != INT64_MIN) {
-                unit.x += dt * c1;
-                unit.y += dt * m1;
+                unit.x += dt * c1v;
+                unit.y += dt * m1v;
                 reinterpret_cast<double2*>(a.pod_cum)[p] = unit;
               }
-              for (uint32_t j = 0; j < nc; ++j) { cc += unit.x; cm += unit.y; }
+              for (uint32_t c = 0; c < nc; ++c) { cc += unit.x; cm += unit.y; }
             } else {
               const uint32_t mb = a.mbase[p];
-              for (uint32_t j = 0; j < fc.y; ++j) {
-                const uint32_t ck = a.ckeys[fc.x + j];
-                double2 cu = reinterpret_cast<double2*>(a.ccum)[mb + j];
+              for (uint32_t c = 0; c < fc.y; ++c) {
+                const uint32_t ck = a.ckeys[fc.x + c];
+                double2 cu = reinterpret_cast<double2*>(a.ccum)[mb + c];
                 if (lt != INT64_MIN) {
-                  cu.x += dt * a.cpu_v[ck & 0x3FFFu];
-                  cu.y += dt * a.mem_v[(ck >> 14) & 0x3FFFu];
-                  reinterpret_cast<double2*>(a.ccum)[mb + j] = cu;
+                  cu.x += dt * cpu_v[ck & 0x3FFFu];
+                  cu.y += dt * mem_v[(ck >> 14) & 0x3FFFu];
+                  reinterpret_cast<double2*>(a.ccum)[mb + c] = cu;
                 }
                 cc += cu.x;
                 cm += cu.y;
@@ -1442,44 +1564,227 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
             reinterpret_cast<double4*>(a.pod_out)[p] = make_double4(0.0, 0.0, 0.0, 0.0);
           }
         }
+        acc_c += vc;
+        acc_m += vm;
       }
-      // segmented inclusive scan over the lanes, keyed by node (contiguous segments)
-      const uint32_t seg = valid ? nl : 0xFFFFu;
+      // the chunk's last pod: close every node left (trailing nodes without pods too)
+      const bool last = has && p_hi == c1;
+      if (last)
+        while (k < nk) close();
+      // segmented inclusive scan of the open tails (keys ascend over the lanes with pods)
+      const uint32_t key = (has && !last) ? k : 0xFFFFFFFFu;
+      double sc = (has && !last) ? acc_c : 0.0, sm = (has && !last) ? acc_m : 0.0;
+      if (lane == 0 && key == carry_k) { sc += carry_c; sm += carry_m; }
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        const double uc = __shfl_up(vc, o), um = __shfl_up(vm, o);
-        const uint32_t us = __shfl_up(seg, o);
-        if (lane >= (uint32_t)o && us == seg) { vc += uc; vm += um; }
+        const double uc = __shfl_up(sc, o), um = __shfl_up(sm, o);
+        const uint32_t uk = __shfl_up(key, o);
+        if (lane >= (uint32_t)o && uk == key) { sc += uc; sm += um; }
       }
-      const uint32_t next = __shfl_down(seg, 1);
-      if (valid && (lane == 63 || next != seg)) {  // segment tail: one lane per node and pass
-        s_acc[wave][seg][0] += vc;
-        s_acc[wave][seg][1] += vm;
+      // the lane before a head ends with that node open: its scan value is the earlier share
+      double pc = __shfl_up(sc, 1), pm = __shfl_up(sm, 1);
+      if (lane == 0) { pc = carry_c; pm = carry_m; }
+      if (head) finalize(head_k, head_c + pc, head_m + pm);
+      carry_c = __shfl(sc, 63);
+      carry_m = __shfl(sm, 63);
+      carry_k = __shfl(key, 63);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // NodeResourceUsage (:195-224) and its integrator (nodeResourceCumulativeUsage, :67-109)
+    for (uint32_t k = lane; k < nk; k += 64) {
+      const double2 v = ss[k];
+      const uint64_t node = na + k;
+      double2 cm = k == lane ? pre_cum : reinterpret_cast<double2*>(a.cum)[node];
+      const int64_t lt = k == lane ? pre_last : a.last_t[node];
+      if (lt != INT64_MIN) {  // now.Sub(c.time).Seconds()
+        const double dt = dur_seconds(a.now - lt);
+        cm.x += dt * v.x;
+        cm.y += dt * v.y;
+        reinterpret_cast<double2*>(a.cum)[node] = cm;
       }
+      a.last_t[node] = a.now;
+      reinterpret_cast<double4*>(a.node_out)[node] = make_double4(v.x, v.y, cm.x, cm.y);
+      tot_c += v.x;
+      tot_m += v.y;
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  double c = 0.0, m = 0.0;
-  if (lane < jn) {
-    const uint64_t node = j0 + lane;
-    c = s_acc[wave][lane][0];
-    m = s_acc[wave][lane][1];
-    double2 cm = reinterpret_cast<double2*>(a.cum)[node];
-    const int64_t lt = a.last_t[node];
-    if (lt != INT64_MIN) {  // now.Sub(c.time).Seconds()
-      const double dt = dur_seconds(a.now - lt);
-      cm.x += dt * c;
-      cm.y += dt * m;
-      reinterpret_cast<double2*>(a.cum)[node] = cm;
-    }
-    a.last_t[node] = a.now;
-    reinterpret_cast<double4*>(a.node_out)[node] = make_double4(c, m, cm.x, cm.y);
   }
   for (int o = 32; o > 0; o >>= 1) {
-    c += __shfl_xor(c, o);
-    m += __shfl_xor(m, o);
+    tot_c += __shfl_xor(tot_c, o);
+    tot_m += __shfl_xor(tot_m, o);
   }
-  if (lane == 0) { s_c[wave] = c; s_m[wave] = m; }
+  if (lane == 0) { s_c[wave] = tot_c; s_m[wave] = tot_m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tc = 0, tm = 0;
+    for (int i = 0; i < kWavesPerBlock; ++i) { tc += s_c[i]; tm += s_m[i]; }
+    a.block_part[blockIdx.x * 2 + 0] = tc;
+    a.block_part[blockIdx.x * 2 + 1] = tm;
+  }
+}
+
+// The common configuration — every pod's containers evaluate alike (no mixed table) and no
+// per-pod outputs — takes usage_fast_kernel: the same chunks, lanes and scan, but a pod's value
+// is one LDS lookup in `podv` (containers x value, summed on the host in spec order exactly as
+// the device loop would), and a node boundary inside a lane is a short masked branch.  Empty
+// nodes are written separately, so closing a node never loops.
+constexpr uint32_t kUFastVals = 2048;  // podv entries staged in LDS
+template <uint32_t WB>
+__global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
+  __shared__ uint32_t s_ptr[kWavesPerBlock][kUChunkNodes + 1];
+  __shared__ double2 s_sum[kWavesPerBlock][kUChunkNodes];
+  __shared__ double s_pv[kUFastVals];
+  __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n_waves = gridDim.x * kWavesPerBlock;
+  uint32_t chunk = blockIdx.x * kWavesPerBlock + wave;
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods * WB);
+  const __amdgpu_buffer_rsrc_t uk_rs = make_rsrc(a.ukey, a.n_pods * 4u);
+  uint4 nch = make_uint4(0u, 0u, 0u, 0u);
+  uint4 nsv[WB], nkv[4];
+  auto load_row = [&](uint4 (&dsv)[WB], uint4 (&dkv)[4], uint32_t r0, uint32_t c0, uint32_t c1) {
+    const uint32_t lf = r0 + lane * kURun;
+    const bool has = max(lf, c0) < min(lf + kURun, c1);
+#pragma unroll
+    for (uint32_t q = 0; q < WB; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, has ? lf * WB + q * 16u : kOOB, 0, 0);
+      dsv[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(uk_rs, has ? lf * 4u + q * 16u : kOOB, 0, 0);
+      dkv[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  if (chunk < a.n_chunks) {
+    nch = a.chunks[chunk];
+    load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+  }
+  for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
+  __syncthreads();
+  const uint32_t nv = a.n_cpu + a.n_mem;  // podv row: cpu values then memory values
+  const uint32_t abit = WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  double tot_c = 0.0, tot_m = 0.0;
+  uint32_t* __restrict__ sp = s_ptr[wave];
+  double2* __restrict__ ss = s_sum[wave];
+  for (; chunk < a.n_chunks; chunk += n_waves) {  // wave-uniform
+    const uint4 ch = nch;
+    const uint32_t c0 = ch.x, c1 = ch.y, na = ch.z, nk = ch.w - ch.z;
+    const uint32_t r_first = c0 & ~7u;
+    uint4 sv[WB], kv[4];
+#pragma unroll
+    for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) kv[q] = nkv[q];
+    const uint32_t nxt = chunk + n_waves;
+    if (nxt < a.n_chunks) nch = a.chunks[nxt];
+    double2 pre_cum = make_double2(0.0, 0.0);
+    int64_t pre_last = INT64_MIN;
+    if (lane < nk) {
+      pre_cum = reinterpret_cast<const double2*>(a.cum)[na + lane];
+      pre_last = a.last_t[na + lane];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the previous chunk is done with sp / ss
+    for (uint32_t j = lane; j <= nk; j += 64) sp[j] = a.node_ptr[na + j];
+    if (nxt < a.n_chunks) load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t k = lane; k < nk; k += 64)  // nodes without pods
+      if (sp[k] == sp[k + 1]) ss[k] = make_double2(0.0, 0.0);
+    double carry_c = 0.0, carry_m = 0.0;
+    uint32_t carry_k = 0xFFFFFFFFu;
+    for (uint32_t r0 = r_first; r0 < c1; r0 += kURow) {  // wave-uniform
+      if (r0 != r_first) load_row(sv, kv, r0, c0, c1);
+      const uint32_t lf = r0 + lane * kURun;
+      const uint32_t p_lo = max(lf, c0), p_hi = min(lf + kURun, c1);
+      const bool has = p_lo < p_hi;
+      // the non-empty node holding the lane's first pod
+      uint32_t k = 0;
+      if (has) {
+        uint32_t lo = 0, hi = nk;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sp[mid] <= p_lo) lo = mid; else hi = mid;
+        }
+        k = lo;
+      }
+      // its start decides whether the lane's first segment is a head (continues earlier lanes)
+      const bool cont = has && sp[k] < p_lo;
+      bool head = false;
+      uint32_t head_k = 0;
+      double acc_c = 0.0, acc_m = 0.0, head_c = 0.0, head_m = 0.0;
+      uint32_t bnd = sp[k + 1];
+#pragma unroll
+      for (int j = 0; j < (int)kURun; ++j) {
+        const uint32_t p = lf + (uint32_t)j;
+        const bool in = p >= p_lo && p < p_hi;
+        if (in && p >= bnd) {  // node k ends before pod p: close it, move to the node holding p
+          if (cont && !head) {
+            head = true; head_k = k; head_c = acc_c; head_m = acc_m;
+          } else {
+            ss[k] = make_double2(acc_c, acc_m);
+          }
+          acc_c = 0.0;
+          acc_m = 0.0;
+          do { ++k; } while (sp[k + 1] <= p);  // past nodes without pods
+          bnd = sp[k + 1];
+        }
+        const uint4 kq = kv[j >> 2];
+        const uint32_t key = (j & 3) == 0 ? kq.x : (j & 3) == 1 ? kq.y : (j & 3) == 2 ? kq.z : kq.w;
+        const bool live = in && run_alive<WB>(sv, j, abit);
+        const uint32_t row = (key >> 28) * nv;
+        const double vc = s_pv[row + (key & 0x3FFFu)], vm = s_pv[row + a.n_cpu + ((key >> 14) & 0x3FFFu)];
+        acc_c += live ? vc : 0.0;
+        acc_m += live ? vm : 0.0;
+      }
+      // a node ending with the lane's last pod is closed here (the next lane starts a new
+      // node); so is the chunk's last node
+      const bool last = has && bnd == p_hi;
+      if (last) {
+        if (cont && !head) {
+          head = true; head_k = k; head_c = acc_c; head_m = acc_m;
+        } else {
+          ss[k] = make_double2(acc_c, acc_m);
+        }
+      }
+      const uint32_t key = (has && !last) ? k : 0xFFFFFFFFu;
+      // the open tail: a lane that closed nothing carries all its pods in it
+      double sc = (has && !last) ? acc_c : 0.0, sm = (has && !last) ? acc_m : 0.0;
+      if (lane == 0 && key == carry_k) { sc += carry_c; sm += carry_m; }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double uc = __shfl_up(sc, o), um = __shfl_up(sm, o);
+        const uint32_t uk = __shfl_up(key, o);
+        if (lane >= (uint32_t)o && uk == key) { sc += uc; sm += um; }
+      }
+      double pc = __shfl_up(sc, 1), pm = __shfl_up(sm, 1);
+      if (lane == 0) { pc = carry_c; pm = carry_m; }
+      if (head) ss[head_k] = make_double2(head_c + pc, head_m + pm);
+      carry_c = __shfl(sc, 63);
+      carry_m = __shfl(sm, 63);
+      carry_k = __shfl(key, 63);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t k = lane; k < nk; k += 64) {
+      const double2 v = ss[k];
+      const uint64_t node = na + k;
+      double2 cm = k == lane ? pre_cum : reinterpret_cast<double2*>(a.cum)[node];
+      const int64_t lt = k == lane ? pre_last : a.last_t[node];
+      if (lt != INT64_MIN) {
+        const double dt = dur_seconds(a.now - lt);
+        cm.x += dt * v.x;
+        cm.y += dt * v.y;
+        reinterpret_cast<double2*>(a.cum)[node] = cm;
+      }
+      a.last_t[node] = a.now;
+      reinterpret_cast<double4*>(a.node_out)[node] = make_double4(v.x, v.y, cm.x, cm.y);
+      tot_c += v.x;
+      tot_m += v.y;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    tot_c += __shfl_xor(tot_c, o);
+    tot_m += __shfl_xor(tot_m, o);
+  }
+  if (lane == 0) { s_c[wave] = tot_c; s_m[wave] = tot_m; }
   __syncthreads();
   if (threadIdx.x == 0) {
     double tc = 0, tm = 0;
@@ -1630,68 +1935,114 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
 
 // count alive objects with (pred & mask[k]) != 0 for each k (mask 0: every alive object):
 // phase histograms and other cluster aggregates.  Each lane streams 16-byte chunks of the
-// state column (8, 4 or 2 words), per-lane counters in registers, one 64-bit atomic per block
-// and mask.
+// state column (8, 4 or 2 words) and tests the raw words (pred bits, alive flag) against the
+// masks — only the n_masks masks asked for (a wave-uniform loop bound) — with per-lane
+// counters in registers, one 64-bit atomic per block and mask.
 constexpr int kMaxCountMasks = 16;
-__global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, StateFmt fmt, uint32_t n,
-                                                       const uint32_t* __restrict__ masks, uint32_t n_masks,
-                                                       unsigned long long* __restrict__ out) {
-  __shared__ unsigned int s_cnt[kMaxCountMasks];
-  __shared__ uint32_t s_masks[kMaxCountMasks];
-  if (threadIdx.x < kMaxCountMasks) {
-    s_cnt[threadIdx.x] = 0;
-    s_masks[threadIdx.x] = threadIdx.x < n_masks ? masks[threadIdx.x] : 0u;
+template <uint32_t WB, int NM>  // NM >= n_masks masks tested (compile time); the rest count nothing used
+__global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, uint32_t n, uint32_t abit,
+                                                       uint32_t pmask, const uint32_t* __restrict__ masks,
+                                                       uint32_t n_masks, uint32_t* __restrict__ part) {
+  __shared__ unsigned int s_cnt[NM];
+  if (threadIdx.x < NM) s_cnt[threadIdx.x] = 0;
+  uint32_t cnt[NM];
+  uint32_t mk[NM];  // wave-uniform: the mask's pred bits
+  bool every[NM];   // mask 0: every alive object
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    cnt[m] = 0;
+    const uint32_t x = (uint32_t)m < n_masks ? masks[m] : 0u;
+    mk[m] = x & pmask;
+    every[m] = x == 0u;
   }
   __syncthreads();
-  uint32_t cnt[kMaxCountMasks];
-  uint32_t mk[kMaxCountMasks];
-#pragma unroll
-  for (int m = 0; m < kMaxCountMasks; ++m) { cnt[m] = 0; mk[m] = s_masks[m]; }
-  const uint32_t wb = fmt.half ? 2u : fmt.narrow ? 4u : 8u;
-  const uint32_t wpc = 16u / wb;  // words per chunk
-  const uint64_t n_chunks = ((uint64_t)n * wb + 15u) / 16u;
+  constexpr uint32_t kWpc = 16u / WB;  // words per chunk
+  const uint64_t n_chunks = ((uint64_t)n * WB + 15u) / 16u;
   const uint4* __restrict__ q = reinterpret_cast<const uint4*>(st);
-  auto tally = [&](uint32_t pred, uint32_t sched) {
-    if (!(sched & KWK_F_ALIVE)) return;
+  auto tally = [&](uint32_t pred, uint32_t flags, bool in) {
+    const uint32_t al = (in && (flags & abit)) ? 1u : 0u;
 #pragma unroll
-    for (int m = 0; m < kMaxCountMasks; ++m)
-      cnt[m] += ((uint32_t)m < n_masks && (mk[m] == 0u || (pred & mk[m]) != 0u)) ? 1u : 0u;
+    for (int m = 0; m < NM; ++m) cnt[m] += (every[m] || (pred & mk[m]) != 0u) ? al : 0u;
   };
-  for (uint64_t ch = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ch < n_chunks; ch += (uint64_t)gridDim.x * kBlock) {
-    const uint4 v = q[ch];
+  auto tally_chunk = [&](const uint4 v, uint64_t c) {
     const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-    const uint64_t i0 = ch * wpc;
-    if (fmt.half) {
+    const uint64_t i0 = c * kWpc;
+    const uint32_t lim = i0 + kWpc <= n ? kWpc : (uint32_t)(n - i0);  // words of the chunk below n
+    if constexpr (WB == 2) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (i0 + j < n) {
-          const uint2 u = fmt_unpack((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, fmt);
-          tally(u.x, u.y);
-        }
+        const uint32_t w = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        tally(w, w, (uint32_t)j < lim);
       }
-    } else if (fmt.narrow) {
+    } else if constexpr (WB == 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (i0 + j < n) {
-          const uint2 u = fmt_unpack(dw[j], fmt);
-          tally(u.x, u.y);
-        }
-      }
+      for (int j = 0; j < 4; ++j) tally(dw[j], dw[j], (uint32_t)j < lim);
     } else {
-      tally(v.x, v.y);
-      if (i0 + 1 < n) tally(v.z, v.w);
+      tally(v.x, v.y, true);
+      tally(v.z, v.w, lim > 1);
     }
+  };
+  // kCountU chunks per lane in flight together, kBlock chunks apart (coalesced)
+  constexpr uint32_t kCountU = 4;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock * kCountU + threadIdx.x; c0 < n_chunks;
+       c0 += (uint64_t)gridDim.x * kBlock * kCountU) {
+    uint4 vs[kCountU];
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u) {
+      const uint64_t c = c0 + u * kBlock;
+      vs[u] = c < n_chunks ? q[c] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u)
+      if (c0 + u * kBlock < n_chunks) tally_chunk(vs[u], c0 + u * kBlock);
   }
 #pragma unroll
-  for (int m = 0; m < kMaxCountMasks; ++m) {
-    if ((uint32_t)m < n_masks) {  // wave-uniform
-      uint32_t c = cnt[m];
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
-    }
+  for (int m = 0; m < NM; ++m) {
+    uint32_t c = cnt[m];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
   }
   __syncthreads();
-  if (threadIdx.x < n_masks && s_cnt[threadIdx.x]) atomicAdd(&out[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+  // one row of partial counts per block (same-address atomics from thousands of blocks
+  // serialise at the L2: 111 us for a 100M-object count, r2d); count_total_kernel sums them
+  if (threadIdx.x < kMaxCountMasks)
+    part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < (uint32_t)NM ? s_cnt[threadIdx.x] : 0u;
+}
+
+// out[m] = sum over the blocks' partial rows (1024 threads: 16 masks x 64 block strides)
+__global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
+                                                           uint32_t n_masks, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s[1024];
+  const uint32_t m = threadIdx.x & (kMaxCountMasks - 1), r = threadIdx.x / kMaxCountMasks;
+  unsigned long long c = 0;
+  for (uint32_t b = r; b < n_blocks; b += 1024 / kMaxCountMasks) c += part[(uint64_t)b * kMaxCountMasks + m];
+  s[threadIdx.x] = c;
+  __syncthreads();
+  for (uint32_t h = 512; h >= kMaxCountMasks; h >>= 1) {
+    if (threadIdx.x < h) s[threadIdx.x] += s[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x < n_masks) out[threadIdx.x] = s[threadIdx.x];
+}
+
+template <uint32_t WB>
+static void launch_count(uint32_t n_masks, dim3 g, hipStream_t s, const void* st, uint32_t n, uint32_t abit,
+                         uint32_t pmask, const uint32_t* masks, uint32_t* part, unsigned long long* out) {
+  if (n_masks <= 2) hipLaunchKernelGGL((count_kernel<WB, 2>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  else if (n_masks <= 4) hipLaunchKernelGGL((count_kernel<WB, 4>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  else if (n_masks <= 8) hipLaunchKernelGGL((count_kernel<WB, 8>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  else hipLaunchKernelGGL((count_kernel<WB, 16>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
+}
+
+// kwk_aggregate's output: per-stage transitions, mask counts, cluster usage as float64
+__global__ void agg_pack_kernel(const unsigned long long* __restrict__ stats, uint32_t n_stages,
+                                const unsigned long long* __restrict__ counts, uint32_t n_masks,
+                                const double* __restrict__ cluster, uint32_t usage, double* __restrict__ out) {
+  const uint32_t t = threadIdx.x;
+  if (t < n_stages) out[t] = (double)stats[3 + t];
+  else if (t < n_stages + n_masks) out[t] = (double)counts[t - n_stages];
+  else if (usage && t < n_stages + n_masks + 2) out[t] = cluster[t - n_stages - n_masks];
 }
 
 // ------------------------------------------------------------------ node leases
@@ -1917,6 +2268,7 @@ struct kwk_engine {
   kwk_fired_rec* d_compact = nullptr;
   uint32_t* d_wave_counts = nullptr;
   uint32_t* d_wave_offsets = nullptr;
+  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
   unsigned long long* d_cum = nullptr;
   unsigned long long* d_stats = nullptr;
   uint64_t steps = 0;
@@ -1935,6 +2287,14 @@ struct kwk_engine {
   int64_t* d_pod_last = nullptr;
   double* d_usage_part = nullptr;
   double* d_cluster = nullptr;
+  double* d_agg = nullptr;        // kwk_aggregate's own output buffer
+  uint32_t* d_count_part = nullptr;  // count_kernel's per-block partial counts
+  unsigned long long* d_agg_counts = nullptr;
+  uint32_t* d_agg_masks = nullptr;
+  double* d_podv = nullptr;       // usage_fast_kernel's pod values per (containers, value id)
+  uint32_t podv_n = 0;
+  uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
+  uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)
   std::vector<uint32_t> h_node_ptr, h_ukey, h_mixed, h_ckeys, h_cptr;
   std::vector<double> h_cpu, h_mem;
@@ -2105,6 +2465,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
+  ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -2126,9 +2487,9 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_cum, e->d_stats,
+                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
-                  e->d_usage_part, e->d_cluster, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
+                  e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
                   e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
                   e->d_lease_nops, e->d_lease_stats};
@@ -2586,12 +2947,13 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   e->compacted = true;
   if (n_waves == 0) return KWK_OK;
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_wave_counts, n_waves,
-                     e->d_wave_offsets);
+  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
+                     e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
   CompactArgs a;
   a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
   a.counts = e->d_wave_counts;
   a.offsets = e->d_wave_offsets;
+  a.group_tot = e->d_seg_groups;
   a.out = e->d_compact;
   a.n_segs = n_waves;
   a.seg_region_shift = e->last_region_shift;
@@ -2705,9 +3067,50 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
-                  e->d_usage_part, e->d_cluster};
+                  e->d_usage_part, e->d_cluster, e->d_uchunk};
   for (void* p : olds) if (p) hipFree(p);
-  const uint32_t ublocks = (n_nodes + kWavesPerBlock * kUG - 1) / (kWavesPerBlock * kUG);
+  // usage_kernel's chunks: whole nodes, at most kUChunkPods pods (one wave row) and kUChunkNodes
+  // nodes each; a node with more pods than a row gets a chunk of its own (the wave carries its
+  // sum from row to row)
+  std::vector<uint4> chunks;
+  for (uint32_t n = 0; n < n_nodes;) {
+    const uint32_t c0 = node_ptr[n];
+    uint32_t nb = n + 1;
+    while (nb < n_nodes && nb - n < kUChunkNodes && node_ptr[nb + 1] - c0 <= kUChunkPods) ++nb;
+    chunks.push_back(make_uint4(c0, node_ptr[nb], n, nb));
+    n = nb;
+  }
+  const uint32_t ublocks = ((uint32_t)chunks.size() + kWavesPerBlock - 1) / kWavesPerBlock;
+  HIP_TRY(hipMalloc(&e->d_uchunk, sizeof(uint4) * (chunks.size() + 1)));
+  if (!chunks.empty())
+    HIP_TRY(hipMemcpy(e->d_uchunk, chunks.data(), sizeof(uint4) * chunks.size(), hipMemcpyHostToDevice));
+  e->n_uchunks = (uint32_t)chunks.size();
+  // usage_fast_kernel's table: row nc = the value of a pod with nc alike containers, summed
+  // container by container (podResourceUsage's order, :170-193) — what usage_kernel's loop adds
+  uint32_t max_nc = 0;
+  for (uint32_t p = 0; p < n_pods; ++p) max_nc = (ukey[p] >> 28) > max_nc ? (ukey[p] >> 28) : max_nc;
+  if (e->d_podv) HIP_TRY(hipFree(e->d_podv));
+  e->d_podv = nullptr;
+  e->podv_n = 0;
+  const size_t nv = (size_t)n_cpu + n_mem;
+  if ((max_nc + 1) * nv <= kUFastVals) {
+    std::vector<double> podv((max_nc + 1) * nv, 0.0);
+    for (uint32_t nc = 1; nc <= max_nc; ++nc) {
+      for (uint32_t i = 0; i < n_cpu; ++i) {
+        double v = 0.0;
+        for (uint32_t c = 0; c < nc; ++c) v += cpu_values[i];
+        podv[nc * nv + i] = v;
+      }
+      for (uint32_t i = 0; i < n_mem; ++i) {
+        double v = 0.0;
+        for (uint32_t c = 0; c < nc; ++c) v += mem_values[i];
+        podv[nc * nv + n_cpu + i] = v;
+      }
+    }
+    HIP_TRY(hipMalloc(&e->d_podv, sizeof(double) * podv.size()));
+    HIP_TRY(hipMemcpy(e->d_podv, podv.data(), sizeof(double) * podv.size(), hipMemcpyHostToDevice));
+    e->podv_n = (uint32_t)podv.size();
+  }
   HIP_TRY(hipMalloc(&e->d_node_ptr, 4 * ((size_t)n_nodes + 1)));
   HIP_TRY(hipMalloc(&e->d_ukey, 4 * ((size_t)n_pods + 1)));
   HIP_TRY(hipMalloc(&e->d_cpu, 8 * (size_t)n_cpu));
@@ -2998,14 +3401,37 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
-  const uint32_t ublocks = (e->n_nodes + kWavesPerBlock * kUG - 1) / (kWavesPerBlock * kUG);
+  const uint32_t ublocks = (e->n_uchunks + kWavesPerBlock - 1) / kWavesPerBlock;
   if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
-  UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->n_nodes, e->n_usage_pods, e->d_node_out,
-               e->d_node_cum, e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
-               e->d_mixed, e->d_ckeys, e->d_mbase, e->d_ccum};
-  hipLaunchKernelGGL(usage_kernel, dim3(ublocks), dim3(kBlock), 0, e->stream, ua);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, ublocks, e->d_cluster);
+  UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, (uint32_t)e->h_cpu.size(),
+               (uint32_t)e->h_mem.size(), e->d_uchunk, e->n_uchunks, e->n_usage_pods, e->d_node_out, e->d_node_cum,
+               e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last, e->d_mixed,
+               e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n};
+  const uint32_t wb = word_bytes(e->fmt);
+  if (!e->has_mixed_keys && !e->d_pod_out && e->podv_n) {  // usage_fast_kernel
+    const void* fk = wb == 2 ? (const void*)usage_fast_kernel<2> : wb == 4 ? (const void*)usage_fast_kernel<4>
+                                                                           : (const void*)usage_fast_kernel<8>;
+    const uint32_t grid = persist_grid(e, fk, ublocks);
+    if (grid) {
+      if (wb == 2) hipLaunchKernelGGL(usage_fast_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      else if (wb == 4) hipLaunchKernelGGL(usage_fast_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      else hipLaunchKernelGGL(usage_fast_kernel<8>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
+  // persistent grid (every block slot the occupancy allows), at most one chunk per wave
+  const void* kern = wb == 2 ? (const void*)usage_kernel<2> : wb == 4 ? (const void*)usage_kernel<4> : (const void*)usage_kernel<8>;
+  const uint32_t grid = persist_grid(e, kern, ublocks);
+  if (grid) {
+    if (wb == 2) hipLaunchKernelGGL(usage_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+    else if (wb == 4) hipLaunchKernelGGL(usage_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+    else hipLaunchKernelGGL(usage_kernel<8>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
@@ -3051,6 +3477,13 @@ kwk_status kwk_usage_read(kwk_engine* e, double* node_out, double* cluster_out) 
   return KWK_OK;
 }
 
+// count_kernel's partial rows: at most n_cus * 32 blocks
+static kwk_status ensure_count_part(kwk_engine* e) {
+  if (!e->d_count_part)
+    HIP_TRY(hipMalloc(&e->d_count_part, sizeof(uint32_t) * kMaxCountMasks * ((size_t)e->n_cus * 32u + 1)));
+  return KWK_OK;
+}
+
 kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uint64_t* counts) {
   if (!e || (n_masks && (!masks || !counts))) return fail(KWK_EINVAL, "null argument");
   if (n_masks > kMaxCountMasks) return fail(KWK_EINVAL, "at most 16 masks");
@@ -3062,15 +3495,76 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
   HIP_TRY(hipMemcpyAsync(d_masks, masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemsetAsync(d_out, 0, 8 * kMaxCountMasks, e->stream));
   if (e->n_active) {
-    const uint64_t chunks = ((uint64_t)e->n_active * word_bytes(e->fmt) + 15u) / 16u;
-    uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);  // ~4 chunks per lane
+    const uint32_t wb = (uint32_t)word_bytes(e->fmt);
+    const uint64_t chunks = ((uint64_t)e->n_active * wb + 15u) / 16u;
+    uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);  // 4 chunks per lane, loaded together
     blocks = blocks < (uint64_t)e->n_cus * 8u ? blocks : (uint64_t)e->n_cus * 8u;
-    hipLaunchKernelGGL(count_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, e->stream, e->d_st, e->fmt, e->n_active,
-                       d_masks, n_masks, d_out);
+    // the alive flag and the pred bits in the raw word (packed: flags at fshift; wide: {pred, sched})
+    const uint32_t abit = wb == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
+    const uint32_t pmask = wb == 8 ? 0xFFFFFFFFu : e->fmt.pmask;
+    const dim3 g((uint32_t)blocks);
+    if (kwk_status st = ensure_count_part(e)) return st;
+    if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
+    else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
+    else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(counts, d_out, 8 * (size_t)n_masks, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, int64_t now_ns, uint32_t flags,
+                         double* out, uint32_t* n_out) {
+  if (!e || !n_out || (n_masks && !masks)) return fail(KWK_EINVAL, "null argument");
+  if (n_masks > kMaxCountMasks) return fail(KWK_EINVAL, "at most 16 masks");
+  const bool usage = (flags & KWK_AGG_USAGE) != 0;
+  if (usage && !e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  const uint32_t n_stages = e->loaded_table ? e->n_stages : 0u;
+  if (!e->d_agg) {
+    HIP_TRY(hipMalloc(&e->d_agg, sizeof(double) * (KWK_MAX_STAGES + kMaxCountMasks + 2)));
+    HIP_TRY(hipMalloc(&e->d_agg_counts, sizeof(unsigned long long) * kMaxCountMasks));
+    HIP_TRY(hipMalloc(&e->d_agg_masks, sizeof(uint32_t) * kMaxCountMasks));
+  }
+  double* dst = out ? out : e->d_agg;
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->cum_rows, e->d_stats);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
+  if (n_masks) {
+    HIP_TRY(hipMemcpyAsync(e->d_agg_masks, masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
+    if (e->n_active) {
+      const uint32_t wb = (uint32_t)word_bytes(e->fmt);
+      const uint64_t chunks = ((uint64_t)e->n_active * wb + 15u) / 16u;
+      uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);
+      blocks = blocks < (uint64_t)e->n_cus * 8u ? blocks : (uint64_t)e->n_cus * 8u;
+      const uint32_t abit = wb == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
+      const uint32_t pmask = wb == 8 ? 0xFFFFFFFFu : e->fmt.pmask;
+      const dim3 g((uint32_t)blocks);
+      if (kwk_status st = ensure_count_part(e)) return st;
+      uint32_t* pp = e->d_count_part;
+      if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
+      else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
+      else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  if (usage)
+    if (kwk_status st = kwk_usage(e, now_ns)) return st;
+  hipLaunchKernelGGL(agg_pack_kernel, dim3(1), dim3(64), 0, e->stream, e->d_stats, n_stages, e->d_agg_counts, n_masks,
+                     e->d_cluster, usage ? 1u : 0u, dst);
+  HIP_TRY(hipGetLastError());
+  *n_out = n_stages + n_masks + (usage ? 2u : 0u);
+  return KWK_OK;
+}
+
+kwk_status kwk_aggregate_read(kwk_engine* e, double* host_out, uint32_t n) {
+  if (!e || (n && !host_out)) return fail(KWK_EINVAL, "null argument");
+  if (n > KWK_MAX_STAGES + kMaxCountMasks + 2) return fail(KWK_EINVAL, "more doubles than kwk_aggregate writes");
+  if (!e->d_agg) return fail(KWK_ESTATE, "kwk_aggregate must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (n) HIP_TRY(hipMemcpy(host_out, e->d_agg, sizeof(double) * n, hipMemcpyDeviceToHost));
   return KWK_OK;
 }
 

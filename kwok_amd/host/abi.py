@@ -143,8 +143,9 @@ EXPORTS = [
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
     "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
-    "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval",
+    "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
 ]
+AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
 
 _lib = None
 
@@ -205,6 +206,8 @@ def lib():
     L.kwk_event_record.argtypes = [C.c_void_p, C.c_uint32]
     L.kwk_event_elapsed.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, _p(C.c_float)]
     L.kwk_count.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.kwk_aggregate.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, _p(C.c_uint32)]
+    L.kwk_aggregate_read.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
     L.kwk_lease_config.argtypes = [C.c_void_p, _p(LeaseParams)]
     L.kwk_lease_set.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_lease_step.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]

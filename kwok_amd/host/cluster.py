@@ -94,3 +94,54 @@ def engine_aggregates(engines, count_masks, count_names, now_ns: int = None, usa
         _, usage = usage_engine.usage_read(node_out=False)
     return Aggregates(names, np.asarray(fired, dtype=np.int64), np.asarray(counts, dtype=np.int64), cnames,
                       np.asarray(usage, dtype=np.float64))
+
+
+class DeviceReport:
+    """A reporting interval's aggregates computed on the device (kwk_aggregate) with no host
+    round trip: per engine [transitions per stage | counts per mask | cluster usage] as float64,
+    laid out back to back — in one torch device buffer all-reduced in place over RCCL when the
+    job has several ranks, else in each engine's own buffer.  `collect` only enqueues (plus, with
+    several ranks, one wait for the engines' streams before the collective); `result` reads the
+    last interval back."""
+
+    def __init__(self, engines, count_masks, count_names, usage_engine=None, dist=None, device=None):
+        self.engines, self.masks, self.count_names, self.usage_engine = engines, count_masks, count_names, usage_engine
+        self.dist = dist if dist is not None and dist.is_initialized() and dist.get_world_size() > 1 else None
+        self.sizes = [len(e.p.names) + len(m) + (2 if e is usage_engine else 0) for e, m in zip(engines, count_masks)]
+        self.buf = None
+        if self.dist is not None:
+            import torch
+            self.buf = torch.zeros(sum(self.sizes), dtype=torch.float64, device=device)
+        self.collected = False
+
+    def collect(self, now_ns: int):
+        off = 0
+        for e, m, size in zip(self.engines, self.masks, self.sizes):
+            ptr = None if self.buf is None else self.buf.data_ptr() + 8 * off
+            n = e.aggregate(m, now_ns, usage=e is self.usage_engine, out_ptr=ptr)
+            assert n == size, (n, size)
+            off += size
+        if self.buf is not None:
+            for e in self.engines:
+                e.sync()
+            self.dist.all_reduce(self.buf)  # RCCL over xGMI
+        self.collected = True
+
+    def result(self) -> Aggregates:
+        if not self.collected:
+            raise RuntimeError("DeviceReport.result before collect")
+        if self.buf is not None:
+            flat = self.buf.cpu().numpy()
+        else:
+            flat = np.concatenate([e.aggregate_read(size) for e, size in zip(self.engines, self.sizes)])
+        names, fired, counts, cnames, usage, off = [], [], [], [], np.zeros(2), 0
+        for e, m, mn, size in zip(self.engines, self.masks, self.count_names, self.sizes):
+            ns = len(e.p.names)
+            names += list(e.p.names)
+            fired += flat[off:off + ns].tolist()
+            counts += flat[off + ns:off + ns + len(m)].tolist()
+            cnames += list(mn)
+            if e is self.usage_engine:
+                usage = flat[off + ns + len(m):off + size].copy()
+            off += size
+        return Aggregates(names, np.rint(fired).astype(np.int64), np.rint(counts).astype(np.int64), cnames, usage)

@@ -279,6 +279,23 @@ class Engine:
         abi.check(abi.lib().kwk_count(self.h, len(m), abi.ptr(m), abi.ptr(out)), "kwk_count")
         return out
 
+    def aggregate(self, masks, now_ns: int = 0, usage: bool = False, out_ptr: Optional[int] = None) -> int:
+        """kwk_aggregate: per-stage transitions, kwk_count of `masks` and (usage) the cluster usage
+        at now_ns, written as float64 on the device — into `out_ptr` (device memory, e.g. an RCCL
+        buffer) or the engine's own buffer (aggregate_read).  Enqueue only; returns the count."""
+        m = np.ascontiguousarray(masks, dtype=np.uint32)
+        self._agg_masks = m  # kept alive until the stream has copied it
+        n = C.c_uint32()
+        abi.check(abi.lib().kwk_aggregate(self.h, len(m), abi.ptr(m) if len(m) else None, now_ns,
+                                          abi.AGG_USAGE if usage else 0, out_ptr, C.byref(n)), "kwk_aggregate")
+        return n.value
+
+    def aggregate_read(self, n: int) -> np.ndarray:
+        """The engine-owned aggregate buffer (synchronises)."""
+        out = np.zeros(n, dtype=np.float64)
+        abi.check(abi.lib().kwk_aggregate_read(self.h, abi.ptr(out), n), "kwk_aggregate_read")
+        return out
+
     # usage
     def usage_config(self, node_ptr, usage_key, cpu_values, mem_values, mixed=None, ckeys=None):
         """kwk_usage_config (+ kwk_usage_mixed when some pod's containers differ): the columns

@@ -9,7 +9,7 @@ import pytest
 import yaml
 
 from kwok_amd import workload as W
-from kwok_amd.host.cluster import Aggregates, engine_aggregates, local_node_ptr, node_block, phase_masks, pod_range
+from kwok_amd.host.cluster import Aggregates, DeviceReport, engine_aggregates, local_node_ptr, node_block, phase_masks, pod_range
 from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "metrics", "usage-from-annotation.yaml")
@@ -64,6 +64,15 @@ def test_shard_engine_aggregates_equal_whole_engine_and_oracle():
                 continue
             a_whole = engine_aggregates([whole], masks, names, now, usage_engine=whole)
             parts = [engine_aggregates([e], masks, names, now, usage_engine=e) for e in shards]
+            # the device path the bench's reporter takes (kwk_aggregate, no host round trip)
+            dev = [DeviceReport([e], masks, names, usage_engine=e) for e in shards]
+            for d in dev:
+                d.collect(now)
+            d_parts = [d.result() for d in dev]
+            for p_host, p_dev in zip(parts, d_parts):
+                assert p_dev.fired_per_stage.tolist() == p_host.fired_per_stage.tolist(), f"step {k}"
+                assert p_dev.counts.tolist() == p_host.counts.tolist(), f"step {k}"
+                np.testing.assert_allclose(p_dev.usage, p_host.usage, rtol=1e-12, err_msg=f"step {k}")
             a_sum = a_whole.unpack(np.sum([p.pack() for p in parts], axis=0))  # what the all-reduce computes
             o_fired, o_counts, o_usage = oracle_aggregates(sim, docs, fired)
             for a in (a_whole, a_sum):

@@ -177,3 +177,110 @@ def test_oracle_cumulative_integrator():
     p = max(pods, key=lambda q: len(q["spec"]["containers"]))
     assert c.pod(docs, p, "cpu", 0) == 0.0
     assert c.pod(docs, p, "cpu", 2 * 10**9) == pytest.approx(2 * usage_ref.pod_usage(docs, p, "cpu"))
+
+
+def _irregular_node_ptr(n_pods):
+    """Node sizes the chunking must get right: empty nodes (first, inner, trailing), 1-pod nodes
+    (more of them than one chunk holds), a node larger than a wave row (its sum carried from row
+    to row), chunk-sized runs, and an odd first pod of a chunk."""
+    sizes = [0, 1, 2500, 0, 0] + [1] * 300 + [7, 0, 1016, 1017, 3]
+    rest = n_pods - sum(sizes)
+    assert rest > 0
+    while rest > 0:
+        sizes.append(min(37, rest))
+        rest -= sizes[-1]
+    sizes += [0, 0]
+    return np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_gpu_usage_irregular_nodes(state):
+    """usage_kernel's chunks of whole nodes (kwk_usage_config) against the oracle's
+    nodeResourceUsage, per node and in total, for the 2-, 4- and 8-byte state formats, with
+    per-pod outputs on."""
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+
+    cl, pods = _cluster(n_nodes=40, n_pods=6000, seed=17)
+    ptr = _irregular_node_ptr(len(pods))
+    prog = _program()
+    keys, cv, mv, mx, ck = usage_columns(prog, pods)
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    cols = ing.columns(pods)
+    eng = Engine(kp, capacity=len(pods), state=state)
+    try:
+        eng.load_stages()
+        eng.load(*cols, ing.record_array())
+        eng.usage_config(ptr, keys, cv, mv, mx, ck)
+        eng.usage_pods(True)
+        gone = np.arange(3, len(pods), 11)
+        eng.delete(gone)
+        alive = np.ones(len(pods), dtype=bool)
+        alive[gone] = False
+        docs = _docs()
+        t0 = 1_700_000_000 * 10**9
+        eng.usage(t0)
+        eng.usage(t0 + 2 * 10**9)
+        node, total = eng.usage_read()
+        want = np.zeros((len(ptr) - 1, 2))
+        for j in range(len(ptr) - 1):
+            pn = [pods[k] for k in range(ptr[j], ptr[j + 1]) if alive[k]]
+            want[j] = (usage_ref.node_usage(docs, pn, "cpu"), usage_ref.node_usage(docs, pn, "memory"))
+        np.testing.assert_allclose(node[:, :2], want, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(node[:, 2:], 2.0 * want, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
+        per_pod = eng.usage_read_pods()
+        np.testing.assert_allclose(per_pod[~alive], 0.0)
+        want_pod = [usage_ref.pod_usage(docs, p, "cpu") for p, a in zip(pods, alive) if a]
+        np.testing.assert_allclose(per_pod[alive, 0], want_pod, rtol=REL_TOL, atol=0)
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_gpu_usage_fast_path_irregular_nodes(state):
+    """The uniform-container configuration (no mixed pods, no per-pod outputs) takes
+    usage_fast_kernel: same irregular node layout, node sums and integrators vs the oracle."""
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+
+    cl, pods = _cluster(n_nodes=40, n_pods=6000, seed=23)
+    ptr = _irregular_node_ptr(len(pods))
+    text = open(GOLDEN).read()
+    prog = UsageProgram(*load_usage_yaml(text))
+    docs = [d for d in yaml.safe_load_all(text) if d]
+    keys, cv, mv, mx, ck = usage_columns(prog, pods)
+    assert mx is None or len(mx) == 0  # every pod's containers alike: the fast kernel's case
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    cols = ing.columns(pods)
+    eng = Engine(kp, capacity=len(pods), state=state)
+    try:
+        eng.load_stages()
+        eng.load(*cols, ing.record_array())
+        eng.usage_config(ptr, keys, cv, mv, mx, ck)
+        gone = np.arange(5, len(pods), 13)
+        eng.delete(gone)
+        alive = np.ones(len(pods), dtype=bool)
+        alive[gone] = False
+        t0 = 1_700_000_000 * 10**9
+        eng.usage(t0)
+        eng.usage(t0 + 3 * 10**9)
+        node, total = eng.usage_read()
+        want = np.zeros((len(ptr) - 1, 2))
+        for j in range(len(ptr) - 1):
+            pn = [pods[k] for k in range(ptr[j], ptr[j + 1]) if alive[k]]
+            want[j] = (usage_ref.node_usage(docs, pn, "cpu"), usage_ref.node_usage(docs, pn, "memory"))
+        np.testing.assert_allclose(node[:, :2], want, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(node[:, 2:], 3.0 * want, rtol=REL_TOL, atol=0)
+        np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
+        assert want[:, 0].min() == 0.0 and want[:, 0].max() > 0  # empty nodes and busy ones
+    finally:
+        eng.close()
