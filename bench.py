@@ -359,6 +359,7 @@ def main():
     ap.add_argument("--pcie-steps", type=int, default=5)
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     args = ap.parse_args()
 
     if args.config != "C5":
@@ -378,6 +379,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:  # ranks beyond the visible GPUs share them (a rehearsal with --dist-backend gloo)
+        import torch
+        local_rank %= max(1, torch.cuda.device_count())
     weak = args.scaling == "weak"
     if args.hbm_only:
         from kwok_amd import build as kbuild
@@ -397,7 +401,7 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
 
     from kwok_amd import build as kbuild
     if rank == 0 and not os.path.exists(kbuild.OUT):

@@ -1946,14 +1946,14 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
   __shared__ unsigned int s_cnt[NM];
   if (threadIdx.x < NM) s_cnt[threadIdx.x] = 0;
   uint32_t cnt[NM];
-  uint32_t mk[NM];  // wave-uniform: the mask's pred bits
-  bool every[NM];   // mask 0: every alive object
+  uint32_t mk[NM];     // wave-uniform: the mask's pred bits
+  uint32_t every[NM];  // 1: mask 0 = every alive object
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     cnt[m] = 0;
     const uint32_t x = (uint32_t)m < n_masks ? masks[m] : 0u;
     mk[m] = x & pmask;
-    every[m] = x == 0u;
+    every[m] = x == 0u ? 1u : 0u;
   }
   __syncthreads();
   constexpr uint32_t kWpc = 16u / WB;  // words per chunk
@@ -1962,7 +1962,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
   auto tally = [&](uint32_t pred, uint32_t flags, bool in) {
     const uint32_t al = (in && (flags & abit)) ? 1u : 0u;
 #pragma unroll
-    for (int m = 0; m < NM; ++m) cnt[m] += (every[m] || (pred & mk[m]) != 0u) ? al : 0u;
+    for (int m = 0; m < NM; ++m) cnt[m] += (((pred & mk[m]) != 0u ? 1u : 0u) | every[m]) & al;
   };
   auto tally_chunk = [&](const uint4 v, uint64_t c) {
     const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
