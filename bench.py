@@ -359,6 +359,7 @@ def main():
     ap.add_argument("--pcie-steps", type=int, default=5)
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
+    ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     args = ap.parse_args()
 
@@ -417,6 +418,9 @@ def main():
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
+    if args.tune_q16:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_Q16, args.tune_q16)
     dt = args.dt_ms * 10**6
     reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None)
     report_every = 0 if args.pmc_child else args.report_every

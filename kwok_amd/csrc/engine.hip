@@ -2293,6 +2293,7 @@ struct kwk_engine {
   uint32_t* d_agg_masks = nullptr;
   double* d_podv = nullptr;       // usage_fast_kernel's pod values per (containers, value id)
   uint32_t podv_n = 0;
+  uint32_t usage_blocks = 0;      // KWK_TUNE_USAGE_BLOCKS (0: occupancy API)
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)
@@ -2602,6 +2603,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_PERSIST16:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_PERSIST16: 0 or 1");
       e->persist16 = value != 0;
+      return KWK_OK;
+    case KWK_TUNE_USAGE_BLOCKS:
+      if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
+      e->usage_blocks = value;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -3411,7 +3416,8 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   if (!e->has_mixed_keys && !e->d_pod_out && e->podv_n) {  // usage_fast_kernel
     const void* fk = wb == 2 ? (const void*)usage_fast_kernel<2> : wb == 4 ? (const void*)usage_fast_kernel<4>
                                                                            : (const void*)usage_fast_kernel<8>;
-    const uint32_t grid = persist_grid(e, fk, ublocks);
+    uint32_t grid = persist_grid(e, fk, ublocks);
+    if (e->usage_blocks) grid = std::min(ublocks, (uint32_t)e->n_cus * e->usage_blocks);
     if (grid) {
       if (wb == 2) hipLaunchKernelGGL(usage_fast_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
       else if (wb == 4) hipLaunchKernelGGL(usage_fast_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);

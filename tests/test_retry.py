@@ -78,3 +78,44 @@ def test_retry_parity_pod_fast():
             compare_state(prog, eng, sim, k)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_retry_backoff_reaches_the_cap():
+    """Retry counts far past the doubling range: the device's due times equal the oracle's
+    backoffDelayByStep through the 32-minute cap (utils.go:133-143), Philox jitter included,
+    and the pending stage is re-queued."""
+    from tests.parity_util import NOW0, build
+    cl = W.make_cluster("C1", 4, 64, seed=5)
+    objs = cl.pods.materialize()
+    prog, eng, sim = build(cl.pod_stage_files, objs)
+    ing = Ingest(prog)
+    seed = 0xBAC0
+    try:
+        now = NOW0
+        pre = [copy.deepcopy(o) for o in sim.objs]
+        eng.step(now, seed, 0)
+        fired = sorted((int(r["slot"]), int(r["stage"])) for r in eng.fired())
+        assert len(fired) >= 20
+        fired = fired[:20]
+        counts = np.array([0, 1, 5, 10, 11, 12, 13, 20, 31, 40, 63, 64, 100, 1000, 10**5, 2**31, 2**32 - 1, 3, 7, 9],
+                          dtype=np.uint32)
+        slots = np.array([i for i, _ in fired], dtype=np.uint32)
+        stages = np.array([s for _, s in fired], dtype=np.uint16)
+        hot = np.zeros(len(fired), dtype=abi.HOT_DTYPE)
+        cls = np.zeros(len(fired), dtype=np.uint16)
+        for j, (i, _) in enumerate(fired):
+            pred, flags, _, _, c = ing.encode(pre[i])
+            hot[j] = (pred, flags | abi.STAGE_NONE, 0)
+            cls[j] = c
+        eng.retry(now, seed, 0, slots, hot, cls, stages, counts)
+        got, _ = eng.read()
+        cap = B["cap_ns"]
+        for j, (i, s) in enumerate(fired):
+            want = retry_ref.retry_due(now, seed, 0, i, 0, int(counts[j]), B)
+            assert int(got["due"][i]) == want, (j, int(counts[j]))
+            assert int(got["sched"][i]) & 0xFF == s
+            if counts[j] >= 12:  # 2^11 s > 32 min: capped, then jittered by up to 20 %
+                assert cap <= want - now <= cap * 1.2 + 1
+    finally:
+        eng.close()

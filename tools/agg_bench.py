@@ -47,6 +47,11 @@ def main():
         t[0] += 10**9
         pods.usage(t[0])
     res["usage"] = timed(pods, usage, args.reps)
+    from kwok_amd.host import abi
+    for b in (2, 3, 4, 5, 6, 8):  # resident blocks per CU of the usage kernel's persistent grid
+        pods.set_tuning(abi.TUNE_USAGE_BLOCKS, b)
+        res[f"usage_blocks{b}"] = timed(pods, usage, args.reps)
+    pods.set_tuning(abi.TUNE_USAGE_BLOCKS, 0)
     res["count"] = timed(pods, lambda: pods.count(pm), args.reps)
     res["fired_compact"] = timed(pods, pods.fired_compact, args.reps)
     res["aggregate"] = timed(pods, lambda: pods.aggregate(pm, t[0], usage=True), args.reps)
