@@ -93,3 +93,39 @@ def test_local_node_ptr():
     ptr = np.array([0, 3, 5, 9, 12])
     assert local_node_ptr(ptr, 1, 3).tolist() == [0, 2, 6]
     assert pod_range(ptr, 1, 3) == (3, 9)
+
+
+class _FakeEngine:
+    """kwk_aggregate's layout without a device: [transitions per stage | counts | usage]."""
+
+    class _P:
+        def __init__(self, names):
+            self.names = names
+
+    def __init__(self, names, fired, counts, usage):
+        self.p = self._P(names)
+        self.fired, self.counts, self.usage = fired, counts, usage
+        self.buf = None
+
+    def aggregate(self, masks, now_ns=0, usage=False, out_ptr=None):
+        assert out_ptr is None and len(masks) == len(self.counts)
+        self.buf = np.array(list(self.fired) + list(self.counts) + (list(self.usage) if usage else []), dtype=np.float64)
+        return len(self.buf)
+
+    def aggregate_read(self, n):
+        return self.buf[:n].copy()
+
+
+def test_device_report_unpacks_engine_aggregates():
+    from kwok_amd.host.cluster import DeviceReport
+    pods = _FakeEngine(["pod-ready", "pod-complete"], [7, 3], [10, 6, 1], [1.5, 2048.0])
+    nodes = _FakeEngine(["node-initialize"], [2], [2, 2], [0.0, 0.0])
+    r = DeviceReport([pods, nodes], [[0, 4, 8], [0, 1]], [["pods", "R", "S"], ["nodes", "N"]], usage_engine=pods)
+    with pytest.raises(RuntimeError):
+        r.result()
+    r.collect(123)
+    a = r.result()
+    assert a.stage_names == ["pod-ready", "pod-complete", "node-initialize"]
+    assert a.fired_per_stage.tolist() == [7, 3, 2]
+    assert a.counts.tolist() == [10, 6, 1, 2, 2] and a.count_names == ["pods", "R", "S", "nodes", "N"]
+    assert a.usage.tolist() == [1.5, 2048.0]

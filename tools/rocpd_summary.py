@@ -2,6 +2,8 @@
 
     python tools/rocpd_summary.py stats <db> [out.csv]        # kernel-trace --stats table
     python tools/rocpd_summary.py pmc <db> [kernel-substring]  # per-kernel counter means per dispatch
+    python tools/rocpd_summary.py window <db> <kernel-substring> <first> <count> [stride]
+                                                           # mean duration of dispatches first, first+stride, ...
 
 `stats` reproduces rocprofv3's kernel_stats.csv columns (Name, Calls, TotalDurationNs,
 AverageNs, Percentage, MinNs, MaxNs).  `pmc` sums each counter over its dimensions
@@ -54,8 +56,23 @@ def pmc(db: str, kernel: str = ""):
     return out
 
 
+def window(db: str, kernel: str, first: int, count: int, stride: int = 1):
+    """Durations (ns) of one kernel's dispatches in launch order, [first, first + count) with a
+    stride: e.g. the timed launches of bench.py (after its warm-up steps; every EV_EVERY-th one is
+    the launch its HIP events sampled)."""
+    c = sqlite3.connect(db)
+    d = [int(v) for n, v in c.execute("select name, duration from kernels order by start") if kernel in n]
+    sel = d[first:first + count:stride]
+    return {"kernel": kernel, "dispatches": len(d), "selected": len(sel), "mean_ns": statistics.mean(sel),
+            "median_ns": statistics.median(sel), "min_ns": min(sel), "max_ns": max(sel), "durations_ns": sel}
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "window":
+        import json
+        print(json.dumps(window(sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]),
+                                int(sys.argv[6]) if len(sys.argv) > 6 else 1)))
+    elif sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
     else:
         for name, cs in pmc(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "").items():
