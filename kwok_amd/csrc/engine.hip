@@ -3130,6 +3130,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   HIP_TRY(hipMemcpy(e->d_cpu, cpu_values, 8 * (size_t)n_cpu, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_mem, mem_values, 8 * (size_t)n_mem, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(e->d_node_cum, 0, 16 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMemset(e->d_cluster, 0, 16));  // totals of a configuration without nodes stay 0
   HIP_TRY(hipMemset(e->d_node_last, 0x80, 8 * ((size_t)n_nodes + 1)));  // INT64_MIN-ish sentinel below
   std::vector<int64_t> lasts((size_t)n_nodes + 1, INT64_MIN);
   HIP_TRY(hipMemcpy(e->d_node_last, lasts.data(), 8 * lasts.size(), hipMemcpyHostToDevice));
