@@ -1957,6 +1957,14 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
   }
   __syncthreads();
   constexpr uint32_t kWpc = 16u / WB;  // words per chunk
+  // the 2-byte format's masks for both halves of a dword
+  const uint32_t a2 = (abit & 0xFFFFu) * 0x10001u;
+  uint32_t m2[NM], every2[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    m2[m] = (mk[m] & 0xFFFFu) * 0x10001u;
+    every2[m] = every[m] ? 0x80008000u : 0u;
+  }
   const uint64_t n_chunks = ((uint64_t)n * WB + 15u) / 16u;
   const uint4* __restrict__ q = reinterpret_cast<const uint4*>(st);
   auto tally = [&](uint32_t pred, uint32_t flags, bool in) {
@@ -1969,10 +1977,20 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
     const uint64_t i0 = c * kWpc;
     const uint32_t lim = i0 + kWpc <= n ? kWpc : (uint32_t)(n - i0);  // words of the chunk below n
     if constexpr (WB == 2) {
+      // two words per dword (SWAR): a half is nonzero iff bit 15 of
+      // ((h & 0x7FFF) + 0x7FFF) | h is set; hits = alive & (every | pred & mask), popcounted
+      const uint32_t lim_m = lim >= 8u ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t w = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-        tally(w, w, (uint32_t)j < lim);
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t d = dw[q];
+        const uint32_t in = lim_m | ((2u * q < lim ? 0x8000u : 0u) | (2u * q + 1u < lim ? 0x80000000u : 0u));
+        const uint32_t al = ((((d & a2) & 0x7FFF7FFFu) + 0x7FFF7FFFu) | (d & a2)) & 0x80008000u & in;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          const uint32_t x = d & m2[m];
+          const uint32_t hit = ((((x & 0x7FFF7FFFu) + 0x7FFF7FFFu) | x) & 0x80008000u) | every2[m];
+          cnt[m] += (uint32_t)__popc(hit & al);
+        }
       }
     } else if constexpr (WB == 4) {
 #pragma unroll
