@@ -128,22 +128,31 @@ def test_shard_invariance_two_engines():
             e.close()
 
 
-def test_count_phase_histogram():
-    """kwk_count (cluster aggregates for the RCCL all-reduce) against the oracle's phases."""
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_count_phase_histogram(state):
+    """kwk_count and kwk_aggregate (cluster aggregates for the RCCL all-reduce) against the
+    oracle's phases, in the 2-, 4- and 8-byte state formats; a ragged object count so the last
+    16-byte chunk is partly past the end."""
     from kwok_amd.host.cluster import phase_masks
     from oracle import refcpu
     from tests.parity_util import NOW0, build
-    cl = W.make_cluster("C1", 20, 400, seed=15)
-    prog, eng, sim = build(cl.pod_stage_files, cl.pods.materialize(), harness=True)
+    cl = W.make_cluster("C1", 20, 403, seed=15)
+    prog, eng, sim = build(cl.pod_stage_files, cl.pods.materialize(), harness=True, state=state)
     try:
         masks = phase_masks(prog, values=("Running", "Succeeded"))
+        fired = np.zeros(len(prog.names), dtype=np.int64)
         for k in range(5):
             eng.step(NOW0 + k * 10**9, 3, k)
-            sim.step(NOW0 + k * 10**9, 3, k)
+            for _, s, _ in sim.step(NOW0 + k * 10**9, 3, k):
+                fired[s] += 1
             got = eng.count([masks["Running"], masks["Succeeded"], 0])
             alive = [o for o in sim.objs if o is not None]
             ph = [(refcpu.query(".status.phase", o) or [None])[0] for o in alive]
-            assert got.tolist() == [ph.count("Running"), ph.count("Succeeded"), len(alive)]
+            want = [ph.count("Running"), ph.count("Succeeded"), len(alive)]
+            assert got.tolist() == want
+            n = eng.aggregate([masks["Running"], masks["Succeeded"], 0])
+            agg = eng.aggregate_read(n)
+            assert agg[:len(fired)].tolist() == fired.tolist() and agg[len(fired):].tolist() == want
     finally:
         eng.close()
 
