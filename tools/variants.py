@@ -31,6 +31,11 @@ VARIANTS = {
                   "delay = (int64_t)((uint64_t)delay + (uint64_t)(jit >> 1));")],
     # the word sweep's fired records / per-stage counts are not written
     "w_noemit": [("      emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);\n", "      (void)f;\n")],
+    # scheduled stages do not store their due time (the due column is only read)
+    "nodue_w": [("    else a.due[i] = due;\n", "    else (void)due;\n")],
+    # the word sweep's phase 3 stores no state lines
+    "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
+                    "        (void)gq;\n")],
 }
 
 
