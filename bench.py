@@ -294,6 +294,29 @@ def cpu_baseline(sample_s: float, seed: int):
                       f"{_cpu_model()} ({os.cpu_count()} logical CPUs visible)"}
 
 
+def cpu_baseline_c2(sample_s: float, seed: int):
+    """The reference-faithful matcher (refcpu: JSON re-parse + Match + Delay, 1 thread) on a
+    C2-shaped sample with the pod-general + chaos stages (weighted picks, jitter draws, value
+    getters): the CPU leg beside the hbm_working_set line."""
+    import yaml
+    from kwok_amd import workload as W
+    from oracle import refcpu
+    cl = W.make_cluster("C2", 200, 20000, seed=seed)
+    lc = refcpu.Lifecycle([yaml.safe_load(open(p)) for p in cl.pod_stage_files])
+    objs = [json.dumps(o, separators=(",", ":")).encode() for o in cl.pods.materialize()]
+    lc.match_batch(objs[:2000], NOW0, seed, 0)  # warm-up
+    t0, n, reps = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < sample_s:
+        lc.match_batch(objs, NOW0, seed, reps + 1)
+        n += len(objs)
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "stage transitions/sec (upper bound: matches/sec)", "cores": 1,
+            "kind": "port",
+            "sample": f"{len(objs)} C2 pod JSON objects x {reps} passes ({dt:.1f} s): JSON re-parse + Match + Delay "
+                      f"(pod-general + pod-chaos stages), 1 thread; CPU {_cpu_model()}"}
+
+
 def cpu_baseline_soa(sample_s: float, seed: int, n_pods: int = 20_000_000):
     """All-cores SoA mode: the compiled pod-fast program stepped over
     integer columns by every host thread this job may use (oracle/refcpu rc_soa_steps), on a
@@ -493,6 +516,8 @@ def main():
     if rank == 0 and world == 1 and args.hbm_nodes > 0 and not args.no_harness:
         log("HBM working-set run: C2 stage mix at 100M pods")
         hbm = measure_hbm_working_set(args, local_rank)
+        if not args.no_cpu_baseline:
+            hbm["cpu_baseline"] = cpu_baseline_c2(args.cpu_sample_s / 2, args.seed)
 
     if rank == 0:
         value = total_fired / max_s
