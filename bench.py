@@ -383,6 +383,8 @@ def main():
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
     ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
+    ap.add_argument("--tune-fsm-kernel", type=int, default=-1,
+                    help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     args = ap.parse_args()
 
@@ -444,6 +446,9 @@ def main():
     if args.tune_q16:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_Q16, args.tune_q16)
+    if args.tune_fsm_kernel >= 0:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
     dt = args.dt_ms * 10**6
     reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None)
     report_every = 0 if args.pmc_child else args.report_every

@@ -847,6 +847,326 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   }
 }
 
+// ------------------------------------------------------------------ 2-byte sweep, transition table only
+// sweep16_kernel with every object's step a lookup: chosen when the transition table holds no
+// general entry (no Philox draw, value record or deletion column anywhere in the compiled
+// program — pod-fast, node-fast), so process_object is not compiled in.  sweep16_kernel is
+// VALU-bound at C5 (r1 SQ passes: ~1230 VALU per wave and tile, ~700 of them in phase 2, whose
+// register pressure from the inlined general path spills SGPRs to VGPR lanes); here a 64-item
+// pass is ~30 VALU.  Same phases, tiles, records, statistics and write-back as sweep16_kernel;
+// the ordering differs where the memory counter is in order (gfx9 vmcnt):
+//  * the table lookups of up to kFsmBatch passes are issued together, then the next tile's
+//    loads (kDepth tiles ahead), so waiting for a lookup never waits for the HBM prefetch;
+//  * the due loads of phase 1 come before the prefetch for the same reason;
+//  * lookups, fired records and due times go through buffer resources (32-bit offsets; an
+//    inactive lane's offset is out of range: loads return 0, stores are dropped).
+// Cold path of sweep16_fsm_kernel: a word whose table entry is general (a Philox draw, a value
+// record or the deletion column) runs process_object with the stage table, match masks and
+// deltas read from global memory (L2).  Returns the entry the table would hold ({new word,
+// fired stage / flag / flags, matched} without kFsmDue: the due time is already stored) and the
+// algorithmic bytes.  (Inlined: an out-of-line call made the persistent kernel fault at C5.)
+template <bool kHarness>
+__device__ __forceinline__ uint2 general16(const SweepArgs& a, uint32_t i, uint32_t raw) {
+  const kwk_stage_table* __restrict__ T = a.table;
+  const uint2 s = fmt_unpack(raw, a.fmt);
+  const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;
+  Fire f{false, 0, 0, 0};
+  uint32_t nm = 0, gen_unused = 0;
+  int64_t due_unused = 0;
+  const uint2 nv = process_object<kHarness, 2>(a, T, a.deltas, T->n_stages, T->fin_group_mask, i, s.x, s.y, due, f, nm,
+                                               a.lut, a.lut_n, gen_unused, due_unused);
+  uint32_t e = fmt_pack(nv.x, nv.y, a.fmt) & 0xFFFFu;
+  e |= (f.stage & 31u) << 16 | (f.fire ? 1u : 0u) << 21 | (f.flags & 7u) << 22 | (nm & 1u) << 25;
+  return make_uint2(e, f.bytes);
+}
+
+constexpr int kFsmBatch = 4;  // passes (64 work items each) whose lookups are in flight together
+constexpr uint32_t kFsmKernelDefault = 2;  // table-only sweep with its prefetch depth (0: never)
+template <bool kHarness, int Q, bool kPersist, int kDepth>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ? 4 : 5))) void sweep16_fsm_kernel(SweepArgs a) {
+  constexpr int K = 8 * Q;                 // words per lane
+  constexpr uint32_t kWave = 64u * K;      // words per wave region
+  constexpr uint32_t kTile = kBlock * K;   // words per block
+  constexpr int B = kFsmBatch;
+  static_assert(kDepth >= 1 && kDepth <= 2 && (kPersist || kDepth == 1), "prefetch depth");
+  __shared__ unsigned int s_stat[kStatWords];
+  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: segment resources stay in SGPRs
+  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * 2u) + 15u) & ~15u);
+  const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+  const uint32_t fbits = a.fsm_bits;
+  const __amdgpu_buffer_rsrc_t fsm_rs = make_rsrc(a.fsm, 4u << (fbits + 1));
+  const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u << (fbits + 1));
+  uint4 va[kDepth][Q];
+  // always Q loads (out of range past the last tile: zeros), so that the compiler's in-order
+  // wait counts are the same on every path
+  auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
+    const uint32_t off = t < n_tiles ? (t * kTile + wave * kWave + lane * 8u) * 2u : kOOB - 4u * 1024u;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, off + (uint32_t)q * 1024u, 0, 0);
+      dst[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  uint32_t tile = blockIdx.x;
+  issue_tile(va[0], tile);
+  if (kDepth > 1) issue_tile(va[1], tile + gridDim.x);
+  const uint32_t n_stages = a.table->n_stages;
+  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  __syncthreads();
+
+  const RawTest R = a.raw;
+  struct {
+    uint32_t m2, d2, a2, t2, l2, s2, n2;
+    uint32_t sm, sd, sa, sl;
+  } X;
+  X.m2 = R.managed * 0x10001u; X.d2 = R.dirty * 0x10001u; X.a2 = R.alive * 0x10001u;
+  X.t2 = R.term * 0x10001u; X.l2 = R.del * 0x10001u;
+  X.s2 = (R.smask << R.sshift) * 0x10001u; X.n2 = (R.none_code << R.sshift) * 0x10001u;
+  X.sm = (uint32_t)(16 - __ffs(R.managed)) & 31u; X.sd = (uint32_t)(16 - __ffs(R.dirty)) & 31u;
+  X.sa = (uint32_t)(16 - __ffs(R.alive)) & 31u; X.sl = (uint32_t)(16 - __ffs(R.del)) & 31u;
+  uint32_t n_matched = 0, n_bytes = 0;  // per lane: matches, algorithmic bytes
+  uint32_t n_lline = 0;                 // per lane: bytes of the phase-3 line stores
+  uint32_t w_bytes = 0, w_line = 0;     // wave-uniform: algorithmic bytes, line bytes - algorithmic bytes (mod 2^32)
+  uint32_t wave_fired = 0;              // wave-uniform
+  uint16_t* __restrict__ wl = s_work[wave];
+  uint4* __restrict__ tq = s_tile[wave];
+  uint16_t* __restrict__ tw = reinterpret_cast<uint16_t*>(tq);
+  uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+
+  // kDepth 1: the tile's words are copied out of v and v receives the next tile's loads right
+  // after this tile's lookups; kDepth 2 (ping-pong over va[0] / va[1]): the tile is worked on in
+  // v itself, which receives the tile 2 grid strides ahead once this one is written back
+  auto tile_body = [&](uint4 (&v)[Q], const uint32_t tile) __attribute__((always_inline)) {
+    const uint32_t wbase = tile * kTile + wave * kWave;
+    const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
+    uint32_t seg_n = 0;  // wave-uniform
+    const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
+    uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * kSeg16;
+    const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg16 * 4u);
+    uint4 cur_copy[Q];
+    if (kDepth == 1) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cur_copy[q] = v[q];
+    }
+    uint4 (&cur)[Q] = kDepth == 1 ? cur_copy : v;
+    // ---- phase 1 (as sweep16_kernel); in a partial tile, row q of the lane holds
+    // c = clamp(n - first word, 0, 8) words: its low words are bits q*4 + [0, (c+1)/2), its
+    // high words bits 16 + q*4 + [0, c/2) (no per-bit constants: they would pin ~25 VGPRs)
+    constexpr uint32_t kHalfMask = (1u << (4 * Q)) - 1u;
+    uint32_t in_range = kHalfMask | kHalfMask << 16;
+    if (!full) {
+      in_range = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t left = (int64_t)a.n - (int64_t)(wbase + (uint32_t)q * 512u + lane * 8u);
+        const uint32_t c = left <= 0 ? 0u : left >= 8 ? 8u : (uint32_t)left;
+        in_range |= (((1u << ((c + 1u) >> 1)) - 1u) << (4 * q)) | (((1u << (c >> 1)) - 1u) << (16 + 4 * q));
+      }
+    }
+    uint32_t pend = 0, need = 0, ready = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t dw[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d = dw[j];
+        const uint32_t mg = (d & X.m2) << X.sm;
+        const uint32_t pe = (((d & X.s2) ^ X.n2) + 0x7FFF7FFFu) & 0x80008000u;
+        uint32_t nb = (d & X.d2) << X.sd;
+        if (kHarness) {
+          nb |= (~d & X.a2) << X.sa;
+          nb |= (((d & X.t2) + 0x7FFF7FFFu) & 0x80008000u) & ~((d & X.l2) << X.sl);
+        }
+        const uint32_t n2 = mg & nb, p2 = mg & pe;
+        const int jj = q * 4 + j;
+        need |= n2 >> (15 - jj);
+        pend |= p2 >> (15 - jj);
+      }
+    }
+    pend &= in_range;
+    need &= in_range;
+    if (__ballot(pend != 0)) {
+#pragma unroll 8
+      for (int t = 0; t < K; ++t) {
+        const int k = t < 4 * Q ? t : 16 + t - 4 * Q;
+        const uint32_t p = (pend >> k) & 1u;
+        const int64_t d = buf_load_i64(due_rs, p ? (wbase + bit_word((uint32_t)k) + lane * 8u) * 8u : kOOB);
+        ready |= (p & (uint32_t)(d <= a.now)) << k;
+      }
+      need |= ready;
+    }
+    n_bytes += 2u * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
+    uint32_t n_work = 0, pos = 0;
+    {
+      const uint32_t cnt = (uint32_t)__popc(need);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const unsigned long long bal = __ballot((cnt >> b) & 1u);
+        pos += (uint32_t)__popcll(bal & lt) << b;
+        n_work += (uint32_t)__popcll(bal) << b;
+      }
+      for (uint32_t m = need; m; m &= m - 1u) {
+        const uint32_t k = (uint32_t)__ffs(m) - 1u;
+        wl[pos++] = (uint16_t)(bit_word(k) + lane * 8u + (((ready >> k) & 1u) << 15));
+      }
+    }
+    // ---- phase 2: lookups of the first kFsmBatch passes (straight-line code, so the
+    // compiler's wait for a lookup counts the prefetch issued after it), then the prefetch
+    uint32_t we[B], raw[B], ent[B];
+    auto fetch = [&](const uint32_t c0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const uint32_t c = c0 + 64u * b + lane;
+        const bool in = c < n_work;
+        const uint32_t x = in ? (uint32_t)wl[c & (kWave - 1u)] : 0u;
+        we[b] = in ? x : 0xFFFFFFFFu;
+        raw[b] = (uint32_t)tw[x & 0x7FFFu];
+        ent[b] = __builtin_amdgcn_raw_buffer_load_b32(fsm_rs, in ? ((((x >> 15) << fbits) | raw[b]) * 4u) : kOOB, 0, 0);
+      }
+    };
+    // fired record + per-stage counts of one 64-item pass (e: the item's table entry)
+    auto emit = [&](const bool fire, const uint32_t w, const uint32_t e) __attribute__((always_inline)) {
+      const unsigned long long bal = __ballot(fire);
+      if (bal) {
+        const uint32_t pos = seg_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        const uint32_t rec = w | ((e >> 16) & 31u) << 13 | ((e >> 22) & 7u) << 18;
+        __builtin_amdgcn_raw_buffer_store_b32(rec, seg_rs, fire ? (1u + pos) * 4u : kOOB, 0, 0);
+        const uint32_t nf = (uint32_t)__popcll(bal);
+        seg_n += nf;
+        w_bytes += 4u * nf;
+        const uint32_t code = fire ? ((e >> 16) & 31u) : 31u;
+        for (uint32_t st = 0; st < n_stages; ++st) {  // per-stage counts: one ballot per stage
+          const unsigned long long same = __ballot(code == st);
+          if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
+        }
+      }
+    };
+    // Items whose entry is general are deferred to one loop after the lookups (records are
+    // unordered within a region): their slots are compacted to the front of the work list,
+    // whose entries up to the current batch are already in registers; their words stay
+    // unchanged in the LDS tile until then.
+    uint32_t n_gen = 0;  // wave-uniform
+    auto pass = [&](const int b) __attribute__((always_inline)) {
+      const uint32_t cwe = we[b], e = ent[b];
+      const bool act = cwe != 0xFFFFFFFFu;
+      const uint32_t w = cwe & 0x7FFFu;
+      const bool gen = act && (e & kFsmGeneral);
+      const unsigned long long gb = __ballot(gen);
+      if (gb) {
+        if (gen) wl[n_gen + __builtin_amdgcn_mbcnt_hi((uint32_t)(gb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)gb, 0u))] = (uint16_t)w;
+        n_gen += (uint32_t)__popcll(gb);
+      }
+      const bool tab = act && !gen;
+      if (tab) {
+        tw[w] = (uint16_t)e;
+        n_matched += (e >> 25) & 1u;
+        n_bytes += ((e >> 26) & 15u) * 2u;
+      }
+      const bool dw = tab && (e & kFsmDue);
+      if (__ballot(dw)) {  // a delayed stage is scheduled (rare for table-only programs)
+        const int64_t dd = buf_load_i64(fdue_rs, dw ? ((((cwe >> 15) << fbits) | raw[b]) * 8u) : kOOB);
+        const int64_t v = sat_add(a.now, dd);
+        const uint32_t off = dw ? (wbase + w) * 8u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, due_rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)((uint64_t)v >> 32), due_rs, off + 4u, 0, 0);
+      }
+      emit(tab && ((e >> 21) & 1u), w, e);
+    };
+    if (n_work) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) tq[q * 64 + lane] = cur[q];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      fetch(0);
+    }
+    if (kPersist && kDepth == 1) issue_tile(v, tile + gridDim.x);
+    if (n_work) {
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+        if (64u * b < n_work) pass(b);  // wave-uniform
+      for (uint32_t c0 = 64u * B; c0 < n_work; c0 += 64u * B) {  // more than kFsmBatch passes
+        fetch(c0);
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+          if (c0 + 64u * b < n_work) pass(b);
+      }
+      // cold: the general items (a Philox draw, a value record or the deletion column)
+      for (uint32_t j = 0; j < n_gen; j += 64u) {
+        const bool in = j + lane < n_gen;
+        const uint32_t w = in ? (uint32_t)wl[j + lane] : 0u;
+        uint32_t e = 0;
+        if (in) {
+          const uint2 r = general16<kHarness>(a, wbase + w, (uint32_t)tw[w]);
+          e = r.x;
+          tw[w] = (uint16_t)e;
+          n_matched += (e >> 25) & 1u;
+          n_bytes += r.y;
+        }
+        emit(in && ((e >> 21) & 1u), w, e);
+      }
+      w_line -= 2u * n_work;  // the words' own writes are replaced by the line stores below
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // ---- phase 3: whole 128-byte lines wherever a word changed
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint4 nv = tq[q * 64 + lane];
+        const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
+        const unsigned long long bal = __ballot(ch);
+        if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
+          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);
+          n_lline += 16u;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    {
+      const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
+      for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
+      if (lane == 0) {
+        seg32[0] = seg_n;
+        a.wave_counts[seg_id] = seg_n;
+      }
+      w_line += 4u * (end - used);  // padding: line bytes only
+    }
+    wave_fired += seg_n;
+    w_bytes += 4u;  // the fired count word
+    if (kPersist && kDepth == 2) issue_tile(v, tile + 2u * gridDim.x);
+  };
+  if constexpr (!kPersist) {
+    if (tile < n_tiles) tile_body(va[0], tile);
+  } else if constexpr (kDepth == 1) {
+    for (; tile < n_tiles; tile += gridDim.x) tile_body(va[0], tile);
+  } else {
+    for (; tile < n_tiles; tile += 2u * gridDim.x) {
+      tile_body(va[0], tile);
+      if (tile + gridDim.x >= n_tiles) break;
+      tile_body(va[1], tile + gridDim.x);
+    }
+  }
+
+  // ---- block statistics
+  for (int off = 32; off > 0; off >>= 1) {
+    n_matched += __shfl_xor(n_matched, off);
+    n_bytes += __shfl_xor(n_bytes, off);
+    n_lline += __shfl_xor(n_lline, off);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_stat[0], n_matched);
+    atomicAdd(&s_stat[1], wave_fired);
+    atomicAdd(&s_stat[2], n_bytes + w_bytes);
+    atomicAdd(&s_stat[kStatLine], n_bytes + w_bytes + n_lline + w_line);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
+    const unsigned int val = s_stat[threadIdx.x];
+    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
+  }
+}
+
 // ------------------------------------------------------------------ 4- and 8-byte state sweep
 // Sweep over the 4-byte packed and the 8-byte wide formats (pod-general / chaos and any
 // program wider than 16 bits: no transition table, every work item runs process_object).
@@ -2276,6 +2596,8 @@ struct kwk_engine {
   int64_t* d_fsm_due = nullptr;
   uint32_t fsm_bits = 0;
   int fsm_harness = -1;       // harness enable the table was built for (-1: no table)
+  bool fsm_pure = false;      // the table has no general entry: sweep16_fsm_kernel can run
+  uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_FSM_KERNEL: 0 never, else its prefetch depth
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -2624,6 +2946,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_PERSIST16: 0 or 1");
       e->persist16 = value != 0;
       return KWK_OK;
+    case KWK_TUNE_FSM_KERNEL:
+      if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
+      e->fsm_kernel = value;
+      return KWK_OK;
     case KWK_TUNE_USAGE_BLOCKS:
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
       e->usage_blocks = value;
@@ -2872,7 +3198,11 @@ static kwk_status build_fsm(kwk_engine* e) {
     hipLaunchKernelGGL(fsm_build_kernel<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, e->d_fsm,
                        e->d_fsm_due);
   HIP_TRY(hipGetLastError());
+  std::vector<uint32_t> tab(n);
+  HIP_TRY(hipMemcpyAsync(tab.data(), e->d_fsm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  e->fsm_pure = true;
+  for (uint32_t x : tab) e->fsm_pure &= !(x & kFsmGeneral);
   e->fsm_harness = a.harness.enable ? 1 : 0;
   return KWK_OK;
 }
@@ -2901,14 +3231,26 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const uint32_t K = 8 * q16, tile = kBlock * K;
     const uint32_t tiles = (e->n_active + tile - 1) / tile;
     uint32_t blocks = tiles;
+    const bool lean = a.fsm && e->fsm_kernel;
 #define LAUNCH16(HV, QV)                                                                                        \
   do {                                                                                                          \
-    const uint32_t pg = e->persist16 ? persist_grid(e, (const void*)sweep16_kernel<HV, QV, true>, tiles) : tiles; \
+    const void* pk = lean ? (e->fsm_kernel == 2 ? (const void*)sweep16_fsm_kernel<HV, QV, true, 2>              \
+                                                : (const void*)sweep16_fsm_kernel<HV, QV, true, 1>)             \
+                          : (const void*)sweep16_kernel<HV, QV, true>;                                          \
+    const uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;                                      \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
-      hipLaunchKernelGGL((sweep16_kernel<HV, QV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);       \
+      if (lean)                                                                                                 \
+        hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
+      else                                                                                                      \
+        hipLaunchKernelGGL((sweep16_kernel<HV, QV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);     \
     } else {                                                                                                    \
       blocks = pg;                                                                                              \
-      hipLaunchKernelGGL((sweep16_kernel<HV, QV, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);        \
+      if (lean && e->fsm_kernel == 2)                                                                           \
+        hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, true, 2>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
+      else if (lean)                                                                                            \
+        hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, true, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
+      else                                                                                                      \
+        hipLaunchKernelGGL((sweep16_kernel<HV, QV, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);      \
     }                                                                                                           \
   } while (0)
     if (q16 == 4) {

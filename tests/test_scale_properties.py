@@ -70,14 +70,19 @@ def test_three_sweeps_agree_at_4m_pods():
 
 
 def test_sweep16_tile_shapes_agree_at_17m_pods():
-    """The 2-byte sweep's tile shapes: Q = 4 (8192-word tiles, persistent grid: at 17M pods
-    the tiles outnumber twice the resident blocks), Q = 2 and Q = 1 (one block per tile) must
-    fire the same sets and leave the same words (kwk_set_tuning KWK_TUNE_Q16)."""
+    """The 2-byte sweep's kernels and tile shapes: the table-only sweep (pod-fast has no general
+    table entry) with the next 2 or 1 tiles in flight and the general sweep16_kernel
+    (KWK_TUNE_FSM_KERNEL 0), at Q = 4 (8192-word tiles, persistent grid: at 17M pods the tiles
+    outnumber twice the resident blocks), Q = 2 and Q = 1 (one block per tile) must fire the
+    same sets, leave the same words and count the same statistics."""
     from kwok_amd.host import abi
+    shapes = {"4": {abi.TUNE_Q16: 4}, "4-d1": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 1},
+              "4-gen": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 0}, "2": {abi.TUNE_Q16: 2},
+              "1": {abi.TUNE_Q16: 1}, "1-gen": {abi.TUNE_Q16: 1, abi.TUNE_FSM_KERNEL: 0}}
     engines = {}
     try:
-        for q in ("4", "2", "1"):
-            engines[q] = _pods("auto", n_nodes=170_000, tuning={abi.TUNE_Q16: int(q)})
+        for q, tuning in shapes.items():
+            engines[q] = _pods("auto", n_nodes=170_000, tuning=tuning)
         assert all(e.stats()["state_bytes"] == 2 for _, e in engines.values())
         now0 = 1_700_000_000 * 10**9
         for k in range(10):
@@ -86,13 +91,21 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
                 e.step(now0 + k * 10**9, 0x6B776F6B, k)
                 keys[q] = _fired_key(e.fired())
             assert len(keys["4"]) > 0
-            assert np.array_equal(keys["4"], keys["2"]) and np.array_equal(keys["4"], keys["1"]), f"step {k}"
+            for q in shapes:
+                assert np.array_equal(keys["4"], keys[q]), f"step {k}: {q}"
         states = {q: e.read()[0] for q, (_, e) in engines.items()}
-        for q in ("2", "1"):
+        for q in shapes:
             for col in ("pred", "sched"):
                 assert np.array_equal(states["4"][col], states[q][col]), (q, col)
         st = {q: e.stats() for q, (_, e) in engines.items()}
-        assert st["4"]["fired_per_stage"] == st["2"]["fired_per_stage"] == st["1"]["fired_per_stage"]
+        for q in shapes:
+            assert st[q]["fired_per_stage"] == st["4"]["fired_per_stage"], q
+            for key in ("fired", "matched"):
+                assert st[q][key] == st["4"][key], (q, key)
+        # byte counts include one fired-count word per (tile, wave) segment: equal per tile shape
+        for q, ref in (("4-d1", "4"), ("4-gen", "4"), ("1-gen", "1")):
+            for key in ("bytes", "line_bytes"):
+                assert st[q][key] == st[ref][key], (q, key)
     finally:
         for _, e in engines.values():
             e.close()

@@ -22,6 +22,11 @@ OUT = os.path.join(ROOT, "tools", "build")
 _P2 = ("const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,\n"
        "                                                       n_matched, lutp, lut_n, gen_unused, due_unused);")
 
+_FORCE = ("const bool lean = a.fsm && e->fsm_kernel;", "const bool lean = a.fsm && e->fsm_kernel;")
+
+_NOCALL = ("          const uint2 r = general16<kHarness>(a, wbase + w, (uint32_t)tw[w]);",
+           "          const uint2 r = make_uint2(0u, 0u);")
+
 VARIANTS = {
     "base": [],
     # phase 2 of the word sweep does nothing (no state change, no fires)
@@ -33,6 +38,30 @@ VARIANTS = {
     "w_noemit": [("      emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);\n", "      (void)f;\n")],
     # scheduled stages do not store their due time (the due column is only read)
     "nodue_w": [("    else a.due[i] = due;\n", "    else (void)due;\n")],
+    # table-only 2-byte sweep (sweep16_fsm_kernel) even when some table entry is general (pod-fast at
+    # C5 reaches none of them: results stay correct there, not in general)
+    "f_force": [_FORCE],
+    # the general 2-byte sweep (sweep16_kernel) for every program
+    "g_old": [("constexpr uint32_t kFsmKernelDefault = 2;", "constexpr uint32_t kFsmKernelDefault = 0;")],
+    "f_force_d1": [_FORCE, ("constexpr uint32_t kFsmKernelDefault = 2;", "constexpr uint32_t kFsmKernelDefault = 1;")],
+    # ... without the out-of-line general path (wrong results if a general entry is reached)
+    "f_nocall_d1": [_FORCE, _NOCALL, ("constexpr uint32_t kFsmKernelDefault = 2;", "constexpr uint32_t kFsmKernelDefault = 1;")],
+    "f_nocall_d2": [_FORCE, _NOCALL],
+    # table-only 2-byte sweep (sweep16_fsm_kernel), C5 cost isolation (run with --c5):
+    # phase 3 stores no lines
+    "f_nop3": [_FORCE, ("          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);\n          n_lline += 16u;",
+                "          (void)gq;\n          n_lline += 16u;")],
+    # no fired records stored
+    "f_norec": [_FORCE, ("__builtin_amdgcn_raw_buffer_store_b32(rec, seg_rs, fire ? (1u + pos) * 4u : kOOB, 0, 0);",
+                 "(void)rec; (void)pos;")],
+    # phase 2 does nothing (the words never change: every later step is the same read + work list)
+    "f_nop2": [_FORCE, ("        if (64u * b < n_work) pass(b);  // wave-uniform", "        (void)b;")],
+    # phase 2 does nothing and phase 3 rewrites every line: the kernel's own read + rewrite stream
+    "f_nop2_all": [_FORCE, ("        if (64u * b < n_work) pass(b);  // wave-uniform", "        (void)b;"),
+                   ("        if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {\n"
+                    "          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);\n          n_lline",
+                    "        if (bal || true) {\n"
+                    "          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);\n          n_lline")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
@@ -74,22 +103,37 @@ def child(name, hbm_nodes, steps):
     print(json.dumps({"variant": name, **r}), flush=True)
 
 
+def child_c5(name, steps):
+    """The C5 bench line (pod sweep timing) with the variant library."""
+    sys.path.insert(0, ROOT)
+    from kwok_amd.host import abi
+    abi.LIB_PATH = os.path.join(OUT, f"libkwok_engine_{name}.so")
+    import bench
+    sys.argv = ["bench.py", "--steps", str(steps), "--warmup", "5", "--no-pmc", "--no-cpu-baseline", "--hbm-nodes", "0",
+                "--pcie-steps", "0"]
+    bench.main()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("cmd", choices=("build", "run", "child"))
     ap.add_argument("names", nargs="*")
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--c5", action="store_true", help="time the C5 pod sweep instead of the C2 working set")
     a = ap.parse_args()
     names = a.names or list(VARIANTS)
     if a.cmd == "build":
         build(names)
     elif a.cmd == "child":
-        child(names[0], a.hbm_nodes, a.steps)
+        if a.c5:
+            child_c5(names[0], a.steps)
+        else:
+            child(names[0], a.hbm_nodes, a.steps)
     else:
         for n in names:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "child", n, "--hbm-nodes", str(a.hbm_nodes),
-                                "--steps", str(a.steps)], timeout=300)
+                                "--steps", str(a.steps)] + (["--c5"] if a.c5 else []), timeout=300)
             if r.returncode != 0:
                 raise SystemExit(f"variant {n}: rc {r.returncode}")
 
