@@ -866,8 +866,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
 // fired stage / flag / flags, matched} without kFsmDue: the due time is already stored) and the
 // algorithmic bytes.  (Inlined: an out-of-line call made the persistent kernel fault at C5.)
 template <bool kHarness>
-__device__ __forceinline__ uint2 general16(const SweepArgs& a, uint32_t i, uint32_t raw) {
-  const kwk_stage_table* __restrict__ T = a.table;
+__device__ __forceinline__ uint2 general16(uint32_t i, uint32_t raw) {
+  // the kernel's SweepArgs (its only argument, at offset 0 of the kernarg segment) and the stage
+  // table are read through a VGPR address: their values land in VGPRs, which the lookup loop
+  // leaves free, instead of taking SGPRs from it (SGPR spills into VGPR lanes cost ~4 us)
+  uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+v"(ka));
+  const SweepArgs& a = *reinterpret_cast<const SweepArgs*>(ka);
+  uint64_t tp = (uint64_t)a.table;
+  asm volatile("" : "+v"(tp));
+  const kwk_stage_table* __restrict__ T = reinterpret_cast<const kwk_stage_table*>(tp);
   const uint2 s = fmt_unpack(raw, a.fmt);
   const int64_t due = ((s.y & 0xFFu) != KWK_STAGE_NONE) ? a.due[i] : 0;
   Fire f{false, 0, 0, 0};
@@ -1100,7 +1108,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         const uint32_t w = in ? (uint32_t)wl[j + lane] : 0u;
         uint32_t e = 0;
         if (in) {
-          const uint2 r = general16<kHarness>(a, wbase + w, (uint32_t)tw[w]);
+          const uint2 r = general16<kHarness>(wbase + w, (uint32_t)tw[w]);
           e = r.x;
           tw[w] = (uint16_t)e;
           n_matched += (e >> 25) & 1u;

@@ -24,7 +24,7 @@ _P2 = ("const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, f
 
 _FORCE = ("const bool lean = a.fsm && e->fsm_kernel;", "const bool lean = a.fsm && e->fsm_kernel;")
 
-_NOCALL = ("          const uint2 r = general16<kHarness>(a, wbase + w, (uint32_t)tw[w]);",
+_NOCALL = ("          const uint2 r = general16<kHarness>(wbase + w, (uint32_t)tw[w]);",
            "          const uint2 r = make_uint2(0u, 0u);")
 
 VARIANTS = {
