@@ -535,7 +535,8 @@ def main():
                 "traffic_note": (f"rocprofv3 PMC child passes of this workload ({traffic['launches']} pod-sweep launches): "
                                  f"FETCH_SIZE x 2 = {traffic['read']} B read + WRITE_SIZE = {traffic['write']} B written "
                                  "per launch" if traffic else f"null: {pmc_err}"),
-                "kernel": ("sweep16_kernel" if sb == 2 else "sweepw_kernel") + " (pods)",
+                "kernel": ("sweep16_fsm_kernel" if sb == 2 and args.tune_fsm_kernel != 0 else
+                           "sweep16_kernel" if sb == 2 else "sweepw_kernel") + " (pods)",
                 "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
