@@ -1693,7 +1693,11 @@ struct UsageArgs {
   double* __restrict__ ccum;        // per container of a mixed pod: {cpu, mem} integrators
   const double* __restrict__ podv;  // usage_fast_kernel: pod values per (containers, value id), see kwk_usage_config
   uint32_t podv_n;                  // entries of podv
+  const uint8_t* __restrict__ ukey8;  // usage_fast_kernel<WB, true>: per pod, an index into kv
+  const double2* __restrict__ kv;     // {cpu, mem} value of each distinct usage key (<= kUKeyDict)
+  uint32_t kv_n;
 };
+constexpr uint32_t kUKeyDict = 256;  // distinct usage keys that take the 1-byte key column
 
 // a pod's usage_key: containers (bits 28..31) x one interned value each, or 0 containers =
 // a pod whose containers differ: bits 0..27 index its {first, count} entry of the mixed table
@@ -1958,20 +1962,25 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
 // the device loop would), and a node boundary inside a lane is a short masked branch.  Empty
 // nodes are written separately, so closing a node never loops.
 constexpr uint32_t kUFastVals = 2048;  // podv entries staged in LDS
-template <uint32_t WB>
+// kKey8: the pods' usage keys as one byte each (an index into the distinct keys' {cpu, mem}
+// values, kwk_usage_config builds it when at most kUKeyDict keys occur): 16 bytes per lane's run
+// instead of 64, one LDS read per pod instead of two and no key decode
+template <uint32_t WB, bool kKey8 = false>
 __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
+  constexpr uint32_t KQ = kKey8 ? 1u : 4u;  // 16-byte key chunks per lane's run
   __shared__ uint32_t s_ptr[kWavesPerBlock][kUChunkNodes + 1];
   __shared__ double2 s_sum[kWavesPerBlock][kUChunkNodes];
-  __shared__ double s_pv[kUFastVals];
+  __shared__ double s_pv[kKey8 ? 1 : kUFastVals];
+  __shared__ double2 s_kv[kKey8 ? kUKeyDict : 1];
   __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
   uint32_t chunk = blockIdx.x * kWavesPerBlock + wave;
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods * WB);
-  const __amdgpu_buffer_rsrc_t uk_rs = make_rsrc(a.ukey, a.n_pods * 4u);
+  const __amdgpu_buffer_rsrc_t uk_rs = kKey8 ? make_rsrc(a.ukey8, a.n_pods) : make_rsrc(a.ukey, a.n_pods * 4u);
   uint4 nch = make_uint4(0u, 0u, 0u, 0u);
-  uint4 nsv[WB], nkv[4];
-  auto load_row = [&](uint4 (&dsv)[WB], uint4 (&dkv)[4], uint32_t r0, uint32_t c0, uint32_t c1) {
+  uint4 nsv[WB], nkv[KQ];
+  auto load_row = [&](uint4 (&dsv)[WB], uint4 (&dkv)[KQ], uint32_t r0, uint32_t c0, uint32_t c1) {
     const uint32_t lf = r0 + lane * kURun;
     const bool has = max(lf, c0) < min(lf + kURun, c1);
 #pragma unroll
@@ -1980,8 +1989,8 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
       dsv[q] = make_uint4(c[0], c[1], c[2], c[3]);
     }
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const auto c = __builtin_amdgcn_raw_buffer_load_b128(uk_rs, has ? lf * 4u + q * 16u : kOOB, 0, 0);
+    for (uint32_t q = 0; q < KQ; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(uk_rs, has ? lf * (kKey8 ? 1u : 4u) + q * 16u : kOOB, 0, 0);
       dkv[q] = make_uint4(c[0], c[1], c[2], c[3]);
     }
   };
@@ -1989,7 +1998,11 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
     nch = a.chunks[chunk];
     load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
   }
-  for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
+  if (kKey8) {
+    for (uint32_t j = threadIdx.x; j < a.kv_n; j += kBlock) s_kv[j] = a.kv[j];
+  } else {
+    for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
+  }
   __syncthreads();
   const uint32_t nv = a.n_cpu + a.n_mem;  // podv row: cpu values then memory values
   const uint32_t abit = WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
@@ -2000,11 +2013,11 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
     const uint4 ch = nch;
     const uint32_t c0 = ch.x, c1 = ch.y, na = ch.z, nk = ch.w - ch.z;
     const uint32_t r_first = c0 & ~7u;
-    uint4 sv[WB], kv[4];
+    uint4 sv[WB], kv[KQ];
 #pragma unroll
     for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) kv[q] = nkv[q];
+    for (uint32_t q = 0; q < KQ; ++q) kv[q] = nkv[q];
     const uint32_t nxt = chunk + n_waves;
     if (nxt < a.n_chunks) nch = a.chunks[nxt];
     double2 pre_cum = make_double2(0.0, 0.0);
@@ -2057,11 +2070,21 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
           do { ++k; } while (sp[k + 1] <= p);  // past nodes without pods
           bnd = sp[k + 1];
         }
-        const uint4 kq = kv[j >> 2];
-        const uint32_t key = (j & 3) == 0 ? kq.x : (j & 3) == 1 ? kq.y : (j & 3) == 2 ? kq.z : kq.w;
         const bool live = in && run_alive<WB>(sv, j, abit);
-        const uint32_t row = (key >> 28) * nv;
-        const double vc = s_pv[row + (key & 0x3FFFu)], vm = s_pv[row + a.n_cpu + ((key >> 14) & 0x3FFFu)];
+        double vc, vm;
+        if constexpr (kKey8) {
+          const uint4 kq = kv[0];
+          const uint32_t d = (j >> 2) == 0 ? kq.x : (j >> 2) == 1 ? kq.y : (j >> 2) == 2 ? kq.z : kq.w;
+          const double2 v = s_kv[(d >> (8 * (j & 3))) & 0xFFu];
+          vc = v.x;
+          vm = v.y;
+        } else {
+          const uint4 kq = kv[j >> 2];
+          const uint32_t key = (j & 3) == 0 ? kq.x : (j & 3) == 1 ? kq.y : (j & 3) == 2 ? kq.z : kq.w;
+          const uint32_t row = (key >> 28) * nv;
+          vc = s_pv[row + (key & 0x3FFFu)];
+          vm = s_pv[row + a.n_cpu + ((key >> 14) & 0x3FFFu)];
+        }
         acc_c += live ? vc : 0.0;
         acc_m += live ? vm : 0.0;
       }
@@ -2598,6 +2621,7 @@ struct kwk_engine {
   uint32_t q16 = kQ16;        // 2-byte sweep: 16-byte chunks per lane (1 | 2 | 4)
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
+  bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
   uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
@@ -2627,6 +2651,9 @@ struct kwk_engine {
   uint32_t n_nodes = 0, n_usage_pods = 0;
   uint32_t* d_node_ptr = nullptr;
   uint32_t* d_ukey = nullptr;
+  uint8_t* d_ukey8 = nullptr;   // usage_fast_kernel<WB, true>: 1-byte key column (<= kUKeyDict distinct keys)
+  double2* d_kv = nullptr;      // {cpu, mem} per distinct key
+  uint32_t kv_n = 0;
   double* d_cpu = nullptr;
   double* d_mem = nullptr;
   double* d_node_out = nullptr;
@@ -2843,7 +2870,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
                   e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
-                  e->d_lease_nops, e->d_lease_stats};
+                  e->d_lease_nops, e->d_lease_stats, e->d_ukey8, e->d_kv};
   for (void* p : ptrs) if (p) hipFree(p);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
@@ -2957,6 +2984,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_FSM_KERNEL:
       if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
       e->fsm_kernel = value;
+      return KWK_OK;
+    case KWK_TUNE_USAGE_KEY8:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
+      e->usage_key8 = value != 0;
       return KWK_OK;
     case KWK_TUNE_USAGE_BLOCKS:
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
@@ -3465,8 +3496,13 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   uint32_t max_nc = 0;
   for (uint32_t p = 0; p < n_pods; ++p) max_nc = (ukey[p] >> 28) > max_nc ? (ukey[p] >> 28) : max_nc;
   if (e->d_podv) HIP_TRY(hipFree(e->d_podv));
+  if (e->d_ukey8) HIP_TRY(hipFree(e->d_ukey8));
+  if (e->d_kv) HIP_TRY(hipFree(e->d_kv));
   e->d_podv = nullptr;
+  e->d_ukey8 = nullptr;
+  e->d_kv = nullptr;
   e->podv_n = 0;
+  e->kv_n = 0;
   const size_t nv = (size_t)n_cpu + n_mem;
   if ((max_nc + 1) * nv <= kUFastVals) {
     std::vector<double> podv((max_nc + 1) * nv, 0.0);
@@ -3485,6 +3521,32 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
     HIP_TRY(hipMalloc(&e->d_podv, sizeof(double) * podv.size()));
     HIP_TRY(hipMemcpy(e->d_podv, podv.data(), sizeof(double) * podv.size(), hipMemcpyHostToDevice));
     e->podv_n = (uint32_t)podv.size();
+    // distinct keys -> 1-byte column + {cpu, mem} values (the same podv entries, so the sums are
+    // bit-identical to the 4-byte-key kernel's)
+    std::vector<uint32_t> dict;
+    std::vector<uint8_t> k8(n_pods);
+    bool fits = true;
+    for (uint32_t p = 0; p < n_pods && fits; ++p) {
+      uint32_t d = 0;
+      while (d < dict.size() && dict[d] != ukey[p]) ++d;  // few distinct keys: linear search
+      if (d == dict.size()) {
+        if (dict.size() == kUKeyDict) { fits = false; break; }
+        dict.push_back(ukey[p]);
+      }
+      k8[p] = (uint8_t)d;
+    }
+    if (fits && n_pods) {
+      std::vector<double2> kv(dict.size());
+      for (size_t d = 0; d < dict.size(); ++d) {
+        const uint32_t k = dict[d], row = (k >> 28) * (uint32_t)nv;
+        kv[d] = make_double2(podv[row + (k & 0x3FFFu)], podv[row + n_cpu + ((k >> 14) & 0x3FFFu)]);
+      }
+      HIP_TRY(hipMalloc(&e->d_ukey8, (size_t)n_pods + 16));
+      HIP_TRY(hipMalloc(&e->d_kv, sizeof(double2) * kv.size()));
+      HIP_TRY(hipMemcpy(e->d_ukey8, k8.data(), n_pods, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(e->d_kv, kv.data(), sizeof(double2) * kv.size(), hipMemcpyHostToDevice));
+      e->kv_n = (uint32_t)kv.size();
+    }
   }
   HIP_TRY(hipMalloc(&e->d_node_ptr, 4 * ((size_t)n_nodes + 1)));
   HIP_TRY(hipMalloc(&e->d_ukey, 4 * ((size_t)n_pods + 1)));
@@ -3782,15 +3844,21 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
   UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, (uint32_t)e->h_cpu.size(),
                (uint32_t)e->h_mem.size(), e->d_uchunk, e->n_uchunks, e->n_usage_pods, e->d_node_out, e->d_node_cum,
                e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last, e->d_mixed,
-               e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n};
+               e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n, e->d_ukey8, e->d_kv, e->kv_n};
   const uint32_t wb = word_bytes(e->fmt);
   if (!e->has_mixed_keys && !e->d_pod_out && e->podv_n) {  // usage_fast_kernel
-    const void* fk = wb == 2 ? (const void*)usage_fast_kernel<2> : wb == 4 ? (const void*)usage_fast_kernel<4>
-                                                                           : (const void*)usage_fast_kernel<8>;
+    const bool k8 = e->d_ukey8 != nullptr && e->usage_key8;
+    const void* fk = k8 ? (wb == 2 ? (const void*)usage_fast_kernel<2, true> : wb == 4 ? (const void*)usage_fast_kernel<4, true>
+                                                                                    : (const void*)usage_fast_kernel<8, true>)
+                        : (wb == 2 ? (const void*)usage_fast_kernel<2> : wb == 4 ? (const void*)usage_fast_kernel<4>
+                                                                                 : (const void*)usage_fast_kernel<8>);
     uint32_t grid = persist_grid(e, fk, ublocks);
     if (e->usage_blocks) grid = std::min(ublocks, (uint32_t)e->n_cus * e->usage_blocks);
     if (grid) {
-      if (wb == 2) hipLaunchKernelGGL(usage_fast_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      if (k8 && wb == 2) hipLaunchKernelGGL((usage_fast_kernel<2, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      else if (k8 && wb == 4) hipLaunchKernelGGL((usage_fast_kernel<4, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      else if (k8) hipLaunchKernelGGL((usage_fast_kernel<8, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
+      else if (wb == 2) hipLaunchKernelGGL(usage_fast_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
       else if (wb == 4) hipLaunchKernelGGL(usage_fast_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
       else hipLaunchKernelGGL(usage_fast_kernel<8>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
       HIP_TRY(hipGetLastError());

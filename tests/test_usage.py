@@ -284,3 +284,54 @@ def test_gpu_usage_fast_path_irregular_nodes(state):
         assert want[:, 0].min() == 0.0 and want[:, 0].max() > 0  # empty nodes and busy ones
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("state", ["auto", "u32"])
+def test_gpu_usage_key8_column_matches_4byte_keys(state):
+    """kwk_usage_config builds a 1-byte usage-key column when at most 256 distinct keys occur
+    (the C5 pods have 2): usage_fast_kernel<WB, true> must give node sums and integrators
+    bit-identical to the 4-byte-key kernel (KWK_TUNE_USAGE_KEY8 0), and equal to numpy."""
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+
+    cl, pods = _cluster(n_nodes=40, n_pods=6000, seed=29)
+    ptr = _irregular_node_ptr(len(pods))
+    rng = np.random.default_rng(3)
+    cv, mv = rng.random(60) * 4, rng.random(70) * 2**32
+    ci, mi, nc = rng.integers(0, 60, 200), rng.integers(0, 70, 200), rng.integers(1, 6, 200)
+    dict_keys = (ci | (mi << 14) | (nc << 28)).astype(np.uint32)  # 200 distinct keys
+    pick = rng.integers(0, 200, len(pods))
+    keys = dict_keys[pick]
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    cols = ing.columns(pods)
+    gone = np.arange(7, len(pods), 11)
+    alive = np.ones(len(pods), dtype=bool)
+    alive[gone] = False
+    t0 = 1_700_000_000 * 10**9
+    got = {}
+    for key8 in (1, 0):
+        eng = Engine(kp, capacity=len(pods), state=state)
+        try:
+            eng.set_tuning(abi.TUNE_USAGE_KEY8, key8)
+            eng.load_stages()
+            eng.load(*cols, ing.record_array())
+            eng.usage_config(ptr, keys, cv, mv)
+            eng.delete(gone)
+            eng.usage(t0)
+            eng.usage(t0 + 2 * 10**9)
+            got[key8] = eng.usage_read()
+        finally:
+            eng.close()
+    assert np.array_equal(got[1][0], got[0][0]) and np.array_equal(got[1][1], got[0][1])
+    node, total = got[1]
+    pod_c = np.where(alive, nc[pick] * cv[ci[pick]], 0.0)
+    pod_m = np.where(alive, nc[pick] * mv[mi[pick]], 0.0)
+    want = np.array([[pod_c[ptr[j]:ptr[j + 1]].sum(), pod_m[ptr[j]:ptr[j + 1]].sum()] for j in range(len(ptr) - 1)])
+    np.testing.assert_allclose(node[:, :2], want, rtol=REL_TOL, atol=0)
+    np.testing.assert_allclose(node[:, 2:], 2.0 * want, rtol=REL_TOL, atol=0)
+    np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
