@@ -385,6 +385,8 @@ def main():
     ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
     ap.add_argument("--tune-fsm-kernel", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
+    ap.add_argument("--tune-sweep-blocks", type=int, default=0,
+                    help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     args = ap.parse_args()
 
@@ -446,6 +448,9 @@ def main():
     if args.tune_q16:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_Q16, args.tune_q16)
+    if args.tune_sweep_blocks:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_SWEEP_BLOCKS, args.tune_sweep_blocks)
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)

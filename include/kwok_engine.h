@@ -203,6 +203,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    table-only kernel with 2 (default) or 1 tiles prefetched, or 0 = never */
 #define KWK_TUNE_USAGE_KEY8 6  /* usage fast path: 1-byte usage-key column when at most 256 distinct keys occur,
                                    1 (default) or 0 (the 4-byte keys) */
+#define KWK_TUNE_SWEEP_BLOCKS 7 /* persistent 2-byte sweep: blocks per CU of its grid, 0 (default: the occupancy
+                                   the HIP runtime reports) or 1..8 (fewer than the occupancy: an experiment knob) */
 #define KWK_TUNE_USAGE_BLOCKS 4 /* usage kernels: resident blocks per CU of the persistent grid, 0 (default:
                                    the occupancy the HIP runtime reports) or 1..8 */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);

@@ -2622,6 +2622,7 @@ struct kwk_engine {
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
+  uint32_t sweep_blocks = 0;  // persistent 2-byte sweep: resident blocks per CU (0: the occupancy)
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
   uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
@@ -2985,6 +2986,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
       e->fsm_kernel = value;
       return KWK_OK;
+    case KWK_TUNE_SWEEP_BLOCKS:
+      if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_SWEEP_BLOCKS: 0..8");
+      e->sweep_blocks = value;
+      return KWK_OK;
     case KWK_TUNE_USAGE_KEY8:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
       e->usage_key8 = value != 0;
@@ -3276,7 +3281,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const void* pk = lean ? (e->fsm_kernel == 2 ? (const void*)sweep16_fsm_kernel<HV, QV, true, 2>              \
                                                 : (const void*)sweep16_fsm_kernel<HV, QV, true, 1>)             \
                           : (const void*)sweep16_kernel<HV, QV, true>;                                          \
-    const uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;                                      \
+    uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;                                            \
+    if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);           \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
       if (lean)                                                                                                 \
         hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
