@@ -459,6 +459,9 @@ kwk_status kwk_aggregate_read(kwk_engine* eng, double* host_out, uint32_t n);
  * internal fired segments and per-segment counts (valid after kwk_fired) */
 kwk_status kwk_device_ptrs(kwk_engine* eng, void** state, void** fired, void** wave_counts);
 
+/* the engine's HIP stream (hipStream_t): in-process consumers order their own work after the
+ * engine's (e.g. an RCCL all-reduce of kwk_aggregate's output) with stream waits, no host sync */
+kwk_status kwk_stream(kwk_engine* eng, void** stream);
 /* HIP events recorded on the engine's stream (live kernel timing in bench.py) */
 kwk_status kwk_event_record(kwk_engine* eng, uint32_t idx);
 kwk_status kwk_event_elapsed(kwk_engine* eng, uint32_t a, uint32_t b, float* ms);

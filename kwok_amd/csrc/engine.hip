@@ -4181,6 +4181,12 @@ kwk_status kwk_device_ptrs(kwk_engine* e, void** hot, void** fired, void** wave_
 }
 
 // ---- timing helpers (HIP events on the engine's own stream; bench.py)
+kwk_status kwk_stream(kwk_engine* e, void** stream) {
+  if (!e || !stream) return fail(KWK_EINVAL, "null argument");
+  *stream = (void*)e->stream;
+  return KWK_OK;
+}
+
 kwk_status kwk_event_record(kwk_engine* e, uint32_t idx) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;

@@ -100,9 +100,9 @@ class DeviceReport:
     """A reporting interval's aggregates computed on the device (kwk_aggregate) with no host
     round trip: per engine [transitions per stage | counts per mask | cluster usage] as float64,
     laid out back to back — in one torch device buffer all-reduced in place over RCCL when the
-    job has several ranks, else in each engine's own buffer.  `collect` only enqueues (plus, with
-    several ranks, one wait for the engines' streams before the collective); `result` reads the
-    last interval back."""
+    job has several ranks, else in each engine's own buffer.  `collect` only enqueues: with
+    several ranks the collective is ordered after the engines' streams by stream waits (no host
+    synchronisation); `result` reads the last interval back."""
 
     def __init__(self, engines, count_masks, count_names, usage_engine=None, dist=None, device=None):
         self.engines, self.masks, self.count_names, self.usage_engine = engines, count_masks, count_names, usage_engine
@@ -122,9 +122,22 @@ class DeviceReport:
             assert n == size, (n, size)
             off += size
         if self.buf is not None:
-            for e in self.engines:
-                e.sync()
-            self.dist.all_reduce(self.buf)  # RCCL over xGMI
+            if self.buf.is_cuda:
+                # stream order, no host sync: the collective's stream waits for the engines'
+                # streams, and the engines' later work (the next interval writes this buffer)
+                # waits for the collective
+                import torch
+                cur = torch.cuda.current_stream(self.buf.device)
+                ext = [torch.cuda.ExternalStream(e.stream_handle(), device=self.buf.device) for e in self.engines]
+                for x in ext:
+                    cur.wait_stream(x)
+                self.dist.all_reduce(self.buf)  # RCCL over xGMI
+                for x in ext:
+                    x.wait_stream(cur)
+            else:
+                for e in self.engines:
+                    e.sync()
+                self.dist.all_reduce(self.buf)
         self.collected = True
 
     def result(self) -> Aggregates:

@@ -435,6 +435,12 @@ class Engine:
         abi.check(abi.lib().kwk_lease_sync_pods(pods.h, self.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_lease_sync_pods")
 
     # timing
+    def stream_handle(self) -> int:
+        """kwk_stream: the engine's hipStream_t (for torch.cuda.ExternalStream)."""
+        h = C.c_void_p()
+        abi.check(abi.lib().kwk_stream(self.h, C.byref(h)), "kwk_stream")
+        return int(h.value or 0)
+
     def event_record(self, idx: int):
         abi.check(abi.lib().kwk_event_record(self.h, idx), "kwk_event_record")
 
