@@ -149,8 +149,25 @@ EV_EVERY = 2  # HIP events bracket the pod sweep of every 2nd step: each marker 
 
 
 def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None):
-    """Steps k0..k1-1; ev_base: record HIP events (pod stream) around the pod sweep of every
-    EV_EVERY-th step (events 2i, 2i+1 of sample i)."""
+    """Steps k0..k1-1; ev_base (0): record HIP events (pod stream) around the pod sweep of every
+    EV_EVERY-th step (events 2i, 2i+1 of sample i).  Each engine's steps up to the next
+    reporting point are enqueued by one native call (kwk_step_n: sweep + device compaction per
+    step, the same work as the per-step calls); the pinned-copy run keeps one call per step."""
+    assert ev_base in (None, 0)
+    if pinned is None:
+        last, k = None, k0
+        while k < k1:
+            j = k - k0
+            end = k1
+            if reporter is not None and report_every:
+                end = min(k1, k0 + (j // report_every + 1) * report_every)
+            now = NOW0 + k * dt
+            pods.step_n(end - k, now, dt, seed, k, True, EV_EVERY if ev_base is not None else 0, j)
+            nodes.step_n(end - k, now, dt, seed, k, True)
+            k = end
+            if reporter is not None and report_every and (k - k0) % report_every == 0:
+                last = reporter.collect(NOW0 + (k - 1) * dt)
+        return last, 0
     last = None
     n_fired_host = 0
     for k in range(k0, k1):

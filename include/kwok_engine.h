@@ -269,6 +269,12 @@ kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t st
  * direct DMA — and synchronises.  Records are grouped by sweep region (ascending regions of
  * 512-2048 slots), unordered within a region; each fired slot appears once. */
 kwk_status kwk_fired_compact(kwk_engine* eng);
+/* n steps (now0 + k * dt, step0 + k for k < n), each followed by kwk_fired_compact when compact != 0:
+ * the per-tick loop of kwk_step / kwk_fired_compact enqueued by one call (enqueue only).  With
+ * ev_every > 0, events 2i / 2i + 1 (kwk_event_record) bracket the sweep of every step whose
+ * index j = ev_j0 + k is a multiple of ev_every (i = j / ev_every). */
+kwk_status kwk_step_n(kwk_engine* eng, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
+                      uint32_t compact, uint32_t ev_every, uint32_t ev_j0);
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 /* device pointers of the compacted list and of its u32 count (valid until the next kwk_step) */
 kwk_status kwk_fired_device(kwk_engine* eng, const kwk_fired_rec** recs, const uint32_t** count);

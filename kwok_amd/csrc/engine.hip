@@ -3382,6 +3382,24 @@ kwk_status kwk_fired_compact(kwk_engine* e) {
   return enqueue_compact(e);
 }
 
+kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
+                      uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t j = ev_j0 + k;
+    const bool ev = ev_every && j % ev_every == 0;
+    if (ev)
+      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every))) return st;
+    if (kwk_status st = launch_sweep(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, true)) return st;
+    if (ev)
+      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
+    if (compact)
+      if (kwk_status st = enqueue_compact(e)) return st;
+  }
+  return KWK_OK;
+}
+
 kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
   if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");

@@ -229,6 +229,12 @@ class Engine:
     def step(self, now_ns: int, seed: int, step: int):
         abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
+    def step_n(self, n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact: bool = True, ev_every: int = 0,
+               ev_j0: int = 0):
+        """kwk_step_n: n steps (+ device compaction after each) enqueued by one call."""
+        abi.check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, 1 if compact else 0, ev_every, ev_j0),
+                  "kwk_step_n")
+
     def fired_compact(self):
         """kwk_fired_compact: the last step's fired list compacted on the device (enqueue only)."""
         abi.check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")

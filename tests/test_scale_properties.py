@@ -231,3 +231,34 @@ def test_c2_mix_formats_and_shards_agree_at_4m_pods():
     finally:
         for _, e in eng.values():
             e.close()
+
+
+def test_step_n_equals_per_step_calls():
+    """kwk_step_n (the bench's per-interval call) enqueues exactly the per-tick kwk_step +
+    kwk_fired_compact sequence: same states, statistics and last fired list, with and without
+    the event samples."""
+    engines = {name: _pods("auto", n_nodes=20_000)[1] for name in ("calls", "n", "n_ev")}
+    try:
+        now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
+        for k in range(7):
+            engines["calls"].step(now0 + k * dt, seed, k)
+            engines["calls"].fired_compact()
+        engines["n"].step_n(3, now0, dt, seed, 0)
+        engines["n"].step_n(4, now0 + 3 * dt, dt, seed, 3)
+        engines["n_ev"].step_n(7, now0, dt, seed, 0, True, 2, 0)
+        ref = engines["calls"]
+        r_hot, r_del = ref.read()
+        r_fired = _fired_key(ref.fired())
+        assert len(r_fired) > 0
+        for name in ("n", "n_ev"):
+            e = engines[name]
+            hot, dels = e.read()
+            for col in ("pred", "sched"):
+                assert np.array_equal(hot[col], r_hot[col]), (name, col)
+            assert np.array_equal(_fired_key(e.fired()), r_fired), name
+            for key in ("fired", "matched", "bytes", "line_bytes", "steps"):
+                assert e.stats()[key] == ref.stats()[key], (name, key)
+        assert engines["n_ev"].event_elapsed_ms(4, 5) > 0.0  # sample 2 = step 4
+    finally:
+        for e in engines.values():
+            e.close()
