@@ -2380,6 +2380,74 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
     part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < (uint32_t)NM ? s_cnt[threadIdx.x] : 0u;
 }
 
+// 2-byte words, at most 4 masks and 11 pred bits (pod-fast, node kinds): one LDS lookup per word
+// instead of the SWAR mask tests (~36 VALU per dword at 4 masks, r2zd).  Entry (pred bits |
+// alive << pred_bits) holds, in byte m, 1 if the word counts for mask m; the lane adds entries into
+// one packed counter and unpacks it every 32 words.  Same partial rows as count_kernel.
+constexpr uint32_t kCountLutBits = 12;
+__global__ __launch_bounds__(kBlock) void count16_lut_kernel(const void* __restrict__ st, uint32_t n, uint32_t abit,
+                                                             uint32_t pmask, const uint32_t* __restrict__ masks,
+                                                             uint32_t n_masks, uint32_t* __restrict__ part) {
+  __shared__ uint32_t s_lut[1u << kCountLutBits];
+  __shared__ unsigned int s_cnt[4];
+  const uint32_t pb = 32u - (uint32_t)__clz(pmask);  // pmask = 2^pb - 1
+  const uint32_t apos = (uint32_t)__ffs(abit) - 1u;
+  uint32_t mk[4], every[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t x = (uint32_t)m < n_masks ? masks[m] : 0u;
+    mk[m] = (uint32_t)m < n_masks ? x & pmask : 0u;
+    every[m] = ((uint32_t)m < n_masks && x == 0u) ? 1u : 0u;
+  }
+  for (uint32_t e = threadIdx.x; e < (2u << pb); e += kBlock) {
+    const uint32_t pred = e & pmask, al = e >> pb;
+    uint32_t v = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v |= (al & ((every[m] | ((pred & mk[m]) != 0u ? 1u : 0u)))) << (8 * m);
+    s_lut[e] = v;
+  }
+  if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+  const uint64_t n_chunks = ((uint64_t)n * 2u + 15u) / 16u;
+  const uint4* __restrict__ q = reinterpret_cast<const uint4*>(st);
+  constexpr uint32_t kCountU = 4;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock * kCountU + threadIdx.x; c0 < n_chunks;
+       c0 += (uint64_t)gridDim.x * kBlock * kCountU) {
+    uint4 vs[kCountU];
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u) {
+      const uint64_t c = c0 + u * kBlock;
+      vs[u] = c < n_chunks ? q[c] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    uint32_t acc = 0;  // byte m: words counted for mask m (at most 32 per group)
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u) {
+      const uint64_t i0 = (c0 + u * kBlock) * 8u;
+      const bool whole = i0 + 8u <= n;
+      const uint32_t dw[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const uint32_t w = (h & 1) ? dw[h >> 1] >> 16 : dw[h >> 1] & 0xFFFFu;
+        uint32_t idx = (w & pmask) | (((w >> apos) & 1u) << pb);
+        if (!whole && i0 + (uint64_t)h >= n) idx = 0u;  // entry 0: not alive, counts nothing
+        acc += s_lut[idx];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cnt[m] += (acc >> (8 * m)) & 0xFFu;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    uint32_t c = cnt[m];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxCountMasks)
+    part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < 4u ? s_cnt[threadIdx.x] : 0u;
+}
+
 // out[m] = sum over the blocks' partial rows (1024 threads: 16 masks x 64 block strides)
 __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
                                                            uint32_t n_masks, unsigned long long* __restrict__ out) {
@@ -2399,7 +2467,9 @@ __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __res
 template <uint32_t WB>
 static void launch_count(uint32_t n_masks, dim3 g, hipStream_t s, const void* st, uint32_t n, uint32_t abit,
                          uint32_t pmask, const uint32_t* masks, uint32_t* part, unsigned long long* out) {
-  if (n_masks <= 2) hipLaunchKernelGGL((count_kernel<WB, 2>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  if (WB == 2 && n_masks <= 4 && pmask < (1u << (kCountLutBits - 1)) && abit > pmask)
+    hipLaunchKernelGGL(count16_lut_kernel, g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  else if (n_masks <= 2) hipLaunchKernelGGL((count_kernel<WB, 2>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
   else if (n_masks <= 4) hipLaunchKernelGGL((count_kernel<WB, 4>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
   else if (n_masks <= 8) hipLaunchKernelGGL((count_kernel<WB, 8>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
   else hipLaunchKernelGGL((count_kernel<WB, 16>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
