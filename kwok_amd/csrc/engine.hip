@@ -1487,6 +1487,14 @@ struct CompactArgs {
 
 // one wave per segment; the first 256 records are loaded together with the segment's count and
 // offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it)
+// one kwk_fired_rec {slot, stage, flags} from a packed record, nontemporal (the dense list is
+// written once per step and read by the consumer later: keeping it out of L2 leaves room for
+// the segments being read)
+__device__ __forceinline__ void store_rec_nt(kwk_fired_rec* p, uint32_t slot, uint32_t x) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(u32x2{slot, ((x >> 13) & 31u) | ((x >> 18) & 7u) << 16}, reinterpret_cast<u32x2*>(p));
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1506,12 +1514,11 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const uint32_t j = lane + 64u * k;
-    if (j < c)
-      a.out[off + j] = kwk_fired_rec{base + (r[k] & 0x1FFFu), (uint16_t)((r[k] >> 13) & 31u), (uint16_t)((r[k] >> 18) & 7u)};
+    if (j < c) store_rec_nt(&a.out[off + j], base + (r[k] & 0x1FFFu), r[k]);
   }
   for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
     const uint32_t x = f32[j];
-    a.out[off + j] = kwk_fired_rec{base + (x & 0x1FFFu), (uint16_t)((x >> 13) & 31u), (uint16_t)((x >> 18) & 7u)};
+    store_rec_nt(&a.out[off + j], base + (x & 0x1FFFu), x);
   }
 }
 
