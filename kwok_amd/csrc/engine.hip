@@ -936,6 +936,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   X.s2 = (R.smask << R.sshift) * 0x10001u; X.n2 = (R.none_code << R.sshift) * 0x10001u;
   X.sm = (uint32_t)(16 - __ffs(R.managed)) & 31u; X.sd = (uint32_t)(16 - __ffs(R.dirty)) & 31u;
   X.sa = (uint32_t)(16 - __ffs(R.alive)) & 31u; X.sl = (uint32_t)(16 - __ffs(R.del)) & 31u;
+  uint32_t stc01 = 0, stc23 = 0;        // per lane: fired records of stages 0 | 1 << 16, 2 | 3 << 16
   uint32_t n_matched = 0, n_bytes = 0;  // per lane: matches, algorithmic bytes
   uint32_t n_lline = 0;                 // per lane: bytes of the phase-3 line stores
   uint32_t w_bytes = 0, w_line = 0;     // wave-uniform: algorithmic bytes, line bytes - algorithmic bytes (mod 2^32)
@@ -1048,9 +1049,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
         seg_n += nf;
         w_bytes += 4u * nf;
         const uint32_t code = fire ? ((e >> 16) & 31u) : 31u;
-        for (uint32_t st = 0; st < n_stages; ++st) {  // per-stage counts: one ballot per stage
-          const unsigned long long same = __ballot(code == st);
-          if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
+        if (n_stages <= 4) {  // per-lane 16-bit counters, stages 0-1 / 2-3 (reduced once per block)
+          const uint32_t inc = 1u << (16u * (code & 1u));
+          stc01 += code < 2u ? inc : 0u;
+          stc23 += (code - 2u) < 2u ? inc : 0u;
+        } else {
+          for (uint32_t st = 0; st < n_stages; ++st) {  // one ballot per stage
+            const unsigned long long same = __ballot(code == st);
+            if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
+          }
         }
       }
     };
@@ -1162,7 +1169,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
     n_bytes += __shfl_xor(n_bytes, off);
     n_lline += __shfl_xor(n_lline, off);
   }
+  uint32_t stn[4] = {stc01 & 0xFFFFu, stc01 >> 16, stc23 & 0xFFFFu, stc23 >> 16};
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+    for (int off = 32; off > 0; off >>= 1) stn[st] += __shfl_xor(stn[st], off);
   if (lane == 0) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      if (stn[st]) atomicAdd(&s_stat[3 + st], stn[st]);
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], wave_fired);
     atomicAdd(&s_stat[2], n_bytes + w_bytes);

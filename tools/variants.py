@@ -29,6 +29,7 @@ _NOCALL = ("          const uint2 r = general16<kHarness>(wbase + w, (uint32_t)t
 
 VARIANTS = {
     "base": [],
+    "head": [],
     # phase 2 of the word sweep does nothing (no state change, no fires)
     "w_nophase2": [(_P2, "const uint2 nv = s; (void)due; (void)i; (void)gen_unused; (void)due_unused;")],
     # jitter without its Philox draw
@@ -74,6 +75,9 @@ def build(names):
 
     def one(name):
         s = src
+        if name == "head":  # the committed engine.hip: same-box A/B against the working tree ("base")
+            s = subprocess.run(["git", "show", "HEAD:kwok_amd/csrc/engine.hip"], cwd=ROOT, check=True,
+                               capture_output=True, text=True).stdout
         for old, new in VARIANTS[name]:
             if old not in s:
                 raise SystemExit(f"variant {name}: pattern not found: {old[:60]!r}")
