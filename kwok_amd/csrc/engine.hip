@@ -1032,7 +1032,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
       for (int b = 0; b < B; ++b) {
         const uint32_t c = c0 + 64u * b + lane;
         const bool in = c < n_work;
-        const uint32_t x = in ? (uint32_t)wl[c & (kWave - 1u)] : 0u;
+        const uint32_t x0 = (uint32_t)wl[c & (kWave - 1u)];  // read unconditionally (no exec branch)
+        const uint32_t x = in ? x0 : 0u;
         we[b] = in ? x : 0xFFFFFFFFu;
         raw[b] = (uint32_t)tw[x & 0x7FFFu];
         ent[b] = __builtin_amdgcn_raw_buffer_load_b32(fsm_rs, in ? ((((x >> 15) << fbits) | raw[b]) * 4u) : kOOB, 0, 0);
