@@ -1537,6 +1537,33 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   }
 }
 
+// Hand-back in one launch for small sweeps (at most kSmallSegs segments: the node kinds, the
+// strong-scaling shards): each block sums the counts of every segment before its own (at most
+// 32 KB, L2-resident) instead of waiting for seg_scan_kernel, then expands its four segments as
+// compact_kernel does.  Saves one launch and its gap per step.
+constexpr uint32_t kSmallSegs = 8192;
+__global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  __shared__ uint32_t s_seg[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t first = blockIdx.x * kSegsPerBlock;  // the block's first segment
+  uint32_t sum = 0;
+  for (uint32_t j = threadIdx.x; j < first; j += kBlock) sum += a.counts[j];
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) s_part[wave] = sum;
+  if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < a.n_segs ? a.counts[first + threadIdx.x] : 0u;
+  __syncthreads();
+  const uint32_t seg = first + wave;
+  if (seg >= a.n_segs) return;
+  uint32_t off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
+  const uint32_t c = s_seg[wave];
+  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
+  const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
+  const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
+  for (uint32_t j = lane; j < c; j += 64) store_rec_nt(&a.out[off + j], base + (f32[j] & 0x1FFFu), f32[j]);
+}
+
 // sums the per-block statistics rows [0, n_blocks) (the rows any sweep grid has used)
 __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, uint32_t n_blocks,
                                     unsigned long long* __restrict__ out) {
@@ -3451,8 +3478,6 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   e->compacted = true;
   if (n_waves == 0) return KWK_OK;
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
-  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
-                     e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
   CompactArgs a;
   a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
   a.counts = e->d_wave_counts;
@@ -3463,6 +3488,13 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   a.seg_region_shift = e->last_region_shift;
   a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
+  if (n_waves <= kSmallSegs) {  // one launch: prefix sums inside the expansion
+    hipLaunchKernelGGL(compact_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
+  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
+                     e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
   hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
