@@ -199,8 +199,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_FSM 1        /* 2-byte sweep: precomputed transition table, 1 (default) or 0 */
 #define KWK_TUNE_Q16 2        /* 2-byte sweep: 16-byte chunks per lane, 4 (default), 2 or 1 */
 #define KWK_TUNE_PERSIST16 3  /* 2-byte sweep: persistent grid for large engines, 1 (default) or 0 */
-#define KWK_TUNE_FSM_KERNEL 5  /* 2-byte sweep with a transition table free of general entries: the
-                                   table-only kernel with 2 (default) or 1 tiles prefetched, or 0 = never */
+#define KWK_TUNE_FSM_KERNEL 5  /* 2-byte sweep with a transition table: the table-only kernel (general
+                                   entries deferred to its cold loop) with 2 (default) or 1 tiles
+                                   prefetched, or 0 = the general sweep16 kernel */
 #define KWK_TUNE_USAGE_KEY8 6  /* usage fast path: 1-byte usage-key column when at most 256 distinct keys occur,
                                    1 (default) or 0 (the 4-byte keys) */
 #define KWK_TUNE_SWEEP_BLOCKS 7 /* persistent 2-byte sweep: blocks per CU of its grid, 0 (default: the occupancy

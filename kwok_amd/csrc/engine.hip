@@ -2748,7 +2748,6 @@ struct kwk_engine {
   int64_t* d_fsm_due = nullptr;
   uint32_t fsm_bits = 0;
   int fsm_harness = -1;       // harness enable the table was built for (-1: no table)
-  bool fsm_pure = false;      // the table has no general entry: sweep16_fsm_kernel can run
   uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_FSM_KERNEL: 0 never, else its prefetch depth
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
@@ -3361,11 +3360,7 @@ static kwk_status build_fsm(kwk_engine* e) {
     hipLaunchKernelGGL(fsm_build_kernel<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, e->d_fsm,
                        e->d_fsm_due);
   HIP_TRY(hipGetLastError());
-  std::vector<uint32_t> tab(n);
-  HIP_TRY(hipMemcpyAsync(tab.data(), e->d_fsm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  e->fsm_pure = true;
-  for (uint32_t x : tab) e->fsm_pure &= !(x & kFsmGeneral);
   e->fsm_harness = a.harness.enable ? 1 : 0;
   return KWK_OK;
 }
