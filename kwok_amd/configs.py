@@ -58,6 +58,20 @@ def _timed(engines_step, sync_engines, timing_engine, steps, warmup):
     return wall, timing_engine.event_elapsed_ms(0, 1) / 1e3
 
 
+def _timed_n(run_n, sync_engines, timing_engine, steps, warmup):
+    run_n(0, warmup)
+    for e in sync_engines:
+        e.sync()
+    timing_engine.event_record(0)
+    t0 = time.perf_counter()
+    run_n(warmup, steps)
+    timing_engine.event_record(1)
+    for e in sync_engines:
+        e.sync()
+    wall = time.perf_counter() - t0
+    return wall, timing_engine.event_elapsed_ms(0, 1) / 1e3
+
+
 def run(config: str, steps: int, warmup: int, seed: int) -> dict:
     if config in ("C1", "C2"):
         n_nodes, n_pods = (1000, 100_000) if config == "C1" else (10_000, 1_000_000)
@@ -66,12 +80,12 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         nprog, nodes = _engine(cl.node_stage_files, cl.nodes.variants, cl.nodes.index, False, 1)
         dt = 10**9 if config == "C1" else 500 * 10**6
 
-        def step(k):
-            pods.step(NOW0 + k * dt, seed, k)
-            nodes.step(NOW0 + k * dt, seed, k)
+        def run_n(k0, n):  # kwk_step_n: the steps enqueued by one native call per engine
+            pods.step_n(n, NOW0 + k0 * dt, dt, seed, k0, False)
+            nodes.step_n(n, NOW0 + k0 * dt, dt, seed, k0, False)
 
         s0p, s0n = pods.stats(), nodes.stats()
-        wall, pod_s = _timed(step, (pods, nodes), pods, steps, warmup)
+        wall, pod_s = _timed_n(run_n, (pods, nodes), pods, steps, warmup)
         s1p, s1n = pods.stats(), nodes.stats()
         fired = (s1p["fired"] - s0p["fired"]) + (s1n["fired"] - s0n["fired"])
         pbytes = s1p["bytes"] - s0p["bytes"]
