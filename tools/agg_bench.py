@@ -32,7 +32,11 @@ def main():
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--pods-per-node", type=int, default=100)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--lib", default="", help="engine library to load (a tools/variants.py build)")
     args = ap.parse_args()
+    if args.lib:
+        from kwok_amd.host import abi
+        abi.LIB_PATH = os.path.abspath(args.lib)
     pods, nodes, (pvars, pidx) = bench.build_engines(0, args.nodes, args.pods_per_node, 0, 0x6B776F6B, 0.1)
     bench.configure_usage(pods, pvars, pidx, args.nodes, args.pods_per_node)
     for k in range(6):  # steady-state churn
