@@ -2043,10 +2043,32 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
       dkv[q] = make_uint4(c[0], c[1], c[2], c[3]);
     }
   };
+  // a chunk's node boundaries and its nodes' integrators, loaded one chunk ahead like its row
+  // (they were the first thing each chunk waited for: one global round trip per chunk)
+  uint32_t nnp[3];
+  double2 npc = make_double2(0.0, 0.0);
+  int64_t npl = INT64_MIN;
+  auto load_meta = [&](const uint4 c, uint32_t (&np)[3], double2& pc, int64_t& pl) {
+    const uint32_t na_ = c.z, nk_ = c.w - c.z;  // nk_ <= kUChunkNodes = 128: entries 0..128
+#pragma unroll
+    for (uint32_t t = 0; t < 3; ++t) {
+      const uint32_t j = lane + 64u * t;
+      np[t] = j <= nk_ ? a.node_ptr[na_ + j] : 0u;
+    }
+    pc = make_double2(0.0, 0.0);
+    pl = INT64_MIN;
+    if (lane < nk_) {
+      pc = reinterpret_cast<const double2*>(a.cum)[na_ + lane];
+      pl = a.last_t[na_ + lane];
+    }
+  };
+  uint4 nch2 = make_uint4(0u, 0u, 0u, 0u);  // descriptor two chunks ahead
   if (chunk < a.n_chunks) {
     nch = a.chunks[chunk];
     load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+    load_meta(nch, nnp, npc, npl);
   }
+  if (chunk + n_waves < a.n_chunks) nch2 = a.chunks[chunk + n_waves];
   if (kKey8) {
     for (uint32_t j = threadIdx.x; j < a.kv_n; j += kBlock) s_kv[j] = a.kv[j];
   } else {
@@ -2067,17 +2089,22 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
     for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
 #pragma unroll
     for (uint32_t q = 0; q < KQ; ++q) kv[q] = nkv[q];
+    uint32_t cnp[3];
+#pragma unroll
+    for (uint32_t t = 0; t < 3; ++t) cnp[t] = nnp[t];
+    const double2 pre_cum = npc;
+    const int64_t pre_last = npl;
     const uint32_t nxt = chunk + n_waves;
-    if (nxt < a.n_chunks) nch = a.chunks[nxt];
-    double2 pre_cum = make_double2(0.0, 0.0);
-    int64_t pre_last = INT64_MIN;
-    if (lane < nk) {
-      pre_cum = reinterpret_cast<const double2*>(a.cum)[na + lane];
-      pre_last = a.last_t[na + lane];
-    }
+    nch = nch2;  // the next chunk's descriptor, loaded one chunk ago
+    if (nxt + n_waves < a.n_chunks) nch2 = a.chunks[nxt + n_waves];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the previous chunk is done with sp / ss
-    for (uint32_t j = lane; j <= nk; j += 64) sp[j] = a.node_ptr[na + j];
-    if (nxt < a.n_chunks) load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+#pragma unroll
+    for (uint32_t t = 0; t < 3; ++t)
+      if (lane + 64u * t <= nk) sp[lane + 64u * t] = cnp[t];
+    if (nxt < a.n_chunks) {
+      load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
+      load_meta(nch, nnp, npc, npl);
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t k = lane; k < nk; k += 64)  // nodes without pods
       if (sp[k] == sp[k + 1]) ss[k] = make_double2(0.0, 0.0);
