@@ -1775,6 +1775,32 @@ __device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t
   }
 }
 
+// DPP helpers of the usage kernels' lane scans (GFX9 DPP: row_shr, row_bcast15/31, wave_shr);
+// a lane whose source is outside its row or the row mask keeps `old` (0.0 / the no-node key)
+template <int C, int RM>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, C, RM, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), C, RM, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int C, int RM>
+__device__ __forceinline__ uint32_t dpp_key(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFFu, (int)v, C, RM, 0xF, false);
+}
+template <int C, int RM>
+__device__ __forceinline__ void dpp_seg_step(double& sc, double& sm, const uint32_t key) {
+  const double uc = dpp_f64<C, RM>(sc), um = dpp_f64<C, RM>(sm);
+  const uint32_t uk = dpp_key<C, RM>(key);
+  if (uk == key) { sc += uc; sm += um; }
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // persistent grid: wave w takes chunks w, w + W, ... (W = waves in the grid); the next chunk's
 // descriptor and first row are requested before the current chunk is worked on, so each
 // wave keeps one chunk's loads in flight (one block per chunk paid 3 memory latencies per
@@ -1958,19 +1984,19 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
       const uint32_t key = (has && !last) ? k : 0xFFFFFFFFu;
       double sc = (has && !last) ? acc_c : 0.0, sm = (has && !last) ? acc_m : 0.0;
       if (lane == 0 && key == carry_k) { sc += carry_c; sm += carry_m; }
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double uc = __shfl_up(sc, o), um = __shfl_up(sm, o);
-        const uint32_t uk = __shfl_up(key, o);
-        if (lane >= (uint32_t)o && uk == key) { sc += uc; sm += um; }
-      }
+      dpp_seg_step<0x111, 0xF>(sc, sm, key);  // on DPP lane moves (dpp_seg_step)
+      dpp_seg_step<0x112, 0xF>(sc, sm, key);
+      dpp_seg_step<0x114, 0xF>(sc, sm, key);
+      dpp_seg_step<0x118, 0xF>(sc, sm, key);
+      dpp_seg_step<0x142, 0xA>(sc, sm, key);
+      dpp_seg_step<0x143, 0xC>(sc, sm, key);
       // the lane before a head ends with that node open: its scan value is the earlier share
-      double pc = __shfl_up(sc, 1), pm = __shfl_up(sm, 1);
+      double pc = dpp_f64<0x138, 0xF>(sc), pm = dpp_f64<0x138, 0xF>(sm);  // wave_shr:1
       if (lane == 0) { pc = carry_c; pm = carry_m; }
       if (head) finalize(head_k, head_c + pc, head_m + pm);
-      carry_c = __shfl(sc, 63);
-      carry_m = __shfl(sm, 63);
-      carry_k = __shfl(key, 63);
+      carry_c = readlane_f64(sc, 63);
+      carry_m = readlane_f64(sm, 63);
+      carry_k = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     // NodeResourceUsage (:195-224) and its integrator (nodeResourceCumulativeUsage, :67-109)
@@ -2011,32 +2037,6 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
 // the device loop would), and a node boundary inside a lane is a short masked branch.  Empty
 // nodes are written separately, so closing a node never loops.
 constexpr uint32_t kUFastVals = 2048;  // podv entries staged in LDS
-// DPP helpers of usage_fast_kernel's lane scan (GFX9 DPP: row_shr, row_bcast15/31, wave_shr);
-// a lane whose source is outside its row or the row mask keeps `old` (0.0 / the no-node key)
-template <int C, int RM>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, C, RM, 0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), C, RM, 0xF, false);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-template <int C, int RM>
-__device__ __forceinline__ uint32_t dpp_key(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFFu, (int)v, C, RM, 0xF, false);
-}
-template <int C, int RM>
-__device__ __forceinline__ void dpp_seg_step(double& sc, double& sm, const uint32_t key) {
-  const double uc = dpp_f64<C, RM>(sc), um = dpp_f64<C, RM>(sm);
-  const uint32_t uk = dpp_key<C, RM>(key);
-  if (uk == key) { sc += uc; sm += um; }
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
 // kKey8: the pods' usage keys as one byte each (an index into the distinct keys' {cpu, mem}
 // values, kwk_usage_config builds it when at most kUKeyDict keys occur): 16 bytes per lane's run
 // instead of 64, one LDS read per pod instead of two and no key decode
