@@ -469,7 +469,8 @@ kwk_status kwk_device_ptrs(kwk_engine* eng, void** state, void** fired, void** w
 /* the engine's HIP stream (hipStream_t): in-process consumers order their own work after the
  * engine's (e.g. an RCCL all-reduce of kwk_aggregate's output) with stream waits, no host sync */
 kwk_status kwk_stream(kwk_engine* eng, void** stream);
-/* HIP events recorded on the engine's stream (live kernel timing in bench.py) */
+/* HIP events recorded on the engine's stream (live kernel timing in bench.py); timing-only
+ * events without a system-scope fence: not a memory-visibility point for the host */
 kwk_status kwk_event_record(kwk_engine* eng, uint32_t idx);
 kwk_status kwk_event_elapsed(kwk_engine* eng, uint32_t a, uint32_t b, float* ms);
 uint32_t kwk_abi_version(void);
