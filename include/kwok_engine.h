@@ -208,6 +208,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    the HIP runtime reports) or 1..8 (fewer than the occupancy: an experiment knob) */
 #define KWK_TUNE_USAGE_BLOCKS 4 /* usage kernels: resident blocks per CU of the persistent grid, 0 (default:
                                    the occupancy the HIP runtime reports) or 1..8 */
+#define KWK_TUNE_COMPACT_SMALL 8 /* fired hand-back: the most segments compacted in one launch (each block sums
+                                   the counts before its own), 8192 (default) .. 65536; more use the scan +
+                                   expansion pair; 0 = always the pair */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
 
 /* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */

@@ -1537,11 +1537,10 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   }
 }
 
-// Hand-back in one launch for small sweeps (at most kSmallSegs segments: the node kinds, the
+// Hand-back in one launch for small sweeps (at most kwk_engine::compact_small segments, 8192 by default: the node kinds, the
 // strong-scaling shards): each block sums the counts of every segment before its own (at most
 // 32 KB, L2-resident) instead of waiting for seg_scan_kernel, then expands its four segments as
 // compact_kernel does.  Saves one launch and its gap per step.
-constexpr uint32_t kSmallSegs = 8192;
 __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   __shared__ uint32_t s_part[kWavesPerBlock];
   __shared__ uint32_t s_seg[kWavesPerBlock];
@@ -2848,6 +2847,7 @@ struct kwk_engine {
   double* d_podv = nullptr;       // usage_fast_kernel's pod values per (containers, value id)
   uint32_t podv_n = 0;
   uint32_t usage_blocks = 0;      // KWK_TUNE_USAGE_BLOCKS (0: occupancy API)
+  uint32_t compact_small = 8192;  // KWK_TUNE_COMPACT_SMALL (kSmallSegs)
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)
@@ -3173,6 +3173,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_USAGE_BLOCKS:
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
       e->usage_blocks = value;
+      return KWK_OK;
+    case KWK_TUNE_COMPACT_SMALL:
+      if (value > 65536) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..65536");
+      e->compact_small = value;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -3541,7 +3545,7 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   a.seg_region_shift = e->last_region_shift;
   a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
-  if (n_waves <= kSmallSegs) {  // one launch: prefix sums inside the expansion
+  if (n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
     hipLaunchKernelGGL(compact_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
     HIP_TRY(hipGetLastError());
     return KWK_OK;

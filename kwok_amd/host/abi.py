@@ -84,6 +84,7 @@ class EngineDesc(C.Structure):
 ENGINE_WIDE_STATE = 1
 ENGINE_STATE32 = 2
 TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_USAGE_BLOCKS, TUNE_FSM_KERNEL, TUNE_USAGE_KEY8, TUNE_SWEEP_BLOCKS = 1, 2, 3, 4, 5, 6, 7
+TUNE_COMPACT_SMALL = 8
 
 
 class Lease(C.Structure):

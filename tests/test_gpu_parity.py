@@ -16,18 +16,22 @@ pytestmark = pytest.mark.gpu
 FORMATS = ["auto", "u32", "wide"]
 
 
-@pytest.mark.parametrize("state", FORMATS + ["auto-nofsm", "auto-gen"])
+@pytest.mark.parametrize("state", FORMATS + ["auto-nofsm", "auto-gen", "auto-pair"])
 def test_pod_fast_c1_mini(state):
     """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in every
     device state format (auto = the 2-byte words of the whole-line sweep: the table-only
     kernel by default, the general sweep16_kernel with its transition table (auto-gen) and
-    without it (auto-nofsm))."""
+    without it (auto-nofsm)); auto-pair hands the fired list back through the scan + expansion
+    pair of large sweeps (KWK_TUNE_COMPACT_SMALL 0) instead of the one-launch compaction."""
     tuning = {}
     if state == "auto-nofsm":
         tuning = {abi.TUNE_FSM: 0}
         state = "auto"
     elif state == "auto-gen":
         tuning = {abi.TUNE_FSM_KERNEL: 0}
+        state = "auto"
+    elif state == "auto-pair":
+        tuning = {abi.TUNE_COMPACT_SMALL: 0}
         state = "auto"
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()

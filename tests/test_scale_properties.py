@@ -111,6 +111,29 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
             e.close()
 
 
+def test_handback_pair_equals_one_launch_at_4m_pods():
+    """The fired hand-back's two paths over the same step's segments: the one-launch compaction
+    (at most 8192 segments, the default here) and the scan + expansion pair the C5 sweep takes
+    (KWK_TUNE_COMPACT_SMALL 0) give the same dense list in the same order; every slot once."""
+    from kwok_amd.host import abi
+    prog, eng = _pods("auto")
+    try:
+        now0 = 1_700_000_000 * 10**9
+        for k in range(4):
+            eng.step(now0 + k * 10**9, 0x6B776F6B, k)
+            eng.set_tuning(abi.TUNE_COMPACT_SMALL, 8192)
+            eng.fired_compact()
+            one = eng.fired()
+            eng.set_tuning(abi.TUNE_COMPACT_SMALL, 0)
+            eng.fired_compact()
+            pair = eng.fired()
+            assert len(one) > 0 and np.array_equal(one, pair), f"step {k}"
+            sl = np.sort(pair["slot"].astype(np.int64))
+            assert np.all(np.diff(sl) > 0), f"step {k}: a slot fired twice"
+    finally:
+        eng.close()
+
+
 def test_aggregates_and_handback_at_17m_pods():
     """At 17M pods (the 2-byte sweep's persistent grid): kwk_count and kwk_usage against the
     state read back through kwk_read (numpy), and the device-compacted fired list (one
