@@ -404,6 +404,8 @@ def main():
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
     ap.add_argument("--tune-sweep-blocks", type=int, default=0,
                     help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
+    ap.add_argument("--tune-compact-small", type=int, default=-1,
+                    help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     args = ap.parse_args()
 
@@ -471,6 +473,9 @@ def main():
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
+    if args.tune_compact_small >= 0:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_COMPACT_SMALL, args.tune_compact_small)
     dt = args.dt_ms * 10**6
     reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None)
     report_every = 0 if args.pmc_child else args.report_every
