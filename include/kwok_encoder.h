@@ -34,7 +34,9 @@ typedef struct kwk_encoder kwk_encoder;
  * (KWK_FIRED_DELTA_UNKNOWN) */
 #define KWK_ENCODE_CLASS_UNKNOWN 0xFFFFFFFFu
 
-const char* kwk_encoder_last_error(void);
+/* message of the last failing call on handle h (per handle); h = NULL: the calling thread's
+ * last message (create) */
+const char* kwk_encoder_last_error(const kwk_encoder* h);
 kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out);
 kwk_status kwk_encoder_destroy(kwk_encoder* enc);
 /* objects i = buf[offsets[i], offsets[i+1]) (n + 1 offsets); rows as Ingest.columns gives them

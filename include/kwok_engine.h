@@ -27,7 +27,7 @@
  *      *CumulativeUsage integrators :36-109)
  *
  * Conventions: every function returns kwk_status (0 = ok, < 0 = error; message via
- * kwk_last_error).  No exceptions or panics cross the boundary.  Strings never cross it:
+ * kwk_last_error(eng), kept per engine).  No exceptions or panics cross the boundary.  Strings never cross it:
  * the host interns labels / annotations / phases / finalizers into feature bits and
  * pre-parses *From values.  All calls for one engine come from one thread (the reference
  * runs all matching for a kind on a single preprocess goroutine, pod_controller.go:150).
@@ -190,7 +190,10 @@ typedef struct {
 #define KWK_ENGINE_WIDE_STATE (1u << 0) /* always use the 8-byte state format (never a packed one) */
 #define KWK_ENGINE_STATE32 (1u << 1)    /* never the 2-byte packed format (4-byte packed or wide only) */
 
-const char* kwk_last_error(void);
+/* message of the last failing call on `eng` (kept per engine, so a caller that moves between OS
+ * threads between the failing call and this one — a Go goroutine — still reads its own message);
+ * eng = NULL: the calling thread's last message (kwk_engine_create, kwk_alloc_host / free_host) */
+const char* kwk_last_error(const kwk_engine* eng);
 kwk_status kwk_engine_create(const kwk_engine_desc* desc, kwk_engine** out);
 kwk_status kwk_engine_destroy(kwk_engine* eng);
 
@@ -209,7 +212,7 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_USAGE_BLOCKS 4 /* usage kernels: resident blocks per CU of the persistent grid, 0 (default:
                                    the occupancy the HIP runtime reports) or 1..8 */
 #define KWK_TUNE_COMPACT_SMALL 8 /* fired hand-back: the most segments compacted in one launch (each block sums
-                                   the counts before its own), 8192 (default) .. 65536; more use the scan +
+                                   the counts before its own), 0..8192 (default 8192); more use the scan +
                                    expansion pair; 0 = always the pair */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
 
@@ -270,8 +273,10 @@ kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t st
  * dense device list (enqueue only: call it after kwk_step to keep the list on the device, e.g.
  * for an in-process consumer through kwk_fired_device).  kwk_fired copies the LAST step's list
  * (compacting first if needed) into host memory — a kwk_alloc_host buffer makes the copy a
- * direct DMA — and synchronises.  Records are grouped by sweep region (ascending regions of
- * 512-2048 slots), unordered within a region; each fired slot appears once. */
+ * direct DMA — and synchronises.  Records are grouped by sweep region (ascending regions: a
+ * wave's 512-2048 slots in the 2-byte sweeps, a tile's 2048 / 4096 slots in the 8- / 4-byte word
+ * sweep), unordered within a region; each fired slot appears once.  A step that swept nothing
+ * (no active slots) leaves an empty list. */
 kwk_status kwk_fired_compact(kwk_engine* eng);
 /* n steps (now0 + k * dt, step0 + k for k < n), each followed by kwk_fired_compact when compact != 0:
  * the per-tick loop of kwk_step / kwk_fired_compact enqueued by one call (enqueue only).  With
@@ -442,6 +447,22 @@ kwk_status kwk_lease_stats(kwk_engine* nodes, kwk_lease_counters* out);
  * stage (podsOnNodeSyncWorker, controller.go:559-573) */
 kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr);
 
+/* The fused reconciliation tick (C3 and any node + pod deployment): the per-tick sequence of
+ *   kwk_lease_step(nodes) -> kwk_lease_sync_pods(pods, nodes, node_ptr) -> kwk_step(nodes) ->
+ *   kwk_step(pods)   (+ kwk_fired_compact on both with KWK_TICK_COMPACT)
+ * enqueued by one call, with the two engines' streams ordered by HIP events instead of host
+ * synchronisations (kwk_lease_sync_pods synchronises the node stream each call).  Results are
+ * those of the separate calls.  Lease ops / fired lists / stats are read as after the separate
+ * calls (kwk_lease_ops, kwk_fired on either engine).  kwk_tick_bind registers the pods' node_ptr
+ * (node-sorted pods, as kwk_lease_sync_pods) once; pods = NULL runs the node engine alone (its
+ * lease step only if kwk_lease_config was called).  kwk_tick_n: n ticks at now0 + k * dt,
+ * step0 + k (enqueue only; the last tick's lease ops / fired lists are readable). */
+#define KWK_TICK_COMPACT (1u << 0)
+kwk_status kwk_tick_bind(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr);
+kwk_status kwk_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t flags);
+kwk_status kwk_tick_n(kwk_engine* nodes, kwk_engine* pods, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed,
+                      uint64_t step0, uint32_t flags);
+
 /* cluster aggregates: counts[k] = alive objects with (pred & masks[k]) != 0 (mask 0 = all
  * alive objects), k < 16 — e.g. the phase histogram all-reduced across GPUs (synchronises) */
 kwk_status kwk_count(kwk_engine* eng, uint32_t n_masks, const uint32_t* masks, uint64_t* counts);
@@ -476,6 +497,23 @@ kwk_status kwk_stream(kwk_engine* eng, void** stream);
  * events without a system-scope fence: not a memory-visibility point for the host */
 kwk_status kwk_event_record(kwk_engine* eng, uint32_t idx);
 kwk_status kwk_event_elapsed(kwk_engine* eng, uint32_t a, uint32_t b, float* ms);
+/* which sweep kernel the last kwk_step / kwk_match launched (tests pin the benchmarked shape) */
+#define KWK_SWEEP_NONE 0     /* nothing swept (no active slots) */
+#define KWK_SWEEP_16 1       /* sweep16_kernel: 2-byte words, general phase 2 */
+#define KWK_SWEEP_16_FSM 2   /* sweep16_fsm_kernel: 2-byte words, transition table */
+#define KWK_SWEEP_W4 3       /* sweepw_kernel<4>: 4-byte packed words */
+#define KWK_SWEEP_W8 4       /* sweepw_kernel<8>: 8-byte wide words */
+typedef struct {
+  uint32_t kernel;       /* KWK_SWEEP_* */
+  uint32_t q;            /* 16-byte chunks per lane */
+  uint32_t persistent;   /* 1: persistent grid (grid < tiles) */
+  uint32_t depth;        /* tiles in flight per wave (table-only sweep) */
+  uint32_t grid;         /* workgroups launched */
+  uint32_t tiles;        /* tiles swept */
+  uint32_t harness;      /* 1: the harness variant */
+  uint32_t reserved;
+} kwk_sweep_info;
+kwk_status kwk_last_sweep(kwk_engine* eng, kwk_sweep_info* out);
 uint32_t kwk_abi_version(void);
 uint32_t kwk_tile_objects(void); /* objects per sweep workgroup */
 

@@ -51,7 +51,9 @@ typedef int32_t (*kwk_patch_fn)(void* user, uint32_t func_id, uint32_t argc, con
                                 const uint32_t* argl, const uint8_t* kinds, char* out, uint32_t cap,
                                 uint32_t* out_len);
 
-const char* kwk_patch_last_error(void);
+/* message of the last failing call on handle h (per handle); h = NULL: the calling thread's
+ * last message (create) */
+const char* kwk_patch_last_error(const kwk_patcher* h);
 
 /* spec_json: {"templates": [...], "funcs": [{"name", "const" | "callback"}], "consts": [...]}
  * as written by kwok_amd/host/patchtpl.py:PatchProgram */

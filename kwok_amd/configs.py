@@ -122,12 +122,11 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         nodes.lease_set(le)
         dt = 10 * 10**6
 
-        def step(k):
-            nodes.lease_step(NOW0 + k * dt, seed, k)
-            nodes.step(NOW0 + k * dt, seed, k)
+        def run_n(k0, n):  # kwk_tick_n: lease step + node step per tick, all ticks enqueued by one call
+            nodes.tick_n(None, n, NOW0 + k0 * dt, dt, seed, k0)
 
         s0, l0 = nodes.stats(), nodes.lease_stats()
-        wall, dev_s = _timed(step, (nodes,), nodes, steps, warmup)
+        wall, dev_s = _timed_n(run_n, (nodes,), nodes, steps, warmup)
         s1, l1 = nodes.stats(), nodes.lease_stats()
         fired = s1["fired"] - s0["fired"]
         writes = sum(l1[k] - l0[k] for k in ("creates", "renews", "acquires"))

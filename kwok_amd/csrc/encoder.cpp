@@ -30,9 +30,18 @@
 
 namespace {
 
+// the failing call's message: per handle (the call's own object, see ErrScope) and per thread
+// (calls without a handle: create)
 thread_local std::string g_err;
+thread_local std::string* tl_err = nullptr;
+struct ErrScope {
+  std::string* prev;
+  explicit ErrScope(std::string* target) : prev(tl_err) { tl_err = target; }
+  ~ErrScope() { tl_err = prev; }
+};
 kwk_status fail(kwk_status code, const std::string& msg) {
   g_err = msg;
+  if (tl_err) *tl_err = msg;
   return code;
 }
 
@@ -486,6 +495,7 @@ int64_t f64_to_i64(double x) {
 
 // ------------------------------------------------------------------ encoder
 struct kwk_encoder {
+  std::string err;  // message of the last failing call on this handle
   struct Feature {
     Query q;
     int32_t present_bit = -1;
@@ -693,7 +703,7 @@ void encode_one(const kwk_encoder& E, const char* text, uint32_t len, Row& r) {
 
 extern "C" {
 
-const char* kwk_encoder_last_error(void) { return g_err.c_str(); }
+const char* kwk_encoder_last_error(const kwk_encoder* h) { return h ? h->err.c_str() : g_err.c_str(); }
 
 kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out) {
   if (!spec_json || !out) return fail(KWK_EINVAL, "null argument");
@@ -734,12 +744,14 @@ kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out) {
 }
 
 kwk_status kwk_encoder_destroy(kwk_encoder* e) {
+  ErrScope es_(e ? &e->err : nullptr);
   delete e;
   return KWK_OK;
 }
 
 kwk_status kwk_encode(kwk_encoder* E, uint32_t n, const char* buf, const uint64_t* offsets, uint32_t n_threads,
                       kwk_hot* hot, int64_t* deletion_s, uint32_t* rec_idx, uint16_t* cls, uint32_t* n_unknown_class) {
+  ErrScope es_(E ? &E->err : nullptr);
   if (!E || (n && (!buf || !offsets || !hot || !deletion_s || !rec_idx || !cls))) return fail(KWK_EINVAL, "null argument");
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return fail(KWK_EINVAL, "offsets must be non-decreasing");
@@ -791,6 +803,7 @@ kwk_status kwk_encode(kwk_encoder* E, uint32_t n, const char* buf, const uint64_
 }
 
 kwk_status kwk_encoder_records(kwk_encoder* E, kwk_value* out, uint32_t cap, uint32_t* n_records) {
+  ErrScope es_(E ? &E->err : nullptr);
   if (!E || !n_records) return fail(KWK_EINVAL, "null argument");
   const size_t per = std::max<size_t>(1, E->slots.size());
   const uint32_t n = (uint32_t)(E->slots.empty() ? 0 : E->records.size() / per);

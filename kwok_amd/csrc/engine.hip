@@ -24,12 +24,15 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <set>
 #include <string>
 #include <type_traits>
 #include <utility>
 #include <vector>
 
 #include "../../include/kwok_engine.h"
+
+static void engine_set_error(kwk_engine* e, const std::string& msg);
 
 namespace {
 
@@ -42,10 +45,22 @@ constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kStatWords = 4 + KWK_MAX_STAGES;
 constexpr int kStatLine = 3 + KWK_MAX_STAGES;
 
+// Error messages: every failing call stores its message in the engine it was called on
+// (kwk_last_error(eng)), so a caller that moves between OS threads (a cgo goroutine) reads the
+// message of its own engine's call; calls without an engine (kwk_engine_create, pinned host
+// buffers) leave it in the calling thread's slot (kwk_last_error(NULL)).
 thread_local std::string g_err;
+thread_local kwk_engine* tl_eng = nullptr;  // the engine of the API call running on this thread
+
+struct ErrScope {  // marks the engine an API call works on, for fail()
+  kwk_engine* prev;
+  explicit ErrScope(const kwk_engine* e) : prev(tl_eng) { tl_eng = const_cast<kwk_engine*>(e); }
+  ~ErrScope() { tl_eng = prev; }
+};
 
 kwk_status fail(kwk_status code, const std::string& msg) {
   g_err = msg;
+  if (tl_eng) engine_set_error(tl_eng, msg);
   return code;
 }
 
@@ -1436,7 +1451,9 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
 // kScanGroup segments plus one total per group (all groups in parallel: a single-workgroup scan
 // over the ~50k counts of a 100M-object sweep was latency-bound, 18.5 us, r2b), then one wave
 // per segment adds the totals of the groups before its own and expands its 4-byte records
-// {slot within the wave region: 11, stage: 5, flags: 3} into kwk_fired_rec at its offset of one
+// {slot within the region: bits 0-12, stage: bits 13-17, flags: bits 18-20; a region is a wave's
+// words in the 2-byte sweeps (512-2048 slots), a tile's in the word sweep (2048 / 4096 slots)}
+// into kwk_fired_rec at its offset of one
 // dense list; the last segment's wave writes the list length.  (A single-pass decoupled
 // look-back was measured slower here: with ~12k tiny blocks the look-back chains, not the bytes,
 // set the time — 165 us vs the ~30 us the bytes need.)
@@ -2636,9 +2653,11 @@ __device__ __forceinline__ int64_t lease_next_try(int64_t renew_interval, int64_
   return expire;
 }
 
-__global__ __launch_bounds__(kBlock) void lease_kernel(LeaseArgs a) {
+__global__ __launch_bounds__(kBlock) void lease_kernel(LeaseArgs a, uint32_t* __restrict__ next_n_ops) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
+  // the API-write count of the NEXT lease step starts at 0 (no memset launch per tick)
+  if (i == 0) *next_n_ops = 0u;
   uint32_t op = 0;
   if (i < a.n) {
     kwk_lease L = a.lease[i];
@@ -2785,6 +2804,7 @@ struct kwk_engine {
   uint32_t last_objs = 16;    // words per lane of the last sweep (fired segment stride = 64 * last_objs + 32)
   uint32_t last_region_shift = 0;  // fired segments per record region = 1 << shift (wave: 0, tile: 2)
   bool compacted = false;     // the last sweep's fired list is compacted on the device
+  kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
   kwk_harness harness{};
@@ -2881,12 +2901,30 @@ struct kwk_engine {
   kwk_lease* d_lease = nullptr;
   uint8_t* d_lease_op = nullptr;
   kwk_fired_rec* d_lease_ops = nullptr;
-  uint32_t* d_lease_nops = nullptr;
+  uint32_t* d_lease_nops = nullptr;   // [2]: API writes of the last lease step / zeroed for the next one
+  uint32_t lease_par = 0;               // d_lease_nops entry the next lease step counts into
+  uint32_t lease_last = 0;              // entry of the last lease step (kwk_lease_ops)
+  // kwk_tick_bind (pod engines): the node engine whose lease results the fused tick applies
+  const kwk_engine* tick_nodes = nullptr;
+  uint32_t tick_n_nodes = 0;
+  uint32_t* d_tick_ptr = nullptr;       // node_ptr on the device
+  hipEvent_t ev_lease = nullptr;        // node stream: the tick's lease step is done
+  hipEvent_t ev_podsync = nullptr;      // pod stream: the tick's pod sync has read the lease results
+  bool tick_pending = false;            // ev_podsync recorded by an earlier tick
+  kwk_engine* tick_pods = nullptr;      // node engines: the pod engine of the last fused tick
   unsigned long long* d_lease_stats = nullptr;
   uint64_t lease_steps = 0;
 
   std::vector<hipEvent_t> events;
+  std::string err;            // message of the last failing call on this engine (kwk_last_error)
 };
+
+static void engine_set_error(kwk_engine* e, const std::string& msg) { e->err = msg; }
+
+// live engines: a fused tick links a pod engine and a node engine; destroying either unlinks it
+static std::mutex g_live_mu;
+static std::set<kwk_engine*> g_live;
+
 
 // narrow iff pred + class + stage code + 5 flag bits fit 32 bits, half iff they fit 16
 // 
@@ -2971,7 +3009,7 @@ static kwk_status ensure_stage_buf(kwk_engine* e, size_t bytes) {
 
 extern "C" {
 
-const char* kwk_last_error(void) { return g_err.c_str(); }
+const char* kwk_last_error(const kwk_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
 
 kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   if (!d || !out) return fail(KWK_EINVAL, "null argument");
@@ -3033,12 +3071,26 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.insert(e);
+  }
   *out = e;
   return KWK_OK;
 }
 
 kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (!e) return KWK_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.erase(e);
+    kwk_engine* tn = const_cast<kwk_engine*>(e->tick_nodes);
+    if (tn && g_live.count(tn) && tn->tick_pods == e) tn->tick_pods = nullptr;
+    if (e->tick_pods && g_live.count(e->tick_pods) && e->tick_pods->tick_nodes == e) {
+      e->tick_pods->tick_nodes = nullptr;
+      e->tick_pods->tick_n_nodes = 0;
+    }
+  }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
@@ -3049,6 +3101,9 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
                   e->d_lease_nops, e->d_lease_stats, e->d_ukey8, e->d_kv};
   for (void* p : ptrs) if (p) hipFree(p);
+  if (e->d_tick_ptr) hipFree(e->d_tick_ptr);
+  if (e->ev_lease) hipEventDestroy(e->ev_lease);
+  if (e->ev_podsync) hipEventDestroy(e->ev_podsync);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
@@ -3056,6 +3111,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
 }
 
 kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_delta* deltas) {
+  ErrScope es_(e);
   if (!e || !t) return fail(KWK_EINVAL, "null argument");
   if (t->n_stages > KWK_MAX_STAGES) return fail(KWK_EINVAL, "too many stages");
   if (t->n_classes == 0 && t->n_stages) return fail(KWK_EINVAL, "n_classes must be > 0");
@@ -3142,6 +3198,7 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
 }
 
 kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   switch (key) {
@@ -3175,7 +3232,9 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       e->usage_blocks = value;
       return KWK_OK;
     case KWK_TUNE_COMPACT_SMALL:
-      if (value > 65536) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..65536");
+      // each block of the one-launch compaction re-sums every count before its segments: the
+      // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
+      if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
       return KWK_OK;
     default:
@@ -3184,6 +3243,7 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
 }
 
 kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
+  ErrScope es_(e);
   if (!e || !h) return fail(KWK_EINVAL, "null argument");
   e->harness = *h;
   if (kwk_status st = set_dev(e)) return st;
@@ -3192,6 +3252,7 @@ kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
 
 kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t* del, const uint32_t* rec,
                     const uint16_t* cls, uint32_t n_records, const kwk_value* records) {
+  ErrScope es_(e);
   if (!e || (n && (!hot || !del || !rec || !cls))) return fail(KWK_EINVAL, "null argument");
   if (n > e->capacity) return fail(KWK_ECAP, "n exceeds capacity");
   if (n_records > e->max_records) return fail(KWK_ECAP, "n_records exceeds max_records");
@@ -3228,6 +3289,7 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
 }
 
 kwk_status kwk_set_records(kwk_engine* e, uint32_t first, uint32_t n, const kwk_value* records) {
+  ErrScope es_(e);
   if (!e || (n && !records)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > e->max_records) return fail(KWK_ECAP, "records exceed max_records");
   if (kwk_status st = set_dev(e)) return st;
@@ -3242,11 +3304,13 @@ static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots,
 
 kwk_status kwk_upsert(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
                       const uint32_t* rec, const uint16_t* cls) {
+  ErrScope es_(e);
   return scatter_rows(e, n, slots, hot, del, rec, cls, 1u);
 }
 
 kwk_status kwk_replace(kwk_engine* e, uint32_t n, const uint32_t* slots, const kwk_hot* hot, const int64_t* del,
                        const uint32_t* rec, const uint16_t* cls) {
+  ErrScope es_(e);
   return scatter_rows(e, n, slots, hot, del, rec, cls, 0u);
 }
 
@@ -3291,6 +3355,7 @@ static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots,
 }
 
 kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
+  ErrScope es_(e);
   if (!e || (n && !slots)) return fail(KWK_EINVAL, "null argument");
   if (n == 0) return KWK_OK;
   for (uint32_t j = 0; j < n; ++j)
@@ -3309,6 +3374,7 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
 kwk_status kwk_retry(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n, const uint32_t* slots,
                      const kwk_hot* hot, const uint16_t* cls, const uint16_t* stages, const uint32_t* retry_count,
                      const kwk_backoff* backoff) {
+  ErrScope es_(e);
   if (!e || !backoff || (n && (!slots || !hot || !cls || !stages || !retry_count)))
     return fail(KWK_EINVAL, "null argument");
   if (n == 0) return KWK_OK;
@@ -3431,6 +3497,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   e->compacted = false;
+  e->last_sweep = kwk_sweep_info{};
   if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
@@ -3459,6 +3526,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
                           : (const void*)sweep16_kernel<HV, QV, true>;                                          \
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;                                            \
     if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);           \
+    e->last_sweep = kwk_sweep_info{lean ? (uint32_t)KWK_SWEEP_16_FSM : (uint32_t)KWK_SWEEP_16, QV, 0, 1, tiles,    \
+                                   tiles, HV ? 1u : 0u, 0};                                                     \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
       if (lean)                                                                                                 \
         hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
@@ -3466,6 +3535,9 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
         hipLaunchKernelGGL((sweep16_kernel<HV, QV, false>), dim3(blocks), dim3(kBlock), 0, e->stream, a);     \
     } else {                                                                                                    \
       blocks = pg;                                                                                              \
+      e->last_sweep.persistent = 1;                                                                             \
+      e->last_sweep.grid = pg;                                                                                  \
+      e->last_sweep.depth = lean ? e->fsm_kernel : 1;                                                           \
       if (lean && e->fsm_kernel == 2)                                                                           \
         hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, true, 2>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
       else if (lean)                                                                                            \
@@ -3502,6 +3574,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     if (h) hipLaunchKernelGGL((sweepw_kernel<true, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
     else hipLaunchKernelGGL((sweepw_kernel<false, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   }
+  e->last_sweep = kwk_sweep_info{nar ? (uint32_t)KWK_SWEEP_W4 : (uint32_t)KWK_SWEEP_W8, (uint32_t)kQW, 0, 1, blocks, blocks,
+                                 h ? 1u : 0u, 0};
   e->last_objs = K;
   e->last_region_shift = 2;  // log2(kWavesPerBlock): records carry tile-relative slots
   static_assert(kWavesPerBlock == 4, "region shift");
@@ -3514,14 +3588,17 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
 }
 
 kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  ErrScope es_(e);
   return launch_sweep(e, now_ns, seed, step, true);
 }
 
 kwk_status kwk_match(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  ErrScope es_(e);
   return launch_sweep(e, now_ns, seed, step, false);
 }
 
 kwk_status kwk_sync(kwk_engine* e) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -3533,7 +3610,10 @@ kwk_status kwk_sync(kwk_engine* e) {
 static kwk_status enqueue_compact(kwk_engine* e) {
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   e->compacted = true;
-  if (n_waves == 0) return KWK_OK;
+  if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
+    HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), e->stream));
+    return KWK_OK;
+  }
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
   CompactArgs a;
   a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
@@ -3558,6 +3638,7 @@ static kwk_status enqueue_compact(kwk_engine* e) {
 }
 
 kwk_status kwk_fired_compact(kwk_engine* e) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   return enqueue_compact(e);
@@ -3565,6 +3646,7 @@ kwk_status kwk_fired_compact(kwk_engine* e) {
 
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n; ++k) {
@@ -3582,6 +3664,7 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
 }
 
 kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
+  ErrScope es_(e);
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
   if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
   *recs = e->d_compact;
@@ -3590,6 +3673,7 @@ kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uin
 }
 
 kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(e);
   if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = set_dev(e)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
@@ -3621,6 +3705,7 @@ kwk_status kwk_free_host(void* p) {
 }
 
 kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
+  ErrScope es_(e);
   if (!e || !out) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = set_dev(e)) return st;
   hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->cum_rows,
@@ -3641,6 +3726,7 @@ kwk_status kwk_stats(kwk_engine* e, kwk_step_stats* out) {
 }
 
 kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int64_t* del) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
   if (kwk_status st = set_dev(e)) return st;
@@ -3659,6 +3745,7 @@ kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int
 
 kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* node_ptr, const uint32_t* ukey,
                             uint32_t n_cpu, const double* cpu_values, uint32_t n_mem, const double* mem_values) {
+  ErrScope es_(e);
   if (!e || !node_ptr || !ukey || !cpu_values || !mem_values) return fail(KWK_EINVAL, "null argument");
   if (n_cpu == 0 || n_mem == 0 || n_cpu > 0x4000 || n_mem > 0x4000) return fail(KWK_EINVAL, "dictionary size");
   if (node_ptr[0] != 0) return fail(KWK_EINVAL, "node_ptr[0] must be 0");
@@ -3794,6 +3881,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
 }
 
 kwk_status kwk_usage_mixed(kwk_engine* e, uint32_t n_mixed, const uint32_t* mixed, uint32_t n_ckeys, const uint32_t* ckeys) {
+  ErrScope es_(e);
   if (!e || (n_mixed && !mixed) || (n_ckeys && !ckeys)) return fail(KWK_EINVAL, "null argument");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (n_mixed > kUKeyMixedIndex) return fail(KWK_ECAP, "too many mixed pods");
@@ -3856,6 +3944,7 @@ static kwk_status ensure_cptr(kwk_engine* e) {
 }
 
 kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, double* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(e);
   if (!e || !n_out || (n && cap && !out)) return fail(KWK_EINVAL, "null argument");
   if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
   if ((uint64_t)first + n > e->n_usage_pods) return fail(KWK_EINVAL, "pods beyond the usage configuration");
@@ -3913,6 +4002,7 @@ kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, 
 
 kwk_status kwk_metrics_load(kwk_engine* e, uint32_t n_metrics, const kwk_metric_desc* metrics, uint32_t n_ops,
                             const kwk_metric_op* ops) {
+  ErrScope es_(e);
   if (!e || (n_metrics && !metrics) || (n_ops && !ops)) return fail(KWK_EINVAL, "null argument");
   uint32_t needs = 0;
   for (uint32_t m = 0; m < n_metrics; ++m) {
@@ -3958,6 +4048,7 @@ kwk_status kwk_metrics_load(kwk_engine* e, uint32_t n_metrics, const kwk_metric_
 
 kwk_status kwk_metrics_inputs(kwk_engine* e, const int64_t* pod_created, const int64_t* node_created, const double* started,
                               double zero_time_unix_s) {
+  ErrScope es_(e);
   if (!e || !pod_created || !node_created || !started) return fail(KWK_EINVAL, "null argument");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (kwk_status st = set_dev(e)) return st;
@@ -3979,6 +4070,7 @@ kwk_status kwk_metrics_inputs(kwk_engine* e, const int64_t* pod_created, const i
 
 kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out, uint64_t cap,
                             uint64_t* n_out) {
+  ErrScope es_(e);
   if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
@@ -4041,6 +4133,7 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
 }
 
 kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (e->n_nodes == 0) return KWK_OK;
@@ -4087,6 +4180,7 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
 }
 
 kwk_status kwk_usage_pods(kwk_engine* e, uint32_t enable) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -4108,6 +4202,7 @@ kwk_status kwk_usage_pods(kwk_engine* e, uint32_t enable) {
 }
 
 kwk_status kwk_usage_read_pods(kwk_engine* e, uint32_t first, uint32_t n, double* pod_out) {
+  ErrScope es_(e);
   if (!e || (n && !pod_out)) return fail(KWK_EINVAL, "null argument");
   if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
   if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
@@ -4118,6 +4213,7 @@ kwk_status kwk_usage_read_pods(kwk_engine* e, uint32_t first, uint32_t n, double
 }
 
 kwk_status kwk_usage_read(kwk_engine* e, double* node_out, double* cluster_out) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (kwk_status st = set_dev(e)) return st;
@@ -4135,6 +4231,7 @@ static kwk_status ensure_count_part(kwk_engine* e) {
 }
 
 kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uint64_t* counts) {
+  ErrScope es_(e);
   if (!e || (n_masks && (!masks || !counts))) return fail(KWK_EINVAL, "null argument");
   if (n_masks > kMaxCountMasks) return fail(KWK_EINVAL, "at most 16 masks");
   if (n_masks == 0) return KWK_OK;
@@ -4166,6 +4263,7 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
 
 kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, int64_t now_ns, uint32_t flags,
                          double* out, uint32_t* n_out) {
+  ErrScope es_(e);
   if (!e || !n_out || (n_masks && !masks)) return fail(KWK_EINVAL, "null argument");
   if (n_masks > kMaxCountMasks) return fail(KWK_EINVAL, "at most 16 masks");
   const bool usage = (flags & KWK_AGG_USAGE) != 0;
@@ -4209,6 +4307,7 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
 }
 
 kwk_status kwk_aggregate_read(kwk_engine* e, double* host_out, uint32_t n) {
+  ErrScope es_(e);
   if (!e || (n && !host_out)) return fail(KWK_EINVAL, "null argument");
   if (n > KWK_MAX_STAGES + kMaxCountMasks + 2) return fail(KWK_EINVAL, "more doubles than kwk_aggregate writes");
   if (!e->d_agg) return fail(KWK_ESTATE, "kwk_aggregate must be called first");
@@ -4220,6 +4319,7 @@ kwk_status kwk_aggregate_read(kwk_engine* e, double* host_out, uint32_t n) {
 
 // ---- node leases
 kwk_status kwk_lease_config(kwk_engine* e, const kwk_lease_params* cfg) {
+  ErrScope es_(e);
   if (!e || !cfg) return fail(KWK_EINVAL, "null argument");
   if (cfg->renew_interval_ns <= 0) return fail(KWK_EINVAL, "renew_interval_ns must be > 0");
   if (kwk_status st = set_dev(e)) return st;
@@ -4228,11 +4328,11 @@ kwk_status kwk_lease_config(kwk_engine* e, const kwk_lease_params* cfg) {
     HIP_TRY(hipMalloc(&e->d_lease, sizeof(kwk_lease) * (size_t)e->capacity));
     HIP_TRY(hipMalloc(&e->d_lease_op, (size_t)e->capacity));
     HIP_TRY(hipMalloc(&e->d_lease_ops, sizeof(kwk_fired_rec) * (size_t)e->capacity));
-    HIP_TRY(hipMalloc(&e->d_lease_nops, sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&e->d_lease_nops, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&e->d_lease_stats, sizeof(unsigned long long) * 5));
     HIP_TRY(hipMemset(e->d_lease, 0, sizeof(kwk_lease) * (size_t)e->capacity));
     HIP_TRY(hipMemset(e->d_lease_op, 0, (size_t)e->capacity));
-    HIP_TRY(hipMemset(e->d_lease_nops, 0, sizeof(uint32_t)));
+    HIP_TRY(hipMemset(e->d_lease_nops, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMemset(e->d_lease_stats, 0, sizeof(unsigned long long) * 5));
   }
   e->lease_cfg = *cfg;
@@ -4241,6 +4341,7 @@ kwk_status kwk_lease_config(kwk_engine* e, const kwk_lease_params* cfg) {
 }
 
 kwk_status kwk_lease_set(kwk_engine* e, uint32_t first, uint32_t n, const kwk_lease* leases) {
+  ErrScope es_(e);
   if (!e || (n && !leases)) return fail(KWK_EINVAL, "null argument");
   if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
   if ((uint64_t)first + n > e->capacity) return fail(KWK_ECAP, "lease range beyond capacity");
@@ -4250,19 +4351,25 @@ kwk_status kwk_lease_set(kwk_engine* e, uint32_t first, uint32_t n, const kwk_le
   return KWK_OK;
 }
 
-kwk_status kwk_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
-  if (!e) return fail(KWK_EINVAL, "null engine");
-  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
-  if (kwk_status st = set_dev(e)) return st;
-  HIP_TRY(hipMemsetAsync(e->d_lease_nops, 0, sizeof(uint32_t), e->stream));
+// one lease step (enqueue only): the count it writes was zeroed by the previous step's kernel
+// (or at kwk_lease_config), and it zeroes the other entry for the next step
+static kwk_status enqueue_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  // a fused tick's pod sync (pod stream) may still be reading the previous step's lease results
+  if (e->tick_pods && e->tick_pods->tick_pending) HIP_TRY(hipStreamWaitEvent(e->stream, e->tick_pods->ev_podsync, 0));
   ++e->lease_steps;
-  if (e->n_active == 0) return KWK_OK;
+  const uint32_t cur = e->lease_par;
+  e->lease_last = cur;
+  if (e->n_active == 0) {
+    HIP_TRY(hipMemsetAsync(e->d_lease_nops + cur, 0, sizeof(uint32_t), e->stream));
+    return KWK_OK;
+  }
+  e->lease_par ^= 1u;
   LeaseArgs a;
   a.lease = e->d_lease;
   a.op = e->d_lease_op;
   a.st = e->d_st;
   a.ops = e->d_lease_ops;
-  a.n_ops = e->d_lease_nops;
+  a.n_ops = e->d_lease_nops + cur;
   a.stats = e->d_lease_stats;
   a.fmt = e->fmt;
   a.n = e->n_active;
@@ -4271,13 +4378,23 @@ kwk_status kwk_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t
   a.step = step;
   a.now = now_ns;
   a.cfg = e->lease_cfg;
-  hipLaunchKernelGGL(lease_kernel, dim3((e->n_active + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
+  hipLaunchKernelGGL(lease_kernel, dim3((e->n_active + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a,
+                     e->d_lease_nops + (cur ^ 1u));
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
 
+kwk_status kwk_lease_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
+  if (kwk_status st = set_dev(e)) return st;
+  return enqueue_lease_step(e, now_ns, seed, step);
+}
+
 kwk_status kwk_lease_fail(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t n, const uint32_t* slots,
                           const kwk_lease* old) {
+  ErrScope es_(e);
   if (!e || (n && (!slots || !old))) return fail(KWK_EINVAL, "null argument");
   if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
   if (n == 0) return KWK_OK;
@@ -4304,6 +4421,7 @@ kwk_status kwk_lease_fail(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t
   a.step = step;
   a.now = now_ns;
   a.cfg = e->lease_cfg;
+  a.n_ops = e->d_lease_nops + e->lease_last;
   hipLaunchKernelGGL(lease_fail_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, s_slots, s_old, n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -4311,11 +4429,12 @@ kwk_status kwk_lease_fail(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t
 }
 
 kwk_status kwk_lease_ops(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(e);
   if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
   if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
   if (kwk_status st = set_dev(e)) return st;
   uint32_t n = 0;
-  HIP_TRY(hipMemcpyAsync(&n, e->d_lease_nops, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&n, e->d_lease_nops + e->lease_last, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   *n_out = n;
   if (!out || n == 0) return KWK_OK;
@@ -4325,6 +4444,7 @@ kwk_status kwk_lease_ops(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32
 }
 
 kwk_status kwk_lease_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_lease* out) {
+  ErrScope es_(e);
   if (!e || (n && !out)) return fail(KWK_EINVAL, "null argument");
   if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
   if ((uint64_t)first + n > e->capacity) return fail(KWK_EINVAL, "range beyond capacity");
@@ -4335,6 +4455,7 @@ kwk_status kwk_lease_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_lease* 
 }
 
 kwk_status kwk_lease_stats(kwk_engine* e, kwk_lease_counters* out) {
+  ErrScope es_(e);
   if (!e || !out) return fail(KWK_EINVAL, "null argument");
   if (!e->lease_on) return fail(KWK_ESTATE, "kwk_lease_config must be called first");
   if (kwk_status st = set_dev(e)) return st;
@@ -4350,6 +4471,7 @@ kwk_status kwk_lease_stats(kwk_engine* e, kwk_lease_counters* out) {
 }
 
 kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr) {
+  ErrScope es_(pods);
   if (!pods || !nodes || !node_ptr) return fail(KWK_EINVAL, "null argument");
   if (!nodes->lease_on) return fail(KWK_ESTATE, "node engine has no lease configuration");
   if (n_nodes > nodes->n_active) return fail(KWK_EINVAL, "n_nodes beyond the node engine's objects");
@@ -4371,7 +4493,84 @@ kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32
   return KWK_OK;
 }
 
+// ---- the fused reconciliation tick (C3): lease step -> pod sync -> node step -> pod step
+kwk_status kwk_tick_bind(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr) {
+  ErrScope es_(pods);
+  if (!pods || !nodes || !node_ptr) return fail(KWK_EINVAL, "null argument");
+  if (pods == nodes) return fail(KWK_EINVAL, "pod and node engines must differ");
+  if (!nodes->lease_on) return fail(KWK_ESTATE, "node engine has no lease configuration");
+  if (n_nodes > nodes->capacity) return fail(KWK_EINVAL, "n_nodes beyond the node engine's capacity");
+  if (pods->device != nodes->device) return fail(KWK_EINVAL, "pod and node engines on different devices");
+  if (node_ptr[0] != 0 || node_ptr[n_nodes] > pods->capacity) return fail(KWK_EINVAL, "node_ptr out of range");
+  for (uint32_t j = 0; j < n_nodes; ++j)
+    if (node_ptr[j + 1] < node_ptr[j]) return fail(KWK_EINVAL, "node_ptr must be non-decreasing");
+  if (kwk_status st = set_dev(pods)) return st;
+  HIP_TRY(hipStreamSynchronize(pods->stream));
+  if (pods->d_tick_ptr) HIP_TRY(hipFree(pods->d_tick_ptr));
+  pods->d_tick_ptr = nullptr;
+  HIP_TRY(hipMalloc(&pods->d_tick_ptr, 4 * ((size_t)n_nodes + 1)));
+  HIP_TRY(hipMemcpy(pods->d_tick_ptr, node_ptr, 4 * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
+  if (!pods->ev_lease) HIP_TRY(hipEventCreateWithFlags(&pods->ev_lease, hipEventDisableTiming));
+  if (!pods->ev_podsync) HIP_TRY(hipEventCreateWithFlags(&pods->ev_podsync, hipEventDisableTiming));
+  pods->tick_nodes = nodes;
+  pods->tick_n_nodes = n_nodes;
+  pods->tick_pending = false;
+  return KWK_OK;
+}
+
+static kwk_status enqueue_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_ns, uint64_t seed, uint64_t step,
+                               uint32_t flags) {
+  const bool compact = (flags & KWK_TICK_COMPACT) != 0;
+  // the previous tick's pod sync must have read the lease results before this lease step
+  // rewrites them (cross-stream order by events: no host synchronisation)
+  if (pods) nodes->tick_pods = pods;
+  if (nodes->lease_on)
+    if (kwk_status st = enqueue_lease_step(nodes, now_ns, seed, step)) return st;
+  if (pods && pods->tick_n_nodes && nodes->n_active) {
+    HIP_TRY(hipEventRecord(pods->ev_lease, nodes->stream));
+    HIP_TRY(hipStreamWaitEvent(pods->stream, pods->ev_lease, 0));
+    const uint32_t nn = std::min(pods->tick_n_nodes, nodes->n_active);
+    hipLaunchKernelGGL(lease_pods_kernel, dim3((nn + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0,
+                       pods->stream, pods->d_st, pods->fmt, (const uint32_t*)pods->d_tick_ptr, nodes->d_lease_op,
+                       nodes->d_lease, nodes->lease_cfg.holder_id, nn);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(pods->ev_podsync, pods->stream));
+    pods->tick_pending = true;
+  }
+  if (kwk_status st = launch_sweep(nodes, now_ns, seed, step, true)) return st;
+  if (compact)
+    if (kwk_status st = enqueue_compact(nodes)) return st;
+  if (pods) {
+    if (kwk_status st = launch_sweep(pods, now_ns, seed, step, true)) return st;
+    if (compact)
+      if (kwk_status st = enqueue_compact(pods)) return st;
+  }
+  return KWK_OK;
+}
+
+static kwk_status tick_check(kwk_engine* nodes, kwk_engine* pods) {
+  if (!nodes) return fail(KWK_EINVAL, "null node engine");
+  if (pods && pods->tick_nodes != nodes) return fail(KWK_ESTATE, "kwk_tick_bind(pods, nodes, ...) must come first");
+  return set_dev(nodes);
+}
+
+kwk_status kwk_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t flags) {
+  ErrScope es_(nodes);
+  if (kwk_status st = tick_check(nodes, pods)) return st;
+  return enqueue_tick(nodes, pods, now_ns, seed, step, flags);
+}
+
+kwk_status kwk_tick_n(kwk_engine* nodes, kwk_engine* pods, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed,
+                      uint64_t step0, uint32_t flags) {
+  ErrScope es_(nodes);
+  if (kwk_status st = tick_check(nodes, pods)) return st;
+  for (uint32_t k = 0; k < n; ++k)
+    if (kwk_status st = enqueue_tick(nodes, pods, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, flags)) return st;
+  return KWK_OK;
+}
+
 kwk_status kwk_device_ptrs(kwk_engine* e, void** hot, void** fired, void** wave_counts) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (hot) *hot = e->d_st;
   if (fired) *fired = e->d_fired;
@@ -4380,13 +4579,22 @@ kwk_status kwk_device_ptrs(kwk_engine* e, void** hot, void** fired, void** wave_
 }
 
 // ---- timing helpers (HIP events on the engine's own stream; bench.py)
+kwk_status kwk_last_sweep(kwk_engine* e, kwk_sweep_info* out) {
+  ErrScope es_(e);
+  if (!e || !out) return fail(KWK_EINVAL, "null argument");
+  *out = e->last_sweep;
+  return KWK_OK;
+}
+
 kwk_status kwk_stream(kwk_engine* e, void** stream) {
+  ErrScope es_(e);
   if (!e || !stream) return fail(KWK_EINVAL, "null argument");
   *stream = (void*)e->stream;
   return KWK_OK;
 }
 
 kwk_status kwk_event_record(kwk_engine* e, uint32_t idx) {
+  ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   while (e->events.size() <= idx) {
@@ -4400,6 +4608,7 @@ kwk_status kwk_event_record(kwk_engine* e, uint32_t idx) {
 }
 
 kwk_status kwk_event_elapsed(kwk_engine* e, uint32_t a, uint32_t b, float* ms) {
+  ErrScope es_(e);
   if (!e || !ms || a >= e->events.size() || b >= e->events.size()) return fail(KWK_EINVAL, "bad event index");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipEventSynchronize(e->events[b]));

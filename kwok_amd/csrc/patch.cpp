@@ -33,9 +33,18 @@ namespace {
 using kwkjson::JV;
 using kwkjson::Parser;
 
+// the failing call's message: per handle (the call's own object, see ErrScope) and per thread
+// (calls without a handle: create)
 thread_local std::string g_err;
+thread_local std::string* tl_err = nullptr;
+struct ErrScope {
+  std::string* prev;
+  explicit ErrScope(std::string* target) : prev(tl_err) { tl_err = target; }
+  ~ErrScope() { tl_err = prev; }
+};
 kwk_status fail(kwk_status code, const std::string& msg) {
   g_err = msg;
+  if (tl_err) *tl_err = msg;
   return code;
 }
 
@@ -223,6 +232,7 @@ Node load_node(const JV& j) {
 }  // namespace
 
 struct kwk_patcher {
+  std::string err;  // message of the last failing call on this handle
   std::vector<Template> templates;
   std::vector<Func> funcs;
   std::vector<JV> consts;
@@ -838,7 +848,7 @@ struct Ctx {
 
 extern "C" {
 
-const char* kwk_patch_last_error(void) { return g_err.c_str(); }
+const char* kwk_patch_last_error(const kwk_patcher* h) { return h ? h->err.c_str() : g_err.c_str(); }
 
 kwk_status kwk_patcher_create(const char* spec_json, kwk_patcher** out) {
   if (!spec_json || !out) return fail(KWK_EINVAL, "null argument");
@@ -938,6 +948,7 @@ kwk_status kwk_patcher_create(const char* spec_json, kwk_patcher** out) {
 }
 
 kwk_status kwk_patcher_destroy(kwk_patcher* p) {
+  ErrScope es_(p ? &p->err : nullptr);
   delete p;
   return KWK_OK;
 }
@@ -945,6 +956,7 @@ kwk_status kwk_patcher_destroy(kwk_patcher* p) {
 kwk_status kwk_patch_render(kwk_patcher* p, uint32_t n, const uint16_t* template_ids, const char* objs,
                             const uint64_t* obj_offsets, int64_t now_ns, kwk_patch_fn fn, void* user,
                             uint32_t n_threads, const char** out_data, uint64_t* out_offsets, uint8_t* status) {
+  ErrScope es_(p ? &p->err : nullptr);
   if (!p || !out_data || !out_offsets || (n && (!template_ids || !objs || !obj_offsets || !status)))
     return fail(KWK_EINVAL, "null argument");
   for (uint32_t i = 0; i < n; ++i) {

@@ -75,6 +75,13 @@ class StepStats(C.Structure):
                 ("line_bytes", C.c_uint64)]
 
 
+class SweepInfo(C.Structure):
+    _fields_ = [(k, C.c_uint32) for k in ("kernel", "q", "persistent", "depth", "grid", "tiles", "harness", "reserved")]
+
+
+SWEEP_16, SWEEP_16_FSM, SWEEP_W4, SWEEP_W8 = 1, 2, 3, 4  # KWK_SWEEP_*
+
+
 class EngineDesc(C.Structure):
     _fields_ = [("device", C.c_int32), ("capacity", C.c_uint32), ("value_slots", C.c_uint32),
                 ("max_records", C.c_uint32), ("slot_base", C.c_uint64), ("kind_salt", C.c_uint32),
@@ -145,7 +152,9 @@ EXPORTS = [
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
     "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
     "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
+    "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n",
 ]
+TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
 
 _lib = None
@@ -169,6 +178,7 @@ def lib():
     L = C.CDLL(LIB_PATH)
     s = C.c_int32
     L.kwk_last_error.restype = C.c_char_p
+    L.kwk_last_error.argtypes = [C.c_void_p]
     L.kwk_engine_create.argtypes = [_p(EngineDesc), _p(C.c_void_p)]
     L.kwk_engine_destroy.argtypes = [C.c_void_p]
     L.kwk_load_stages.argtypes = [C.c_void_p, _p(StageTable), C.c_void_p]
@@ -220,6 +230,11 @@ def lib():
     L.kwk_lease_fail.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
     L.kwk_lease_stats.argtypes = [C.c_void_p, _p(LeaseCounters)]
     L.kwk_lease_sync_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_last_sweep.argtypes = [C.c_void_p, _p(SweepInfo)]
+    L.kwk_tick_bind.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_tick.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32]
+    L.kwk_tick_n.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, C.c_uint64,
+                             C.c_uint32]
     L.kwk_abi_version.restype = C.c_uint32
     L.kwk_tile_objects.restype = C.c_uint32
     for name in EXPORTS:
@@ -230,9 +245,11 @@ def lib():
     return L
 
 
-def check(status: int, what: str = ""):
+def check(status: int, what: str = "", eng=None):
+    """Raise EngineError for a failed call; the message is the engine's own (kwk_last_error(eng)),
+    or the calling thread's for calls without an engine."""
     if status != KWK_OK:
-        msg = lib().kwk_last_error().decode(errors="replace")
+        msg = lib().kwk_last_error(eng).decode(errors="replace")
         raise EngineError(f"{what} failed ({status}): {msg}")
 
 

@@ -92,6 +92,7 @@ def lib():
             raise abi.EngineError(f"native encoder library missing: {LIB_PATH} (run python -m kwok_amd.build)")
         L = C.CDLL(LIB_PATH)
         L.kwk_encoder_last_error.restype = C.c_char_p
+        L.kwk_encoder_last_error.argtypes = [C.c_void_p]
         L.kwk_encoder_create.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
         L.kwk_encoder_destroy.argtypes = [C.c_void_p]
         L.kwk_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
@@ -103,9 +104,11 @@ def lib():
     return _lib
 
 
-def _check(st, what):
+def _check(st, what, h=None):
+    """Raise for a failed call; the message is the handle's own (per handle), or the calling
+    thread's for create."""
     if st != 0:
-        raise abi.EngineError(f"{what} failed ({st}): {lib().kwk_encoder_last_error().decode(errors='replace')}")
+        raise abi.EngineError(f"{what} failed ({st}): {lib().kwk_encoder_last_error(h).decode(errors='replace')}")
 
 
 def pack_json(objs: Sequence) -> tuple:
@@ -145,7 +148,7 @@ class NativeIngest:
         unknown = C.c_uint32()
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kwk_encode(self.h, n, buf, abi.ptr(offsets), self.n_threads, abi.ptr(hot), abi.ptr(dels),
-                                abi.ptr(rec), abi.ptr(cls), C.byref(unknown)), "kwk_encode")
+                                abi.ptr(rec), abi.ptr(cls), C.byref(unknown)), "kwk_encode", self.h)
         self.unknown_classes = unknown.value
         return hot, dels, rec, cls
 
@@ -155,8 +158,8 @@ class NativeIngest:
     def record_array(self) -> np.ndarray:
         ns = max(1, len(self.p.slots))
         n = C.c_uint32()
-        _check(lib().kwk_encoder_records(self.h, None, 0, C.byref(n)), "kwk_encoder_records")
+        _check(lib().kwk_encoder_records(self.h, None, 0, C.byref(n)), "kwk_encoder_records", self.h)
         a = np.zeros((max(1, n.value), ns), dtype=abi.VALUE_DTYPE)
         if n.value and self.p.slots:
-            _check(lib().kwk_encoder_records(self.h, abi.ptr(a), n.value, C.byref(n)), "kwk_encoder_records")
+            _check(lib().kwk_encoder_records(self.h, abi.ptr(a), n.value, C.byref(n)), "kwk_encoder_records", self.h)
         return a

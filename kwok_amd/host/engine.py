@@ -147,12 +147,15 @@ class Engine:
         d = abi.EngineDesc(device=device, capacity=capacity, value_slots=max(1, len(program.slots)),
                            max_records=max_records, slot_base=slot_base, kind_salt=kind_salt, flags=flags)
         h = C.c_void_p()
-        abi.check(L.kwk_engine_create(C.byref(d), C.byref(h)), "kwk_engine_create")
+        abi.check(L.kwk_engine_create(C.byref(d), C.byref(h)), "kwk_engine_create")  # thread slot
         self.h = h
         self.capacity = capacity
         self.n = 0
         self.kind_salt = kind_salt
         self.slot_base = slot_base
+
+    def _check(self, status: int, what: str):
+        abi.check(status, what, self.h)
 
     def close(self):
         if getattr(self, "h", None):
@@ -168,14 +171,14 @@ class Engine:
     def load_stages(self, version: int = 1):
         t = self.p.table(version)
         deltas = np.ascontiguousarray(self.p.delta_array())
-        abi.check(abi.lib().kwk_load_stages(self.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
+        self._check(abi.lib().kwk_load_stages(self.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
         h = self.p.harness_struct()
-        abi.check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
+        self._check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
 
     def set_harness(self, enable: bool):
         h = self.p.harness_struct()
         h.enable = 1 if (enable and self.p.harness is not None) else 0
-        abi.check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
+        self._check(abi.lib().kwk_set_harness(self.h, C.byref(h)), "kwk_set_harness")
 
     def load(self, hot, dels, rec, cls, records: Optional[np.ndarray] = None):
         hot = np.ascontiguousarray(hot)
@@ -184,14 +187,14 @@ class Engine:
         cls = np.ascontiguousarray(cls, dtype=np.uint16)
         n_rec = 0 if records is None else records.shape[0]
         recs = None if records is None else np.ascontiguousarray(records)
-        abi.check(abi.lib().kwk_load(self.h, len(hot), abi.ptr(hot), abi.ptr(dels), abi.ptr(rec), abi.ptr(cls), n_rec,
+        self._check(abi.lib().kwk_load(self.h, len(hot), abi.ptr(hot), abi.ptr(dels), abi.ptr(rec), abi.ptr(cls), n_rec,
                                      abi.ptr(recs)), "kwk_load")
         self.n = len(hot)
 
     def upsert(self, slots, hot, dels, rec, cls):
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
         hot = np.ascontiguousarray(hot)
-        abi.check(abi.lib().kwk_upsert(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
+        self._check(abi.lib().kwk_upsert(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
                                        abi.ptr(np.ascontiguousarray(dels, dtype=np.int64)),
                                        abi.ptr(np.ascontiguousarray(rec, dtype=np.uint32)),
                                        abi.ptr(np.ascontiguousarray(cls, dtype=np.uint16))), "kwk_upsert")
@@ -201,18 +204,18 @@ class Engine:
         """kwk_replace: rows written as given (no implicit DIRTY)."""
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
         hot = np.ascontiguousarray(hot)
-        abi.check(abi.lib().kwk_replace(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
+        self._check(abi.lib().kwk_replace(self.h, len(slots), abi.ptr(slots), abi.ptr(hot),
                                         abi.ptr(np.ascontiguousarray(dels, dtype=np.int64)),
                                         abi.ptr(np.ascontiguousarray(rec, dtype=np.uint32)),
                                         abi.ptr(np.ascontiguousarray(cls, dtype=np.uint16))), "kwk_replace")
 
     def set_records(self, records: np.ndarray, first: int = 0):
         recs = np.ascontiguousarray(records)
-        abi.check(abi.lib().kwk_set_records(self.h, first, recs.shape[0], abi.ptr(recs)), "kwk_set_records")
+        self._check(abi.lib().kwk_set_records(self.h, first, recs.shape[0], abi.ptr(recs)), "kwk_set_records")
 
     def delete(self, slots):
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
-        abi.check(abi.lib().kwk_delete(self.h, len(slots), abi.ptr(slots)), "kwk_delete")
+        self._check(abi.lib().kwk_delete(self.h, len(slots), abi.ptr(slots)), "kwk_delete")
 
     def retry(self, now_ns: int, seed: int, step: int, slots, hot, cls, stages, retry_count, backoff=None):
         """kwk_retry: re-queue failed playStage jobs (pod_controller.go:273-284) with the
@@ -223,50 +226,56 @@ class Engine:
         stages = np.ascontiguousarray(stages, dtype=np.uint16)
         rc = np.ascontiguousarray(retry_count, dtype=np.uint32)
         b = abi.Backoff(**(backoff or abi.DEFAULT_BACKOFF))
-        abi.check(abi.lib().kwk_retry(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(hot), abi.ptr(cls),
+        self._check(abi.lib().kwk_retry(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(hot), abi.ptr(cls),
                                       abi.ptr(stages), abi.ptr(rc), C.byref(b)), "kwk_retry")
 
     def step(self, now_ns: int, seed: int, step: int):
-        abi.check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
+        self._check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
     def step_n(self, n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact: bool = True, ev_every: int = 0,
                ev_j0: int = 0):
         """kwk_step_n: n steps (+ device compaction after each) enqueued by one call."""
-        abi.check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, 1 if compact else 0, ev_every, ev_j0),
+        self._check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, 1 if compact else 0, ev_every, ev_j0),
                   "kwk_step_n")
 
     def fired_compact(self):
         """kwk_fired_compact: the last step's fired list compacted on the device (enqueue only)."""
-        abi.check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
+        self._check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
 
     def set_tuning(self, key: int, value: int):
         """kwk_set_tuning: an explicit kernel choice (abi.TUNE_*)."""
-        abi.check(abi.lib().kwk_set_tuning(self.h, key, value), "kwk_set_tuning")
+        self._check(abi.lib().kwk_set_tuning(self.h, key, value), "kwk_set_tuning")
 
     def match(self, now_ns: int, seed: int, step: int):
         """kwk_match: pick + delay for dirty objects, nothing fires."""
-        abi.check(abi.lib().kwk_match(self.h, now_ns, seed, step), "kwk_match")
+        self._check(abi.lib().kwk_match(self.h, now_ns, seed, step), "kwk_match")
+
+    def last_sweep(self) -> dict:
+        """kwk_last_sweep: the kernel shape the last kwk_step / kwk_match launched."""
+        i = abi.SweepInfo()
+        self._check(abi.lib().kwk_last_sweep(self.h, C.byref(i)), "kwk_last_sweep")
+        return {k: getattr(i, k) for k, _ in abi.SweepInfo._fields_}
 
     def sync(self):
-        abi.check(abi.lib().kwk_sync(self.h), "kwk_sync")
+        self._check(abi.lib().kwk_sync(self.h), "kwk_sync")
 
     def fired(self, pinned: Optional["PinnedBuffer"] = None) -> np.ndarray:
         """The last step's fired records (kwk_fired).  With `pinned` (a PinnedBuffer) the copy
         lands in page-locked memory and the returned array is a view of it."""
         n = C.c_uint32()
         L = abi.lib()
-        abi.check(L.kwk_fired(self.h, None, 0, C.byref(n)), "kwk_fired")
+        self._check(L.kwk_fired(self.h, None, 0, C.byref(n)), "kwk_fired")
         if pinned is not None:
             out = pinned.array(abi.FIRED_DTYPE, n.value)
         else:
             out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
         if n.value:
-            abi.check(L.kwk_fired(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired")
+            self._check(L.kwk_fired(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired")
         return out
 
     def stats(self) -> dict:
         s = abi.StepStats()
-        abi.check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
+        self._check(abi.lib().kwk_stats(self.h, C.byref(s)), "kwk_stats")
         return {"steps": s.steps, "matched": s.matched, "fired": s.fired, "bytes": s.bytes,
                 "state_bytes": s.state_bytes, "line_bytes": s.line_bytes,
                 "fired_per_stage": {self.p.names[i]: s.fired_per_stage[i] for i in range(len(self.p.names))}}
@@ -275,14 +284,14 @@ class Engine:
         n = self.n - first if n is None else n
         hot = np.zeros(n, dtype=abi.HOT_DTYPE)
         dels = np.zeros(n, dtype=np.int64)
-        abi.check(abi.lib().kwk_read(self.h, first, n, abi.ptr(hot), abi.ptr(dels)), "kwk_read")
+        self._check(abi.lib().kwk_read(self.h, first, n, abi.ptr(hot), abi.ptr(dels)), "kwk_read")
         return hot, dels
 
     def count(self, masks) -> np.ndarray:
         """kwk_count: alive objects with (pred & mask) != 0 per mask (0 = all alive)."""
         m = np.ascontiguousarray(masks, dtype=np.uint32)
         out = np.zeros(len(m), dtype=np.uint64)
-        abi.check(abi.lib().kwk_count(self.h, len(m), abi.ptr(m), abi.ptr(out)), "kwk_count")
+        self._check(abi.lib().kwk_count(self.h, len(m), abi.ptr(m), abi.ptr(out)), "kwk_count")
         return out
 
     def aggregate(self, masks, now_ns: int = 0, usage: bool = False, out_ptr: Optional[int] = None) -> int:
@@ -292,14 +301,14 @@ class Engine:
         m = np.ascontiguousarray(masks, dtype=np.uint32)
         self._agg_masks = m  # kept alive until the stream has copied it
         n = C.c_uint32()
-        abi.check(abi.lib().kwk_aggregate(self.h, len(m), abi.ptr(m) if len(m) else None, now_ns,
+        self._check(abi.lib().kwk_aggregate(self.h, len(m), abi.ptr(m) if len(m) else None, now_ns,
                                           abi.AGG_USAGE if usage else 0, out_ptr, C.byref(n)), "kwk_aggregate")
         return n.value
 
     def aggregate_read(self, n: int) -> np.ndarray:
         """The engine-owned aggregate buffer (synchronises)."""
         out = np.zeros(n, dtype=np.float64)
-        abi.check(abi.lib().kwk_aggregate_read(self.h, abi.ptr(out), n), "kwk_aggregate_read")
+        self._check(abi.lib().kwk_aggregate_read(self.h, abi.ptr(out), n), "kwk_aggregate_read")
         return out
 
     # usage
@@ -311,12 +320,12 @@ class Engine:
                        np.ascontiguousarray(mem_values, dtype=np.float64)]
         np_, uk, cv, mv = self._uargs
         self.n_nodes = len(np_) - 1
-        abi.check(abi.lib().kwk_usage_config(self.h, self.n_nodes, abi.ptr(np_), abi.ptr(uk), len(cv), abi.ptr(cv),
+        self._check(abi.lib().kwk_usage_config(self.h, self.n_nodes, abi.ptr(np_), abi.ptr(uk), len(cv), abi.ptr(cv),
                                              len(mv), abi.ptr(mv)), "kwk_usage_config")
         mixed = np.zeros(0, dtype=np.uint32) if mixed is None else np.ascontiguousarray(mixed, dtype=np.uint32)
         ckeys = np.zeros(0, dtype=np.uint32) if ckeys is None else np.ascontiguousarray(ckeys, dtype=np.uint32)
         if len(mixed) or np.any((uk >> 28) == 0):
-            abi.check(abi.lib().kwk_usage_mixed(self.h, len(mixed) // 2, abi.ptr(mixed), len(ckeys), abi.ptr(ckeys)),
+            self._check(abi.lib().kwk_usage_mixed(self.h, len(mixed) // 2, abi.ptr(mixed), len(ckeys), abi.ptr(ckeys)),
                       "kwk_usage_mixed")
         # containers per pod (series of a container metric)
         nc = (uk >> 28).astype(np.int64)
@@ -330,10 +339,10 @@ class Engine:
         n = self.n - first if n is None else n
         cnt = C.c_uint32()
         L = abi.lib()
-        abi.check(L.kwk_usage_read_containers(self.h, first, n, None, 0, C.byref(cnt)), "kwk_usage_read_containers")
+        self._check(L.kwk_usage_read_containers(self.h, first, n, None, 0, C.byref(cnt)), "kwk_usage_read_containers")
         out = np.zeros((cnt.value, 4), dtype=np.float64)
         if cnt.value:
-            abi.check(L.kwk_usage_read_containers(self.h, first, n, abi.ptr(out), cnt.value, C.byref(cnt)),
+            self._check(L.kwk_usage_read_containers(self.h, first, n, abi.ptr(out), cnt.value, C.byref(cnt)),
                       "kwk_usage_read_containers")
         return out
 
@@ -349,44 +358,44 @@ class Engine:
         ops = (abi.MetricOp * max(1, len(flat)))()
         for i, (op, x) in enumerate(flat):
             ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
-        abi.check(abi.lib().kwk_metrics_load(self.h, len(programs), descs, len(flat), ops), "kwk_metrics_load")
+        self._check(abi.lib().kwk_metrics_load(self.h, len(programs), descs, len(flat), ops), "kwk_metrics_load")
 
     def metrics_inputs(self, pod_created_ns, node_created_ns, node_started, zero_time_unix_s: float):
         self._minputs = [np.ascontiguousarray(pod_created_ns, dtype=np.int64),
                          np.ascontiguousarray(node_created_ns, dtype=np.int64),
                          np.ascontiguousarray(node_started, dtype=np.float64)]
         a, b, c = self._minputs
-        abi.check(abi.lib().kwk_metrics_inputs(self.h, abi.ptr(a), abi.ptr(b), abi.ptr(c), zero_time_unix_s),
+        self._check(abi.lib().kwk_metrics_inputs(self.h, abi.ptr(a), abi.ptr(b), abi.ptr(c), zero_time_unix_s),
                   "kwk_metrics_inputs")
 
     def metrics_eval(self, now_ns: int, node_first: int, n_nodes: int) -> np.ndarray:
         cnt = C.c_uint64()
         L = abi.lib()
-        abi.check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, None, 0, C.byref(cnt)), "kwk_metrics_eval")
+        self._check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, None, 0, C.byref(cnt)), "kwk_metrics_eval")
         out = np.zeros(cnt.value, dtype=np.float64)
         if cnt.value:
-            abi.check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, abi.ptr(out), cnt.value, C.byref(cnt)),
+            self._check(L.kwk_metrics_eval(self.h, now_ns, node_first, n_nodes, abi.ptr(out), cnt.value, C.byref(cnt)),
                       "kwk_metrics_eval")
         return out
 
     def usage(self, now_ns: int):
-        abi.check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")
+        self._check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")
 
     def usage_pods(self, enable: bool = True):
-        abi.check(abi.lib().kwk_usage_pods(self.h, 1 if enable else 0), "kwk_usage_pods")
+        self._check(abi.lib().kwk_usage_pods(self.h, 1 if enable else 0), "kwk_usage_pods")
 
     def usage_read_pods(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
         """n x {cpu, mem, cpu_cumulative, mem_cumulative} per pod slot."""
         n = self.n - first if n is None else n
         out = np.zeros((n, 4), dtype=np.float64)
-        abi.check(abi.lib().kwk_usage_read_pods(self.h, first, n, abi.ptr(out)), "kwk_usage_read_pods")
+        self._check(abi.lib().kwk_usage_read_pods(self.h, first, n, abi.ptr(out)), "kwk_usage_read_pods")
         return out
 
     def usage_read(self, node_out: bool = True):
         """(per-node {cpu, mem, cpu_cumulative, mem_cumulative} or None, cluster {cpu, mem})."""
         node = np.zeros((self.n_nodes, 4), dtype=np.float64) if node_out else None
         cl = np.zeros(2, dtype=np.float64)
-        abi.check(abi.lib().kwk_usage_read(self.h, abi.ptr(node), abi.ptr(cl)), "kwk_usage_read")
+        self._check(abi.lib().kwk_usage_read(self.h, abi.ptr(node), abi.ptr(cl)), "kwk_usage_read")
         return node, cl
 
     # node leases (NodeLeaseController, node_lease_controller.go)
@@ -398,28 +407,28 @@ class Engine:
         p = abi.LeaseParams(holder_id=holder_id, lease_duration_s=lease_duration_s,
                             renew_interval_ns=renew_interval_ns, renew_jitter=renew_jitter,
                             manage_nodes=1 if manage_nodes else 0)
-        abi.check(abi.lib().kwk_lease_config(self.h, C.byref(p)), "kwk_lease_config")
+        self._check(abi.lib().kwk_lease_config(self.h, C.byref(p)), "kwk_lease_config")
 
     def lease_set(self, leases: np.ndarray, first: int = 0):
         a = np.ascontiguousarray(leases, dtype=abi.LEASE_DTYPE)
-        abi.check(abi.lib().kwk_lease_set(self.h, first, len(a), abi.ptr(a)), "kwk_lease_set")
+        self._check(abi.lib().kwk_lease_set(self.h, first, len(a), abi.ptr(a)), "kwk_lease_set")
 
     def lease_step(self, now_ns: int, seed: int, step: int):
-        abi.check(abi.lib().kwk_lease_step(self.h, now_ns, seed, step), "kwk_lease_step")
+        self._check(abi.lib().kwk_lease_step(self.h, now_ns, seed, step), "kwk_lease_step")
 
     def lease_ops(self) -> np.ndarray:
         n = C.c_uint32()
         L = abi.lib()
-        abi.check(L.kwk_lease_ops(self.h, None, 0, C.byref(n)), "kwk_lease_ops")
+        self._check(L.kwk_lease_ops(self.h, None, 0, C.byref(n)), "kwk_lease_ops")
         out = np.zeros(n.value, dtype=abi.FIRED_DTYPE)
         if n.value:
-            abi.check(L.kwk_lease_ops(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_lease_ops")
+            self._check(L.kwk_lease_ops(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_lease_ops")
         return out
 
     def lease_read(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
         n = self.n - first if n is None else n
         out = np.zeros(n, dtype=abi.LEASE_DTYPE)
-        abi.check(abi.lib().kwk_lease_read(self.h, first, n, abi.ptr(out)), "kwk_lease_read")
+        self._check(abi.lib().kwk_lease_read(self.h, first, n, abi.ptr(out)), "kwk_lease_read")
         return out
 
     def lease_fail(self, now_ns: int, seed: int, step: int, slots, old: np.ndarray):
@@ -427,30 +436,46 @@ class Engine:
         step; `old` = the leases the informer still holds."""
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
         old = np.ascontiguousarray(old, dtype=abi.LEASE_DTYPE)
-        abi.check(abi.lib().kwk_lease_fail(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(old)),
+        self._check(abi.lib().kwk_lease_fail(self.h, now_ns, seed, step, len(slots), abi.ptr(slots), abi.ptr(old)),
                   "kwk_lease_fail")
 
     def lease_stats(self) -> dict:
         c = abi.LeaseCounters()
-        abi.check(abi.lib().kwk_lease_stats(self.h, C.byref(c)), "kwk_lease_stats")
+        self._check(abi.lib().kwk_lease_stats(self.h, C.byref(c)), "kwk_lease_stats")
         return {k: getattr(c, k) for k, _ in abi.LeaseCounters._fields_}
 
     def lease_sync_pods(self, pods: "Engine", node_ptr):
         """Pods on the nodes synced by this engine's last lease step (podsOnNodeSyncWorker)."""
         ptr = np.ascontiguousarray(node_ptr, dtype=np.uint32)
-        abi.check(abi.lib().kwk_lease_sync_pods(pods.h, self.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_lease_sync_pods")
+        self._check(abi.lib().kwk_lease_sync_pods(pods.h, self.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_lease_sync_pods")
+
+    # the fused reconciliation tick (this engine = the node engine)
+    def tick_bind(self, nodes: "Engine", node_ptr):
+        """kwk_tick_bind on this POD engine: the node engine and node_ptr its fused ticks use."""
+        ptr = np.ascontiguousarray(node_ptr, dtype=np.uint32)
+        self._check(abi.lib().kwk_tick_bind(self.h, nodes.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_tick_bind")
+
+    def tick(self, pods: Optional["Engine"], now_ns: int, seed: int, step: int, compact: bool = False):
+        """kwk_tick: lease step -> pod sync -> node step -> pod step, one call (enqueue only)."""
+        self._check(abi.lib().kwk_tick(self.h, pods.h if pods is not None else None, now_ns, seed, step,
+                                       abi.TICK_COMPACT if compact else 0), "kwk_tick")
+
+    def tick_n(self, pods: Optional["Engine"], n: int, now0_ns: int, dt_ns: int, seed: int, step0: int,
+               compact: bool = False):
+        self._check(abi.lib().kwk_tick_n(self.h, pods.h if pods is not None else None, n, now0_ns, dt_ns, seed, step0,
+                                         abi.TICK_COMPACT if compact else 0), "kwk_tick_n")
 
     # timing
     def stream_handle(self) -> int:
         """kwk_stream: the engine's hipStream_t (for torch.cuda.ExternalStream)."""
         h = C.c_void_p()
-        abi.check(abi.lib().kwk_stream(self.h, C.byref(h)), "kwk_stream")
+        self._check(abi.lib().kwk_stream(self.h, C.byref(h)), "kwk_stream")
         return int(h.value or 0)
 
     def event_record(self, idx: int):
-        abi.check(abi.lib().kwk_event_record(self.h, idx), "kwk_event_record")
+        self._check(abi.lib().kwk_event_record(self.h, idx), "kwk_event_record")
 
     def event_elapsed_ms(self, a: int, b: int) -> float:
         ms = C.c_float()
-        abi.check(abi.lib().kwk_event_elapsed(self.h, a, b, C.byref(ms)), "kwk_event_elapsed")
+        self._check(abi.lib().kwk_event_elapsed(self.h, a, b, C.byref(ms)), "kwk_event_elapsed")
         return float(ms.value)

@@ -528,6 +528,7 @@ def lib():
             raise abi.EngineError(f"native patch library missing: {LIB_PATH} (run python -m kwok_amd.build)")
         L = C.CDLL(LIB_PATH)
         L.kwk_patch_last_error.restype = C.c_char_p
+        L.kwk_patch_last_error.argtypes = [C.c_void_p]
         L.kwk_patcher_create.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
         L.kwk_patcher_destroy.argtypes = [C.c_void_p]
         L.kwk_patch_render.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int64, _FN,
@@ -538,9 +539,11 @@ def lib():
     return _lib
 
 
-def _check(st, what):
+def _check(st, what, h=None):
+    """Raise for a failed call; the message is the handle's own (per handle), or the calling
+    thread's for create."""
     if st != 0:
-        raise abi.EngineError(f"{what} failed ({st}): {lib().kwk_patch_last_error().decode(errors='replace')}")
+        raise abi.EngineError(f"{what} failed ({st}): {lib().kwk_patch_last_error(h).decode(errors='replace')}")
 
 
 def _arg_value(kind: int, text: str):
@@ -630,7 +633,7 @@ class PatchProgram:
         data = C.c_char_p()
         _check(lib().kwk_patch_render(self.h, n, abi.ptr(tids), buf, abi.ptr(offsets), int(now_ns), self._fn, None,
                                       self.n_threads, C.byref(data), abi.ptr(out_offs), abi.ptr(status)),
-               "kwk_patch_render")
+               "kwk_patch_render", self.h)
         total = int(out_offs[-1])
         return (C.string_at(data, total) if total else b""), out_offs, status
 

@@ -34,7 +34,12 @@ def sat_add(a: int, b: int) -> int:
 
 class OracleSim:
     def __init__(self, stage_docs: Sequence[dict], objs: Sequence[dict], harness: bool = False,
-                 terminal=("Succeeded", "Failed"), slot_base: int = 0, kind_salt: int = 0):
+                 terminal=("Succeeded", "Failed"), slot_base: int = 0, kind_salt: int = 0,
+                 slots: Optional[Sequence[int]] = None):
+        """slots: the engine slot of each object (default: objs[i] is slot i).  Objects are
+        independent within a step (a pod reads only its own fields; its node's lease state comes
+        in through set_managed) and the Philox counter is the global slot, so a deterministic
+        sample of a large engine's slots is simulated exactly by passing their slot numbers."""
         # NewLifecycle drops stages with a nil selector (lifecycle.go:199-201)
         docs = [d for d in stage_docs if (d.get("spec") or {}).get("selector") is not None]
         self.lc = refcpu.Lifecycle(list(stage_docs))
@@ -54,6 +59,8 @@ class OracleSim:
         self.terminal = set(terminal)
         self.slot_base = slot_base
         self.kind_salt = kind_salt
+        self.slots = list(range(n)) if slots is None else [int(x) for x in slots]
+        assert len(self.slots) == n
 
     def _is_terminal(self, o) -> bool:
         ph = refcpu.query(".status.phase", o) or []
@@ -82,7 +89,7 @@ class OracleSim:
             if self.dirty[i]:
                 self.dirty[i] = False
                 self.matcherr[i] = False
-                s, d = self.lc.match(o, now_ns, key, step, self.slot_base + i)
+                s, d = self.lc.match(o, now_ns, key, step, self.slot_base + self.slots[i])
                 if s == -2:
                     self.matcherr[i] = True
                 elif s is not None:
@@ -101,7 +108,7 @@ class OracleSim:
                     if changed:
                         self.dirty[i] = True
                         flags |= 2
-                fired.append((i, s, flags))
+                fired.append((self.slots[i], s, flags))
         return fired
 
     def set_managed(self, i: int, held: bool, resync: bool):

@@ -44,8 +44,17 @@ def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state
     return prog, eng, sim
 
 
-def compare_state(prog, eng, sim, step):
-    hot, dels = eng.read()
+def compare_state(prog, eng, sim, step, rows=None):
+    """Every simulated object's device row against the oracle: alive, pending stage, due,
+    feature bits (recomputed by the oracle's jq), deletion column, dirty flag.  rows: the
+    device rows (hot, deletion_s) at sim.slots, when the caller has read them already."""
+    if rows is None:
+        hot, dels = eng.read()
+        if sim.slots != list(range(len(sim.objs))):
+            idx = np.asarray(sim.slots, dtype=np.int64)
+            hot, dels = hot[idx], dels[idx]
+    else:
+        hot, dels = rows
     desc = prog.describe()
     bad = []
     for i, o in enumerate(sim.objs):

@@ -181,12 +181,46 @@ def test_state_format_repack_on_table_reload():
                 if k == 3:
                     t.pred_bits = 0
                 deltas = np.ascontiguousarray(prog.delta_array())
-                abi.check(abi.lib().kwk_load_stages(eng.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages")
+                abi.check(abi.lib().kwk_load_stages(eng.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages", eng.h)
                 assert eng.stats()["state_bytes"] == (8 if k == 3 else 2)
             now = NOW0 + k * 10**9
             eng.step(now, 9, k)
             got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
             assert got == sorted(sim.step(now, 9, k)), f"step {k}"
             compare_state(prog, eng, sim, k)
+    finally:
+        eng.close()
+
+
+def test_device_list_empty_after_sweeping_nothing():
+    """a step over no active slots must leave an EMPTY device-compacted list, not the
+    previous step's count (an in-process consumer of kwk_fired_device would re-render patches
+    for objects that fired a step earlier)."""
+    import ctypes as C
+    from kwok_amd.host import abi
+    from tests.parity_util import build
+    files = W.stage_paths(W.POD_FAST)
+    prog, eng, _ = build(files, [W.pod_object(f"p{i}", "node-0") for i in range(300)], harness=False)
+    try:
+        L = abi.lib()
+
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+
+        def device_count():
+            recs, cnt = C.c_void_p(), C.c_void_p()
+            abi.check(L.kwk_fired_device(eng.h, C.byref(recs), C.byref(cnt)), "kwk_fired_device", eng.h)
+            eng.sync()
+            out = C.c_uint32(0xFFFFFFFF)
+            assert hip.hipMemcpy(C.byref(out), cnt, 4, 2) == 0  # hipMemcpyDeviceToHost
+            return out.value
+        eng.step(10**18, 1, 0)
+        eng.fired_compact()
+        assert device_count() == 300  # every pod matched pod-ready and fired
+        eng.load(np.zeros(0, dtype=abi.HOT_DTYPE), [], [], [])
+        eng.step(10**18 + 10**9, 1, 1)
+        eng.fired_compact()
+        assert device_count() == 0
+        assert len(eng.fired()) == 0
     finally:
         eng.close()

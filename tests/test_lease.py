@@ -159,12 +159,14 @@ def test_controller_scenario_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
-def test_c3_nodes_leases_pods_parity(state):
+@pytest.mark.parametrize("state,fused", [("auto", False), ("u32", False), ("wide", False), ("auto", True),
+                                         ("u32", True)])
+def test_c3_nodes_leases_pods_parity(state, fused):
     """C3 shape at 96 nodes (node-initialize + node-heartbeat 20 s / 25 s, leases 40 s with a
     10 s +- 4% renew, 250 ms tick for 50 s) with 4 pod-fast pods per node: lease step ->
     node MANAGED / resync -> node sweep -> pod resync -> pod sweep, every step bit-exact
-    (lease records, lease API writes, fired sets, object states) against the oracle."""
+    (lease records, lease API writes, fired sets, object states) against the oracle — as
+    separate calls, and (fused) as one kwk_tick per step (HIP-event stream order)."""
     from tests.parity_util import NOW0, build, compare_state
     rng = np.random.default_rng(33)
     n_nodes, ppn = 96, 4
@@ -197,9 +199,14 @@ def test_c3_nodes_leases_pods_parity(state):
         neng.lease_set(to_array(leases))
         lsim = LR.LeaseSim(leases, me, 40, 10 * 10**9, 0.04, kind_salt=1)
         seed = 0x77
+        if fused:
+            peng.tick_bind(neng, node_ptr)
         for k in range(200):
             now = NOW0 + k * 250 * 10**6
-            neng.lease_step(now, seed, k)
+            if fused:
+                neng.tick(peng, now, seed, k, compact=(k % 2 == 0))
+            else:
+                neng.lease_step(now, seed, k)
             ops = lsim.step(now, seed, k)
             assert sorted((int(r["slot"]), int(r["stage"])) for r in neng.lease_ops()) == sorted(ops), f"step {k}"
             assert_leases_equal(neng.lease_read(), lsim.leases, k)
@@ -208,9 +215,11 @@ def test_c3_nodes_leases_pods_parity(state):
                 nsim.set_managed(i, h, op != LR.OP_BUSY)
                 for p in range(node_ptr[i], node_ptr[i + 1]):
                     psim.set_managed(p, h, op != LR.OP_BUSY)
-            neng.lease_sync_pods(peng, node_ptr)
+            if not fused:
+                neng.lease_sync_pods(peng, node_ptr)
             for eng, sim, prog in ((neng, nsim, nprog), (peng, psim, pprog)):
-                eng.step(now, seed, k)
+                if not fused:
+                    eng.step(now, seed, k)
                 got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
                 assert got == sorted(sim.step(now, seed, k)), f"step {k}"
                 compare_state(prog, eng, sim, k)
@@ -279,3 +288,59 @@ def test_c3_lease_write_failures_parity():
     finally:
         neng.close()
         peng.close()
+
+
+@pytest.mark.gpu
+def test_tick_n_equals_separate_calls():
+    """kwk_tick_n (the C3 bench's per-interval call) enqueues exactly the per-tick sequence of
+    separate calls: same leases, lease statistics, node / pod states, statistics and last fired
+    lists / lease ops, for a node + pod pair and for a node engine alone."""
+    from tests.parity_util import NOW0, build
+    rng = np.random.default_rng(35)
+    n_nodes, ppn = 300, 5
+    nodes = [W.node_object(f"node-{i}") for i in range(n_nodes)]
+    pods = [W.pod_object(f"pod-{i}", f"node-{i // ppn}", job=(i % 10 == 0)) for i in range(n_nodes * ppn)]
+    node_ptr = np.arange(0, n_nodes * ppn + 1, ppn, dtype=np.uint32)
+    leases = to_array(c3_leases(n_nodes, NOW0, rng))
+    pairs = []
+    try:
+        for _ in range(3):
+            _, ne, _ = build(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), nodes, kind_salt=1)
+            _, pe, _ = build(W.stage_paths(W.POD_FAST), pods, harness=True)
+            ne.lease_config(1, 40, 10 * 10**9, 0.04)
+            ne.lease_set(leases)
+            pairs.append((ne, pe))
+        seed, dt, n = 0x79, 100 * 10**6, 37
+        (ne0, pe0), (ne1, pe1), (ne2, _) = pairs
+        for k in range(n):  # separate calls
+            ne0.lease_step(NOW0 + k * dt, seed, k)
+            ne0.lease_sync_pods(pe0, node_ptr)
+            ne0.step(NOW0 + k * dt, seed, k)
+            ne0.fired_compact()
+            pe0.step(NOW0 + k * dt, seed, k)
+            pe0.fired_compact()
+        pe1.tick_bind(ne1, node_ptr)
+        ne1.tick_n(pe1, 20, NOW0, dt, seed, 0, compact=True)
+        ne1.tick_n(pe1, n - 20, NOW0 + 20 * dt, dt, seed, 20, compact=True)
+        ne2.tick_n(None, n, NOW0, dt, seed, 0, compact=True)  # the node engine alone (the C3 bench)
+        for name, a, b in (("nodes", ne0, ne1), ("pods", pe0, pe1)):
+            ha, hb = a.read()[0], b.read()[0]
+            for col in ("pred", "sched"):
+                assert np.array_equal(ha[col], hb[col]), (name, col)
+            pend = (ha["sched"] & 0xFF) != 0xFF
+            assert np.array_equal(ha["due"][pend], hb["due"][pend]), name
+            fa, fb = a.fired(), b.fired()
+            assert np.array_equal(np.sort(fa["slot"]), np.sort(fb["slot"])), name
+            for key in ("fired", "matched", "steps", "bytes"):
+                assert a.stats()[key] == b.stats()[key], (name, key)
+        assert np.array_equal(ne0.lease_read(), ne1.lease_read())
+        assert ne0.lease_stats() == ne1.lease_stats()
+        oa, ob = ne0.lease_ops(), ne1.lease_ops()
+        assert sorted(oa["slot"].tolist()) == sorted(ob["slot"].tolist())
+        # node engine alone: its leases advance exactly as the pair's (pods only read them)
+        assert np.array_equal(ne0.lease_read(), ne2.lease_read())
+        assert ne0.stats()["fired"] > 0 and pe0.stats()["fired"] > 0
+    finally:
+        for ne, pe in pairs:
+            ne.close()
+            pe.close()

@@ -1,0 +1,113 @@
+"""The benchmarked sweep kernels against the oracle at the sizes they run.
+
+The small-cluster parity tests (test_gpu_parity.py) exercise the one-block-per-tile kernel
+shapes; the bench's C5 pod sweep runs `sweep16_fsm_kernel<harness, 4, persistent, depth 2>`,
+which only launches once the 8192-word tiles outnumber twice the resident blocks (~17M pods
+on 256 CUs), and the C2 mix runs `sweepw_kernel<4>` over millions of pods.  Here both run at
+those sizes and a deterministic sample of slots (every 997th / 4999th) is checked against
+`OracleSim` at every step: the fired records of the sampled slots (slot, stage, flags), and
+each sampled object's pending stage, due time, feature bits, deletion column and dirty flag.
+
+Objects are independent within a step (a pod reads only its own fields) and the
+Philox counter is the global slot, so simulating the sampled objects alone is
+exact: reference `pkg/utils/lifecycle/lifecycle.go:125-191,313-341` (Match, Delay),
+`pkg/kwok/controllers/pod_controller.go:196-360` (preprocess, playStage)."""
+import numpy as np
+import pytest
+
+from tests.parity_util import compare_state
+
+pytestmark = pytest.mark.gpu
+
+NOW0 = 1_700_000_000 * 10**9
+SEED = 0x6B776F6B
+
+
+def _sampled_run(prog, eng, stage_files, variants, index, slots, steps, dt_ns, kernel, persistent):
+    from kwok_amd.host import abi
+    from oracle.next_ref import load_stage_docs
+    from oracle.sim import OracleSim
+    objs = [variants[int(index[s])] for s in slots]
+    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=True, slots=slots)
+    sample = np.asarray(slots, dtype=np.int64)
+    total = 0
+    for k in range(steps):
+        now = NOW0 + k * dt_ns
+        eng.step(now, SEED, k)
+        info = eng.last_sweep()
+        assert info["kernel"] == kernel and info["persistent"] == persistent and info["harness"] == 1, info
+        if persistent:
+            assert info["grid"] < info["tiles"] and info["depth"] == 2, info
+        f = eng.fired()
+        assert len(np.unique(f["slot"])) == len(f), f"step {k}: a slot fired twice"
+        sel = f[np.isin(f["slot"].astype(np.int64), sample)]
+        got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in sel)
+        exp = sorted(sim.step(now, SEED, k))
+        assert got == exp, f"step {k}: device-only {sorted(set(got) - set(exp))[:6]} oracle-only " \
+                           f"{sorted(set(exp) - set(got))[:6]}"
+        total += len(exp)
+        hot, dels = eng.read()
+        compare_state(prog, eng, sim, k, rows=(hot[sample], dels[sample]))
+    return total
+
+
+def test_c5_persistent_table_sweep_sampled_oracle():
+    """C5 pod shape (pod-fast, 100 pods per node, 10 % Job-owned, harness churn) at 20M pods:
+    the persistent, depth-2 table-only 2-byte sweep, every 4999th slot checked each step."""
+    from bench import shard_pod_variants
+    from kwok_amd import workload as W
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    n = 20_000_000
+    files = W.stage_paths(W.POD_FAST)
+    pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+    prog = KindProgram(load_stage_files(*files), HarnessSpec())
+    prog.explore(pvars)
+    ing = Ingest(prog)
+    idx = shard_pod_variants(0, n, SEED, 0.1)
+    hot, dels, rec, cls = ing.variant_columns(pvars, idx)
+    eng = Engine(prog, capacity=n)
+    try:
+        eng.load_stages()
+        eng.set_harness(True)
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        del hot, dels, rec, cls
+        slots = list(range(3, n, 4999))
+        assert int(np.sum(idx[slots])) > 100  # Job-owned pods (pod-complete) are in the sample
+        total = _sampled_run(prog, eng, files, pvars, idx, slots, 10, 10**9, abi.SWEEP_16_FSM, 1)
+        assert total > 2 * len(slots)
+        assert eng.stats()["state_bytes"] == 2
+    finally:
+        eng.close()
+
+
+def test_c2_word_sweep_sampled_oracle():
+    """C2 stage mix (pod-general + chaos: weighted picks, jitter draws, value records, the
+    deletion column) at 4M pods through `sweepw_kernel<4>`, every 997th slot each step."""
+    from kwok_amd import workload as W
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    n = 4_000_000
+    files = W.stage_paths(W.POD_GENERAL + W.POD_CHAOS)
+    pvars, pidx = W.c2_pod_variants(0, n, seed=SEED, job_frac=0.1)
+    prog = KindProgram(load_stage_files(*files), HarnessSpec())
+    prog.explore(pvars)
+    ing = Ingest(prog)
+    hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+    eng = Engine(prog, capacity=n, state="u32", max_records=max(1, len(ing.records)) + 16)
+    try:
+        eng.load_stages()
+        eng.set_harness(True)
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        assert eng.stats()["state_bytes"] == 4
+        slots = list(range(1, n, 997))
+        total = _sampled_run(prog, eng, files, pvars, pidx, slots, 24, 500 * 10**6, abi.SWEEP_W4, 0)
+        assert total > len(slots)
+        fired = {k: v for k, v in eng.stats()["fired_per_stage"].items() if v}
+        assert any("failed" in name for name in fired), fired  # weighted picks ran
+    finally:
+        eng.close()
