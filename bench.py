@@ -132,13 +132,23 @@ class Reporter:
     per-stage transitions, phase histograms, cluster usage) and, with several GPUs, summed in
     place by one RCCL all-reduce — no host round trip except the wait before the collective."""
 
-    def __init__(self, pods, nodes, dist, device):
+    def __init__(self, pods, nodes, dist, device, collective="torch", local_rank=0):
         from kwok_amd.host.cluster import DeviceReport, phase_masks
         pm = phase_masks(pods.p, values=("Running", "Succeeded", "Failed"))
         nm = phase_masks(nodes.p, values=("Running",))
         masks = [[0] + list(pm.values()), [0] + list(nm.values())]
         names = [["pods"] + [f"pods_{k}" for k in pm], ["nodes"] + [f"nodes_{k}" for k in nm]]
-        self.report = DeviceReport([pods, nodes], masks, names, usage_engine=pods, dist=dist, device=device)
+        self.comm = None
+        if collective == "native" and dist is not None:
+            # libkwok_comm: the torch-free RCCL path a Go host links (include/kwok_comm.h); the
+            # 128-byte unique id travels over the existing process group
+            from kwok_amd.host.comm import NativeComm, NativeReport, unique_id
+            box = [unique_id() if dist.get_rank() == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            self.comm = NativeComm(box[0], dist.get_rank(), dist.get_world_size(), local_rank)
+            self.report = NativeReport(self.comm, [pods, nodes], masks, names, usage_engine=pods)
+        else:
+            self.report = DeviceReport([pods, nodes], masks, names, usage_engine=pods, dist=dist, device=device)
 
     def collect(self, now_ns):
         self.report.collect(now_ns)
@@ -407,6 +417,8 @@ def main():
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
+    ap.add_argument("--collective", choices=("torch", "native"), default="torch",
+                    help="aggregate all-reduce: torch.distributed (default) or libkwok_comm (RCCL, no torch; N > 1)")
     args = ap.parse_args()
 
     if args.config != "C5":
@@ -477,7 +489,7 @@ def main():
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_COMPACT_SMALL, args.tune_compact_small)
     dt = args.dt_ms * 10**6
-    reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None)
+    reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None, args.collective, local_rank)
     report_every = 0 if args.pmc_child else args.report_every
 
     log(f"setup {setup_s:.1f} s; warmup {args.warmup} steps")
@@ -550,6 +562,8 @@ def main():
                 "note": "each step's fired lists copied (kwk_fired, 8 B per transition) into kwk_alloc_host buffers"}
         for p in pin:
             p.close()
+    if reporter.comm is not None:
+        reporter.comm.close()
     pods.close()
     nodes.close()
 

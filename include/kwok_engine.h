@@ -385,6 +385,34 @@ kwk_status kwk_metrics_inputs(kwk_engine* pods, const int64_t* pod_created_ns, c
 kwk_status kwk_metrics_eval(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out,
                             uint64_t cap, uint64_t* n_out);
 
+/* Histogram Metric CRs (kind: histogram; pkg/kwok/metrics/metrics.go:133-160,356-462,
+ * histogram.go:81-164): per series every bucket's value program runs (a lowered CEL value, as
+ * above), uint64(value) — Go's float64 -> uint64 conversion on amd64 — is stored at the bucket's
+ * le (a later bucket with an equal le overwrites), and the exposition's bucket counts are
+ * computed as histogram.Write does.  One record of n_visible + 3 uint64 words per series:
+ *   [0, n_visible)   cumulative counts of the visible buckets, ascending le
+ *   n_visible        the +Inf bucket's cumulative count (histogram.Write: only keys above the last
+ *                    visible bound land there)
+ *   n_visible + 1    sample count;  n_visible + 2: sample sum (float64 bits)
+ * A dead pod's record is all ones (no series: ListPods skips it).  Series order as
+ * kwk_metrics_eval, histogram by histogram. */
+typedef struct {
+  double le;          /* MetricBucket.Le */
+  uint32_t hidden;    /* MetricBucket.Hidden: evaluated and stored, not a visible bucket */
+  uint32_t first_op;  /* the bucket's value program */
+  uint32_t n_ops;
+  uint32_t reserved;
+} kwk_metric_bucket;  /* 24 bytes */
+typedef struct {
+  uint32_t dimension;   /* KWK_METRIC_DIM_* */
+  uint32_t first_bucket, n_buckets;  /* 1..64 buckets */
+  uint32_t reserved;
+} kwk_histogram_desc;
+kwk_status kwk_histograms_load(kwk_engine* pods, uint32_t n_hist, const kwk_histogram_desc* hists, uint32_t n_buckets,
+                               const kwk_metric_bucket* buckets, uint32_t n_ops, const kwk_metric_op* ops);
+kwk_status kwk_histograms_eval(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, uint64_t* out,
+                               uint64_t cap, uint64_t* n_out);
+
 /* ------------------------------------------------------------------ node leases */
 /* NodeLeaseController (pkg/kwok/controllers/node_lease_controller.go) on a NODE engine: one
  * lease record per node slot — the informer's cached coordination/v1 Lease plus the

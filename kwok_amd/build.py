@@ -20,6 +20,9 @@ ENC_OUT = os.path.join(PKG, "lib", "libkwok_encoder.so")
 PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
 PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
 PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
+COMM_SRC = [os.path.join(PKG, "csrc", "comm.cpp")]
+COMM_HDR = [os.path.join(ROOT, "include", "kwok_comm.h"), os.path.join(ROOT, "include", "kwok_engine.h")]
+COMM_OUT = os.path.join(PKG, "lib", "libkwok_comm.so")
 ARCH = "gfx950"  # MI355X only
 
 
@@ -54,10 +57,30 @@ def build_patch(force: bool = False, verbose: bool = False) -> str:
     return _host_lib(PATCH_OUT, PATCH_SRC, PATCH_HDR, force, verbose)
 
 
+def build_comm(force: bool = False, verbose: bool = False) -> str:
+    """The RCCL cluster-aggregate collective (host code over librccl + the engine's streams)."""
+    if not force and not _stale(COMM_OUT, COMM_SRC + COMM_HDR + [OUT]):
+        return COMM_OUT
+    cmd = ["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"),
+           "-o", COMM_OUT + ".tmp"] + \
+        COMM_SRC + ["-L", os.path.dirname(OUT), "-lkwok_engine", "-lrccl", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(COMM_OUT + ".tmp", COMM_OUT)
+    return COMM_OUT
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     build_encoder(force, verbose)
     if os.path.exists(PATCH_SRC[0]):
         build_patch(force, verbose)
+    _build_engine(force, verbose)
+    build_comm(force, verbose)
+    return OUT
+
+
+def _build_engine(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(OUT, SRC + HDR):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)

@@ -22,6 +22,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <set>
@@ -2339,30 +2341,33 @@ __device__ __forceinline__ double since_seconds(int64_t now, int64_t created) {
   return dur_seconds(d);
 }
 
-__global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
-  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-  if (s >= a.n_series) return;
-  uint32_t node = 0, pod = 0, j = 0;
+// the series s of a metric: its node, pod and container index (false: a dead pod, no series)
+__device__ __forceinline__ bool metric_series(const MetricArgs& a, uint32_t s, uint32_t& node, uint32_t& pod,
+                                              uint32_t& j) {
+  node = 0; pod = 0; j = 0;
   if (a.dim == KWK_METRIC_DIM_NODE) {
     node = a.n0 + s;
-  } else {
-    if (a.dim == KWK_METRIC_DIM_CONTAINER) {
-      const uint32_t c = a.c0 + s;
-      pod = seg_of(a.cptr, a.p0, a.p1, c);
-      j = c - a.cptr[pod];
-    } else {
-      pod = a.p0 + s;
-    }
-    if (!(load_state(a.st, pod, a.fmt).y & KWK_F_ALIVE)) {
-      a.out[s] = __builtin_nan("");
-      return;
-    }
-    node = seg_of(a.node_ptr, a.n0, a.n1, pod);
+    return true;
   }
+  if (a.dim == KWK_METRIC_DIM_CONTAINER) {
+    const uint32_t c = a.c0 + s;
+    pod = seg_of(a.cptr, a.p0, a.p1, c);
+    j = c - a.cptr[pod];
+  } else {
+    pod = a.p0 + s;
+  }
+  if (!(load_state(a.st, pod, a.fmt).y & KWK_F_ALIVE)) return false;
+  node = seg_of(a.node_ptr, a.n0, a.n1, pod);
+  return true;
+}
+
+// one lowered CEL value program for one series
+__device__ double run_metric_program(const MetricArgs& a, const kwk_metric_op* __restrict__ ops, uint32_t n_ops,
+                                     uint32_t node, uint32_t pod, uint32_t j) {
   double stk[8];
   int sp = 0;
-  for (uint32_t i = 0; i < a.n_ops; ++i) {
-    const kwk_metric_op op = a.ops[i];
+  for (uint32_t i = 0; i < n_ops; ++i) {
+    const kwk_metric_op op = ops[i];
     switch (op.op) {
       case KWK_MOP_CONST: stk[sp++] = op.value; break;
       case KWK_MOP_LOAD: {
@@ -2406,7 +2411,86 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
       default: break;
     }
   }
-  a.out[s] = sp > 0 ? stk[sp - 1] : 0.0;
+  return sp > 0 ? stk[sp - 1] : 0.0;
+}
+
+__global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
+  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+  if (s >= a.n_series) return;
+  uint32_t node, pod, j;
+  if (!metric_series(a, s, node, pod, j)) {
+    a.out[s] = __builtin_nan("");
+    return;
+  }
+  a.out[s] = run_metric_program(a, a.ops, a.n_ops, node, pod, j);
+}
+
+// Go's uint64(float64) on amd64 (the compiler's float64ToUint64 lowering): x < 2^63 ->
+// CVTTSD2SQ (truncation; -Inf, NaN-free values <= -2^63 give the "integer indefinite"
+// 0x8000000000000000), else CVTTSD2SQ(x - 2^63) | 1 << 63 (NaN and x >= 2^64: 1 << 63)
+__device__ __forceinline__ uint64_t go_f64_to_u64(double x) {
+  constexpr uint64_t kInd = 0x8000000000000000ull;
+  auto cvtt = [](double v) -> uint64_t {
+    if (!(v > -9223372036854775808.0 && v < 9223372036854775808.0)) return kInd;
+    return (uint64_t)(int64_t)v;
+  };
+  if (x < 9223372036854775808.0) return cvtt(x);
+  return cvtt(x - 9223372036854775808.0) | kInd;
+}
+
+// Histogram metrics (metrics.go:356-462 updateHistogram; histogram.go:81-164 Set / Write): per
+// series every bucket's value program runs, uint64(value) is Set at the bucket's le (a later
+// bucket with the same le overwrites), and Write turns the stored (le, count) pairs — ascending
+// le — into the cumulative counts of the visible upper bounds (ascending) plus +Inf, the sample
+// count and the sample sum (sum += le * count in key order), exactly as histogram.Write does
+// (note: +Inf only collects keys above the last visible bound).  The host orders the keys and
+// bounds (Go's sort.Float64s order) per histogram.
+struct HistDesc {
+  uint32_t first_bucket, n_buckets;  // buckets [first, first + n) of the bucket table
+  uint32_t first_key, n_keys;        // bucket indices (relative) of the distinct le, ascending
+  uint32_t first_bound, n_bounds;    // visible upper bounds, ascending
+  uint32_t out_words;                // n_bounds + 3
+  uint32_t dim;
+};
+constexpr uint32_t kMaxHistBuckets = 64;
+__global__ __launch_bounds__(kBlock) void histogram_kernel(MetricArgs a, HistDesc h,
+                                                           const kwk_metric_bucket* __restrict__ buckets,
+                                                           const uint32_t* __restrict__ keys,
+                                                           const double* __restrict__ bounds,
+                                                           uint64_t* __restrict__ out) {
+  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+  if (s >= a.n_series) return;
+  uint64_t* o = out + (uint64_t)s * h.out_words;
+  uint32_t node, pod, j;
+  if (!metric_series(a, s, node, pod, j)) {  // a dead pod: no series (count slot = all ones)
+    for (uint32_t w = 0; w < h.out_words; ++w) o[w] = ~0ull;
+    return;
+  }
+  uint64_t val[kMaxHistBuckets];
+  for (uint32_t b = 0; b < h.n_buckets; ++b) {
+    const kwk_metric_bucket B = buckets[h.first_bucket + b];
+    val[b] = go_f64_to_u64(run_metric_program(a, a.ops + B.first_op, B.n_ops, node, pod, j));
+  }
+  const uint32_t nb = h.n_bounds + 1;  // + the +Inf bucket
+  for (uint32_t w = 0; w < nb; ++w) o[w] = 0;
+  uint32_t bi = 0;
+  uint64_t count = 0;
+  double sum = 0.0;
+  for (uint32_t k = 0; k < h.n_keys; ++k) {
+    const uint32_t b = keys[h.first_key + k];
+    const double le = buckets[h.first_bucket + b].le;
+    // cumulative count of previous buckets (histogram.go:128-133): the bound past the last
+    // visible one is +Inf, which no le exceeds
+    while (bi < nb && bi < h.n_bounds && le > bounds[h.first_bound + bi]) {
+      ++bi;
+      o[bi] += count;
+    }
+    o[bi] += val[b];
+    count += val[b];
+    sum += le * (double)val[b];
+  }
+  o[nb] = count;
+  o[nb + 1] = (uint64_t)__double_as_longlong(sum);
 }
 
 // count alive objects with (pred & mask[k]) != 0 for each k (mask 0: every alive object):
@@ -2890,6 +2974,15 @@ struct kwk_engine {
   double zero_time_unix_s = 0.0;
   double* d_mout = nullptr;
   size_t mout_cap = 0;
+  // histogram Metric programs (kwk_histograms_load)
+  kwk_metric_op* d_hops = nullptr;
+  kwk_metric_bucket* d_hbuckets = nullptr;
+  uint32_t* d_hkeys = nullptr;
+  double* d_hbounds = nullptr;
+  std::vector<HistDesc> hists;
+  uint32_t hist_inputs_needed = 0;
+  uint64_t* d_hout = nullptr;
+  size_t hout_cap = 0;
 
   // staging for upserts
   void* d_stage_buf = nullptr;
@@ -3099,7 +3192,8 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
                   e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
-                  e->d_lease_nops, e->d_lease_stats, e->d_ukey8, e->d_kv};
+                  e->d_lease_nops, e->d_lease_stats, e->d_ukey8, e->d_kv, e->d_hops, e->d_hbuckets, e->d_hkeys,
+                  e->d_hbounds, e->d_hout};
   for (void* p : ptrs) if (p) hipFree(p);
   if (e->d_tick_ptr) hipFree(e->d_tick_ptr);
   if (e->ev_lease) hipEventDestroy(e->ev_lease);
@@ -4000,41 +4094,77 @@ kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, 
   return KWK_OK;
 }
 
+// the series inputs of one metric over nodes [n0, n1) (pods [p0, p1), containers from c0)
+static MetricArgs metric_args(kwk_engine* e, uint32_t dim, int64_t now_ns, uint32_t n0, uint32_t n1, uint32_t p0,
+                              uint32_t p1, uint32_t c0, uint32_t n_nodes) {
+  MetricArgs a{};
+  a.dim = dim;
+  a.n0 = n0; a.n1 = n1; a.p0 = p0; a.p1 = p1; a.c0 = c0;
+  const uint32_t c1 = e->h_cptr[p1];
+  a.n_series = dim == KWK_METRIC_DIM_NODE ? n_nodes : dim == KWK_METRIC_DIM_POD ? (p1 - p0) : (c1 - c0);
+  a.st = e->d_st;
+  a.fmt = e->fmt;
+  a.node_ptr = e->d_node_ptr;
+  a.cptr = e->d_cptr;
+  a.ukey = e->d_ukey;
+  a.mixed = e->d_mixed;
+  a.ckeys = e->d_ckeys;
+  a.mbase = e->d_mbase;
+  a.cpu_v = e->d_cpu;
+  a.mem_v = e->d_mem;
+  a.pod_out = e->d_pod_out;
+  a.pod_cum = e->d_pod_cum;
+  a.ccum = e->d_ccum;
+  a.node_out = e->d_node_out;
+  a.pod_created = e->d_pod_created;
+  a.node_created = e->d_node_created;
+  a.node_started = e->d_node_started;
+  a.now = now_ns;
+  a.zero_time_unix_s = e->zero_time_unix_s;
+  return a;
+}
+
+// validates one lowered value program of `dimension` (kwk_metrics_load / kwk_histograms_load)
+static kwk_status check_metric_program(const kwk_metric_op* ops, uint32_t first, uint32_t n, uint32_t n_ops,
+                                       uint32_t dimension, uint32_t& needs) {
+  if (dimension > KWK_METRIC_DIM_CONTAINER) return fail(KWK_EINVAL, "metric dimension");
+  if (n == 0 || n > 64 || (uint64_t)first + n > n_ops) return fail(KWK_EINVAL, "metric ops range");
+  int depth = 0;
+  for (uint32_t i = first; i < first + n; ++i) {
+    const kwk_metric_op& op = ops[i];
+    if (op.op == KWK_MOP_CONST || op.op == KWK_MOP_LOAD) {
+      if (++depth > 8) return fail(KWK_EINVAL, "metric program deeper than 8");
+      if (op.op == KWK_MOP_LOAD) {
+        if (op.arg > KWK_MIN_STARTED_CONTAINERS) return fail(KWK_EINVAL, "metric input");
+        if (op.arg >= KWK_MIN_POD_SINCE) needs = 1;
+        if (dimension == KWK_METRIC_DIM_NODE && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_POD_CUM_MEM)
+          return fail(KWK_EINVAL, "a node metric cannot read pod / container inputs");
+        if (dimension == KWK_METRIC_DIM_NODE && (op.arg == KWK_MIN_POD_SINCE || op.arg == KWK_MIN_POD_CREATED))
+          return fail(KWK_EINVAL, "a node metric cannot read pod inputs");
+        if (dimension == KWK_METRIC_DIM_POD && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_CONTAINER_CUM_MEM)
+          return fail(KWK_EINVAL, "a pod metric cannot read container inputs");
+      }
+    } else if (op.op == KWK_MOP_NEG) {
+      if (depth < 1) return fail(KWK_EINVAL, "metric program underflow");
+    } else if (op.op >= KWK_MOP_ADD && op.op <= KWK_MOP_DIV) {
+      if (depth < 2) return fail(KWK_EINVAL, "metric program underflow");
+      --depth;
+    } else {
+      return fail(KWK_EINVAL, "metric op");
+    }
+  }
+  if (depth != 1) return fail(KWK_EINVAL, "a metric program leaves one value");
+  return KWK_OK;
+}
+
 kwk_status kwk_metrics_load(kwk_engine* e, uint32_t n_metrics, const kwk_metric_desc* metrics, uint32_t n_ops,
                             const kwk_metric_op* ops) {
   ErrScope es_(e);
   if (!e || (n_metrics && !metrics) || (n_ops && !ops)) return fail(KWK_EINVAL, "null argument");
   uint32_t needs = 0;
-  for (uint32_t m = 0; m < n_metrics; ++m) {
-    const kwk_metric_desc& d = metrics[m];
-    if (d.dimension > KWK_METRIC_DIM_CONTAINER) return fail(KWK_EINVAL, "metric dimension");
-    if (d.n_ops == 0 || d.n_ops > 64 || (uint64_t)d.first_op + d.n_ops > n_ops) return fail(KWK_EINVAL, "metric ops range");
-    int depth = 0;
-    for (uint32_t i = d.first_op; i < d.first_op + d.n_ops; ++i) {
-      const kwk_metric_op& op = ops[i];
-      if (op.op == KWK_MOP_CONST || op.op == KWK_MOP_LOAD) {
-        if (++depth > 8) return fail(KWK_EINVAL, "metric program deeper than 8");
-        if (op.op == KWK_MOP_LOAD) {
-          if (op.arg > KWK_MIN_STARTED_CONTAINERS) return fail(KWK_EINVAL, "metric input");
-          if (op.arg >= KWK_MIN_POD_SINCE) needs = 1;
-          if (d.dimension == KWK_METRIC_DIM_NODE && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_POD_CUM_MEM)
-            return fail(KWK_EINVAL, "a node metric cannot read pod / container inputs");
-          if (d.dimension == KWK_METRIC_DIM_NODE && (op.arg == KWK_MIN_POD_SINCE || op.arg == KWK_MIN_POD_CREATED))
-            return fail(KWK_EINVAL, "a node metric cannot read pod inputs");
-          if (d.dimension == KWK_METRIC_DIM_POD && op.arg >= KWK_MIN_CONTAINER_CPU && op.arg <= KWK_MIN_CONTAINER_CUM_MEM)
-            return fail(KWK_EINVAL, "a pod metric cannot read container inputs");
-        }
-      } else if (op.op == KWK_MOP_NEG) {
-        if (depth < 1) return fail(KWK_EINVAL, "metric program underflow");
-      } else if (op.op >= KWK_MOP_ADD && op.op <= KWK_MOP_DIV) {
-        if (depth < 2) return fail(KWK_EINVAL, "metric program underflow");
-        --depth;
-      } else {
-        return fail(KWK_EINVAL, "metric op");
-      }
-    }
-    if (depth != 1) return fail(KWK_EINVAL, "a metric program leaves one value");
-  }
+  for (uint32_t m = 0; m < n_metrics; ++m)
+    if (kwk_status st = check_metric_program(ops, metrics[m].first_op, metrics[m].n_ops, n_ops, metrics[m].dimension, needs))
+      return st;
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (e->d_mops) HIP_TRY(hipFree(e->d_mops));
@@ -4096,31 +4226,9 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
   }
   uint64_t off = 0;
   for (const auto& m : e->metrics) {
-    MetricArgs a;
+    MetricArgs a = metric_args(e, m.dimension, now_ns, n0, n1, p0, p1, c0, n_nodes);
     a.ops = e->d_mops + m.first_op;
     a.n_ops = m.n_ops;
-    a.dim = m.dimension;
-    a.n0 = n0; a.n1 = n1; a.p0 = p0; a.p1 = p1; a.c0 = c0;
-    a.n_series = m.dimension == KWK_METRIC_DIM_NODE ? n_nodes : m.dimension == KWK_METRIC_DIM_POD ? (p1 - p0) : (c1 - c0);
-    a.st = e->d_st;
-    a.fmt = e->fmt;
-    a.node_ptr = e->d_node_ptr;
-    a.cptr = e->d_cptr;
-    a.ukey = e->d_ukey;
-    a.mixed = e->d_mixed;
-    a.ckeys = e->d_ckeys;
-    a.mbase = e->d_mbase;
-    a.cpu_v = e->d_cpu;
-    a.mem_v = e->d_mem;
-    a.pod_out = e->d_pod_out;
-    a.pod_cum = e->d_pod_cum;
-    a.ccum = e->d_ccum;
-    a.node_out = e->d_node_out;
-    a.pod_created = e->d_pod_created;
-    a.node_created = e->d_node_created;
-    a.node_started = e->d_node_started;
-    a.now = now_ns;
-    a.zero_time_unix_s = e->zero_time_unix_s;
     a.out = e->d_mout + off;
     if (a.n_series)
       hipLaunchKernelGGL(metrics_kernel, dim3((a.n_series + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
@@ -4128,6 +4236,118 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
     off += a.n_series;
   }
   HIP_TRY(hipMemcpyAsync(out, e->d_mout, 8 * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+// Go's sort.Float64s order (NaN first, then ascending)
+static bool go_float_less(double x, double y) { return x < y || (std::isnan(x) && !std::isnan(y)); }
+
+kwk_status kwk_histograms_load(kwk_engine* e, uint32_t n_hist, const kwk_histogram_desc* hists, uint32_t n_buckets,
+                               const kwk_metric_bucket* buckets, uint32_t n_ops, const kwk_metric_op* ops) {
+  ErrScope es_(e);
+  if (!e || (n_hist && !hists) || (n_buckets && !buckets) || (n_ops && !ops)) return fail(KWK_EINVAL, "null argument");
+  uint32_t needs = 0;
+  std::vector<HistDesc> hd(n_hist);
+  std::vector<uint32_t> keys;
+  std::vector<double> bounds;
+  for (uint32_t h = 0; h < n_hist; ++h) {
+    const kwk_histogram_desc& d = hists[h];
+    if (d.n_buckets == 0 || d.n_buckets > kMaxHistBuckets || (uint64_t)d.first_bucket + d.n_buckets > n_buckets)
+      return fail(KWK_EINVAL, "histogram " + std::to_string(h) + ": buckets range (1..64 buckets)");
+    for (uint32_t b = d.first_bucket; b < d.first_bucket + d.n_buckets; ++b)
+      if (kwk_status st = check_metric_program(ops, buckets[b].first_op, buckets[b].n_ops, n_ops, d.dimension, needs))
+        return st;
+    HistDesc x{};
+    x.dim = d.dimension;
+    x.first_bucket = d.first_bucket;
+    x.n_buckets = d.n_buckets;
+    // stored keys: one per distinct le, the last bucket setting it wins (histogram.Set); ascending
+    std::vector<uint32_t> k;
+    for (uint32_t b = 0; b < d.n_buckets; ++b) {
+      const double le = buckets[d.first_bucket + b].le;
+      bool dup = false;
+      for (uint32_t& q : k)
+        if (buckets[d.first_bucket + q].le == le || (std::isnan(le) && std::isnan(buckets[d.first_bucket + q].le))) {
+          q = b;
+          dup = true;
+        }
+      if (!dup) k.push_back(b);
+    }
+    std::stable_sort(k.begin(), k.end(), [&](uint32_t p, uint32_t q) {
+      return go_float_less(buckets[d.first_bucket + p].le, buckets[d.first_bucket + q].le);
+    });
+    std::vector<double> vb;  // the visible upper bounds (getOrRegisterHistogram skips hidden ones), sorted
+    for (uint32_t b = 0; b < d.n_buckets; ++b)
+      if (!buckets[d.first_bucket + b].hidden) vb.push_back(buckets[d.first_bucket + b].le);
+    std::stable_sort(vb.begin(), vb.end(), go_float_less);
+    x.first_key = (uint32_t)keys.size();
+    x.n_keys = (uint32_t)k.size();
+    x.first_bound = (uint32_t)bounds.size();
+    x.n_bounds = (uint32_t)vb.size();
+    x.out_words = x.n_bounds + 3;
+    keys.insert(keys.end(), k.begin(), k.end());
+    bounds.insert(bounds.end(), vb.begin(), vb.end());
+    hd[h] = x;
+  }
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (void** q : {(void**)&e->d_hops, (void**)&e->d_hbuckets, (void**)&e->d_hkeys, (void**)&e->d_hbounds}) {
+    if (*q) HIP_TRY(hipFree(*q));
+    *q = nullptr;
+  }
+  HIP_TRY(hipMalloc(&e->d_hops, sizeof(kwk_metric_op) * ((size_t)n_ops + 1)));
+  HIP_TRY(hipMalloc(&e->d_hbuckets, sizeof(kwk_metric_bucket) * ((size_t)n_buckets + 1)));
+  HIP_TRY(hipMalloc(&e->d_hkeys, sizeof(uint32_t) * (keys.size() + 1)));
+  HIP_TRY(hipMalloc(&e->d_hbounds, sizeof(double) * (bounds.size() + 1)));
+  if (n_ops) HIP_TRY(hipMemcpy(e->d_hops, ops, sizeof(kwk_metric_op) * n_ops, hipMemcpyHostToDevice));
+  if (n_buckets) HIP_TRY(hipMemcpy(e->d_hbuckets, buckets, sizeof(kwk_metric_bucket) * n_buckets, hipMemcpyHostToDevice));
+  if (!keys.empty()) HIP_TRY(hipMemcpy(e->d_hkeys, keys.data(), sizeof(uint32_t) * keys.size(), hipMemcpyHostToDevice));
+  if (!bounds.empty())
+    HIP_TRY(hipMemcpy(e->d_hbounds, bounds.data(), sizeof(double) * bounds.size(), hipMemcpyHostToDevice));
+  e->hists = hd;
+  e->hist_inputs_needed = needs;
+  return KWK_OK;
+}
+
+kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, uint64_t* out,
+                               uint64_t cap, uint64_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
+  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
+  if (e->hist_inputs_needed && !e->d_pod_created) return fail(KWK_ESTATE, "kwk_metrics_inputs must be called first");
+  if ((uint64_t)node_first + n_nodes > e->n_nodes) return fail(KWK_EINVAL, "nodes beyond the usage configuration");
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = ensure_cptr(e)) return st;
+  const uint32_t n0 = node_first, n1 = node_first + n_nodes;
+  const uint32_t p0 = e->h_node_ptr[n0], p1 = e->h_node_ptr[n1];
+  const uint32_t c0 = e->h_cptr[p0];
+  uint64_t total = 0;
+  for (const auto& h : e->hists)
+    total += (uint64_t)metric_args(e, h.dim, now_ns, n0, n1, p0, p1, c0, n_nodes).n_series * h.out_words;
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "histogram buffer too small: need " + std::to_string(total));
+  if (total > e->hout_cap) {
+    if (e->d_hout) HIP_TRY(hipFree(e->d_hout));
+    e->d_hout = nullptr;
+    HIP_TRY(hipMalloc(&e->d_hout, 8 * total));
+    e->hout_cap = total;
+  }
+  uint64_t off = 0;
+  for (const auto& h : e->hists) {
+    MetricArgs a = metric_args(e, h.dim, now_ns, n0, n1, p0, p1, c0, n_nodes);
+    a.ops = e->d_hops;
+    if (a.n_series)
+      hipLaunchKernelGGL(histogram_kernel, dim3((a.n_series + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, h,
+                         (const kwk_metric_bucket*)e->d_hbuckets, (const uint32_t*)e->d_hkeys,
+                         (const double*)e->d_hbounds, e->d_hout + off);
+    HIP_TRY(hipGetLastError());
+    off += (uint64_t)a.n_series * h.out_words;
+  }
+  HIP_TRY(hipMemcpyAsync(out, e->d_hout, 8 * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }

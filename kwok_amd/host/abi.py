@@ -130,6 +130,16 @@ class MetricDesc(C.Structure):
 METRIC_DIM = {"node": 0, "pod": 1, "container": 2}
 
 
+class MetricBucket(C.Structure):
+    _fields_ = [("le", C.c_double), ("hidden", C.c_uint32), ("first_op", C.c_uint32), ("n_ops", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class HistogramDesc(C.Structure):
+    _fields_ = [("dimension", C.c_uint32), ("first_bucket", C.c_uint32), ("n_buckets", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
 class Backoff(C.Structure):
     """kwk_backoff = wait.Backoff; default = defaultBackoff (controllers/utils.go:133-135)."""
     _fields_ = [("duration_ns", C.c_int64), ("factor", C.c_double), ("jitter", C.c_double), ("cap_ns", C.c_int64)]
@@ -138,6 +148,7 @@ class Backoff(C.Structure):
 DEFAULT_BACKOFF = dict(duration_ns=10**9, factor=2.0, jitter=0.2, cap_ns=32 * 60 * 10**9)
 
 assert C.sizeof(MetricOp) == 16 and C.sizeof(MetricDesc) == 16
+assert C.sizeof(MetricBucket) == 24 and C.sizeof(HistogramDesc) == 16
 assert C.sizeof(Hot) == 16 and C.sizeof(Value) == 16 and C.sizeof(StageDesc) == 96
 assert C.sizeof(Lease) == 32 == LEASE_DTYPE.itemsize and C.sizeof(LeaseParams) == 32
 assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.itemsize == 8
@@ -152,7 +163,7 @@ EXPORTS = [
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
     "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
     "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
-    "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n",
+    "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
@@ -192,6 +203,9 @@ def lib():
     L.kwk_metrics_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_metrics_inputs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double]
     L.kwk_metrics_eval.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _p(C.c_uint64)]
+    L.kwk_histograms_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.kwk_histograms_eval.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
+                                      _p(C.c_uint64)]
     L.kwk_set_records.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.kwk_delete.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_retry.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,

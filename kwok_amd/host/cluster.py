@@ -147,6 +147,10 @@ class DeviceReport:
             flat = self.buf.cpu().numpy()
         else:
             flat = np.concatenate([e.aggregate_read(size) for e, size in zip(self.engines, self.sizes)])
+        return self.decode(flat)
+
+    def decode(self, flat: np.ndarray) -> Aggregates:
+        """The packed float64 aggregates (this report's layout) -> Aggregates."""
         names, fired, counts, cnames, usage, off = [], [], [], [], np.zeros(2), 0
         for e, m, mn, size in zip(self.engines, self.masks, self.count_names, self.sizes):
             ns = len(e.p.names)

@@ -360,6 +360,35 @@ class Engine:
             ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
         self._check(abi.lib().kwk_metrics_load(self.h, len(programs), descs, len(flat), ops), "kwk_metrics_load")
 
+    def histograms_load(self, histograms):
+        """histograms: [(dimension name, [(le, hidden, [(op, arg), ...]), ...])] (cel.lower per bucket)."""
+        from . import cel
+        descs = (abi.HistogramDesc * max(1, len(histograms)))()
+        buckets, flat = [], []
+        for i, (dim, bks) in enumerate(histograms):
+            descs[i] = abi.HistogramDesc(abi.METRIC_DIM[dim], len(buckets), len(bks), 0)
+            for le, hidden, prog in bks:
+                buckets.append(abi.MetricBucket(float(le), 1 if hidden else 0, len(flat), len(prog), 0))
+                flat += prog
+        barr = (abi.MetricBucket * max(1, len(buckets)))(*buckets)
+        ops = (abi.MetricOp * max(1, len(flat)))()
+        for i, (op, x) in enumerate(flat):
+            ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
+        self._check(abi.lib().kwk_histograms_load(self.h, len(histograms), descs, len(buckets), barr, len(flat), ops),
+                    "kwk_histograms_load")
+
+    def histograms_eval(self, now_ns: int, node_first: int, n_nodes: int) -> np.ndarray:
+        """Every histogram's series records (uint64 words, see kwk_histograms_eval)."""
+        cnt = C.c_uint64()
+        L = abi.lib()
+        self._check(L.kwk_histograms_eval(self.h, now_ns, node_first, n_nodes, None, 0, C.byref(cnt)),
+                    "kwk_histograms_eval")
+        out = np.zeros(cnt.value, dtype=np.uint64)
+        if cnt.value:
+            self._check(L.kwk_histograms_eval(self.h, now_ns, node_first, n_nodes, abi.ptr(out), cnt.value,
+                                              C.byref(cnt)), "kwk_histograms_eval")
+        return out
+
     def metrics_inputs(self, pod_created_ns, node_created_ns, node_started, zero_time_unix_s: float):
         self._minputs = [np.ascontiguousarray(pod_created_ns, dtype=np.int64),
                          np.ascontiguousarray(node_created_ns, dtype=np.int64),

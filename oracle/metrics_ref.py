@@ -67,3 +67,45 @@ class MetricsOracle:
         out["node_cpu_usage_seconds_total"].append(((), self.cum.advance(("node", name), node_cpu, now_ns)))
         out["node_memory_working_set_bytes"].append(((), node_mem))
         return out
+
+
+def go_float64_to_uint64(x: float) -> int:
+    """uint64(x) for a float64 x as Go compiles it for amd64 (cmd/compile ssagen
+    float64ToUint64: `if x < 2^63 { r = CVTTSD2SQ(x) } else { r = CVTTSD2SQ(x - 2^63) | 1<<63 }`;
+    CVTTSD2SQ of a NaN or of a value outside the int64 range is 0x8000000000000000)."""
+    two63 = float(1 << 63)
+
+    def cvttsd2sq(v: float) -> int:
+        if v != v or v >= two63 or v < -two63:
+            return 1 << 63
+        return int(v) % (1 << 64)  # truncation toward zero, two's complement bits
+
+    if x < two63:
+        return cvttsd2sq(x)
+    return cvttsd2sq(x - two63) | (1 << 63)
+
+
+def histogram_series(buckets, values):
+    """One histogram series as the reference builds and writes it: updateHistogram calls
+    histogram.Set(b.Le, uint64(value)) for every bucket in CR order (metrics.go:380-390; a
+    later equal le overwrites: SyncMap.Store, histogram.go:161-164); getOrRegisterHistogram
+    passes the non-hidden le's as Buckets (metrics.go:143-149), NewHistogram sorts them
+    (histogram.go:88); Write (histogram.go:107-148) walks the stored keys in ascending order.
+    buckets: [(le, hidden)], values: float64 bucket values -> (bounds, counts incl. +Inf,
+    sample count, sample sum)."""
+    stored = {}
+    for (le, _), v in zip(buckets, values):
+        stored[le] = go_float64_to_uint64(v)
+    upper = sorted(le for le, hidden in buckets if not hidden) + [float("inf")]
+    cum = [0] * len(upper)
+    idx = 0
+    count = 0
+    total = 0.0
+    for le in sorted(stored):
+        while idx < len(upper) and le > upper[idx]:
+            idx += 1
+            cum[idx] = (cum[idx] + count) % (1 << 64)
+        cum[idx] = (cum[idx] + stored[le]) % (1 << 64)
+        count = (count + stored[le]) % (1 << 64)
+        total += le * float(stored[le])
+    return upper[:-1], cum, count, total

@@ -86,3 +86,46 @@ def test_shard_engine_aggregates_equal_whole_engine_and_oracle():
         whole.close()
         for e in shards:
             e.close()
+
+
+@pytest.mark.gpu
+def test_native_rccl_report_world1_equals_engine_aggregates():
+    """libkwok_comm (the torch-free collective a Go host links, include/kwok_comm.h) at world
+    size 1: kwk_aggregate into the communicator's buffer, ncclAllReduce in place ordered after
+    the engines' streams by events, read back — equal to the host-side aggregates of the same
+    engines (a one-rank sum is the identity; the N > 1 path is the driver's scaling run)."""
+    from kwok_amd.host.comm import NativeComm, NativeReport, unique_id
+    from tests.parity_util import NOW0, build
+    cl = W.make_cluster("C4", 6, 240, seed=37)
+    objs = cl.pods.materialize()
+    for i, o in enumerate(objs):
+        if i % 4 == 0:
+            o["metadata"]["ownerReferences"] = [{"apiVersion": "batch/v1", "kind": "Job", "name": f"j{i}", "uid": f"u{i}"}]
+    text = open(GOLDEN).read()
+    up = UsageProgram(*load_usage_yaml(text))
+    prog, pods, _ = build(cl.pod_stage_files, objs, harness=True)
+    nprog, nodes, _ = build(cl.node_stage_files, cl.nodes.materialize(), kind_salt=1)
+    pods.usage_config(cl.node_ptr, *usage_columns(up, objs))
+    pm = phase_masks(prog, values=("Running", "Succeeded"))
+    masks = [[0, pm["Running"], pm["Succeeded"]], [0]]
+    names = [["pods", "Running", "Succeeded"], ["nodes"]]
+    comm = NativeComm(unique_id(), 0, 1, 0)
+    try:
+        rep = NativeReport(comm, [pods, nodes], masks, names, usage_engine=pods)
+        for k in range(9):
+            now = NOW0 + k * 10**9
+            pods.step(now, 5, k)
+            nodes.step(now, 5, k)
+            if k % 3 != 2:
+                continue
+            rep.collect(now)
+            got = rep.result()
+            want = engine_aggregates([pods, nodes], masks, names, now, usage_engine=pods)
+            assert got.fired_per_stage.tolist() == want.fired_per_stage.tolist(), k
+            assert got.counts.tolist() == want.counts.tolist(), k
+            np.testing.assert_allclose(got.usage, want.usage, rtol=1e-12)
+            assert got.fired_per_stage.sum() > 0
+    finally:
+        comm.close()
+        pods.close()
+        nodes.close()

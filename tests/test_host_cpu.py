@@ -30,6 +30,23 @@ def _header_functions():
     return sorted(set(re.findall(r"^\s*(?:kwk_status|const char\*|uint32_t)\s+(kwk_\w+)\s*\(", text, re.M)))
 
 
+@pytest.mark.parametrize("header,lib", [("kwok_engine.h", "libkwok_engine.so"), ("kwok_encoder.h", "libkwok_encoder.so"),
+                                        ("kwok_patch.h", "libkwok_patch.so"), ("kwok_comm.h", "libkwok_comm.so")])
+def test_every_header_declaration_is_exported(header, lib):
+    """Each C-ABI library loads (no GPU needed) and defines every function its include/*.h
+    declares (a header's own declarations, not the engine types it includes)."""
+    from kwok_amd import build
+    build.build()
+    path = os.path.join(ROOT, "kwok_amd", "lib", lib)
+    ctypes.CDLL(path)
+    text = open(os.path.join(ROOT, "include", header)).read()
+    declared = set(re.findall(r"^\s*(?:kwk_status|const char\*|uint32_t)\s+(kwk_\w+)\s*\(", text, re.M))
+    assert declared
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (kwk_\w+)", out))
+    assert declared <= exported, sorted(declared - exported)
+
+
 def test_abi_exports_every_header_symbol():
     from kwok_amd import build
     build.build()

@@ -173,3 +173,170 @@ def test_gpu_container_usage_and_metric_scrape():
             t += 2_500_000_000 + 123_457 * k
     finally:
         eng.close()
+
+
+HIST_YAML = """
+kind: Metric
+apiVersion: kwok.x-k8s.io/v1alpha1
+metadata:
+  name: histograms
+spec:
+  path: /metrics/nodes/{nodeName}/metrics/histograms
+  metrics:
+  - name: pod_memory_mib
+    help: pod memory in MiB as bucket counts
+    kind: histogram
+    dimension: pod
+    labels:
+    - name: pod
+      value: pod.metadata.name
+    buckets:
+    - le: 1
+      value: pod.Usage("memory") / 1048576.0
+    - le: 0.5
+      hidden: true
+      value: "2.5"
+    - le: 10
+      value: pod.Usage("cpu") * 1000.0
+    - le: 1
+      value: "3.0"
+    - le: 100
+      value: pod.Usage("cpu") * -5.0
+  - name: node_cpu_hist
+    help: node histogram, the last bucket below a hidden one
+    kind: histogram
+    dimension: node
+    buckets:
+    - le: 2
+      hidden: true
+      value: "1.0"
+    - le: 1
+      value: node.Usage("memory") / 1048576.0
+    - le: 3
+      hidden: true
+      value: "7.9"
+  - name: container_cpu_milli
+    kind: histogram
+    dimension: container
+    labels:
+    - name: container
+      value: container.name
+    - name: pod
+      value: pod.metadata.name
+    buckets:
+    - le: 0.25
+      value: pod.Usage("cpu", container.name) * 1000.0
+    - le: 0.5
+      value: pod.Usage("memory", container.name) / 1048576.0
+"""
+
+
+def _hist_expected(name, pod, node_mem, docs, container=None):
+    """The bucket values of HIST_YAML restated by hand (oracle usage callbacks), per metric."""
+    from oracle import usage_ref
+    if name == "pod_memory_mib":
+        mem = sum(usage_ref.container_usage(docs, pod, c["name"], "memory") for c in pod["spec"]["containers"])
+        cpu = sum(usage_ref.container_usage(docs, pod, c["name"], "cpu") for c in pod["spec"]["containers"])
+        return [(1.0, False), (0.5, True), (10.0, False), (1.0, False), (100.0, False)], \
+            [mem / 1048576.0, 2.5, cpu * 1000.0, 3.0, cpu * -5.0]
+    if name == "node_cpu_hist":
+        return [(2.0, True), (1.0, False), (3.0, True)], [1.0, node_mem / 1048576.0, 7.9]  # node memory (exact sum)
+    cpu = usage_ref.container_usage(docs, pod, container, "cpu")
+    mem = usage_ref.container_usage(docs, pod, container, "memory")
+    return [(0.25, False), (0.5, False)], [cpu * 1000.0, mem / 1048576.0]
+
+
+def test_histogram_write_host_form_equals_oracle():
+    """The host fallback of histogram Set + Write and the float64 -> uint64 conversion against
+    the oracle's restatement (histogram.go:107-164, Go's amd64 conversion), on edge values:
+    duplicate le (last Set wins), hidden buckets, keys above every visible bound, negative / NaN
+    / huge values (wrapping uint64 counts)."""
+    from kwok_amd.host.metrics import go_uint64, histogram_write
+    from oracle.metrics_ref import go_float64_to_uint64, histogram_series
+    for x in (0.0, -0.0, 0.99, 1.5, -0.5, -1.5, -1e300, 2.0**63 - 1024, 2.0**63, 2.0**64, 1e300, float("nan"),
+              float("inf"), float("-inf"), 12345.678):
+        assert go_uint64(x) == go_float64_to_uint64(x), x
+    rng = np.random.default_rng(7)
+    for trial in range(300):
+        n = int(rng.integers(1, 7))
+        les = [float(rng.choice([0.1, 0.5, 1.0, 2.0, 5.0, 10.0])) for _ in range(n)]
+        hidden = [bool(rng.random() < 0.3) for _ in range(n)]
+        vals = [float(rng.choice([0.0, 1.0, 2.7, 100.0, -3.0, 7e18, 1.9e19])) for _ in range(n)]
+        host = histogram_write(list(zip(les, hidden)), [go_uint64(v) for v in vals])
+        bounds, counts, count, total = histogram_series(list(zip(les, hidden)), vals)
+        assert host["bounds"] == bounds and host["counts"] == counts and host["count"] == count, trial
+        assert host["sum"] == total, trial
+
+
+def test_histogram_metric_yaml_lowers():
+    _, configs = load_metric_yaml(HIST_YAML)
+    mp = MetricsProgram(configs)
+    assert [c.kind for c in configs] == ["histogram"] * 3 and mp.host_metrics == []
+    assert len(mp.hist_programs) == 3 and len(mp.hist_programs[0][1]) == 5
+
+
+@pytest.mark.gpu
+def test_gpu_histogram_metrics_scrape():
+    """Histogram Metric CRs evaluated on the device (kwk_histograms_eval) against the oracle's
+    restatement of updateHistogram + histogram.Write (oracle/metrics_ref.py), node by node over
+    two evaluations with dead pods: bucket counts, sample counts exactly; sample sums within
+    1e-6 relative (north_star's tolerance for usage-derived floats)."""
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    from oracle import usage_ref
+    from oracle.metrics_ref import histogram_series
+    cl, pods, text = _mixed_cluster()
+    docs = [d for d in yaml.safe_load_all(text) if d]
+    cols = usage_columns(UsageProgram(*load_usage_yaml(text)), pods)
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pods)
+    ing = Ingest(kp)
+    eng = Engine(kp, capacity=len(pods))
+    nodes = cl.nodes.materialize()
+    try:
+        eng.load_stages()
+        eng.load(*ing.columns(pods), ing.record_array())
+        eng.usage_config(cl.node_ptr, *cols)
+        eng.usage_pods(True)
+        _, configs = load_metric_yaml(HIST_YAML)
+        mp = MetricsProgram(configs)
+        mp.load(eng)
+        alive = np.ones(len(pods), dtype=bool)
+        t = 1_700_000_000 * 10**9
+        checked = 0
+        for k in range(2):
+            if k == 1:
+                gone = np.arange(2, len(pods), 7)
+                eng.delete(gone)
+                alive[gone] = False
+            eng.usage(t)
+            for j in range(len(nodes)):
+                lo, hi = int(cl.node_ptr[j]), int(cl.node_ptr[j + 1])
+                slots = [pods[i] if alive[i] else None for i in range(lo, hi)]
+                dev = mp.scrape(eng, t, j, [nodes[j]], slots, cl.node_ptr)
+                live = [p for p in slots if p is not None]
+                node_mem = sum(usage_ref.container_usage(docs, p, c["name"], "memory")
+                               for p in live for c in p["spec"]["containers"])
+                want = {"node_cpu_hist": [((), _hist_expected("node_cpu_hist", None, node_mem, docs))],
+                        "pod_memory_mib": [((("pod", p["metadata"]["name"]),), _hist_expected("pod_memory_mib", p, 0, docs))
+                                           for p in live],
+                        "container_cpu_milli": [((("container", c["name"]), ("pod", p["metadata"]["name"])),
+                                                 _hist_expected("container_cpu_milli", p, 0, docs, c["name"]))
+                                                for p in live for c in p["spec"]["containers"]]}
+                for name, series in want.items():
+                    d = dict(dev[name])
+                    assert set(d) == {lab for lab, _ in series}, (name, j)
+                    for lab, (bks, vals) in series:
+                        bounds, counts, count, total = histogram_series(bks, vals)
+                        got = d[lab]
+                        assert got["bounds"] == bounds and got["counts"] == counts and got["count"] == count, \
+                            (name, lab, k, got, counts)
+                        assert got["sum"] == pytest.approx(total, rel=REL, abs=1e-9), (name, lab, k)
+                        checked += 1
+            out = mp.exposition(dev)
+            assert "# TYPE pod_memory_mib histogram" in out and 'le="+Inf"' in out
+            t += 3_000_000_000
+        assert checked > 500
+    finally:
+        eng.close()
