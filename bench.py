@@ -120,7 +120,7 @@ def configure_usage(pods, pvars, pidx, n_nodes_local, pods_per_node):
     """kwk_usage_config for the shard: the default usage-from-annotation ClusterResourceUsage
     (kustomize/metrics/usage/usage-from-annotation.yaml) evaluated once per variant."""
     from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
-    path = os.path.join(ROOT, "tests", "golden", "metrics", "usage-from-annotation.yaml")
+    path = os.path.join(ROOT, "kwok_amd", "metrics", "usage-from-annotation.yaml")
     up = UsageProgram(*load_usage_yaml(open(path).read()))
     vkeys, cv, mv, mx, ck = usage_columns(up, pvars)
     node_ptr = np.arange(n_nodes_local + 1, dtype=np.uint32) * np.uint32(pods_per_node)
@@ -155,6 +155,8 @@ class Reporter:
         return self.report
 
 
+SWEEP_NAMES = {1: "sweep16_kernel", 2: "sweep16_fsm_kernel", 3: "sweepw_kernel<4>", 4: "sweepw_kernel<8>",
+               5: "sweep8_kernel"}  # kwk_last_sweep kernel codes (KWK_SWEEP_*)
 EV_EVERY = 2  # HIP events bracket the pod sweep of every 2nd step: each marker idles the stream ~5 us (r2b)
 
 
@@ -429,7 +431,9 @@ def main():
         r = configs.run(args.config, args.steps, args.warmup, args.seed)
         line = {"metric": r.pop("metric"), "value": round(r.pop("value"), 1), "n_gpus": 1, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(r.pop("ms_per_step"), 4), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "u32/i64" if args.config != "C4" else "f64",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": ({1: "u8", 2: "u16", 4: "u32", 8: "u32x2"}.get(r.get("state_bytes_per_object"), "u32") + "/i64"
+                          if args.config != "C4" else "f64"),
                 "data": "synthetic (seeded kwokctl-shaped objects), cache-resident working set",
                 "config": {"workload": r.pop("workload")}, "detail": r}
         print(json.dumps(line), flush=True)
@@ -517,6 +521,7 @@ def main():
     elapsed = time.perf_counter() - t0
     agg_dict = agg.result().as_dict() if agg is not None else None  # the last interval's all-reduced aggregates
     s1p, s1n = pods.stats(), nodes.stats()
+    pod_kernel = pods.last_sweep()
     n_ev = (args.steps + EV_EVERY - 1) // EV_EVERY
     if world > 1:  # sampled after the timed region (the same steps continued)
         k0 = args.warmup + args.steps
@@ -585,8 +590,8 @@ def main():
                 "traffic_note": (f"rocprofv3 PMC child passes of this workload ({traffic['launches']} pod-sweep launches): "
                                  f"FETCH_SIZE x 2 = {traffic['read']} B read + WRITE_SIZE = {traffic['write']} B written "
                                  "per launch" if traffic else f"null: {pmc_err}"),
-                "kernel": ("sweep16_fsm_kernel" if sb == 2 and args.tune_fsm_kernel != 0 else
-                           "sweep16_kernel" if sb == 2 else "sweepw_kernel") + " (pods)",
+                "kernel": SWEEP_NAMES.get(pod_kernel["kernel"], "?") + (" persistent" if pod_kernel["persistent"] else "")
+                          + " (pods)",
                 "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
@@ -605,7 +610,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "stage transitions/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_s / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
-            "dtype": {2: "u16", 4: "u32", 8: "u32x2"}[sb] + "/i64",
+            "dtype": {1: "u8", 2: "u16", 4: "u32", 8: "u32x2"}[sb] + "/i64",
             "data": "synthetic (seeded kwokctl-shaped pods/nodes; pod-fast + node-fast/heartbeat stages)",
             "config": {"workload": f"C5: {total_nodes:,} nodes / {total_nodes * args.pods_per_node:,} pods in total "
                                    f"over {world} GPU(s), pod-fast + node-initialize/heartbeat, harness churn "

@@ -61,7 +61,8 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
     """The RCCL cluster-aggregate collective (host code over librccl + the engine's streams)."""
     if not force and not _stale(COMM_OUT, COMM_SRC + COMM_HDR + [OUT]):
         return COMM_OUT
-    cmd = ["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"),
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-Wno-unused-value", "-I", os.path.join(ROOT, "include"),
            "-o", COMM_OUT + ".tmp"] + \
         COMM_SRC + ["-L", os.path.dirname(OUT), "-lkwok_engine", "-lrccl", "-Wl,-rpath,$ORIGIN"]
     if verbose:

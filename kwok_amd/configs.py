@@ -25,8 +25,7 @@ from .host.engine import Engine, Ingest
 from .host.stages import load_stage_files
 
 NOW0 = 1_700_000_000 * 10**9
-USAGE_YAML = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "metrics",
-                          "usage-from-annotation.yaml")
+USAGE_YAML = os.path.join(W.METRICS_DIR, "usage-from-annotation.yaml")
 
 
 def _engine(stage_files, variants, index, harness, kind_salt, device=0):

@@ -164,13 +164,18 @@ __device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool de
 //          [pred: pred_bits][class: cbits][stage code: sbits][flags: 5]
 //          flags = sched bits 8..12 (ALIVE DIRTY MANAGED HASREC MATCHERR); stage code n_stages = none.
 // half   : the same packing in one u16 per slot when it fits 16 bits (narrow = half = 1).
+// byte   : one id byte per slot indexing a dictionary of the half words that can occur (a table-
+//          only program; narrow = half = byte = 1): id2w / w2id on the device.
 struct StateFmt {
   uint32_t narrow;
   uint32_t half;
+  uint32_t byte;
   uint32_t pmask;
   uint32_t cshift, cmask;
   uint32_t sshift, smask, none_code;
   uint32_t fshift;
+  const uint16_t* id2w;  // byte: the word of each id
+  const uint8_t* w2id;   // byte: the id of each half word (0xFF: none)
 };
 
 __host__ __device__ __forceinline__ uint2 fmt_unpack(uint32_t w, const StateFmt& f) {
@@ -190,11 +195,13 @@ __host__ __device__ __forceinline__ uint32_t fmt_pack(uint32_t pred, uint32_t sc
 
 // small kernels (scatter / delete / usage / count) branch on the format at run time
 __device__ __forceinline__ uint2 load_state(const void* st, uint64_t i, const StateFmt& f) {
+  if (f.byte) return fmt_unpack(f.id2w[reinterpret_cast<const uint8_t*>(st)[i]], f);
   if (f.half) return fmt_unpack(reinterpret_cast<const uint16_t*>(st)[i], f);
   return f.narrow ? fmt_unpack(reinterpret_cast<const uint32_t*>(st)[i], f) : reinterpret_cast<const uint2*>(st)[i];
 }
 __device__ __forceinline__ void store_state(void* st, uint64_t i, uint2 v, const StateFmt& f) {
-  if (f.half) reinterpret_cast<uint16_t*>(st)[i] = (uint16_t)fmt_pack(v.x, v.y, f);
+  if (f.byte) reinterpret_cast<uint8_t*>(st)[i] = f.w2id[fmt_pack(v.x, v.y, f) & 0xFFFFu];
+  else if (f.half) reinterpret_cast<uint16_t*>(st)[i] = (uint16_t)fmt_pack(v.x, v.y, f);
   else if (f.narrow) reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
   else reinterpret_cast<uint2*>(st)[i] = v;
 }
@@ -1207,6 +1214,255 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   }
 }
 
+// ------------------------------------------------------------------ 1-byte state sweep
+// When the compiled program is a finite state machine that needs nothing beyond the 2-byte word
+// (pod-fast, node-fast: no Philox draw, value record or deletion column reachable) the words
+// that can occur are few — the closure of the resident words under the transition table, delete,
+// the lease MANAGED / DIRTY updates and upserts: 44 for pod-fast with the bench harness, 20 for
+// node-fast + heartbeat — so the device keeps one byte per object, an index into a dictionary of
+// at most 255 words.  The id's top bits carry what phase 1 tests:
+//   bit 7  the word needs work whatever its due time (managed, and dirty or harness churn)
+//   bit 6  a stage is queued on a managed object (work once its due time has passed)
+//   bit 5  alive (usage / counts)        bits 0-4: index within that class
+// so the idle test is two mask-and-shift ops per 4 objects, and the transition of a work item
+// is one lookup in a 512-entry id table staged in LDS (no L2 gather).  The column halves: the
+// C5 state stream is 100 MB instead of 200 MB, read once and rewritten as whole 128-byte lines.
+constexpr uint32_t kIdNeed = 0x80u, kIdPend = 0x40u, kIdAlive = 0x20u, kIdIndex = 0x1Fu;
+constexpr uint32_t kIdInvalid = 0xFFu;  // not in the dictionary (never stored: the host closes it)
+constexpr int kQ8 = 2;                  // 16-byte chunks per lane: 32 ids per lane, 2048 per wave
+
+// wave-region offset (minus lane * 16) of bit k of a lane's phase-1 masks in the 1-byte sweep:
+// bit k = b * 8 + q * 4 + j  <->  chunk q, dword j, byte b (so a dword's four flags land with
+// one mask-and-shift each)
+__device__ __forceinline__ constexpr uint32_t bit_id8(const uint32_t k) {
+  return ((k >> 2) & 1u) * 1024u + (k & 3u) * 4u + (k >> 3);
+}
+
+template <bool kPersist, int kDepth>
+__global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
+  constexpr int Q = kQ8;
+  constexpr int K = 16 * Q;                // ids per lane
+  constexpr uint32_t kWave = 64u * K;      // ids per wave region
+  constexpr uint32_t kTile = kBlock * K;   // ids per block
+  constexpr uint32_t kSeg8 = 64u * K + 32u;
+  static_assert(kDepth >= 1 && kDepth <= 2 && (kPersist || kDepth == 1), "prefetch depth");
+  static_assert(kWave <= 8192 && K == 32, "13-bit record slots, 32-bit lane masks");
+  __shared__ unsigned int s_stat[kStatWords];
+  __shared__ uint32_t s_fsm[512];
+  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, (a.n + 15u) & ~15u);
+  const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+  const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
+  uint4 va[kDepth][Q];
+  auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
+    const uint32_t off = t < n_tiles ? t * kTile + wave * kWave + lane * 16u : kOOB - 2048u;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, off + (uint32_t)q * 1024u, 0, 0);
+      dst[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  uint32_t tile = blockIdx.x;
+  issue_tile(va[0], tile);
+  if (kDepth > 1) issue_tile(va[kDepth - 1], tile + gridDim.x);
+  const uint32_t n_stages = a.table->n_stages;
+  for (uint32_t j = threadIdx.x; j < 512u; j += kBlock) s_fsm[j] = a.fsm[j];
+  if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  __syncthreads();
+
+  uint32_t stc01 = 0, stc23 = 0;        // per lane: fired records of stages 0 | 1 << 16, 2 | 3 << 16
+  uint32_t n_matched = 0, n_bytes = 0;  // per lane
+  uint32_t n_lline = 0;                 // per lane: bytes of the phase-3 line stores
+  uint32_t w_bytes = 0, w_line = 0;     // wave-uniform
+  uint32_t wave_fired = 0;              // wave-uniform
+  uint16_t* __restrict__ wl = s_work[wave];
+  uint4* __restrict__ tq = s_tile[wave];
+  uint8_t* __restrict__ tb = reinterpret_cast<uint8_t*>(tq);
+  uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+
+  auto tile_body = [&](uint4 (&v)[Q], const uint32_t tile) __attribute__((always_inline)) {
+    const uint32_t wbase = tile * kTile + wave * kWave;
+    const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
+    uint32_t seg_n = 0;  // wave-uniform
+    const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
+    uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * kSeg8;
+    const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg8 * 4u);
+    uint4 cur_copy[Q];
+    if (kDepth == 1) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cur_copy[q] = v[q];
+    }
+    uint4 (&cur)[Q] = kDepth == 1 ? cur_copy : v;
+    if (kPersist && kDepth == 1) issue_tile(v, tile + gridDim.x);
+    // ---- phase 1: the id's need / pend bits, one mask-and-shift per dword and flag
+    uint32_t in_range = 0xFFFFFFFFu;
+    if (!full) {
+      in_range = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t left = (int64_t)a.n - (int64_t)(wbase + (uint32_t)q * 1024u + lane * 16u);
+        const uint32_t c = left <= 0 ? 0u : left >= 16 ? 16u : (uint32_t)left;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+#pragma unroll
+          for (uint32_t b = 0; b < 4; ++b) in_range |= (j * 4u + b < c ? 1u : 0u) << (b * 8u + (uint32_t)q * 4u + j);
+      }
+    }
+    uint32_t need = 0, pend = 0, ready = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t dw[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t jj = (uint32_t)(q * 4 + j);
+        need |= (dw[j] & 0x80808080u) >> (7u - jj);
+        pend |= ((dw[j] << 1) & 0x80808080u) >> (7u - jj);
+      }
+    }
+    need &= in_range;
+    pend &= in_range;
+    if (__ballot(pend != 0)) {  // a queued stage: is it due?
+#pragma unroll 8
+      for (int k = 0; k < K; ++k) {
+        const uint32_t p = (pend >> k) & 1u;
+        const int64_t d = buf_load_i64(due_rs, p ? (wbase + bit_id8((uint32_t)k) + lane * 16u) * 8u : kOOB);
+        ready |= (p & (uint32_t)(d <= a.now)) << k;
+      }
+      need |= ready;
+    }
+    n_bytes += (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
+    uint32_t n_work = 0, pos = 0;
+    {
+      const uint32_t cnt = (uint32_t)__popc(need);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const unsigned long long bal = __ballot((cnt >> b) & 1u);
+        pos += (uint32_t)__popcll(bal & lt) << b;
+        n_work += (uint32_t)__popcll(bal) << b;
+      }
+      for (uint32_t m = need; m; m &= m - 1u) {
+        const uint32_t k = (uint32_t)__ffs(m) - 1u;
+        wl[pos++] = (uint16_t)(bit_id8(k) + lane * 16u + (((ready >> k) & 1u) << 15));
+      }
+    }
+    if (n_work) {
+      // ---- phase 2: one LDS table lookup per work item
+#pragma unroll
+      for (int q = 0; q < Q; ++q) tq[q * 64 + lane] = cur[q];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : 0xFFFFFFFFu;
+      for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
+        const uint32_t we = nwe;
+        if (c + 64u < n_work) nwe = c + 64u + lane < n_work ? (uint32_t)wl[c + 64u + lane] : 0xFFFFFFFFu;
+        const bool act = we != 0xFFFFFFFFu;
+        const uint32_t w = we & 0x7FFu, rdy = (we >> 15) & 1u;
+        const uint32_t id = act ? (uint32_t)tb[w] : 0u;
+        const uint32_t e = s_fsm[(rdy << 8) | id];
+        if (act) {
+          tb[w] = (uint8_t)e;
+          n_matched += (e >> 25) & 1u;
+          n_bytes += ((e >> 26) & 15u) * 2u - 1u;  // the table counts a 2-byte word write
+        }
+        const bool dw = act && (e & kFsmDue);
+        if (__ballot(dw)) {  // a delayed stage is scheduled
+          const int64_t dd = buf_load_i64(fdue_rs, dw ? ((rdy << 8) | id) * 8u : kOOB);
+          const int64_t t = sat_add(a.now, dd);
+          const uint32_t off = dw ? (wbase + w) * 8u : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, due_rs, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)((uint64_t)t >> 32), due_rs, off + 4u, 0, 0);
+        }
+        const bool fire = act && ((e >> 21) & 1u);
+        const unsigned long long bal = __ballot(fire);
+        if (bal) {
+          const uint32_t p = seg_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          const uint32_t rec = w | ((e >> 16) & 31u) << 13 | ((e >> 22) & 7u) << 18;
+          __builtin_amdgcn_raw_buffer_store_b32(rec, seg_rs, fire ? (1u + p) * 4u : kOOB, 0, 0);
+          const uint32_t nf = (uint32_t)__popcll(bal);
+          seg_n += nf;
+          w_bytes += 4u * nf;
+          const uint32_t code = fire ? ((e >> 16) & 31u) : 31u;
+          if (n_stages <= 4) {
+            const uint32_t inc = 1u << (16u * (code & 1u));
+            stc01 += code < 2u ? inc : 0u;
+            stc23 += (code - 2u) < 2u ? inc : 0u;
+          } else {
+            for (uint32_t st = 0; st < n_stages; ++st) {
+              const unsigned long long same = __ballot(code == st);
+              if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
+            }
+          }
+        }
+      }
+      w_line -= n_work;  // the ids' own writes are replaced by the line stores below
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // ---- phase 3: whole 128-byte lines wherever an id changed
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint4 nv = tq[q * 64 + lane];
+        const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
+        const unsigned long long bal = __ballot(ch);
+        if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
+          store_chunk_nt(&gq[(wbase + (uint32_t)q * 1024u + lane * 16u) / 16u], nv);
+          n_lline += 16u;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    {
+      const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
+      for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
+      if (lane == 0) {
+        seg32[0] = seg_n;
+        a.wave_counts[seg_id] = seg_n;
+      }
+      w_line += 4u * (end - used);
+    }
+    wave_fired += seg_n;
+    w_bytes += 4u;
+    if (kPersist && kDepth == 2) issue_tile(v, tile + 2u * gridDim.x);
+  };
+  if constexpr (!kPersist) {
+    if (tile < n_tiles) tile_body(va[0], tile);
+  } else if constexpr (kDepth == 1) {
+    for (; tile < n_tiles; tile += gridDim.x) tile_body(va[0], tile);
+  } else {
+    for (; tile < n_tiles; tile += 2u * gridDim.x) {
+      tile_body(va[0], tile);
+      if (tile + gridDim.x >= n_tiles) break;
+      tile_body(va[kDepth - 1], tile + gridDim.x);
+    }
+  }
+
+  for (int off = 32; off > 0; off >>= 1) {
+    n_matched += __shfl_xor(n_matched, off);
+    n_bytes += __shfl_xor(n_bytes, off);
+    n_lline += __shfl_xor(n_lline, off);
+  }
+  uint32_t stn[4] = {stc01 & 0xFFFFu, stc01 >> 16, stc23 & 0xFFFFu, stc23 >> 16};
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+    for (int off = 32; off > 0; off >>= 1) stn[st] += __shfl_xor(stn[st], off);
+  if (lane == 0) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      if (stn[st]) atomicAdd(&s_stat[3 + st], stn[st]);
+    atomicAdd(&s_stat[0], n_matched);
+    atomicAdd(&s_stat[1], wave_fired);
+    atomicAdd(&s_stat[2], n_bytes + w_bytes);
+    atomicAdd(&s_stat[kStatLine], n_bytes + w_bytes + n_lline + w_line);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
+    const unsigned int val = s_stat[threadIdx.x];
+    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
+  }
+}
+
 // ------------------------------------------------------------------ 4- and 8-byte state sweep
 // Sweep over the 4-byte packed and the 8-byte wide formats (pod-general / chaos and any
 // program wider than 16 bits: no transition table, every work item runs process_object).
@@ -1778,7 +2034,12 @@ __device__ __forceinline__ double dur_seconds(int64_t d) {
 // alive flag of pod j of a lane's run (kURun words of WB bytes in WB 16-byte chunks)
 template <uint32_t WB>
 __device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t abit) {
-  if constexpr (WB == 2) {
+  if constexpr (WB == 1) {  // 1-byte ids: the alive bit is an id bit (kIdAlive)
+    const uint4 c = sv[0];
+    const int d = j >> 2;
+    const uint32_t w = d == 0 ? c.x : d == 1 ? c.y : d == 2 ? c.z : c.w;
+    return ((w >> (8 * (j & 3))) & abit) != 0;
+  } else if constexpr (WB == 2) {
     const uint4 c = sv[j >> 3];
     const int d = (j >> 1) & 3;
     const uint32_t w = d == 0 ? c.x : d == 1 ? c.y : d == 2 ? c.z : c.w;
@@ -1864,7 +2125,7 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
   const double* __restrict__ cpu_v = lds_vals ? s_val : a.cpu_v;
   const double* __restrict__ mem_v = lds_vals ? s_val + a.n_cpu : a.mem_v;
   // the alive flag in the raw word (packed: at fshift; wide: in sched)
-  const uint32_t abit = WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  const uint32_t abit = WB == 1 ? kIdAlive : WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
   double tot_c = 0.0, tot_m = 0.0;  // per lane: the nodes it finalised
   uint32_t* __restrict__ sp = s_ptr[wave];
   double2* __restrict__ ss = s_sum[wave];
@@ -2120,7 +2381,7 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   }
   __syncthreads();
   const uint32_t nv = a.n_cpu + a.n_mem;  // podv row: cpu values then memory values
-  const uint32_t abit = WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  const uint32_t abit = WB == 1 ? kIdAlive : WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
   double tot_c = 0.0, tot_m = 0.0;
   uint32_t* __restrict__ sp = s_ptr[wave];
   double2* __restrict__ ss = s_sum[wave];
@@ -2655,6 +2916,78 @@ __global__ __launch_bounds__(kBlock) void count16_lut_kernel(const void* __restr
     part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < 4u ? s_cnt[threadIdx.x] : 0u;
 }
 
+// 1-byte ids: one LDS lookup per id and group of four masks — entry [g][id] holds, in byte m, 1 if
+// the id's word counts for mask 4g + m (alive and, unless the mask is 0, (pred & mask) != 0); each
+// block builds its table from the dictionary.  Same partial rows as count_kernel.
+template <int NG>  // mask groups of four (n_masks <= 4 * NG)
+__global__ __launch_bounds__(kBlock) void count8_kernel(const void* __restrict__ st, uint32_t n, StateFmt fmt,
+                                                        const uint32_t* __restrict__ masks, uint32_t n_masks,
+                                                        uint32_t* __restrict__ part) {
+  __shared__ uint32_t s_lut[NG][256];
+  __shared__ unsigned int s_cnt[4 * NG];
+  for (uint32_t e = threadIdx.x; e < 256u * NG; e += kBlock) {
+    const uint32_t g = e >> 8, id = e & 255u;
+    const uint2 v = fmt_unpack(fmt.id2w[id], fmt);
+    const uint32_t al = (v.y & KWK_F_ALIVE) ? 1u : 0u;
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {
+      const uint32_t k = 4u * g + m;
+      if (k < n_masks) {
+        const uint32_t mk = masks[k];
+        x |= (al & ((mk == 0u || (v.x & mk) != 0u) ? 1u : 0u)) << (8 * m);
+      }
+    }
+    s_lut[g][id] = x;
+  }
+  if (threadIdx.x < 4 * NG) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t cnt[4 * NG];
+#pragma unroll
+  for (int m = 0; m < 4 * NG; ++m) cnt[m] = 0;
+  const uint64_t n_chunks = ((uint64_t)n + 15u) / 16u;
+  const uint4* __restrict__ q = reinterpret_cast<const uint4*>(st);
+  constexpr uint32_t kCountU = 4;  // 64 ids per lane and round: byte counters stay below 256
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock * kCountU + threadIdx.x; c0 < n_chunks;
+       c0 += (uint64_t)gridDim.x * kBlock * kCountU) {
+    uint4 vs[kCountU];
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u) {
+      const uint64_t c = c0 + u * kBlock;
+      vs[u] = c < n_chunks ? q[c] : make_uint4(0u, 0u, 0u, 0u);  // id 0: not alive
+    }
+    uint32_t acc[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kCountU; ++u) {
+      const uint64_t i0 = (c0 + u * kBlock) * 16u;
+      const bool whole = i0 + 16u <= n;
+      const uint32_t dw[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        uint32_t id = (dw[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+        if (!whole && i0 + (uint64_t)h >= n) id = 0u;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[g] += s_lut[g][id];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) cnt[4 * g + m] += (acc[g] >> (8 * m)) & 0xFFu;
+  }
+#pragma unroll
+  for (int m = 0; m < 4 * NG; ++m) {
+    uint32_t c = cnt[m];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_cnt[m], c);
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxCountMasks)
+    part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < 4u * NG ? s_cnt[threadIdx.x] : 0u;
+}
+
 // out[m] = sum over the blocks' partial rows (1024 threads: 16 masks x 64 block strides)
 __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
                                                            uint32_t n_masks, unsigned long long* __restrict__ out) {
@@ -2669,6 +3002,14 @@ __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __res
     __syncthreads();
   }
   if (threadIdx.x < n_masks) out[threadIdx.x] = s[threadIdx.x];
+}
+
+static void launch_count8(uint32_t n_masks, dim3 g, hipStream_t s, const void* st, uint32_t n, const StateFmt& fmt,
+                          const uint32_t* masks, uint32_t* part, unsigned long long* out) {
+  if (n_masks <= 4) hipLaunchKernelGGL((count8_kernel<1>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
+  else if (n_masks <= 8) hipLaunchKernelGGL((count8_kernel<2>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
+  else hipLaunchKernelGGL((count8_kernel<4>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
+  hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
 }
 
 template <uint32_t WB>
@@ -2910,6 +3251,19 @@ struct kwk_engine {
   uint32_t fsm_bits = 0;
   int fsm_harness = -1;       // harness enable the table was built for (-1: no table)
   uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_FSM_KERNEL: 0 never, else its prefetch depth
+  // the 1-byte format (StateFmt.byte): a dictionary of the half words that can occur
+  bool allow_byte = true;     // KWK_ENGINE_STATE16 clears it
+  bool byte_tune = true;      // KWK_TUNE_BYTE_STATE
+  bool byte_ok = false;       // the transition table exists for the loaded program and harness
+  std::vector<uint32_t> h_fsm;    // host copy of the 2-byte transition table (closure, id table)
+  std::vector<int64_t> h_fsm_due;
+  std::vector<uint16_t> h_id2w;   // [256] word of each id
+  std::vector<uint8_t> h_w2id;    // [65536] id of each half word (kIdInvalid: none)
+  uint32_t id_fill[8] = {};       // ids used per class (need, pend, alive)
+  uint16_t* d_id2w = nullptr;
+  uint8_t* d_w2id = nullptr;
+  uint32_t* d_fsm8 = nullptr;     // [2][256] id transition table of sweep8_kernel
+  int64_t* d_fsm8_due = nullptr;
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -3046,14 +3400,17 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
 
 static kwk_status build_fsm(kwk_engine* e);
 
-static size_t word_bytes(const StateFmt& f) { return f.half ? 2 : f.narrow ? 4 : 8; }
+static size_t word_bytes(const StateFmt& f) { return f.byte ? 1 : f.half ? 2 : f.narrow ? 4 : 8; }
 
 static bool same_fmt(const StateFmt& a, const StateFmt& b) { return memcmp(&a, &b, sizeof(StateFmt)) == 0; }
 
-// host-side conversion of device state words <-> (pred, sched)
-static std::vector<uint2> unpack_words(const std::vector<uint8_t>& raw, const StateFmt& f, uint32_t n) {
+// host-side conversion of device state words <-> (pred, sched); the 1-byte format through the
+// engine's dictionary
+static std::vector<uint2> unpack_words(const kwk_engine* e, const std::vector<uint8_t>& raw, const StateFmt& f, uint32_t n) {
   std::vector<uint2> out(n);
-  if (f.half) {
+  if (f.byte) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(e->h_id2w[raw[i]], f);
+  } else if (f.half) {
     const uint16_t* w = reinterpret_cast<const uint16_t*>(raw.data());
     for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
   } else if (f.narrow) {
@@ -3065,9 +3422,11 @@ static std::vector<uint2> unpack_words(const std::vector<uint8_t>& raw, const St
   return out;
 }
 
-static std::vector<uint8_t> pack_words(const std::vector<uint2>& v, const StateFmt& f) {
+static std::vector<uint8_t> pack_words(const kwk_engine* e, const std::vector<uint2>& v, const StateFmt& f) {
   std::vector<uint8_t> raw(word_bytes(f) * v.size());
-  if (f.half) {
+  if (f.byte) {
+    for (size_t i = 0; i < v.size(); ++i) raw[i] = e->h_w2id[fmt_pack(v[i].x, v[i].y, f) & 0xFFFFu];
+  } else if (f.half) {
     uint16_t* w = reinterpret_cast<uint16_t*>(raw.data());
     for (size_t i = 0; i < v.size(); ++i) w[i] = (uint16_t)fmt_pack(v[i].x, v[i].y, f);
   } else if (f.narrow) {
@@ -3100,6 +3459,215 @@ static kwk_status ensure_stage_buf(kwk_engine* e, size_t bytes) {
   return KWK_OK;
 }
 
+// ---- the 1-byte format's dictionary
+// class of a half word: bit 2 needs work whatever its due (managed, and dirty or the harness
+// churns it), bit 1 a queued stage (managed), bit 0 alive — the id's top three bits
+static uint32_t word_class(const kwk_engine* e, uint32_t w) {
+  const StateFmt& f = e->fmt;
+  const uint32_t fl = (w >> f.fshift) & 0x1Fu;  // sched bits 8..12
+  const bool alive = fl & (KWK_F_ALIVE >> 8), dirty = fl & (KWK_F_DIRTY >> 8), managed = fl & (KWK_F_MANAGED >> 8);
+  const uint32_t pred = w & f.pmask;
+  const bool pend = managed && ((w >> f.sshift) & f.smask) != f.none_code;
+  bool need = false;
+  if (managed) {
+    need = dirty;
+    if (e->harness.enable) {
+      const uint32_t term = e->harness.terminal_mask & f.pmask, del = e->harness.deletion_bit & f.pmask;
+      need = need || !alive || ((pred & term) != 0 && (pred & del) == 0);
+    }
+  }
+  return (need ? 4u : 0u) | (pend ? 2u : 0u) | (alive ? 1u : 0u);
+}
+
+// the words a half word can become on the device: the transition table for the lookups the sweep
+// makes (need -> not ready, queued -> ready), kwk_delete, and the lease updates of MANAGED /
+// DIRTY; false if a reachable lookup is general (a Philox draw, a record or the deletion column)
+static bool word_successors(const kwk_engine* e, uint32_t w, std::vector<uint32_t>& out) {
+  const uint32_t cls = word_class(e, w);
+  const uint32_t bits = e->fsm_bits;
+  if (cls & 4u) {
+    const uint32_t t = e->h_fsm[w];
+    if (t & kFsmGeneral) return false;
+    out.push_back(t & 0xFFFFu);
+  }
+  if (cls & 2u) {
+    const uint32_t t = e->h_fsm[(1u << bits) | w];
+    if (t & kFsmGeneral) return false;
+    out.push_back(t & 0xFFFFu);
+  }
+  const uint2 v = fmt_unpack(w, e->fmt);
+  auto add = [&](uint32_t sched) { out.push_back(fmt_pack(v.x, sched, e->fmt) & 0xFFFFu); };
+  add((v.y & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE);  // kwk_delete
+  add(v.y | KWK_F_MANAGED);   // lease_kernel / lease_pods_kernel: Held()
+  add(v.y & ~KWK_F_MANAGED);
+  add(v.y | KWK_F_DIRTY);     // a successful lease sync re-matches
+  add(v.y & ~KWK_F_DIRTY);    // kwk_lease_fail undoes it
+  return true;
+}
+
+static void dict_reset(kwk_engine* e) {
+  e->h_id2w.assign(256, 0);
+  e->h_w2id.assign(65536, (uint8_t)kIdInvalid);
+  for (uint32_t& c : e->id_fill) c = 0;
+  e->h_w2id[0] = 0;  // id 0 = word 0 (padding, never-loaded slots): not alive, not managed
+  e->id_fill[0] = 1;
+}
+
+// adds the closure of `seeds` to the dictionary; false (dictionary unchanged) if a class runs out
+// of ids or a general transition is reachable
+static bool dict_extend(kwk_engine* e, const std::vector<uint32_t>& seeds, bool& changed) {
+  changed = false;
+  std::vector<uint32_t> added, frontier, next;
+  std::vector<uint8_t> seen(65536, 0);
+  for (uint32_t w : seeds) {
+    w &= 0xFFFFu;
+    if (e->h_w2id[w] == kIdInvalid && !seen[w]) {
+      seen[w] = 1;
+      frontier.push_back(w);
+    }
+  }
+  uint32_t fill[8];
+  memcpy(fill, e->id_fill, sizeof(fill));
+  while (!frontier.empty()) {
+    next.clear();
+    for (uint32_t w : frontier) {
+      const uint32_t c = word_class(e, w);
+      if (fill[c] >= (c == 7u ? kIdIndex : kIdIndex + 1u)) return false;  // 0xFF stays invalid
+      ++fill[c];
+      added.push_back(w);
+      std::vector<uint32_t> succ;
+      if (!word_successors(e, w, succ)) return false;
+      for (uint32_t x : succ)
+        if (e->h_w2id[x] == kIdInvalid && !seen[x]) {
+          seen[x] = 1;
+          next.push_back(x);
+        }
+    }
+    frontier.swap(next);
+  }
+  for (uint32_t w : added) {
+    const uint32_t c = word_class(e, w);
+    const uint32_t id = (c << 5) | e->id_fill[c]++;
+    e->h_id2w[id] = (uint16_t)w;
+    e->h_w2id[w] = (uint8_t)id;
+  }
+  changed = !added.empty();
+  return true;
+}
+
+// the dictionary and the id transition table on the device (synchronous)
+static kwk_status dict_upload(kwk_engine* e) {
+  std::vector<uint32_t> t8(512);
+  std::vector<int64_t> d8(512, 0);
+  const uint32_t bits = e->fsm_bits;
+  for (uint32_t id = 0; id < 256; ++id) {
+    const uint32_t w = e->h_id2w[id];
+    const bool used = id == 0 || (id != kIdInvalid && (id & kIdIndex) < e->id_fill[id >> 5]);
+    for (uint32_t rdy = 0; rdy < 2; ++rdy) {
+      const uint32_t t = e->h_fsm[(rdy << bits) | w];
+      uint32_t x = id;  // unused ids and lookups the sweep never makes: no change, nothing fires
+      if (used && !(t & kFsmGeneral) && e->h_w2id[t & 0xFFFFu] != kIdInvalid) {
+        x = (t & 0xFFFF0000u) | e->h_w2id[t & 0xFFFFu];
+        d8[(rdy << 8) | id] = e->h_fsm_due[(rdy << bits) | w];
+      }
+      t8[(rdy << 8) | id] = x;
+    }
+  }
+  HIP_TRY(hipMemcpy(e->d_id2w, e->h_id2w.data(), sizeof(uint16_t) * 256, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_w2id, e->h_w2id.data(), 65536, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_fsm8, t8.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_fsm8_due, d8.data(), sizeof(int64_t) * 512, hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+// resident rows [0, n_active) as (pred, sched) (synchronises)
+static kwk_status read_rows(kwk_engine* e, std::vector<uint2>& rows) {
+  const uint32_t n = e->n_active;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
+  if (n) HIP_TRY(hipMemcpy(raw.data(), e->d_st, raw.size(), hipMemcpyDeviceToHost));
+  rows = unpack_words(e, raw, e->fmt, n);
+  return KWK_OK;
+}
+
+// writes rows [0, n) in format nf and makes nf current (the dictionary must hold their words)
+static kwk_status write_rows(kwk_engine* e, const std::vector<uint2>& rows, const StateFmt& nf) {
+  const std::vector<uint8_t> out = pack_words(e, rows, nf);
+  if (!out.empty()) HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
+  e->fmt = nf;
+  return KWK_OK;
+}
+
+// the format without the dictionary (2-byte words when the program fits 16 bits)
+static StateFmt base_fmt(const StateFmt& f) {
+  StateFmt b = f;
+  b.byte = 0;
+  b.id2w = nullptr;
+  b.w2id = nullptr;
+  return b;
+}
+
+static bool byte_allowed(const kwk_engine* e) {
+  return e->fmt.half && e->byte_ok && e->allow_byte && e->byte_tune && e->use_fsm && e->fsm_kernel != 0 &&
+         e->fsm_harness >= 0;
+}
+
+// the 1-byte format when the program allows it and the dictionary closes over `rows`, else the
+// base format; sets e->fmt (and uploads the dictionary) without writing the state column
+static kwk_status pick_format(kwk_engine* e, const std::vector<uint2>& rows, StateFmt& nf) {
+  nf = base_fmt(e->fmt);
+  if (!(nf.half && byte_allowed(e))) return KWK_OK;
+  const StateFmt saved = e->fmt;
+  e->fmt = nf;  // word_class reads the half layout
+  dict_reset(e);
+  std::vector<uint32_t> seeds;
+  seeds.reserve(rows.size() + 1);
+  std::vector<uint8_t> seen(65536, 0);
+  for (const uint2& r : rows) {
+    const uint32_t w = fmt_pack(r.x, r.y, nf) & 0xFFFFu;
+    if (!seen[w]) { seen[w] = 1; seeds.push_back(w); }
+  }
+  bool changed = false;
+  const bool ok = dict_extend(e, seeds, changed);
+  e->fmt = saved;
+  if (!ok) return KWK_OK;
+  if (kwk_status st = dict_upload(e)) return st;
+  nf.byte = 1;
+  nf.id2w = e->d_id2w;
+  nf.w2id = e->d_w2id;
+  return KWK_OK;
+}
+
+// re-decides the format for the resident objects (after a table / harness / tuning change)
+static kwk_status refresh_format(kwk_engine* e) {
+  std::vector<uint2> rows;
+  if (kwk_status st = read_rows(e, rows)) return st;
+  StateFmt nf;
+  if (kwk_status st = pick_format(e, rows, nf)) return st;
+  return write_rows(e, rows, nf);
+}
+
+// rows about to be written by an upsert / replace / retry: in the 1-byte format their words join
+// the dictionary, or the engine returns to the 2-byte words
+static kwk_status admit_rows(kwk_engine* e, const std::vector<uint2>& incoming) {
+  if (!e->fmt.byte) return KWK_OK;
+  std::vector<uint32_t> seeds;
+  for (const uint2& r : incoming) seeds.push_back(fmt_pack(r.x, r.y, e->fmt) & 0xFFFFu);
+  bool changed = false;
+  if (dict_extend(e, seeds, changed)) return changed ? dict_upload(e) : KWK_OK;
+  std::vector<uint2> rows;
+  if (kwk_status st = read_rows(e, rows)) return st;
+  return write_rows(e, rows, base_fmt(e->fmt));
+}
+
+// leaves the 1-byte format (a call the table-only sweep does not cover, e.g. kwk_match)
+static kwk_status leave_byte(kwk_engine* e) {
+  if (!e->fmt.byte) return KWK_OK;
+  std::vector<uint2> rows;
+  if (kwk_status st = read_rows(e, rows)) return st;
+  return write_rows(e, rows, base_fmt(e->fmt));
+}
+
 extern "C" {
 
 const char* kwk_last_error(const kwk_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
@@ -3122,6 +3690,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->n_blocks_cap = (d->capacity + kBlock * kMinObjPerThread - 1) / (kBlock * kMinObjPerThread);
   e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
   e->allow_half = (d->flags & KWK_ENGINE_STATE32) == 0;
+  e->allow_byte = (d->flags & (KWK_ENGINE_STATE32 | KWK_ENGINE_STATE16 | KWK_ENGINE_WIDE_STATE)) == 0;
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
   if (hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || e->n_cus <= 0)
@@ -3154,6 +3723,10 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
+  ALLOC(e->d_id2w, sizeof(uint16_t) * 256);
+  ALLOC(e->d_w2id, 65536);
+  ALLOC(e->d_fsm8, sizeof(uint32_t) * 512);
+  ALLOC(e->d_fsm8_due, sizeof(int64_t) * 512);
   hipError_t er = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, "hipStreamCreate"); }
   hipMemsetAsync(e->d_st, 0, sizeof(uint2) * st_slots, e->stream);
@@ -3193,7 +3766,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
                   e->d_mbase, e->d_cptr, e->d_mops, e->d_pod_created, e->d_node_created, e->d_node_started, e->d_mout,
                   e->d_lease_nops, e->d_lease_stats, e->d_ukey8, e->d_kv, e->d_hops, e->d_hbuckets, e->d_hkeys,
-                  e->d_hbounds, e->d_hout};
+                  e->d_hbounds, e->d_hout, e->d_id2w, e->d_w2id, e->d_fsm8, e->d_fsm8_due};
   for (void* p : ptrs) if (p) hipFree(p);
   if (e->d_tick_ptr) hipFree(e->d_tick_ptr);
   if (e->ev_lease) hipEventDestroy(e->ev_lease);
@@ -3227,11 +3800,11 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
       const uint32_t n = e->n_active;
       std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
       HIP_TRY(hipMemcpy(raw.data(), e->d_st, raw.size(), hipMemcpyDeviceToHost));
-      std::vector<uint2> v = unpack_words(raw, e->fmt, n);
+      std::vector<uint2> v = unpack_words(e, raw, e->fmt, n);
       for (uint32_t i = 0; i < n; ++i)
         if (!fits_fmt(nf, t->n_stages, v[i].x, v[i].y) || (v[i].y >> KWK_CLASS_SHIFT) >= (t->n_classes ? t->n_classes : 1))
           return fail(KWK_EINVAL, "resident object " + std::to_string(i) + " does not fit the new stage table");
-      std::vector<uint8_t> out = pack_words(v, nf);
+      std::vector<uint8_t> out = pack_words(e, v, nf);
       HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
     }
     e->fmt = nf;
@@ -3288,7 +3861,8 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   e->n_stages = t->n_stages;
   e->n_classes = t->n_classes;
   e->loaded_table = true;
-  return build_fsm(e);
+  if (kwk_status st = build_fsm(e)) return st;
+  return refresh_format(e);
 }
 
 kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
@@ -3300,7 +3874,12 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FSM: 0 or 1");
       e->use_fsm = value != 0;
       HIP_TRY(hipStreamSynchronize(e->stream));
-      return build_fsm(e);
+      if (kwk_status st = build_fsm(e)) return st;
+      return refresh_format(e);
+    case KWK_TUNE_BYTE_STATE:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_BYTE_STATE: 0 or 1");
+      e->byte_tune = value != 0;
+      return refresh_format(e);
     case KWK_TUNE_Q16:
       if (value != 1 && value != 2 && value != 4) return fail(KWK_EINVAL, "KWK_TUNE_Q16: 1, 2 or 4");
       e->q16 = value;
@@ -3312,7 +3891,7 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_FSM_KERNEL:
       if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
       e->fsm_kernel = value;
-      return KWK_OK;
+      return refresh_format(e);
     case KWK_TUNE_SWEEP_BLOCKS:
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_SWEEP_BLOCKS: 0..8");
       e->sweep_blocks = value;
@@ -3339,9 +3918,15 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
 kwk_status kwk_set_harness(kwk_engine* e, const kwk_harness* h) {
   ErrScope es_(e);
   if (!e || !h) return fail(KWK_EINVAL, "null argument");
-  e->harness = *h;
   if (kwk_status st = set_dev(e)) return st;
-  return build_fsm(e);
+  // the 1-byte ids encode what the harness makes "work": re-read the rows before it changes
+  std::vector<uint2> rows;
+  if (kwk_status st = read_rows(e, rows)) return st;
+  e->harness = *h;
+  if (kwk_status st = build_fsm(e)) return st;
+  StateFmt nf;
+  if (kwk_status st = pick_format(e, rows, nf)) return st;
+  return write_rows(e, rows, nf);
 }
 
 kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t* del, const uint32_t* rec,
@@ -3367,7 +3952,11 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
         return fail(KWK_EINVAL, "object " + std::to_string(i) + ": pred bits / stage beyond the loaded stage table");
       due[i] = hot[i].due;
     }
-    const std::vector<uint8_t> raw = pack_words(st, e->fmt);
+    // the loaded objects replace the resident ones: the format follows their words
+    StateFmt nf;
+    if (kwk_status s2 = pick_format(e, st, nf)) return s2;
+    e->fmt = nf;
+    const std::vector<uint8_t> raw = pack_words(e, st, e->fmt);
     HIP_TRY(hipMemcpy(e->d_st, raw.data(), raw.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
   }
@@ -3422,6 +4011,13 @@ static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots,
     max_slot = slots[j] > max_slot ? slots[j] : max_slot;
   }
   if (kwk_status st = set_dev(e)) return st;
+  {  // the words the scatter writes (1-byte format: they join the dictionary first)
+    std::vector<uint2> rows(n);
+    for (uint32_t j = 0; j < n; ++j)
+      rows[j] = make_uint2(hot[j].pred, (hot[j].sched & ~KWK_CLASS_MASK) | ((uint32_t)cls[j] << KWK_CLASS_SHIFT) |
+                                            (mark_dirty ? KWK_F_DIRTY : 0u));
+    if (kwk_status st = admit_rows(e, rows)) return st;
+  }
   const size_t bytes = (size_t)n * (4 + sizeof(kwk_hot) + 8 + 4 + 2) + 64;
   if (kwk_status st = ensure_stage_buf(e, bytes)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -3480,6 +4076,13 @@ kwk_status kwk_retry(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step
     if (!fits_fmt(e->fmt, e->n_stages, hot[j].pred, stages[j])) return fail(KWK_EINVAL, "pred bits beyond the stage table");
   }
   if (kwk_status st = set_dev(e)) return st;
+  {  // the rows the retry writes (retry_kernel)
+    std::vector<uint2> rows(n);
+    for (uint32_t j = 0; j < n; ++j)
+      rows[j] = make_uint2(hot[j].pred, (hot[j].sched & ~(KWK_CLASS_MASK | 0xFFu | KWK_F_DIRTY)) |
+                                            ((uint32_t)cls[j] << KWK_CLASS_SHIFT) | (uint32_t)stages[j]);
+    if (kwk_status st = admit_rows(e, rows)) return st;
+  }
   const size_t bytes = (size_t)n * (4 + sizeof(kwk_hot) + 2 + 2 + 4) + 64;
   if (kwk_status st = ensure_stage_buf(e, bytes)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -3560,6 +4163,7 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
 // (re)build the 2-byte format's transition table for the loaded stage table and harness
 static kwk_status build_fsm(kwk_engine* e) {
   e->fsm_harness = -1;
+  e->byte_ok = false;
   if (!e->fmt.half || !e->loaded_table || !e->use_fsm) return KWK_OK;
   const uint32_t bits = e->fmt.fshift + 5;
   if (bits > 16) return KWK_OK;
@@ -3584,6 +4188,12 @@ static kwk_status build_fsm(kwk_engine* e) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->fsm_harness = a.harness.enable ? 1 : 0;
+  // host copy: the 1-byte format's closure and id table are derived from it
+  e->h_fsm.resize(n);
+  e->h_fsm_due.resize(n);
+  HIP_TRY(hipMemcpy(e->h_fsm.data(), e->d_fsm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(e->h_fsm_due.data(), e->d_fsm_due, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  e->byte_ok = true;
   return KWK_OK;
 }
 
@@ -3604,6 +4214,36 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     a.fsm_bits = e->fsm_bits;
   }
 
+  if (e->fmt.byte) {  // 1-byte ids: the table-only id sweep (fire only: kwk_match leaves the format)
+    if (!fire) return fail(KWK_ESTATE, "the 1-byte format sweeps with fire only");
+    a.fsm = e->d_fsm8;
+    a.fsm_due = e->d_fsm8_due;
+    constexpr uint32_t tile = kBlock * 16 * kQ8;
+    const uint32_t tiles = (e->n_active + tile - 1) / tile;
+    const void* pk = e->fsm_kernel == 2 ? (const void*)sweep8_kernel<true, 2> : (const void*)sweep8_kernel<true, 1>;
+    uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
+    if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);
+    uint32_t blocks = tiles;
+    e->last_sweep = kwk_sweep_info{KWK_SWEEP_8, (uint32_t)kQ8, 0, 1, tiles, tiles, a.harness.enable ? 1u : 0u, 0};
+    if (2 * pg > tiles) {  // the persistent loop would run about once: one block per tile
+      hipLaunchKernelGGL((sweep8_kernel<false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    } else {
+      blocks = pg;
+      e->last_sweep.persistent = 1;
+      e->last_sweep.grid = pg;
+      e->last_sweep.depth = e->fsm_kernel;
+      if (e->fsm_kernel == 2) hipLaunchKernelGGL((sweep8_kernel<true, 2>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+      else hipLaunchKernelGGL((sweep8_kernel<true, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    }
+    HIP_TRY(hipGetLastError());
+    e->last_objs = 16 * kQ8;
+    e->last_region_shift = 0;
+    e->last_blocks = tiles;
+    e->last_grid = blocks;
+    e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
+    ++e->steps;
+    return KWK_OK;
+  }
   if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
     // small engines (a node kind, the cache-resident configs) take 2048-word tiles so that
     // the grid still spreads over every CU
@@ -3688,6 +4328,9 @@ kwk_status kwk_step(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step)
 
 kwk_status kwk_match(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step) {
   ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  if (kwk_status st = leave_byte(e)) return st;  // match-only runs the general word sweep
   return launch_sweep(e, now_ns, seed, step, false);
 }
 
@@ -3830,7 +4473,7 @@ kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int
     std::vector<int64_t> due(n);
     HIP_TRY(hipMemcpy(raw.data(), (const char*)e->d_st + word_bytes(e->fmt) * first, raw.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(due.data(), e->d_due + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
-    const std::vector<uint2> st = unpack_words(raw, e->fmt, n);
+    const std::vector<uint2> st = unpack_words(e, raw, e->fmt, n);
     for (uint32_t i = 0; i < n; ++i) hot[i] = kwk_hot{st[i].x, st[i].y, due[i]};
   }
   if (del) HIP_TRY(hipMemcpy(del, e->d_del + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
@@ -4060,7 +4703,7 @@ kwk_status kwk_usage_read_containers(kwk_engine* e, uint32_t first, uint32_t n, 
   HIP_TRY(hipStreamSynchronize(e->stream));
   std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
   HIP_TRY(hipMemcpy(raw.data(), (const char*)e->d_st + word_bytes(e->fmt) * first, raw.size(), hipMemcpyDeviceToHost));
-  const std::vector<uint2> st = unpack_words(raw, e->fmt, n);
+  const std::vector<uint2> st = unpack_words(e, raw, e->fmt, n);
   std::vector<double> unit(2 * (size_t)n);
   HIP_TRY(hipMemcpy(unit.data(), e->d_pod_cum + 2 * (size_t)first, 16 * (size_t)n, hipMemcpyDeviceToHost));
   std::vector<double> cc;
@@ -4364,35 +5007,29 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
                e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last, e->d_mixed,
                e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n, e->d_ukey8, e->d_kv, e->kv_n};
   const uint32_t wb = word_bytes(e->fmt);
+  // the kernels are specialised on the state word's bytes (1: dictionary ids, 2, 4, 8)
+#define USAGE_KERNEL(K, ...) (wb == 1 ? (const void*)K<1 __VA_ARGS__> : wb == 2 ? (const void*)K<2 __VA_ARGS__>   \
+                              : wb == 4 ? (const void*)K<4 __VA_ARGS__> : (const void*)K<8 __VA_ARGS__>)
   if (!e->has_mixed_keys && !e->d_pod_out && e->podv_n) {  // usage_fast_kernel
     const bool k8 = e->d_ukey8 != nullptr && e->usage_key8;
-    const void* fk = k8 ? (wb == 2 ? (const void*)usage_fast_kernel<2, true> : wb == 4 ? (const void*)usage_fast_kernel<4, true>
-                                                                                    : (const void*)usage_fast_kernel<8, true>)
-                        : (wb == 2 ? (const void*)usage_fast_kernel<2> : wb == 4 ? (const void*)usage_fast_kernel<4>
-                                                                                 : (const void*)usage_fast_kernel<8>);
+    const void* fk = k8 ? USAGE_KERNEL(usage_fast_kernel, , true) : USAGE_KERNEL(usage_fast_kernel);
     uint32_t grid = persist_grid(e, fk, ublocks);
     if (e->usage_blocks) grid = std::min(ublocks, (uint32_t)e->n_cus * e->usage_blocks);
     if (grid) {
-      if (k8 && wb == 2) hipLaunchKernelGGL((usage_fast_kernel<2, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      else if (k8 && wb == 4) hipLaunchKernelGGL((usage_fast_kernel<4, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      else if (k8) hipLaunchKernelGGL((usage_fast_kernel<8, true>), dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      else if (wb == 2) hipLaunchKernelGGL(usage_fast_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      else if (wb == 4) hipLaunchKernelGGL(usage_fast_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      else hipLaunchKernelGGL(usage_fast_kernel<8>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-      HIP_TRY(hipGetLastError());
+      void* args[] = {&ua};
+      HIP_TRY(hipLaunchKernel(fk, dim3(grid), dim3(kBlock), args, 0, e->stream));
     }
     hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
   // persistent grid (every block slot the occupancy allows), at most one chunk per wave
-  const void* kern = wb == 2 ? (const void*)usage_kernel<2> : wb == 4 ? (const void*)usage_kernel<4> : (const void*)usage_kernel<8>;
+  const void* kern = USAGE_KERNEL(usage_kernel);
+#undef USAGE_KERNEL
   const uint32_t grid = persist_grid(e, kern, ublocks);
   if (grid) {
-    if (wb == 2) hipLaunchKernelGGL(usage_kernel<2>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-    else if (wb == 4) hipLaunchKernelGGL(usage_kernel<4>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-    else hipLaunchKernelGGL(usage_kernel<8>, dim3(grid), dim3(kBlock), 0, e->stream, ua);
-    HIP_TRY(hipGetLastError());
+    void* args[] = {&ua};
+    HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(kBlock), args, 0, e->stream));
   }
   hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
   HIP_TRY(hipGetLastError());
@@ -4471,7 +5108,8 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
     const uint32_t pmask = wb == 8 ? 0xFFFFFFFFu : e->fmt.pmask;
     const dim3 g((uint32_t)blocks);
     if (kwk_status st = ensure_count_part(e)) return st;
-    if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
+    if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, d_masks, e->d_count_part, d_out);
+    else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
     else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
     else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
     HIP_TRY(hipGetLastError());
@@ -4511,7 +5149,8 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
       const dim3 g((uint32_t)blocks);
       if (kwk_status st = ensure_count_part(e)) return st;
       uint32_t* pp = e->d_count_part;
-      if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
+      if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, e->d_agg_masks, pp, e->d_agg_counts);
+      else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
       else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
       else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
       HIP_TRY(hipGetLastError());

@@ -17,7 +17,11 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 CLUSTER_SEED = 0x6B776F6B
-STAGE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "stages")
+# the default Stage CRs kwok ships (kustomize/stage/**, byte-identical copies; the reference embeds
+# them, kustomize/stage/*/embed.go)
+STAGE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stages")
+# the default usage / Metric CRs (kustomize/metrics/**)
+METRICS_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "metrics")
 
 POD_FAST = ["pod/fast/pod-ready.yaml", "pod/fast/pod-complete.yaml", "pod/fast/pod-delete.yaml"]
 POD_GENERAL = ["pod/general/pod-create.yaml", "pod/general/pod-init-container-running.yaml",

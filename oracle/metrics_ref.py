@@ -1,7 +1,7 @@
 """ORACLE / TEST INFRASTRUCTURE — not product code.
 
 The values of kwok's shipped Metric CR (kustomize/metrics/resource/metrics-resource.yaml,
-copied as tests/golden/metrics/metrics-resource.yaml) restated per metric name for one node
+shipped as kwok_amd/metrics/metrics-resource.yaml) restated per metric name for one node
 scrape (pkg/kwok/metrics/metrics.go:168-354: node series, one per pod of the node, one per
 container of those pods), with the usage callbacks of pkg/kwok/server/metrics_resource_usage.go
 answered by oracle/usage_ref.py.  The CEL is not interpreted here: each value below is the

@@ -12,7 +12,7 @@ from kwok_amd import workload as W
 from kwok_amd.host.cluster import Aggregates, DeviceReport, engine_aggregates, local_node_ptr, node_block, phase_masks, pod_range
 from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
 
-GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "metrics", "usage-from-annotation.yaml")
+GOLDEN = os.path.join(os.path.dirname(os.path.dirname(__file__)), "kwok_amd", "metrics", "usage-from-annotation.yaml")
 REL_TOL = 1e-6
 
 

@@ -13,29 +13,30 @@ from tests.parity_util import run
 pytestmark = pytest.mark.gpu
 
 
-FORMATS = ["auto", "u32", "wide"]
+FORMATS = ["auto", "u16", "u32", "wide"]
 
 
-@pytest.mark.parametrize("state", FORMATS + ["auto-nofsm", "auto-gen", "auto-pair"])
+@pytest.mark.parametrize("state", FORMATS + ["auto-nofsm", "auto-gen", "auto-pair", "u16-pair"])
 def test_pod_fast_c1_mini(state):
     """C1 shape (pod-fast, 10% Job-owned, harness churn) at 40 nodes x 10 pods, in every
-    device state format (auto = the 2-byte words of the whole-line sweep: the table-only
-    kernel by default, the general sweep16_kernel with its transition table (auto-gen) and
-    without it (auto-nofsm)); auto-pair hands the fired list back through the scan + expansion
-    pair of large sweeps (KWK_TUNE_COMPACT_SMALL 0) instead of the one-launch compaction."""
-    tuning = {}
+    device state format: auto = the 1-byte dictionary ids of sweep8_kernel (pod-fast is
+    table-only), u16 = the 2-byte words (the table-only sweep16_fsm_kernel), the general
+    sweep16_kernel with its transition table (auto-gen: leaves the 1-byte format) and without it
+    (auto-nofsm); *-pair hand the fired list back through the scan + expansion pair of large
+    sweeps (KWK_TUNE_COMPACT_SMALL 0) instead of the one-launch compaction."""
+    tuning, kernel = {}, {"auto": abi.SWEEP_8, "u16": abi.SWEEP_16_FSM, "u32": abi.SWEEP_W4, "wide": abi.SWEEP_W8}.get(state)
     if state == "auto-nofsm":
-        tuning = {abi.TUNE_FSM: 0}
-        state = "auto"
+        tuning, kernel, state = {abi.TUNE_FSM: 0}, abi.SWEEP_16, "auto"
     elif state == "auto-gen":
-        tuning = {abi.TUNE_FSM_KERNEL: 0}
-        state = "auto"
+        tuning, kernel, state = {abi.TUNE_FSM_KERNEL: 0}, abi.SWEEP_16, "auto"
     elif state == "auto-pair":
-        tuning = {abi.TUNE_COMPACT_SMALL: 0}
-        state = "auto"
+        tuning, kernel, state = {abi.TUNE_COMPACT_SMALL: 0}, abi.SWEEP_8, "auto"
+    elif state == "u16-pair":
+        tuning, kernel, state = {abi.TUNE_COMPACT_SMALL: 0}, abi.SWEEP_16_FSM, "u16"
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state, tuning=tuning)
+    total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state, tuning=tuning,
+                     expect_kernel=kernel)
     assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
 
 
@@ -51,7 +52,7 @@ def test_pod_general_c2_mini(wide):
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
 
-@pytest.mark.parametrize("state", ["auto", "auto-nofsm", "u32"])
+@pytest.mark.parametrize("state", ["auto", "u16", "auto-nofsm", "u32"])
 def test_node_fast_heartbeat(state):
     tuning = {}
     if state == "auto-nofsm":
@@ -136,7 +137,7 @@ def test_shard_invariance_two_engines():
             e.close()
 
 
-@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+@pytest.mark.parametrize("state", ["auto", "u16", "u32", "wide"])
 def test_count_phase_histogram(state):
     """kwk_count and kwk_aggregate (cluster aggregates for the RCCL all-reduce) against the
     oracle's phases, in the 2-, 4- and 8-byte state formats; a ragged object count so the last
@@ -167,7 +168,7 @@ def test_count_phase_histogram(state):
 
 def test_state_format_repack_on_table_reload():
     """kwk_load_stages with objects resident and a table that needs the other state format
-    (pred_bits = 0 -> 32 bits -> wide, then back to the 2-byte packed words) repacks them in place; the run
+    (pred_bits = 0 -> 32 bits -> wide, then back to 16 bits: the 1-byte dictionary ids) repacks them in place; the run
     stays bit-exact with the oracle."""
     import ctypes as C
     from kwok_amd.host import abi
@@ -182,7 +183,7 @@ def test_state_format_repack_on_table_reload():
                     t.pred_bits = 0
                 deltas = np.ascontiguousarray(prog.delta_array())
                 abi.check(abi.lib().kwk_load_stages(eng.h, C.byref(t), abi.ptr(deltas)), "kwk_load_stages", eng.h)
-                assert eng.stats()["state_bytes"] == (8 if k == 3 else 2)
+                assert eng.stats()["state_bytes"] == (8 if k == 3 else 1)  # back to 16 bits: the 1-byte ids
             now = NOW0 + k * 10**9
             eng.step(now, 9, k)
             got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
@@ -222,5 +223,90 @@ def test_device_list_empty_after_sweeping_nothing():
         eng.fired_compact()
         assert device_count() == 0
         assert len(eng.fired()) == 0
+    finally:
+        eng.close()
+
+
+def test_byte_format_dictionary_lifecycle():
+    """The 1-byte dictionary format through the calls that bring new words: upserts
+    of objects in other states join the dictionary (still 1 byte, bit-exact with the oracle); a
+    harness change re-assigns the ids; an upsert whose words overflow an id class returns the
+    engine to the 2-byte words in place; kwk_match leaves the 1-byte format.  Every step is checked
+    against the oracle."""
+    from kwok_amd.host import abi
+    from tests.parity_util import NOW0, build, compare_state
+    files = W.stage_paths(W.POD_FAST)
+    objs = [W.pod_object(f"p{i}", "node-0", job=(i % 3 == 0)) for i in range(300)]
+    prog, eng, sim = build(files, objs, harness=True)
+    try:
+        assert eng.stats()["state_bytes"] == 1
+        seed = 0x51
+        from kwok_amd.host.engine import Ingest
+
+        def step(k):
+            eng.step(NOW0 + k * 10**9, seed, k)
+            got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
+            assert got == sorted(sim.step(NOW0 + k * 10**9, seed, k)), k
+            compare_state(prog, eng, sim, k)
+
+        def upsert(slots, new_objs):
+            import copy
+            ing = Ingest(prog)
+            hot, dels, rec, cls = ing.columns(new_objs)
+            eng.upsert(np.array(slots), hot, dels, rec, cls)
+            from oracle.next_ref import omitempty
+            for s, o in zip(slots, new_objs):
+                sim.objs[s] = omitempty(copy.deepcopy(o))
+                sim.orig[s] = copy.deepcopy(sim.objs[s])
+                sim.dirty[s] = True
+                sim.pending[s] = None
+        for k in range(3):
+            step(k)
+        # Running pods with a podIP and a finalizer: words outside the first closure
+        run = []
+        for i in range(10):
+            o = W.pod_object(f"q{i}", "node-0")
+            o["metadata"]["finalizers"] = ["kwok.x-k8s.io/fake"]
+            o["status"] = {"phase": "Running", "podIP": "10.0.0.9"}
+            run.append(o)
+        upsert(list(range(10)), run)
+        assert eng.stats()["state_bytes"] == 1
+        for k in range(3, 6):
+            step(k)
+        eng.set_harness(False)  # the ids encode the harness's "needs work": re-assigned in place
+        sim.harness = False
+        assert eng.stats()["state_bytes"] == 1
+        step(6)
+        eng.set_harness(True)
+        sim.harness = True
+        step(7)
+        # every combination of the program's feature bits at once: more words than an id class holds
+        n_bits = prog.table().pred_bits
+        many = []
+        for i in range(2 ** min(n_bits, 7)):
+            o = W.pod_object(f"m{i}", "node-0", job=bool(i & 1))
+            if i & 2:
+                o["metadata"]["deletionTimestamp"] = "2023-11-14T22:13:20Z"
+            st = {}
+            if i & 4:
+                st["podIP"] = "10.0.0.7"
+            st["phase"] = ["Pending", "Running", "Succeeded", "Failed"][(i >> 3) & 3]
+            if st["phase"] == "Running":  # pod-complete's template indexes the container statuses
+                st["containerStatuses"] = [{"name": "container-0", "image": "busybox", "ready": True, "restartCount": 0,
+                                            "state": {"running": {"startedAt": "2023-11-14T22:13:20Z"}}}]
+            o["status"] = st
+            if i & 32:
+                o["metadata"]["finalizers"] = ["kwok.x-k8s.io/fake"]
+            many.append(o)
+        hot, _, _, _ = Ingest(prog).columns(many)
+        upsert(list(range(20, 20 + len(many))), many)
+        if len(set(hot["pred"].tolist())) > 31:
+            assert eng.stats()["state_bytes"] == 2, "an overflowing id class must return to the 2-byte words"
+        for k in range(8, 11):
+            step(k)
+        eng.set_tuning(abi.TUNE_BYTE_STATE, 1)  # back to the ids if they fit (they may not)
+        step(11)
+        eng.match(NOW0 + 12 * 10**9, seed, 12)  # match-only: the general sweep on 2-byte words
+        assert eng.stats()["state_bytes"] == 2
     finally:
         eng.close()

@@ -21,8 +21,8 @@ from kwok_amd.host.usage import UsageProgram, load_usage_yaml, usage_columns
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VEC = json.load(open(os.path.join(HERE, "golden", "cel_vectors.json")))
-USAGE = os.path.join(HERE, "golden", "metrics", "usage-from-annotation.yaml")
-METRICS = os.path.join(HERE, "golden", "metrics", "metrics-resource.yaml")
+USAGE = os.path.join(os.path.dirname(HERE), "kwok_amd", "metrics", "usage-from-annotation.yaml")
+METRICS = os.path.join(os.path.dirname(HERE), "kwok_amd", "metrics", "metrics-resource.yaml")
 REL = 1e-6
 
 

@@ -31,7 +31,7 @@ def test_bench_pod_variants_are_shard_invariant():
     assert 0.08 < full.mean() < 0.12
 
 
-GOLDEN_USAGE = os.path.join(ROOT, "tests", "golden", "metrics", "usage-from-annotation.yaml")
+GOLDEN_USAGE = os.path.join(ROOT, "kwok_amd", "metrics", "usage-from-annotation.yaml")
 
 
 def _shard_aggregates(pods, slot_base, steps, files):

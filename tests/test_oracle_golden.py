@@ -105,6 +105,7 @@ def test_go_parse_rfc3339(s, want):
 
 # ----------------------------------------------------------------- stage golden fixtures
 STAGE_DIR = os.path.join(os.path.dirname(__file__), "golden", "stages")
+SHIPPED_STAGES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kwok_amd", "stages")
 
 
 def _stage_cases():
@@ -121,7 +122,10 @@ def load_stage_case(path):
     stage_files = [l.split(":", 1)[1].strip() for l in text.splitlines() if l.startswith("# @Stage:")]
     stages = []
     for sf in stage_files:
-        for doc in yaml.safe_load_all(open(os.path.normpath(os.path.join(os.path.dirname(path), sf)))):
+        # the fixture names its stage relative to the reference's kustomize/stage tree, which the
+        # product ships as kwok_amd/stages (the fixtures stay here, under tests/golden/stages)
+        rel = os.path.relpath(os.path.normpath(os.path.join(os.path.dirname(path), sf)), STAGE_DIR)
+        for doc in yaml.safe_load_all(open(os.path.join(SHIPPED_STAGES, rel))):
             if doc:
                 stages.append(doc)
     obj = yaml.safe_load(text)

@@ -27,7 +27,8 @@ from kwok_amd.host.stages import load_stage_files, stage_from_v1alpha1
 HERE = os.path.dirname(os.path.abspath(__file__))
 STAGE_DIR = os.path.join(HERE, "golden", "stages")
 NOW = 1_700_000_000_123_456_789
-FILES = sorted(f for f in glob.glob(os.path.join(STAGE_DIR, "**", "*.yaml"), recursive=True) if "testdata" not in f)
+SHIPPED = os.path.join(os.path.dirname(HERE), "kwok_amd", "stages")
+FILES = sorted(glob.glob(os.path.join(SHIPPED, "**", "*.yaml"), recursive=True))
 
 
 def _ip(prefix, *args):
@@ -217,7 +218,7 @@ def test_native_equals_host_renderer_edge_values():
 
 
 def test_rfc3339nano_and_no_fraction():
-    stages = load_stage_files(os.path.join(STAGE_DIR, "node", "heartbeat", "node-heartbeat.yaml"))
+    stages = load_stage_files(os.path.join(SHIPPED, "node", "heartbeat", "node-heartbeat.yaml"))
     pp = _program(stages)
     node = W.node_object("n0")
     for ns in (0, 1_700_000_000 * 10**9, 1_700_000_000 * 10**9 + 120_000_000, 951_782_400 * 10**9 + 1):

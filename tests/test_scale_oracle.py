@@ -46,21 +46,34 @@ def _sampled_run(prog, eng, stage_files, variants, index, slots, steps, dt_ns, k
         assert got == exp, f"step {k}: device-only {sorted(set(got) - set(exp))[:6]} oracle-only " \
                            f"{sorted(set(exp) - set(got))[:6]}"
         total += len(exp)
-        hot, dels = eng.read()
-        compare_state(prog, eng, sim, k, rows=(hot[sample], dels[sample]))
+        compare_state(prog, eng, sim, k, rows=_rows_at(eng, slots))
     return total
 
 
-def test_c5_persistent_table_sweep_sampled_oracle():
-    """C5 pod shape (pod-fast, 100 pods per node, 10 % Job-owned, harness churn) at 20M pods:
-    the persistent, depth-2 table-only 2-byte sweep, every 4999th slot checked each step."""
+def _rows_at(eng, slots):
+    """(hot, deletion_s) of the sampled slots only (kwk_read per slot: the sample is small)."""
+    from kwok_amd.host import abi
+    hot = np.zeros(len(slots), dtype=abi.HOT_DTYPE)
+    dels = np.zeros(len(slots), dtype=np.int64)
+    for j, s in enumerate(slots):
+        h, d = eng.read(int(s), 1)
+        hot[j], dels[j] = h[0], d[0]
+    return hot, dels
+
+
+@pytest.mark.parametrize("state", ["auto", "u16"])
+def test_c5_persistent_table_sweep_sampled_oracle(state):
+    """C5 pod shape (pod-fast, 100 pods per node, 10 % Job-owned, harness churn) at the sizes
+    where the sweeps run persistent with two tiles in flight: the 1-byte dictionary-id sweep
+    (auto: sweep8_kernel, the bench's kernel; 8192-id tiles, 40M pods) and the 2-byte table-only
+    sweep (u16: sweep16_fsm_kernel, 20M pods), every ~10000th / 4999th slot checked each step."""
     from bench import shard_pod_variants
     from kwok_amd import workload as W
     from kwok_amd.host import abi
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
-    n = 20_000_000
+    n = 40_000_000 if state == "auto" else 20_000_000
     files = W.stage_paths(W.POD_FAST)
     pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
     prog = KindProgram(load_stage_files(*files), HarnessSpec())
@@ -68,17 +81,18 @@ def test_c5_persistent_table_sweep_sampled_oracle():
     ing = Ingest(prog)
     idx = shard_pod_variants(0, n, SEED, 0.1)
     hot, dels, rec, cls = ing.variant_columns(pvars, idx)
-    eng = Engine(prog, capacity=n)
+    eng = Engine(prog, capacity=n, state=state)
     try:
         eng.load_stages()
         eng.set_harness(True)
         eng.load(hot, dels, rec, cls, ing.record_array())
         del hot, dels, rec, cls
-        slots = list(range(3, n, 4999))
+        slots = list(range(3, n, 9973 if state == "auto" else 4999))
         assert int(np.sum(idx[slots])) > 100  # Job-owned pods (pod-complete) are in the sample
-        total = _sampled_run(prog, eng, files, pvars, idx, slots, 10, 10**9, abi.SWEEP_16_FSM, 1)
+        kernel = abi.SWEEP_8 if state == "auto" else abi.SWEEP_16_FSM
+        total = _sampled_run(prog, eng, files, pvars, idx, slots, 10, 10**9, kernel, 1)
         assert total > len(slots)  # every pod became ready once, Job pods completed, deletions re-created
-        assert eng.stats()["state_bytes"] == 2
+        assert eng.stats()["state_bytes"] == (1 if state == "auto" else 2)
     finally:
         eng.close()
 

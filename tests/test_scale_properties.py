@@ -40,10 +40,10 @@ def _fired_key(f):
 
 
 def test_three_sweeps_agree_at_4m_pods():
-    engines = {s: _pods(s) for s in ("auto", "u32", "wide")}
+    engines = {s: _pods(s) for s in ("auto", "u16", "u32", "wide")}
     try:
         sb = {s: e.stats()["state_bytes"] for s, (_, e) in engines.items()}
-        assert sb == {"auto": 2, "u32": 4, "wide": 8}, sb
+        assert sb == {"auto": 1, "u16": 2, "u32": 4, "wide": 8}, sb
         now0 = 1_700_000_000 * 10**9
         for k in range(STEPS):
             keys = {}
@@ -52,16 +52,17 @@ def test_three_sweeps_agree_at_4m_pods():
                 f = e.fired()
                 assert len(np.unique(f["slot"])) == len(f), f"{s} step {k}: a slot fired twice"
                 keys[s] = _fired_key(f)
-            assert np.array_equal(keys["auto"], keys["u32"]) and np.array_equal(keys["auto"], keys["wide"]), f"step {k}"
+            for s in ("u16", "u32", "wide"):
+                assert np.array_equal(keys["auto"], keys[s]), f"step {k}: {s}"
             assert len(keys["auto"]) > 0
         states = {s: e.read() for s, (_, e) in engines.items()}
-        for s in ("u32", "wide"):
+        for s in ("u16", "u32", "wide"):
             for col in ("pred", "sched"):
                 assert np.array_equal(states["auto"][0][col], states[s][0][col]), (s, col)
             pend = (states["auto"][0]["sched"] & 0xFF) != 0xFF
             assert np.array_equal(states["auto"][0]["due"][pend], states[s][0]["due"][pend]), s
         st = {s: e.stats() for s, (_, e) in engines.items()}
-        for s in ("u32", "wide"):
+        for s in ("u16", "u32", "wide"):
             assert st[s]["fired"] == st["auto"]["fired"] and st[s]["fired_per_stage"] == st["auto"]["fired_per_stage"]
         assert sum(st["auto"]["fired_per_stage"].values()) == st["auto"]["fired"]
     finally:
@@ -79,11 +80,15 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
     shapes = {"4": {abi.TUNE_Q16: 4}, "4-d1": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 1},
               "4-gen": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 0}, "2": {abi.TUNE_Q16: 2},
               "1": {abi.TUNE_Q16: 1}, "1-gen": {abi.TUNE_Q16: 1, abi.TUNE_FSM_KERNEL: 0}}
+    byte_shapes = {"id8": {}, "id8-d1": {abi.TUNE_FSM_KERNEL: 1}}  # the 1-byte id sweep, 2 / 1 tiles in flight
     engines = {}
     try:
         for q, tuning in shapes.items():
+            engines[q] = _pods("u16", n_nodes=170_000, tuning=tuning)
+        for q, tuning in byte_shapes.items():
             engines[q] = _pods("auto", n_nodes=170_000, tuning=tuning)
-        assert all(e.stats()["state_bytes"] == 2 for _, e in engines.values())
+        assert all(e.stats()["state_bytes"] == (1 if q.startswith("id8") else 2) for q, (_, e) in engines.items())
+        shapes.update(byte_shapes)
         now0 = 1_700_000_000 * 10**9
         for k in range(10):
             keys = {}
@@ -103,7 +108,7 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
             for key in ("fired", "matched"):
                 assert st[q][key] == st["4"][key], (q, key)
         # byte counts include one fired-count word per (tile, wave) segment: equal per tile shape
-        for q, ref in (("4-d1", "4"), ("4-gen", "4"), ("1-gen", "1")):
+        for q, ref in (("4-d1", "4"), ("4-gen", "4"), ("1-gen", "1"), ("id8-d1", "id8")):
             for key in ("bytes", "line_bytes"):
                 assert st[q][key] == st[ref][key], (q, key)
     finally:
