@@ -376,6 +376,58 @@ def cpu_baseline_soa(sample_s: float, seed: int, n_pods: int = 20_000_000):
                       f"columns (harness churn, match, pick, delay, fire, delta), {cores} threads; CPU {_cpu_model()}"}
 
 
+def cpu_baseline_c3(sample_s: float, seed: int):
+    """The reference-faithful matcher (refcpu: JSON re-parse + Match + Delay, 1 thread) over node
+    objects with node-initialize + node-heartbeat (the C3 stage set), half of them Ready (the
+    heartbeat matches, its jitter drawn), half fresh (node-initialize)."""
+    import yaml
+    from kwok_amd import workload as W
+    from oracle import refcpu
+    lc = refcpu.Lifecycle([yaml.safe_load(open(p)) for p in W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT)])
+    objs = []
+    for i in range(20000):
+        o = W.node_object(f"node-{i}")
+        if i % 2:
+            o["status"]["phase"] = "Running"
+            o["status"]["conditions"] = [{"type": "Ready", "status": "True"}]
+        objs.append(json.dumps(o, separators=(",", ":")).encode())
+    lc.match_batch(objs[:2000], NOW0, seed, 0)
+    t0, n, reps = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < sample_s:
+        lc.match_batch(objs, NOW0, seed, reps + 1)
+        n += len(objs)
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "node transitions/sec (upper bound: matches/sec)", "cores": 1,
+            "kind": "port",
+            "sample": f"{len(objs)} node JSON objects x {reps} passes ({dt:.1f} s): JSON re-parse + Match + Delay "
+                      f"(node-initialize + node-heartbeat), 1 thread; CPU {_cpu_model()}"}
+
+
+def cpu_baseline_c4(sample_s: float, seed: int):
+    """The oracle's usage restatement (oracle/usage_ref: getResourceUsage + the
+    usage-from-annotation expression + the Quantity parse, per container, 1 thread) over a C4
+    sample: container usage evaluations per second, as a scrape would evaluate them."""
+    import yaml
+    from kwok_amd import workload as W
+    from oracle import usage_ref
+    docs = [d for d in yaml.safe_load_all(open(os.path.join(ROOT, "kwok_amd", "metrics", "usage-from-annotation.yaml")))
+            if d]
+    pods = W.make_cluster("C4", 100, 5000, seed=seed).pods.materialize()
+    t0, n, reps = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < sample_s:
+        for p in pods:
+            for c in p["spec"]["containers"]:
+                usage_ref.container_usage(docs, p, c["name"], "cpu")
+                usage_ref.container_usage(docs, p, c["name"], "memory")
+                n += 1
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "container usage evaluations/sec", "cores": 1, "kind": "port",
+            "sample": f"{len(pods)} C4 pods x {reps} passes ({dt:.1f} s): cpu + memory usage per container "
+                      f"(ResourceUsage lookup, usage-from-annotation, Quantity parse), 1 thread; CPU {_cpu_model()}"}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -429,13 +481,20 @@ def main():
         if not os.path.exists(kbuild.OUT):
             kbuild.build()
         r = configs.run(args.config, args.steps, args.warmup, args.seed)
+        roof = r.pop("roofline", None)
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = {"C1": lambda: cpu_baseline(args.cpu_sample_s / 2, args.seed),
+                   "C2": lambda: cpu_baseline_c2(args.cpu_sample_s / 2, args.seed),
+                   "C3": lambda: cpu_baseline_c3(args.cpu_sample_s / 2, args.seed),
+                   "C4": lambda: cpu_baseline_c4(args.cpu_sample_s / 2, args.seed)}[args.config]()
         line = {"metric": r.pop("metric"), "value": round(r.pop("value"), 1), "n_gpus": 1, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(r.pop("ms_per_step"), 4), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
                 "dtype": ({1: "u8", 2: "u16", 4: "u32", 8: "u32x2"}.get(r.get("state_bytes_per_object"), "u32") + "/i64"
                           if args.config != "C4" else "f64"),
                 "data": "synthetic (seeded kwokctl-shaped objects), cache-resident working set",
-                "config": {"workload": r.pop("workload")}, "detail": r}
+                "config": {"workload": r.pop("workload")}, "roofline": roof, "cpu_baseline": cpu, "detail": r}
         print(json.dumps(line), flush=True)
         return
 

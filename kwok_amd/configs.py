@@ -71,6 +71,21 @@ def _timed_n(run_n, sync_engines, timing_engine, steps, warmup):
     return wall, timing_engine.event_elapsed_ms(0, 1) / 1e3
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md
+
+
+def _roofline(bytes_per_step: float, seconds_per_step: float, what: str, working_set_mb: float) -> dict:
+    """The dominant device work of a C1-C4 step against the HBM roofline.  These working sets fit
+    the 256 MB Infinity Cache: the fraction is of the HBM peak, but the bytes are
+    cache-served, so it is a throughput figure, not an HBM claim (the HBM claim is C5 / C2 at
+    100M pods, bench.py's default line)."""
+    achieved = bytes_per_step / seconds_per_step / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": what,
+            "bytes_per_step": int(bytes_per_step), "working_set_MB": round(working_set_mb, 1),
+            "note": "cache-resident working set: Infinity-Cache served, HBM roofline not applicable"}
+
+
 def run(config: str, steps: int, warmup: int, seed: int) -> dict:
     if config in ("C1", "C2"):
         n_nodes, n_pods = (1000, 100_000) if config == "C1" else (10_000, 1_000_000)
@@ -88,7 +103,9 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         s1p, s1n = pods.stats(), nodes.stats()
         fired = (s1p["fired"] - s0p["fired"]) + (s1n["fired"] - s0n["fired"])
         pbytes = s1p["bytes"] - s0p["bytes"]
+        ws_mb = n_pods * (s1p["state_bytes"] + 8) / 1e6  # state + due columns
         out = {"metric": "stage transitions/sec", "value": fired / wall, "ms_per_step": wall / steps * 1e3,
+               "roofline": _roofline(pbytes / steps, pod_s / steps, "pod sweep (kwk_step_stats bytes)", ws_mb),
                "pod_sweep_us": pod_s / steps * 1e6, "algorithmic_GBps": pbytes / pod_s / 1e9,
                "state_bytes_per_object": s1p["state_bytes"], "transitions_per_step": fired / steps,
                "workload": f"{config}: {n_nodes} nodes / {n_pods} pods, sim dt {dt / 1e6:.0f} ms, harness churn",
@@ -129,8 +146,15 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         s1, l1 = nodes.stats(), nodes.lease_stats()
         fired = s1["fired"] - s0["fired"]
         writes = sum(l1[k] - l0[k] for k in ("creates", "renews", "acquires"))
+        syncs = writes + (l1["busy"] - l0["busy"])
+        # the tick's algorithmic bytes: the node sweep's count, every lease record read (32 B) and
+        # each synced record written back (32 B)
+        tbytes = (s1["bytes"] - s0["bytes"]) + steps * n_nodes * 32 + syncs * 32
         out = {"metric": "node transitions + lease writes /sec", "value": (fired + writes) / wall,
                "ms_per_step": wall / steps * 1e3, "device_us_per_step": dev_s / steps * 1e6,
+               "roofline": _roofline(tbytes / steps, dev_s / steps, "lease step + node sweep per tick",
+                                     n_nodes * (32 + s1["state_bytes"] + 8) / 1e6),
+               "state_bytes_per_object": s1["state_bytes"],
                "node_transitions_per_step": fired / steps, "lease_writes_per_step": writes / steps,
                "lease_counts": {k: l1[k] - l0[k] for k in ("creates", "renews", "acquires", "busy")},
                "workload": f"C3: {n_nodes} nodes, node-initialize + node-heartbeat (20 s / 25 s) + leases "
@@ -156,6 +180,8 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         ubytes = n_pods * (4 + 4) + n_nodes * (4 + 32 + 24)
         out = {"metric": "container usage evaluations/sec", "value": containers * steps / wall,
                "ms_per_step": wall / steps * 1e3, "device_us_per_step": dev_s / steps * 1e6,
+               "roofline": _roofline(ubytes, dev_s / steps, "usage evaluation (state + usage key per pod, "
+                                     "node_ptr + outputs + integrators per node)", ubytes / 1e6),
                "algorithmic_GBps": ubytes / (dev_s / steps) / 1e9, "containers": containers,
                "cluster_cpu": float(cluster[0]), "cluster_memory": float(cluster[1]),
                "workload": f"C4: {n_nodes} nodes / {n_pods} pods, 1-4 containers, 50 % annotated, "
