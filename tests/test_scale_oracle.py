@@ -23,19 +23,20 @@ NOW0 = 1_700_000_000 * 10**9
 SEED = 0x6B776F6B
 
 
-def _sampled_run(prog, eng, stage_files, variants, index, slots, steps, dt_ns, kernel, persistent):
+def _sampled_run(prog, eng, stage_files, variants, index, slots, steps, dt_ns, kernel, persistent, kind_salt=0,
+                 harness=True):
     from kwok_amd.host import abi
     from oracle.next_ref import load_stage_docs
     from oracle.sim import OracleSim
     objs = [variants[int(index[s])] for s in slots]
-    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=True, slots=slots)
+    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=harness, slots=slots, kind_salt=kind_salt)
     sample = np.asarray(slots, dtype=np.int64)
     total = 0
     for k in range(steps):
         now = NOW0 + k * dt_ns
         eng.step(now, SEED, k)
         info = eng.last_sweep()
-        assert info["kernel"] == kernel and info["persistent"] == persistent and info["harness"] == 1, info
+        assert info["kernel"] == kernel and info["persistent"] == persistent and info["harness"] == int(harness), info
         if persistent:
             assert info["grid"] < info["tiles"] and info["depth"] == 2, info
         f = eng.fired()
@@ -123,5 +124,43 @@ def test_c2_word_sweep_sampled_oracle():
         assert total > len(slots)
         fired = {k: v for k, v in eng.stats()["fired_per_stage"].items() if v}
         assert any("failed" in name for name in fired), fired  # weighted picks ran
+    finally:
+        eng.close()
+
+
+def test_node_heartbeat_persistent_cold_path_sampled_oracle():
+    """The cold path of the persistent table sweep: node-initialize +
+    node-heartbeat (delay + Philox jitter: general table entries, run by `process_object` in
+    the per-tile cold loop) over 20M nodes, so `sweep16_fsm_kernel<false, 4, persistent,
+    depth 2>` runs on a persistent grid and every heartbeat goes through the cold loop;
+    every 4999th slot checked against the oracle at each step.  The out-of-line variant of that
+    loop faulted on the small engine of test_node_fast_heartbeat; this is the
+    shared code it called, at the size where the grid strides."""
+    from kwok_amd import workload as W
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    n = 20_000_000
+    files = W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT)
+    nvars = [W.node_object("n"), W.node_object("n", annotations={"example.com/zone": "b"})]
+    prog = KindProgram(load_stage_files(*files))
+    prog.explore(nvars)
+    ing = Ingest(prog)
+    idx = (np.arange(n, dtype=np.int64) * 2654435761 >> 7) & 1
+    hot, dels, rec, cls = ing.variant_columns(nvars, idx)
+    eng = Engine(prog, capacity=n, kind_salt=1)
+    try:
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        del hot, dels, rec, cls
+        assert eng.stats()["state_bytes"] == 2  # jitter: not table-only, so not the 1-byte ids
+        slots = list(range(7, n, 4999))
+        # 2 s per step: node-initialize, then heartbeats every 20 s + up to 5 s of jitter
+        total = _sampled_run(prog, eng, files, nvars, idx, slots, 16, 2 * 10**9, abi.SWEEP_16_FSM, 1,
+                             kind_salt=1, harness=False)
+        per = eng.stats()["fired_per_stage"]
+        assert per["node-initialize"] == n and per["node-heartbeat"] > n // 2, per
+        assert total >= 2 * len(slots)
     finally:
         eng.close()
