@@ -1230,15 +1230,104 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
 constexpr uint32_t kIdNeed = 0x80u, kIdPend = 0x40u, kIdAlive = 0x20u, kIdIndex = 0x1Fu;
 constexpr uint32_t kIdInvalid = 0xFFu;  // not in the dictionary (never stored: the host closes it)
 constexpr int kQ8 = 2;                  // 16-byte chunks per lane: 32 ids per lane, 2048 per wave
+// id transition entry (dict_upload): [7:0] new id, [15:11] the 2-byte fired record's high bits
+// (stage 11-12 when the program has <= 4 stages, flags 13-15), [20:16] fired stage, [23:21]
+// fired flags, [28:24] algorithmic bytes of the item beyond its 1-byte read, [29] writes due =
+// now + fsm_due[entry], [30] matched, [31] fired.  Lookups the sweep never makes (and unused ids,
+// kIdInvalid among them) hold the id itself: no change, nothing fires.
+constexpr uint32_t kId8Rec16 = 0xF800u, kId8Due = 1u << 29, kId8Match = 1u << 30, kId8Fire = 1u << 31;
+// SweepArgs::fsm_bits of the 1-byte sweep: the table holds a kId8Due entry
+constexpr uint32_t kId8AnyDue = 1u;
+// fired records of the 1-byte sweep: 2 bytes {LDS offset: 11, stage: 2, flags: 3} after a 16-byte
+// header {count, 0, 0, 0} when the program has <= 4 stages (kStages4), else the 4-byte records
+// {LDS offset: 13, stage: 5, flags: 3} after the count word as in the other sweeps
+constexpr uint32_t kRec16Header = 16;
 
-// wave-region offset (minus lane * 16) of bit k of a lane's phase-1 masks in the 1-byte sweep:
-// bit k = b * 8 + q * 4 + j  <->  chunk q, dword j, byte b (so a dword's four flags land with
-// one mask-and-shift each)
-__device__ __forceinline__ constexpr uint32_t bit_id8(const uint32_t k) {
-  return ((k >> 2) & 1u) * 1024u + (k & 3u) * 4u + (k >> 3);
+// A wave's 2048 ids sit in its 2 KiB LDS tile dword-major: dword jj (0-7) of every lane in one
+// 256-byte row.  Bit k of a lane's phase-1 masks is byte b = k >> 3 of its dword jj = k & 7
+// (dword j = jj & 3 of chunk q = jj >> 2): one mask-and-shift per dword and flag.  Fired records
+// carry the LDS offset (11 bits); compaction maps it back to the slot (id8_slot).
+__device__ __forceinline__ uint32_t lds_id8(const uint32_t k) { return (k & 7u) * 256u + (k >> 3); }
+// slot within the wave region of LDS offset x (row q of the region = 1 KiB, lane = 16 bytes of it)
+__host__ __device__ __forceinline__ uint32_t id8_slot(const uint32_t x) {
+  const uint32_t jj = x >> 8, lane = (x >> 2) & 63u, b = x & 3u;
+  return (jj >> 2) * 1024u + lane * 16u + (jj & 3u) * 4u + b;
+}
+__device__ __forceinline__ unsigned long long ballot(const bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+// inclusive prefix sum over the wave's lanes on DPP lane moves: row_shr 1 / 2 / 4 / 8 within each
+// row of 16, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3)
+template <int C, int RM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, C, RM, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += dpp_u32<0x111, 0xF>(v);
+  v += dpp_u32<0x112, 0xF>(v);
+  v += dpp_u32<0x114, 0xF>(v);
+  v += dpp_u32<0x118, 0xF>(v);
+  v += dpp_u32<0x142, 0xA>(v);
+  v += dpp_u32<0x143, 0xC>(v);
+  return v;
 }
 
-template <bool kPersist, int kDepth>
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
+// One 64-item pass of the 1-byte sweep's phase 2.  Work-list entries are absolute LDS byte
+// addresses of ids (tiles are 2 KiB aligned: the low 11 bits are the tile offset); an inactive
+// lane's entry points at its own byte of a row of kIdInvalid, whose lookup is the identity.
+// kSlow: entries carry "the queued stage is due" at bit 15, or the table schedules delayed
+// stages.  kStages4: the fired records go to the wave's LDS work list (their positions lie
+// behind the entries still to be read), 2 bytes each, and the per-stage counts to scalar
+// registers; else 4-byte records straight to the segment and LDS counters.
+template <bool kSlow, bool kStages4>
+__device__ __forceinline__ void id8_pass(const uint32_t we, const uint32_t* __restrict__ s_fsm, uint16_t* __restrict__ wl,
+                                         const __amdgpu_buffer_rsrc_t seg_rs, uint32_t& seg_n, uint32_t& n_bytes,
+                                         uint32_t& n_matched, uint32_t (&stc)[4], unsigned int* s_stat, uint32_t n_stages,
+                                         uint32_t lane, bool any_due, const __amdgpu_buffer_rsrc_t fdue_rs,
+                                         const __amdgpu_buffer_rsrc_t due_rs, uint32_t wbase, int64_t now) {
+  const uint32_t addr = kSlow ? (we & 0x7FFFu) : we;
+  const uint32_t r = kSlow ? (we >> 7) & 0x100u : 0u;
+  lds_u8* p = (lds_u8*)(size_t)addr;
+  const uint32_t key = r | (uint32_t)*p;
+  const uint32_t e = s_fsm[key];
+  *p = (uint8_t)e;
+  n_bytes += (e >> 24) & 31u;
+  n_matched += (e >> 30) & 1u;
+  if (kSlow && any_due && (e & kId8Due)) {  // a delayed stage is scheduled (rare for table-only programs)
+    const int64_t dd = buf_load_i64(fdue_rs, key * 8u);
+    const int64_t t = sat_add(now, dd);
+    const uint32_t off = (wbase + id8_slot(addr & 0x7FFu)) * 8u;
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, due_rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)((uint64_t)t >> 32), due_rs, off + 4u, 0, 0);
+  }
+  const bool fire = (int32_t)e < 0;
+  const unsigned long long bal = ballot(fire);
+  if (bal) {  // wave-uniform
+    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, seg_n));
+    if constexpr (kStages4) {
+      if (fire) wl[pos] = (uint16_t)((addr & 0x7FFu) | (e & kId8Rec16));
+      const uint32_t code = (e >> 11) & 3u;
+#pragma unroll
+      for (uint32_t st = 0; st < 4; ++st) stc[st] += (uint32_t)__popcll(ballot(code == st) & bal);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32((addr & 0x7FFu) | ((e >> 3) & 0x1FE000u), seg_rs, fire ? (1u + pos) * 4u : kOOB,
+                                            0, 0);
+      const uint32_t code = (e >> 16) & 31u;
+      for (uint32_t st = 0; st < n_stages; ++st) {
+        const unsigned long long same = ballot(code == st) & bal;
+        if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
+      }
+    }
+    seg_n += (uint32_t)__popcll(bal);
+  }
+}
+
+template <bool kPersist, int kDepth, bool kStages4>
 __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   constexpr int Q = kQ8;
   constexpr int K = 16 * Q;                // ids per lane
@@ -1246,17 +1335,19 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   constexpr uint32_t kTile = kBlock * K;   // ids per block
   constexpr uint32_t kSeg8 = 64u * K + 32u;
   static_assert(kDepth >= 1 && kDepth <= 2 && (kPersist || kDepth == 1), "prefetch depth");
-  static_assert(kWave <= 8192 && K == 32, "13-bit record slots, 32-bit lane masks");
-  __shared__ unsigned int s_stat[kStatWords];
+  static_assert(kWave == 2048 && K == 32, "11-bit record offsets, 32-bit lane masks");
+  __shared__ __attribute__((aligned(2048))) uint32_t s_tile[kWavesPerBlock][4 * Q][64];
+  __shared__ __attribute__((aligned(16))) uint16_t s_work[kWavesPerBlock][kWave];
+  __shared__ uint32_t s_inv[kWavesPerBlock][64];  // kIdInvalid bytes: the inactive lanes' entries
   __shared__ uint32_t s_fsm[512];
-  __shared__ uint16_t s_work[kWavesPerBlock][kWave];
-  __shared__ uint4 s_tile[kWavesPerBlock][64 * Q];
+  __shared__ unsigned int s_stat[kStatWords];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, (a.n + 15u) & ~15u);
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
+  const __amdgpu_buffer_rsrc_t cnt_rs = make_rsrc(a.wave_counts, n_tiles * kWavesPerBlock * 4u);
   uint4 va[kDepth][Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
     const uint32_t off = t < n_tiles ? t * kTile + wave * kWave + lane * 16u : kOOB - 2048u;
@@ -1270,26 +1361,40 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   issue_tile(va[0], tile);
   if (kDepth > 1) issue_tile(va[kDepth - 1], tile + gridDim.x);
   const uint32_t n_stages = a.table->n_stages;
-  for (uint32_t j = threadIdx.x; j < 512u; j += kBlock) s_fsm[j] = a.fsm[j];
+  const bool any_due = (a.fsm_bits & kId8AnyDue) != 0;
+  // two table entries per thread, no loop: the wait for them (which drains the tile loads issued
+  // above) is on every path into the tile loop, so its waits count only the loop's own operations
+  static_assert(kBlock * 2 == 512, "id table staging");
+  {
+    const uint32_t t0 = a.fsm[threadIdx.x], t1 = a.fsm[threadIdx.x + kBlock];
+    s_fsm[threadIdx.x] = t0;
+    s_fsm[threadIdx.x + kBlock] = t1;
+  }
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
+  s_inv[wave][lane] = 0xFFFFFFFFu;
   __syncthreads();
 
-  uint32_t stc01 = 0, stc23 = 0;        // per lane: fired records of stages 0 | 1 << 16, 2 | 3 << 16
+  uint32_t stc[4] = {0u, 0u, 0u, 0u};   // wave-uniform: fired records of stages 0-3 (kStages4)
   uint32_t n_matched = 0, n_bytes = 0;  // per lane
   uint32_t n_lline = 0;                 // per lane: bytes of the phase-3 line stores
   uint32_t w_bytes = 0, w_line = 0;     // wave-uniform
   uint32_t wave_fired = 0;              // wave-uniform
+  uint32_t* __restrict__ tw = &s_tile[wave][0][0];
   uint16_t* __restrict__ wl = s_work[wave];
-  uint4* __restrict__ tq = s_tile[wave];
-  uint8_t* __restrict__ tb = reinterpret_cast<uint8_t*>(tq);
-  uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+  const __amdgpu_buffer_rsrc_t gq_rs = make_rsrc(a.st, (a.n + 2047u) & ~2047u);  // whole lines of the padded column
+  const uint32_t lane_lds = lds_addr(tw) + lane * 4u;  // 2 KiB aligned tile
+  const uint32_t inv_ent = lds_addr(&s_inv[wave][lane]);
 
+  // tile_body also runs for one tile past the last (the second half of the last pair of the
+  // persistent loop, which has no exit in between: the in-order wait counts stay the same on
+  // every path): its loads are out of range (zeros: no work) and so are its stores
   auto tile_body = [&](uint4 (&v)[Q], const uint32_t tile) __attribute__((always_inline)) {
+    const bool real = tile < n_tiles;  // wave-uniform
     const uint32_t wbase = tile * kTile + wave * kWave;
     const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
     uint32_t seg_n = 0;  // wave-uniform
-    const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
-    uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * kSeg8;
+    const uint32_t seg_id = tile * kWavesPerBlock + wave;
+    uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + (uint64_t)seg_id * kSeg8;
     const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg8 * 4u);
     uint4 cur_copy[Q];
     if (kDepth == 1) {
@@ -1325,95 +1430,111 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
     }
     need &= in_range;
     pend &= in_range;
-    if (__ballot(pend != 0)) {  // a queued stage: is it due?
-#pragma unroll 8
+    if (ballot(pend != 0)) {  // a queued stage: is it due? (4 loads in flight: registers stay low)
+#pragma unroll 4
       for (int k = 0; k < K; ++k) {
         const uint32_t p = (pend >> k) & 1u;
-        const int64_t d = buf_load_i64(due_rs, p ? (wbase + bit_id8((uint32_t)k) + lane * 16u) * 8u : kOOB);
+        const uint32_t slot = id8_slot(lds_id8((uint32_t)k) + lane * 4u);
+        const int64_t d = buf_load_i64(due_rs, p ? (wbase + slot) * 8u : kOOB);
         ready |= (p & (uint32_t)(d <= a.now)) << k;
       }
       need |= ready;
     }
     n_bytes += (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
     uint32_t n_work = 0, pos = 0;
-    {
+    {  // exclusive prefix of the lanes' item counts (DPP scan) and the wave's total
       const uint32_t cnt = (uint32_t)__popc(need);
-      const unsigned long long lt = (1ull << lane) - 1ull;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        const unsigned long long bal = __ballot((cnt >> b) & 1u);
-        pos += (uint32_t)__popcll(bal & lt) << b;
-        n_work += (uint32_t)__popcll(bal) << b;
-      }
-      for (uint32_t m = need; m; m &= m - 1u) {
-        const uint32_t k = (uint32_t)__ffs(m) - 1u;
-        wl[pos++] = (uint16_t)(bit_id8(k) + lane * 16u + (((ready >> k) & 1u) << 15));
-      }
+      const uint32_t incl = wave_incl_scan(cnt);
+      pos = incl - cnt;
+      n_work = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
-    if (n_work) {
-      // ---- phase 2: one LDS table lookup per work item
+    if (n_work) {  // wave-uniform
+      // ---- phase 2: the ids to the LDS tile, the work list (absolute LDS addresses of the ids in
+      // slot order per lane), then one lookup in the id table per item, 64 items per pass
 #pragma unroll
-      for (int q = 0; q < Q; ++q) tq[q * 64 + lane] = cur[q];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : 0xFFFFFFFFu;
-      for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
-        const uint32_t we = nwe;
-        if (c + 64u < n_work) nwe = c + 64u + lane < n_work ? (uint32_t)wl[c + 64u + lane] : 0xFFFFFFFFu;
-        const bool act = we != 0xFFFFFFFFu;
-        const uint32_t w = we & 0x7FFu, rdy = (we >> 15) & 1u;
-        const uint32_t id = act ? (uint32_t)tb[w] : 0u;
-        const uint32_t e = s_fsm[(rdy << 8) | id];
-        if (act) {
-          tb[w] = (uint8_t)e;
-          n_matched += (e >> 25) & 1u;
-          n_bytes += ((e >> 26) & 15u) * 2u - 1u;  // the table counts a 2-byte word write
-        }
-        const bool dw = act && (e & kFsmDue);
-        if (__ballot(dw)) {  // a delayed stage is scheduled
-          const int64_t dd = buf_load_i64(fdue_rs, dw ? ((rdy << 8) | id) * 8u : kOOB);
-          const int64_t t = sat_add(a.now, dd);
-          const uint32_t off = dw ? (wbase + w) * 8u : kOOB;
-          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, due_rs, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)((uint64_t)t >> 32), due_rs, off + 4u, 0, 0);
-        }
-        const bool fire = act && ((e >> 21) & 1u);
-        const unsigned long long bal = __ballot(fire);
-        if (bal) {
-          const uint32_t p = seg_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          const uint32_t rec = w | ((e >> 16) & 31u) << 13 | ((e >> 22) & 7u) << 18;
-          __builtin_amdgcn_raw_buffer_store_b32(rec, seg_rs, fire ? (1u + p) * 4u : kOOB, 0, 0);
-          const uint32_t nf = (uint32_t)__popcll(bal);
-          seg_n += nf;
-          w_bytes += 4u * nf;
-          const uint32_t code = fire ? ((e >> 16) & 31u) : 31u;
-          if (n_stages <= 4) {
-            const uint32_t inc = 1u << (16u * (code & 1u));
-            stc01 += code < 2u ? inc : 0u;
-            stc23 += (code - 2u) < 2u ? inc : 0u;
-          } else {
-            for (uint32_t st = 0; st < n_stages; ++st) {
-              const unsigned long long same = __ballot(code == st);
-              if (same && lane == 0) atomicAdd(&s_stat[3 + st], (unsigned)__popcll(same));
-            }
+      for (int q = 0; q < Q; ++q) {
+        tw[(q * 4 + 0) * 64 + lane] = cur[q].x;
+        tw[(q * 4 + 1) * 64 + lane] = cur[q].y;
+        tw[(q * 4 + 2) * 64 + lane] = cur[q].z;
+        tw[(q * 4 + 3) * 64 + lane] = cur[q].w;
+      }
+      const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
+      const bool slow = rdy || any_due;          // ... or due times may be written
+      {
+        uint32_t m = need;
+        uint16_t* wp = wl + pos;
+        if (rdy) {
+          while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            *wp++ = (uint16_t)((lane_lds + lds_id8(k)) | ((ready >> k) & 1u) << 15);
+          }
+        } else {
+          while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            *wp++ = (uint16_t)(lane_lds + lds_id8(k));
           }
         }
       }
-      w_line -= n_work;  // the ids' own writes are replaced by the line stores below
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      // ---- phase 3: whole 128-byte lines wherever an id changed
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const uint4 nv = tq[q * 64 + lane];
-        const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
-        const unsigned long long bal = __ballot(ch);
-        if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
-          store_chunk_nt(&gq[(wbase + (uint32_t)q * 1024u + lane * 16u) / 16u], nv);
-          n_lline += 16u;
+      // the next pass's entries are read while this pass works (an entry past the list: the
+      // lane's kIdInvalid byte)
+      uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : inv_ent;
+      for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
+        const uint32_t we = nwe;
+        if (c + 64u < n_work) {
+          const uint32_t x = (uint32_t)wl[(c + 64u + lane) & (kWave - 1u)];
+          nwe = c + 64u + lane < n_work ? x : inv_ent;
         }
+        if (slow)
+          id8_pass<true, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
+                                   fdue_rs, due_rs, wbase, a.now);
+        else
+          id8_pass<false, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
+                                    fdue_rs, due_rs, wbase, a.now);
       }
+      n_lline -= (uint32_t)__popc(need);  // the ids' own writes are replaced by the line stores below
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    {
+    // ---- phase 3 and the hand-back segment: a fixed set of stores per tile (whole 128-byte lines
+    // wherever an id changed, the staged records, the header), each lane's offset out of range
+    // where it has nothing to store — no exec branch around a store, so that the compiler's
+    // in-order wait for the next prefetched tile counts exactly the stores issued after it
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      uint4 nv = cur[q];
+      if (n_work)
+        nv = make_uint4(tw[(q * 4 + 0) * 64 + lane], tw[(q * 4 + 1) * 64 + lane], tw[(q * 4 + 2) * 64 + lane],
+                        tw[(q * 4 + 3) * 64 + lane]);
+      const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
+      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{nv.x, nv.y, nv.z, nv.w}, gq_rs,
+                                             st ? wbase + (uint32_t)q * 1024u + lane * 16u : kOOB, 0, 2 /* nt */);
+      n_lline += st ? 16u : 0u;
+    }
+    if constexpr (kStages4) {
+      // records: seg_n 2-byte records from the work list, as 16-byte chunks of whole 128-byte
+      // lines (the tail of the last line is padding)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint32_t n_chunks = ((seg_n * 2u + 127u) & ~127u) / 16u;
+      const uint4* wq = reinterpret_cast<const uint4*>(wl);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t ci = r * 64u + lane;
+        const uint4 x = wq[ci];
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{x.x, x.y, x.z, x.w}, seg_rs,
+                                               ci < n_chunks ? kRec16Header + ci * 16u : kOOB, 0, 0);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{seg_n, 0u, 0u, 0u}, seg_rs, lane == 0 && real ? 0u : kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(seg_n, cnt_rs, lane == 0 && real ? seg_id * 4u : kOOB, 0, 0);
+      if (real) {
+        w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
+        w_bytes += 2u * seg_n + 4u;
+      }
+    } else if (real) {
       const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
       for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
       if (lane == 0) {
@@ -1421,9 +1542,9 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
         a.wave_counts[seg_id] = seg_n;
       }
       w_line += 4u * (end - used);
+      w_bytes += 4u * seg_n + 4u;
     }
     wave_fired += seg_n;
-    w_bytes += 4u;
     if (kPersist && kDepth == 2) issue_tile(v, tile + 2u * gridDim.x);
   };
   if constexpr (!kPersist) {
@@ -1433,7 +1554,6 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   } else {
     for (; tile < n_tiles; tile += 2u * gridDim.x) {
       tile_body(va[0], tile);
-      if (tile + gridDim.x >= n_tiles) break;
       tile_body(va[kDepth - 1], tile + gridDim.x);
     }
   }
@@ -1443,14 +1563,12 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
     n_bytes += __shfl_xor(n_bytes, off);
     n_lline += __shfl_xor(n_lline, off);
   }
-  uint32_t stn[4] = {stc01 & 0xFFFFu, stc01 >> 16, stc23 & 0xFFFFu, stc23 >> 16};
-#pragma unroll
-  for (int st = 0; st < 4; ++st)
-    for (int off = 32; off > 0; off >>= 1) stn[st] += __shfl_xor(stn[st], off);
   if (lane == 0) {
+    if constexpr (kStages4) {
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
-      if (stn[st]) atomicAdd(&s_stat[3 + st], stn[st]);
+      for (int st = 0; st < 4; ++st)
+        if (stc[st]) atomicAdd(&s_stat[3 + st], stc[st]);
+    }
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], wave_fired);
     atomicAdd(&s_stat[2], n_bytes + w_bytes);
@@ -1775,8 +1893,23 @@ struct CompactArgs {
   uint32_t stride;
 };
 
-// one wave per segment; the first 256 records are loaded together with the segment's count and
-// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it)
+// record kinds: 4-byte {slot within the region: 13, stage: 5, flags: 3} after the count word;
+// the 1-byte sweep's 4-byte records with an LDS offset in the slot field (id8_slot); its 2-byte
+// records {LDS offset: 11, stage: 2, flags: 3} after a 16-byte header
+enum : int { kRecSlot = 0, kRecId8 = 1, kRecId8Half = 2 };
+
+// record j of a segment as (slot within the region, 4-byte layout for the stage / flags)
+template <int kRec>
+__device__ __forceinline__ uint2 rec_at(const uint32_t* __restrict__ seg, uint32_t j) {
+  if constexpr (kRec == kRecId8Half) {
+    const uint32_t x = reinterpret_cast<const uint16_t*>(seg + kRec16Header / 4u)[j];
+    return make_uint2(id8_slot(x & 0x7FFu), ((x >> 11) & 3u) << 13 | ((x >> 13) & 7u) << 18);
+  } else {
+    const uint32_t x = seg[1u + j];
+    return make_uint2(kRec == kRecId8 ? id8_slot(x & 0x7FFu) : x & 0x1FFFu, x);
+  }
+}
+
 // one kwk_fired_rec {slot, stage, flags} from a packed record, nontemporal (the dense list is
 // written once per step and read by the consumer later: keeping it out of L2 leaves room for
 // the segments being read)
@@ -1785,15 +1918,18 @@ __device__ __forceinline__ void store_rec_nt(kwk_fired_rec* p, uint32_t slot, ui
   __builtin_nontemporal_store(u32x2{slot, ((x >> 13) & 31u) | ((x >> 18) & 7u) << 16}, reinterpret_cast<u32x2*>(p));
 }
 
+// one wave per segment; the first 256 records are loaded together with the segment's count and
+// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it)
+template <int kRec>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t seg = blockIdx.x * kSegsPerBlock + wave;
   if (seg >= a.n_segs) return;
-  const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
-  uint32_t r[kPre];
+  const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
+  uint2 r[kPre];
 #pragma unroll
-  for (int k = 0; k < kPre; ++k) r[k] = f32[lane + 64u * k];
+  for (int k = 0; k < kPre; ++k) r[k] = rec_at<kRec>(sp, lane + 64u * k);
   const uint32_t c = a.counts[seg];
   uint32_t gp = 0;  // records of the groups before this segment's
   for (uint32_t g = lane; g < seg / kScanGroup; g += 64) gp += a.group_tot[g];
@@ -1804,11 +1940,11 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const uint32_t j = lane + 64u * k;
-    if (j < c) store_rec_nt(&a.out[off + j], base + (r[k] & 0x1FFFu), r[k]);
+    if (j < c) store_rec_nt(&a.out[off + j], base + r[k].x, r[k].y);
   }
   for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
-    const uint32_t x = f32[j];
-    store_rec_nt(&a.out[off + j], base + (x & 0x1FFFu), x);
+    const uint2 x = rec_at<kRec>(sp, j);
+    store_rec_nt(&a.out[off + j], base + x.x, x.y);
   }
 }
 
@@ -1816,6 +1952,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // strong-scaling shards): each block sums the counts of every segment before its own (at most
 // 32 KB, L2-resident) instead of waiting for seg_scan_kernel, then expands its four segments as
 // compact_kernel does.  Saves one launch and its gap per step.
+template <int kRec>
 __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   __shared__ uint32_t s_part[kWavesPerBlock];
   __shared__ uint32_t s_seg[kWavesPerBlock];
@@ -1833,9 +1970,12 @@ __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
   const uint32_t c = s_seg[wave];
   if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
-  const uint32_t* __restrict__ f32 = a.fired32 + (uint64_t)seg * a.stride + 1u;
+  const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
   const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
-  for (uint32_t j = lane; j < c; j += 64) store_rec_nt(&a.out[off + j], base + (f32[j] & 0x1FFFu), f32[j]);
+  for (uint32_t j = lane; j < c; j += 64) {
+    const uint2 x = rec_at<kRec>(sp, j);
+    store_rec_nt(&a.out[off + j], base + x.x, x.y);
+  }
 }
 
 // sums the per-block statistics rows [0, n_blocks) (the rows any sweep grid has used)
@@ -3228,6 +3368,7 @@ struct kwk_engine {
   uint32_t cum_rows = 0;      // statistics rows any sweep grid has written (<= n_blocks_cap)
   uint32_t last_objs = 16;    // words per lane of the last sweep (fired segment stride = 64 * last_objs + 32)
   uint32_t last_region_shift = 0;  // fired segments per record region = 1 << shift (wave: 0, tile: 2)
+  int last_rec = 0;                // record kind of the last sweep's segments (kRecSlot / kRecId8 / kRecId8Half)
   bool compacted = false;     // the last sweep's fired list is compacted on the device
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
@@ -3264,6 +3405,7 @@ struct kwk_engine {
   uint8_t* d_w2id = nullptr;
   uint32_t* d_fsm8 = nullptr;     // [2][256] id transition table of sweep8_kernel
   int64_t* d_fsm8_due = nullptr;
+  bool fsm8_due_any = false;      // some d_fsm8 entry schedules a delayed stage (kId8Due)
   int64_t* d_due = nullptr;   // due time per slot
   int64_t* d_del = nullptr;
   uint32_t* d_rec = nullptr;
@@ -3558,6 +3700,7 @@ static bool dict_extend(kwk_engine* e, const std::vector<uint32_t>& seeds, bool&
 // the dictionary and the id transition table on the device (synchronous)
 static kwk_status dict_upload(kwk_engine* e) {
   std::vector<uint32_t> t8(512);
+  e->fsm8_due_any = false;
   std::vector<int64_t> d8(512, 0);
   const uint32_t bits = e->fsm_bits;
   for (uint32_t id = 0; id < 256; ++id) {
@@ -3567,7 +3710,12 @@ static kwk_status dict_upload(kwk_engine* e) {
       const uint32_t t = e->h_fsm[(rdy << bits) | w];
       uint32_t x = id;  // unused ids and lookups the sweep never makes: no change, nothing fires
       if (used && !(t & kFsmGeneral) && e->h_w2id[t & 0xFFFFu] != kIdInvalid) {
-        x = (t & 0xFFFF0000u) | e->h_w2id[t & 0xFFFFu];
+        // the 2-byte entry ([20:16] stage, [21] fired, [24:22] flags, [25] matched, [29:26]
+        // bytes / 2 counting a 2-byte word write, [30] due) in the id layout (kId8*)
+        const uint32_t bytes8 = ((t >> 26) & 15u) * 2u - 1u, stage = (t >> 16) & 31u, flags = (t >> 22) & 7u;
+        x = e->h_w2id[t & 0xFFFFu] | (stage & 3u) << 11 | flags << 13 | stage << 16 | flags << 21 | bytes8 << 24 |
+            ((t & kFsmDue) ? kId8Due : 0u) | ((t >> 25) & 1u) * kId8Match | ((t >> 21) & 1u) * kId8Fire;
+        if (t & kFsmDue) e->fsm8_due_any = true;
         d8[(rdy << 8) | id] = e->h_fsm_due[(rdy << bits) | w];
       }
       t8[(rdy << 8) | id] = x;
@@ -4218,26 +4366,31 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     if (!fire) return fail(KWK_ESTATE, "the 1-byte format sweeps with fire only");
     a.fsm = e->d_fsm8;
     a.fsm_due = e->d_fsm8_due;
+    a.fsm_bits = e->fsm8_due_any ? kId8AnyDue : 0u;
     constexpr uint32_t tile = kBlock * 16 * kQ8;
     const uint32_t tiles = (e->n_active + tile - 1) / tile;
-    const void* pk = e->fsm_kernel == 2 ? (const void*)sweep8_kernel<true, 2> : (const void*)sweep8_kernel<true, 1>;
+    const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
+#define K8(P, D) (s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
+    const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
     if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);
     uint32_t blocks = tiles;
     e->last_sweep = kwk_sweep_info{KWK_SWEEP_8, (uint32_t)kQ8, 0, 1, tiles, tiles, a.harness.enable ? 1u : 0u, 0};
-    if (2 * pg > tiles) {  // the persistent loop would run about once: one block per tile
-      hipLaunchKernelGGL((sweep8_kernel<false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
-    } else {
+    const void* kern = K8(false, 1);
+    if (2 * pg <= tiles) {  // else the persistent loop would run about once: one block per tile
       blocks = pg;
       e->last_sweep.persistent = 1;
       e->last_sweep.grid = pg;
       e->last_sweep.depth = e->fsm_kernel;
-      if (e->fsm_kernel == 2) hipLaunchKernelGGL((sweep8_kernel<true, 2>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
-      else hipLaunchKernelGGL((sweep8_kernel<true, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+      kern = pk;
     }
+#undef K8
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(kern, dim3(blocks), dim3(kBlock), args, 0, e->stream));
     HIP_TRY(hipGetLastError());
     e->last_objs = 16 * kQ8;
     e->last_region_shift = 0;
+    e->last_rec = s4 ? kRecId8Half : kRecId8;
     e->last_blocks = tiles;
     e->last_grid = blocks;
     e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
@@ -4290,6 +4443,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
 #undef LAUNCH16
     e->last_objs = K;
     e->last_region_shift = 0;
+    e->last_rec = kRecSlot;
     HIP_TRY(hipGetLastError());
     e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
     e->last_grid = blocks;
@@ -4312,6 +4466,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
                                  h ? 1u : 0u, 0};
   e->last_objs = K;
   e->last_region_shift = 2;  // log2(kWavesPerBlock): records carry tile-relative slots
+  e->last_rec = kRecSlot;
   static_assert(kWavesPerBlock == 4, "region shift");
   HIP_TRY(hipGetLastError());
   e->last_blocks = blocks;
@@ -4362,14 +4517,21 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   a.seg_region_shift = e->last_region_shift;
   a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
+  const int rk = e->last_rec;
+  void* args[] = {&a};
   if (n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
-    hipLaunchKernelGGL(compact_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
-    HIP_TRY(hipGetLastError());
+    const void* k = rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half>
+                    : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8>
+                                      : (const void*)compact_small_kernel<kRecSlot>;
+    HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
     return KWK_OK;
   }
   hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
                      e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
-  hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+  const void* k = rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half>
+                  : rk == kRecId8   ? (const void*)compact_kernel<kRecId8>
+                                    : (const void*)compact_kernel<kRecSlot>;
+  HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }

@@ -63,6 +63,14 @@ VARIANTS = {
                     "          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);\n          n_lline",
                     "        if (bal || true) {\n"
                     "          store_chunk_nt(&gq[(wbase + (uint32_t)q * 512u + lane * 8u) / 8u], nv);\n          n_lline")],
+    # no value-record loads: objects with a record take the stage defaults (C2 cost isolation of
+    # the dependent rec_idx -> record round trips of phase 2)
+    "w_norec": [("  if (!(sched & KWK_F_HASREC)) return {def, def_ok};", "  return {def, def_ok};"),
+                ("  if (sched & KWK_F_HASREC) {\n    if constexpr (kProbe) { gen = 1; return false; }",
+                 "  if (false) {\n    if constexpr (kProbe) { gen = 1; return false; }")],
+    # no deletion-column loads (pod-delete's jitterDurationFrom)
+    "w_nodel": [("    const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;",
+                 "    const int64_t dels = KWK_DEL_ABSENT;")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
