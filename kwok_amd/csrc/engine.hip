@@ -1244,13 +1244,19 @@ constexpr uint32_t kId8AnyDue = 1u;
 constexpr uint32_t kRec16Header = 16;
 
 // A wave's 2048 ids sit in its 2 KiB LDS tile dword-major: dword jj (0-7) of every lane in one
-// 256-byte row.  Bit k of a lane's phase-1 masks is byte b = k >> 3 of its dword jj = k & 7
-// (dword j = jj & 3 of chunk q = jj >> 2): one mask-and-shift per dword and flag.  Fired records
-// carry the LDS offset (11 bits); compaction maps it back to the slot (id8_slot).
-__device__ __forceinline__ uint32_t lds_id8(const uint32_t k) { return (k & 7u) * 256u + (k >> 3); }
+// 256-byte row, lane L's at column L ^ jj, so that the items of one lane (consecutive in the work
+// list) fall in different banks and a row's store / load by all lanes is a permutation.  Bit k
+// of a lane's phase-1 masks is byte b = k >> 3 of its dword jj = k & 7 (dword j = jj & 3 of chunk
+// q = jj >> 2): one mask-and-shift per dword and flag.  Fired records carry the LDS offset
+// (11 bits); compaction maps it back to the slot (id8_slot).
+__device__ __forceinline__ uint32_t lds_id8(const uint32_t k, const uint32_t lane4) {
+  const uint32_t jj = k & 7u;
+  return jj << 8 | (lane4 ^ jj << 2) | k >> 3;
+}
+__device__ __forceinline__ uint32_t lds_col8(const uint32_t jj, const uint32_t lane) { return jj * 64u + (lane ^ jj); }
 // slot within the wave region of LDS offset x (row q of the region = 1 KiB, lane = 16 bytes of it)
 __host__ __device__ __forceinline__ uint32_t id8_slot(const uint32_t x) {
-  const uint32_t jj = x >> 8, lane = (x >> 2) & 63u, b = x & 3u;
+  const uint32_t jj = x >> 8, lane = ((x >> 2) & 63u) ^ jj, b = x & 3u;
   return (jj >> 2) * 1024u + lane * 16u + (jj & 3u) * 4u + b;
 }
 __device__ __forceinline__ unsigned long long ballot(const bool b) { return __builtin_amdgcn_ballot_w64(b); }
@@ -1382,7 +1388,8 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   uint32_t* __restrict__ tw = &s_tile[wave][0][0];
   uint16_t* __restrict__ wl = s_work[wave];
   const __amdgpu_buffer_rsrc_t gq_rs = make_rsrc(a.st, (a.n + 2047u) & ~2047u);  // whole lines of the padded column
-  const uint32_t lane_lds = lds_addr(tw) + lane * 4u;  // 2 KiB aligned tile
+  const uint32_t tile_lds = lds_addr(tw);  // 2 KiB aligned
+  const uint32_t lane4 = lane * 4u;
   const uint32_t inv_ent = lds_addr(&s_inv[wave][lane]);
 
   // tile_body also runs for one tile past the last (the second half of the last pair of the
@@ -1434,7 +1441,7 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
 #pragma unroll 4
       for (int k = 0; k < K; ++k) {
         const uint32_t p = (pend >> k) & 1u;
-        const uint32_t slot = id8_slot(lds_id8((uint32_t)k) + lane * 4u);
+        const uint32_t slot = id8_slot(lds_id8((uint32_t)k, lane4));
         const int64_t d = buf_load_i64(due_rs, p ? (wbase + slot) * 8u : kOOB);
         ready |= (p & (uint32_t)(d <= a.now)) << k;
       }
@@ -1453,10 +1460,10 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
       // slot order per lane), then one lookup in the id table per item, 64 items per pass
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        tw[(q * 4 + 0) * 64 + lane] = cur[q].x;
-        tw[(q * 4 + 1) * 64 + lane] = cur[q].y;
-        tw[(q * 4 + 2) * 64 + lane] = cur[q].z;
-        tw[(q * 4 + 3) * 64 + lane] = cur[q].w;
+        tw[lds_col8(q * 4 + 0, lane)] = cur[q].x;
+        tw[lds_col8(q * 4 + 1, lane)] = cur[q].y;
+        tw[lds_col8(q * 4 + 2, lane)] = cur[q].z;
+        tw[lds_col8(q * 4 + 3, lane)] = cur[q].w;
       }
       const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
       const bool slow = rdy || any_due;          // ... or due times may be written
@@ -1467,13 +1474,13 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
           while (m) {
             const uint32_t k = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            *wp++ = (uint16_t)((lane_lds + lds_id8(k)) | ((ready >> k) & 1u) << 15);
+            *wp++ = (uint16_t)((tile_lds | lds_id8(k, lane4)) | ((ready >> k) & 1u) << 15);
           }
         } else {
           while (m) {
             const uint32_t k = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            *wp++ = (uint16_t)(lane_lds + lds_id8(k));
+            *wp++ = (uint16_t)(tile_lds | lds_id8(k, lane4));
           }
         }
       }
@@ -1505,8 +1512,8 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
     for (int q = 0; q < Q; ++q) {
       uint4 nv = cur[q];
       if (n_work)
-        nv = make_uint4(tw[(q * 4 + 0) * 64 + lane], tw[(q * 4 + 1) * 64 + lane], tw[(q * 4 + 2) * 64 + lane],
-                        tw[(q * 4 + 3) * 64 + lane]);
+        nv = make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)], tw[lds_col8(q * 4 + 2, lane)],
+                        tw[lds_col8(q * 4 + 3, lane)]);
       const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
       const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -3647,6 +3654,15 @@ static bool word_successors(const kwk_engine* e, uint32_t w, std::vector<uint32_
   return true;
 }
 
+// index within class c of its j-th id: classes start 4 banks apart (class 7 at 0, so that its
+// last index, 0xFF = kIdInvalid, is never reached), so the id-table entries that the
+// 1-byte sweep's lanes look up together rarely share an LDS bank
+static uint32_t id8_index(uint32_t c, uint32_t j) { return c == 7u ? j : (j + 4u * c) & kIdIndex; }
+static uint32_t id8_rank(uint32_t id) {
+  const uint32_t c = id >> 5;
+  return c == 7u ? (id & kIdIndex) : ((id & kIdIndex) - 4u * c) & kIdIndex;
+}
+
 static void dict_reset(kwk_engine* e) {
   e->h_id2w.assign(256, 0);
   e->h_w2id.assign(65536, (uint8_t)kIdInvalid);
@@ -3689,7 +3705,7 @@ static bool dict_extend(kwk_engine* e, const std::vector<uint32_t>& seeds, bool&
   }
   for (uint32_t w : added) {
     const uint32_t c = word_class(e, w);
-    const uint32_t id = (c << 5) | e->id_fill[c]++;
+    const uint32_t id = (c << 5) | id8_index(c, e->id_fill[c]++);
     e->h_id2w[id] = (uint16_t)w;
     e->h_w2id[w] = (uint8_t)id;
   }
@@ -3705,7 +3721,7 @@ static kwk_status dict_upload(kwk_engine* e) {
   const uint32_t bits = e->fsm_bits;
   for (uint32_t id = 0; id < 256; ++id) {
     const uint32_t w = e->h_id2w[id];
-    const bool used = id == 0 || (id != kIdInvalid && (id & kIdIndex) < e->id_fill[id >> 5]);
+    const bool used = id == 0 || (id != kIdInvalid && id8_rank(id) < e->id_fill[id >> 5]);
     for (uint32_t rdy = 0; rdy < 2; ++rdy) {
       const uint32_t t = e->h_fsm[(rdy << bits) | w];
       uint32_t x = id;  // unused ids and lookups the sweep never makes: no change, nothing fires

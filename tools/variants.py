@@ -71,6 +71,17 @@ VARIANTS = {
     # no deletion-column loads (pod-delete's jitterDurationFrom)
     "w_nodel": [("    const int64_t dels = need_del ? a.del_s[i] : KWK_DEL_ABSENT;",
                  "    const int64_t dels = KWK_DEL_ABSENT;")],
+    # 1-byte sweep (run with --c5): no phase 2, every line of the column rewritten — the kernel's
+    # own read + rewrite stream (wrong results: the ids never change)
+    "s8_stream": [("    if (n_work) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile",
+                   "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
+                  ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
+                   "      const bool st = real || ch;")],
+    # ... and no line stores: the read stream alone
+    "s8_read": [("    if (n_work) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile",
+                 "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
+                ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
+                 "      const bool st = !real && ch;")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
