@@ -888,7 +888,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
 // record or the deletion column) runs process_object with the stage table, match masks and
 // deltas read from global memory (L2).  Returns the entry the table would hold ({new word,
 // fired stage / flag / flags, matched} without kFsmDue: the due time is already stored) and the
-// algorithmic bytes.  (Inlined: an out-of-line call made the persistent kernel fault at C5.)
+// algorithmic bytes.  (Inlined.  A round-2 build that made this a `noinline` function taking the
+// kernel's SweepArgs by reference faulted twice — the one-block-per-tile Q = 1 node engine of
+// test_node_fast_heartbeat and the C5 bench — and was reverted; DESIGN.md §5 records what its ISA
+// shows and why the shared code it called is not the cause.)
 template <bool kHarness>
 __device__ __forceinline__ uint2 general16(uint32_t i, uint32_t raw) {
   // the kernel's SweepArgs (its only argument, at offset 0 of the kernarg segment) and the stage
