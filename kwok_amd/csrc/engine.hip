@@ -3453,6 +3453,8 @@ struct kwk_engine {
   double* d_agg = nullptr;        // kwk_aggregate's own output buffer
   uint32_t* d_count_part = nullptr;  // count_kernel's per-block partial counts
   unsigned long long* d_agg_counts = nullptr;
+  uint32_t agg_masks[16] = {};    // the masks last copied to d_agg_masks (kMaxCountMasks)
+  uint32_t agg_n_masks = 0;
   uint32_t* d_agg_masks = nullptr;
   double* d_podv = nullptr;       // usage_fast_kernel's pod values per (containers, value id)
   uint32_t podv_n = 0;
@@ -4389,6 +4391,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     constexpr uint32_t tile = kBlock * 16 * kQ8;
     const uint32_t tiles = (e->n_active + tile - 1) / tile;
     const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
+
 #define K8(P, D) (s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
@@ -5317,9 +5320,16 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
   double* dst = out ? out : e->d_agg;
   hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->cum_rows, e->d_stats);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
+  // count_total_kernel overwrites the counts it produces: zeroed only when no count runs.  The
+  // masks go to the device only when they change (a pageable copy would stall the host, r3 trace)
+  if (!(n_masks && e->n_active))
+    HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
   if (n_masks) {
-    HIP_TRY(hipMemcpyAsync(e->d_agg_masks, masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
+    if (n_masks != e->agg_n_masks || memcmp(masks, e->agg_masks, 4 * (size_t)n_masks) != 0) {
+      memcpy(e->agg_masks, masks, 4 * (size_t)n_masks);
+      e->agg_n_masks = n_masks;
+      HIP_TRY(hipMemcpyAsync(e->d_agg_masks, e->agg_masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
+    }
     if (e->n_active) {
       const uint32_t wb = (uint32_t)word_bytes(e->fmt);
       const uint64_t chunks = ((uint64_t)e->n_active * wb + 15u) / 16u;

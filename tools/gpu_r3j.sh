@@ -2,7 +2,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-r3j}
 mkdir -p $O && cd $R
-timeout -k 10 600 python tools/variants.py run --c5 --steps 20 base s8_stream s8_read > $O/c5_variants.jsonl 2> $O/c5_variants.err || { tail -20 $O/c5_variants.err; exit 1; }
+timeout -k 10 600 python tools/variants.py run base s8_stream s8_read --c5 --steps 20 > $O/c5_variants.jsonl 2> $O/c5_variants.err || { tail -20 $O/c5_variants.err; exit 1; }
 python -c "
 import json
 for l in open('$O/c5_variants.jsonl'):
