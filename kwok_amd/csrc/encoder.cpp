@@ -552,24 +552,107 @@ struct Row {
   std::string err;
 };
 
-void prune_meta(JV& obj) {  // omitempty after the apiserver round trip (nextstate.prune_empty)
+// Typed-object presence (expression.ToJSONStandard, query.go:72-88; host mirror typed.py): the
+// reference's queries see json.Marshal of the typed *corev1.Pod / *corev1.Node, so an omitempty
+// field holding the zero value of its string / number / bool / slice / map type is absent, a
+// struct-typed field or a field without omitempty is present, a pointer is present unless nil, a
+// zero metav1.Time is null (dropped by Query.Execute like an absent value).  The table holds the
+// k8s.io/api v0.30.2 core/v1 tags of the fields on the queried paths; other fields keep a
+// non-empty value.  The apiserver's JSON is already in this form; hand-written objects and
+// patched ones (the apiserver round trip drops what a patch emptied) are rewritten.
+enum PKind : uint8_t { P_KEEP, P_STRUCT, P_PTR, P_LIST, P_LIST_KEEP, P_TIME };
+struct PField { const char* type; const char* key; PKind kind; const char* sub; };
+const PField kPresence[] = {
+    {"Pod", "metadata", P_STRUCT, "ObjectMeta"}, {"Pod", "spec", P_STRUCT, "PodSpec"},
+    {"Pod", "status", P_STRUCT, "PodStatus"},
+    {"Node", "metadata", P_STRUCT, "ObjectMeta"}, {"Node", "spec", P_STRUCT, ""},
+    {"Node", "status", P_STRUCT, "NodeStatus"},
+    {"ObjectMeta", "creationTimestamp", P_TIME, ""}, {"ObjectMeta", "deletionTimestamp", P_TIME, ""},
+    {"ObjectMeta", "ownerReferences", P_LIST, "OwnerReference"}, {"ObjectMeta", "managedFields", P_LIST, ""},
+    {"OwnerReference", "apiVersion", P_KEEP, ""}, {"OwnerReference", "kind", P_KEEP, ""},
+    {"OwnerReference", "name", P_KEEP, ""}, {"OwnerReference", "uid", P_KEEP, ""},
+    {"PodSpec", "containers", P_LIST_KEEP, "Container"}, {"PodSpec", "initContainers", P_LIST, "Container"},
+    {"PodSpec", "ephemeralContainers", P_LIST, "Container"},
+    {"Container", "name", P_KEEP, ""}, {"Container", "resources", P_STRUCT, ""},
+    {"PodStatus", "conditions", P_LIST, "PodCondition"}, {"PodStatus", "startTime", P_TIME, ""},
+    {"PodStatus", "initContainerStatuses", P_LIST, "ContainerStatus"},
+    {"PodStatus", "containerStatuses", P_LIST, "ContainerStatus"},
+    {"PodStatus", "ephemeralContainerStatuses", P_LIST, "ContainerStatus"},
+    {"PodCondition", "type", P_KEEP, ""}, {"PodCondition", "status", P_KEEP, ""},
+    {"PodCondition", "lastProbeTime", P_TIME, ""}, {"PodCondition", "lastTransitionTime", P_TIME, ""},
+    {"ContainerStatus", "name", P_KEEP, ""}, {"ContainerStatus", "ready", P_KEEP, ""},
+    {"ContainerStatus", "restartCount", P_KEEP, ""}, {"ContainerStatus", "image", P_KEEP, ""},
+    {"ContainerStatus", "imageID", P_KEEP, ""}, {"ContainerStatus", "state", P_STRUCT, "ContainerState"},
+    {"ContainerStatus", "lastState", P_STRUCT, "ContainerState"},
+    {"ContainerState", "waiting", P_PTR, ""}, {"ContainerState", "running", P_PTR, "ContainerStateRunning"},
+    {"ContainerState", "terminated", P_PTR, "ContainerStateTerminated"},
+    {"ContainerStateRunning", "startedAt", P_TIME, ""},
+    {"ContainerStateTerminated", "exitCode", P_KEEP, ""}, {"ContainerStateTerminated", "startedAt", P_TIME, ""},
+    {"ContainerStateTerminated", "finishedAt", P_TIME, ""},
+    {"NodeStatus", "conditions", P_LIST, "NodeCondition"}, {"NodeStatus", "daemonEndpoints", P_STRUCT, ""},
+    {"NodeStatus", "nodeInfo", P_STRUCT, "NodeSystemInfo"},
+    {"NodeCondition", "type", P_KEEP, ""}, {"NodeCondition", "status", P_KEEP, ""},
+    {"NodeCondition", "lastHeartbeatTime", P_TIME, ""}, {"NodeCondition", "lastTransitionTime", P_TIME, ""},
+    {"NodeSystemInfo", "machineID", P_KEEP, ""}, {"NodeSystemInfo", "systemUUID", P_KEEP, ""},
+    {"NodeSystemInfo", "bootID", P_KEEP, ""}, {"NodeSystemInfo", "kernelVersion", P_KEEP, ""},
+    {"NodeSystemInfo", "osImage", P_KEEP, ""}, {"NodeSystemInfo", "containerRuntimeVersion", P_KEEP, ""},
+    {"NodeSystemInfo", "kubeletVersion", P_KEEP, ""}, {"NodeSystemInfo", "kubeProxyVersion", P_KEEP, ""},
+    {"NodeSystemInfo", "operatingSystem", P_KEEP, ""}, {"NodeSystemInfo", "architecture", P_KEEP, ""},
+};
+
+const PField* presence_field(const char* type, const std::string& key) {
+  for (const PField& f : kPresence)
+    if (strcmp(f.type, type) == 0 && key == f.key) return &f;
+  return nullptr;
+}
+
+// encoding/json isEmptyValue for what JSON holds
+bool zero_value(const JV& v) {
+  switch (v.t) {
+    case JV::NUL: return true;
+    case JV::BOOL: return !v.b;
+    case JV::NUM: return strtod(v.s.c_str(), nullptr) == 0.0;
+    case JV::STR: return v.s.empty();
+    default: return v.a.empty();
+  }
+}
+
+void typed_presence(JV& obj, const char* type) {
   if (obj.t != JV::OBJ) return;
-  for (size_t i = 0; i < obj.k.size(); ++i) {
-    if (obj.k[i] != "metadata" || obj.a[i].t != JV::OBJ) continue;
-    JV& md = obj.a[i];
-    for (size_t j = md.k.size(); j-- > 0;) {
-      const std::string& k = md.k[j];
-      if (k != "finalizers" && k != "labels" && k != "annotations" && k != "ownerReferences") continue;
-      const JV& v = md.a[j];
-      const bool empty = v.t == JV::NUL || ((v.t == JV::ARR || v.t == JV::OBJ) && v.a.empty()) ||
-                         (v.t == JV::STR && v.s.empty()) || (v.t == JV::BOOL && !v.b) ||
-                         (v.t == JV::NUM && strtod(v.s.c_str(), nullptr) == 0.0);
-      if (empty) {
-        md.k.erase(md.k.begin() + (long)j);
-        md.a.erase(md.a.begin() + (long)j);
+  // duplicate keys: the last one is what json.Unmarshal keeps
+  for (size_t i = obj.k.size(); i-- > 0;) {
+    bool later = false;
+    for (size_t j = i + 1; j < obj.k.size(); ++j) later |= obj.k[j] == obj.k[i];
+    bool drop = later;
+    if (!drop) {
+      JV& v = obj.a[i];
+      const PField* f = presence_field(type, obj.k[i]);
+      if (v.t == JV::NUL) drop = true;
+      else if (!f) drop = zero_value(v);
+      else switch (f->kind) {
+        case P_KEEP: break;
+        case P_TIME: drop = v.t == JV::STR && v.s.empty(); break;
+        case P_STRUCT:
+        case P_PTR: typed_presence(v, f->sub); break;
+        case P_LIST:
+        case P_LIST_KEEP:
+          if (v.t == JV::ARR)
+            for (JV& x : v.a) typed_presence(x, f->sub);
+          drop = f->kind == P_LIST && zero_value(v);
+          break;
       }
     }
+    if (drop) {
+      obj.k.erase(obj.k.begin() + (long)i);
+      obj.a.erase(obj.a.begin() + (long)i);
+    }
   }
+}
+
+void typed_presence(JV& obj) {
+  const JV* kind = obj.t == JV::OBJ ? obj.get("kind") : nullptr;
+  const bool known = kind && kind->t == JV::STR && (kind->s == "Pod" || kind->s == "Node");
+  typed_presence(obj, known ? kind->s.c_str() : "");
 }
 
 std::string class_key(const kwk_encoder& E, const JV& obj) {
@@ -625,7 +708,7 @@ void encode_one(const kwk_encoder& E, const char* text, uint32_t len, Row& r) {
   JV obj;
   Parser P{text, text + len};
   if (!P.value(obj) || obj.t != JV::OBJ) { r.err = "invalid JSON object"; return; }
-  prune_meta(obj);
+  typed_presence(obj);
   std::vector<const JV*> out;
   // feature bits (KindProgram.pred_of)
   for (const auto& f : E.features) {

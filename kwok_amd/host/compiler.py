@@ -36,6 +36,7 @@ from .goparse import f64_to_i64, parse_duration, parse_int, parse_rfc3339nano
 from .gotpl import Renderer, rfc3339nano
 from .jq import Query, has_value
 from .nextstate import apply_next, merge_patch, json_patch, prune_empty, render_patches
+from .typed import typed_presence
 from .stages import Stage
 
 FIN_QUERIES = {".metadata.finalizers", ".metadata.finalizers.[]", ".metadata.finalizers[]"}
@@ -105,8 +106,9 @@ _IDENTITY_META = ("name", "generateName", "namespace", "uid", "resourceVersion",
 
 def class_key(obj: dict) -> str:
     """Object class for next-state deltas: the spec shape, with per-object identity
-    (names, node name, owner names/uids, labels/annotations) and all dynamic state removed."""
-    o = copy.deepcopy(obj)
+    (names, node name, owner names/uids, labels/annotations) and all dynamic state removed;
+    of the typed presence, so that spellings of the same typed object share a class."""
+    o = copy.deepcopy(typed_presence(obj))
     o.pop("status", None)
     md = o.get("metadata") or {}
     for k in _IDENTITY_META:

@@ -13,6 +13,7 @@ from typing import List, Optional
 
 from .gotpl import Renderer
 from .stages import Stage, StageFinalizers
+from .typed import typed_presence
 
 
 def finalizers_modify(meta: Optional[List[str]], fin: StageFinalizers):
@@ -109,14 +110,9 @@ def json_patch(obj, ops):
 
 
 def prune_empty(obj):
-    """Re-apply omitempty after a patch: the apiserver round-trips through the typed object,
-    so empty finalizer lists / maps disappear (metav1.ObjectMeta `omitempty`)."""
-    md = obj.get("metadata")
-    if isinstance(md, dict):
-        for k in ("finalizers", "labels", "annotations", "ownerReferences"):
-            if k in md and not md[k]:
-                del md[k]
-    return obj
+    """The object after the apiserver's typed round trip (a patch that empties an omitempty field
+    removes it): typed.typed_presence, which the informer's objects and ToJSONStandard agree on."""
+    return typed_presence(obj)
 
 
 def apply_next(stage: Stage, obj: dict, renderer: Renderer):

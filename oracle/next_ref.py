@@ -31,6 +31,7 @@ import re
 from typing import Callable, Dict, List, Optional, Tuple
 
 from . import refcpu
+from .typed_json import to_json_standard
 
 
 class RenderError(RuntimeError):
@@ -518,13 +519,9 @@ def json_patch(obj, ops):
 
 
 def omitempty(obj):
-    """The apiserver stores typed objects: empty metadata lists / maps (omitempty) vanish."""
-    md = obj.get("metadata")
-    if isinstance(md, dict):
-        for k in ("finalizers", "labels", "annotations", "ownerReferences"):
-            if k in md and not md[k]:
-                del md[k]
-    return obj
+    """The apiserver stores typed objects: what a patch empties vanishes (omitempty), and a
+    query sees the typed presence (ToJSONStandard): typed_json.to_json_standard."""
+    return to_json_standard(obj)
 
 
 def _canon(o) -> str:
