@@ -77,7 +77,7 @@ def node_range(n_nodes, rank, world, weak):
     return node_block(n_nodes, world, rank)
 
 
-def build_engines(node_lo, node_hi, pods_per_node, device, seed, job_frac, wide_state=False, mix="fast"):
+def build_engines(node_lo, node_hi, pods_per_node, device, seed, job_frac, wide_state=False, mix="fast", state="auto"):
     """Pod and node engines of one shard.  mix "fast": pod-fast (C1/C5 stage mix, 2-byte words);
     "general": pod-general + pod-chaos (C2 stage mix, 4-byte words)."""
     from kwok_amd import workload as W
@@ -98,6 +98,7 @@ def build_engines(node_lo, node_hi, pods_per_node, device, seed, job_frac, wide_
     ping = Ingest(pprog)
     phot, pdel, prec, pcls = ping.variant_columns(pvars, pidx)
     pods = Engine(pprog, capacity=pod_hi - pod_lo, device=device, slot_base=pod_lo, kind_salt=0, wide_state=wide_state,
+                  state=state,
                   max_records=max(1, len(ping.records)) + 16)
     pods.load_stages()
     pods.load(phot, pdel, prec, pcls, ping.record_array())
@@ -207,10 +208,12 @@ def sweep_bytes(s0, s1):
 
 def measure_hbm_working_set(args, device):
     """The C2 stage mix (pod-general + chaos: weighted picks, jitter, value records) at 100M
-    pods on one GPU: 4-byte words = 0.4 GB of state + 0.8 GB of due times, beyond the 256 MiB
+    pods on one GPU: 8-byte records of a packed word fused with its relative due time = 0.8 GB
+    (4-byte words + the 8-byte due column = 1.2 GB before round 3), beyond the 256 MiB
     Infinity Cache, so the roofline fraction is an HBM claim."""
     n_nodes = args.hbm_nodes
-    pods, nodes, _ = build_engines(0, n_nodes, args.pods_per_node, device, args.seed, args.job_frac, mix="general")
+    pods, nodes, _ = build_engines(0, n_nodes, args.pods_per_node, device, args.seed, args.job_frac, mix="general",
+                                   state=getattr(args, "hbm_state", "auto"))
     try:
         dt = 500 * 10**6
         steps, warm = args.hbm_steps, args.hbm_warmup
@@ -224,6 +227,8 @@ def measure_hbm_working_set(args, device):
         nodes.sync()
         wall = time.perf_counter() - t0
         s1 = pods.stats()
+        from kwok_amd.host import abi
+        fused = pods.last_sweep()["kernel"] == abi.SWEEP_WD
         n_ev = (steps + EV_EVERY - 1) // EV_EVERY
         sweep_ms = statistics.mean(pods.event_elapsed_ms(2 * i, 2 * i + 1) for i in range(n_ev))
         b, lb = sweep_bytes(s0, s1)
@@ -231,7 +236,8 @@ def measure_hbm_working_set(args, device):
         ach = b / steps / (us * 1e-6) / 1e9
         return {"workload": f"C2 stage mix at {n_nodes * args.pods_per_node:,} pods ({n_nodes:,} nodes): pod-general + "
                             "pod-chaos, harness churn, 0.5 s per step",
-                "kernel": ("sweepw_kernel<4-byte>" if s1["state_bytes"] == 4 else "sweepw_kernel<8-byte>") + " (pods)",
+                "kernel": {4: "sweepw_kernel<4-byte words, due column>", 8: "sweepw_kernel<8-byte fused records>"
+                           if fused else "sweepw_kernel<8-byte wide words, due column>"}[int(s1["state_bytes"])] + " (pods)",
                 "state_bytes_per_object": int(s1["state_bytes"]),
                 "state_column_GB": round(n_nodes * args.pods_per_node * int(s1["state_bytes"]) / 1e9, 3),
                 "transitions_per_s": round((s1["fired"] - s0["fired"]) / wall, 1),
@@ -457,6 +463,8 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child passes (traffic null)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000, help="nodes of the C2-mix HBM working-set run (0: off)")
+    ap.add_argument("--hbm-state", default="auto", choices=("auto", "u32", "wide"),
+                    help="pod state format of the C2-mix run (auto: the fused 8-byte records)")
     ap.add_argument("--hbm-steps", type=int, default=10)
     ap.add_argument("--hbm-only", action="store_true", help="diagnostic: only the C2-mix HBM working-set run")
     ap.add_argument("--hbm-warmup", type=int, default=12)

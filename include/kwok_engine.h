@@ -172,8 +172,8 @@ typedef struct {
   uint64_t fired;         /* stage transitions */
   uint64_t bytes;         /* algorithmic bytes moved by the sweep */
   uint64_t fired_per_stage[KWK_MAX_STAGES];
-  uint64_t state_bytes;   /* bytes per object of the device state stream: 1 (dictionary id), 2 or 4 (packed)
-                           * or 8 (wide) */
+  uint64_t state_bytes;   /* bytes per object of the device state stream: 1 (dictionary id), 2 or 4 (packed),
+                           * 8 (wide, or a packed word fused with its relative due time) */
   uint64_t line_bytes;    /* `bytes` with state writes counted as the whole 128-byte lines the 2-byte
                            * sweep stores (= bytes for the word-granular 4/8-byte sweeps) */
 } kwk_step_stats;
@@ -191,6 +191,8 @@ typedef struct {
 #define KWK_ENGINE_WIDE_STATE (1u << 0) /* always use the 8-byte state format (never a packed one) */
 #define KWK_ENGINE_STATE32 (1u << 1)    /* never the 2-byte packed format (4-byte packed or wide only) */
 #define KWK_ENGINE_STATE16 (1u << 2)    /* never the 1-byte dictionary format (2-byte words at most narrow) */
+#define KWK_ENGINE_SPLIT_DUE (1u << 3)  /* never the fused 8-byte record {packed word, relative due}: 4-byte
+                                         * words and the separate 8-byte due column */
 
 /* message of the last failing call on `eng` (kept per engine, so a caller that moves between OS
  * threads between the failing call and this one — a Go goroutine — still reads its own message);
@@ -218,6 +220,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
+#define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
+                                  (default 1: one workgroup per tile) */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
 
 /* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */
@@ -536,6 +540,7 @@ kwk_status kwk_event_elapsed(kwk_engine* eng, uint32_t a, uint32_t b, float* ms)
 #define KWK_SWEEP_W4 3       /* sweepw_kernel<4>: 4-byte packed words */
 #define KWK_SWEEP_W8 4       /* sweepw_kernel<8>: 8-byte wide words */
 #define KWK_SWEEP_8 5        /* sweep8_kernel: 1-byte dictionary ids, id transition table in LDS */
+#define KWK_SWEEP_WD 6       /* sweepw_kernel<8, fused>: 8-byte records {packed word, 36-bit relative due} */
 typedef struct {
   uint32_t kernel;       /* KWK_SWEEP_* */
   uint32_t q;            /* 16-byte chunks per lane */

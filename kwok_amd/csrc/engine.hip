@@ -166,10 +166,17 @@ __device__ __forceinline__ Getter eval_getter(int32_t slot, int64_t def, bool de
 // half   : the same packing in one u16 per slot when it fits 16 bits (narrow = half = 1).
 // byte   : one id byte per slot indexing a dictionary of the half words that can occur (a table-
 //          only program; narrow = half = byte = 1): id2w / w2id on the device.
+// fused  : one 8-byte record per slot, uint2 {x: packed word (bits 0..27) | due bits 32..35 at
+//          28..31, y: due bits 0..31} when the packed word fits 28 bits (narrow = dw = 1): the
+//          due time D relative to the engine's epoch rides with the word, so the word sweep reads
+//          one stream; D = kDwFar means "in the side column" (the due column, for due times outside
+//          [epoch, epoch + 2^36 - 1) ns, ~68.7 s; written and read only for those).
 struct StateFmt {
   uint32_t narrow;
   uint32_t half;
   uint32_t byte;
+  uint32_t dw;
+  int64_t epoch;         // dw: the due times' origin (ns)
   uint32_t pmask;
   uint32_t cshift, cmask;
   uint32_t sshift, smask, none_code;
@@ -193,17 +200,60 @@ __host__ __device__ __forceinline__ uint32_t fmt_pack(uint32_t pred, uint32_t sc
          (((sched >> 8) & 0x1Fu) << f.fshift);
 }
 
+// the fused record's relative due (StateFmt.dw)
+constexpr uint32_t kDwShift = 28;                     // due bits 32..35 sit at word bits 28..31
+constexpr uint32_t kDwWordMask = (1u << kDwShift) - 1u;
+constexpr uint64_t kDwFar = (1ull << 36) - 1ull;      // "the due time is in the side column"
+constexpr uint64_t kDwRebase = 1ull << 34;            // the epoch moves when now is this far past it
+__host__ __device__ __forceinline__ uint64_t dw_get(uint2 r) {
+  return ((uint64_t)(r.x >> kDwShift) << 32) | r.y;
+}
+__host__ __device__ __forceinline__ uint2 dw_put(uint2 r, uint64_t d) {
+  return make_uint2((r.x & kDwWordMask) | ((uint32_t)(d >> 32) << kDwShift), (uint32_t)d);
+}
+// D of an absolute due time (kDwFar: outside the window, the side column holds it)
+__host__ __device__ __forceinline__ uint64_t dw_enc(int64_t due, int64_t epoch) {
+  if (due < epoch) return kDwFar;
+  const uint64_t d = (uint64_t)due - (uint64_t)epoch;  // exact: due >= epoch
+  return d < kDwFar ? d : kDwFar;
+}
+__host__ __device__ __forceinline__ int64_t dw_abs(uint64_t d, int64_t epoch) {
+  return (int64_t)((uint64_t)epoch + d);
+}
+
 // small kernels (scatter / delete / usage / count) branch on the format at run time
 __device__ __forceinline__ uint2 load_state(const void* st, uint64_t i, const StateFmt& f) {
   if (f.byte) return fmt_unpack(f.id2w[reinterpret_cast<const uint8_t*>(st)[i]], f);
   if (f.half) return fmt_unpack(reinterpret_cast<const uint16_t*>(st)[i], f);
+  if (f.dw) return fmt_unpack(reinterpret_cast<const uint32_t*>(st)[2 * i], f);  // fmt_unpack ignores the due bits
   return f.narrow ? fmt_unpack(reinterpret_cast<const uint32_t*>(st)[i], f) : reinterpret_cast<const uint2*>(st)[i];
 }
+// the word only: a fused record keeps its due bits
 __device__ __forceinline__ void store_state(void* st, uint64_t i, uint2 v, const StateFmt& f) {
-  if (f.byte) reinterpret_cast<uint8_t*>(st)[i] = f.w2id[fmt_pack(v.x, v.y, f) & 0xFFFFu];
-  else if (f.half) reinterpret_cast<uint16_t*>(st)[i] = (uint16_t)fmt_pack(v.x, v.y, f);
-  else if (f.narrow) reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
-  else reinterpret_cast<uint2*>(st)[i] = v;
+  if (f.byte) {
+    reinterpret_cast<uint8_t*>(st)[i] = f.w2id[fmt_pack(v.x, v.y, f) & 0xFFFFu];
+  } else if (f.half) {
+    reinterpret_cast<uint16_t*>(st)[i] = (uint16_t)fmt_pack(v.x, v.y, f);
+  } else if (f.dw) {
+    uint32_t* p = reinterpret_cast<uint32_t*>(st) + 2 * i;
+    *p = (*p & ~kDwWordMask) | fmt_pack(v.x, v.y, f);
+  } else if (f.narrow) {
+    reinterpret_cast<uint32_t*>(st)[i] = fmt_pack(v.x, v.y, f);
+  } else {
+    reinterpret_cast<uint2*>(st)[i] = v;
+  }
+}
+// word and due time together (scatter, retry)
+__device__ __forceinline__ void store_state_due(void* st, int64_t* due_col, uint64_t i, uint2 v, int64_t due,
+                                                const StateFmt& f) {
+  if (f.dw) {
+    const uint64_t d = dw_enc(due, f.epoch);
+    reinterpret_cast<uint2*>(st)[i] = dw_put(make_uint2(fmt_pack(v.x, v.y, f), 0u), d);
+    if (d == kDwFar) due_col[i] = due;
+  } else {
+    store_state(st, i, v, f);
+    due_col[i] = due;
+  }
 }
 
 // the word sweep is specialised per format
@@ -249,6 +299,8 @@ struct SweepArgs {
   const uint32_t* __restrict__ fsm;  // 2-byte sweep: per-(due ready, word) transition entries (or null)
   const int64_t* __restrict__ fsm_due;
   uint32_t fsm_bits;
+  int64_t dw_epoch_old;          // fused format: the epoch the records hold (fmt.epoch: the one written)
+  uint32_t dw_rebase;            // fused format: the epoch moves this sweep (every pending record re-encoded)
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -446,8 +498,9 @@ __device__ __forceinline__ void fire_object(const SweepArgs& a, const kwk_stage_
 // caller writes it back); writes the due column itself when a newly scheduled stage stays
 // pending past this step (a stage that fires in the same step never needs its due stored).
 // kProbe: see match_object; the due time a scheduled stage would store goes to due_w (gen and
-// due_w are unused otherwise)
-template <bool kHarness, uint32_t kWordBytes, bool kProbe = false>
+// due_w are unused otherwise).  kDueOut (the fused format): the due time goes to due_w and gen = 1
+// instead of the due column (the caller encodes it into the record)
+template <bool kHarness, uint32_t kWordBytes, bool kProbe = false, bool kDueOut = false>
 __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_stage_table* __restrict__ T,
                                                const kwk_delta* __restrict__ deltas, uint32_t n_stages,
                                                uint32_t fin_group, uint64_t i, uint32_t pred, uint32_t sched,
@@ -485,9 +538,15 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
                                                    pred, sched, f);
   }
   if (scheduled && (sched & 0xFFu) < n_stages) {
-    if constexpr (kProbe) due_w = due;
-    else a.due[i] = due;
-    f.bytes += 8;
+    if constexpr (kProbe) {
+      due_w = due;
+    } else if constexpr (kDueOut) {
+      due_w = due;
+      gen = 1;
+    } else {
+      a.due[i] = due;
+    }
+    if constexpr (!kDueOut) f.bytes += 8;  // fused: part of the record write below
   }
   f.bytes += kWordBytes;  // the state write-back (done by the caller)
   return make_uint2(pred, sched);
@@ -1608,6 +1667,8 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
 //           (tile, wave) segment;
 //  phase 3  aligned 8-lane groups (one 128-byte line) holding a changed word are stored whole.
 constexpr int kQW = 4;                 // 16-byte chunks per lane: 16 (4-byte) / 8 (8-byte) words per lane
+constexpr int kQWD = 4;                // fused records: 8 per lane, 2048-object tiles (16 per lane: 129 VGPRs,
+                                       // 3 waves per SIMD, 630 vs 541 us at C2, r3p)
 constexpr int kLdsDeltasW = 128;       // (class, stage) deltas staged in LDS by the word sweep
 
 template <uint32_t kWB> struct WordOf { typedef uint32_t T; };
@@ -1620,39 +1681,50 @@ __device__ __forceinline__ uint32_t chunk_word(const uint4& c, int j, uint32_t*)
 __device__ __forceinline__ uint2 chunk_word(const uint4& c, int j, uint2*) {
   return j == 0 ? make_uint2(c.x, c.y) : make_uint2(c.z, c.w);
 }
-__device__ __forceinline__ uint32_t flag_word(uint32_t w) { return w; }  // word holding flags + stage
-__device__ __forceinline__ uint32_t flag_word(uint2 w) { return w.y; }
+template <bool kDW> __device__ __forceinline__ uint32_t flag_word(uint32_t w) { return w; }  // word holding flags + stage
+template <bool kDW> __device__ __forceinline__ uint32_t flag_word(uint2 w) { return kDW ? w.x : w.y; }
+__device__ __forceinline__ bool same_word(uint32_t a, uint32_t b) { return a == b; }
+__device__ __forceinline__ bool same_word(uint2 a, uint2 b) { return a.x == b.x && a.y == b.y; }
+__device__ __forceinline__ void set_chunk_word(uint4& c, int j, uint2 w) {
+  if (j == 0) { c.x = w.x; c.y = w.y; } else { c.z = w.x; c.w = w.y; }
+}
 __device__ __forceinline__ uint32_t pred_word(uint32_t w) { return w; }  // word holding pred
 __device__ __forceinline__ uint32_t pred_word(uint2 w) { return w.x; }
 
-template <bool kHarness, uint32_t kWB>
+template <bool kHarness, uint32_t kWB, bool kDW = false>
 __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
+  static_assert(!kDW || kWB == 8, "fused records are 8 bytes");
   typedef typename WordOf<kWB>::T W;
+  constexpr int kQ = kDW ? kQWD : kQW;     // 16-byte chunks per lane
   constexpr int kC = 16 / (int)kWB;        // words per chunk
-  constexpr int K = kC * kQW;              // words per lane
+  constexpr int K = kC * kQ;              // words per lane
   constexpr uint32_t kWave = 64u * K;      // words per wave region
   constexpr uint32_t kTile = kBlock * K;   // words per tile (one block)
   static_assert(kTile <= 8192, "fired records carry a 13-bit slot within the tile");
   __shared__ unsigned int s_stat[kStatWords];
   __shared__ kwk_delta s_delta[kLdsDeltasW];
   __shared__ uint16_t s_work[kTile];
-  __shared__ uint4 s_tile[kWavesPerBlock][64 * kQW];
+  __shared__ uint4 s_tile[kWavesPerBlock][64 * kQ];
   __shared__ uint32_t s_lut[kLutLdsW];
   __shared__ uint32_t s_cnt[kWavesPerBlock][2];
+  __shared__ uint32_t s_dirty[kWavesPerBlock];  // per wave region: bit l = its 128-byte line l changed
   __shared__ kwk_stage_table s_tab;
+  static_assert(kQ * 8 <= 32, "one dirty-line word per wave region");
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t tile = blockIdx.x;        // one block per tile
-  const uint32_t tbase = tile * kTile;
-  const uint32_t wbase = tbase + wave * kWave;
-  // the tile's stream is issued before the LDS set-up so its latency overlaps it
+  const uint32_t n_tiles = (a.n + kTile - 1u) / kTile;
+  uint32_t tile = blockIdx.x;  // tiles blockIdx.x, + gridDim.x, ... (one per block unless the grid is smaller)
   const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, ((a.n * kWB) + 15u) & ~15u);
-  uint4 cur[kQW];
+  uint4 cur[kQ];
+  auto load_tile = [&](uint32_t t) {
+    const uint32_t wb = t * kTile + wave * kWave;
 #pragma unroll
-  for (int q = 0; q < kQW; ++q) {
-    const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wbase + (uint32_t)q * 64u * kC + lane * kC) * kWB, 0, 0);
-    cur[q] = make_uint4(c[0], c[1], c[2], c[3]);
-  }
+    for (int q = 0; q < kQ; ++q) {
+      const auto c = __builtin_amdgcn_raw_buffer_load_b128(st_rs, (wb + (uint32_t)q * 64u * kC + lane * kC) * kWB, 0, 0);
+      cur[q] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  };
+  load_tile(tile);  // the first tile's stream is issued before the LDS set-up so its latency overlaps it
   {
     const uint32_t nw = (offsetof(kwk_stage_table, stages) + a.table->n_stages * sizeof(kwk_stage_desc)) / 4;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.table);
@@ -1677,8 +1749,15 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   const StateFmt fmt = a.fmt;
   const RawTest R = a.raw;
   uint32_t n_matched = 0, n_bytes = 0, n_line = 0;  // per lane
+  uint32_t wave_fired = 0;
   uint4* __restrict__ tq = s_tile[wave];
   W* __restrict__ tw = reinterpret_cast<W*>(&s_tile[0][0]);  // the whole tile: slot t = wave * kWave + offset
+  // LDS reuse across tiles needs no extra barrier: s_cnt / s_work of a tile are read before its
+  // second / third barrier, and each wave rewrites only its own tq rows and dirty word.  The next
+  // tile's stream is in flight (in `cur`, free once the tile is in LDS) while this one is worked.
+  for (; tile < n_tiles; tile += gridDim.x) {
+  const uint32_t tbase = tile * kTile;
+  const uint32_t wbase = tbase + wave * kWave;
   const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
   const uint64_t seg_id = (uint64_t)tile * kWavesPerBlock + wave;
   uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + seg_id * (kWave + 32u);
@@ -1686,13 +1765,13 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   uint32_t seg_n = 0;  // wave-uniform
 
   // ---- phase 1: bit k = q * kC + j of a lane's masks <-> word q * 64 * kC + lane * kC + j
-  uint32_t need = 0, heavy = 0, pend = 0, in_range = 0;
+  uint32_t need = 0, heavy = 0, pend = 0, in_range = 0, pend_all = 0;
 #pragma unroll
-  for (int q = 0; q < kQW; ++q) {
+  for (int q = 0; q < kQ; ++q) {
 #pragma unroll
     for (int j = 0; j < kC; ++j) {
       const W w = chunk_word(cur[q], j, (W*)nullptr);
-      const uint32_t fw = flag_word(w), pw = pred_word(w);
+      const uint32_t fw = flag_word<kDW>(w), pw = pred_word(w);
       const uint32_t off = (uint32_t)q * 64u * kC + lane * kC + (uint32_t)j;
       const uint32_t in = (full || wbase + off < a.n) ? 1u : 0u;
       const uint32_t mg = (fw & R.managed) ? in : 0u;
@@ -1703,22 +1782,73 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
       heavy |= (mg & nb) << k;
       pend |= (mg & pe) << k;
       in_range |= in << k;
+      if constexpr (kDW) pend_all |= (in & pe) << k;
     }
   }
   need = heavy;
   uint32_t ready = 0;
-  if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
-    const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+  if constexpr (kDW) {
+    // the due time rides in the record: D <= now - epoch, or the side column for D = kDwFar
+    if (__ballot(pend != 0)) {
+      const int64_t e0 = a.dw_epoch_old;
+      const bool now_ok = a.now >= e0;
+      const uint64_t thr = now_ok ? (uint64_t)a.now - (uint64_t)e0 : 0ull;
+      uint32_t far = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint32_t p = (pend >> k) & 1u;
-      const uint32_t off = (uint32_t)(k / kC) * 64u * kC + lane * kC + (uint32_t)(k % kC);
-      const int64_t d = buf_load_i64(due_rs, p ? (wbase + off) * 8u : kOOB);
-      ready |= (p & (uint32_t)(d <= a.now)) << k;
+      for (int k = 0; k < K; ++k) {
+        const uint64_t d = dw_get(chunk_word(cur[k / kC], k % kC, (W*)nullptr));
+        const uint32_t p = (pend >> k) & 1u;
+        ready |= (p & (uint32_t)(d != kDwFar && now_ok && d <= thr)) << k;
+        far |= (p & (uint32_t)(d == kDwFar)) << k;
+      }
+      if (__ballot(far != 0)) {  // cold: due times outside the window
+        const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint32_t f = (far >> k) & 1u;
+          const uint32_t off = (uint32_t)(k / kC) * 64u * kC + lane * kC + (uint32_t)(k % kC);
+          const int64_t d = buf_load_i64(due_rs, f ? (wbase + off) * 8u : kOOB);
+          ready |= (f & (uint32_t)(d <= a.now)) << k;
+        }
+        n_bytes += 8u * (uint32_t)__popc(far);
+      }
+      need |= ready;
     }
-    need |= ready;
+    if (a.dw_rebase && __ballot(pend_all != 0)) {
+      // cold (every ~17 s of simulated time): every queued stage's due time re-encoded against
+      // the new epoch; times leaving the window go to the side column
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+#pragma unroll
+        for (int j = 0; j < kC; ++j) {
+          const int k = q * kC + j;
+          if ((pend_all >> k) & 1u) {
+            const uint64_t i = (uint64_t)wbase + (uint32_t)q * 64u * kC + lane * kC + (uint32_t)j;
+            uint2 w = chunk_word(cur[q], j, (uint2*)nullptr);
+            const uint64_t d = dw_get(w);
+            const int64_t due = d != kDwFar ? dw_abs(d, a.dw_epoch_old) : a.due[i];
+            const uint64_t d2 = dw_enc(due, a.fmt.epoch);
+            if (d2 == kDwFar && d != kDwFar) a.due[i] = due;
+            set_chunk_word(cur[q], j, dw_put(w, d2));
+          }
+        }
+      }
+    }
+    n_bytes += kWB * (uint32_t)__popc(in_range);
+  } else {
+    if (__ballot(pend != 0)) {  // some object of the wave has a queued stage: is it due?
+      const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t p = (pend >> k) & 1u;
+        const uint32_t off = (uint32_t)(k / kC) * 64u * kC + lane * kC + (uint32_t)(k % kC);
+        const int64_t d = buf_load_i64(due_rs, p ? (wbase + off) * 8u : kOOB);
+        ready |= (p & (uint32_t)(d <= a.now)) << k;
+      }
+      need |= ready;
+    }
+    n_bytes += kWB * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
   }
-  n_bytes += kWB * (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
   // One work list per tile, sorted by kind: the fire-only items (a due stage, nothing to
   // match) of all four waves first, then the items that match (dirty / harness).  The waves
   // then take 64 consecutive items at a time: passes are full, and a pass runs the matcher
@@ -1740,9 +1870,11 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   if (lane == 0) {
     s_cnt[wave][0] = n_l;
     s_cnt[wave][1] = n_h;
+    s_dirty[wave] = 0u;
   }
 #pragma unroll
-  for (int q = 0; q < kQW; ++q) tq[q * 64 + lane] = cur[q];
+  for (int q = 0; q < kQ; ++q) tq[q * 64 + lane] = cur[q];
+  if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);  // block-uniform
   __syncthreads();
   uint32_t tot_l = 0, n_work = 0;  // block-uniform
 #pragma unroll
@@ -1772,31 +1904,47 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
         const uint32_t we = s_work[jw];
         off = we & 0x7FFFu;
         const uint64_t i = tbase + off;
-        const uint2 s = sw_decode(tw[off], fmt);
+        const W r = tw[off];
+        uint2 s;
+        if constexpr (kDW) s = fmt_unpack(r.x, fmt);
+        else s = sw_decode(r, fmt);
         // the queued stage's due time matters only as "due <= now" (a new match overwrites
         // it), which phase 1 already decided
         const int64_t due = (we >> 15) ? INT64_MIN : INT64_MAX;
-        uint32_t gen_unused = 0;
-        int64_t due_unused = 0;
-        const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,
-                                                       n_matched, lutp, lut_n, gen_unused, due_unused);
+        uint32_t due_set = 0;
+        int64_t due_w = 0;
+        const uint2 nv = process_object<kHarness, kWB, false, kDW>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due,
+                                                                   f, n_matched, lutp, lut_n, due_set, due_w);
         W out;
-        sw_encode(out, nv, fmt);
+        if constexpr (kDW) {  // the word, and D when a stage was scheduled (its due time leaves with the record)
+          out = make_uint2((r.x & ~kDwWordMask) | fmt_pack(nv.x, nv.y, fmt), r.y);
+          if (due_set) {
+            const uint64_t d = dw_enc(due_w, a.fmt.epoch);
+            out = dw_put(out, d);
+            if (d == kDwFar) a.due[i] = due_w;
+          }
+        } else {
+          sw_encode(out, nv, fmt);
+        }
         tw[off] = out;
+        if (!same_word(out, r)) atomicOr(&s_dirty[off / kWave], 1u << (((off % kWave) * kWB) >> 7));
         n_line -= kWB;  // the word's own write is replaced by the line stores below
       }
       n_bytes += f.bytes;
       emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);
     }
     __syncthreads();
+  }
+  const bool rebase = kDW && a.dw_rebase;  // block-uniform: every line is stored
+  if (n_work || rebase) {
     // ---- phase 3: whole 128-byte lines of the wave's region wherever a word changed
     uint4* __restrict__ gq = reinterpret_cast<uint4*>(a.st);
+    const uint32_t dirty = s_dirty[wave];
 #pragma unroll
-    for (int q = 0; q < kQW; ++q) {
+    for (int q = 0; q < kQ; ++q) {
       const uint4 nv = tq[q * 64 + lane];
-      const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
-      const unsigned long long bal = __ballot(ch);
-      if ((bal >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull)) {
+      // lane's chunk lies in line q * 8 + lane / 8 of the wave region (8 lanes x 16 B per line)
+      if (rebase || ((dirty >> (q * 8 + (lane >> 3))) & 1u)) {
         store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);
         n_line += 16u;
       }
@@ -1812,6 +1960,8 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
     n_line += 4u * (uint32_t)__popc((uint32_t)(lane < end - used));
   }
   n_bytes += lane == 0 ? 4u : 0u;  // the fired count word
+  wave_fired += seg_n;
+  }
 
   for (int o = 32; o > 0; o >>= 1) {
     n_matched += __shfl_xor(n_matched, o);
@@ -1820,7 +1970,7 @@ __global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
   }
   if (lane == 0) {
     atomicAdd(&s_stat[0], n_matched);
-    atomicAdd(&s_stat[1], seg_n);
+    atomicAdd(&s_stat[1], wave_fired);
     atomicAdd(&s_stat[2], n_bytes);
     atomicAdd(&s_stat[kStatLine], n_bytes + n_line);
   }
@@ -2027,8 +2177,7 @@ __global__ void scatter_kernel(ScatterArgs a) {
   kwk_hot h = a.s_hot[j];
   h.sched = (h.sched & ~KWK_CLASS_MASK) | ((uint32_t)a.s_cls[j] << KWK_CLASS_SHIFT);
   if (a.mark_dirty) h.sched |= KWK_F_DIRTY;
-  store_state(a.st, i, make_uint2(h.pred, h.sched), a.fmt);
-  a.due[i] = h.due;
+  store_state_due(a.st, a.due, i, make_uint2(h.pred, h.sched), h.due, a.fmt);
   a.del_s[i] = a.s_del[j];
   a.rec_idx[i] = a.s_rec[j];
 }
@@ -2101,8 +2250,8 @@ __global__ void retry_kernel(RetryArgs a) {
   // the unchanged object, its job queued again (no event: not dirty)
   const uint32_t sched = (a.hot[j].sched & ~(KWK_CLASS_MASK | 0xFFu | KWK_F_DIRTY)) |
                          ((uint32_t)a.cls[j] << KWK_CLASS_SHIFT) | (uint32_t)a.stages[j];
-  store_state(a.st, i, make_uint2(a.hot[j].pred, sched), a.fmt);
-  a.due[i] = sat_add(a.now, delay);  // addStageJob -> AddWeightAfter(job, 1, retryDelay)
+  // addStageJob -> AddWeightAfter(job, 1, retryDelay)
+  store_state_due(a.st, a.due, i, make_uint2(a.hot[j].pred, sched), sat_add(a.now, delay), a.fmt);
 }
 
 __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uint32_t n) {
@@ -2112,6 +2261,25 @@ __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uin
   uint2 v = load_state(st, i, fmt);
   v.y = (v.y & ~(KWK_F_ALIVE | KWK_F_DIRTY | 0xFFu)) | KWK_STAGE_NONE;
   store_state(st, i, v, fmt);
+}
+
+// the fused format's due times <-> the due column.  fold: every record's D from the column
+// (kDwFar where the time is outside the window: the column already holds it); unfold: the column
+// from every record whose D is in the window (the column is then exact for every slot)
+__global__ void dw_fold_kernel(uint2* __restrict__ st, const int64_t* __restrict__ due, uint32_t first, uint32_t n,
+                               int64_t epoch) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = first + j;
+  st[i] = dw_put(st[i], dw_enc(due[i], epoch));
+}
+__global__ void dw_unfold_kernel(const uint2* __restrict__ st, int64_t* __restrict__ due, uint32_t first, uint32_t n,
+                                 int64_t epoch) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = first + j;
+  const uint64_t d = dw_get(st[i]);
+  if (d != kDwFar) due[i] = dw_abs(d, epoch);
 }
 
 // ------------------------------------------------------------------ resource usage
@@ -2183,7 +2351,7 @@ __device__ __forceinline__ double dur_seconds(int64_t d) {
 
 // alive flag of pod j of a lane's run (kURun words of WB bytes in WB 16-byte chunks)
 template <uint32_t WB>
-__device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t abit) {
+__device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t abit, bool px) {
   if constexpr (WB == 1) {  // 1-byte ids: the alive bit is an id bit (kIdAlive)
     const uint4 c = sv[0];
     const int d = j >> 2;
@@ -2200,7 +2368,8 @@ __device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t
     return ((d == 0 ? c.x : d == 1 ? c.y : d == 2 ? c.z : c.w) & abit) != 0;
   } else {
     const uint4 c = sv[j >> 1];
-    return (((j & 1) ? c.w : c.y) & abit) != 0;  // the sched word of {pred, sched}
+    // the sched word of {pred, sched}; px: the packed word of a fused record
+    return ((px ? ((j & 1) ? c.z : c.x) : ((j & 1) ? c.w : c.y)) & abit) != 0;
   }
 }
 
@@ -2275,7 +2444,8 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
   const double* __restrict__ cpu_v = lds_vals ? s_val : a.cpu_v;
   const double* __restrict__ mem_v = lds_vals ? s_val + a.n_cpu : a.mem_v;
   // the alive flag in the raw word (packed: at fshift; wide: in sched)
-  const uint32_t abit = WB == 1 ? kIdAlive : WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  const uint32_t abit = WB == 1 ? kIdAlive : (WB == 8 && !a.fmt.dw) ? (uint32_t)KWK_F_ALIVE
+                                                                   : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
   double tot_c = 0.0, tot_m = 0.0;  // per lane: the nodes it finalised
   uint32_t* __restrict__ sp = s_ptr[wave];
   double2* __restrict__ ss = s_sum[wave];
@@ -2349,7 +2519,7 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
         while (p >= bnd) close();
         const uint4 kq = kv[j >> 2];
         const uint32_t key = (j & 3) == 0 ? kq.x : (j & 3) == 1 ? kq.y : (j & 3) == 2 ? kq.z : kq.w;
-        const bool alive = run_alive<WB>(sv, j, abit);
+        const bool alive = run_alive<WB>(sv, j, abit, a.fmt.dw != 0);
         const uint32_t nc = key >> 28;
         double vc = 0.0, vm = 0.0, c1v = 0.0, m1v = 0.0;
         uint2 fc = make_uint2(0u, 0u);
@@ -2531,7 +2701,8 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   }
   __syncthreads();
   const uint32_t nv = a.n_cpu + a.n_mem;  // podv row: cpu values then memory values
-  const uint32_t abit = WB == 1 ? kIdAlive : WB == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
+  const uint32_t abit = WB == 1 ? kIdAlive : (WB == 8 && !a.fmt.dw) ? (uint32_t)KWK_F_ALIVE
+                                                                   : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
   double tot_c = 0.0, tot_m = 0.0;
   uint32_t* __restrict__ sp = s_ptr[wave];
   double2* __restrict__ ss = s_sum[wave];
@@ -2601,7 +2772,7 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
           do { ++k; } while (sp[k + 1] <= p);  // past nodes without pods
           bnd = sp[k + 1];
         }
-        const bool live = in && run_alive<WB>(sv, j, abit);
+        const bool live = in && run_alive<WB>(sv, j, abit, a.fmt.dw != 0);
         double vc, vm;
         if constexpr (kKey8) {
           const uint4 kq = kv[0];
@@ -2913,7 +3084,7 @@ constexpr int kMaxCountMasks = 16;
 template <uint32_t WB, int NM>  // NM >= n_masks masks tested (compile time); the rest count nothing used
 __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, uint32_t n, uint32_t abit,
                                                        uint32_t pmask, const uint32_t* __restrict__ masks,
-                                                       uint32_t n_masks, uint32_t* __restrict__ part) {
+                                                       uint32_t n_masks, uint32_t* __restrict__ part, uint32_t px) {
   __shared__ unsigned int s_cnt[NM];
   if (threadIdx.x < NM) s_cnt[threadIdx.x] = 0;
   uint32_t cnt[NM];
@@ -2967,8 +3138,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 4; ++j) tally(dw[j], dw[j], (uint32_t)j < lim);
     } else {
-      tally(v.x, v.y, true);
-      tally(v.z, v.w, lim > 1);
+      tally(v.x, px ? v.x : v.y, true);  // px: flags in the packed word of a fused record
+      tally(v.z, px ? v.z : v.w, lim > 1);
     }
   };
   // kCountU chunks per lane in flight together, kBlock chunks apart (coalesced)
@@ -3164,13 +3335,14 @@ static void launch_count8(uint32_t n_masks, dim3 g, hipStream_t s, const void* s
 
 template <uint32_t WB>
 static void launch_count(uint32_t n_masks, dim3 g, hipStream_t s, const void* st, uint32_t n, uint32_t abit,
-                         uint32_t pmask, const uint32_t* masks, uint32_t* part, unsigned long long* out) {
+                         uint32_t pmask, const uint32_t* masks, uint32_t* part, unsigned long long* out,
+                         uint32_t px = 0) {
   if (WB == 2 && n_masks <= 4 && pmask < (1u << (kCountLutBits - 1)) && abit > pmask)
     hipLaunchKernelGGL(count16_lut_kernel, g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
-  else if (n_masks <= 2) hipLaunchKernelGGL((count_kernel<WB, 2>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
-  else if (n_masks <= 4) hipLaunchKernelGGL((count_kernel<WB, 4>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
-  else if (n_masks <= 8) hipLaunchKernelGGL((count_kernel<WB, 8>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
-  else hipLaunchKernelGGL((count_kernel<WB, 16>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part);
+  else if (n_masks <= 2) hipLaunchKernelGGL((count_kernel<WB, 2>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
+  else if (n_masks <= 4) hipLaunchKernelGGL((count_kernel<WB, 4>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
+  else if (n_masks <= 8) hipLaunchKernelGGL((count_kernel<WB, 8>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
+  else hipLaunchKernelGGL((count_kernel<WB, 16>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
   hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
 }
 
@@ -3404,6 +3576,8 @@ struct kwk_engine {
   uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_FSM_KERNEL: 0 never, else its prefetch depth
   // the 1-byte format (StateFmt.byte): a dictionary of the half words that can occur
   bool allow_byte = true;     // KWK_ENGINE_STATE16 clears it
+  bool allow_dw = true;       // KWK_ENGINE_SPLIT_DUE clears it: never the fused record
+  uint32_t word_tpb = 1;      // KWK_TUNE_WORD_TILES: tiles per workgroup of the word sweep
   bool byte_tune = true;      // KWK_TUNE_BYTE_STATE
   bool byte_ok = false;       // the transition table exists for the loaded program and harness
   std::vector<uint32_t> h_fsm;    // host copy of the 2-byte transition table (closure, id table)
@@ -3527,9 +3701,10 @@ static std::mutex g_live_mu;
 static std::set<kwk_engine*> g_live;
 
 
-// narrow iff pred + class + stage code + 5 flag bits fit 32 bits, half iff they fit 16
-// 
-static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stages, bool allow_narrow, bool allow_half) {
+// narrow iff pred + class + stage code + 5 flag bits fit 32 bits, half iff they fit 16, fused
+// (dw) iff they fit 28 and not 16
+static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stages, bool allow_narrow, bool allow_half,
+                         bool allow_dw) {
   auto bitlen = [](uint32_t x) {
     uint32_t b = 0;
     while (x) { ++b; x >>= 1; }
@@ -3542,6 +3717,7 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
   if (!allow_narrow || pb + cb + sb + 5 > 32) return f;
   f.narrow = 1;
   f.half = (allow_half && pb + cb + sb + 5 <= 16) ? 1u : 0u;
+  f.dw = (allow_dw && !f.half && pb + cb + sb + 5 <= kDwShift) ? 1u : 0u;
   f.pmask = (1u << pb) - 1u;
   f.cshift = pb;
   f.cmask = cb ? ((1u << cb) - 1u) : 0u;
@@ -3554,9 +3730,14 @@ static StateFmt make_fmt(uint32_t pred_bits, uint32_t n_classes, uint32_t n_stag
 
 static kwk_status build_fsm(kwk_engine* e);
 
-static size_t word_bytes(const StateFmt& f) { return f.byte ? 1 : f.half ? 2 : f.narrow ? 4 : 8; }
+static size_t word_bytes(const StateFmt& f) { return f.byte ? 1 : f.half ? 2 : f.dw ? 8 : f.narrow ? 4 : 8; }
 
-static bool same_fmt(const StateFmt& a, const StateFmt& b) { return memcmp(&a, &b, sizeof(StateFmt)) == 0; }
+// the layout only (the fused format's epoch moves with time)
+static bool same_fmt(const StateFmt& a, const StateFmt& b) {
+  StateFmt x = a, y = b;
+  x.epoch = y.epoch = 0;
+  return memcmp(&x, &y, sizeof(StateFmt)) == 0;
+}
 
 // host-side conversion of device state words <-> (pred, sched); the 1-byte format through the
 // engine's dictionary
@@ -3567,6 +3748,9 @@ static std::vector<uint2> unpack_words(const kwk_engine* e, const std::vector<ui
   } else if (f.half) {
     const uint16_t* w = reinterpret_cast<const uint16_t*>(raw.data());
     for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
+  } else if (f.dw) {  // the word of each record (due times: dw_unfold + the due column)
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(raw.data());
+    for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[2 * (size_t)i], f);
   } else if (f.narrow) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(raw.data());
     for (uint32_t i = 0; i < n; ++i) out[i] = fmt_unpack(w[i], f);
@@ -3583,6 +3767,9 @@ static std::vector<uint8_t> pack_words(const kwk_engine* e, const std::vector<ui
   } else if (f.half) {
     uint16_t* w = reinterpret_cast<uint16_t*>(raw.data());
     for (size_t i = 0; i < v.size(); ++i) w[i] = (uint16_t)fmt_pack(v[i].x, v[i].y, f);
+  } else if (f.dw) {  // records with D = 0 (dw_fold sets it from the due column)
+    uint32_t* w = reinterpret_cast<uint32_t*>(raw.data());
+    for (size_t i = 0; i < v.size(); ++i) w[2 * i] = fmt_pack(v[i].x, v[i].y, f);
   } else if (f.narrow) {
     uint32_t* w = reinterpret_cast<uint32_t*>(raw.data());
     for (size_t i = 0; i < v.size(); ++i) w[i] = fmt_pack(v[i].x, v[i].y, f);
@@ -3749,9 +3936,26 @@ static kwk_status dict_upload(kwk_engine* e) {
   return KWK_OK;
 }
 
-// resident rows [0, n_active) as (pred, sched) (synchronises)
+// the fused format: records' D from the due column / the due column made exact (stream-ordered)
+static kwk_status dw_fold(kwk_engine* e, uint32_t first, uint32_t n) {
+  if (!e->fmt.dw || n == 0) return KWK_OK;
+  hipLaunchKernelGGL(dw_fold_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
+                     reinterpret_cast<uint2*>(e->d_st), e->d_due, first, n, e->fmt.epoch);
+  HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+static kwk_status dw_unfold(kwk_engine* e, uint32_t first, uint32_t n) {
+  if (!e->fmt.dw || n == 0) return KWK_OK;
+  hipLaunchKernelGGL(dw_unfold_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
+                     reinterpret_cast<const uint2*>(e->d_st), e->d_due, first, n, e->fmt.epoch);
+  HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
+// resident rows [0, n_active) as (pred, sched) (synchronises; the due column is left exact)
 static kwk_status read_rows(kwk_engine* e, std::vector<uint2>& rows) {
   const uint32_t n = e->n_active;
+  if (kwk_status st = dw_unfold(e, 0, n)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
   std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
   if (n) HIP_TRY(hipMemcpy(raw.data(), e->d_st, raw.size(), hipMemcpyDeviceToHost));
@@ -3764,7 +3968,7 @@ static kwk_status write_rows(kwk_engine* e, const std::vector<uint2>& rows, cons
   const std::vector<uint8_t> out = pack_words(e, rows, nf);
   if (!out.empty()) HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
   e->fmt = nf;
-  return KWK_OK;
+  return dw_fold(e, 0, (uint32_t)rows.size());
 }
 
 // the format without the dictionary (2-byte words when the program fits 16 bits)
@@ -3860,6 +4064,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   e->force_wide = (d->flags & KWK_ENGINE_WIDE_STATE) != 0;
   e->allow_half = (d->flags & KWK_ENGINE_STATE32) == 0;
   e->allow_byte = (d->flags & (KWK_ENGINE_STATE32 | KWK_ENGINE_STATE16 | KWK_ENGINE_WIDE_STATE)) == 0;
+  e->allow_dw = (d->flags & KWK_ENGINE_SPLIT_DUE) == 0;
   kwk_status st = set_dev(e);
   if (st) { delete e; return st; }
   if (hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || e->n_cus <= 0)
@@ -3963,10 +4168,13 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
   if (t->pred_bits > 32) return fail(KWK_EINVAL, "pred_bits > 32");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  const StateFmt nf = make_fmt(t->pred_bits, t->n_classes, t->n_stages, !e->force_wide, e->allow_half);
+  StateFmt nf = make_fmt(t->pred_bits, t->n_classes, t->n_stages, !e->force_wide, e->allow_half, e->allow_dw);
+  nf.epoch = e->fmt.epoch;
   if (!same_fmt(nf, e->fmt)) {
     if (e->n_active) {  // repack the resident objects into the new format
       const uint32_t n = e->n_active;
+      if (kwk_status st = dw_unfold(e, 0, n)) return st;  // the due column exact before leaving the fused format
+      HIP_TRY(hipStreamSynchronize(e->stream));
       std::vector<uint8_t> raw(word_bytes(e->fmt) * (size_t)n);
       HIP_TRY(hipMemcpy(raw.data(), e->d_st, raw.size(), hipMemcpyDeviceToHost));
       std::vector<uint2> v = unpack_words(e, raw, e->fmt, n);
@@ -3975,6 +4183,8 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
           return fail(KWK_EINVAL, "resident object " + std::to_string(i) + " does not fit the new stage table");
       std::vector<uint8_t> out = pack_words(e, v, nf);
       HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
+      e->fmt = nf;
+      if (kwk_status st = dw_fold(e, 0, n)) return st;
     }
     e->fmt = nf;
   }
@@ -4073,6 +4283,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
       e->usage_blocks = value;
       return KWK_OK;
+    case KWK_TUNE_WORD_TILES:
+      if (value < 1 || value > 16) return fail(KWK_EINVAL, "KWK_TUNE_WORD_TILES: 1..16");
+      e->word_tpb = value;
+      return KWK_OK;
     case KWK_TUNE_COMPACT_SMALL:
       // each block of the one-launch compaction re-sums every count before its segments: the
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
@@ -4128,6 +4342,7 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
     const std::vector<uint8_t> raw = pack_words(e, st, e->fmt);
     HIP_TRY(hipMemcpy(e->d_st, raw.data(), raw.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    if (kwk_status s2 = dw_fold(e, 0, n)) return s2;
   }
   HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_rec, rec, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
@@ -4326,6 +4541,8 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
   a.fsm = nullptr;
   a.fsm_due = nullptr;
   a.fsm_bits = 0;
+  a.dw_epoch_old = e->fmt.epoch;
+  a.dw_rebase = 0;
   return a;
 }
 
@@ -4474,24 +4691,39 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     return KWK_OK;
   }
   // 4- / 8-byte words: whole-line write-back word sweep, one block per tile
-  const uint32_t K = (uint32_t)kQW * (nar ? 4u : 2u);
+  const bool dw = e->fmt.dw != 0;
+  const uint32_t K = dw ? (uint32_t)kQWD * 2u : (uint32_t)kQW * (nar ? 4u : 2u);
   const uint32_t tile = kBlock * K;
-  const uint32_t blocks = (e->n_active + tile - 1) / tile;
-  if (nar) {
+  const uint32_t tiles = (e->n_active + tile - 1) / tile;
+  const uint32_t tpb = e->word_tpb;  // tiles per block
+  const uint32_t blocks = (tiles + tpb - 1) / tpb;
+  if (dw) {
+    // the fused records' epoch follows the clock: re-encoded (inside this sweep) once now is
+    // more than 2^34 ns (~17 s) past it or before it, so that due times up to ~51 s ahead of now
+    // stay in the 2^36 ns window
+    const int64_t e0 = e->fmt.epoch;
+    if (now_ns < e0 || (uint64_t)now_ns - (uint64_t)e0 > kDwRebase) {
+      e->fmt.epoch = now_ns;
+      a.fmt.epoch = now_ns;
+      a.dw_rebase = 1;
+    }
+    if (h) hipLaunchKernelGGL((sweepw_kernel<true, 8, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    else hipLaunchKernelGGL((sweepw_kernel<false, 8, true>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
+  } else if (nar) {
     if (h) hipLaunchKernelGGL((sweepw_kernel<true, 4>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
     else hipLaunchKernelGGL((sweepw_kernel<false, 4>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   } else {
     if (h) hipLaunchKernelGGL((sweepw_kernel<true, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
     else hipLaunchKernelGGL((sweepw_kernel<false, 8>), dim3(blocks), dim3(kBlock), 0, e->stream, a);
   }
-  e->last_sweep = kwk_sweep_info{nar ? (uint32_t)KWK_SWEEP_W4 : (uint32_t)KWK_SWEEP_W8, (uint32_t)kQW, 0, 1, blocks, blocks,
-                                 h ? 1u : 0u, 0};
+  e->last_sweep = kwk_sweep_info{dw ? (uint32_t)KWK_SWEEP_WD : nar ? (uint32_t)KWK_SWEEP_W4 : (uint32_t)KWK_SWEEP_W8,
+                                 (uint32_t)(dw ? kQWD : kQW), blocks < tiles ? 1u : 0u, 1, blocks, tiles, h ? 1u : 0u, 0};
   e->last_objs = K;
   e->last_region_shift = 2;  // log2(kWavesPerBlock): records carry tile-relative slots
   e->last_rec = kRecSlot;
   static_assert(kWavesPerBlock == 4, "region shift");
   HIP_TRY(hipGetLastError());
-  e->last_blocks = blocks;
+  e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
   e->last_grid = blocks;
   e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
   ++e->steps;
@@ -4658,6 +4890,13 @@ kwk_status kwk_read(kwk_engine* e, uint32_t first, uint32_t n, kwk_hot* hot, int
     HIP_TRY(hipMemcpy(raw.data(), (const char*)e->d_st + word_bytes(e->fmt) * first, raw.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(due.data(), e->d_due + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
     const std::vector<uint2> st = unpack_words(e, raw, e->fmt, n);
+    if (e->fmt.dw) {  // D in the window, else the due column's value
+      const uint2* r = reinterpret_cast<const uint2*>(raw.data());
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t d = dw_get(r[i]);
+        if (d != kDwFar) due[i] = dw_abs(d, e->fmt.epoch);
+      }
+    }
     for (uint32_t i = 0; i < n; ++i) hot[i] = kwk_hot{st[i].x, st[i].y, due[i]};
   }
   if (del) HIP_TRY(hipMemcpy(del, e->d_del + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
@@ -5288,14 +5527,16 @@ kwk_status kwk_count(kwk_engine* e, uint32_t n_masks, const uint32_t* masks, uin
     uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);  // 4 chunks per lane, loaded together
     blocks = blocks < (uint64_t)e->n_cus * 8u ? blocks : (uint64_t)e->n_cus * 8u;
     // the alive flag and the pred bits in the raw word (packed: flags at fshift; wide: {pred, sched})
-    const uint32_t abit = wb == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
-    const uint32_t pmask = wb == 8 ? 0xFFFFFFFFu : e->fmt.pmask;
+    const bool wide = wb == 8 && !e->fmt.dw;
+    const uint32_t abit = wide ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
+    const uint32_t pmask = wide ? 0xFFFFFFFFu : e->fmt.pmask;
     const dim3 g((uint32_t)blocks);
     if (kwk_status st = ensure_count_part(e)) return st;
     if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, d_masks, e->d_count_part, d_out);
     else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
     else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
-    else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out);
+    else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, d_masks, e->d_count_part, d_out,
+                         e->fmt.dw);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(counts, d_out, 8 * (size_t)n_masks, hipMemcpyDeviceToHost, e->stream));
@@ -5335,15 +5576,17 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
       const uint64_t chunks = ((uint64_t)e->n_active * wb + 15u) / 16u;
       uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);
       blocks = blocks < (uint64_t)e->n_cus * 8u ? blocks : (uint64_t)e->n_cus * 8u;
-      const uint32_t abit = wb == 8 ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
-      const uint32_t pmask = wb == 8 ? 0xFFFFFFFFu : e->fmt.pmask;
+      const bool wide = wb == 8 && !e->fmt.dw;
+      const uint32_t abit = wide ? (uint32_t)KWK_F_ALIVE : (uint32_t)(KWK_F_ALIVE >> 8) << e->fmt.fshift;
+      const uint32_t pmask = wide ? 0xFFFFFFFFu : e->fmt.pmask;
       const dim3 g((uint32_t)blocks);
       if (kwk_status st = ensure_count_part(e)) return st;
       uint32_t* pp = e->d_count_part;
       if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, e->d_agg_masks, pp, e->d_agg_counts);
       else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
       else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
-      else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
+      else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts,
+                           e->fmt.dw);
       HIP_TRY(hipGetLastError());
     }
   }

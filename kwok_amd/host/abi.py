@@ -79,7 +79,7 @@ class SweepInfo(C.Structure):
     _fields_ = [(k, C.c_uint32) for k in ("kernel", "q", "persistent", "depth", "grid", "tiles", "harness", "reserved")]
 
 
-SWEEP_16, SWEEP_16_FSM, SWEEP_W4, SWEEP_W8, SWEEP_8 = 1, 2, 3, 4, 5  # KWK_SWEEP_*
+SWEEP_16, SWEEP_16_FSM, SWEEP_W4, SWEEP_W8, SWEEP_8, SWEEP_WD = 1, 2, 3, 4, 5, 6  # KWK_SWEEP_*
 
 
 class EngineDesc(C.Structure):
@@ -91,9 +91,11 @@ class EngineDesc(C.Structure):
 ENGINE_WIDE_STATE = 1
 ENGINE_STATE32 = 2
 ENGINE_STATE16 = 4   # never the 1-byte dictionary format
+ENGINE_SPLIT_DUE = 8  # never the fused 8-byte record {packed word, relative due}
 TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_USAGE_BLOCKS, TUNE_FSM_KERNEL, TUNE_USAGE_KEY8, TUNE_SWEEP_BLOCKS = 1, 2, 3, 4, 5, 6, 7
 TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
+TUNE_WORD_TILES = 10
 
 
 class Lease(C.Structure):

@@ -138,14 +138,17 @@ class Engine:
     def __init__(self, program: KindProgram, capacity: int, device: int = 0, slot_base: int = 0, kind_salt: int = 0,
                  max_records: int = 1 << 16, wide_state: bool = False, state: str = "auto"):
         """state: "auto" (the narrowest format: 1-byte dictionary ids for table-only programs
-        whose words close within 255 ids, else the packed 2 or 4 bytes the stage table fits, else
-        8), "u16" (never the 1-byte ids), "u32" (never fewer than 4 bytes) or "wide" (always 8
-        bytes; = wide_state)."""
+        whose words close within 255 ids, else the packed 2 bytes the stage table fits, else the
+        8-byte record of a packed word fused with its relative due time when the word fits 28
+        bits, else 4-byte words, else 8), "u16" (never the 1-byte ids), "dw" (never fewer than 4
+        bytes: the fused record when it fits), "u32" (4-byte packed words and the separate due
+        column) or "wide" (always 8 bytes; = wide_state)."""
         self.p = program
         L = abi.lib()
         if wide_state:
             state = "wide"
-        flags = {"auto": 0, "u16": abi.ENGINE_STATE16, "u32": abi.ENGINE_STATE32, "wide": abi.ENGINE_WIDE_STATE}[state]
+        flags = {"auto": 0, "u16": abi.ENGINE_STATE16, "dw": abi.ENGINE_STATE32,
+                 "u32": abi.ENGINE_STATE32 | abi.ENGINE_SPLIT_DUE, "wide": abi.ENGINE_WIDE_STATE}[state]
         d = abi.EngineDesc(device=device, capacity=capacity, value_slots=max(1, len(program.slots)),
                            max_records=max_records, slot_base=slot_base, kind_salt=kind_salt, flags=flags)
         h = C.c_void_p()

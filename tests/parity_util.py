@@ -17,7 +17,8 @@ NOW0 = 1_700_000_000 * 10**9
 def expected_state_bytes(prog, state="auto"):
     """Mirror of make_fmt (engine.hip): packed word = pred | class | stage code | 5 flags; the set
     of sizes the engine may pick ("auto" on a 16-bit program: the 1-byte dictionary ids when the
-    program is table-only and its words close within 255 ids, else the 2-byte words)."""
+    program is table-only and its words close within 255 ids, else the 2-byte words; a word of
+    at most 28 bits not held in 2 bytes: the 8-byte fused record unless "u32")."""
     if state == "wide":
         return {8}
     t = prog.table()
@@ -27,6 +28,8 @@ def expected_state_bytes(prog, state="auto"):
         return {1, 2}
     if bits <= 16 and state == "u16":
         return {2}
+    if bits <= 28 and state != "u32":
+        return {8}
     return {4} if bits <= 32 else {8}
 
 
@@ -87,8 +90,9 @@ def compare_state(prog, eng, sim, step, rows=None):
 
 
 def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False,
-        state="auto", tuning=None, expect_kernel=None):
-    """expect_kernel: the abi.SWEEP_* every step must launch (the shape under test)."""
+        state="auto", tuning=None, expect_kernel=None, nows=None):
+    """expect_kernel: the abi.SWEEP_* every step must launch (the shape under test); nows: the
+    clock of each step (default NOW0 + k * dt_ns)."""
     if wide_state:
         state = "wide"
     prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state, tuning=tuning)
@@ -96,7 +100,7 @@ def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0
     per_stage = np.zeros(len(prog.names), dtype=np.int64)
     try:
         for k in range(steps):
-            now = NOW0 + k * dt_ns
+            now = NOW0 + k * dt_ns if nows is None else nows[k]
             eng.step(now, seed, k)
             if expect_kernel is not None:
                 assert eng.last_sweep()["kernel"] == expect_kernel, (k, eng.last_sweep())

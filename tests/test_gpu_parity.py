@@ -13,7 +13,7 @@ from tests.parity_util import run
 pytestmark = pytest.mark.gpu
 
 
-FORMATS = ["auto", "u16", "u32", "wide"]
+FORMATS = ["auto", "u16", "u32", "dw", "wide"]
 
 
 @pytest.mark.parametrize("state", FORMATS + ["auto-nofsm", "auto-gen", "auto-pair", "u16-pair"])
@@ -22,9 +22,11 @@ def test_pod_fast_c1_mini(state):
     device state format: auto = the 1-byte dictionary ids of sweep8_kernel (pod-fast is
     table-only), u16 = the 2-byte words (the table-only sweep16_fsm_kernel), the general
     sweep16_kernel with its transition table (auto-gen: leaves the 1-byte format) and without it
-    (auto-nofsm); *-pair hand the fired list back through the scan + expansion pair of large
-    sweeps (KWK_TUNE_COMPACT_SMALL 0) instead of the one-launch compaction."""
-    tuning, kernel = {}, {"auto": abi.SWEEP_8, "u16": abi.SWEEP_16_FSM, "u32": abi.SWEEP_W4, "wide": abi.SWEEP_W8}.get(state)
+    (auto-nofsm); dw = the 8-byte records of a packed word fused with its relative due time;
+    *-pair hand the fired list back through the scan + expansion pair of large sweeps
+    (KWK_TUNE_COMPACT_SMALL 0) instead of the one-launch compaction."""
+    tuning, kernel = {}, {"auto": abi.SWEEP_8, "u16": abi.SWEEP_16_FSM, "u32": abi.SWEEP_W4, "dw": abi.SWEEP_WD,
+                          "wide": abi.SWEEP_W8}.get(state)
     if state == "auto-nofsm":
         tuning, kernel, state = {abi.TUNE_FSM: 0}, abi.SWEEP_16, "auto"
     elif state == "auto-gen":
@@ -40,19 +42,42 @@ def test_pod_fast_c1_mini(state):
     assert per["pod-ready"] >= 400 and per["pod-complete"] > 0 and per["pod-delete"] > 0
 
 
-@pytest.mark.parametrize("wide", [False, True], ids=["packed-state", "wide-state"])
-def test_pod_general_c2_mini(wide):
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_pod_general_c2_mini(state):
     """C2 shape: pod-general + chaos, init containers, override annotations (valid and
     invalid ints / durations / RFC3339), chaos labels, deletionTimestamps; weighted picks
-    and Philox jitter."""
+    and Philox jitter.  auto = the fused 8-byte records (28-bit words), u32 = 4-byte words and
+    the separate due column, wide = 8-byte {pred, sched}."""
     cl = W.make_cluster("C2", 50, 600, seed=12)
     objs = cl.pods.materialize()
-    total, per = run(cl.pod_stage_files, objs, steps=40, dt_ns=500 * 10**6, harness=True, wide_state=wide)
+    kernel = {"auto": abi.SWEEP_WD, "u32": abi.SWEEP_W4, "wide": abi.SWEEP_W8}[state]
+    total, per = run(cl.pod_stage_files, objs, steps=40, dt_ns=500 * 10**6, harness=True, state=state,
+                     expect_kernel=kernel)
     assert per["pod-create"] > 0 and per["pod-ready"] > 0 and per["pod-delete"] > 0
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
 
-@pytest.mark.parametrize("state", ["auto", "u16", "auto-nofsm", "u32"])
+@pytest.mark.parametrize("clock", ["jumps", "backwards", "from-zero"])
+def test_fused_due_epoch(clock):
+    """The fused records' due times against the oracle where the epoch moves: steps of 9-40 s
+    (re-encoded every ~17 s, due times past the 68.7 s window in the side column: the C2
+    deletion jitter reaches 30 s, RFC3339 overrides lie years back), a clock that runs backwards
+    (the epoch follows it down), and a clock starting at 0 (objects loaded with due times
+    relative to epoch 0)."""
+    from tests.parity_util import NOW0
+    cl = W.make_cluster("C2", 30, 400, seed=21)
+    objs = cl.pods.materialize()
+    if clock == "jumps":
+        nows = [NOW0 + sum((9 + 31 * (k % 2)) * 10**9 for k in range(j)) for j in range(24)]
+    elif clock == "backwards":
+        nows = [NOW0 + (k if k < 10 else 20 - k) * 3 * 10**9 + (k % 3) * 10**8 for k in range(20)]
+    else:
+        nows = [k * 700 * 10**6 for k in range(30)]
+    run(cl.pod_stage_files, objs, steps=len(nows), dt_ns=0, harness=True, state="auto", expect_kernel=abi.SWEEP_WD,
+        nows=nows)
+
+
+@pytest.mark.parametrize("state", ["auto", "u16", "auto-nofsm", "u32", "dw"])
 def test_node_fast_heartbeat(state):
     tuning = {}
     if state == "auto-nofsm":
@@ -137,7 +162,7 @@ def test_shard_invariance_two_engines():
             e.close()
 
 
-@pytest.mark.parametrize("state", ["auto", "u16", "u32", "wide"])
+@pytest.mark.parametrize("state", ["auto", "u16", "u32", "dw", "wide"])
 def test_count_phase_histogram(state):
     """kwk_count and kwk_aggregate (cluster aggregates for the RCCL all-reduce) against the
     oracle's phases, in the 2-, 4- and 8-byte state formats; a ragged object count so the last

@@ -160,7 +160,7 @@ def test_controller_scenario_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("state,fused", [("auto", False), ("u32", False), ("wide", False), ("auto", True),
-                                         ("u32", True)])
+                                         ("u32", True), ("dw", False), ("dw", True)])
 def test_c3_nodes_leases_pods_parity(state, fused):
     """C3 shape at 96 nodes (node-initialize + node-heartbeat 20 s / 25 s, leases 40 s with a
     10 s +- 4% renew, 250 ms tick for 50 s) with 4 pod-fast pods per node: lease step ->

@@ -98,9 +98,12 @@ def test_c5_persistent_table_sweep_sampled_oracle(state):
         eng.close()
 
 
-def test_c2_word_sweep_sampled_oracle():
+@pytest.mark.parametrize("state", ["u32", "auto"])
+def test_c2_word_sweep_sampled_oracle(state):
     """C2 stage mix (pod-general + chaos: weighted picks, jitter draws, value records, the
-    deletion column) at 4M pods through `sweepw_kernel<4>`, every 997th slot each step."""
+    deletion column) at 4M pods through `sweepw_kernel<4>` (u32: 4-byte words + the due column)
+    and `sweepw_kernel<8, fused>` (auto: the 8-byte records with the relative due time, the
+    benchmarked C2 kernel), every 997th slot each step."""
     from kwok_amd import workload as W
     from kwok_amd.host import abi
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
@@ -113,14 +116,15 @@ def test_c2_word_sweep_sampled_oracle():
     prog.explore(pvars)
     ing = Ingest(prog)
     hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
-    eng = Engine(prog, capacity=n, state="u32", max_records=max(1, len(ing.records)) + 16)
+    eng = Engine(prog, capacity=n, state=state, max_records=max(1, len(ing.records)) + 16)
     try:
         eng.load_stages()
         eng.set_harness(True)
         eng.load(hot, dels, rec, cls, ing.record_array())
-        assert eng.stats()["state_bytes"] == 4
+        assert eng.stats()["state_bytes"] == (4 if state == "u32" else 8)
         slots = list(range(1, n, 997))
-        total = _sampled_run(prog, eng, files, pvars, pidx, slots, 24, 500 * 10**6, abi.SWEEP_W4, 0)
+        kernel = abi.SWEEP_W4 if state == "u32" else abi.SWEEP_WD
+        total = _sampled_run(prog, eng, files, pvars, pidx, slots, 24, 500 * 10**6, kernel, 0)
         assert total > len(slots)
         fired = {k: v for k, v in eng.stats()["fired_per_stage"].items() if v}
         assert any("failed" in name for name in fired), fired  # weighted picks ran

@@ -218,15 +218,17 @@ def _c2_pods(prog, lo, hi, state):
 
 
 def test_c2_mix_formats_and_shards_agree_at_4m_pods():
-    """The word sweep on the C2 stage mix at 4M pods: the 4-byte and 8-byte formats and two
-    half-cluster shards (global-slot RNG keys) fire the same (slot, stage, flags) sets and leave
-    the same objects, step after step; the weighted-pick / jitter / record paths all run."""
+    """The word sweep on the C2 stage mix at 4M pods: the 4-byte, fused 8-byte and wide 8-byte
+    formats and two half-cluster shards (global-slot RNG keys) fire the same (slot, stage, flags)
+    sets and leave the same objects, step after step; the weighted-pick / jitter / record paths
+    all run."""
     n = 4_000_000
     prog = _c2_program(n)
-    eng = {"u32": _c2_pods(prog, 0, n, "u32"), "wide": _c2_pods(prog, 0, n, "wide"),
+    eng = {"u32": _c2_pods(prog, 0, n, "u32"), "wide": _c2_pods(prog, 0, n, "wide"), "dw": _c2_pods(prog, 0, n, "auto"),
            "s0": _c2_pods(prog, 0, n // 2, "u32"), "s1": _c2_pods(prog, n // 2, n, "u32")}
     try:
         assert eng["u32"][1].stats()["state_bytes"] == 4 and eng["wide"][1].stats()["state_bytes"] == 8
+        assert eng["dw"][1].stats()["state_bytes"] == 8
         now0 = 1_700_000_000 * 10**9
         total = 0
         for k in range(24):
@@ -241,17 +243,21 @@ def test_c2_mix_formats_and_shards_agree_at_4m_pods():
                 keys[s] = _fired_key(f)
             shards = np.sort(np.concatenate([keys["s0"], keys["s1"]]))
             assert np.array_equal(keys["u32"], keys["wide"]), f"step {k}: formats differ"
+            assert np.array_equal(keys["u32"], keys["dw"]), f"step {k}: fused format differs"
             assert np.array_equal(keys["u32"], shards), f"step {k}: shards differ"
             total += len(keys["u32"])
         assert total > n // 2
         a = eng["u32"][1].read()[0]
         w = eng["wide"][1].read()[0]
+        d = eng["dw"][1].read()[0]
         s0, s1 = eng["s0"][1].read()[0], eng["s1"][1].read()[0]
         for col in ("pred", "sched"):
             assert np.array_equal(a[col], w[col]), col
+            assert np.array_equal(a[col], d[col]), col
             assert np.array_equal(a[col], np.concatenate([s0[col], s1[col]])), col
         pend = (a["sched"] & 0xFF) != 0xFF
         assert np.array_equal(a["due"][pend], w["due"][pend])
+        assert np.array_equal(a["due"][pend], d["due"][pend])
         st = eng["u32"][1].stats()
         fired = {name: c for name, c in st["fired_per_stage"].items() if c}
         assert {"pod-create", "pod-ready", "pod-complete", "pod-delete"} <= set(fired), fired

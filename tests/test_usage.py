@@ -194,7 +194,7 @@ def _irregular_node_ptr(n_pods):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+@pytest.mark.parametrize("state", ["auto", "u32", "dw", "wide"])
 def test_gpu_usage_irregular_nodes(state):
     """usage_kernel's chunks of whole nodes (kwk_usage_config) against the oracle's
     nodeResourceUsage, per node and in total, for the 2-, 4- and 8-byte state formats, with
@@ -242,7 +242,7 @@ def test_gpu_usage_irregular_nodes(state):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+@pytest.mark.parametrize("state", ["auto", "u32", "dw", "wide"])
 def test_gpu_usage_fast_path_irregular_nodes(state):
     """The uniform-container configuration (no mixed pods, no per-pod outputs) takes
     usage_fast_kernel: same irregular node layout, node sums and integrators vs the oracle."""
@@ -287,7 +287,7 @@ def test_gpu_usage_fast_path_irregular_nodes(state):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("state", ["auto", "u32"])
+@pytest.mark.parametrize("state", ["auto", "u32", "dw"])
 def test_gpu_usage_key8_column_matches_4byte_keys(state):
     """kwk_usage_config builds a 1-byte usage-key column when at most 256 distinct keys occur
     (the C5 pods have 2): usage_fast_kernel<WB, true> must give node sums and integrators

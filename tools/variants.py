@@ -19,8 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "kwok_amd", "csrc", "engine.hip")
 OUT = os.path.join(ROOT, "tools", "build")
 
-_P2 = ("const uint2 nv = process_object<kHarness, kWB>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due, f,\n"
-       "                                                       n_matched, lutp, lut_n, gen_unused, due_unused);")
+_P2 = ("const uint2 nv = process_object<kHarness, kWB, false, kDW>(a, T, deltas, n_stages, fin_group, i, s.x, s.y, due,\n"
+       "                                                                   f, n_matched, lutp, lut_n, due_set, due_w);")
+
+_PF_EARLY = ("  if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);  // block-uniform\n", "")
+_PF_LATE = ("  const bool rebase = kDW && a.dw_rebase;",
+            "  if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);\n  const bool rebase = kDW && a.dw_rebase;")
 
 _FORCE = ("const bool lean = a.fsm && e->fsm_kernel;", "const bool lean = a.fsm && e->fsm_kernel;")
 
@@ -31,7 +35,7 @@ VARIANTS = {
     "base": [],
     "head": [],
     # phase 2 of the word sweep does nothing (no state change, no fires)
-    "w_nophase2": [(_P2, "const uint2 nv = s; (void)due; (void)i; (void)gen_unused; (void)due_unused;")],
+    "w_nophase2": [(_P2, "const uint2 nv = s; (void)due; (void)i;")],
     # jitter without its Philox draw
     "nojitter": [("delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));",
                   "delay = (int64_t)((uint64_t)delay + (uint64_t)(jit >> 1));")],
@@ -82,6 +86,13 @@ VARIANTS = {
                  "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
                 ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
                  "      const bool st = !real && ch;")],
+    # word sweep: 2 / 4 tiles per workgroup (a loop over tiles, the LDS set-up once)
+    "tpb2": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 2;")],
+    "tpb4": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 4;")],
+    "tpb8": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 8;")],
+    # ... the next tile's stream issued after phase 2 (its registers not live across process_object)
+    "tpb4_late": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 4;"), _PF_EARLY, _PF_LATE],
+    "tpb8_late": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 8;"), _PF_EARLY, _PF_LATE],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
@@ -115,15 +126,15 @@ def build(names):
             print(so, flush=True)
 
 
-def child(name, hbm_nodes, steps):
+def child(name, hbm_nodes, steps, state="auto"):
     sys.path.insert(0, ROOT)
     from kwok_amd.host import abi
     abi.LIB_PATH = os.path.join(OUT, f"libkwok_engine_{name}.so")
     import bench
     args = argparse.Namespace(hbm_nodes=hbm_nodes, pods_per_node=100, seed=0x6B776F6B, job_frac=0.1,
-                              hbm_steps=steps, hbm_warmup=12)
+                              hbm_steps=steps, hbm_warmup=12, hbm_state=state)
     r = bench.measure_hbm_working_set(args, 0)
-    print(json.dumps({"variant": name, **r}), flush=True)
+    print(json.dumps({"variant": name, "state": state, **r}), flush=True)
 
 
 def child_c5(name, steps):
@@ -144,6 +155,7 @@ def main():
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--c5", action="store_true", help="time the C5 pod sweep instead of the C2 working set")
+    ap.add_argument("--state", default="auto", help="C2 pod state format (auto: fused records, u32: split due)")
     a = ap.parse_args()
     names = a.names or list(VARIANTS)
     if a.cmd == "build":
@@ -152,11 +164,11 @@ def main():
         if a.c5:
             child_c5(names[0], a.steps)
         else:
-            child(names[0], a.hbm_nodes, a.steps)
+            child(names[0], a.hbm_nodes, a.steps, a.state)
     else:
         for n in names:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "child", n, "--hbm-nodes", str(a.hbm_nodes),
-                                "--steps", str(a.steps)] + (["--c5"] if a.c5 else []), timeout=300)
+                                "--steps", str(a.steps), "--state", a.state] + (["--c5"] if a.c5 else []), timeout=300)
             if r.returncode != 0:
                 raise SystemExit(f"variant {n}: rc {r.returncode}")
 
