@@ -124,7 +124,9 @@ def test_c2_word_sweep_sampled_oracle(state):
         assert eng.stats()["state_bytes"] == (4 if state == "u32" else 8)
         slots = list(range(1, n, 997))
         kernel = abi.SWEEP_W4 if state == "u32" else abi.SWEEP_WD
-        total = _sampled_run(prog, eng, files, pvars, pidx, slots, 24, 500 * 10**6, kernel, 0)
+        # fused: 1953 tiles over 5 workgroups per CU, each looping over its tiles; 4-byte: 977 tiles,
+        # one workgroup each
+        total = _sampled_run(prog, eng, files, pvars, pidx, slots, 24, 500 * 10**6, kernel, 1 if state == "auto" else 0)
         assert total > len(slots)
         fired = {k: v for k, v in eng.stats()["fired_per_stage"].items() if v}
         assert any("failed" in name for name in fired), fired  # weighted picks ran

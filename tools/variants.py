@@ -86,13 +86,15 @@ VARIANTS = {
                  "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
                 ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
                  "      const bool st = !real && ch;")],
-    # word sweep: 2 / 4 tiles per workgroup (a loop over tiles, the LDS set-up once)
-    "tpb2": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 2;")],
-    "tpb4": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 4;")],
-    "tpb8": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 8;")],
+    # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
+    # set-up once, the next tile's stream in flight)
+    "tpb1": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 1;")],
+    "tpb2": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 2;")],
+    "tpb4": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 4;")],
+    "tpb8": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 8;")],
     # ... the next tile's stream issued after phase 2 (its registers not live across process_object)
-    "tpb4_late": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 4;"), _PF_EARLY, _PF_LATE],
-    "tpb8_late": [("  uint32_t word_tpb = 1;", "  uint32_t word_tpb = 8;"), _PF_EARLY, _PF_LATE],
+    "tpb4_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 4;"), _PF_EARLY, _PF_LATE],
+    "tpb8_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 8;"), _PF_EARLY, _PF_LATE],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
