@@ -86,6 +86,9 @@ VARIANTS = {
                  "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
                 ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
                  "      const bool st = !real && ch;")],
+    # word sweep capped at 5 waves per SIMD (VGPRs <= 102; the next tile in flight costs ~20-40)
+    "lb5": [("__global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {",
+             "__global__ __launch_bounds__(kBlock, 5) void sweepw_kernel(SweepArgs a) {")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
     # set-up once, the next tile's stream in flight)
     "tpb1": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 1;")],
