@@ -1667,6 +1667,8 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
 //           (tile, wave) segment;
 //  phase 3  aligned 8-lane groups (one 128-byte line) holding a changed word are stored whole.
 constexpr int kQW = 4;                 // 16-byte chunks per lane: 16 (4-byte) / 8 (8-byte) words per lane
+constexpr int kDwMinBlocks = 6;        // fused word sweep: resident workgroups per CU the VGPR cap allows
+                                       // (80 VGPRs + 24 B of scratch; 467-470 vs 477-479 us at 5, r3w)
 constexpr int kQWD = 4;                // fused records: 8 per lane, 2048-object tiles (16 per lane: 129 VGPRs,
                                        // 3 waves per SIMD, 630 vs 541 us at C2, r3p)
 constexpr int kLdsDeltasW = 128;       // (class, stage) deltas staged in LDS by the word sweep
@@ -1691,8 +1693,11 @@ __device__ __forceinline__ void set_chunk_word(uint4& c, int j, uint2 w) {
 __device__ __forceinline__ uint32_t pred_word(uint32_t w) { return w; }  // word holding pred
 __device__ __forceinline__ uint32_t pred_word(uint2 w) { return w.x; }
 
+// fused records: a VGPR cap for 6 waves per SIMD (the next tile in flight pushed the kernel to
+// 108 VGPRs / 4 waves: 528 -> 481 us at 5 waves, r3v, -> 467-470 us at 6, r3w; the LDS tile
+// allows 6 workgroups per CU); the 4-byte words lose with a cap (522 -> 579 us at 5)
 template <bool kHarness, uint32_t kWB, bool kDW = false>
-__global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kBlock, kDW ? kDwMinBlocks : 1) void sweepw_kernel(SweepArgs a) {
   static_assert(!kDW || kWB == 8, "fused records are 8 bytes");
   typedef typename WordOf<kWB>::T W;
   constexpr int kQ = kDW ? kQWD : kQW;     // 16-byte chunks per lane

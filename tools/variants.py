@@ -86,15 +86,15 @@ VARIANTS = {
                  "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
                 ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
                  "      const bool st = !real && ch;")],
-    # word sweep capped at 5 waves per SIMD (VGPRs <= 102; the next tile in flight costs ~20-40)
-    "lb5": [("__global__ __launch_bounds__(kBlock) void sweepw_kernel(SweepArgs a) {",
-             "__global__ __launch_bounds__(kBlock, 5) void sweepw_kernel(SweepArgs a) {")],
+    # fused word sweep capped at 5 waves per SIMD instead of 6
+    "lb5": [("constexpr int kDwMinBlocks = 6;", "constexpr int kDwMinBlocks = 5;")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
     # set-up once, the next tile's stream in flight)
     "tpb1": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 1;")],
     "tpb2": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 2;")],
     "tpb4": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 4;")],
     "tpb8": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 8;")],
+    "tpb16": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 16;")],
     # ... the next tile's stream issued after phase 2 (its registers not live across process_object)
     "tpb4_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 4;"), _PF_EARLY, _PF_LATE],
     "tpb8_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 8;"), _PF_EARLY, _PF_LATE],
