@@ -26,6 +26,10 @@ _PF_EARLY = ("  if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);  //
 _PF_LATE = ("  const bool rebase = kDW && a.dw_rebase;",
             "  if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);\n  const bool rebase = kDW && a.dw_rebase;")
 
+_S8_INV = [("  __shared__ uint32_t s_inv[kWavesPerBlock][64];", "  __shared__ uint32_t s_inv[64];"),
+           ("  s_inv[wave][lane] = 0xFFFFFFFFu;", "  s_inv[lane] = 0xFFFFFFFFu;"),
+           ("lds_addr(&s_inv[wave][lane])", "lds_addr(&s_inv[lane])")]
+
 _FORCE = ("const bool lean = a.fsm && e->fsm_kernel;", "const bool lean = a.fsm && e->fsm_kernel;")
 
 _NOCALL = ("          const uint2 r = general16<kHarness>(wbase + w, (uint32_t)tw[w]);",
@@ -86,6 +90,12 @@ VARIANTS = {
                  "    if (false) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile"),
                 ("      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);",
                  "      const bool st = !real && ch;")],
+    # sweep8: one kIdInvalid row shared by the block's waves (LDS 27.8 -> 27.0 KB: 6 workgroups per CU
+    # fit) / and a VGPR cap for 6 waves per SIMD (run with --c5; r3x: 52.5-53.6 / 53.6-53.9 vs
+    # 52.7-52.8 us, not kept)
+    "s8_inv": _S8_INV,
+    "s8_lb6": _S8_INV + [("__global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {",
+                          "__global__ __launch_bounds__(kBlock, 6) void sweep8_kernel(SweepArgs a) {")],
     # fused word sweep capped at 5 waves per SIMD instead of 6
     "lb5": [("constexpr int kDwMinBlocks = 6;", "constexpr int kDwMinBlocks = 5;")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
