@@ -565,6 +565,11 @@ def main():
 
     log(f"setup {setup_s:.1f} s; warmup {args.warmup} steps")
     run_steps(pods, nodes, args.seed, dt, 0, args.warmup)
+    if report_every and args.warmup:
+        # the warm-up covers one reporting interval too: its one-time work (the aggregate and count
+        # buffers' allocation, the masks' upload, occupancy queries, the communicator's first
+        # collective) stays out of the timed region like the steps' own
+        reporter.collect(NOW0 + (args.warmup - 1) * dt)
     pods.sync()
     nodes.sync()
     s0p, s0n = pods.stats(), nodes.stats()

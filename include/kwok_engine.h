@@ -220,8 +220,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
-#define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16,
-                                  or 0 (default: 8 fused, 4 otherwise; at least 5 workgroups per CU) */
+#define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
+                                  (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
+                                  per CU) */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
 
 /* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */

@@ -4703,8 +4703,10 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   const uint32_t tiles = (e->n_active + tile - 1) / tile;
   // tiles per workgroup (the next tile's stream in flight while one is worked: 8 for the fused
   // records, 4 for the 4-byte words, r3r), but at least ~5 workgroups per CU
+  // (an explicit KWK_TUNE_WORD_TILES is taken as it is: the parity tests loop small engines)
   const uint32_t tpb = e->word_tpb ? e->word_tpb : dw ? 8u : 4u;
-  const uint32_t blocks = std::min(tiles, std::max((tiles + tpb - 1) / tpb, (uint32_t)e->n_cus * 5u));
+  const uint32_t blocks = e->word_tpb ? (tiles + tpb - 1) / tpb
+                                      : std::min(tiles, std::max((tiles + tpb - 1) / tpb, (uint32_t)e->n_cus * 5u));
   if (dw) {
     // the fused records' epoch follows the clock: re-encoded (inside this sweep) once now is
     // more than 2^34 ns (~17 s) past it or before it, so that due times up to ~51 s ahead of now

@@ -57,6 +57,18 @@ def test_pod_general_c2_mini(state):
     assert per["pod-container-running-failed"] + per["pod-init-container-running-failed"] > 0
 
 
+@pytest.mark.parametrize("state", ["auto", "u32", "wide"])
+def test_word_sweep_tile_loop(state):
+    """The word sweep's workgroups looping over several tiles (KWK_TUNE_WORD_TILES 2: every
+    second tile's stream in flight while the first is worked, the LDS dirty-line mask deciding
+    the line stores) on a C2 cluster of several tiles, against the oracle at every step."""
+    cl = W.make_cluster("C2", 120, 12000, seed=23)
+    objs = cl.pods.materialize()
+    kernel = {"auto": abi.SWEEP_WD, "u32": abi.SWEEP_W4, "wide": abi.SWEEP_W8}[state]
+    run(cl.pod_stage_files, objs, steps=8, dt_ns=700 * 10**6, harness=True, state=state,
+        tuning={abi.TUNE_WORD_TILES: 2}, expect_kernel=kernel)
+
+
 @pytest.mark.parametrize("clock", ["jumps", "backwards", "from-zero"])
 def test_fused_due_epoch(clock):
     """The fused records' due times against the oracle where the epoch moves: steps of 9-40 s
