@@ -1352,6 +1352,11 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // stages.  kStages4: the fired records go to the wave's LDS work list (their positions lie
 // behind the entries still to be read), 2 bytes each, and the per-stage counts to scalar
 // registers; else 4-byte records straight to the segment and LDS counters.
+template <bool kStages4>
+__device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, uint16_t* __restrict__ wl,
+                                         const __amdgpu_buffer_rsrc_t seg_rs, uint32_t& seg_n, uint32_t (&stc)[4],
+                                         unsigned int* s_stat, uint32_t n_stages, uint32_t lane);
+
 template <bool kSlow, bool kStages4>
 __device__ __forceinline__ void id8_pass(const uint32_t we, const uint32_t* __restrict__ s_fsm, uint16_t* __restrict__ wl,
                                          const __amdgpu_buffer_rsrc_t seg_rs, uint32_t& seg_n, uint32_t& n_bytes,
@@ -1373,6 +1378,40 @@ __device__ __forceinline__ void id8_pass(const uint32_t we, const uint32_t* __re
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, due_rs, off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)((uint64_t)t >> 32), due_rs, off + 4u, 0, 0);
   }
+  id8_fire<kStages4>(addr, e, wl, seg_rs, seg_n, stc, s_stat, n_stages, lane);
+}
+
+// kN passes whose LDS round trips overlap (table-only ids, no due path): every entry's byte, then
+// every lookup, then every write — the passes touch distinct bytes (an inactive lane's entries
+// are its kIdInvalid byte, whose lookup writes it back unchanged)
+constexpr uint32_t kId8Batch = 4;  // passes per step of the id loop (vs 1: C5 step 93.7-95.1 -> 91.4-93.8 us,
+                                   // sweep 50.9-51.6 -> 49.2-51.2 us, r3zc alternating)
+template <bool kStages4, uint32_t kN>
+__device__ __forceinline__ void id8_passn(const uint32_t (&we)[kN], const uint32_t* __restrict__ s_fsm,
+                                          uint16_t* __restrict__ wl, const __amdgpu_buffer_rsrc_t seg_rs, uint32_t& seg_n,
+                                          uint32_t& n_bytes, uint32_t& n_matched, uint32_t (&stc)[4],
+                                          unsigned int* s_stat, uint32_t n_stages, uint32_t lane) {
+  uint32_t k[kN], e[kN];
+#pragma unroll
+  for (uint32_t j = 0; j < kN; ++j) k[j] = (uint32_t)*(lds_u8*)(size_t)we[j];
+#pragma unroll
+  for (uint32_t j = 0; j < kN; ++j) e[j] = s_fsm[k[j]];
+#pragma unroll
+  for (uint32_t j = 0; j < kN; ++j) *(lds_u8*)(size_t)we[j] = (uint8_t)e[j];
+#pragma unroll
+  for (uint32_t j = 0; j < kN; ++j) {
+    n_bytes += (e[j] >> 24) & 31u;
+    n_matched += (e[j] >> 30) & 1u;
+    id8_fire<kStages4>(we[j], e[j], wl, seg_rs, seg_n, stc, s_stat, n_stages, lane);
+  }
+}
+
+// the fired ballot of one pass: records staged at the list's consumed front (<= 4 stages) or
+// stored to the segment, per-stage counts
+template <bool kStages4>
+__device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, uint16_t* __restrict__ wl,
+                                         const __amdgpu_buffer_rsrc_t seg_rs, uint32_t& seg_n, uint32_t (&stc)[4],
+                                         unsigned int* s_stat, uint32_t n_stages, uint32_t lane) {
   const bool fire = (int32_t)e < 0;
   const unsigned long long bal = ballot(fire);
   if (bal) {  // wave-uniform
@@ -1549,19 +1588,38 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       // the next pass's entries are read while this pass works (an entry past the list: the
       // lane's kIdInvalid byte)
-      uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : inv_ent;
-      for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
-        const uint32_t we = nwe;
-        if (c + 64u < n_work) {
-          const uint32_t x = (uint32_t)wl[(c + 64u + lane) & (kWave - 1u)];
-          nwe = c + 64u + lane < n_work ? x : inv_ent;
-        }
-        if (slow)
+      if (slow) {
+        uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : inv_ent;
+        for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
+          const uint32_t we = nwe;
+          if (c + 64u < n_work) {
+            const uint32_t x = (uint32_t)wl[(c + 64u + lane) & (kWave - 1u)];
+            nwe = c + 64u + lane < n_work ? x : inv_ent;
+          }
           id8_pass<true, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
                                    fdue_rs, due_rs, wbase, a.now);
-        else
-          id8_pass<false, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
-                                    fdue_rs, due_rs, wbase, a.now);
+        }
+      } else {
+        // kId8Batch passes per step (their LDS round trips overlap); the next step's entries are
+        // read while these work (records of passes < c + 64 * kId8Batch land below it)
+        constexpr uint32_t kB = kId8Batch;
+        uint32_t nw[kB];
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) nw[j] = 64u * j + lane < n_work ? (uint32_t)wl[64u * j + lane] : inv_ent;
+        for (uint32_t c = 0; c < n_work; c += 64u * kB) {  // wave-uniform
+          uint32_t we[kB];
+#pragma unroll
+          for (uint32_t j = 0; j < kB; ++j) we[j] = nw[j];
+          if (c + 64u * kB < n_work) {
+#pragma unroll
+            for (uint32_t j = 0; j < kB; ++j) {
+              const uint32_t i = c + 64u * (kB + j) + lane;
+              const uint32_t x = (uint32_t)wl[i & (kWave - 1u)];
+              nw[j] = i < n_work ? x : inv_ent;
+            }
+          }
+          id8_passn<kStages4, kB>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane);
+        }
       }
       n_lline -= (uint32_t)__popc(need);  // the ids' own writes are replaced by the line stores below
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

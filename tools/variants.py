@@ -96,6 +96,9 @@ VARIANTS = {
     "s8_inv": _S8_INV,
     "s8_lb6": _S8_INV + [("__global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {",
                           "__global__ __launch_bounds__(kBlock, 6) void sweep8_kernel(SweepArgs a) {")],
+    # sweep8: 1 / 2 id passes per loop step instead of 4 (run with --c5)
+    "id8b1": [("constexpr uint32_t kId8Batch = 4;", "constexpr uint32_t kId8Batch = 1;")],
+    "id8b2": [("constexpr uint32_t kId8Batch = 4;", "constexpr uint32_t kId8Batch = 2;")],
     # fused word sweep capped at 5 waves per SIMD instead of 6
     "lb5": [("constexpr int kDwMinBlocks = 6;", "constexpr int kDwMinBlocks = 5;")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
