@@ -3379,7 +3379,17 @@ __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __res
   __shared__ unsigned long long s[1024];
   const uint32_t m = threadIdx.x & (kMaxCountMasks - 1), r = threadIdx.x / kMaxCountMasks;
   unsigned long long c = 0;
-  for (uint32_t b = r; b < n_blocks; b += 1024 / kMaxCountMasks) c += part[(uint64_t)b * kMaxCountMasks + m];
+  constexpr uint32_t kRows = 1024 / kMaxCountMasks;  // rows summed in parallel
+  for (uint32_t b = r; b < n_blocks; b += 8 * kRows) {  // 8 loads in flight per thread (was one at a time: 9.6 us)
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t bb = b + j * kRows;
+      v[j] = bb < n_blocks ? part[(uint64_t)bb * kMaxCountMasks + m] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) c += v[j];
+  }
   s[threadIdx.x] = c;
   __syncthreads();
   for (uint32_t h = 512; h >= kMaxCountMasks; h >>= 1) {
