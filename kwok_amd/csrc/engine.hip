@@ -2330,20 +2330,23 @@ __global__ void delete_kernel(void* st, StateFmt fmt, const uint32_t* slots, uin
 // the fused format's due times <-> the due column.  fold: every record's D from the column
 // (kDwFar where the time is outside the window: the column already holds it); unfold: the column
 // from every record whose D is in the window (the column is then exact for every slot)
+// (grid-stride over a bounded grid.  At 100M slots either shape takes 110-140 ms per call in the
+// kernel trace (r3ze one workgroup per 256 slots, r3zf grid-stride) for 2.4 GB of traffic: not
+// dispatch-bound, cause not found; load-time only)
 __global__ void dw_fold_kernel(uint2* __restrict__ st, const int64_t* __restrict__ due, uint32_t first, uint32_t n,
                                int64_t epoch) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = first + j;
-  st[i] = dw_put(st[i], dw_enc(due[i], epoch));
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const uint32_t i = first + j;
+    st[i] = dw_put(st[i], dw_enc(due[i], epoch));
+  }
 }
 __global__ void dw_unfold_kernel(const uint2* __restrict__ st, int64_t* __restrict__ due, uint32_t first, uint32_t n,
                                  int64_t epoch) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = first + j;
-  const uint64_t d = dw_get(st[i]);
-  if (d != kDwFar) due[i] = dw_abs(d, epoch);
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const uint32_t i = first + j;
+    const uint64_t d = dw_get(st[i]);
+    if (d != kDwFar) due[i] = dw_abs(d, epoch);
+  }
 }
 
 // ------------------------------------------------------------------ resource usage
@@ -4013,14 +4016,16 @@ static kwk_status dict_upload(kwk_engine* e) {
 // the fused format: records' D from the due column / the due column made exact (stream-ordered)
 static kwk_status dw_fold(kwk_engine* e, uint32_t first, uint32_t n) {
   if (!e->fmt.dw || n == 0) return KWK_OK;
-  hipLaunchKernelGGL(dw_fold_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
+  const uint32_t g = std::min((n + kBlock - 1) / kBlock, (uint32_t)e->n_cus * 32u);
+  hipLaunchKernelGGL(dw_fold_kernel, dim3(g), dim3(kBlock), 0, e->stream,
                      reinterpret_cast<uint2*>(e->d_st), e->d_due, first, n, e->fmt.epoch);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
 static kwk_status dw_unfold(kwk_engine* e, uint32_t first, uint32_t n) {
   if (!e->fmt.dw || n == 0) return KWK_OK;
-  hipLaunchKernelGGL(dw_unfold_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream,
+  const uint32_t g = std::min((n + kBlock - 1) / kBlock, (uint32_t)e->n_cus * 32u);
+  hipLaunchKernelGGL(dw_unfold_kernel, dim3(g), dim3(kBlock), 0, e->stream,
                      reinterpret_cast<const uint2*>(e->d_st), e->d_due, first, n, e->fmt.epoch);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
