@@ -3868,6 +3868,15 @@ static kwk_status set_dev(kwk_engine* e) {
   return KWK_OK;
 }
 
+// host -> device on the engine's stream, complete on return.  A pageable hipMemcpy on the null
+// stream may return with its DMA still in flight, and the engine's stream is non-blocking: a
+// kernel enqueued next on it ran concurrently with the upload (dw_fold_kernel after a 100M-object
+// kwk_load: 110-140 ms, overlapping the copy, vs 0.48 ms ordered after it, r3zf / r3zg)
+static hipError_t upload(const kwk_engine* e, void* dst, const void* src, size_t bytes) {
+  const hipError_t r = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream);
+  return r != hipSuccess ? r : hipStreamSynchronize(e->stream);
+}
+
 static kwk_status ensure_stage_buf(kwk_engine* e, size_t bytes) {
   if (bytes <= e->stage_bytes) return KWK_OK;
   if (e->d_stage_buf) HIP_TRY(hipFree(e->d_stage_buf));
@@ -4006,10 +4015,10 @@ static kwk_status dict_upload(kwk_engine* e) {
       t8[(rdy << 8) | id] = x;
     }
   }
-  HIP_TRY(hipMemcpy(e->d_id2w, e->h_id2w.data(), sizeof(uint16_t) * 256, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_w2id, e->h_w2id.data(), 65536, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_fsm8, t8.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_fsm8_due, d8.data(), sizeof(int64_t) * 512, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_id2w, e->h_id2w.data(), sizeof(uint16_t) * 256));
+  HIP_TRY(upload(e, e->d_w2id, e->h_w2id.data(), 65536));
+  HIP_TRY(upload(e, e->d_fsm8, t8.data(), sizeof(uint32_t) * 512));
+  HIP_TRY(upload(e, e->d_fsm8_due, d8.data(), sizeof(int64_t) * 512));
   return KWK_OK;
 }
 
@@ -4045,9 +4054,11 @@ static kwk_status read_rows(kwk_engine* e, std::vector<uint2>& rows) {
 // writes rows [0, n) in format nf and makes nf current (the dictionary must hold their words)
 static kwk_status write_rows(kwk_engine* e, const std::vector<uint2>& rows, const StateFmt& nf) {
   const std::vector<uint8_t> out = pack_words(e, rows, nf);
-  if (!out.empty()) HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
+  if (!out.empty()) HIP_TRY(hipMemcpyAsync(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice, e->stream));
   e->fmt = nf;
-  return dw_fold(e, 0, (uint32_t)rows.size());
+  if (kwk_status st = dw_fold(e, 0, (uint32_t)rows.size())) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));  // `out` goes with this frame
+  return KWK_OK;
 }
 
 // the format without the dictionary (2-byte words when the program fits 16 bits)
@@ -4261,13 +4272,14 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
         if (!fits_fmt(nf, t->n_stages, v[i].x, v[i].y) || (v[i].y >> KWK_CLASS_SHIFT) >= (t->n_classes ? t->n_classes : 1))
           return fail(KWK_EINVAL, "resident object " + std::to_string(i) + " does not fit the new stage table");
       std::vector<uint8_t> out = pack_words(e, v, nf);
-      HIP_TRY(hipMemcpy(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpyAsync(e->d_st, out.data(), out.size(), hipMemcpyHostToDevice, e->stream));
       e->fmt = nf;
       if (kwk_status st = dw_fold(e, 0, n)) return st;
+      HIP_TRY(hipStreamSynchronize(e->stream));
     }
     e->fmt = nf;
   }
-  HIP_TRY(hipMemcpy(e->d_table, t, sizeof(kwk_stage_table), hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_table, t, sizeof(kwk_stage_table)));
   // the match set of every pred value, when pred_bits is small (Lifecycle.match, lifecycle.go:51-63)
   // match-mask tables (match_mask): one exact table up to 8 pred bits, else one per pred byte
   // for the stages whose clauses each lie within one byte
@@ -4308,14 +4320,14 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
           }
       }
     }
-    HIP_TRY(hipMemcpy(e->d_lut, lut.data(), sizeof(uint32_t) * e->lut_n, hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_lut, lut.data(), sizeof(uint32_t) * e->lut_n));
   }
   if (e->d_deltas) HIP_TRY(hipFree(e->d_deltas));
   e->d_deltas = nullptr;
   const size_t nd = (size_t)(t->n_classes ? t->n_classes : 1) * (t->n_stages ? t->n_stages : 1);
   HIP_TRY(hipMalloc(&e->d_deltas, sizeof(kwk_delta) * nd));
-  if (deltas && t->n_stages) HIP_TRY(hipMemcpy(e->d_deltas, deltas, sizeof(kwk_delta) * nd, hipMemcpyHostToDevice));
-  else HIP_TRY(hipMemset(e->d_deltas, 0xFF, sizeof(kwk_delta) * nd));
+  if (deltas && t->n_stages) HIP_TRY(upload(e, e->d_deltas, deltas, sizeof(kwk_delta) * nd));
+  else HIP_TRY(hipMemsetAsync(e->d_deltas, 0xFF, sizeof(kwk_delta) * nd, e->stream));
   e->n_stages = t->n_stages;
   e->n_classes = t->n_classes;
   e->loaded_table = true;
@@ -4419,17 +4431,21 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
     if (kwk_status s2 = pick_format(e, st, nf)) return s2;
     e->fmt = nf;
     const std::vector<uint8_t> raw = pack_words(e, st, e->fmt);
-    HIP_TRY(hipMemcpy(e->d_st, raw.data(), raw.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    // on the engine's stream, so that the fold (and every later kernel) is ordered after the
+    // uploads whatever a pageable hipMemcpy's return means for its DMA; synchronised before the
+    // host buffers go
+    HIP_TRY(hipMemcpyAsync(e->d_st, raw.data(), raw.size(), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_due, due.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, e->stream));
     if (kwk_status s2 = dw_fold(e, 0, n)) return s2;
+    HIP_TRY(hipStreamSynchronize(e->stream));
   }
-  HIP_TRY(hipMemcpy(e->d_del, del, sizeof(int64_t) * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_rec, rec, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_del, del, sizeof(int64_t) * n));
+  HIP_TRY(upload(e, e->d_rec, rec, sizeof(uint32_t) * n));
   if (n_records)
     HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
                       hipMemcpyHostToDevice));
   if (n < e->n_active)
-    HIP_TRY(hipMemset((char*)e->d_st + word_bytes(e->fmt) * n, 0, word_bytes(e->fmt) * (size_t)(e->n_active - n)));
+    HIP_TRY(hipMemsetAsync((char*)e->d_st + word_bytes(e->fmt) * n, 0, word_bytes(e->fmt) * (size_t)(e->n_active - n), e->stream));
   e->n_active = n;
   return KWK_OK;
 }
@@ -4490,14 +4506,14 @@ static kwk_status scatter_rows(kwk_engine* e, uint32_t n, const uint32_t* slots,
   uint32_t* s_slots = (uint32_t*)p; p += 4 * (size_t)n;
   uint32_t* s_rec = (uint32_t*)p; p += 4 * (size_t)n;
   uint16_t* s_cls = (uint16_t*)p;
-  HIP_TRY(hipMemcpy(s_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_del, del, 8 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_rec, rec, 4 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, s_hot, hot, sizeof(kwk_hot) * n));
+  HIP_TRY(upload(e, s_del, del, 8 * (size_t)n));
+  HIP_TRY(upload(e, s_slots, slots, 4 * (size_t)n));
+  HIP_TRY(upload(e, s_rec, rec, 4 * (size_t)n));
+  HIP_TRY(upload(e, s_cls, cls, 2 * (size_t)n));
   if (max_slot + 1 > e->n_active) {
-    HIP_TRY(hipMemset((char*)e->d_st + word_bytes(e->fmt) * e->n_active, 0,
-                      word_bytes(e->fmt) * (size_t)(max_slot + 1 - e->n_active)));
+    HIP_TRY(hipMemsetAsync((char*)e->d_st + word_bytes(e->fmt) * e->n_active, 0,
+                           word_bytes(e->fmt) * (size_t)(max_slot + 1 - e->n_active), e->stream));
     e->n_active = max_slot + 1;
   }
   ScatterArgs a{e->d_st, e->fmt, e->d_due, e->d_del, e->d_rec, s_slots, s_hot, s_del, s_rec, s_cls, n, mark_dirty};
@@ -4516,7 +4532,7 @@ kwk_status kwk_delete(kwk_engine* e, uint32_t n, const uint32_t* slots) {
   if (kwk_status st = set_dev(e)) return st;
   if (kwk_status st = ensure_stage_buf(e, 4 * (size_t)n)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(e->d_stage_buf, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_stage_buf, slots, 4 * (size_t)n));
   hipLaunchKernelGGL(delete_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, e->d_st,
                      e->fmt, (const uint32_t*)e->d_stage_buf, n);
   HIP_TRY(hipGetLastError());
@@ -4555,11 +4571,11 @@ kwk_status kwk_retry(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step
   uint32_t* s_rc = (uint32_t*)p; p += 4 * (size_t)n;
   uint16_t* s_cls = (uint16_t*)p; p += 2 * (size_t)n;
   uint16_t* s_stg = (uint16_t*)p;
-  HIP_TRY(hipMemcpy(s_hot, hot, sizeof(kwk_hot) * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_rc, retry_count, 4 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_cls, cls, 2 * (size_t)n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_stg, stages, 2 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, s_hot, hot, sizeof(kwk_hot) * n));
+  HIP_TRY(upload(e, s_slots, slots, 4 * (size_t)n));
+  HIP_TRY(upload(e, s_rc, retry_count, 4 * (size_t)n));
+  HIP_TRY(upload(e, s_cls, cls, 2 * (size_t)n));
+  HIP_TRY(upload(e, s_stg, stages, 2 * (size_t)n));
   RetryArgs a{e->d_st, e->fmt, e->d_due, s_slots, s_hot, s_cls, s_stg, s_rc, *backoff, n, e->slot_base,
               seed ^ ((uint64_t)e->kind_salt << 32), step, now_ns};
   hipLaunchKernelGGL(retry_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
@@ -5025,7 +5041,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   const uint32_t ublocks = ((uint32_t)chunks.size() + kWavesPerBlock - 1) / kWavesPerBlock;
   HIP_TRY(hipMalloc(&e->d_uchunk, sizeof(uint4) * (chunks.size() + 1)));
   if (!chunks.empty())
-    HIP_TRY(hipMemcpy(e->d_uchunk, chunks.data(), sizeof(uint4) * chunks.size(), hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_uchunk, chunks.data(), sizeof(uint4) * chunks.size()));
   e->n_uchunks = (uint32_t)chunks.size();
   // usage_fast_kernel's table: row nc = the value of a pod with nc alike containers, summed
   // container by container (podResourceUsage's order, :170-193) — what usage_kernel's loop adds
@@ -5055,7 +5071,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
       }
     }
     HIP_TRY(hipMalloc(&e->d_podv, sizeof(double) * podv.size()));
-    HIP_TRY(hipMemcpy(e->d_podv, podv.data(), sizeof(double) * podv.size(), hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_podv, podv.data(), sizeof(double) * podv.size()));
     e->podv_n = (uint32_t)podv.size();
     // distinct keys -> 1-byte column + {cpu, mem} values (the same podv entries, so the sums are
     // bit-identical to the 4-byte-key kernel's)
@@ -5079,8 +5095,8 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
       }
       HIP_TRY(hipMalloc(&e->d_ukey8, (size_t)n_pods + 16));
       HIP_TRY(hipMalloc(&e->d_kv, sizeof(double2) * kv.size()));
-      HIP_TRY(hipMemcpy(e->d_ukey8, k8.data(), n_pods, hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(e->d_kv, kv.data(), sizeof(double2) * kv.size(), hipMemcpyHostToDevice));
+      HIP_TRY(upload(e, e->d_ukey8, k8.data(), n_pods));
+      HIP_TRY(upload(e, e->d_kv, kv.data(), sizeof(double2) * kv.size()));
       e->kv_n = (uint32_t)kv.size();
     }
   }
@@ -5093,15 +5109,15 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   HIP_TRY(hipMalloc(&e->d_node_last, 8 * ((size_t)n_nodes + 1)));
   HIP_TRY(hipMalloc(&e->d_usage_part, 16 * ((size_t)ublocks + 1)));
   HIP_TRY(hipMalloc(&e->d_cluster, 16));
-  HIP_TRY(hipMemcpy(e->d_node_ptr, node_ptr, 4 * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_ukey, ukey, 4 * (size_t)n_pods, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_cpu, cpu_values, 8 * (size_t)n_cpu, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_mem, mem_values, 8 * (size_t)n_mem, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(e->d_node_cum, 0, 16 * ((size_t)n_nodes + 1)));
-  HIP_TRY(hipMemset(e->d_cluster, 0, 16));  // totals of a configuration without nodes stay 0
-  HIP_TRY(hipMemset(e->d_node_last, 0x80, 8 * ((size_t)n_nodes + 1)));  // INT64_MIN-ish sentinel below
+  HIP_TRY(upload(e, e->d_node_ptr, node_ptr, 4 * ((size_t)n_nodes + 1)));
+  HIP_TRY(upload(e, e->d_ukey, ukey, 4 * (size_t)n_pods));
+  HIP_TRY(upload(e, e->d_cpu, cpu_values, 8 * (size_t)n_cpu));
+  HIP_TRY(upload(e, e->d_mem, mem_values, 8 * (size_t)n_mem));
+  HIP_TRY(hipMemsetAsync(e->d_node_cum, 0, 16 * ((size_t)n_nodes + 1), e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_cluster, 0, 16, e->stream));  // totals of a configuration without nodes stay 0
+  HIP_TRY(hipMemsetAsync(e->d_node_last, 0x80, 8 * ((size_t)n_nodes + 1), e->stream));  // INT64_MIN-ish sentinel below
   std::vector<int64_t> lasts((size_t)n_nodes + 1, INT64_MIN);
-  HIP_TRY(hipMemcpy(e->d_node_last, lasts.data(), 8 * lasts.size(), hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_node_last, lasts.data(), 8 * lasts.size()));
   e->n_nodes = n_nodes;
   e->n_usage_pods = n_pods;
   e->has_mixed_keys = mixed_keys;
@@ -5120,7 +5136,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   e->d_cptr = nullptr;
   e->d_mbase = nullptr;
   e->h_mbase.clear();
-  if (e->d_pod_cum) HIP_TRY(hipMemset(e->d_pod_cum, 0, 16 * (size_t)e->capacity));
+  if (e->d_pod_cum) HIP_TRY(hipMemsetAsync(e->d_pod_cum, 0, 16 * (size_t)e->capacity, e->stream));
   return KWK_OK;
 }
 
@@ -5157,10 +5173,10 @@ kwk_status kwk_usage_mixed(kwk_engine* e, uint32_t n_mixed, const uint32_t* mixe
   HIP_TRY(hipMalloc(&e->d_ckeys, 4 * ((size_t)n_ckeys + 1)));
   HIP_TRY(hipMalloc(&e->d_ccum, 16 * ((size_t)nint + 1)));
   HIP_TRY(hipMalloc(&e->d_mbase, 4 * ((size_t)e->n_usage_pods + 1)));
-  if (n_mixed) HIP_TRY(hipMemcpy(e->d_mixed, mixed, 8 * (size_t)n_mixed, hipMemcpyHostToDevice));
-  if (n_ckeys) HIP_TRY(hipMemcpy(e->d_ckeys, ckeys, 4 * (size_t)n_ckeys, hipMemcpyHostToDevice));
-  if (e->n_usage_pods) HIP_TRY(hipMemcpy(e->d_mbase, e->h_mbase.data(), 4 * (size_t)e->n_usage_pods, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(e->d_ccum, 0, 16 * ((size_t)nint + 1)));
+  if (n_mixed) HIP_TRY(upload(e, e->d_mixed, mixed, 8 * (size_t)n_mixed));
+  if (n_ckeys) HIP_TRY(upload(e, e->d_ckeys, ckeys, 4 * (size_t)n_ckeys));
+  if (e->n_usage_pods) HIP_TRY(upload(e, e->d_mbase, e->h_mbase.data(), 4 * (size_t)e->n_usage_pods));
+  HIP_TRY(hipMemsetAsync(e->d_ccum, 0, 16 * ((size_t)nint + 1), e->stream));
   e->h_mixed.assign(mixed, mixed + 2 * (size_t)n_mixed);
   e->h_ckeys.assign(ckeys, ckeys + n_ckeys);
   return KWK_OK;
@@ -5183,7 +5199,7 @@ static kwk_status ensure_cptr(kwk_engine* e) {
   }
   e->h_cptr[e->n_usage_pods] = (uint32_t)c;
   HIP_TRY(hipMalloc(&e->d_cptr, 4 * e->h_cptr.size()));
-  HIP_TRY(hipMemcpy(e->d_cptr, e->h_cptr.data(), 4 * e->h_cptr.size(), hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_cptr, e->h_cptr.data(), 4 * e->h_cptr.size()));
   return KWK_OK;
 }
 
@@ -5320,7 +5336,7 @@ kwk_status kwk_metrics_load(kwk_engine* e, uint32_t n_metrics, const kwk_metric_
   if (e->d_mops) HIP_TRY(hipFree(e->d_mops));
   e->d_mops = nullptr;
   HIP_TRY(hipMalloc(&e->d_mops, sizeof(kwk_metric_op) * ((size_t)n_ops + 1)));
-  if (n_ops) HIP_TRY(hipMemcpy(e->d_mops, ops, sizeof(kwk_metric_op) * n_ops, hipMemcpyHostToDevice));
+  if (n_ops) HIP_TRY(upload(e, e->d_mops, ops, sizeof(kwk_metric_op) * n_ops));
   e->metrics.assign(metrics, metrics + n_metrics);
   e->metric_inputs_needed = needs;
   return KWK_OK;
@@ -5339,10 +5355,10 @@ kwk_status kwk_metrics_inputs(kwk_engine* e, const int64_t* pod_created, const i
   HIP_TRY(hipMalloc(&e->d_node_created, 8 * ((size_t)e->n_nodes + 1)));
   HIP_TRY(hipMalloc(&e->d_node_started, 8 * ((size_t)e->n_nodes + 1)));
   if (e->n_usage_pods)
-    HIP_TRY(hipMemcpy(e->d_pod_created, pod_created, 8 * (size_t)e->n_usage_pods, hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_pod_created, pod_created, 8 * (size_t)e->n_usage_pods));
   if (e->n_nodes) {
-    HIP_TRY(hipMemcpy(e->d_node_created, node_created, 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_node_started, started, 8 * (size_t)e->n_nodes, hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_node_created, node_created, 8 * (size_t)e->n_nodes));
+    HIP_TRY(upload(e, e->d_node_started, started, 8 * (size_t)e->n_nodes));
   }
   e->zero_time_unix_s = zero_time_unix_s;
   return KWK_OK;
@@ -5450,11 +5466,11 @@ kwk_status kwk_histograms_load(kwk_engine* e, uint32_t n_hist, const kwk_histogr
   HIP_TRY(hipMalloc(&e->d_hbuckets, sizeof(kwk_metric_bucket) * ((size_t)n_buckets + 1)));
   HIP_TRY(hipMalloc(&e->d_hkeys, sizeof(uint32_t) * (keys.size() + 1)));
   HIP_TRY(hipMalloc(&e->d_hbounds, sizeof(double) * (bounds.size() + 1)));
-  if (n_ops) HIP_TRY(hipMemcpy(e->d_hops, ops, sizeof(kwk_metric_op) * n_ops, hipMemcpyHostToDevice));
-  if (n_buckets) HIP_TRY(hipMemcpy(e->d_hbuckets, buckets, sizeof(kwk_metric_bucket) * n_buckets, hipMemcpyHostToDevice));
-  if (!keys.empty()) HIP_TRY(hipMemcpy(e->d_hkeys, keys.data(), sizeof(uint32_t) * keys.size(), hipMemcpyHostToDevice));
+  if (n_ops) HIP_TRY(upload(e, e->d_hops, ops, sizeof(kwk_metric_op) * n_ops));
+  if (n_buckets) HIP_TRY(upload(e, e->d_hbuckets, buckets, sizeof(kwk_metric_bucket) * n_buckets));
+  if (!keys.empty()) HIP_TRY(upload(e, e->d_hkeys, keys.data(), sizeof(uint32_t) * keys.size()));
   if (!bounds.empty())
-    HIP_TRY(hipMemcpy(e->d_hbounds, bounds.data(), sizeof(double) * bounds.size(), hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_hbounds, bounds.data(), sizeof(double) * bounds.size()));
   e->hists = hd;
   e->hist_inputs_needed = needs;
   return KWK_OK;
@@ -5558,10 +5574,10 @@ kwk_status kwk_usage_pods(kwk_engine* e, uint32_t enable) {
   HIP_TRY(hipMalloc(&e->d_pod_out, 32 * n));
   HIP_TRY(hipMalloc(&e->d_pod_cum, 16 * n));
   HIP_TRY(hipMalloc(&e->d_pod_last, 8 * n));
-  HIP_TRY(hipMemset(e->d_pod_out, 0, 32 * n));
-  HIP_TRY(hipMemset(e->d_pod_cum, 0, 16 * n));
+  HIP_TRY(hipMemsetAsync(e->d_pod_out, 0, 32 * n, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_pod_cum, 0, 16 * n, e->stream));
   std::vector<int64_t> lasts(n, INT64_MIN);
-  HIP_TRY(hipMemcpy(e->d_pod_last, lasts.data(), 8 * n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, e->d_pod_last, lasts.data(), 8 * n));
   return KWK_OK;
 }
 
@@ -5707,10 +5723,10 @@ kwk_status kwk_lease_config(kwk_engine* e, const kwk_lease_params* cfg) {
     HIP_TRY(hipMalloc(&e->d_lease_ops, sizeof(kwk_fired_rec) * (size_t)e->capacity));
     HIP_TRY(hipMalloc(&e->d_lease_nops, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&e->d_lease_stats, sizeof(unsigned long long) * 5));
-    HIP_TRY(hipMemset(e->d_lease, 0, sizeof(kwk_lease) * (size_t)e->capacity));
-    HIP_TRY(hipMemset(e->d_lease_op, 0, (size_t)e->capacity));
-    HIP_TRY(hipMemset(e->d_lease_nops, 0, 2 * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(e->d_lease_stats, 0, sizeof(unsigned long long) * 5));
+    HIP_TRY(hipMemsetAsync(e->d_lease, 0, sizeof(kwk_lease) * (size_t)e->capacity, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_lease_op, 0, (size_t)e->capacity, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_lease_nops, 0, 2 * sizeof(uint32_t), e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_lease_stats, 0, sizeof(unsigned long long) * 5, e->stream));
   }
   e->lease_cfg = *cfg;
   e->lease_on = true;
@@ -5724,7 +5740,7 @@ kwk_status kwk_lease_set(kwk_engine* e, uint32_t first, uint32_t n, const kwk_le
   if ((uint64_t)first + n > e->capacity) return fail(KWK_ECAP, "lease range beyond capacity");
   if (kwk_status st = set_dev(e)) return st;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  if (n) HIP_TRY(hipMemcpy(e->d_lease + first, leases, sizeof(kwk_lease) * n, hipMemcpyHostToDevice));
+  if (n) HIP_TRY(upload(e, e->d_lease + first, leases, sizeof(kwk_lease) * n));
   return KWK_OK;
 }
 
@@ -5782,8 +5798,8 @@ kwk_status kwk_lease_fail(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t
   HIP_TRY(hipStreamSynchronize(e->stream));
   kwk_lease* s_old = (kwk_lease*)e->d_stage_buf;
   uint32_t* s_slots = (uint32_t*)((char*)e->d_stage_buf + sizeof(kwk_lease) * n);
-  HIP_TRY(hipMemcpy(s_old, old, sizeof(kwk_lease) * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s_slots, slots, 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(upload(e, s_old, old, sizeof(kwk_lease) * n));
+  HIP_TRY(upload(e, s_slots, slots, 4 * (size_t)n));
   LeaseArgs a;
   a.lease = e->d_lease;
   a.op = e->d_lease_op;
@@ -5886,7 +5902,7 @@ kwk_status kwk_tick_bind(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_n
   if (pods->d_tick_ptr) HIP_TRY(hipFree(pods->d_tick_ptr));
   pods->d_tick_ptr = nullptr;
   HIP_TRY(hipMalloc(&pods->d_tick_ptr, 4 * ((size_t)n_nodes + 1)));
-  HIP_TRY(hipMemcpy(pods->d_tick_ptr, node_ptr, 4 * ((size_t)n_nodes + 1), hipMemcpyHostToDevice));
+  HIP_TRY(upload(pods, pods->d_tick_ptr, node_ptr, 4 * ((size_t)n_nodes + 1)));
   if (!pods->ev_lease) HIP_TRY(hipEventCreateWithFlags(&pods->ev_lease, hipEventDisableTiming));
   if (!pods->ev_podsync) HIP_TRY(hipEventCreateWithFlags(&pods->ev_podsync, hipEventDisableTiming));
   pods->tick_nodes = nodes;
