@@ -296,3 +296,61 @@ def test_step_n_equals_per_step_calls():
     finally:
         for e in engines.values():
             e.close()
+
+
+def test_fused_records_load_read_step_at_4m_pods():
+    """The fused records' due times at scale: 4M C2 pods loaded with a queued stage on every third
+    pod, its due time inside the 68.7 s window of the first step's epoch, years before it, or
+    hours after it (the due column), read back exactly (fold on load, decode on read), then
+    stepped with 20 s between steps (the epoch moves every step: re-encoded, far times to and
+    from the column) — the fused engine leaves every row and fires every transition exactly as
+    the 4-byte-word engine with its separate due column does."""
+    from kwok_amd import workload as W
+    from kwok_amd.host import abi
+    from kwok_amd.host.engine import Engine, Ingest
+    n = 4_000_000
+    prog = _c2_program(n)
+    pvars, pidx = W.c2_pod_variants(0, n, seed=0x6B776F6B, job_frac=0.1)
+    ing = Ingest(prog)
+    hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+    rng = np.random.default_rng(77)
+    now0 = 1_700_000_000 * 10**9
+    sel = np.arange(0, n, 3)
+    n_stages = len(prog.names)
+    hot["sched"][sel] = (hot["sched"][sel] & ~np.uint32(0xFF)) | rng.integers(0, n_stages, len(sel)).astype(np.uint32)
+    kind = rng.integers(0, 3, len(sel))
+    hot["due"][sel] = np.where(kind == 0, now0 + rng.integers(0, 60 * 10**9, len(sel)),
+                               np.where(kind == 1, now0 - 3 * 10**17, now0 + rng.integers(10**12, 10**13, len(sel))))
+    engs = {}
+    try:
+        for st in ("u32", "auto"):
+            eng = Engine(prog, capacity=n, state=st, max_records=max(1, len(ing.records)) + 16)
+            eng.load_stages()
+            eng.set_harness(True)
+            eng.load(hot, dels, rec, cls, ing.record_array())
+            engs[st] = eng
+        assert engs["auto"].stats()["state_bytes"] == 8 and engs["u32"].stats()["state_bytes"] == 4
+
+        def rows_equal(tag):
+            a, _ = engs["u32"].read()
+            b, _ = engs["auto"].read()
+            assert np.array_equal(a["pred"], b["pred"]) and np.array_equal(a["sched"], b["sched"]), tag
+            pend = (a["sched"] & 0xFF) != 0xFF
+            assert np.array_equal(a["due"][pend], b["due"][pend]), tag
+            return a, pend
+        a, pend = rows_equal("load")
+        assert np.array_equal(a["due"][sel], hot["due"][sel])  # read back exactly as loaded
+        for k in range(4):
+            now = now0 + k * 20 * 10**9
+            keys = []
+            for st in ("u32", "auto"):
+                engs[st].step(now, 0x6B776F6B, k)
+                f = engs[st].fired()
+                keys.append(np.sort(f["slot"].astype(np.uint64) << 32 | f["stage"].astype(np.uint64) << 16
+                                    | f["flags"].astype(np.uint64)))
+            assert engs["auto"].last_sweep()["kernel"] == abi.SWEEP_WD
+            assert np.array_equal(keys[0], keys[1]), f"step {k}: fired sets differ"
+            rows_equal(f"step {k}")
+    finally:
+        for e in engs.values():
+            e.close()
