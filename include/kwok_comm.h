@@ -37,7 +37,9 @@ kwk_status kwk_comm_init(const uint8_t id[KWK_COMM_ID_BYTES], int32_t rank, int3
                          kwk_comm** out);
 kwk_status kwk_comm_destroy(kwk_comm* c);
 /* a device buffer of n float64 owned by the communicator (reallocated when n grows): the target
- * of kwk_aggregate(eng, ..., out = *dev + offset, ...) for each engine */
+ * of kwk_aggregate(eng, ..., out = *dev + offset, ...) for each engine.  Growing it frees the
+ * previous buffer: every pointer an earlier call returned is invalid from then on (size the
+ * buffer once, for all the reports that share the communicator, before handing pointers out) */
 kwk_status kwk_comm_buffer(kwk_comm* c, uint64_t n, double** dev);
 /* in-place sum of the first n doubles of the buffer across all ranks, ordered after the work
  * queued on `engines` and before their later work (enqueue only) */

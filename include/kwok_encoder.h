@@ -44,6 +44,11 @@ kwk_status kwk_encoder_destroy(kwk_encoder* enc);
  * counted in *n_unknown_class); value records are interned across calls, in object order */
 kwk_status kwk_encode(kwk_encoder* enc, uint32_t n, const char* buf, const uint64_t* offsets, uint32_t n_threads,
                       kwk_hot* hot, int64_t* deletion_s, uint32_t* rec_idx, uint16_t* cls, uint32_t* n_unknown_class);
+/* classes_json: {class key: id} of classes the stage compiler registered after this encoder was
+ * created (a class first seen at run time, KWK_ENCODE_CLASS_UNKNOWN): later kwk_encode calls give
+ * their objects that id.  The record table is kept (ids already loaded stay valid); a known key
+ * must keep its id */
+kwk_status kwk_encoder_add_classes(kwk_encoder* enc, const char* classes_json);
 /* the interned records so far: n_records x (slots) kwk_value, for kwk_load / kwk_set_records */
 kwk_status kwk_encoder_records(kwk_encoder* enc, kwk_value* out, uint32_t cap, uint32_t* n_records);
 

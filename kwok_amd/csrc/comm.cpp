@@ -114,7 +114,10 @@ kwk_status kwk_comm_buffer(kwk_comm* c, uint64_t n, double** dev) {
     if (c->buf) HIP_OK(hipFree(c->buf));
     c->buf = nullptr;
     HIP_OK(hipMalloc(&c->buf, 8 * n));
-    HIP_OK(hipMemset(c->buf, 0, 8 * n));
+    // zeroed on the communicator's stream and complete on return: the engines write into the
+    // buffer from their own non-blocking streams, which would not wait for a null-stream memset
+    HIP_OK(hipMemsetAsync(c->buf, 0, 8 * n, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
     c->cap = n;
   }
   *dev = c->buf;

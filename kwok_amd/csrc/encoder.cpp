@@ -885,6 +885,23 @@ kwk_status kwk_encode(kwk_encoder* E, uint32_t n, const char* buf, const uint64_
   return KWK_OK;
 }
 
+kwk_status kwk_encoder_add_classes(kwk_encoder* E, const char* classes_json) {
+  ErrScope es_(E ? &E->err : nullptr);
+  if (!E || !classes_json) return fail(KWK_EINVAL, "null argument");
+  JV cls;
+  Parser P{classes_json, classes_json + strlen(classes_json)};
+  if (!P.value(cls) || cls.t != JV::OBJ) return fail(KWK_EINVAL, "classes: invalid JSON object");
+  for (size_t i = 0; i < cls.k.size(); ++i) {
+    if (cls.a[i].t != JV::NUM || !cls.a[i].is_int) return fail(KWK_EINVAL, "classes: ids must be integers");
+    const long id = atol(cls.a[i].s.c_str());
+    if (id < 0 || id >= 0xFFFF) return fail(KWK_EINVAL, "classes: id out of range");
+    const auto it = E->classes.find(cls.k[i]);
+    if (it != E->classes.end() && it->second != (uint32_t)id) return fail(KWK_EINVAL, "classes: a known class changes its id");
+    E->classes[cls.k[i]] = (uint32_t)id;
+  }
+  return KWK_OK;
+}
+
 kwk_status kwk_encoder_records(kwk_encoder* E, kwk_value* out, uint32_t cap, uint32_t* n_records) {
   ErrScope es_(E ? &E->err : nullptr);
   if (!E || !n_records) return fail(KWK_EINVAL, "null argument");

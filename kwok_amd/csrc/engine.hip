@@ -4442,8 +4442,7 @@ kwk_status kwk_load(kwk_engine* e, uint32_t n, const kwk_hot* hot, const int64_t
   HIP_TRY(upload(e, e->d_del, del, sizeof(int64_t) * n));
   HIP_TRY(upload(e, e->d_rec, rec, sizeof(uint32_t) * n));
   if (n_records)
-    HIP_TRY(hipMemcpy(e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots,
-                      hipMemcpyHostToDevice));
+    HIP_TRY(upload(e, e->d_values, records, sizeof(kwk_value) * (size_t)n_records * e->value_slots));
   if (n < e->n_active)
     HIP_TRY(hipMemsetAsync((char*)e->d_st + word_bytes(e->fmt) * n, 0, word_bytes(e->fmt) * (size_t)(e->n_active - n), e->stream));
   e->n_active = n;
@@ -4455,9 +4454,9 @@ kwk_status kwk_set_records(kwk_engine* e, uint32_t first, uint32_t n, const kwk_
   if (!e || (n && !records)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > e->max_records) return fail(KWK_ECAP, "records exceed max_records");
   if (kwk_status st = set_dev(e)) return st;
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(e->d_values + (size_t)first * e->value_slots, records, sizeof(kwk_value) * (size_t)n * e->value_slots,
-                    hipMemcpyHostToDevice));
+  // on the engine's stream (ordered after every enqueued sweep, complete on return): a pageable
+  // null-stream copy could still be in flight when the next sweep reads the records
+  HIP_TRY(upload(e, e->d_values + (size_t)first * e->value_slots, records, sizeof(kwk_value) * (size_t)n * e->value_slots));
   return KWK_OK;
 }
 
@@ -4800,9 +4799,9 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     // the fused records' epoch follows the clock: re-encoded (inside this sweep) once now is
     // more than 2^34 ns (~17 s) past it or before it, so that due times up to ~51 s ahead of now
     // stay in the 2^36 ns window
+    // (the host's epoch moves only once the re-encoding sweep is enqueued, below)
     const int64_t e0 = e->fmt.epoch;
     if (now_ns < e0 || (uint64_t)now_ns - (uint64_t)e0 > kDwRebase) {
-      e->fmt.epoch = now_ns;
       a.fmt.epoch = now_ns;
       a.dw_rebase = 1;
     }
@@ -4823,6 +4822,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   e->last_rec = kRecSlot;
   static_assert(kWavesPerBlock == 4, "region shift");
   HIP_TRY(hipGetLastError());
+  if (dw) e->fmt.epoch = a.fmt.epoch;  // the records now hold due times relative to it
   e->last_blocks = tiles;  // fired segments / wave counts are per (tile, wave)
   e->last_grid = blocks;
   e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
@@ -5667,6 +5667,9 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
     HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
   if (n_masks) {
     if (n_masks != e->agg_n_masks || memcmp(masks, e->agg_masks, 4 * (size_t)n_masks) != 0) {
+      // the previous masks' copy may still be queued on the stream (it reads e->agg_masks when
+      // it runs): drain it before the array is overwritten (masks change rarely)
+      HIP_TRY(hipStreamSynchronize(e->stream));
       memcpy(e->agg_masks, masks, 4 * (size_t)n_masks);
       e->agg_n_masks = n_masks;
       HIP_TRY(hipMemcpyAsync(e->d_agg_masks, e->agg_masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));

@@ -60,9 +60,12 @@ class NativeComm:
         self.rank, self.world = rank, world
 
     def buffer(self, n: int) -> int:
+        """The communicator's device buffer for n float64 (growing it frees the previous one:
+        a report holding an older pointer fails loudly in collect, see NativeReport)."""
         p = C.c_void_p()
         _check(lib().kwk_comm_buffer(self.h, n, C.byref(p)), "kwk_comm_buffer", self.h)
-        return int(p.value)
+        self.base = int(p.value)
+        return self.base
 
     def allreduce(self, n: int, engines):
         arr = (C.c_void_p * max(1, len(engines)))(*[e.h.value for e in engines])
@@ -97,6 +100,9 @@ class NativeReport:
         self.base = comm.buffer(self.n)
 
     def collect(self, now_ns: int):
+        if self.comm.base != self.base:
+            raise abi.EngineError("the communicator's buffer was reallocated by a larger report after this one "
+                                  "was created: size the buffer for every report first")
         off = 0
         L = self._layout
         for e, m, size in zip(self.engines, L.masks, L.sizes):

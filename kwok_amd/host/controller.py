@@ -124,7 +124,9 @@ class KindController:
                 self.objs[i] = new
             # every fired object's new state re-encoded by libkwok_encoder (the informer event's row)
             live = [(i, new, ch) for i, new, ch in applied if new is not None]
-            enc = self.nenc.columns([new for _, new, _ in live]) if live else None
+            # a class first seen now is registered with the compiler and the row re-encoded
+            # natively, so its record id points into the native encoder's record table
+            enc = self.nenc.columns([new for _, new, _ in live], register=True) if live else None
             self.last_rows = {}
             unknown = {int(rec["slot"]) for rec in fired if int(rec["flags"]) & abi.FIRED_DELTA_UNKNOWN}
             for j, (i, new, changed) in enumerate(live):
@@ -132,8 +134,6 @@ class KindController:
                 row = (int(h["pred"]), int(h["sched"]) & ~abi.STAGE_NONE, int(d), int(rc), int(c))
                 self.last_rows[i] = row
                 if i in unknown:
-                    if row[4] == 0xFFFF:  # a class the spec has not seen: the Python compiler registers it
-                        row = self.ing.encode(new)
                     slots.append(i)
                     rows.append((row, changed))
         else:

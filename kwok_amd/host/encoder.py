@@ -98,7 +98,9 @@ def lib():
         L.kwk_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
         L.kwk_encoder_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
-        for n in ("kwk_encoder_create", "kwk_encoder_destroy", "kwk_encode", "kwk_encoder_records"):
+        L.kwk_encoder_add_classes.argtypes = [C.c_void_p, C.c_char_p]
+        for n in ("kwk_encoder_create", "kwk_encoder_destroy", "kwk_encode", "kwk_encoder_records",
+                  "kwk_encoder_add_classes"):
             getattr(L, n).restype = C.c_int32
         _lib = L
     return _lib
@@ -152,8 +154,27 @@ class NativeIngest:
         self.unknown_classes = unknown.value
         return hot, dels, rec, cls
 
-    def columns(self, objs: Sequence):
-        return self.encode_buffer(*pack_json(objs))
+    def refresh_classes(self):
+        """Hand the classes the stage compiler registered since to the native encoder
+        (kwk_encoder_add_classes); its record table stays as it is."""
+        _check(lib().kwk_encoder_add_classes(self.h, json.dumps(dict(self.p.class_ids)).encode()),
+               "kwk_encoder_add_classes", self.h)
+
+    def columns(self, objs: Sequence, register: bool = False):
+        """register: objects of a class the compiler has not seen get it registered (their
+        deltas are then UNKNOWN until explored) and are re-encoded natively, so that every row's
+        record id points into this encoder's record table."""
+        out = self.encode_buffer(*pack_json(objs))
+        unknown = np.flatnonzero(out[3] == CLASS_UNKNOWN)
+        if register and len(unknown):
+            for i in unknown:
+                self.p.class_of(json.loads(objs[i]) if isinstance(objs[i], (bytes, bytearray)) else objs[i])
+            self.refresh_classes()
+            again = self.encode_buffer(*pack_json([objs[i] for i in unknown]))
+            for col, new in zip(out, again):
+                col[unknown] = new
+            assert not np.any(out[3] == CLASS_UNKNOWN)
+        return out
 
     def record_array(self) -> np.ndarray:
         ns = max(1, len(self.p.slots))

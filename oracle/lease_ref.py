@@ -93,8 +93,13 @@ class LeaseSim:
     them in parallel; they are independent)."""
 
     def __init__(self, leases: List[Lease], holder_id: int, lease_duration_s: int, renew_interval_ns: int,
-                 renew_jitter: float = 0.04, slot_base: int = 0, kind_salt: int = 1):
+                 renew_jitter: float = 0.04, slot_base: int = 0, kind_salt: int = 1, slots=None):
+        """slots: the engine slot of each lease (default leases[i] is slot i): a deterministic
+        sample of a large engine's nodes is simulated exactly (leases are independent, the Philox
+        counter is the global slot)."""
         self.leases = [replace(l) for l in leases]
+        self.slots = list(range(len(leases))) if slots is None else [int(x) for x in slots]
+        assert len(self.slots) == len(self.leases)
         self.me = holder_id
         self.duration_s = lease_duration_s
         self.renew_interval = renew_interval_ns
@@ -109,7 +114,7 @@ class LeaseSim:
         for i, L in enumerate(self.leases):
             if (L.flags & (HOLD | QUEUED)) != (HOLD | QUEUED) or L.next_try_ns > now_ns:
                 continue
-            dur = jitter(self.renew_interval, self.jitter, float64_hook(key, self.slot_base + i, step))
+            dur = jitter(self.renew_interval, self.jitter, float64_hook(key, self.slot_base + self.slots[i], step))
             now_us = now_ns - now_ns % 1000
             ok = False
             if L.flags & EXISTS:
@@ -148,7 +153,7 @@ class LeaseSim:
         that ran at (now_ns, step) was rejected; the cached lease stays `old`, the controller's
         hold / queue flags stay, AddWeightAfter(node, 1, dur) with the same dur."""
         key = seed ^ (self.kind_salt << 32)
-        dur = jitter(self.renew_interval, self.jitter, float64_hook(key, self.slot_base + i, step))
+        dur = jitter(self.renew_interval, self.jitter, float64_hook(key, self.slot_base + self.slots[i], step))
         ctl = self.leases[i].flags & (HOLD | QUEUED)
         L = replace(old)
         L.flags = (L.flags & ~(HOLD | QUEUED)) | ctl

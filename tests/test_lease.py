@@ -344,3 +344,107 @@ def test_tick_n_equals_separate_calls():
         for ne, pe in pairs:
             ne.close()
             pe.close()
+
+
+@pytest.mark.gpu
+def test_c3_config_size_tick_n_sampled_oracle():
+    """C3 at its configuration size: 100k nodes (node-initialize +
+    node-heartbeat 20 s / 25 s, leases 40 s with a 10 s +- 4 % renew) and 2 pod-fast pods per
+    node, driven by kwk_tick_n (lease step -> pod sync -> node step -> pod step per tick, the C3
+    bench's call) in calls of 1 and 3 ticks of 250 ms for 60 s.  Every 997th node and its pods
+    are simulated by the oracle (lease_ref.LeaseSim / OracleSim over the sampled slots: leases
+    are independent and the Philox counter is the global slot); after every call the last tick's
+    lease API writes, lease records, fired sets, object states and MANAGED flags of the sample
+    are bit-exact.  Reference: node_lease_controller.go:108-338, controller.go:285-288."""
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    from oracle.next_ref import load_stage_docs
+    from oracle.sim import OracleSim
+    from tests.parity_util import NOW0, compare_state
+    from tests.test_scale_oracle import _rows_at
+    n_nodes, ppn, me = 100_000, 2, 1
+    n_pods = n_nodes * ppn
+    rng = np.random.default_rng(36)
+    leases = c3_leases(n_nodes, NOW0, rng)
+    nfiles, pfiles = W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), W.stage_paths(W.POD_FAST)
+    nvars, pvars = [W.node_object("node")], [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+    nidx = np.zeros(n_nodes, dtype=np.int32)
+    pidx = (((np.arange(n_pods, dtype=np.int64) * 2654435761) >> 9) % 10 == 0).astype(np.int32)
+    node_ptr = np.arange(0, n_pods + 1, ppn, dtype=np.uint32)
+    held0 = np.array([LR.held(L, me) for L in leases])
+    engines = []
+    try:
+        progs = []
+        for files, variants, idx, harness, salt, cap in ((nfiles, nvars, nidx, False, 1, n_nodes),
+                                                         (pfiles, pvars, pidx, True, 0, n_pods)):
+            prog = KindProgram(load_stage_files(*files), HarnessSpec() if harness else None)
+            prog.explore(variants)
+            ing = Ingest(prog)
+            hot, dels, rec, cls = ing.variant_columns(variants, idx)
+            owner = np.arange(cap) if not harness else np.arange(cap) // ppn
+            hot["sched"][~held0[owner]] &= ~np.uint32(abi.F_MANAGED)  # readOnly until the lease is held
+            eng = Engine(prog, capacity=cap, kind_salt=salt)
+            engines.append(eng)
+            eng.load_stages()
+            eng.set_harness(harness)
+            eng.load(hot, dels, rec, cls, ing.record_array())
+            progs.append(prog)
+        neng, peng = engines
+        nprog, pprog = progs
+        neng.lease_config(me, 40, 10 * 10**9, 0.04)
+        neng.lease_set(to_array(leases))
+        peng.tick_bind(neng, node_ptr)
+        nslots = list(range(5, n_nodes, 997))
+        pslots = [p for i in nslots for p in range(int(node_ptr[i]), int(node_ptr[i + 1]))]
+        lsim = LR.LeaseSim([leases[i] for i in nslots], me, 40, 10 * 10**9, 0.04, kind_salt=1, slots=nslots)
+        nsim = OracleSim(load_stage_docs(*nfiles), [nvars[0]] * len(nslots), kind_salt=1, slots=nslots)
+        psim = OracleSim(load_stage_docs(*pfiles), [pvars[int(pidx[p])] for p in pslots], harness=True, slots=pslots)
+        for j, i in enumerate(nslots):
+            nsim.managed[j] = bool(held0[i])
+            for q in range(ppn):
+                psim.managed[j * ppn + q] = bool(held0[i])
+        nset, pset = np.asarray(nslots, dtype=np.int64), np.asarray(pslots, dtype=np.int64)
+        seed, dt, k, call = 0x7A, 250 * 10**6, 0, 0
+        counts = {"ops": 0, "node": 0, "pod": 0}
+        while k < 240:
+            n = 1 if call % 2 == 0 else 3
+            neng.tick_n(peng, n, NOW0 + k * dt, dt, seed, k, compact=True)
+            for t in range(k, k + n):
+                now = NOW0 + t * dt
+                ops = lsim.step(now, seed, t)
+                for j, op in ops:
+                    h = LR.held(lsim.leases[j], me)
+                    nsim.set_managed(j, h, op != LR.OP_BUSY)
+                    for q in range(ppn):
+                        psim.set_managed(j * ppn + q, h, op != LR.OP_BUSY)
+                nexp = nsim.step(now, seed, t)
+                pexp = psim.step(now, seed, t)
+            k += n
+            call += 1
+            got_ops = neng.lease_ops()
+            sel = got_ops[np.isin(got_ops["slot"].astype(np.int64), nset)]
+            assert sorted((int(r["slot"]), int(r["stage"])) for r in sel) == \
+                sorted((nslots[j], op) for j, op in ops), f"tick {k - 1}: lease ops"
+            got_leases = np.concatenate([neng.lease_read(i, 1) for i in nslots])
+            assert_leases_equal(got_leases, lsim.leases, k - 1)
+            for eng, sim, prog, sset, exp, name in ((neng, nsim, nprog, nset, nexp, "node"),
+                                                    (peng, psim, pprog, pset, pexp, "pod")):
+                f = eng.fired()
+                f = f[np.isin(f["slot"].astype(np.int64), sset)]
+                assert sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in f) == sorted(exp), \
+                    f"tick {k - 1}: {name} fired"
+                rows = _rows_at(eng, sim.slots)
+                compare_state(prog, eng, sim, k - 1, rows=rows)
+                assert [bool(x & abi.F_MANAGED) for x in rows[0]["sched"]] == sim.managed, f"tick {k - 1}: {name} managed"
+                counts[name] += len(exp)
+            counts["ops"] += len(ops)
+        st = neng.lease_stats()
+        assert st["creates"] > 40_000 and st["renews"] > 0 and st["acquires"] > 0 and st["busy"] > 0, st
+        assert counts["ops"] > 0 and counts["node"] > 0 and counts["pod"] > 0, counts
+        per = neng.stats()["fired_per_stage"]
+        assert per["node-heartbeat"] > 0, per
+    finally:
+        for e in engines:
+            e.close()

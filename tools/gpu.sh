@@ -1,0 +1,91 @@
+# The one GPU runner (replaces round 1-3's per-call scripts; see profiles/r*/README.md for what
+# each call produced).  Runs on the gpurun box from the repo root; every GPU step has its own
+# time limit and the steps are chained: the first failing step ends the call.
+#
+# Usage: bash tools/gpu.sh <tag> <step> [<step> ...]      outputs under gpurun_out/<tag>/
+#   tests[=<pytest -k expr>]   GPU test suite (or a selection)
+#   smoke                      __graft_entry__.smoke()
+#   bench[=<bench.py args>]    the driver's bench command (default --gpus 1 --steps 20 --warmup 5)
+#   prof                       kernel trace + stats of the driver's bench command (kernel_stats.csv)
+#   configs                    bench.py --config C1..C4 lines (configs_C1_C4.jsonl)
+#   c2prof                     C2 working set: kernel trace + FETCH_SIZE / WRITE_SIZE passes
+#   sq                         SQ counter passes over the C5 pod sweep and the C2 word sweep
+#   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/build/<so>, alternating x2
+#   variants=<args>            tools/variants.py run <args> (cost-isolation builds)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; T=$1; shift; O=$R/gpurun_out/$T
+mkdir -p $O && cd $R
+TRACE() { cd /tmp && export TMPDIR=/tmp; }
+B1="--gpus 1 --steps 20 --warmup 5"
+for step in "$@"; do
+  name=${step%%=*}; arg=""; [ "$name" != "$step" ] && arg=${step#*=}
+  echo "== $name $arg"
+  case $name in
+    tests)
+      K=(); [ -n "$arg" ] && K=(-k "$arg")
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+        > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+      tail -2 $O/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 500 python -u bench.py ${arg:-$B1} > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$O/bench.json').read().splitlines()[-1]);r=d['roofline'];print(d['value'],d['ms_per_step'],r.get('avg_launch_us'),r['frac'],r['traffic'],r.get('line_frac'))
+h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_us'),h.get('frac'),h.get('line_frac'));print('pcie',d.get('pcie_inclusive'))" ;;
+    prof)
+      TRACE
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py $B1 --no-pmc --no-cpu-baseline \
+        > $O/prof_bench.json 2> $O/prof_bench.err || { tail -30 $O/prof_bench.err; exit 1; }
+      cd $R && python tools/rocpd_summary.py stats $(find $O/prof -name '*.db' | head -1) $O/kernel_stats.csv && cut -c1-150 $O/kernel_stats.csv | head -14 ;;
+    configs)
+      for c in C1 C2 C3 C4; do
+        timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 5 >> $O/configs_C1_C4.jsonl 2> $O/config_$c.err || { tail -30 $O/config_$c.err; exit 1; }
+        tail -1 $O/configs_C1_C4.jsonl | cut -c1-300
+      done ;;
+    c2prof)
+      TRACE
+      H="$R/bench.py --hbm-only --hbm-steps 4 --hbm-warmup 12"
+      timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/c2fetch -o run -- python3 $H > $O/c2fetch.log 2>&1 || { tail -20 $O/c2fetch.log; exit 1; }
+      timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/c2write -o run -- python3 $H > $O/c2write.log 2>&1 || { tail -20 $O/c2write.log; exit 1; }
+      timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/c2trace -o run -- python3 $R/bench.py --hbm-only --hbm-steps 10 --hbm-warmup 12 \
+        > $O/c2trace.log 2>&1 || { tail -20 $O/c2trace.log; exit 1; }
+      cd $R
+      for c in fetch write; do python tools/rocpd_summary.py pmc $(find $O/c2$c -name '*.db' | head -1) sweepw > $O/c2$c.txt; done
+      python tools/rocpd_summary.py stats $(find $O/c2trace -name '*.db' | head -1) $O/c2_kernel_stats.csv && cut -c1-150 $O/c2_kernel_stats.csv | head -6
+      cut -c1-200 $O/c2fetch.txt $O/c2write.txt ;;
+    sq)
+      TRACE
+      B="$R/bench.py --pmc-child --steps 6 --warmup 4 --no-cpu-baseline"
+      H="$R/bench.py --hbm-only --hbm-steps 4 --hbm-warmup 12"
+      S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
+      S2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+      for p in 1 2; do
+        S=S$p
+        timeout -s KILL 150 rocprofv3 --pmc ${!S} -d $O/c5sq$p -o run -- python3 $B > $O/c5sq$p.log 2>&1 || { tail -20 $O/c5sq$p.log; exit 1; }
+        timeout -s KILL 200 rocprofv3 --pmc ${!S} -d $O/c2sq$p -o run -- python3 $H > $O/c2sq$p.log 2>&1 || { tail -20 $O/c2sq$p.log; exit 1; }
+      done
+      cd $R
+      for d in c5sq1 c5sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweep8; done > $O/c5_sq.txt
+      for d in c2sq1 c2sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweepw; done > $O/c2_sq.txt
+      cat $O/c5_sq.txt $O/c2_sq.txt ;;
+    ab)
+      cp kwok_amd/lib/libkwok_engine.so $O/cur.so
+      for i in 1 2; do
+        for v in cur other; do
+          if [ $v = other ]; then cp tools/build/$arg kwok_amd/lib/libkwok_engine.so; else cp $O/cur.so kwok_amd/lib/libkwok_engine.so; fi
+          timeout -k 10 200 python -u bench.py $B1 --no-pmc --no-cpu-baseline > $O/${v}_$i.json 2> $O/${v}_$i.err \
+            || { cp $O/cur.so kwok_amd/lib/libkwok_engine.so; tail -20 $O/${v}_$i.err; exit 1; }
+          python -c "import json; d=json.load(open('$O/${v}_$i.json')); print('$v', $i, d['value'], 'ms/step', d['ms_per_step'], 'sweep us', d['detail']['pod_sweep_us_mean'])"
+        done
+      done
+      cp $O/cur.so kwok_amd/lib/libkwok_engine.so && rm -f $O/cur.so ;;
+    variants)
+      timeout -k 10 600 python -u tools/variants.py run $arg > $O/variants.jsonl 2> $O/variants.err || { tail -30 $O/variants.err; exit 1; }
+      cut -c1-300 $O/variants.jsonl ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+  cd $R
+done
+echo "gpu.sh $T done"
