@@ -15,11 +15,17 @@ HDR = [os.path.join(ROOT, "include", "kwok_engine.h")]
 OUT = os.path.join(PKG, "lib", "libkwok_engine.so")
 DOM_HDR = os.path.join(PKG, "csrc", "json_dom.hpp")
 ENC_SRC = [os.path.join(PKG, "csrc", "encoder.cpp")]
-ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
+ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR,
+           os.path.join(PKG, "csrc", "host_common.hpp"), os.path.join(PKG, "csrc", "nextstate.hpp"),
+           os.path.join(PKG, "csrc", "gotpl.hpp")]
 ENC_OUT = os.path.join(PKG, "lib", "libkwok_encoder.so")
 PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
 PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
 PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
+COMPILER_SRC = [os.path.join(PKG, "csrc", "compiler.cpp")]
+COMPILER_HDR = [os.path.join(ROOT, "include", "kwok_compiler.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR] + \
+    [os.path.join(PKG, "csrc", h) for h in ("host_common.hpp", "gotpl.hpp", "patchtpl.hpp", "nextstate.hpp")]
+COMPILER_OUT = os.path.join(PKG, "lib", "libkwok_compiler.so")
 COMM_SRC = [os.path.join(PKG, "csrc", "comm.cpp")]
 COMM_HDR = [os.path.join(ROOT, "include", "kwok_comm.h"), os.path.join(ROOT, "include", "kwok_engine.h")]
 COMM_OUT = os.path.join(PKG, "lib", "libkwok_comm.so")
@@ -52,6 +58,11 @@ def build_encoder(force: bool = False, verbose: bool = False) -> str:
     return _host_lib(ENC_OUT, ENC_SRC, ENC_HDR, force, verbose)
 
 
+def build_compiler(force: bool = False, verbose: bool = False) -> str:
+    """The native Stage compiler (lifecycle.NewLifecycle behind the C ABI)."""
+    return _host_lib(COMPILER_OUT, COMPILER_SRC, COMPILER_HDR, force, verbose)
+
+
 def build_patch(force: bool = False, verbose: bool = False) -> str:
     """The native patch renderer (precompiled merge-patch byte templates)."""
     return _host_lib(PATCH_OUT, PATCH_SRC, PATCH_HDR, force, verbose)
@@ -74,6 +85,7 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     build_encoder(force, verbose)
+    build_compiler(force, verbose)
     if os.path.exists(PATCH_SRC[0]):
         build_patch(force, verbose)
     _build_engine(force, verbose)

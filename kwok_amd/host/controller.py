@@ -49,7 +49,8 @@ class KindController:
             from .encoder import NativeIngest
             from .patchtpl import PatchProgram
             self.nenc = NativeIngest(program, n_threads=n_threads)
-            self.patcher = PatchProgram(program.stages, self.funcs, n_threads=n_threads)
+            native_prog = program if hasattr(program, "patch_spec") else None  # libkwok_compiler's spec
+            self.patcher = PatchProgram(program.stages, self.funcs, n_threads=n_threads, program=native_prog)
 
     def close(self):
         if self.native:

@@ -72,6 +72,8 @@ def query_steps(src: str) -> List[list]:
 
 
 def encoder_spec(program: KindProgram) -> str:
+    if hasattr(program, "encoder_spec"):  # native_compiler.NativeProgram: libkwok_compiler writes it
+        return program.encoder_spec()
     if program.applied_bits:
         raise EncoderUnsupported("'patch already applied' features need the host renderer")
     feats = [{"steps": query_steps(f.src), "present_bit": f.present_bit, "literals": dict(f.lit_bits)}

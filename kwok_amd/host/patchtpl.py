@@ -565,7 +565,9 @@ class PatchProgram:
     """
 
     def __init__(self, stages, funcs: Optional[Dict[str, object]] = None, version: str = "v0.6.0",
-                 n_threads: int = 1):
+                 n_threads: int = 1, program=None):
+        """program: a native_compiler.NativeProgram — the spec and template ids come from
+        libkwok_compiler (kwk_program_patch_spec) instead of this module's compiler."""
         funcs = dict(funcs or {})
         self.n_threads = n_threads
         self.callbacks: Dict[int, Callable] = {}
@@ -583,6 +585,16 @@ class PatchProgram:
         self.template_of: Dict[Tuple[int, int], int] = {}   # (stage index, patch index) -> template id
         self.unsupported: Dict[Tuple[int, int], str] = {}
         self.stages = list(stages)
+        if program is not None:
+            self.spec, self.template_of = program.patch_spec(funcs, version)
+            for si, st in enumerate(self.stages):
+                for pi in range(len(st.next.patches)):
+                    if (si, pi) not in self.template_of:
+                        self.unsupported[(si, pi)] = "not compiled by libkwok_compiler"
+            self.h = C.c_void_p()
+            _check(lib().kwk_patcher_create(self.spec.encode(), C.byref(self.h)), "kwk_patcher_create")
+            self._fn = _FN(self._callback)
+            return
         for si, st in enumerate(self.stages):
             for pi, p in enumerate(st.next.patches):
                 if p.type not in ("merge", "strategic"):

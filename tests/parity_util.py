@@ -33,20 +33,35 @@ def expected_state_bytes(prog, state="auto"):
     return {4} if bits <= 32 else {8}
 
 
-def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto", tuning=None):
-    stages = load_stage_files(*stage_files)
-    prog = KindProgram(stages, HarnessSpec() if harness else None)
-    prog.explore(objs)
-    assert not prog.delta_conflicts, prog.delta_conflicts
-    ing = Ingest(prog)
-    hot, dels, rec, cls = ing.columns(objs)
+def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto", tuning=None,
+          compiler="python"):
+    """compiler: "python" (KindProgram + the Python Ingest) or "native" (libkwok_compiler's
+    kwk_compile_stages / kwk_program_explore, rows from libkwok_encoder built from its spec: the
+    Go host's path, no Python compiler involved)."""
+    if compiler == "native":
+        from kwok_amd.host.encoder import NativeIngest
+        from kwok_amd.host.native_compiler import NativeProgram, stage_docs_from_files
+        prog = NativeProgram(stage_docs_from_files(*stage_files), HarnessSpec() if harness else None)
+        prog.explore(objs)
+        ing = NativeIngest(prog)
+        hot, dels, rec, cls = ing.columns(objs, register=True)
+        records = ing.record_array()
+        ing.close()
+    else:
+        stages = load_stage_files(*stage_files)
+        prog = KindProgram(stages, HarnessSpec() if harness else None)
+        prog.explore(objs)
+        assert not prog.delta_conflicts, prog.delta_conflicts
+        ing = Ingest(prog)
+        hot, dels, rec, cls = ing.columns(objs)
+        records = ing.record_array()
     eng = Engine(prog, capacity=max(1, len(objs)), kind_salt=kind_salt, slot_base=slot_base, wide_state=wide_state,
-                 state=state)
+                 state=state, max_records=max(1 << 16, len(records) + 16))
     for k, v in (tuning or {}).items():
         eng.set_tuning(k, v)
     eng.load_stages()
     eng.set_harness(harness)
-    eng.load(hot, dels, rec, cls, ing.record_array())
+    eng.load(hot, dels, rec, cls, records)
     sim = OracleSim(load_stage_docs(*stage_files), objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base)
     return prog, eng, sim
 
@@ -90,12 +105,13 @@ def compare_state(prog, eng, sim, step, rows=None):
 
 
 def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False,
-        state="auto", tuning=None, expect_kernel=None, nows=None):
+        state="auto", tuning=None, expect_kernel=None, nows=None, compiler="python"):
     """expect_kernel: the abi.SWEEP_* every step must launch (the shape under test); nows: the
     clock of each step (default NOW0 + k * dt_ns)."""
     if wide_state:
         state = "wide"
-    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state, tuning=tuning)
+    prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state, tuning=tuning,
+                           compiler=compiler)
     total = 0
     per_stage = np.zeros(len(prog.names), dtype=np.int64)
     try:

@@ -16,7 +16,7 @@ from kwok_amd.host import abi
 pytestmark = pytest.mark.gpu
 
 
-def _run(cl, steps, dt_ns, seed):
+def _run(cl, steps, dt_ns, seed, compiler="python"):
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.controller import KindController
     from kwok_amd.host.encoder import NativeIngest
@@ -26,13 +26,18 @@ def _run(cl, steps, dt_ns, seed):
     from oracle.sim import OracleSim, oracle_pred
     from tests.parity_util import NOW0, compare_state
     objs = cl.pods.materialize()
-    prog = KindProgram(load_stage_files(*cl.pod_stage_files))
+    if compiler == "native":  # the Go host's path: libkwok_compiler, no Python compiler
+        from kwok_amd.host.native_compiler import NativeProgram, stage_docs_from_files
+        prog = NativeProgram(stage_docs_from_files(*cl.pod_stage_files))
+        ing = None
+    else:
+        prog = KindProgram(load_stage_files(*cl.pod_stage_files))
+        ing = Ingest(prog)
     prog.explore(objs)
-    ing = Ingest(prog)
     # the initial list too goes through the native encoder
     nat = NativeIngest(prog)
     hot, dels, rec, cls = nat.columns(objs)
-    eng = Engine(prog, capacity=len(objs), max_records=max(1, len(ing.records)) + 64)
+    eng = Engine(prog, capacity=len(objs), max_records=len(nat.record_array()) + 64)
     ctl = KindController(prog, eng, ing, objs, native=True)
     sim = OracleSim(load_stage_docs(*cl.pod_stage_files), objs)
     desc = prog.describe()
@@ -72,3 +77,17 @@ def test_native_controller_c2_pod_general():
     cl = W.make_cluster("C2", 30, 400, seed=62)
     checked, ctl = _run(cl, steps=30, dt_ns=500 * 10**6, seed=0x62)
     assert checked >= 400
+
+
+@pytest.mark.parametrize("config", ["C1", "C2"])
+def test_native_controller_with_native_compiler(config):
+    """The whole Go-host path with no Python compiler: libkwok_compiler's table / deltas / encoder
+    spec / patch spec, libkwok_encoder rows, libkwok_patch renders, the engine — stepped beside the
+    oracle (fired sets, host object cache = oracle objects, re-encoded feature bits)."""
+    if config == "C1":
+        checked, ctl = _run(W.make_cluster("C1", 20, 300, seed=63), steps=6, dt_ns=10**9, seed=0x63, compiler="native")
+        assert checked >= 300 and ctl.host_renders == 0
+    else:
+        checked, ctl = _run(W.make_cluster("C2", 30, 400, seed=64), steps=30, dt_ns=500 * 10**6, seed=0x64,
+                            compiler="native")
+        assert checked >= 400

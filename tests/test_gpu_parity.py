@@ -101,6 +101,34 @@ def test_node_fast_heartbeat(state):
     assert per["node-initialize"] == 64 and per["node-heartbeat"] > 0
 
 
+@pytest.mark.parametrize("case", ["pod-fast", "pod-general", "node-heartbeat", "node-chaos"])
+def test_native_compiler_tables_parity(case):
+    """The engine loaded from the NATIVE Stage compiler (kwk_compile_stages / kwk_program_explore /
+    kwk_program_table / _deltas / _harness) with rows from libkwok_encoder built from its spec —
+    the Go host's path, no Python compiler — bit-exact against the oracle at every step: pod-fast
+    (1-byte ids), pod-general + chaos (fused records, value records), node-fast + node-heartbeat
+    ("patch already applied" bits evaluated by the native encoder) and node-chaos (weights)."""
+    if case == "pod-fast":
+        cl = W.make_cluster("C1", 30, 300, seed=71)
+        run(cl.pod_stage_files, cl.pods.materialize(), steps=10, dt_ns=10**9, harness=True, compiler="native",
+            expect_kernel=abi.SWEEP_8)
+    elif case == "pod-general":
+        cl = W.make_cluster("C2", 40, 500, seed=72)
+        run(cl.pod_stage_files, cl.pods.materialize(), steps=36, dt_ns=500 * 10**6, harness=True, compiler="native",
+            expect_kernel=abi.SWEEP_WD)
+    elif case == "node-heartbeat":
+        cl = W.make_cluster("C1", 64, 64, seed=73)
+        _, per = run(cl.node_stage_files, cl.nodes.materialize(), steps=30, dt_ns=2 * 10**9, kind_salt=1,
+                     compiler="native")
+        assert per["node-initialize"] == 64 and per["node-heartbeat"] > 0
+    else:
+        objs = [W.node_object(f"node-{i}", labels={"node-not-ready.stage.kwok.x-k8s.io": "true"} if i % 3 == 0 else None,
+                              annotations={"node-not-ready.stage.kwok.x-k8s.io/weight": str(i % 5)} if i % 2 else None)
+                for i in range(90)]
+        run(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT + W.NODE_CHAOS), objs, steps=25, dt_ns=3 * 10**9, kind_salt=1,
+            compiler="native")
+
+
 def test_node_chaos_weights():
     """node-not-ready (weight 10000) beside node-heartbeat (weight 0): weighted pick path."""
     objs = [W.node_object(f"node-{i}", labels={"node-not-ready.stage.kwok.x-k8s.io": "true"} if i % 3 == 0 else None,
