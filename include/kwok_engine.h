@@ -131,7 +131,11 @@ typedef struct {
   uint32_t version;
   uint32_t pred_bits;          /* feature bits in use: pred < 2^pred_bits (0 = all 32).  With the class
                                 * and stage counts this picks the device state format */
-  uint32_t reserved[3];
+  uint32_t disregard_mask;     /* need() (pod_controller.go:392-409, node_controller.go:153-166): a changed
+                                * object with a pred bit in this mask is not re-matched (its watch event
+                                * is skipped: disregardStatusWith{Annotation,Label}Selector); a queued
+                                * stage stays queued.  0 = no disregard selectors */
+  uint32_t reserved[2];
   kwk_stage_desc stages[KWK_MAX_STAGES];
 } kwk_stage_table;
 

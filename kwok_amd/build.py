@@ -17,14 +17,14 @@ DOM_HDR = os.path.join(PKG, "csrc", "json_dom.hpp")
 ENC_SRC = [os.path.join(PKG, "csrc", "encoder.cpp")]
 ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR,
            os.path.join(PKG, "csrc", "host_common.hpp"), os.path.join(PKG, "csrc", "nextstate.hpp"),
-           os.path.join(PKG, "csrc", "gotpl.hpp")]
+           os.path.join(PKG, "csrc", "gotpl.hpp"), os.path.join(PKG, "csrc", "labelsel.hpp")]
 ENC_OUT = os.path.join(PKG, "lib", "libkwok_encoder.so")
 PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
 PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
 PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
 COMPILER_SRC = [os.path.join(PKG, "csrc", "compiler.cpp")]
 COMPILER_HDR = [os.path.join(ROOT, "include", "kwok_compiler.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR] + \
-    [os.path.join(PKG, "csrc", h) for h in ("host_common.hpp", "gotpl.hpp", "patchtpl.hpp", "nextstate.hpp")]
+    [os.path.join(PKG, "csrc", h) for h in ("host_common.hpp", "gotpl.hpp", "patchtpl.hpp", "nextstate.hpp", "labelsel.hpp")]
 COMPILER_OUT = os.path.join(PKG, "lib", "libkwok_compiler.so")
 COMM_SRC = [os.path.join(PKG, "csrc", "comm.cpp")]
 COMM_HDR = [os.path.join(ROOT, "include", "kwok_comm.h"), os.path.join(ROOT, "include", "kwok_engine.h")]

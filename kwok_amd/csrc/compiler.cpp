@@ -28,6 +28,7 @@
 #include "../../include/kwok_engine.h"
 #include "gotpl.hpp"
 #include "host_common.hpp"
+#include "labelsel.hpp"
 #include "nextstate.hpp"
 #include "patchtpl.hpp"
 
@@ -611,6 +612,8 @@ struct kwk_program {
   std::string terminal_query = ".status.phase", deletion_query = ".metadata.deletionTimestamp";
   std::vector<std::string> terminal_values{"Succeeded", "Failed"};
   uint32_t deletion_bit = 0, terminal_mask = 0, keep_mask = 0;
+  kwklabels::Disregard disregard;  // need()'s selectors (options "disregard")
+  int disregard_bit = -1;
 
   std::vector<std::string> class_keys;  // id -> key
   std::map<std::string, uint32_t> class_ids;
@@ -812,7 +815,8 @@ struct kwk_program {
       deletion_bit = present(deletion_query);
       terminal_mask = lits(terminal_query, terminal_values);
     }
-    uint32_t keep = 0;
+    if (disregard.active()) disregard_bit = bit();  // labels / annotations: kept on re-creation
+    uint32_t keep = disregard_bit < 0 ? 0u : 1u << disregard_bit;
     for (const std::string& key : feature_order) {
       const Feature& f = features.at(key);
       const std::vector<std::string> p = path_prefix(f.src);
@@ -864,6 +868,7 @@ struct kwk_program {
     }
     for (const auto& sb : applied_bits)
       if (patch_applied(stages[(size_t)sb.first], obj)) pred |= 1u << sb.second;
+    if (disregard_bit >= 0 && disregard.disregarded(obj)) pred |= 1u << disregard_bit;
     return pred;
   }
 
@@ -1057,10 +1062,19 @@ struct kwk_program {
                .set("finalizer_other_bit", fin_other_bit < 0 ? PJ::null() : PJ::integer(fin_other_bit))
                .set("value_slots", vs)
                .set("classes", PJ::integer((long long)class_keys.size()))
-               .set("uses_deletion_column", PJ::boolean(uses_deletion_column()));
+               .set("uses_deletion_column", PJ::boolean(uses_deletion_column()))
+               .set("disregard", disregard_pj());
     std::string o;
     kwkpatch::pj_dump(o, d);
     return o;
+  }
+
+  PJ disregard_pj() const {
+    if (disregard_bit < 0) return PJ::null();
+    return PJ::dict()
+        .set("bit", PJ::integer(disregard_bit))
+        .set("annotation_selector", PJ::str(disregard.ann_text))
+        .set("label_selector", PJ::str(disregard.lab_text));
   }
 
   std::string encoder_spec() const {
@@ -1090,6 +1104,7 @@ struct kwk_program {
                .set("slots", sl)
                .set("classes", cls)
                .set("identity_meta", im);
+    if (disregard_bit >= 0) d.set("disregard", disregard_pj());
     if (!applied_bits.empty()) {
       // "patch already applied" bits (the host encoder_spec rejects them): the encoder renders the
       // stage's patches with the static renderer and compares, as KindProgram._patch_applied
@@ -1191,6 +1206,11 @@ kwk_status kwk_compile_stages(const char* stages_json, const char* options_json,
     for (const Stage& s : P->stages) P->names.push_back(s.name);
     if (options_json) {
       const JV opt = parse_json(options_json, options_json + strlen(options_json), "options");
+      if (const JV* dg = opt.get("disregard"); dg && dg->t == JV::OBJ) {
+        const JV* a = dg->get("annotation_selector");
+        const JV* l = dg->get("label_selector");
+        P->disregard = kwklabels::Disregard(a && a->t == JV::STR ? a->s : "", l && l->t == JV::STR ? l->s : "");
+      }
       if (const JV* h = opt.get("harness"); h && h->t != JV::NUL && !(h->t == JV::BOOL && !h->b)) {
         P->harness = true;
         if (h->t == JV::OBJ) {
@@ -1247,6 +1267,7 @@ kwk_status kwk_program_table(const kwk_program* p, uint32_t version, kwk_stage_t
   out->n_classes = p->class_keys.empty() ? 1u : (uint32_t)p->class_keys.size();
   out->version = version;
   out->pred_bits = (uint32_t)p->nbits;
+  out->disregard_mask = p->disregard_bit < 0 ? 0u : 1u << p->disregard_bit;
   for (size_t i = 0; i < p->desc.size(); ++i) out->stages[i] = p->desc[i];
   return KWK_OK;
 }

@@ -27,6 +27,7 @@
 #include "../../include/kwok_engine.h"
 #include "../../include/kwok_encoder.h"
 #include "host_common.hpp"
+#include "labelsel.hpp"
 #include "nextstate.hpp"
 
 namespace {
@@ -333,6 +334,8 @@ struct kwk_encoder {
     std::vector<kwknext::Patch> patches;
   };
   std::vector<Applied> applied;
+  kwklabels::Disregard disregard;  // need()'s selectors -> one feature bit
+  int disregard_bit = -1;
   std::unordered_map<std::string, uint32_t> classes;
   std::vector<std::string> identity_meta;
   // interned value records (kwk_value x slots each), in order of first appearance
@@ -376,6 +379,7 @@ void encode_one(const kwk_encoder& E, const char* text, uint32_t len, Row& r, kw
   }
   for (const auto& ap : E.applied)
     if (kwknext::patch_applied(ap.patches, obj, *R)) r.pred |= 1u << ap.bit;
+  if (E.disregard_bit >= 0 && E.disregard.disregarded(obj)) r.pred |= 1u << E.disregard_bit;
   const JV* md = obj.get("metadata");
   if (E.fin_other_bit >= 0 && md && md->t == JV::OBJ) {
     if (const JV* fins = md->get("finalizers"))
@@ -491,6 +495,19 @@ kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out) {
       }
       E->applied.push_back(std::move(A));
     }
+  if (const JV* dg = spec.get("disregard"); dg && dg->t == JV::OBJ) {
+    const JV* bit = dg->get("bit");
+    const JV* a = dg->get("annotation_selector");
+    const JV* l = dg->get("label_selector");
+    if (!bit || bit->t != JV::NUM || !a || a->t != JV::STR || !l || l->t != JV::STR)
+      return fail(KWK_EINVAL, "encoder spec: disregard");
+    try {
+      E->disregard = kwklabels::Disregard(a->s, l->s);
+    } catch (const std::exception& ex) {
+      return fail(KWK_EINVAL, std::string("encoder spec: disregard selector: ") + ex.what());
+    }
+    E->disregard_bit = atoi(bit->s.c_str());
+  }
   if (const JV* im = spec.get("identity_meta"))
     for (const JV& k : im->a) E->identity_meta.push_back(k.s);
   *out = E.release();

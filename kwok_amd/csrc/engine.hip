@@ -530,8 +530,15 @@ __device__ __forceinline__ uint2 process_object(const SweepArgs& a, const kwk_st
   bool scheduled = false;
   if (sched & KWK_F_ALIVE) {
     if (sched & KWK_F_DIRTY) {
-      scheduled = match_object<kProbe>(a, T, n_stages, i, pred, sched, due, f.bytes, lut, lut_n, gen);
-      n_matched += scheduled ? 1 : 0;
+      if (pred & T->disregard_mask) {
+        // need() is false (disregardStatusWith{Annotation,Label}Selector, pod_controller.go:397-407,
+        // node_controller.go:153-166): watchResources skips the event — no re-match, a queued job
+        // stays queued (it still fires)
+        sched &= ~KWK_F_DIRTY;
+      } else {
+        scheduled = match_object<kProbe>(a, T, n_stages, i, pred, sched, due, f.bytes, lut, lut_n, gen);
+        n_matched += scheduled ? 1 : 0;
+      }
     }
     const uint32_t st = sched & 0xFFu;
     if (a.fire && st < n_stages && due <= a.now) fire_object(a, T, deltas, n_stages, fin_group, sched >> KWK_CLASS_SHIFT, st,

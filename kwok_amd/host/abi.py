@@ -52,7 +52,8 @@ class StageDesc(C.Structure):
 
 class StageTable(C.Structure):
     _fields_ = [("n_stages", C.c_uint32), ("fin_group_mask", C.c_uint32), ("n_classes", C.c_uint32),
-                ("version", C.c_uint32), ("pred_bits", C.c_uint32), ("reserved", C.c_uint32 * 3),
+                ("version", C.c_uint32), ("pred_bits", C.c_uint32), ("disregard_mask", C.c_uint32),
+                ("reserved", C.c_uint32 * 2),
                 ("stages", StageDesc * MAX_STAGES)]
 
 

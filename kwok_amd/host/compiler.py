@@ -138,13 +138,18 @@ def exploration_funcs():
 class KindProgram:
     """Compiled Stage set for one resourceRef (one engine)."""
 
-    def __init__(self, stages: Sequence[Stage], harness: Optional[HarnessSpec] = None):
+    def __init__(self, stages: Sequence[Stage], harness: Optional[HarnessSpec] = None, disregard=None):
+        """disregard: a labelsel.DisregardSpec (the kwok configuration's
+        disregardStatusWith{Annotation,Label}Selector): need()'s result becomes one feature bit, and
+        a changed object with it set is not re-matched (kwk_stage_table.disregard_mask)."""
         # NewLifecycle drops stages with a nil selector (lifecycle.go:199-201)
         self.stages: List[Stage] = [s for s in stages if s.selector is not None]
         if len(self.stages) > abi.MAX_STAGES:
             raise CompileError(f"{len(self.stages)} stages > {abi.MAX_STAGES}")
         self.names = [s.name for s in self.stages]
         self.harness = harness
+        self.disregard = disregard if (disregard is not None and disregard.active) else None
+        self.disregard_bit: Optional[int] = None
         self.features: Dict[str, Feature] = {}
         self.nbits = 0
         self.fin_bits: Dict[str, int] = {}
@@ -339,8 +344,10 @@ class KindProgram:
         if self.harness is not None:
             self.deletion_bit = self._present(self.harness.deletion_query)
             self.terminal_mask = self._lits(self.harness.terminal_query, list(self.harness.terminal_values))
+        if self.disregard is not None:  # need()'s selector part: labels / annotations (spec, kept on re-creation)
+            self.disregard_bit = self._bit()
         # keep mask for harness re-creation: features that do not read status / deletion / finalizers
-        keep = 0
+        keep = 0 if self.disregard_bit is None else 1 << self.disregard_bit
         for f in self.features.values():
             p = path_prefix(f.src)
             dyn = (not p) or p[0] == "status" or p[:2] in (["metadata", "deletionTimestamp"],
@@ -369,6 +376,8 @@ class KindProgram:
         for s, b in self.applied_bits.items():
             if self._patch_applied(self.stages[s], obj):
                 pred |= 1 << b
+        if self.disregard is not None and self.disregard.disregarded(obj):
+            pred |= 1 << self.disregard_bit
         return pred
 
     def _patch_applied(self, st: Stage, obj: dict) -> bool:
@@ -587,6 +596,7 @@ class KindProgram:
         t.n_classes = max(1, len(self.class_ids))
         t.version = version
         t.pred_bits = self.nbits
+        t.disregard_mask = 0 if self.disregard_bit is None else 1 << self.disregard_bit
         for i, d in enumerate(self.stage_desc):
             t.stages[i] = d
         return t
@@ -627,4 +637,7 @@ class KindProgram:
                 "applied_bits": {self.names[s]: b for s, b in self.applied_bits.items()},
                 "finalizers": dict(self.fin_bits), "finalizer_other_bit": self.fin_other_bit,
                 "value_slots": [list(s) for s in self.slots], "classes": len(self.class_ids),
-                "uses_deletion_column": self.uses_deletion_column}
+                "uses_deletion_column": self.uses_deletion_column,
+                "disregard": None if self.disregard is None else {
+                    "bit": self.disregard_bit, "annotation_selector": self.disregard.annotation_selector,
+                    "label_selector": self.disregard.label_selector}}

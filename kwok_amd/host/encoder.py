@@ -79,9 +79,11 @@ def encoder_spec(program: KindProgram) -> str:
     feats = [{"steps": query_steps(f.src), "present_bit": f.present_bit, "literals": dict(f.lit_bits)}
              for f in program.features.values()]
     slots = [{"type": typ, "steps": query_steps(src)} for typ, src in program.slots]
-    return json.dumps({"features": feats, "finalizers": dict(program.fin_bits),
-                       "finalizer_other_bit": program.fin_other_bit, "slots": slots,
-                       "classes": dict(program.class_ids), "identity_meta": list(_IDENTITY_META)})
+    spec = {"features": feats, "finalizers": dict(program.fin_bits), "finalizer_other_bit": program.fin_other_bit,
+            "slots": slots, "classes": dict(program.class_ids), "identity_meta": list(_IDENTITY_META)}
+    if program.disregard is not None:  # need()'s selectors, evaluated by the encoder into one bit
+        spec["disregard"] = program.describe()["disregard"]
+    return json.dumps(spec)
 
 
 _lib = None

@@ -71,14 +71,18 @@ def stage_docs_from_files(*paths: str) -> List[dict]:
 class NativeProgram:
     """One resourceRef's Stage list compiled by libkwok_compiler (kwk_compile_stages)."""
 
-    def __init__(self, stage_docs: Sequence[dict], harness=None):
-        """harness: None, True (the default HarnessSpec) or a compiler.HarnessSpec."""
-        opts = None
+    def __init__(self, stage_docs: Sequence[dict], harness=None, disregard=None):
+        """harness: None, True (the default HarnessSpec) or a compiler.HarnessSpec; disregard: a
+        labelsel.DisregardSpec (need()'s selectors)."""
+        o = {}
         if harness is not None:
-            h = {} if harness is True else {"terminal_query": harness.terminal_query,
-                                            "terminal_values": list(harness.terminal_values),
-                                            "deletion_query": harness.deletion_query}
-            opts = json.dumps({"harness": h}).encode()
+            o["harness"] = {} if harness is True else {"terminal_query": harness.terminal_query,
+                                                       "terminal_values": list(harness.terminal_values),
+                                                       "deletion_query": harness.deletion_query}
+        if disregard is not None and disregard.active:
+            o["disregard"] = {"annotation_selector": disregard.annotation_selector,
+                              "label_selector": disregard.label_selector}
+        opts = json.dumps(o).encode() if o else None
         self.harness = harness
         self.h = C.c_void_p()
         st = lib().kwk_compile_stages(json.dumps(list(stage_docs)).encode(), opts, C.byref(self.h))

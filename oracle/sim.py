@@ -21,7 +21,7 @@ from __future__ import annotations
 import copy
 from typing import List, Optional, Sequence
 
-from . import refcpu
+from . import labels_ref, refcpu
 from .next_ref import Funcs, StageNext, format_rfc3339nano, omitempty, strip_for_recreate
 
 INT64_MAX = (1 << 63) - 1
@@ -35,11 +35,14 @@ def sat_add(a: int, b: int) -> int:
 class OracleSim:
     def __init__(self, stage_docs: Sequence[dict], objs: Sequence[dict], harness: bool = False,
                  terminal=("Succeeded", "Failed"), slot_base: int = 0, kind_salt: int = 0,
-                 slots: Optional[Sequence[int]] = None):
+                 slots: Optional[Sequence[int]] = None, disregard=None):
         """slots: the engine slot of each object (default: objs[i] is slot i).  Objects are
         independent within a step (a pod reads only its own fields; its node's lease state comes
         in through set_managed) and the Philox counter is the global slot, so a deterministic
-        sample of a large engine's slots is simulated exactly by passing their slot numbers."""
+        sample of a large engine's slots is simulated exactly by passing their slot numbers.
+        disregard: (annotation selector, label selector) of need() (pod_controller.go:397-407): a
+        changed object they disregard is not re-matched (its event is skipped; a queued job stays)."""
+        self.disregard = disregard
         # NewLifecycle drops stages with a nil selector (lifecycle.go:199-201)
         docs = [d for d in stage_docs if (d.get("spec") or {}).get("selector") is not None]
         self.lc = refcpu.Lifecycle(list(stage_docs))
@@ -86,6 +89,8 @@ class OracleSim:
                     self.dirty[i] = True
             if o is None:
                 continue
+            if self.dirty[i] and self.disregard is not None and labels_ref.disregarded(*self.disregard, o):
+                self.dirty[i] = False  # watchResources: need() is false, the event is skipped
             if self.dirty[i]:
                 self.dirty[i] = False
                 self.matcherr[i] = False
@@ -148,4 +153,7 @@ def oracle_pred(desc: dict, obj: dict) -> int:
         for x in (obj.get("metadata") or {}).get("finalizers") or []:
             b = desc["finalizers"].get(x)
             pred |= 1 << (desc["finalizer_other_bit"] if b is None else b)
+    dg = desc.get("disregard")
+    if dg and labels_ref.disregarded(dg["annotation_selector"], dg["label_selector"], obj):
+        pred |= 1 << dg["bit"]
     return pred

@@ -34,14 +34,14 @@ def expected_state_bytes(prog, state="auto"):
 
 
 def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state=False, state="auto", tuning=None,
-          compiler="python"):
+          compiler="python", disregard=None):
     """compiler: "python" (KindProgram + the Python Ingest) or "native" (libkwok_compiler's
     kwk_compile_stages / kwk_program_explore, rows from libkwok_encoder built from its spec: the
     Go host's path, no Python compiler involved)."""
     if compiler == "native":
         from kwok_amd.host.encoder import NativeIngest
         from kwok_amd.host.native_compiler import NativeProgram, stage_docs_from_files
-        prog = NativeProgram(stage_docs_from_files(*stage_files), HarnessSpec() if harness else None)
+        prog = NativeProgram(stage_docs_from_files(*stage_files), HarnessSpec() if harness else None, disregard=disregard)
         prog.explore(objs)
         ing = NativeIngest(prog)
         hot, dels, rec, cls = ing.columns(objs, register=True)
@@ -49,7 +49,7 @@ def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state
         ing.close()
     else:
         stages = load_stage_files(*stage_files)
-        prog = KindProgram(stages, HarnessSpec() if harness else None)
+        prog = KindProgram(stages, HarnessSpec() if harness else None, disregard=disregard)
         prog.explore(objs)
         assert not prog.delta_conflicts, prog.delta_conflicts
         ing = Ingest(prog)
@@ -62,7 +62,8 @@ def build(stage_files, objs, harness=False, kind_salt=0, slot_base=0, wide_state
     eng.load_stages()
     eng.set_harness(harness)
     eng.load(hot, dels, rec, cls, records)
-    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base)
+    sim = OracleSim(load_stage_docs(*stage_files), objs, harness=harness, kind_salt=kind_salt, slot_base=slot_base,
+                    disregard=None if disregard is None else (disregard.annotation_selector, disregard.label_selector))
     return prog, eng, sim
 
 
@@ -105,13 +106,13 @@ def compare_state(prog, eng, sim, step, rows=None):
 
 
 def run(stage_files, objs, steps, dt_ns, harness=False, seed=0x5EED, kind_salt=0, check_state=True, wide_state=False,
-        state="auto", tuning=None, expect_kernel=None, nows=None, compiler="python"):
+        state="auto", tuning=None, expect_kernel=None, nows=None, compiler="python", disregard=None):
     """expect_kernel: the abi.SWEEP_* every step must launch (the shape under test); nows: the
     clock of each step (default NOW0 + k * dt_ns)."""
     if wide_state:
         state = "wide"
     prog, eng, sim = build(stage_files, objs, harness=harness, kind_salt=kind_salt, state=state, tuning=tuning,
-                           compiler=compiler)
+                           compiler=compiler, disregard=disregard)
     total = 0
     per_stage = np.zeros(len(prog.names), dtype=np.int64)
     try:
