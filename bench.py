@@ -3,8 +3,9 @@
 One *step* = one reconciliation pass of the HIP engines over the whole resident cluster
 (pods + nodes): harness churn, match of changed objects, weighted pick + delay/jitter,
 firing of due objects, their next-state deltas, and the fired hand-back — each engine's
-fired list compacted into one dense device list every step (kwk_fired_compact; the Go host
-would DMA it from there).  Every `--report-every` steps (the reporting interval) the cluster
+fired list compacted into one dense device list every step (kwk_fired_compact_packed: 4-byte
+records, 27-bit slot | 5-bit stage; --handback rec: kwk_fired_compact's 8-byte kwk_fired_rec; the
+Go host would DMA it from there).  Every `--report-every` steps (the reporting interval) the cluster
 aggregates are computed on the device and summed over all GPUs with one RCCL all-reduce:
 per-stage transition counts, the pod / node phase histograms (kwk_count) and the cluster
 CPU / memory usage (kwk_usage over the default usage-from-annotation ClusterResourceUsage).
@@ -161,7 +162,11 @@ SWEEP_NAMES = {1: "sweep16_kernel", 2: "sweep16_fsm_kernel", 3: "sweepw_kernel<4
 EV_EVERY = 2  # HIP events bracket the pod sweep of every 2nd step: each marker idles the stream ~5 us (r2b)
 
 
-def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None):
+HANDBACK = {"packed": "packed", "rec": True}  # --handback: kwk_step_n's compaction (4-byte packed / kwk_fired_rec)
+
+
+def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None,
+              handback="packed"):
     """Steps k0..k1-1; ev_base (0): record HIP events (pod stream) around the pod sweep of every
     EV_EVERY-th step (events 2i, 2i+1 of sample i).  Each engine's steps up to the next
     reporting point are enqueued by one native call (kwk_step_n: sweep + device compaction per
@@ -175,8 +180,8 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
             if reporter is not None and report_every:
                 end = min(k1, k0 + (j // report_every + 1) * report_every)
             now = NOW0 + k * dt
-            pods.step_n(end - k, now, dt, seed, k, True, EV_EVERY if ev_base is not None else 0, j)
-            nodes.step_n(end - k, now, dt, seed, k, True)
+            pods.step_n(end - k, now, dt, seed, k, HANDBACK[handback], EV_EVERY if ev_base is not None else 0, j)
+            nodes.step_n(end - k, now, dt, seed, k, HANDBACK[handback])
             k = end
             if reporter is not None and report_every and (k - k0) % report_every == 0:
                 last = reporter.collect(NOW0 + (k - 1) * dt)
@@ -192,11 +197,15 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
         pods.step(now, seed, k)
         if timed:
             pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
-        pods.fired_compact()
+        packed = handback == "packed"
+        pods.fired_compact(packed)
         nodes.step(now, seed, k)
-        nodes.fired_compact()
+        nodes.fired_compact(packed)
         if pinned is not None:  # PCIe-inclusive: every fired record copied to pinned host memory
-            n_fired_host += len(pods.fired(pinned[0])) + len(nodes.fired(pinned[1]))
+            if packed:
+                n_fired_host += len(pods.fired_packed(pinned[0])) + len(nodes.fired_packed(pinned[1]))
+            else:
+                n_fired_host += len(pods.fired(pinned[0])) + len(nodes.fired(pinned[1]))
         if reporter is not None and report_every and (j + 1) % report_every == 0:
             last = reporter.collect(now)
     return last, n_fired_host
@@ -217,12 +226,13 @@ def measure_hbm_working_set(args, device):
     try:
         dt = 500 * 10**6
         steps, warm = args.hbm_steps, args.hbm_warmup
-        run_steps(pods, nodes, args.seed, dt, 0, warm)
+        hb = getattr(args, "handback", "packed")
+        run_steps(pods, nodes, args.seed, dt, 0, warm, handback=hb)
         pods.sync()
         nodes.sync()
         s0 = pods.stats()
         t0 = time.perf_counter()
-        run_steps(pods, nodes, args.seed, dt, warm, warm + steps, ev_base=0)
+        run_steps(pods, nodes, args.seed, dt, warm, warm + steps, ev_base=0, handback=hb)
         pods.sync()
         nodes.sync()
         wall = time.perf_counter() - t0
@@ -479,6 +489,9 @@ def main():
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
+    ap.add_argument("--handback", choices=("packed", "rec"), default="packed",
+                    help="fired hand-back per step: packed 4-byte records (kwk_fired_compact_packed, 27-bit slot | "
+                         "5-bit stage) or 8-byte kwk_fired_rec (kwk_fired_compact)")
     ap.add_argument("--collective", choices=("torch", "native"), default="torch",
                     help="aggregate all-reduce: torch.distributed (default) or libkwok_comm (RCCL, no torch; N > 1)")
     args = ap.parse_args()
@@ -564,7 +577,7 @@ def main():
     report_every = 0 if args.pmc_child else args.report_every
 
     log(f"setup {setup_s:.1f} s; warmup {args.warmup} steps")
-    run_steps(pods, nodes, args.seed, dt, 0, args.warmup)
+    run_steps(pods, nodes, args.seed, dt, 0, args.warmup, handback=args.handback)
     if report_every and args.warmup:
         # the warm-up covers one reporting interval too: its one-time work (the aggregate and count
         # buffers' allocation, the masks' upload, occupancy queries, the communicator's first
@@ -586,7 +599,8 @@ def main():
     # at N = 1 (the roofline line); with several ranks they are sampled after it (below), so the
     # scaling runs time the steps alone
     agg, _ = run_steps(pods, nodes, args.seed, dt, args.warmup, args.warmup + args.steps,
-                       ev_base=0 if world == 1 else None, reporter=reporter, report_every=report_every)
+                       ev_base=0 if world == 1 else None, reporter=reporter, report_every=report_every,
+                       handback=args.handback)
     pods.sync()
     nodes.sync()
     barrier()
@@ -597,7 +611,7 @@ def main():
     n_ev = (args.steps + EV_EVERY - 1) // EV_EVERY
     if world > 1:  # sampled after the timed region (the same steps continued)
         k0 = args.warmup + args.steps
-        run_steps(pods, nodes, args.seed, dt, k0, k0 + args.steps, ev_base=0)
+        run_steps(pods, nodes, args.seed, dt, k0, k0 + args.steps, ev_base=0, handback=args.handback)
         pods.sync()
         nodes.sync()
     sweep_ms = [pods.event_elapsed_ms(2 * i, 2 * i + 1) for i in range(n_ev)]
@@ -629,14 +643,16 @@ def main():
         k0 = args.warmup + args.steps
         s2p, s2n = pods.stats(), nodes.stats()
         t1 = time.perf_counter()
-        _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin)
+        _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin, handback=args.handback)
         wall = time.perf_counter() - t1
         s3p, s3n = pods.stats(), nodes.stats()
         nf = (s3p["fired"] - s2p["fired"]) + (s3n["fired"] - s2n["fired"])
         assert n_host == nf, (n_host, nf)
         pcie = {"value": round(nf / wall, 1), "unit": "stage transitions/sec", "steps": args.pcie_steps,
                 "fired_records_to_host_per_step": nf / args.pcie_steps, "ms_per_step": round(wall / args.pcie_steps * 1e3, 4),
-                "note": "each step's fired lists copied (kwk_fired, 8 B per transition) into kwk_alloc_host buffers"}
+                "note": "each step's fired lists copied into kwk_alloc_host buffers: " + (
+                    "kwk_fired_packed, 4 B per transition" if args.handback == "packed" else
+                    "kwk_fired, 8 B per transition")}
         for p in pin:
             p.close()
     if reporter.comm is not None:
@@ -687,7 +703,8 @@ def main():
             "config": {"workload": f"C5: {total_nodes:,} nodes / {total_nodes * args.pods_per_node:,} pods in total "
                                    f"over {world} GPU(s), pod-fast + node-initialize/heartbeat, harness churn "
                                    "(Succeeded -> delete -> re-create), 10% Job-owned; per step: sweep + fired "
-                                   f"hand-back (device compaction); every {args.report_every} steps: phase "
+                                   f"hand-back (device compaction into {'packed 4-byte' if args.handback == 'packed' else '8-byte kwk_fired_rec'}"
+                                   f" records); every {args.report_every} steps: phase "
                                    "histograms + cluster usage + per-stage counts all-reduced over RCCL",
                        "nodes": total_nodes, "pods": total_nodes * args.pods_per_node,
                        "nodes_per_gpu": nhi - nlo, "parallelism": f"node-shard{world}", "sim_dt_ms": args.dt_ms},

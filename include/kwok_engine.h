@@ -300,6 +300,19 @@ kwk_status kwk_step_n(kwk_engine* eng, uint32_t n, int64_t now0_ns, int64_t dt_n
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 /* device pointers of the compacted list and of its u32 count (valid until the next kwk_step) */
 kwk_status kwk_fired_device(kwk_engine* eng, const kwk_fired_rec** recs, const uint32_t** count);
+/* The same hand-back as 4-byte packed records, half the bytes over HBM and PCIe:
+ * KWK_FIRED_PACKED_STAGE(r) = r >> 27 (stage index), KWK_FIRED_PACKED_SLOT(r) = r & (2^27 - 1); same
+ * order as kwk_fired.  The flags of kwk_fired_rec are not carried: DELETED is the stage's
+ * KWK_NEXT_DELETE, DELTA_UNKNOWN the (class, stage) delta the host loaded, REMATCH is the device's
+ * own business (kwk_fired still returns all three).  Engines of at most 2^27 slots (KWK_ECAP
+ * otherwise).  kwk_step_n(..., compact = KWK_COMPACT_PACKED, ...) / KWK_TICK_COMPACT_PACKED enqueue
+ * it per step. */
+#define KWK_COMPACT_PACKED 2u
+#define KWK_FIRED_PACKED_STAGE(r) ((uint32_t)(r) >> 27)
+#define KWK_FIRED_PACKED_SLOT(r) ((uint32_t)(r) & 0x7FFFFFFu)
+kwk_status kwk_fired_compact_packed(kwk_engine* eng);
+kwk_status kwk_fired_packed(kwk_engine* eng, uint32_t* out, uint32_t cap, uint32_t* n_out);
+kwk_status kwk_fired_packed_device(kwk_engine* eng, const uint32_t** recs, const uint32_t** count);
 /* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */
 kwk_status kwk_alloc_host(uint64_t bytes, void** out);
 kwk_status kwk_free_host(void* p);
@@ -499,6 +512,7 @@ kwk_status kwk_lease_sync_pods(kwk_engine* pods, const kwk_engine* nodes, uint32
  * lease step only if kwk_lease_config was called).  kwk_tick_n: n ticks at now0 + k * dt,
  * step0 + k (enqueue only; the last tick's lease ops / fired lists are readable). */
 #define KWK_TICK_COMPACT (1u << 0)
+#define KWK_TICK_COMPACT_PACKED (1u << 1) /* the hand-back as packed 4-byte records (kwk_fired_compact_packed) */
 kwk_status kwk_tick_bind(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_nodes, const uint32_t* node_ptr);
 kwk_status kwk_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_ns, uint64_t seed, uint64_t step, uint32_t flags);
 kwk_status kwk_tick_n(kwk_engine* nodes, kwk_engine* pods, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed,

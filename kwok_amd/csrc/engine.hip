@@ -2064,6 +2064,7 @@ __global__ __launch_bounds__(kBlock, kDW ? kDwMinBlocks : 1) void sweepw_kernel(
 // dense list; the last segment's wave writes the list length.  (A single-pass decoupled
 // look-back was measured slower here: with ~12k tiny blocks the look-back chains, not the bytes,
 // set the time — 165 us vs the ~30 us the bytes need.)
+constexpr uint32_t kPackedSlots = 1u << 27;                // packed fired records: 27-bit slots
 constexpr uint32_t kScanPer = 16;                         // counts per thread
 constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 4096 counts per group (one workgroup)
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
@@ -2149,9 +2150,21 @@ __device__ __forceinline__ void store_rec_nt(kwk_fired_rec* p, uint32_t slot, ui
   __builtin_nontemporal_store(u32x2{slot, ((x >> 13) & 31u) | ((x >> 18) & 7u) << 16}, reinterpret_cast<u32x2*>(p));
 }
 
+// the packed 4-byte record {stage: 31..27, slot: 26..0} (kwk_fired_packed), nontemporal
+__device__ __forceinline__ void store_packed_nt(uint32_t* p, uint32_t slot, uint32_t x) {
+  __builtin_nontemporal_store(((x >> 13) & 31u) << 27 | slot, p);
+}
+
+template <bool kPacked>
+__device__ __forceinline__ void store_out(const CompactArgs& a, uint32_t at, uint32_t slot, uint32_t x) {
+  if constexpr (kPacked) store_packed_nt(reinterpret_cast<uint32_t*>(a.out) + at, slot, x);
+  else store_rec_nt(&a.out[at], slot, x);
+}
+
 // one wave per segment; the first 256 records are loaded together with the segment's count and
-// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it)
-template <int kRec>
+// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it).  kPacked:
+// 4-byte records (kwk_fired_packed) instead of kwk_fired_rec — half the bytes written
+template <int kRec, bool kPacked = false>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2171,11 +2184,11 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const uint32_t j = lane + 64u * k;
-    if (j < c) store_rec_nt(&a.out[off + j], base + r[k].x, r[k].y);
+    if (j < c) store_out<kPacked>(a, off + j, base + r[k].x, r[k].y);
   }
   for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
     const uint2 x = rec_at<kRec>(sp, j);
-    store_rec_nt(&a.out[off + j], base + x.x, x.y);
+    store_out<kPacked>(a, off + j, base + x.x, x.y);
   }
 }
 
@@ -2183,7 +2196,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // strong-scaling shards): each block sums the counts of every segment before its own (at most
 // 32 KB, L2-resident) instead of waiting for seg_scan_kernel, then expands its four segments as
 // compact_kernel does.  Saves one launch and its gap per step.
-template <int kRec>
+template <int kRec, bool kPacked = false>
 __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   __shared__ uint32_t s_part[kWavesPerBlock];
   __shared__ uint32_t s_seg[kWavesPerBlock];
@@ -2205,7 +2218,7 @@ __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
   for (uint32_t j = lane; j < c; j += 64) {
     const uint2 x = rec_at<kRec>(sp, j);
-    store_rec_nt(&a.out[off + j], base + x.x, x.y);
+    store_out<kPacked>(a, off + j, base + x.x, x.y);
   }
 }
 
@@ -3636,6 +3649,7 @@ struct kwk_engine {
   uint32_t last_region_shift = 0;  // fired segments per record region = 1 << shift (wave: 0, tile: 2)
   int last_rec = 0;                // record kind of the last sweep's segments (kRecSlot / kRecId8 / kRecId8Half)
   bool compacted = false;     // the last sweep's fired list is compacted on the device
+  bool compacted_packed = false;  // ... as 4-byte packed records (kwk_fired_compact_packed)
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
@@ -4860,9 +4874,10 @@ kwk_status kwk_sync(kwk_engine* e) {
 
 // fired hand-back on the device: per-(tile, wave) counts -> exclusive scan -> dense list in
 // d_compact, total at d_wave_offsets[n_waves] (enqueue only)
-static kwk_status enqueue_compact(kwk_engine* e) {
+static kwk_status enqueue_compact(kwk_engine* e, bool packed = false) {
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   e->compacted = true;
+  e->compacted_packed = packed;
   if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
     HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), e->stream));
     return KWK_OK;
@@ -4881,17 +4896,23 @@ static kwk_status enqueue_compact(kwk_engine* e) {
   const int rk = e->last_rec;
   void* args[] = {&a};
   if (n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
-    const void* k = rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half>
-                    : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8>
-                                      : (const void*)compact_small_kernel<kRecSlot>;
+    const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half, true>
+                              : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8, true>
+                                                : (const void*)compact_small_kernel<kRecSlot, true>)
+                           : (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half>
+                              : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8>
+                                                : (const void*)compact_small_kernel<kRecSlot>);
     HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
     return KWK_OK;
   }
   hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
                      e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
-  const void* k = rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half>
-                  : rk == kRecId8   ? (const void*)compact_kernel<kRecId8>
-                                    : (const void*)compact_kernel<kRecSlot>;
+  const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, true>
+                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, true>
+                                              : (const void*)compact_kernel<kRecSlot, true>)
+                         : (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half>
+                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8>
+                                              : (const void*)compact_kernel<kRecSlot>);
   HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
   HIP_TRY(hipGetLastError());
   return KWK_OK;
@@ -4904,10 +4925,54 @@ kwk_status kwk_fired_compact(kwk_engine* e) {
   return enqueue_compact(e);
 }
 
+static kwk_status packed_ok(const kwk_engine* e) {
+  if (e->capacity > kPackedSlots) return fail(KWK_ECAP, "packed fired records hold 27-bit slots: engine capacity > 2^27");
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_compact_packed(kwk_engine* e) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = packed_ok(e)) return st;
+  if (kwk_status st = set_dev(e)) return st;
+  return enqueue_compact(e, true);
+}
+
+kwk_status kwk_fired_packed_device(kwk_engine* e, const uint32_t** recs, const uint32_t** count) {
+  ErrScope es_(e);
+  if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
+  if (!e->compacted || !e->compacted_packed) return fail(KWK_ESTATE, "kwk_fired_compact_packed must follow kwk_step");
+  *recs = reinterpret_cast<const uint32_t*>(e->d_compact);
+  *count = e->d_wave_offsets;
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_packed(kwk_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = packed_ok(e)) return st;
+  if (kwk_status st = set_dev(e)) return st;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (n_waves == 0) { *n_out = 0; return KWK_OK; }
+  if (!e->compacted || !e->compacted_packed)
+    if (kwk_status st = enqueue_compact(e, true)) return st;
+  uint32_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
+  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
   ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
+  if (compact == KWK_COMPACT_PACKED)
+    if (kwk_status st = packed_ok(e)) return st;
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t j = ev_j0 + k;
@@ -4918,7 +4983,7 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
     if (ev)
       if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
     if (compact)
-      if (kwk_status st = enqueue_compact(e)) return st;
+      if (kwk_status st = enqueue_compact(e, compact == KWK_COMPACT_PACKED)) return st;
   }
   return KWK_OK;
 }
@@ -4926,7 +4991,7 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
 kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
   ErrScope es_(e);
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
-  if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
+  if (!e->compacted || e->compacted_packed) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
   *recs = e->d_compact;
   *count = e->d_wave_offsets;
   return KWK_OK;
@@ -4938,7 +5003,7 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (kwk_status st = set_dev(e)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
-  if (!e->compacted)
+  if (!e->compacted || e->compacted_packed)  // the segments are intact: expand them as kwk_fired_rec
     if (kwk_status st = enqueue_compact(e)) return st;
   uint32_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -5923,7 +5988,8 @@ kwk_status kwk_tick_bind(kwk_engine* pods, const kwk_engine* nodes, uint32_t n_n
 
 static kwk_status enqueue_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_ns, uint64_t seed, uint64_t step,
                                uint32_t flags) {
-  const bool compact = (flags & KWK_TICK_COMPACT) != 0;
+  const bool compact = (flags & (KWK_TICK_COMPACT | KWK_TICK_COMPACT_PACKED)) != 0;
+  const bool packed = (flags & KWK_TICK_COMPACT_PACKED) != 0;
   // the previous tick's pod sync must have read the lease results before this lease step
   // rewrites them (cross-stream order by events: no host synchronisation)
   if (pods) nodes->tick_pods = pods;
@@ -5942,11 +6008,11 @@ static kwk_status enqueue_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_
   }
   if (kwk_status st = launch_sweep(nodes, now_ns, seed, step, true)) return st;
   if (compact)
-    if (kwk_status st = enqueue_compact(nodes)) return st;
+    if (kwk_status st = enqueue_compact(nodes, packed)) return st;
   if (pods) {
     if (kwk_status st = launch_sweep(pods, now_ns, seed, step, true)) return st;
     if (compact)
-      if (kwk_status st = enqueue_compact(pods)) return st;
+      if (kwk_status st = enqueue_compact(pods, packed)) return st;
   }
   return KWK_OK;
 }

@@ -169,8 +169,11 @@ EXPORTS = [
     "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
     "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
+    "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
+TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
+COMPACT_PACKED = 2  # kwk_step_n compact = KWK_COMPACT_PACKED
 AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
 
 _lib = None
@@ -222,6 +225,9 @@ def lib():
     L.kwk_step_n.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                              C.c_uint32]
     L.kwk_fired_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
+    L.kwk_fired_compact_packed.argtypes = [C.c_void_p]
+    L.kwk_fired_packed.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_fired_packed_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
     L.kwk_set_tuning.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]

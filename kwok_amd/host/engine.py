@@ -237,15 +237,30 @@ class Engine:
     def step(self, now_ns: int, seed: int, step: int):
         self._check(abi.lib().kwk_step(self.h, now_ns, seed, step), "kwk_step")
 
-    def step_n(self, n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact: bool = True, ev_every: int = 0,
+    def step_n(self, n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact=True, ev_every: int = 0,
                ev_j0: int = 0):
-        """kwk_step_n: n steps (+ device compaction after each) enqueued by one call."""
-        self._check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, 1 if compact else 0, ev_every, ev_j0),
-                  "kwk_step_n")
+        """kwk_step_n: n steps (+ device compaction after each) enqueued by one call; compact =
+        True (kwk_fired_rec), "packed" (4-byte records) or False."""
+        c = abi.COMPACT_PACKED if compact == "packed" else (1 if compact else 0)
+        self._check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, c, ev_every, ev_j0), "kwk_step_n")
 
-    def fired_compact(self):
-        """kwk_fired_compact: the last step's fired list compacted on the device (enqueue only)."""
-        self._check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
+    def fired_compact(self, packed: bool = False):
+        """kwk_fired_compact (/ _packed): the last step's fired list compacted on the device (enqueue only)."""
+        if packed:
+            self._check(abi.lib().kwk_fired_compact_packed(self.h), "kwk_fired_compact_packed")
+        else:
+            self._check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
+
+    def fired_packed(self, pinned: Optional["PinnedBuffer"] = None) -> np.ndarray:
+        """The last step's fired list as packed u32 records (kwk_fired_packed): stage = r >> 27,
+        slot = r & (2**27 - 1)."""
+        n = C.c_uint32()
+        L = abi.lib()
+        self._check(L.kwk_fired_packed(self.h, None, 0, C.byref(n)), "kwk_fired_packed")
+        out = pinned.array(np.uint32, n.value) if pinned is not None else np.zeros(n.value, dtype=np.uint32)
+        if n.value:
+            self._check(L.kwk_fired_packed(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_packed")
+        return out
 
     def set_tuning(self, key: int, value: int):
         """kwk_set_tuning: an explicit kernel choice (abi.TUNE_*)."""
@@ -489,15 +504,19 @@ class Engine:
         ptr = np.ascontiguousarray(node_ptr, dtype=np.uint32)
         self._check(abi.lib().kwk_tick_bind(self.h, nodes.h, len(ptr) - 1, abi.ptr(ptr)), "kwk_tick_bind")
 
-    def tick(self, pods: Optional["Engine"], now_ns: int, seed: int, step: int, compact: bool = False):
+    @staticmethod
+    def _tick_flags(compact) -> int:
+        return abi.TICK_COMPACT_PACKED if compact == "packed" else (abi.TICK_COMPACT if compact else 0)
+
+    def tick(self, pods: Optional["Engine"], now_ns: int, seed: int, step: int, compact=False):
         """kwk_tick: lease step -> pod sync -> node step -> pod step, one call (enqueue only)."""
         self._check(abi.lib().kwk_tick(self.h, pods.h if pods is not None else None, now_ns, seed, step,
-                                       abi.TICK_COMPACT if compact else 0), "kwk_tick")
+                                       self._tick_flags(compact)), "kwk_tick")
 
     def tick_n(self, pods: Optional["Engine"], n: int, now0_ns: int, dt_ns: int, seed: int, step0: int,
-               compact: bool = False):
+               compact=False):
         self._check(abi.lib().kwk_tick_n(self.h, pods.h if pods is not None else None, n, now0_ns, dt_ns, seed, step0,
-                                         abi.TICK_COMPACT if compact else 0), "kwk_tick_n")
+                                         self._tick_flags(compact)), "kwk_tick_n")
 
     # timing
     def stream_handle(self) -> int:

@@ -139,6 +139,55 @@ def test_handback_pair_equals_one_launch_at_4m_pods():
         eng.close()
 
 
+@pytest.mark.parametrize("state", ["auto", "u16", "dw"])
+def test_packed_handback_equals_records_at_4m_pods(state):
+    """The packed hand-back (kwk_fired_compact_packed / kwk_fired_packed: 4-byte records, stage in
+    bits 31-27, slot in 26-0) over the same step's segments as the 8-byte list, through both
+    compaction paths (one launch at <= 8192 segments, the scan + expansion pair above): the same
+    (slot, stage) sequence; kwk_fired after a packed compaction re-expands the full records
+    (flags included); kwk_step_n with KWK_COMPACT_PACKED leaves the same packed list as the
+    per-step calls.  1-byte ids (sweep8), 2-byte words, fused 8-byte records (C2 mix)."""
+    from kwok_amd.host import abi
+    if state == "dw":
+        from kwok_amd import workload as W
+        from kwok_amd.host.compiler import HarnessSpec, KindProgram
+        from kwok_amd.host.engine import Engine, Ingest
+        from kwok_amd.host.stages import load_stage_files
+        n = 4_000_000
+        pvars, pidx = W.c2_pod_variants(0, n, seed=0x6B776F6B, job_frac=0.1)
+        prog = KindProgram(load_stage_files(*W.stage_paths(W.POD_GENERAL + W.POD_CHAOS)), HarnessSpec())
+        prog.explore(pvars)
+        ing = Ingest(prog)
+        hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+        eng = Engine(prog, capacity=n, max_records=max(1, len(ing.records)) + 16)
+        eng.load_stages()
+        eng.set_harness(True)
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        dt = 500 * 10**6
+    else:
+        prog, eng = _pods(state)
+        dt = 10**9
+    try:
+        now0 = 1_700_000_000 * 10**9
+        for k in range(4):
+            eng.step(now0 + k * dt, 0x6B776F6B, k)
+            for small in (8192, 0):
+                eng.set_tuning(abi.TUNE_COMPACT_SMALL, small)
+                eng.fired_compact(packed=True)
+                pk = eng.fired_packed()
+                full = eng.fired()  # re-expanded from the same segments
+                assert len(pk) == len(full) > 0, (k, small)
+                assert np.array_equal(pk & np.uint32(0x7FFFFFF), full["slot"]), (k, small)
+                assert np.array_equal(pk >> np.uint32(27), full["stage"].astype(np.uint32)), (k, small)
+        ref = eng.fired_packed()
+        eng.step_n(1, now0 + 4 * dt, dt, 0x6B776F6B, 4, "packed")
+        a = eng.fired_packed()
+        eng2_full = eng.fired()
+        assert np.array_equal(a & np.uint32(0x7FFFFFF), eng2_full["slot"]) and len(a) > 0 and len(ref) > 0
+    finally:
+        eng.close()
+
+
 def test_aggregates_and_handback_at_17m_pods():
     """At 17M pods (the 2-byte sweep's persistent grid): kwk_count and kwk_usage against the
     state read back through kwk_read (numpy), and the device-compacted fired list (one

@@ -10,7 +10,10 @@
 #   configs                    bench.py --config C1..C4 lines (configs_C1_C4.jsonl)
 #   c2prof                     C2 working set: kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #   sq                         SQ counter passes over the C5 pod sweep and the C2 word sweep
-#   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/build/<so>, alternating x2
+#   shards                     the bench at the per-rank shard sizes of N = 8 / 4 / 2 (strong scaling:
+#                              125k / 250k / 500k nodes) + a kernel trace of the 125k-node shard
+#   dist                       2 ranks sharing the GPU over gloo (the N > 1 bench path) vs one rank
+#   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/ab/<so>, alternating x2
 #   variants=<args>            tools/variants.py run <args> (cost-isolation builds)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; T=$1; shift; O=$R/gpurun_out/$T
@@ -70,11 +73,27 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
       for d in c5sq1 c5sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweep8; done > $O/c5_sq.txt
       for d in c2sq1 c2sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweepw; done > $O/c2_sq.txt
       cat $O/c5_sq.txt $O/c2_sq.txt ;;
+    shards)
+      S="--no-cpu-baseline --no-pmc --hbm-nodes 0 --pcie-steps 0 --steps 40 --warmup 5"
+      for n in 125000 250000 500000; do
+        timeout -k 10 200 python -u bench.py --nodes $n $S > $O/shard_$n.json 2> $O/shard_$n.err || { tail -20 $O/shard_$n.err; exit 1; }
+        python -c "import json; d=json.load(open('$O/shard_$n.json')); print($n, d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'])"
+      done
+      TRACE
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/shard_prof -o run -- python3 $R/bench.py --nodes 125000 $S \
+        > $O/shard_prof.json 2> $O/shard_prof.err || { tail -30 $O/shard_prof.err; exit 1; }
+      cd $R && python tools/rocpd_summary.py stats $(find $O/shard_prof -name '*.db' | head -1) $O/shard_kernel_stats.csv \
+        && cut -c1-150 $O/shard_kernel_stats.csv | head -14 ;;
+    dist)
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 \
+        bench.py --gpus 2 --steps 6 --warmup 2 --nodes 200000 --dist-backend gloo --no-cpu-baseline --no-pmc --hbm-nodes 0 \
+        --pcie-steps 0 --report-every 3 > $O/bench_dist.json 2> $O/bench_dist.err || { tail -30 $O/bench_dist.err; exit 1; }
+      cut -c1-300 $O/bench_dist.json ;;
     ab)
       cp kwok_amd/lib/libkwok_engine.so $O/cur.so
       for i in 1 2; do
         for v in cur other; do
-          if [ $v = other ]; then cp tools/build/$arg kwok_amd/lib/libkwok_engine.so; else cp $O/cur.so kwok_amd/lib/libkwok_engine.so; fi
+          if [ $v = other ]; then cp tools/ab/$arg kwok_amd/lib/libkwok_engine.so; else cp $O/cur.so kwok_amd/lib/libkwok_engine.so; fi
           timeout -k 10 200 python -u bench.py $B1 --no-pmc --no-cpu-baseline > $O/${v}_$i.json 2> $O/${v}_$i.err \
             || { cp $O/cur.so kwok_amd/lib/libkwok_engine.so; tail -20 $O/${v}_$i.err; exit 1; }
           python -c "import json; d=json.load(open('$O/${v}_$i.json')); print('$v', $i, d['value'], 'ms/step', d['ms_per_step'], 'sweep us', d['detail']['pod_sweep_us_mean'])"
