@@ -211,6 +211,89 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
     return last, n_fired_host
 
 
+def synth_ipv4(first: int, n: int, lead: int, stride: int) -> np.ndarray:
+    """[length][text] rows of distinct-looking IPv4 strings "<lead>.ddd.ddd.ddd" (octets 100-255,
+    14 characters) for slots first..first+n: the bench's stand-in for the controller's per-pod
+    funcPodIPWith / funcNodeIPWith values (pod_controller.go:563-600)."""
+    s = np.arange(first, first + n, dtype=np.int64)
+    rows = np.zeros((n, stride), dtype=np.uint8)
+    rows[:, 0] = 14
+    rows[:, 1:3] = np.frombuffer(str(lead).encode(), dtype=np.uint8)
+    for k, div in enumerate((156 * 156, 156, 1)):
+        o = 100 + (s // div) % 156
+        base = 3 + 4 * k
+        rows[:, base] = ord(".")
+        rows[:, base + 1] = ord("0") + o // 100
+        rows[:, base + 2] = ord("0") + (o // 10) % 10
+        rows[:, base + 3] = ord("0") + o % 10
+    return rows
+
+
+def measure_patch_emit(pods, pvars, pidx, args, dt, k0):
+    """Device patch emission (include/kwok_emit.h) over the C5 pod lists: per step, the pod sweep
+    with packed hand-back, then kwk_emit expands the fired list into the merge-patch bytes of every
+    fired pod (pod-ready / pod-complete statusTemplate; pod-delete has none) on the device.  The
+    skeletons come from the variant objects (kwk_patch_skeleton / kwk_patch_object_values); the
+    per-pod call values (NodeIPWith / PodIPWith) are synthetic IPv4 text (synth_ipv4); guard bits
+    start from the variants' status and are carried by the emitter.  Timed with HIP events around
+    the three emission kernels; bytes = the patch bytes written."""
+    from kwok_amd.host import emit
+    from kwok_amd.host.patchtpl import PatchProgram
+    pprog = pods.p
+    pp = PatchProgram(pprog.stages, {"NodeIPWith": lambda *a: "10.100.100.100", "PodIPWith": lambda *a: "11.100.100.100"})
+    vcls = [pprog.class_of(v, register=False) for v in pvars]
+    ep = emit.EmitProgram(pprog.stages, pp, dict(zip(vcls, pvars)), len(pprog.class_ids), stride=16)
+    wv = []
+    for c, v in zip(vcls, pvars):
+        acc = 0
+        for tid in range(ep.host_tid):
+            sk = ep.skel.get((c, tid))
+            if sk is not None:
+                acc |= int(pp.object_values(tid, [v], sk["text"], sk["calls"], ep.stride)[1][0]) << tid
+        wv.append(c | ep.guard_bits(v) << 16 | acc << 32)
+    n = pods.capacity
+    em = emit.Emitter(pods, n, ep)
+    chunk = 1 << 24
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        em.set_rows(a, np.asarray(wv, dtype=np.uint64)[pidx[a:b]], {})
+        for c in range(ep.n_columns):
+            em.set_column(c, a, synth_ipv4(a, b - a, 10 + c, ep.stride))
+    max_skel = max((sum(len(x.encode()) for x in sk["lits"]) + 40 * len(sk["slots"]) for sk in ep.skel.values()),
+                   default=1)
+    times, nbytes, recs, emitted = [], 0, 0, 0
+    for k in range(k0, k0 + args.emit_steps + 1):  # the first step sizes the output buffers (untimed)
+        now = NOW0 + k * dt
+        pods.step_n(1, now, dt, args.seed, k, "packed")
+        em.emit(now, packed=True)
+        ni, nb = em.result()
+        if ni < 0:
+            ni = -ni - 1
+            em.reserve(int(ni * 1.5) + 1024, int(max(nb, ni * max_skel) * 1.5) + 4096)
+            em.emit(now, packed=True)
+            ni, nb = em.result()
+            assert ni >= 0, "emission reservation"
+        if k == k0:
+            continue
+        times.append(em.elapsed_ms())
+        ni, ne, nb = em.stats()
+        nbytes += nb
+        recs += ni
+        emitted += ne
+    em.close()
+    t = sum(times) / 1e3
+    return {"patches_per_s": round(emitted / t, 1) if t else None, "unit": "merge patches/sec (device bytes)",
+            "steps": args.emit_steps, "items_per_step": recs / max(1, len(times)),
+            "host_items_per_step": (recs - emitted) / max(1, len(times)),
+            "patch_bytes_per_step": nbytes / max(1, len(times)),
+            "avg_emit_us": round(statistics.mean(times) * 1e3, 2) if times else None,
+            "written_GBps": round(nbytes / t / 1e9, 1) if t else None,
+            "write_frac_of_hbm_peak": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4) if t else None,
+            "skeletons": len(ep.skel), "guards": [["/".join(p), "/".join(b)] for p, b in ep.guards],
+            "note": "kwk_emit after each pod step (packed list): emit_size + emit_scan + emit_write kernels, "
+                    "HIP events; call values synthetic IPv4 text; parity: tests/test_gpu_emit.py"}
+
+
 def sweep_bytes(s0, s1):
     return s1["bytes"] - s0["bytes"], s1["line_bytes"] - s0["line_bytes"]
 
@@ -479,6 +562,7 @@ def main():
     ap.add_argument("--hbm-only", action="store_true", help="diagnostic: only the C2-mix HBM working-set run")
     ap.add_argument("--hbm-warmup", type=int, default=12)
     ap.add_argument("--pcie-steps", type=int, default=5)
+    ap.add_argument("--emit-steps", type=int, default=5, help="device patch emission steps after the timed run (0: off)")
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
     ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
@@ -556,7 +640,6 @@ def main():
     pods, nodes, (pvars, pidx) = build_engines(nlo, nhi, args.pods_per_node, local_rank, args.seed, args.job_frac,
                                                wide_state=args.wide_state)
     configure_usage(pods, pvars, pidx, nhi - nlo, args.pods_per_node)
-    del pidx
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
@@ -655,6 +738,11 @@ def main():
                     "kwk_fired, 8 B per transition")}
         for p in pin:
             p.close()
+    patch_emit = None
+    if args.emit_steps > 0 and world == 1:
+        log("device patch emission run")
+        patch_emit = measure_patch_emit(pods, pvars, pidx, args, dt, args.warmup + args.steps + max(0, args.pcie_steps))
+    del pidx
     if reporter.comm is not None:
         reporter.comm.close()
     pods.close()
@@ -712,6 +800,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_soa": cpu_soa,
             "pcie_inclusive": pcie,
+            "patch_emit": patch_emit,
             "hbm_working_set": hbm,
             "aggregates": agg_dict,
             "detail": {"transitions_per_step": total_fired / args.steps, "per_stage_rank0": per_stage,

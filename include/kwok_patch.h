@@ -69,6 +69,35 @@ kwk_status kwk_patch_render(kwk_patcher* p, uint32_t n, const uint16_t* template
                             const uint64_t* obj_offsets, int64_t now_ns, kwk_patch_fn fn, void* user,
                             uint32_t n_threads, const char** out_data, uint64_t* out_offsets, uint8_t* status);
 
+/* ---- skeletons for device emission (kwok_emit.h)
+ *
+ * The skeleton of template `tid` over an object class: the template rendered over the class's
+ * representative `obj` with every per-object input kept out — the object's status and identity
+ * (what the compiler's class key drops: status, metadata identity keys and ownerReferences,
+ * spec.nodeName / hostname) are not read, Now and each call of a callback function become slots.
+ * Eligible only when those inputs reach the patch solely as slot text, as call arguments
+ * (identity, not status: a call's value is fixed per object) or through the Stages' status guard
+ * `index $root.status.<list> $i` in `range $i, ... := <class-level list>` (its one effect is the
+ * error when the status list is shorter; the device checks a per-object bit instead).
+ * *out_json (owned by the patcher until its next skeleton call):
+ *   {"eligible": true, "text": <the patch with slot markers>, "lits": [n_slots + 1 literal runs],
+ *    "slots": [slot ids: 0 = Now, 1 + c = call site c], "calls": n_call_sites,
+ *    "guards": [[<status list path>, <range list path>], ...]}
+ *   or {"eligible": false, "reason": "..."}.
+ * Objects of the class render (kwk_patch_render) to the literal runs with the slots filled in —
+ * Now as RFC3339Nano, call c as its value — when kwk_patch_object_values accepts them. */
+kwk_status kwk_patch_skeleton(kwk_patcher* p, uint32_t tid, const char* obj, uint64_t len, const char** out_json,
+                              uint64_t* out_len);
+
+/* Per object i (the objects of one class): renders template tid in skeleton mode with the call
+ * sites evaluated for real (fn), ok[i] = 1 when the result equals `skeleton` (the class's "text")
+ * and every call value fits stride - 1 bytes of characters JSON and YAML carry unchanged
+ * (printable ASCII without " \ ' < > &).  values[(i * n_calls + c) * stride] = [length][bytes] of
+ * call site c (length 0xFF: unusable). */
+kwk_status kwk_patch_object_values(kwk_patcher* p, uint32_t tid, uint32_t n, const char* objs, const uint64_t* obj_offsets,
+                                   const char* skeleton, uint64_t skeleton_len, kwk_patch_fn fn, void* user,
+                                   uint32_t n_threads, uint32_t n_calls, uint32_t stride, uint8_t* values, uint8_t* ok);
+
 #ifdef __cplusplus
 }
 #endif

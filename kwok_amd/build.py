@@ -20,7 +20,8 @@ ENC_HDR = [os.path.join(ROOT, "include", "kwok_encoder.h"), os.path.join(ROOT, "
            os.path.join(PKG, "csrc", "gotpl.hpp"), os.path.join(PKG, "csrc", "labelsel.hpp")]
 ENC_OUT = os.path.join(PKG, "lib", "libkwok_encoder.so")
 PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
-PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR]
+PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR,
+             os.path.join(PKG, "csrc", "timefmt.hpp")]
 PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
 COMPILER_SRC = [os.path.join(PKG, "csrc", "compiler.cpp")]
 COMPILER_HDR = [os.path.join(ROOT, "include", "kwok_compiler.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR] + \
@@ -29,6 +30,10 @@ COMPILER_OUT = os.path.join(PKG, "lib", "libkwok_compiler.so")
 COMM_SRC = [os.path.join(PKG, "csrc", "comm.cpp")]
 COMM_HDR = [os.path.join(ROOT, "include", "kwok_comm.h"), os.path.join(ROOT, "include", "kwok_engine.h")]
 COMM_OUT = os.path.join(PKG, "lib", "libkwok_comm.so")
+EMIT_SRC = [os.path.join(PKG, "csrc", "emit.hip")]
+EMIT_HDR = [os.path.join(ROOT, "include", "kwok_emit.h"), os.path.join(ROOT, "include", "kwok_engine.h"),
+            os.path.join(PKG, "csrc", "timefmt.hpp")]
+EMIT_OUT = os.path.join(PKG, "lib", "libkwok_emit.so")
 ARCH = "gfx950"  # MI355X only
 
 
@@ -83,6 +88,20 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
     return COMM_OUT
 
 
+def build_emit(force: bool = False, verbose: bool = False) -> str:
+    """The device patch emitter (HIP kernels over the engine's fired lists, linked to the engine)."""
+    if not force and not _stale(EMIT_OUT, EMIT_SRC + EMIT_HDR + [OUT]):
+        return EMIT_OUT
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-Wno-unused-value", "-I", os.path.join(ROOT, "include"), "-o", EMIT_OUT + ".tmp"] + \
+        EMIT_SRC + ["-L", os.path.dirname(OUT), "-lkwok_engine", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(EMIT_OUT + ".tmp", EMIT_OUT)
+    return EMIT_OUT
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     build_encoder(force, verbose)
     build_compiler(force, verbose)
@@ -90,6 +109,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         build_patch(force, verbose)
     _build_engine(force, verbose)
     build_comm(force, verbose)
+    build_emit(force, verbose)
     return OUT
 
 

@@ -1,0 +1,692 @@
+// Device patch emission (include/kwok_emit.h): the merge-patch bytes of a step's fired objects,
+// expanded from per-(class, template) skeletons on the engine's stream.
+//
+// Reference: playStage renders each fired object's Stage patches (pkg/utils/lifecycle/
+// next.go:73-160, pkg/utils/gotpl/renderer.go:59-124) — here the host's one-time skeleton build
+// (patch.cpp: kwk_patch_skeleton / kwk_patch_object_values) leaves only Now and the objects' call
+// values (funcPodIPWith / funcNodeIPWith, pod_controller.go:563-600) to fill per fire.
+//
+// Three launches per list, sized by the device-resident record count (no host round trip):
+//   emit_size_kernel   per 1024-record tile: items and bytes (a gather of one 8-byte word per record)
+//   emit_scan_kernel   one workgroup: exclusive bases of the tiles, the totals
+//   emit_write_kernel  per tile again: each record's items / offsets, its guard word, then each wave
+//                      writes its 256 records' bytes, 64 lanes over every literal run and value
+// Roofline: HBM-bound on the patch bytes written (plus 8 bytes read per record and the literal
+// runs, L2-resident); the byte copy is 1-byte stores coalesced per wave.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kwok_emit.h"
+#include "timefmt.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+thread_local std::string* tl_err = nullptr;
+struct ErrScope {
+  std::string* prev;
+  explicit ErrScope(std::string* target) : prev(tl_err) { tl_err = target; }
+  ~ErrScope() { tl_err = prev; }
+};
+kwk_status fail(kwk_status code, const std::string& msg) {
+  g_err = msg;
+  if (tl_err) *tl_err = msg;
+  return code;
+}
+#define HIP_TRY(x)                                                                                \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) return fail(KWK_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr uint32_t kBlock = 256, kPer = 4, kTile = kBlock * kPer;  // records per tile
+constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
+constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
+constexpr uint32_t kScanBlock = 1024;
+
+struct Prog {
+  const uint32_t* stage_tpl_ptr;
+  const uint16_t* stage_tpl;
+  const uint8_t* stage_delete;
+  const int32_t* skel_of;
+  const kwk_emit_skel* skels;
+  const kwk_emit_piece* pieces;
+  const char* lits;
+  const uint8_t* fresh;
+  uint8_t* const* cols;
+  const uint32_t* stride;
+  uint32_t n_classes, n_templates, n_stages;
+};
+
+struct EmitArgs {
+  Prog p;
+  const kwk_fired_rec* recs;  // or
+  const uint32_t* packed;
+  const uint32_t* count;
+  uint64_t* words;
+  uint32_t capacity;
+  uint32_t max_recs;                 // records the tile arrays cover (capacity rounded up)
+  uint32_t* tile_items;              // per tile: items, then (emit_scan_kernel) the exclusive base
+  unsigned long long* tile_bytes;    // per tile: bytes, then the base
+  unsigned long long* totals;        // [0] items, [1] bytes, [2] the list is longer than max_recs, [3] items emitted
+  kwk_emit_item* items;
+  uint64_t* offsets;
+  char* out;
+  unsigned long long cap_items, cap_bytes;
+  uint32_t now_len;
+  char now[40];
+};
+
+struct Rec {
+  uint32_t slot, stage;
+  bool valid;
+};
+
+__device__ __forceinline__ Rec fetch(const EmitArgs& a, uint32_t r) {
+  Rec x;
+  if (a.packed) {
+    const uint32_t v = a.packed[r];
+    x.slot = v & 0x7FFFFFFu;
+    x.stage = v >> 27;
+  } else {
+    const kwk_fired_rec f = a.recs[r];
+    x.slot = f.slot;
+    x.stage = f.stage;
+  }
+  x.valid = x.slot < a.capacity;
+  return x;
+}
+
+// bytes of one skeleton for this slot, or -1 when a value is unusable
+__device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const kwk_emit_skel& S, uint32_t slot) {
+  long long b = 0;
+  for (uint32_t q = 0; q < S.n_pieces; ++q) {
+    const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
+    b += P.lit_len;
+    if (P.slot == 0) {
+      b += a.now_len;
+    } else if (P.slot != KWK_EMIT_NO_SLOT) {
+      const uint32_t c = P.slot - 1u;
+      const uint32_t len = a.p.cols[c][(uint64_t)slot * a.p.stride[c]];
+      if (len == 0xFFu) return -1;
+      b += len;
+    }
+  }
+  return b;
+}
+
+__device__ __forceinline__ int skel_index(const EmitArgs& a, uint64_t w, uint32_t tid) {
+  const uint32_t cls = (uint32_t)(w & 0xFFFFu), g = (uint32_t)(w >> 16) & 0xFFu;
+  if (cls >= a.p.n_classes || tid >= 32u || !((w >> (32u + tid)) & 1u)) return -1;
+  const int k = a.p.skel_of[cls * a.p.n_templates + tid];
+  if (k < 0) return -1;
+  const uint32_t need = a.p.skels[k].need;
+  return (g & need) == need ? k : -1;
+}
+
+struct Size {
+  uint32_t items, ok;  // ok: bit j = the stage's j-th template is emitted here
+  unsigned long long bytes;
+};
+
+__device__ __forceinline__ Size rec_size(const EmitArgs& a, const Rec& x, uint64_t w) {
+  Size s{0u, 0u, 0ull};
+  if (x.stage >= a.p.n_stages) return s;
+  const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
+  for (uint32_t j = t0; j < t1; ++j) {
+    ++s.items;
+    const int k = x.valid ? skel_index(a, w, a.p.stage_tpl[j]) : -1;
+    if (k < 0) continue;
+    const long long b = skel_bytes(a, a.p.skels[k], x.slot);
+    if (b < 0) continue;
+    s.ok |= 1u << (j - t0);
+    s.bytes += (unsigned long long)b;
+  }
+  return s;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl(T v, uint32_t lane) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(v, o);
+    if (lane >= (uint32_t)o) v += y;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void emit_size_kernel(EmitArgs a) {
+  __shared__ uint32_t s_i[kWaves];
+  __shared__ unsigned long long s_b[kWaves];
+  const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    uint32_t it = 0;
+    unsigned long long by = 0;
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t r = t * kTile + threadIdx.x * kPer + k;
+      if (r >= n) break;
+      const Rec x = fetch(a, r);
+      const Size s = rec_size(a, x, x.valid ? a.words[x.slot] : 0ull);
+      it += s.items;
+      by += s.bytes;
+    }
+    it = wave_sum(it);
+    by = wave_sum(by);
+    if (lane == 0) {
+      s_i[wave] = it;
+      s_b[wave] = by;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t ti = 0;
+      unsigned long long tb = 0;
+      for (uint32_t w = 0; w < kWaves; ++w) {
+        ti += s_i[w];
+        tb += s_b[w];
+      }
+      a.tile_items[t] = ti;
+      a.tile_bytes[t] = tb;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
+  __shared__ uint32_t s_i[kScanBlock / 64];
+  __shared__ unsigned long long s_b[kScanBlock / 64];
+  const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t run_i = 0;
+  unsigned long long run_b = 0;
+  for (uint32_t base = 0; base < n_tiles; base += kScanBlock) {
+    const uint32_t t = base + threadIdx.x;
+    const uint32_t vi = t < n_tiles ? a.tile_items[t] : 0u;
+    const unsigned long long vb = t < n_tiles ? a.tile_bytes[t] : 0ull;
+    const uint32_t ii = wave_incl(vi, lane);
+    const unsigned long long ib = wave_incl(vb, lane);
+    if (lane == 63) {
+      s_i[wave] = ii;
+      s_b[wave] = ib;
+    }
+    __syncthreads();
+    uint32_t pi = 0, ti = 0;
+    unsigned long long pb = 0, tb = 0;
+    for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
+      if (w < wave) {
+        pi += s_i[w];
+        pb += s_b[w];
+      }
+      ti += s_i[w];
+      tb += s_b[w];
+    }
+    if (t < n_tiles) {
+      a.tile_items[t] = run_i + pi + ii - vi;
+      a.tile_bytes[t] = run_b + pb + ib - vb;
+    }
+    run_i += ti;
+    run_b += tb;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.totals[0] = run_i;
+    a.totals[1] = run_b;
+    a.totals[2] = *a.count > a.max_recs ? 1ull : 0ull;
+    a.totals[3] = 0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
+  __shared__ uint32_t s_slot[kTile];
+  __shared__ uint32_t s_meta[kTile];  // ok mask [15:0] | stage [23:16] | class in s_cls
+  __shared__ uint32_t s_cls[kTile];
+  __shared__ unsigned long long s_base[kTile];
+  __shared__ uint32_t s_wi[kWaves];
+  __shared__ unsigned long long s_wb[kWaves];
+  __shared__ char s_now[40];
+  const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
+  const unsigned long long tot_i = a.totals[0], tot_b = a.totals[1];
+  if (tot_i > a.cap_items || tot_b > a.cap_bytes || a.totals[2]) return;  // KWK_ECAP: nothing is written
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.offsets[tot_i] = tot_b;
+  if (threadIdx.x < 40) s_now[threadIdx.x] = a.now[threadIdx.x];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t n_ok = 0;
+  for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    Rec x[kPer];
+    uint64_t w[kPer];
+    Size s[kPer];
+    uint32_t it = 0;
+    unsigned long long by = 0;
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t r = t * kTile + threadIdx.x * kPer + k;
+      s[k] = Size{0u, 0u, 0ull};
+      x[k] = Rec{0u, 0xFFFFFFFFu, false};
+      w[k] = 0;
+      if (r < n) {
+        x[k] = fetch(a, r);
+        w[k] = x[k].valid ? a.words[x[k].slot] : 0ull;
+        s[k] = rec_size(a, x[k], w[k]);
+      }
+      it += s[k].items;
+      by += s[k].bytes;
+      n_ok += (uint32_t)__popc(s[k].ok);
+    }
+    // block-exclusive prefix of the threads' items / bytes, plus the tile's base
+    const uint32_t ii = wave_incl(it, lane);
+    const unsigned long long ib = wave_incl(by, lane);
+    if (lane == 63) {
+      s_wi[wave] = ii;
+      s_wb[wave] = ib;
+    }
+    __syncthreads();
+    uint32_t item = a.tile_items[t] + ii - it;
+    unsigned long long pos = a.tile_bytes[t] + ib - by;
+    for (uint32_t v = 0; v < wave; ++v) {
+      item += s_wi[v];
+      pos += s_wb[v];
+    }
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t lr = threadIdx.x * kPer + k, r = t * kTile + lr;
+      s_slot[lr] = x[k].slot;
+      s_meta[lr] = s[k].ok | (r < n ? (x[k].stage & 0xFFu) << 16 : 0xFFu << 16);
+      s_cls[lr] = (uint32_t)(w[k] & 0xFFFFu);
+      s_base[lr] = pos;
+      if (r >= n || x[k].stage >= a.p.n_stages) continue;
+      const uint32_t t0 = a.p.stage_tpl_ptr[x[k].stage], t1 = a.p.stage_tpl_ptr[x[k].stage + 1];
+      uint32_t g = (uint32_t)(w[k] >> 16) & 0xFFu;
+      for (uint32_t j = t0; j < t1; ++j, ++item) {
+        const uint32_t tid = a.p.stage_tpl[j];
+        const bool ok = (s[k].ok >> (j - t0)) & 1u;
+        a.items[item] = kwk_emit_item{r, (uint16_t)tid, (uint8_t)(ok ? KWK_EMIT_OK : KWK_EMIT_HOST), 0};
+        a.offsets[item] = pos;
+        if (ok) {
+          const kwk_emit_skel& S = a.p.skels[skel_index(a, w[k], tid)];
+          pos += (unsigned long long)skel_bytes(a, S, x[k].slot);
+          g = (g & S.keep) | S.set;
+        }
+      }
+      // the object's guard bits after the patches (all items emitted here; else the host sets them)
+      const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
+      if (x[k].valid && s[k].ok == all) {
+        const uint32_t cls = (uint32_t)(w[k] & 0xFFFFu);
+        if (a.p.stage_delete[x[k].stage] && cls < a.p.n_classes) g = a.p.fresh[cls];
+        const uint64_t nw = (w[k] & ~(0xFFull << 16)) | (uint64_t)g << 16;
+        if (nw != w[k]) a.words[x[k].slot] = nw;
+      }
+    }
+    __syncthreads();
+    // bytes: wave `wave` writes records [wave * 256, wave * 256 + 256) of the tile, 64 lanes per run
+    for (uint32_t lr = wave * kWaveRecs; lr < (wave + 1) * kWaveRecs; ++lr) {
+      const uint32_t meta = s_meta[lr];
+      const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
+      if (stage >= a.p.n_stages || !ok) continue;
+      const uint32_t slot = s_slot[lr], cls = s_cls[lr];
+      unsigned long long p = s_base[lr];
+      const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
+      for (uint32_t j = t0; j < t1; ++j) {
+        if (!((ok >> (j - t0)) & 1u)) continue;
+        const int sk = a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]];
+        const kwk_emit_skel S = a.p.skels[sk];
+        for (uint32_t q = 0; q < S.n_pieces; ++q) {
+          const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
+          const char* src = a.p.lits + P.lit_off;
+          for (uint32_t o = lane; o < P.lit_len; o += 64u) a.out[p + o] = src[o];
+          p += P.lit_len;
+          if (P.slot == 0) {
+            if (lane < a.now_len) a.out[p + lane] = s_now[lane];
+            p += a.now_len;
+          } else if (P.slot != KWK_EMIT_NO_SLOT) {
+            const uint32_t c = P.slot - 1u;
+            const uint8_t* v = a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
+            const uint32_t len = v[0];
+            for (uint32_t o = lane; o < len; o += 64u) a.out[p + o] = (char)v[1 + o];
+            p += len;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  n_ok = wave_sum(n_ok);
+  if (lane == 0 && n_ok) atomicAdd(&a.totals[3], (unsigned long long)n_ok);
+}
+
+}  // namespace
+
+struct kwk_emitter {
+  std::string err;
+  kwk_engine* eng = nullptr;
+  hipStream_t stream = nullptr;
+  int device = 0;
+  uint32_t capacity = 0, n_columns = 0, max_tiles = 0, grid = 0;
+  Prog p{};
+  std::vector<void*> allocs;
+  std::vector<uint32_t> stride;
+  std::vector<uint8_t*> cols;
+  uint64_t* d_words = nullptr;
+  uint32_t* d_tile_items = nullptr;
+  unsigned long long* d_tile_bytes = nullptr;
+  unsigned long long* d_totals = nullptr;
+  kwk_emit_item* d_items = nullptr;
+  uint64_t* d_offsets = nullptr;
+  char* d_out = nullptr;
+  uint64_t cap_items = 0, cap_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool emitted = false;
+
+  ~kwk_emitter() {
+    hipSetDevice(device);
+    if (stream) hipStreamSynchronize(stream);
+    for (void* x : allocs) hipFree(x);
+    if (d_items) hipFree(d_items);
+    if (d_offsets) hipFree(d_offsets);
+    if (d_out) hipFree(d_out);
+    if (ev0) hipEventDestroy(ev0);
+    if (ev1) hipEventDestroy(ev1);
+  }
+};
+
+namespace {
+
+template <typename T>
+kwk_status upload(kwk_emitter* em, T** dst, const T* src, size_t n) {
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, std::max<size_t>(1, n) * sizeof(T)));
+  em->allocs.push_back(d);
+  if (n) HIP_TRY(hipMemcpy(d, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *dst = static_cast<T*>(d);
+  return KWK_OK;
+}
+
+kwk_status check_program(const kwk_emit_program* g) {
+  if (!g->stage_tpl_ptr || !g->stage_delete || (g->n_classes && !g->fresh_guards) ||
+      (g->n_classes * g->n_templates && !g->skel_of))
+    return fail(KWK_EINVAL, "emit program: null array");
+  if (g->n_templates > 32) return fail(KWK_EINVAL, "emit program: more than 32 templates");
+  if ((uint64_t)g->n_classes * g->n_templates > (1u << 26)) return fail(KWK_EINVAL, "emit program: too many skeletons");
+  if (g->stage_tpl_ptr[0] != 0) return fail(KWK_EINVAL, "emit program: stage_tpl_ptr[0] != 0");
+  for (uint32_t s = 0; s < g->n_stages; ++s) {
+    const uint32_t a = g->stage_tpl_ptr[s], b = g->stage_tpl_ptr[s + 1];
+    if (b < a || b - a > kMaxStageTpl) return fail(KWK_EINVAL, "emit program: stage template ranges");
+  }
+  const uint32_t n_st = g->stage_tpl_ptr[g->n_stages];
+  if (n_st && !g->stage_tpl) return fail(KWK_EINVAL, "emit program: null stage_tpl");
+  for (uint32_t j = 0; j < n_st; ++j)
+    if (g->stage_tpl[j] >= g->n_templates) return fail(KWK_EINVAL, "emit program: template id out of range");
+  for (uint64_t i = 0; i < (uint64_t)g->n_classes * g->n_templates; ++i)
+    if (g->skel_of[i] < -1 || g->skel_of[i] >= (int64_t)g->n_skels) return fail(KWK_EINVAL, "emit program: skeleton index");
+  if ((g->n_skels && !g->skels) || (g->n_pieces && !g->pieces) || (g->n_lit_bytes && !g->lits) ||
+      (g->n_columns && !g->column_stride))
+    return fail(KWK_EINVAL, "emit program: null array");
+  for (uint32_t k = 0; k < g->n_skels; ++k) {
+    const kwk_emit_skel& S = g->skels[k];
+    if ((uint64_t)S.first_piece + S.n_pieces > g->n_pieces) return fail(KWK_EINVAL, "emit program: piece range");
+  }
+  for (uint32_t q = 0; q < g->n_pieces; ++q) {
+    const kwk_emit_piece& P = g->pieces[q];
+    if ((uint64_t)P.lit_off + P.lit_len > g->n_lit_bytes) return fail(KWK_EINVAL, "emit program: literal range");
+    if (P.slot != KWK_EMIT_NO_SLOT && P.slot > g->n_columns) return fail(KWK_EINVAL, "emit program: slot out of range");
+  }
+  for (uint32_t c = 0; c < g->n_columns; ++c)
+    if (g->column_stride[c] < 2 || g->column_stride[c] > 256) return fail(KWK_EINVAL, "emit program: column stride 2..256");
+  return KWK_OK;
+}
+
+kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
+  em->p.n_classes = g->n_classes;
+  em->p.n_templates = g->n_templates;
+  em->p.n_stages = g->n_stages;
+  const uint32_t n_st = g->stage_tpl_ptr[g->n_stages];
+  if (kwk_status st = upload(em, const_cast<uint32_t**>(&em->p.stage_tpl_ptr), g->stage_tpl_ptr, g->n_stages + 1)) return st;
+  if (kwk_status st = upload(em, const_cast<uint16_t**>(&em->p.stage_tpl), g->stage_tpl, n_st)) return st;
+  if (kwk_status st = upload(em, const_cast<uint8_t**>(&em->p.stage_delete), g->stage_delete, g->n_stages)) return st;
+  if (kwk_status st = upload(em, const_cast<int32_t**>(&em->p.skel_of), g->skel_of, (size_t)g->n_classes * g->n_templates))
+    return st;
+  if (kwk_status st = upload(em, const_cast<kwk_emit_skel**>(&em->p.skels), g->skels, g->n_skels)) return st;
+  if (kwk_status st = upload(em, const_cast<kwk_emit_piece**>(&em->p.pieces), g->pieces, g->n_pieces)) return st;
+  if (kwk_status st = upload(em, const_cast<char**>(&em->p.lits), g->lits, g->n_lit_bytes)) return st;
+  if (kwk_status st = upload(em, const_cast<uint8_t**>(&em->p.fresh), g->fresh_guards, g->n_classes)) return st;
+  em->n_columns = g->n_columns;
+  em->stride.assign(g->column_stride, g->column_stride + g->n_columns);
+  for (uint32_t c = 0; c < g->n_columns; ++c) {
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)em->capacity * em->stride[c] + 1));
+    em->allocs.push_back(d);
+    HIP_TRY(hipMemset(d, 0xFF, (size_t)em->capacity * em->stride[c] + 1));  // every value unusable until set
+    em->cols.push_back(static_cast<uint8_t*>(d));
+  }
+  if (kwk_status st = upload(em, const_cast<uint8_t***>(&em->p.cols), em->cols.data(), em->cols.size())) return st;
+  if (kwk_status st = upload(em, const_cast<uint32_t**>(&em->p.stride), em->stride.data(), em->stride.size())) return st;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)std::max(1u, em->capacity) * 8));
+  em->allocs.push_back(d);
+  HIP_TRY(hipMemset(d, 0, (size_t)std::max(1u, em->capacity) * 8));  // class 0, nothing accepted: all to the host
+  em->d_words = static_cast<uint64_t*>(d);
+  em->max_tiles = (em->capacity + kTile - 1) / kTile + 1;
+  HIP_TRY(hipMalloc(&d, (size_t)em->max_tiles * 4));
+  em->allocs.push_back(d);
+  em->d_tile_items = static_cast<uint32_t*>(d);
+  HIP_TRY(hipMalloc(&d, (size_t)em->max_tiles * 8));
+  em->allocs.push_back(d);
+  em->d_tile_bytes = static_cast<unsigned long long*>(d);
+  HIP_TRY(hipMalloc(&d, 4 * 8));
+  em->allocs.push_back(d);
+  em->d_totals = static_cast<unsigned long long*>(d);
+  HIP_TRY(hipMemset(d, 0, 4 * 8));
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, em->device));
+  em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 4u));
+  HIP_TRY(hipEventCreate(&em->ev0));
+  HIP_TRY(hipEventCreate(&em->ev1));
+  return KWK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kwk_emit_last_error(const kwk_emitter* em) { return em ? em->err.c_str() : g_err.c_str(); }
+
+kwk_status kwk_emitter_create(kwk_engine* eng, uint32_t capacity, const kwk_emit_program* prog, kwk_emitter** out) {
+  ErrScope es_(nullptr);
+  if (!eng || !prog || !out) return fail(KWK_EINVAL, "null argument");
+  if (capacity > (1u << 27)) return fail(KWK_EINVAL, "capacity above 2^27 slots");
+  if (kwk_status st = check_program(prog)) return st;
+  void* s = nullptr;
+  if (kwk_stream(eng, &s) != KWK_OK) return fail(KWK_EINVAL, std::string("kwk_stream: ") + kwk_last_error(eng));
+  auto* em = new kwk_emitter();
+  em->eng = eng;
+  em->stream = static_cast<hipStream_t>(s);
+  em->capacity = capacity;
+  hipError_t e = hipStreamGetDevice(em->stream, &em->device);
+  if (e != hipSuccess) {
+    delete em;
+    return fail(KWK_EHIP, std::string("hipStreamGetDevice: ") + hipGetErrorString(e));
+  }
+  kwk_status st = KWK_OK;
+  if (hipSetDevice(em->device) != hipSuccess) st = fail(KWK_EHIP, "hipSetDevice");
+  if (!st) st = emitter_init(em, prog);
+  if (st) {
+    delete em;
+    return st;
+  }
+  *out = em;
+  return KWK_OK;
+}
+
+kwk_status kwk_emitter_destroy(kwk_emitter* em) {
+  delete em;
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_set_words(kwk_emitter* em, uint32_t first, uint32_t n, const uint64_t* words) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
+  if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  if (n) HIP_TRY(hipMemcpy(em->d_words + first, words, (size_t)n * 8, hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_get_words(kwk_emitter* em, uint32_t first, uint32_t n, uint64_t* words) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
+  if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  if (n) HIP_TRY(hipMemcpy(words, em->d_words + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_set_column(kwk_emitter* em, uint32_t c, uint32_t first, uint32_t n, const uint8_t* data) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || (n && !data)) return fail(KWK_EINVAL, "null argument");
+  if (c >= em->n_columns) return fail(KWK_EINVAL, "column out of range");
+  if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  if (n)
+    HIP_TRY(hipMemcpy(em->cols[c] + (size_t)first * em->stride[c], data, (size_t)n * em->stride[c], hipMemcpyHostToDevice));
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_reserve(kwk_emitter* em, uint32_t max_items, uint64_t max_bytes) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em) return fail(KWK_EINVAL, "null emitter");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  if (max_items > em->cap_items) {
+    if (em->d_items) HIP_TRY(hipFree(em->d_items));
+    if (em->d_offsets) HIP_TRY(hipFree(em->d_offsets));
+    em->d_items = nullptr;
+    em->d_offsets = nullptr;
+    em->cap_items = 0;
+    HIP_TRY(hipMalloc(&em->d_items, (size_t)max_items * sizeof(kwk_emit_item)));
+    HIP_TRY(hipMalloc(&em->d_offsets, ((size_t)max_items + 1) * 8));
+    em->cap_items = max_items;
+  }
+  if (max_bytes > em->cap_bytes) {
+    if (em->d_out) HIP_TRY(hipFree(em->d_out));
+    em->d_out = nullptr;
+    em->cap_bytes = 0;
+    HIP_TRY(hipMalloc(&em->d_out, (size_t)max_bytes));
+    em->cap_bytes = max_bytes;
+  }
+  return KWK_OK;
+}
+
+kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em) return fail(KWK_EINVAL, "null emitter");
+  EmitArgs a{};
+  a.p = em->p;
+  if (source == KWK_EMIT_FROM_RECORDS) {
+    if (kwk_fired_device(em->eng, &a.recs, &a.count) != KWK_OK)
+      return fail(KWK_ESTATE, std::string("kwk_fired_device: ") + kwk_last_error(em->eng));
+  } else if (source == KWK_EMIT_FROM_PACKED) {
+    if (kwk_fired_packed_device(em->eng, &a.packed, &a.count) != KWK_OK)
+      return fail(KWK_ESTATE, std::string("kwk_fired_packed_device: ") + kwk_last_error(em->eng));
+  } else {
+    return fail(KWK_EINVAL, "source must be KWK_EMIT_FROM_RECORDS or KWK_EMIT_FROM_PACKED");
+  }
+  HIP_TRY(hipSetDevice(em->device));
+  if (!em->d_offsets)
+    if (kwk_status st = kwk_emit_reserve(em, 1, 1)) return st;
+  a.words = em->d_words;
+  a.capacity = em->capacity;
+  a.max_recs = (em->max_tiles - 1) * kTile;
+  a.tile_items = em->d_tile_items;
+  a.tile_bytes = em->d_tile_bytes;
+  a.totals = em->d_totals;
+  a.items = em->d_items;
+  a.offsets = em->d_offsets;
+  a.out = em->d_out;
+  a.cap_items = em->cap_items;
+  a.cap_bytes = em->cap_bytes;
+  const std::string now = kwkfmt::rfc3339nano(now_ns);
+  if (now.size() >= sizeof a.now) return fail(KWK_EINVAL, "Now() text too long");
+  memcpy(a.now, now.data(), now.size());
+  a.now_len = (uint32_t)now.size();
+  // the list's count lives on the device: every tile loop reads it; the grid covers the capacity
+  HIP_TRY(hipEventRecord(em->ev0, em->stream));
+  hipLaunchKernelGGL(emit_size_kernel, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(emit_write_kernel, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(em->ev1, em->stream));
+  em->emitted = true;
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_result(kwk_emitter* em, uint32_t* n_items, uint64_t* n_bytes) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || !n_items || !n_bytes) return fail(KWK_EINVAL, "null argument");
+  if (!em->emitted) return fail(KWK_ESTATE, "kwk_emit must come first");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  unsigned long long t[3];
+  HIP_TRY(hipMemcpy(t, em->d_totals, sizeof t, hipMemcpyDeviceToHost));
+  *n_items = (uint32_t)t[0];
+  *n_bytes = t[1];
+  if (t[2]) return fail(KWK_ECAP, "the fired list is longer than the emitter's capacity");
+  if (t[0] > em->cap_items || t[1] > em->cap_bytes)
+    return fail(KWK_ECAP, "emission exceeds the reservation: kwk_emit_reserve(" + std::to_string(t[0]) + ", " +
+                              std::to_string(t[1]) + ") and emit again");
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_stats(kwk_emitter* em, uint32_t* n_items, uint32_t* n_emitted, uint64_t* n_bytes) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || !n_items || !n_emitted || !n_bytes) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = kwk_emit_result(em, n_items, n_bytes)) return st;
+  unsigned long long t = 0;
+  HIP_TRY(hipMemcpy(&t, em->d_totals + 3, 8, hipMemcpyDeviceToHost));
+  *n_emitted = (uint32_t)t;
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_device(kwk_emitter* em, const kwk_emit_item** items, const uint64_t** offsets, const char** bytes) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em) return fail(KWK_EINVAL, "null emitter");
+  if (items) *items = em->d_items;
+  if (offsets) *offsets = em->d_offsets;
+  if (bytes) *bytes = em->d_out;
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_copy(kwk_emitter* em, kwk_emit_item* items, uint64_t* offsets, char* bytes) {
+  ErrScope es_(em ? &em->err : nullptr);
+  uint32_t ni = 0;
+  uint64_t nb = 0;
+  if (kwk_status st = kwk_emit_result(em, &ni, &nb)) return st;
+  if ((ni && (!items || !offsets)) || (nb && !bytes) || !offsets) return fail(KWK_EINVAL, "null argument");
+  if (ni) HIP_TRY(hipMemcpy(items, em->d_items, (size_t)ni * sizeof(kwk_emit_item), hipMemcpyDeviceToHost));
+  if (ni) HIP_TRY(hipMemcpy(offsets, em->d_offsets, ((size_t)ni + 1) * 8, hipMemcpyDeviceToHost));
+  else offsets[0] = 0;
+  if (nb) HIP_TRY(hipMemcpy(bytes, em->d_out, (size_t)nb, hipMemcpyDeviceToHost));
+  return KWK_OK;
+}
+
+kwk_status kwk_emit_elapsed(kwk_emitter* em, float* ms) {
+  ErrScope es_(em ? &em->err : nullptr);
+  if (!em || !ms) return fail(KWK_EINVAL, "null argument");
+  if (!em->emitted) return fail(KWK_ESTATE, "kwk_emit must come first");
+  HIP_TRY(hipSetDevice(em->device));
+  HIP_TRY(hipEventSynchronize(em->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, em->ev0, em->ev1));
+  return KWK_OK;
+}
+
+}  // extern "C"

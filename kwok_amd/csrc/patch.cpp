@@ -27,6 +27,7 @@
 #include "../../include/kwok_engine.h"
 #include "../../include/kwok_patch.h"
 #include "json_dom.hpp"
+#include "timefmt.hpp"
 
 namespace {
 
@@ -49,6 +50,11 @@ kwk_status fail(kwk_status code, const std::string& msg) {
 }
 
 struct NeedsRender {};  // thrown while rendering one object: fall back to the host renderer
+// skeleton mode: the template's bytes depend on more than the object's class, Now and the values
+// of its call sites (see kwk_patch_skeleton)
+struct Ineligible {
+  const char* why;
+};
 struct BadSpec {
   std::string what;
 };
@@ -237,6 +243,7 @@ struct kwk_patcher {
   std::vector<Func> funcs;
   std::vector<JV> consts;
   std::string out;  // the last render's patches
+  std::string skel;  // the last kwk_patch_skeleton result
 };
 
 namespace {
@@ -247,6 +254,12 @@ enum VK : uint8_t { V_MISSING, V_NIL, V_BOOL, V_NUM, V_STR, V_ARR, V_OBJ };
 struct Val {
   VK k = V_MISSING;
   bool b = false;
+  // skeleton mode only (see Skel): 1 = per-object data, not read (status, identity); 2 = holds
+  // such data below it (the object, its metadata / spec)
+  uint8_t taint = 0;
+  int8_t sent = -1;     // skeleton mode: a slot's value (0 = Now, 1 + c = call site c)
+  int32_t path = -1;    // skeleton mode: interned root-relative path of a value read from the object
+  int32_t idx_of = -1;  // skeleton mode: a range index over the array at this path
   const std::string* sp = nullptr;  // V_NUM / V_STR text held by the DOM or the program
   std::string own;                  // computed V_NUM / V_STR text
   const JV* j = nullptr;            // V_ARR / V_OBJ
@@ -477,33 +490,70 @@ int basic(const Val& v) {
   }
 }
 
-std::string rfc3339nano(int64_t ns) {
-  int64_t sec = ns / 1000000000, frac = ns % 1000000000;
-  if (frac < 0) { frac += 1000000000; sec -= 1; }
-  int64_t days = sec / 86400, rem = sec % 86400;
-  if (rem < 0) { rem += 86400; days -= 1; }
-  // civil_from_days (proleptic Gregorian)
-  days += 719468;
-  const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
-  const int64_t doe = days - era * 146097;
-  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-  int64_t y = yoe + era * 400;
-  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
-  const int64_t mp = (5 * doy + 2) / 153;
-  const int64_t d = doy - (153 * mp + 2) / 5 + 1;
-  const int64_t m = mp < 10 ? mp + 3 : mp - 9;
-  if (m <= 2) ++y;
-  char buf[64];
-  snprintf(buf, sizeof buf, "%04lld-%02lld-%02lldT%02lld:%02lld:%02lld", (long long)y, (long long)m, (long long)d,
-           (long long)(rem / 3600), (long long)(rem / 60 % 60), (long long)(rem % 60));
-  std::string s(buf);
-  if (frac) {
-    snprintf(buf, sizeof buf, ".%09lld", (long long)frac);
-    std::string f(buf);
-    while (f.back() == '0') f.pop_back();
-    s += f;
+using kwkfmt::rfc3339nano;
+
+// ------------------------------------------------------------------ skeleton mode
+// A template rendered over a class representative with every per-object input replaced: the
+// object's status and identity (the parts kwok_amd/host/compiler.py:class_key drops — status,
+// metadata identity keys and ownerReferences, spec.nodeName / hostname) are never read, Now and
+// every call of a controller function become slots.  The render succeeds only if those inputs
+// reach the output solely as slot text (Quote'd / single-quoted scalars), call arguments
+// (identity only: a call's value is fixed per object) or the one status read the pod Stages make,
+// `index $root.status.<list> $i` inside `range $i, ... := <class-level list>` whose only effect is
+// its error when the status list is shorter (a guard: the device checks a per-object bit instead).
+// Every object of the class then renders to the skeleton's bytes with the slots filled in.
+constexpr const char* kMarker = "\xF4\x8F\xBF\xBD";  // U+10FFFD: JSON and YAML carry it unchanged
+constexpr size_t kMarkerLen = 4;
+constexpr int kMaxSites = 24;
+
+struct Skel {
+  bool calls = false;  // per-object mode: call sites evaluated for real, their values recorded
+  int in_ext = 0;      // > 0 while a call's arguments are evaluated
+  std::vector<std::vector<std::string>> paths{{}};  // [0] = the object itself
+  std::vector<std::pair<int, int>> guards;          // (status list path, range collection path)
+  std::vector<const Expr*> sites;
+  std::vector<std::string> values;
+  uint32_t markers = 0;
+
+  int extend(int base, const std::string& name) {
+    std::vector<std::string> p = paths[(size_t)base];
+    p.push_back(name);
+    for (size_t i = 0; i < paths.size(); ++i)
+      if (paths[i] == p) return (int)i;
+    paths.push_back(std::move(p));
+    return (int)paths.size() - 1;
   }
-  return s + "Z";
+  // 0 class-level, 1 per-object, 2 an ancestor of per-object fields (compiler.py class_key)
+  int taint_of(int id) const {
+    static const char* identity[] = {"name", "generateName", "namespace", "uid", "resourceVersion", "creationTimestamp",
+                                     "generation", "managedFields", "deletionTimestamp", "deletionGracePeriodSeconds",
+                                     "finalizers", "labels", "annotations", "selfLink", "ownerReferences"};
+    const std::vector<std::string>& p = paths[(size_t)id];
+    if (p.empty()) return 2;
+    if (p[0] == "status") return 1;
+    if (p[0] == "metadata") {
+      if (p.size() == 1) return 2;
+      for (const char* k : identity)
+        if (p[1] == k) return 1;
+      return 0;
+    }
+    if (p[0] == "spec") {
+      if (p.size() == 1) return 2;
+      return p[1] == "nodeName" || p[1] == "hostname" ? 1 : 0;
+    }
+    return 0;
+  }
+  void marker(std::string& o, int id) {
+    o += kMarker;
+    o += (char)('A' + id);
+    o += kMarker;
+    ++markers;
+  }
+};
+
+// a value whose data is per-object (or a slot's) must not be tested, printed or transformed
+inline bool safe_value_char(unsigned char c) {
+  return c >= 0x20 && c <= 0x7E && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&' && c != '\'';
 }
 
 // ------------------------------------------------------------------ rendering
@@ -519,16 +569,58 @@ struct Ctx {
   std::string* out = nullptr;
   JV empty_obj;
   std::vector<char> fbuf;
+  Skel* sk = nullptr;  // skeleton mode
 
   explicit Ctx(const kwk_patcher& p) : P(p) { empty_obj.t = JV::OBJ; fbuf.resize(256); }
 
+  // skeleton mode: v is consumed (tested, printed, transformed, passed to a call)
+  void use(const Val& v) const {
+    if (!sk) return;
+    if (v.sent >= 0) throw Ineligible{"a Now / call value is tested or transformed"};
+    if (v.taint == 1) throw Ineligible{"per-object data reaches the output or a test"};
+    if (v.taint == 2 && (sk->in_ext == 0 || v.path == 0)) throw Ineligible{"a value holding per-object data is consumed"};
+  }
+
+  Val field_sk(Val v, const std::vector<std::string>& names) {
+    for (const std::string& name : names) {
+      const int np = v.path >= 0 ? sk->extend(v.path, name) : -1;
+      if (v.taint == 1) {
+        v.path = np;
+        continue;
+      }
+      if (v.k == V_MISSING) return Val{};  // absent for the whole class (the parent's presence is)
+      if (v.k != V_OBJ) throw NeedsRender{};
+      const int t = np >= 0 ? sk->taint_of(np) : 0;
+      if (t == 1) {
+        if (sk->in_ext == 0) {
+          Val x;
+          x.taint = 1;
+          x.path = np;
+          v = x;
+          continue;
+        }
+        if (sk->paths[(size_t)np][0] == "status") throw Ineligible{"a call argument reads status"};
+      }
+      const JV* x = v.j->get(name);
+      v = x ? from_jv(x) : Val{};
+      v.path = np;
+      v.taint = t == 2 ? 2 : 0;
+    }
+    return v;
+  }
+
   Val eval(const Expr& e, const Val& dot) {
     switch (e.k) {
-      case E_ROOT: return from_jv(root);
+      case E_ROOT: {
+        Val r = from_jv(root);
+        if (sk) { r.path = 0; r.taint = 2; }
+        return r;
+      }
       case E_DOT: return dot;
       case E_VAR: return vars[(size_t)e.i];
       case E_FIELD: {
         Val v = eval(e.a[0], dot);
+        if (sk) return field_sk(v, e.path);
         for (const std::string& name : e.path) {
           if (v.k == V_MISSING) return v;
           if (v.k != V_OBJ) throw NeedsRender{};  // nil pointer / field of a non-map
@@ -566,6 +658,7 @@ struct Ctx {
         Val v;
         for (const Expr& x : e.a) {
           v = eval(x, dot);
+          use(v);
           if ((e.k == E_OR) == truth(v)) return v;
         }
         return v;
@@ -573,16 +666,20 @@ struct Ctx {
       case E_NOT: {
         Val r;
         r.k = V_BOOL;
-        r.b = !truth(eval(e.a[0], dot));
+        const Val x = eval(e.a[0], dot);
+        use(x);
+        r.b = !truth(x);
         return r;
       }
       case E_EQ:
       case E_NE: {
         const Val a = eval(e.a[0], dot);
+        use(a);
         const int ka = basic(a);
         bool eq = false;
         for (size_t i = 1; i < e.a.size() && !eq; ++i) {
           const Val b = eval(e.a[i], dot);
+          use(b);
           const int kb = basic(b);
           if (ka != kb) {
             if (ka && kb) throw NeedsRender{};  // incompatible types for comparison
@@ -600,8 +697,21 @@ struct Ctx {
       }
       case E_INDEX: {
         Val x = eval(e.a[0], dot);
+        if (sk && x.taint == 1 && sk->in_ext == 0) {  // the status guard, or ineligible
+          const Val key = e.a.size() == 2 ? eval(e.a[1], dot) : Val{};
+          if (e.a.size() != 2 || key.taint || key.sent >= 0 || key.idx_of < 0 || x.path < 0 ||
+              sk->paths[(size_t)x.path].size() != 2 || sk->paths[(size_t)x.path][0] != "status")
+            throw Ineligible{"per-object data indexed"};
+          const std::pair<int, int> g{x.path, key.idx_of};
+          if (std::find(sk->guards.begin(), sk->guards.end(), g) == sk->guards.end()) sk->guards.push_back(g);
+          Val t;
+          t.taint = 1;
+          return t;
+        }
+        use(x);
         for (size_t i = 1; i < e.a.size(); ++i) {
           const Val key = eval(e.a[i], dot);
+          use(key);
           if (x.k == V_OBJ) {
             const JV* y = x.j->get(sprint(key));
             if (y) x = from_jv(y);
@@ -626,6 +736,7 @@ struct Ctx {
       }
       case E_LEN: {
         const Val v = eval(e.a[0], dot);
+        use(v);
         size_t n;
         if (v.k == V_ARR || v.k == V_OBJ) n = v.j->a.size();
         else if (v.k == V_STR) {
@@ -638,11 +749,17 @@ struct Ctx {
         r.own = std::to_string(n);
         return r;
       }
-      case E_QUOTE: return str_val(quote_text(eval(e.a[0], dot)));
+      case E_QUOTE: {
+        const Val v = eval(e.a[0], dot);
+        if (sk && v.sent >= 0) return v;  // Quote of a slot value: its text (slot values need no quoting)
+        use(v);
+        return str_val(quote_text(v));
+      }
       case E_NOW: {
         Val r;
         r.k = V_STR;
         r.sp = &now;
+        if (sk) r.sent = 0;
         return r;
       }
       case E_EXT: {
@@ -653,11 +770,30 @@ struct Ctx {
           r.sp = &f.value;
           return r;
         }
+        int site = -1;
+        if (sk && sk->in_ext == 0) {  // a call site: its value is a slot
+          if (std::find(sk->sites.begin(), sk->sites.end(), &e) != sk->sites.end())
+            throw Ineligible{"a call site evaluated twice"};
+          if ((int)sk->sites.size() >= kMaxSites) throw Ineligible{"too many call sites"};
+          site = (int)sk->sites.size();
+          sk->sites.push_back(&e);
+          if (!sk->calls) {  // the arguments are checked, the value is the slot
+            ++sk->in_ext;
+            for (const Expr& x : e.a) use(eval(x, dot));
+            --sk->in_ext;
+            Val r;
+            r.k = V_STR;
+            r.sent = (int8_t)(1 + site);
+            return r;
+          }
+        }
         if (!fn) throw NeedsRender{};
         std::vector<std::string> texts;
         std::vector<uint8_t> kinds;
+        if (site >= 0) ++sk->in_ext;
         for (const Expr& x : e.a) {
           const Val v = eval(x, dot);
+          use(v);
           kinds.push_back((uint8_t)v.k);
           if (v.k == V_ARR || v.k == V_OBJ) {
             std::string o;
@@ -682,6 +818,14 @@ struct Ctx {
                   (uint32_t)fbuf.size(), &len);
         }
         if (st != 0 || len > fbuf.size()) throw NeedsRender{};
+        if (site >= 0) {
+          --sk->in_ext;
+          sk->values.emplace_back(fbuf.data(), len);
+          Val r;
+          r.k = V_STR;
+          r.sent = (int8_t)(1 + site);
+          return r;
+        }
         return str_val(std::string(fbuf.data(), len));
       }
     }
@@ -695,6 +839,7 @@ struct Ctx {
   // range over a value (text/template walkRange): arrays by index, maps by sorted key
   template <class F>
   void range(const Val& it, int vi, int ve, F body) {
+    use(it);
     if (it.k == V_MISSING) return;
     if (it.k == V_ARR) {
       for (size_t i = 0; i < it.j->a.size(); ++i) {
@@ -703,6 +848,7 @@ struct Ctx {
           Val idx;
           idx.k = V_NUM;
           idx.own = std::to_string(i);
+          if (sk) idx.idx_of = it.path;
           vars[(size_t)vi] = idx;
         }
         if (ve >= 0) vars[(size_t)ve] = elem;
@@ -740,7 +886,13 @@ struct Ctx {
       if (p.k == P_TEXT) {
         acc += p.text;
       } else if (p.k == P_VAL) {
-        const std::string t = sprint(eval(T->exprs[(size_t)p.expr], dot));
+        const Val v = eval(T->exprs[(size_t)p.expr], dot);
+        if (sk && v.sent >= 0) {
+          sk->marker(acc, v.sent);
+          continue;
+        }
+        use(v);
+        const std::string t = sprint(v);
         for (char c : t)  // inside '...': printable ASCII without a quote stays as it is
           if (c < 0x20 || c > 0x7E || c == '\'') throw NeedsRender{};
         acc += t;
@@ -764,7 +916,9 @@ struct Ctx {
           items(it.items, elem, count);
         });
       } else {
-        if (truth(eval(T->exprs[(size_t)it.expr], dot))) items(it.items, dot, count);
+        const Val c = eval(T->exprs[(size_t)it.expr], dot);
+        use(c);
+        if (truth(c)) items(it.items, dot, count);
         else items(it.else_items, dot, count);
       }
     }
@@ -775,12 +929,25 @@ struct Ctx {
     switch (n.k) {
       case N_LIT: o += n.lit; return;
       case N_Q: {
-        const std::string s = quote_text(eval(T->exprs[(size_t)n.expr], dot));
+        const Val v = eval(T->exprs[(size_t)n.expr], dot);
+        if (sk && v.sent >= 0) {
+          o += '"';
+          sk->marker(o, v.sent);
+          o += '"';
+          return;
+        }
+        use(v);
+        const std::string s = quote_text(v);
         check_yaml_dq(s);
         go_string(o, s);
         return;
       }
-      case N_RAW: emit_plain(o, sprint(eval(T->exprs[(size_t)n.expr], dot))); return;
+      case N_RAW: {
+        const Val v = eval(T->exprs[(size_t)n.expr], dot);
+        use(v);
+        emit_plain(o, sprint(v));
+        return;
+      }
       case N_SQ: {
         std::string acc;
         sq(acc, n.pieces, dot);
@@ -790,7 +957,9 @@ struct Ctx {
       case N_MAP: {
         for (const Guard& g : n.guards) {
           if (g.parent < 0 || regs[(size_t)g.parent]) {
-            const bool t = truth(eval(T->exprs[(size_t)g.expr], dot));
+            const Val gv = eval(T->exprs[(size_t)g.expr], dot);
+            use(gv);
+            const bool t = truth(gv);
             regs[(size_t)g.then_reg] = t;
             regs[(size_t)g.else_reg] = !t;
           } else {
@@ -825,22 +994,30 @@ struct Ctx {
     if (!ps.value(obj)) return false;
     ps.ws();
     if (ps.p != ps.e) return false;
-    T = &t;
-    root = &obj;
-    vars.assign((size_t)t.n_vars, Val{});
-    regs.assign((size_t)t.n_regs, 0);
     const size_t mark = out->size();
     try {
-      Val dot = from_jv(root);
-      out->append(t.head);
-      run_sets(t.prologue, dot);
-      node(t.body, dot);
-      out->append(t.tail);
+      body(t, obj);
     } catch (const NeedsRender&) {
       out->resize(mark);
       return false;
     }
     return true;
+  }
+
+  void body(const Template& t, const JV& obj) {
+    T = &t;
+    root = &obj;
+    vars.assign((size_t)t.n_vars, Val{});
+    regs.assign((size_t)t.n_regs, 0);
+    Val dot = from_jv(root);
+    if (sk) {
+      dot.path = 0;
+      dot.taint = 2;
+    }
+    out->append(t.head);
+    run_sets(t.prologue, dot);
+    node(t.body, dot);
+    out->append(t.tail);
   }
 };
 
@@ -1003,6 +1180,160 @@ kwk_status kwk_patch_render(kwk_patcher* p, uint32_t n, const uint16_t* template
   }
   out_offsets[n] = off;
   *out_data = p->out.data();
+  return KWK_OK;
+}
+
+// ------------------------------------------------------------------ skeletons (device emission)
+namespace {
+
+// JSON string of arbitrary bytes the renderer produced (valid UTF-8)
+void json_str(std::string& o, const std::string& s) {
+  try {
+    go_string(o, s);
+  } catch (const NeedsRender&) {
+    o += "\"\"";
+  }
+}
+
+// split a skeleton text at its slot markers: literal runs and slot ids
+bool split_skeleton(const std::string& t, uint32_t markers, std::vector<std::string>& lits, std::vector<int>& slots) {
+  lits.assign(1, std::string());
+  slots.clear();
+  size_t i = 0;
+  while (i < t.size()) {
+    if (t.compare(i, kMarkerLen, kMarker) == 0) {
+      if (i + 2 * kMarkerLen + 1 > t.size() || t.compare(i + kMarkerLen + 1, kMarkerLen, kMarker) != 0) return false;
+      const int id = t[i + kMarkerLen] - 'A';
+      if (id < 0 || id > kMaxSites) return false;
+      slots.push_back(id);
+      lits.emplace_back();
+      i += 2 * kMarkerLen + 1;
+      continue;
+    }
+    lits.back() += t[i++];
+  }
+  return slots.size() == markers;
+}
+
+}  // namespace
+
+kwk_status kwk_patch_skeleton(kwk_patcher* p, uint32_t tid, const char* obj, uint64_t len, const char** out_json,
+                              uint64_t* out_len) {
+  ErrScope es_(p ? &p->err : nullptr);
+  if (!p || !obj || !out_json || !out_len) return fail(KWK_EINVAL, "null argument");
+  if (tid >= p->templates.size()) return fail(KWK_EINVAL, "template id out of range");
+  JV o;
+  Parser ps{obj, obj + len};
+  if (!ps.value(o)) return fail(KWK_EINVAL, "object is not JSON");
+  Skel sk;
+  Ctx c(*p);
+  c.sk = &sk;
+  std::string text;
+  c.out = &text;
+  std::string& r = p->skel;
+  r.clear();
+  const char* why = nullptr;
+  try {
+    c.body(p->templates[tid], o);
+  } catch (const Ineligible& x) {
+    why = x.why;
+  } catch (const NeedsRender&) {
+    why = "the template does not render natively for this class";
+  }
+  std::vector<std::string> lits;
+  std::vector<int> slots;
+  if (!why && !split_skeleton(text, sk.markers, lits, slots)) why = "the object holds the slot marker";
+  if (why) {
+    r = "{\"eligible\":false,\"reason\":";
+    json_str(r, why);
+    r += "}";
+  } else {
+    r = "{\"eligible\":true,\"text\":";
+    json_str(r, text);
+    r += ",\"lits\":[";
+    for (size_t i = 0; i < lits.size(); ++i) {
+      if (i) r += ',';
+      json_str(r, lits[i]);
+    }
+    r += "],\"slots\":[";
+    for (size_t i = 0; i < slots.size(); ++i) r += (i ? "," : "") + std::to_string(slots[i]);
+    r += "],\"calls\":" + std::to_string(sk.sites.size()) + ",\"guards\":[";
+    for (size_t g = 0; g < sk.guards.size(); ++g) {
+      r += g ? ",[" : "[";
+      for (int side = 0; side < 2; ++side) {
+        const std::vector<std::string>& path = sk.paths[(size_t)(side ? sk.guards[g].second : sk.guards[g].first)];
+        r += side ? ",[" : "[";
+        for (size_t k = 0; k < path.size(); ++k) {
+          if (k) r += ',';
+          json_str(r, path[k]);
+        }
+        r += ']';
+      }
+      r += ']';
+    }
+    r += "]}";
+  }
+  *out_json = r.data();
+  *out_len = r.size();
+  return KWK_OK;
+}
+
+kwk_status kwk_patch_object_values(kwk_patcher* p, uint32_t tid, uint32_t n, const char* objs, const uint64_t* obj_offsets,
+                                   const char* skeleton, uint64_t skeleton_len, kwk_patch_fn fn, void* user,
+                                   uint32_t n_threads, uint32_t n_calls, uint32_t stride, uint8_t* values, uint8_t* ok) {
+  ErrScope es_(p ? &p->err : nullptr);
+  if (!p || (n && (!objs || !obj_offsets || !ok || !skeleton || (n_calls && !values)))) return fail(KWK_EINVAL, "null argument");
+  if (tid >= p->templates.size()) return fail(KWK_EINVAL, "template id out of range");
+  if (n_calls && (stride < 2 || stride > 256)) return fail(KWK_EINVAL, "stride must be 2..256");
+  for (uint32_t i = 0; i < n; ++i)
+    if (obj_offsets[i + 1] < obj_offsets[i]) return fail(KWK_EINVAL, "object offsets not ascending");
+  const std::string want(skeleton, skeleton_len);
+  const uint32_t nt = std::max(1u, std::min(n_threads, std::max(1u, n / 64)));
+  auto work = [&](uint32_t t) {
+    const uint32_t lo = (uint32_t)((uint64_t)n * t / nt), hi = (uint32_t)((uint64_t)n * (t + 1) / nt);
+    Ctx c(*p);
+    c.fn = fn;
+    c.user = user;
+    std::string text;
+    c.out = &text;
+    for (uint32_t i = lo; i < hi; ++i) {
+      uint8_t* v = values ? values + (uint64_t)i * n_calls * stride : nullptr;
+      for (uint32_t k = 0; k < n_calls; ++k) v[(uint64_t)k * stride] = 0xFF;
+      ok[i] = 0;
+      JV o;
+      Parser ps{objs + obj_offsets[i], objs + obj_offsets[i + 1]};
+      if (!ps.value(o)) continue;
+      Skel sk;
+      sk.calls = true;
+      c.sk = &sk;
+      text.clear();
+      try {
+        c.body(p->templates[tid], o);
+      } catch (const Ineligible&) {
+        continue;
+      } catch (const NeedsRender&) {
+        continue;
+      }
+      if (text != want || sk.values.size() != n_calls) continue;
+      bool good = true;
+      for (uint32_t k = 0; k < n_calls; ++k) {
+        const std::string& x = sk.values[k];
+        bool safe = x.size() + 1 <= stride;
+        for (char ch : x) safe = safe && safe_value_char((unsigned char)ch);
+        if (!safe) { good = false; continue; }
+        v[(uint64_t)k * stride] = (uint8_t)x.size();
+        memcpy(v + (uint64_t)k * stride + 1, x.data(), x.size());
+      }
+      ok[i] = good ? 1 : 0;
+    }
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
   return KWK_OK;
 }
 

@@ -45,6 +45,7 @@ class KindController:
         self.native_renders = 0   # patches rendered by kwk_patch_render
         self.host_renders = 0     # patches the native renderer handed back (NEEDS_RENDER / unsupported)
         self.last_rows = {}       # slot -> kwk_encode row of every object the last step fired (native)
+        self.last_patches = {}    # (slot, patch index) -> the patch bytes the last step applied (native)
         if native:
             from .encoder import NativeIngest
             from .patchtpl import PatchProgram
@@ -98,6 +99,7 @@ class KindController:
                 self.host_renders += 1
             else:
                 self.native_renders += 1
+        self.last_patches = {(items[k][0], pi): b for (k, pi), b in out_bytes.items()}
         result = []
         for k, (i, s, obj, changed) in enumerate(items):
             st = self.p.stages[s]
@@ -118,6 +120,12 @@ class KindController:
         the DELTA_UNKNOWN ones re-encoded and written back (kwk_replace)."""
         self.eng.step(now_ns, seed, step)
         fired = self.eng.fired()
+        self.handle(fired, now_ns)
+        return fired
+
+    def handle(self, fired, now_ns: int):
+        """The hand-back of one step's fired list (kwk_fired records): patches applied to the
+        cache, the DELTA_UNKNOWN rows written back."""
         slots, rows = [], []
         if self.native:
             applied = self._apply_native(fired, now_ns)
@@ -168,4 +176,3 @@ class KindController:
                 self.eng.set_records(self.ing.record_array())
             self.eng.replace(np.asarray(slots, dtype=np.uint32), hot, dels, recs, cls)
             self.round_trips += n
-        return fired

@@ -533,7 +533,13 @@ def lib():
         L.kwk_patcher_destroy.argtypes = [C.c_void_p]
         L.kwk_patch_render.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int64, _FN,
                                        C.c_void_p, C.c_uint32, C.POINTER(C.c_char_p), C.c_void_p, C.c_void_p]
-        for n in ("kwk_patcher_create", "kwk_patcher_destroy", "kwk_patch_render"):
+        L.kwk_patch_skeleton.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_uint64)]
+        L.kwk_patch_object_values.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_char_p, C.c_void_p, C.c_char_p,
+                                              C.c_uint64, _FN, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                              C.c_void_p]
+        for n in ("kwk_patcher_create", "kwk_patcher_destroy", "kwk_patch_render", "kwk_patch_skeleton",
+                  "kwk_patch_object_values"):
             getattr(L, n).restype = C.c_int32
         _lib = L
     return _lib
@@ -655,3 +661,25 @@ class PatchProgram:
         buf, offs = pack_json(objs)
         out, o, st = self.render_buffer(np.asarray(template_ids), buf, offs, now_ns)
         return [out[int(o[i]):int(o[i + 1])] if st[i] == STATUS_OK else None for i in range(len(objs))]
+
+    def skeleton(self, tid: int, obj) -> dict:
+        """kwk_patch_skeleton: the template's skeleton over obj's class (see kwok_patch.h)."""
+        b = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj, separators=(",", ":")).encode()
+        data, n = C.c_void_p(), C.c_uint64()
+        _check(lib().kwk_patch_skeleton(self.h, int(tid), bytes(b), len(b), C.byref(data), C.byref(n)),
+               "kwk_patch_skeleton", self.h)
+        return json.loads(C.string_at(data, n.value).decode())
+
+    def object_values(self, tid: int, objs: Sequence, skeleton_text: str, n_calls: int, stride: int):
+        """kwk_patch_object_values -> (values uint8 [n, n_calls, stride], ok uint8 [n])."""
+        from .encoder import pack_json
+        buf, offs = pack_json(objs) if not isinstance(objs, tuple) else objs
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        n = len(offs) - 1
+        vals = np.zeros((n, max(n_calls, 0), stride), dtype=np.uint8)
+        ok = np.zeros(n, dtype=np.uint8)
+        sk = skeleton_text.encode()
+        _check(lib().kwk_patch_object_values(self.h, int(tid), n, buf, abi.ptr(offs), sk, len(sk), self._fn, None,
+                                             self.n_threads, n_calls, stride, abi.ptr(vals) if n_calls else None,
+                                             abi.ptr(ok)), "kwk_patch_object_values", self.h)
+        return vals, ok

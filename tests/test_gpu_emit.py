@@ -1,0 +1,109 @@
+"""Device patch emission on the GPU (include/kwok_emit.h): the native controller loop of
+tests/test_controller_native.py with libkwok_emit beside it.  Every step, kwk_emit expands the
+engine's fired list (kwk_fired records on even steps, 4-byte packed records on odd ones) on the
+device; each item it emits equals, byte for byte, the patch the controller rendered for that
+object with kwk_patch_render (itself checked against the oracle's next state there), and each
+item it leaves to the host is one the skeleton cannot stand for (status guard not met, template
+ineligible for the class).  After the host's hand-back, the guard bits the device carried equal
+the guards evaluated on the host's objects.
+
+Reference: pkg/kwok/controllers/pod_controller.go:290-360 (playStage), pkg/utils/lifecycle/
+next.go:73-160, pkg/utils/gotpl/renderer.go:59-124."""
+import collections
+
+import numpy as np
+import pytest
+
+from kwok_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cl, steps, dt_ns, seed):
+    from kwok_amd.host import emit
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.controller import KindController
+    from kwok_amd.host.encoder import NativeIngest
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    from tests.parity_util import NOW0
+    from tests.test_patch import FUNCS
+    objs = cl.pods.materialize()
+    prog = KindProgram(load_stage_files(*cl.pod_stage_files))
+    prog.explore(objs)
+    nat = NativeIngest(prog)
+    hot, dels, rec, cls = nat.columns(objs)
+    eng = Engine(prog, capacity=len(objs), max_records=len(nat.record_array()) + 64)
+    ctl = KindController(prog, eng, Ingest(prog), objs, funcs=FUNCS, native=True)
+    classes = [prog.class_of(o, register=False) for o in ctl.objs]
+    reps = {}
+    for o, c in zip(ctl.objs, classes):
+        reps.setdefault(c, o)
+    ep = emit.EmitProgram(prog.stages, ctl.patcher, reps, len(prog.class_ids))
+    em = emit.Emitter(eng, len(objs), ep)
+    counts = collections.Counter()
+    try:
+        words, cols = ep.rows(ctl.objs, classes)
+        em.set_rows(0, words, cols)
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, nat.record_array())
+        for k in range(steps):
+            now = NOW0 + k * dt_ns
+            packed = k % 2 == 1
+            eng.step(now, seed, k)
+            if packed:
+                eng.fired_compact(packed=True)
+            items, offs, out = em.run(now, packed=packed)
+            fired = eng.fired()
+            pre = {int(r["slot"]): ctl.objs[int(r["slot"])] for r in fired}
+            ctl.handle(fired, now)
+            # the items: every patch of every fired stage, in list order
+            want_items = [(j, t) for j, r in enumerate(fired) for t in ep.stage_tpl[int(r["stage"])]]
+            assert [(int(i["rec"]), int(i["tid"])) for i in items] == want_items, f"step {k}"
+            host_slots = set()
+            pos = collections.Counter()
+            for n, it in enumerate(items):
+                r = fired[int(it["rec"])]
+                slot, stage = int(r["slot"]), int(r["stage"])
+                pi = pos[int(it["rec"])]
+                pos[int(it["rec"])] += 1
+                c = classes[slot]
+                if int(it["status"]) == emit.STATUS_OK:
+                    got = out[int(offs[n]):int(offs[n + 1])]
+                    assert got == ctl.last_patches[(slot, pi)], (k, slot, prog.stages[stage].name)
+                    counts["device"] += 1
+                    continue
+                host_slots.add(slot)
+                sk = ep.skel.get((c, int(it["tid"])))
+                if sk is not None:  # eligible: the object's guard was not met before this fire
+                    assert not all(emit.guard_holds(pre[slot], g) for g in sk["guard_list"]), (k, slot)
+                    counts["guard"] += 1
+                else:
+                    counts["host"] += 1
+            # the host sets the words of the objects it rendered (or deleted) itself
+            live = [s for s in host_slots if ctl.objs[s] is not None]
+            if live:
+                w, cc = ep.rows([ctl.objs[s] for s in live], [classes[s] for s in live])
+                em.set_slots(np.asarray(live), w, cc)
+            dev = em.words(0, len(objs))
+            for s, o in enumerate(ctl.objs):
+                if o is not None:
+                    assert (int(dev[s]) >> 16) & 0xFF == ep.guard_bits(o), (k, s)
+        return counts
+    finally:
+        em.close()
+        ctl.close()
+        nat.close()
+        eng.close()
+
+
+def test_gpu_emit_c2_pod_general_equals_native_render():
+    cl = W.make_cluster("C2", 30, 400, seed=91)
+    c = _run(cl, steps=30, dt_ns=500 * 10**6, seed=0x91)
+    assert c["device"] >= 400, c
+
+
+def test_gpu_emit_c1_pod_fast_equals_native_render():
+    cl = W.make_cluster("C1", 20, 300, seed=92)
+    c = _run(cl, steps=8, dt_ns=10**9, seed=0x92)
+    assert c["device"] >= 300 and c["host"] == 0, c

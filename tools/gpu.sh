@@ -84,6 +84,16 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
         > $O/shard_prof.json 2> $O/shard_prof.err || { tail -30 $O/shard_prof.err; exit 1; }
       cd $R && python tools/rocpd_summary.py stats $(find $O/shard_prof -name '*.db' | head -1) $O/shard_kernel_stats.csv \
         && cut -c1-150 $O/shard_kernel_stats.csv | head -14 ;;
+    shardtune)  # the 125k-node shard under pod-sweep grid / hand-back tunings: "<label>:<bench args>;..."
+      S="--nodes 125000 --no-cpu-baseline --no-pmc --hbm-nodes 0 --pcie-steps 0 --steps 40 --warmup 5"
+      IFS=';' read -ra V <<< "${arg:-base:}"
+      for i in 1 2; do
+        for v in "${V[@]}"; do
+          l=${v%%:*}; x=${v#*:}
+          timeout -k 10 200 python -u bench.py $S $x > $O/st_${l}_$i.json 2> $O/st_${l}_$i.err || { tail -20 $O/st_${l}_$i.err; exit 1; }
+          python -c "import json; d=json.load(open('$O/st_${l}_$i.json')); print('$l', $i, d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'])"
+        done
+      done ;;
     dist)
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 \
         bench.py --gpus 2 --steps 6 --warmup 2 --nodes 200000 --dist-backend gloo --no-cpu-baseline --no-pmc --hbm-nodes 0 \
