@@ -169,8 +169,9 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
               handback="packed"):
     """Steps k0..k1-1; ev_base (0): record HIP events (pod stream) around the pod sweep of every
     EV_EVERY-th step (events 2i, 2i+1 of sample i).  Each engine's steps up to the next
-    reporting point are enqueued by one native call (kwk_step_n: sweep + device compaction per
-    step, the same work as the per-step calls); the pinned-copy run keeps one call per step."""
+    reporting point are enqueued by one native call (kwk_step_n_pair: per step the pod sweep + device
+    compaction, then the node engine's, the same work as the per-step calls); the pinned-copy run
+    keeps one call per step."""
     assert ev_base in (None, 0)
     if pinned is None:
         last, k = None, k0
@@ -180,8 +181,9 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
             if reporter is not None and report_every:
                 end = min(k1, k0 + (j // report_every + 1) * report_every)
             now = NOW0 + k * dt
-            pods.step_n(end - k, now, dt, seed, k, HANDBACK[handback], EV_EVERY if ev_base is not None else 0, j)
-            nodes.step_n(end - k, now, dt, seed, k, HANDBACK[handback])
+            # pods and nodes enqueued step by step in turn (kwk_step_n_pair): the node stream starts
+            # with the pod stream instead of after the host has enqueued every pod step
+            pods.step_n_pair(nodes, end - k, now, dt, seed, k, HANDBACK[handback], EV_EVERY if ev_base is not None else 0, j)
             k = end
             if reporter is not None and report_every and (k - k0) % report_every == 0:
                 last = reporter.collect(NOW0 + (k - 1) * dt)
@@ -570,6 +572,8 @@ def main():
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
     ap.add_argument("--tune-sweep-blocks", type=int, default=0,
                     help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
+    ap.add_argument("--tune-compact-lb", type=int, default=-1,
+                    help="diagnostic: KWK_TUNE_COMPACT_LB for both engines (1: one-pass look-back, the default)")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
@@ -652,6 +656,10 @@ def main():
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
+    if args.tune_compact_lb >= 0:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_COMPACT_LB, args.tune_compact_lb)
+        nodes.set_tuning(abi.TUNE_COMPACT_LB, args.tune_compact_lb)
     if args.tune_compact_small >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_COMPACT_SMALL, args.tune_compact_small)

@@ -224,6 +224,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
+#define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1 (default),
+                                  or 0 (the scan + expansion pair / the one-launch small compaction above) */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */
@@ -297,6 +299,11 @@ kwk_status kwk_fired_compact(kwk_engine* eng);
  * index j = ev_j0 + k is a multiple of ev_every (i = j / ev_every). */
 kwk_status kwk_step_n(kwk_engine* eng, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0);
+/* kwk_step_n over two engines of one shard (the pod and node kinds), enqueued step by step in turn —
+ * eng's sweep (+ events) and hand-back, then other's — so that neither stream waits for the host
+ * to finish enqueuing the other's n steps; events go on eng's stream only.  Messages: eng's handle. */
+kwk_status kwk_step_n_pair(kwk_engine* eng, kwk_engine* other, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed,
+                           uint64_t step0, uint32_t compact, uint32_t ev_every, uint32_t ev_j0);
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
 /* device pointers of the compacted list and of its u32 count (valid until the next kwk_step) */
 kwk_status kwk_fired_device(kwk_engine* eng, const kwk_fired_rec** recs, const uint32_t** count);

@@ -47,6 +47,7 @@ constexpr uint32_t kBlock = 256, kPer = 4, kTile = kBlock * kPer;  // records pe
 constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
 constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
 constexpr uint32_t kScanBlock = 1024;
+constexpr uint32_t kStageBytes = 6144;  // per-wave LDS window of the staged byte writes
 
 struct Prog {
   const uint32_t* stage_tpl_ptr;
@@ -149,6 +150,46 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Rec& x, uint64
   return s;
 }
 
+// the bytes of a record's emitted items: put(global position, byte) for each, 64 lanes per run;
+// returns the position after them
+template <typename Put>
+__device__ __forceinline__ unsigned long long put_record(const EmitArgs& a, uint32_t stage, uint32_t ok, uint32_t slot,
+                                                         uint32_t cls, unsigned long long p, uint32_t lane,
+                                                         const char* s_now, Put put) {
+  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
+  for (uint32_t j = t0; j < t1; ++j) {
+    if (!((ok >> (j - t0)) & 1u)) continue;
+    const kwk_emit_skel S = a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]];
+    for (uint32_t q = 0; q < S.n_pieces; ++q) {
+      const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
+      const char* src = a.p.lits + P.lit_off;
+      for (uint32_t o = lane; o < P.lit_len; o += 64u) put(p + o, src[o]);
+      p += P.lit_len;
+      if (P.slot == 0) {
+        if (lane < a.now_len) put(p + lane, s_now[lane]);
+        p += a.now_len;
+      } else if (P.slot != KWK_EMIT_NO_SLOT) {
+        const uint32_t c = P.slot - 1u;
+        const uint8_t* v = a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
+        const uint32_t len = v[0];
+        for (uint32_t o = lane; o < len; o += 64u) put(p + o, (char)v[1 + o]);
+        p += len;
+      }
+    }
+  }
+  return p;
+}
+
+__device__ __forceinline__ unsigned long long rec_bytes(const EmitArgs& a, uint32_t stage, uint32_t ok, uint32_t slot,
+                                                        uint32_t cls) {
+  unsigned long long b = 0;
+  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
+  for (uint32_t j = t0; j < t1; ++j)
+    if ((ok >> (j - t0)) & 1u)
+      b += (unsigned long long)skel_bytes(a, a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]], slot);
+  return b;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -245,7 +286,9 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
+template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
+  __shared__ __attribute__((aligned(16))) char s_buf[kStaged ? kWaves * kStageBytes : 16];
   __shared__ uint32_t s_slot[kTile];
   __shared__ uint32_t s_meta[kTile];  // ok mask [15:0] | stage [23:16] | class in s_cls
   __shared__ uint32_t s_cls[kTile];
@@ -324,35 +367,58 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       }
     }
     __syncthreads();
-    // bytes: wave `wave` writes records [wave * 256, wave * 256 + 256) of the tile, 64 lanes per run
-    for (uint32_t lr = wave * kWaveRecs; lr < (wave + 1) * kWaveRecs; ++lr) {
-      const uint32_t meta = s_meta[lr];
-      const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
-      if (stage >= a.p.n_stages || !ok) continue;
-      const uint32_t slot = s_slot[lr], cls = s_cls[lr];
-      unsigned long long p = s_base[lr];
-      const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
-      for (uint32_t j = t0; j < t1; ++j) {
-        if (!((ok >> (j - t0)) & 1u)) continue;
-        const int sk = a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]];
-        const kwk_emit_skel S = a.p.skels[sk];
-        for (uint32_t q = 0; q < S.n_pieces; ++q) {
-          const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
-          const char* src = a.p.lits + P.lit_off;
-          for (uint32_t o = lane; o < P.lit_len; o += 64u) a.out[p + o] = src[o];
-          p += P.lit_len;
-          if (P.slot == 0) {
-            if (lane < a.now_len) a.out[p + lane] = s_now[lane];
-            p += a.now_len;
-          } else if (P.slot != KWK_EMIT_NO_SLOT) {
-            const uint32_t c = P.slot - 1u;
-            const uint8_t* v = a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
-            const uint32_t len = v[0];
-            for (uint32_t o = lane; o < len; o += 64u) a.out[p + o] = (char)v[1 + o];
-            p += len;
+    // bytes: wave `wave` writes records [wave * 256, wave * 256 + 256) of the tile, whose output
+    // is one contiguous span, 64 lanes per literal run / value
+    const uint32_t r0 = wave * kWaveRecs, r1 = r0 + kWaveRecs;
+    if constexpr (!kStaged) {
+      for (uint32_t lr = r0; lr < r1; ++lr) {
+        const uint32_t meta = s_meta[lr];
+        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
+        if (stage >= a.p.n_stages || !ok) continue;
+        put_record(a, stage, ok, s_slot[lr], s_cls[lr], s_base[lr], lane, s_now,
+                   [&](unsigned long long g, char c) { a.out[g] = c; });
+      }
+    } else {
+      // staged: the span goes through a per-wave LDS window [w0, w0 + kStageBytes) (w0 16-byte
+      // aligned) and leaves as 16-byte stores; only the span's two edges take byte stores
+      char* buf = s_buf + wave * kStageBytes;
+      unsigned long long w0 = s_base[r0] & ~15ull, lo = s_base[r0], hi = lo;
+      auto flush = [&](unsigned long long f_lo, unsigned long long f_hi) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (unsigned long long A = (f_lo & ~15ull) + lane * 16ull; A < f_hi; A += 1024ull) {
+          const uint32_t li = (uint32_t)(A - w0);
+          if (A >= f_lo && A + 16u <= f_hi) {
+            *reinterpret_cast<uint4*>(a.out + A) = *reinterpret_cast<const uint4*>(buf + li);
+          } else {
+            for (uint32_t b = 0; b < 16u; ++b)
+              if (A + b >= f_lo && A + b < f_hi) a.out[A + b] = buf[li + b];
           }
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      };
+      for (uint32_t lr = r0; lr < r1; ++lr) {
+        const uint32_t meta = s_meta[lr];
+        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
+        if (stage >= a.p.n_stages || !ok) continue;
+        const uint32_t slot = s_slot[lr], cls = s_cls[lr];
+        const unsigned long long p = s_base[lr];
+        const unsigned long long end = p + rec_bytes(a, stage, ok, slot, cls);
+        if (end - w0 > kStageBytes) {  // the window is full: out with everything before this record
+          flush(lo, p);  // (the chunk holding p is finished by byte stores from both sides)
+          w0 = p & ~15ull;
+          lo = p;
+          if (end - w0 > kStageBytes) {  // larger than the window: straight to global memory
+            put_record(a, stage, ok, slot, cls, p, lane, s_now, [&](unsigned long long g, char c) { a.out[g] = c; });
+            lo = hi = end;
+            w0 = end & ~15ull;
+            continue;
+          }
+        }
+        put_record(a, stage, ok, slot, cls, p, lane, s_now,
+                   [&](unsigned long long g, char c) { buf[(uint32_t)(g - w0)] = c; });
+        hi = end;
       }
+      if (hi > lo) flush(lo, hi);
     }
     __syncthreads();
   }
@@ -590,10 +656,11 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   if (!em) return fail(KWK_EINVAL, "null emitter");
   EmitArgs a{};
   a.p = em->p;
-  if (source == KWK_EMIT_FROM_RECORDS) {
+  const uint32_t from = source & 0xFFu;
+  if (from == KWK_EMIT_FROM_RECORDS) {
     if (kwk_fired_device(em->eng, &a.recs, &a.count) != KWK_OK)
       return fail(KWK_ESTATE, std::string("kwk_fired_device: ") + kwk_last_error(em->eng));
-  } else if (source == KWK_EMIT_FROM_PACKED) {
+  } else if (from == KWK_EMIT_FROM_PACKED) {
     if (kwk_fired_packed_device(em->eng, &a.packed, &a.count) != KWK_OK)
       return fail(KWK_ESTATE, std::string("kwk_fired_packed_device: ") + kwk_last_error(em->eng));
   } else {
@@ -623,7 +690,10 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(emit_write_kernel, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  if (source & KWK_EMIT_BYTE_STORES)
+    hipLaunchKernelGGL(emit_write_kernel<false>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  else
+    hipLaunchKernelGGL(emit_write_kernel<true>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(em->ev1, em->stream));
   em->emitted = true;

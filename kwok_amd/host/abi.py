@@ -97,6 +97,7 @@ TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_USAGE_BLOCKS, TUNE_FSM_KERNEL, TUNE_USA
 TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
+TUNE_COMPACT_LB = 11
 
 
 class Lease(C.Structure):
@@ -162,7 +163,7 @@ assert HOT_DTYPE.itemsize == 16 and VALUE_DTYPE.itemsize == 16 and FIRED_DTYPE.i
 EXPORTS = [
     "kwk_last_error", "kwk_engine_create", "kwk_engine_destroy", "kwk_load_stages", "kwk_set_harness", "kwk_load",
     "kwk_upsert", "kwk_set_records", "kwk_delete", "kwk_step", "kwk_match", "kwk_fired", "kwk_stats", "kwk_read", "kwk_sync",
-    "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed", "kwk_stream", "kwk_step_n",
+    "kwk_usage_config", "kwk_usage", "kwk_usage_read", "kwk_device_ptrs", "kwk_event_record", "kwk_event_elapsed", "kwk_stream", "kwk_step_n", "kwk_step_n_pair",
     "kwk_abi_version", "kwk_tile_objects", "kwk_count", "kwk_lease_config", "kwk_lease_set", "kwk_lease_step",
     "kwk_lease_ops", "kwk_lease_read", "kwk_lease_stats", "kwk_lease_sync_pods", "kwk_usage_pods",
     "kwk_usage_read_pods", "kwk_retry", "kwk_lease_fail", "kwk_set_tuning", "kwk_fired_compact", "kwk_fired_device",
@@ -224,6 +225,8 @@ def lib():
     L.kwk_fired_compact.argtypes = [C.c_void_p]
     L.kwk_step_n.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                              C.c_uint32]
+    L.kwk_step_n_pair.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, C.c_uint64,
+                                  C.c_uint32, C.c_uint32, C.c_uint32]
     L.kwk_fired_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_fired_compact_packed.argtypes = [C.c_void_p]
     L.kwk_fired_packed.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]

@@ -244,6 +244,13 @@ class Engine:
         c = abi.COMPACT_PACKED if compact == "packed" else (1 if compact else 0)
         self._check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, c, ev_every, ev_j0), "kwk_step_n")
 
+    def step_n_pair(self, other: "Engine", n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact=True,
+                    ev_every: int = 0, ev_j0: int = 0):
+        """kwk_step_n_pair: this engine's and `other`'s steps enqueued in turn, step by step."""
+        c = abi.COMPACT_PACKED if compact == "packed" else (1 if compact else 0)
+        self._check(abi.lib().kwk_step_n_pair(self.h, other.h, n, now0_ns, dt_ns, seed, step0, c, ev_every, ev_j0),
+                    "kwk_step_n_pair")
+
     def fired_compact(self, packed: bool = False):
         """kwk_fired_compact (/ _packed): the last step's fired list compacted on the device (enqueue only)."""
         if packed:

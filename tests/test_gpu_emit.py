@@ -1,7 +1,7 @@
 """Device patch emission on the GPU (include/kwok_emit.h): the native controller loop of
 tests/test_controller_native.py with libkwok_emit beside it.  Every step, kwk_emit expands the
-engine's fired list (kwk_fired records on even steps, 4-byte packed records on odd ones) on the
-device; each item it emits equals, byte for byte, the patch the controller rendered for that
+engine's fired list (kwk_fired records on even steps, 4-byte packed records on odd ones; the
+LDS-staged 16-byte writes, and every other pair of steps the byte-store path) on the device; each item it emits equals, byte for byte, the patch the controller rendered for that
 object with kwk_patch_render (itself checked against the oracle's next state there), and each
 item it leaves to the host is one the skeleton cannot stand for (status guard not met, template
 ineligible for the class).  After the host's hand-back, the guard bits the device carried equal
@@ -51,9 +51,8 @@ def _run(cl, steps, dt_ns, seed):
             now = NOW0 + k * dt_ns
             packed = k % 2 == 1
             eng.step(now, seed, k)
-            if packed:
-                eng.fired_compact(packed=True)
-            items, offs, out = em.run(now, packed=packed)
+            eng.fired_compact(packed=packed)
+            items, offs, out = em.run(now, packed=packed, byte_stores=k % 4 >= 2)
             fired = eng.fired()
             pre = {int(r["slot"]): ctl.objs[int(r["slot"])] for r in fired}
             ctl.handle(fired, now)

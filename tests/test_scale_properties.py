@@ -116,23 +116,32 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
             e.close()
 
 
-def test_handback_pair_equals_one_launch_at_4m_pods():
-    """The fired hand-back's two paths over the same step's segments: the one-launch compaction
-    (at most 8192 segments, the default here) and the scan + expansion pair the C5 sweep takes
-    (KWK_TUNE_COMPACT_SMALL 0) give the same dense list in the same order; every slot once."""
+HANDBACK_PATHS = ((1, 8192), (0, 8192), (0, 0))  # (KWK_TUNE_COMPACT_LB, KWK_TUNE_COMPACT_SMALL)
+
+
+def _handback_path(eng, path):
     from kwok_amd.host import abi
+    eng.set_tuning(abi.TUNE_COMPACT_LB, path[0])
+    eng.set_tuning(abi.TUNE_COMPACT_SMALL, path[1])
+
+
+def test_handback_pair_equals_one_launch_at_4m_pods():
+    """The fired hand-back's three paths over the same step's segments: the one-pass look-back
+    compaction (the default), the one-launch compaction that re-sums the counts (at most 8192
+    segments) and the scan + expansion pair (KWK_TUNE_COMPACT_LB 0, KWK_TUNE_COMPACT_SMALL 0)
+    give the same dense list in the same order; every slot once."""
     prog, eng = _pods("auto")
     try:
         now0 = 1_700_000_000 * 10**9
         for k in range(4):
             eng.step(now0 + k * 10**9, 0x6B776F6B, k)
-            eng.set_tuning(abi.TUNE_COMPACT_SMALL, 8192)
-            eng.fired_compact()
-            one = eng.fired()
-            eng.set_tuning(abi.TUNE_COMPACT_SMALL, 0)
-            eng.fired_compact()
-            pair = eng.fired()
-            assert len(one) > 0 and np.array_equal(one, pair), f"step {k}"
+            lists = []
+            for path in HANDBACK_PATHS:
+                _handback_path(eng, path)
+                eng.fired_compact()
+                lists.append(eng.fired())
+            one, pair = lists[0], lists[-1]
+            assert len(one) > 0 and all(np.array_equal(one, x) for x in lists[1:]), f"step {k}"
             sl = np.sort(pair["slot"].astype(np.int64))
             assert np.all(np.diff(sl) > 0), f"step {k}: a slot fired twice"
     finally:
@@ -143,7 +152,7 @@ def test_handback_pair_equals_one_launch_at_4m_pods():
 def test_packed_handback_equals_records_at_4m_pods(state):
     """The packed hand-back (kwk_fired_compact_packed / kwk_fired_packed: 4-byte records, stage in
     bits 31-27, slot in 26-0) over the same step's segments as the 8-byte list, through both
-    compaction paths (one launch at <= 8192 segments, the scan + expansion pair above): the same
+    compaction paths (look-back, one launch at <= 8192 segments, the scan + expansion pair above): the same
     (slot, stage) sequence; kwk_fired after a packed compaction re-expands the full records
     (flags included); kwk_step_n with KWK_COMPACT_PACKED leaves the same packed list as the
     per-step calls.  1-byte ids (sweep8), 2-byte words, fused 8-byte records (C2 mix)."""
@@ -171,14 +180,15 @@ def test_packed_handback_equals_records_at_4m_pods(state):
         now0 = 1_700_000_000 * 10**9
         for k in range(4):
             eng.step(now0 + k * dt, 0x6B776F6B, k)
-            for small in (8192, 0):
-                eng.set_tuning(abi.TUNE_COMPACT_SMALL, small)
+            for small in HANDBACK_PATHS:
+                _handback_path(eng, small)
                 eng.fired_compact(packed=True)
                 pk = eng.fired_packed()
                 full = eng.fired()  # re-expanded from the same segments
                 assert len(pk) == len(full) > 0, (k, small)
                 assert np.array_equal(pk & np.uint32(0x7FFFFFF), full["slot"]), (k, small)
                 assert np.array_equal(pk >> np.uint32(27), full["stage"].astype(np.uint32)), (k, small)
+        _handback_path(eng, HANDBACK_PATHS[0])
         ref = eng.fired_packed()
         eng.step_n(1, now0 + 4 * dt, dt, 0x6B776F6B, 4, "packed")
         a = eng.fired_packed()
