@@ -224,8 +224,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
-#define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1 (default),
-                                  or 0 (the scan + expansion pair / the one-launch small compaction above) */
+#define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1, or 0
+                                  (default: the scan + expansion pair / the one-launch small compaction above;
+                                  the look-back measured 73 us against 27 us at C5) */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */

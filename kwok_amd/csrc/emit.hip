@@ -7,10 +7,13 @@
 // values (funcPodIPWith / funcNodeIPWith, pod_controller.go:563-600) to fill per fire.
 //
 // Three launches per list, sized by the device-resident record count (no host round trip):
-//   emit_size_kernel   per 1024-record tile: items and bytes (a gather of one 8-byte word per record)
+//   emit_size_kernel   per 256-record tile (one per thread): items and bytes (a gather of one 8-byte
+//                      word per record)
 //   emit_scan_kernel   one workgroup: exclusive bases of the tiles, the totals
 //   emit_write_kernel  per tile again: each record's items / offsets, its guard word, then each wave
-//                      writes its 256 records' bytes, 64 lanes over every literal run and value
+//                      writes its 64 records' bytes (one contiguous span), 64 lanes over every literal
+//                      run and value, through an LDS window that leaves as 16-byte stores
+// The skeleton pieces and literal runs are staged in LDS when they fit (12 KiB of literals).
 // Roofline: HBM-bound on the patch bytes written (plus 8 bytes read per record and the literal
 // runs, L2-resident); the byte copy is 1-byte stores coalesced per wave.
 #include <hip/hip_runtime.h>
@@ -43,11 +46,13 @@ kwk_status fail(kwk_status code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(KWK_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-constexpr uint32_t kBlock = 256, kPer = 4, kTile = kBlock * kPer;  // records per tile
+constexpr uint32_t kBlock = 256, kTile = kBlock;  // records per tile: one per thread, 64 per wave
 constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
 constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
 constexpr uint32_t kScanBlock = 1024;
-constexpr uint32_t kStageBytes = 6144;  // per-wave LDS window of the staged byte writes
+constexpr uint32_t kStageBytes = 4096;  // per-wave LDS window of the staged writes
+constexpr uint32_t kLdsPieces = 512;    // skeleton tables staged in LDS when they fit
+constexpr uint32_t kLdsLits = 12288;
 
 struct Prog {
   const uint32_t* stage_tpl_ptr;
@@ -60,7 +65,8 @@ struct Prog {
   const uint8_t* fresh;
   uint8_t* const* cols;
   const uint32_t* stride;
-  uint32_t n_classes, n_templates, n_stages;
+  uint32_t n_classes, n_templates, n_stages, n_pieces;
+  uint32_t n_lits;
 };
 
 struct EmitArgs {
@@ -81,6 +87,30 @@ struct EmitArgs {
   uint32_t now_len;
   char now[40];
 };
+
+// the skeleton pieces and literal runs a kernel reads: LDS copies when the program's fit
+struct Tables {
+  const kwk_emit_piece* pieces;
+  const char* lits;
+};
+
+template <bool kLds>
+__device__ __forceinline__ Tables stage_tables(const EmitArgs& a, kwk_emit_piece* s_pieces, uint32_t* s_lits) {
+  if constexpr (kLds) {
+    for (uint32_t j = threadIdx.x; j < a.p.n_pieces; j += blockDim.x) s_pieces[j] = a.p.pieces[j];
+    const uint32_t nw = (a.p.n_lits + 3u) / 4u;
+    for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
+      uint32_t w = 0;
+      for (uint32_t b = 0; b < 4u; ++b)
+        if (4u * j + b < a.p.n_lits) w |= (uint32_t)(uint8_t)a.p.lits[4u * j + b] << (8u * b);
+      s_lits[j] = w;
+    }
+    __syncthreads();
+    return Tables{s_pieces, reinterpret_cast<const char*>(s_lits)};
+  } else {
+    return Tables{a.p.pieces, a.p.lits};
+  }
+}
 
 struct Rec {
   uint32_t slot, stage;
@@ -103,10 +133,11 @@ __device__ __forceinline__ Rec fetch(const EmitArgs& a, uint32_t r) {
 }
 
 // bytes of one skeleton for this slot, or -1 when a value is unusable
-__device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const kwk_emit_skel& S, uint32_t slot) {
+__device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S,
+                                                uint32_t slot) {
   long long b = 0;
   for (uint32_t q = 0; q < S.n_pieces; ++q) {
-    const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
+    const kwk_emit_piece P = T.pieces[S.first_piece + q];
     b += P.lit_len;
     if (P.slot == 0) {
       b += a.now_len;
@@ -134,7 +165,7 @@ struct Size {
   unsigned long long bytes;
 };
 
-__device__ __forceinline__ Size rec_size(const EmitArgs& a, const Rec& x, uint64_t w) {
+__device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, const Rec& x, uint64_t w) {
   Size s{0u, 0u, 0ull};
   if (x.stage >= a.p.n_stages) return s;
   const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
@@ -142,7 +173,7 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Rec& x, uint64
     ++s.items;
     const int k = x.valid ? skel_index(a, w, a.p.stage_tpl[j]) : -1;
     if (k < 0) continue;
-    const long long b = skel_bytes(a, a.p.skels[k], x.slot);
+    const long long b = skel_bytes(a, T, a.p.skels[k], x.slot);
     if (b < 0) continue;
     s.ok |= 1u << (j - t0);
     s.bytes += (unsigned long long)b;
@@ -150,44 +181,35 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Rec& x, uint64
   return s;
 }
 
-// the bytes of a record's emitted items: put(global position, byte) for each, 64 lanes per run;
-// returns the position after them
+// the bytes of a record's emitted items: put(global position, byte) for each, 64 lanes per run
+// (a value's length and bytes are loaded together)
 template <typename Put>
-__device__ __forceinline__ unsigned long long put_record(const EmitArgs& a, uint32_t stage, uint32_t ok, uint32_t slot,
-                                                         uint32_t cls, unsigned long long p, uint32_t lane,
-                                                         const char* s_now, Put put) {
+__device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, uint32_t stage, uint32_t ok,
+                                           uint32_t slot, uint32_t cls, unsigned long long p, uint32_t lane,
+                                           const char* s_now, Put put) {
   const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
   for (uint32_t j = t0; j < t1; ++j) {
     if (!((ok >> (j - t0)) & 1u)) continue;
     const kwk_emit_skel S = a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]];
     for (uint32_t q = 0; q < S.n_pieces; ++q) {
-      const kwk_emit_piece P = a.p.pieces[S.first_piece + q];
-      const char* src = a.p.lits + P.lit_off;
+      const kwk_emit_piece P = T.pieces[S.first_piece + q];
+      const char* src = T.lits + P.lit_off;
       for (uint32_t o = lane; o < P.lit_len; o += 64u) put(p + o, src[o]);
       p += P.lit_len;
       if (P.slot == 0) {
         if (lane < a.now_len) put(p + lane, s_now[lane]);
         p += a.now_len;
       } else if (P.slot != KWK_EMIT_NO_SLOT) {
-        const uint32_t c = P.slot - 1u;
-        const uint8_t* v = a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
+        const uint32_t c = P.slot - 1u, sd = a.p.stride[c];
+        const uint8_t* v = a.p.cols[c] + (uint64_t)slot * sd;
         const uint32_t len = v[0];
-        for (uint32_t o = lane; o < len; o += 64u) put(p + o, (char)v[1 + o]);
+        const char b0 = lane + 1u < sd ? (char)v[1 + lane] : 0;
+        if (lane < len) put(p + lane, b0);
+        for (uint32_t o = lane + 64u; o < len; o += 64u) put(p + o, (char)v[1 + o]);
         p += len;
       }
     }
   }
-  return p;
-}
-
-__device__ __forceinline__ unsigned long long rec_bytes(const EmitArgs& a, uint32_t stage, uint32_t ok, uint32_t slot,
-                                                        uint32_t cls) {
-  unsigned long long b = 0;
-  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
-  for (uint32_t j = t0; j < t1; ++j)
-    if ((ok >> (j - t0)) & 1u)
-      b += (unsigned long long)skel_bytes(a, a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]], slot);
-  return b;
 }
 
 template <typename T>
@@ -205,21 +227,24 @@ __device__ __forceinline__ T wave_incl(T v, uint32_t lane) {
   return v;
 }
 
+template <bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_size_kernel(EmitArgs a) {
+  __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
+  __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
   __shared__ uint32_t s_i[kWaves];
   __shared__ unsigned long long s_b[kWaves];
+  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
     uint32_t it = 0;
     unsigned long long by = 0;
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t r = t * kTile + threadIdx.x * kPer + k;
-      if (r >= n) break;
+    const uint32_t r = t * kTile + threadIdx.x;
+    if (r < n) {
       const Rec x = fetch(a, r);
-      const Size s = rec_size(a, x, x.valid ? a.words[x.slot] : 0ull);
-      it += s.items;
-      by += s.bytes;
+      const Size s = rec_size(a, T, x, x.valid ? a.words[x.slot] : 0ull);
+      it = s.items;
+      by = s.bytes;
     }
     it = wave_sum(it);
     by = wave_sum(by);
@@ -242,6 +267,8 @@ __global__ __launch_bounds__(kBlock) void emit_size_kernel(EmitArgs a) {
   }
 }
 
+// 8 consecutive tiles per thread: 8192 tiles per pass of the one workgroup
+constexpr uint32_t kScanPer = 8;
 __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   __shared__ uint32_t s_i[kScanBlock / 64];
   __shared__ unsigned long long s_b[kScanBlock / 64];
@@ -249,12 +276,21 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint32_t run_i = 0;
   unsigned long long run_b = 0;
-  for (uint32_t base = 0; base < n_tiles; base += kScanBlock) {
-    const uint32_t t = base + threadIdx.x;
-    const uint32_t vi = t < n_tiles ? a.tile_items[t] : 0u;
-    const unsigned long long vb = t < n_tiles ? a.tile_bytes[t] : 0ull;
-    const uint32_t ii = wave_incl(vi, lane);
-    const unsigned long long ib = wave_incl(vb, lane);
+  for (uint32_t base = 0; base < n_tiles; base += kScanBlock * kScanPer) {
+    const uint32_t t0 = base + threadIdx.x * kScanPer;
+    uint32_t vi[kScanPer];
+    unsigned long long vb[kScanPer];
+    uint32_t si = 0;
+    unsigned long long sb = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      vi[k] = t0 + k < n_tiles ? a.tile_items[t0 + k] : 0u;
+      vb[k] = t0 + k < n_tiles ? a.tile_bytes[t0 + k] : 0ull;
+      si += vi[k];
+      sb += vb[k];
+    }
+    const uint32_t ii = wave_incl(si, lane);
+    const unsigned long long ib = wave_incl(sb, lane);
     if (lane == 63) {
       s_i[wave] = ii;
       s_b[wave] = ib;
@@ -270,9 +306,16 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
       ti += s_i[w];
       tb += s_b[w];
     }
-    if (t < n_tiles) {
-      a.tile_items[t] = run_i + pi + ii - vi;
-      a.tile_bytes[t] = run_b + pb + ib - vb;
+    uint32_t ei = run_i + pi + ii - si;
+    unsigned long long eb = run_b + pb + ib - sb;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      if (t0 + k < n_tiles) {
+        a.tile_items[t0 + k] = ei;
+        a.tile_bytes[t0 + k] = eb;
+      }
+      ei += vi[k];
+      eb += vb[k];
     }
     run_i += ti;
     run_b += tb;
@@ -286,101 +329,94 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
-template <bool kStaged>
+template <bool kStaged, bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   __shared__ __attribute__((aligned(16))) char s_buf[kStaged ? kWaves * kStageBytes : 16];
+  __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
+  __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
   __shared__ uint32_t s_slot[kTile];
-  __shared__ uint32_t s_meta[kTile];  // ok mask [15:0] | stage [23:16] | class in s_cls
+  __shared__ uint32_t s_meta[kTile];  // ok mask [15:0] | stage [23:16]
   __shared__ uint32_t s_cls[kTile];
-  __shared__ unsigned long long s_base[kTile];
+  __shared__ unsigned long long s_base[kTile + 1];  // [r] = record r's first byte, [r + 1] its end
   __shared__ uint32_t s_wi[kWaves];
   __shared__ unsigned long long s_wb[kWaves];
   __shared__ char s_now[40];
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const unsigned long long tot_i = a.totals[0], tot_b = a.totals[1];
   if (tot_i > a.cap_items || tot_b > a.cap_bytes || a.totals[2]) return;  // KWK_ECAP: nothing is written
+  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
   if (blockIdx.x == 0 && threadIdx.x == 0) a.offsets[tot_i] = tot_b;
   if (threadIdx.x < 40) s_now[threadIdx.x] = a.now[threadIdx.x];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint32_t n_ok = 0;
   for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-    Rec x[kPer];
-    uint64_t w[kPer];
-    Size s[kPer];
-    uint32_t it = 0;
-    unsigned long long by = 0;
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t r = t * kTile + threadIdx.x * kPer + k;
-      s[k] = Size{0u, 0u, 0ull};
-      x[k] = Rec{0u, 0xFFFFFFFFu, false};
-      w[k] = 0;
-      if (r < n) {
-        x[k] = fetch(a, r);
-        w[k] = x[k].valid ? a.words[x[k].slot] : 0ull;
-        s[k] = rec_size(a, x[k], w[k]);
-      }
-      it += s[k].items;
-      by += s[k].bytes;
-      n_ok += (uint32_t)__popc(s[k].ok);
+    const uint32_t lr = threadIdx.x, r = t * kTile + lr;
+    Rec x{0u, 0xFFFFFFFFu, false};
+    uint64_t w = 0;
+    Size sz{0u, 0u, 0ull};
+    if (r < n) {
+      x = fetch(a, r);
+      w = x.valid ? a.words[x.slot] : 0ull;
+      sz = rec_size(a, T, x, w);
     }
-    // block-exclusive prefix of the threads' items / bytes, plus the tile's base
-    const uint32_t ii = wave_incl(it, lane);
-    const unsigned long long ib = wave_incl(by, lane);
+    n_ok += (uint32_t)__popc(sz.ok);
+    // block-exclusive prefix of the records' items / bytes, plus the tile's base
+    const uint32_t ii = wave_incl(sz.items, lane);
+    const unsigned long long ib = wave_incl(sz.bytes, lane);
     if (lane == 63) {
       s_wi[wave] = ii;
       s_wb[wave] = ib;
     }
     __syncthreads();
-    uint32_t item = a.tile_items[t] + ii - it;
-    unsigned long long pos = a.tile_bytes[t] + ib - by;
+    uint32_t item = a.tile_items[t] + ii - sz.items;
+    unsigned long long pos = a.tile_bytes[t] + ib - sz.bytes;
     for (uint32_t v = 0; v < wave; ++v) {
       item += s_wi[v];
       pos += s_wb[v];
     }
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t lr = threadIdx.x * kPer + k, r = t * kTile + lr;
-      s_slot[lr] = x[k].slot;
-      s_meta[lr] = s[k].ok | (r < n ? (x[k].stage & 0xFFu) << 16 : 0xFFu << 16);
-      s_cls[lr] = (uint32_t)(w[k] & 0xFFFFu);
-      s_base[lr] = pos;
-      if (r >= n || x[k].stage >= a.p.n_stages) continue;
-      const uint32_t t0 = a.p.stage_tpl_ptr[x[k].stage], t1 = a.p.stage_tpl_ptr[x[k].stage + 1];
-      uint32_t g = (uint32_t)(w[k] >> 16) & 0xFFu;
+    s_slot[lr] = x.slot;
+    s_meta[lr] = sz.ok | (r < n ? (x.stage & 0xFFu) << 16 : 0xFFu << 16);
+    s_cls[lr] = (uint32_t)(w & 0xFFFFu);
+    s_base[lr] = pos;
+    if (lr == kTile - 1) s_base[kTile] = pos + sz.bytes;
+    if (r < n && x.stage < a.p.n_stages) {
+      const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
+      uint32_t g = (uint32_t)(w >> 16) & 0xFFu;
       for (uint32_t j = t0; j < t1; ++j, ++item) {
         const uint32_t tid = a.p.stage_tpl[j];
-        const bool ok = (s[k].ok >> (j - t0)) & 1u;
+        const bool ok = (sz.ok >> (j - t0)) & 1u;
         a.items[item] = kwk_emit_item{r, (uint16_t)tid, (uint8_t)(ok ? KWK_EMIT_OK : KWK_EMIT_HOST), 0};
         a.offsets[item] = pos;
         if (ok) {
-          const kwk_emit_skel& S = a.p.skels[skel_index(a, w[k], tid)];
-          pos += (unsigned long long)skel_bytes(a, S, x[k].slot);
+          const kwk_emit_skel& S = a.p.skels[skel_index(a, w, tid)];
+          pos += (unsigned long long)skel_bytes(a, T, S, x.slot);
           g = (g & S.keep) | S.set;
         }
       }
       // the object's guard bits after the patches (all items emitted here; else the host sets them)
       const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
-      if (x[k].valid && s[k].ok == all) {
-        const uint32_t cls = (uint32_t)(w[k] & 0xFFFFu);
-        if (a.p.stage_delete[x[k].stage] && cls < a.p.n_classes) g = a.p.fresh[cls];
-        const uint64_t nw = (w[k] & ~(0xFFull << 16)) | (uint64_t)g << 16;
-        if (nw != w[k]) a.words[x[k].slot] = nw;
+      if (x.valid && sz.ok == all) {
+        const uint32_t cls = (uint32_t)(w & 0xFFFFu);
+        if (a.p.stage_delete[x.stage] && cls < a.p.n_classes) g = a.p.fresh[cls];
+        const uint64_t nw = (w & ~(0xFFull << 16)) | (uint64_t)g << 16;
+        if (nw != w) a.words[x.slot] = nw;
       }
     }
     __syncthreads();
-    // bytes: wave `wave` writes records [wave * 256, wave * 256 + 256) of the tile, whose output
-    // is one contiguous span, 64 lanes per literal run / value
+    // bytes: wave `wave` writes records [wave * 64, wave * 64 + 64) of the tile, whose output is
+    // one contiguous span, 64 lanes per literal run / value
     const uint32_t r0 = wave * kWaveRecs, r1 = r0 + kWaveRecs;
     if constexpr (!kStaged) {
-      for (uint32_t lr = r0; lr < r1; ++lr) {
-        const uint32_t meta = s_meta[lr];
+      for (uint32_t q = r0; q < r1; ++q) {
+        const uint32_t meta = s_meta[q];
         const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
         if (stage >= a.p.n_stages || !ok) continue;
-        put_record(a, stage, ok, s_slot[lr], s_cls[lr], s_base[lr], lane, s_now,
-                   [&](unsigned long long g, char c) { a.out[g] = c; });
+        put_record(a, T, stage, ok, s_slot[q], s_cls[q], s_base[q], lane, s_now,
+                   [&](unsigned long long gp, char c) { a.out[gp] = c; });
       }
     } else {
       // staged: the span goes through a per-wave LDS window [w0, w0 + kStageBytes) (w0 16-byte
-      // aligned) and leaves as 16-byte stores; only the span's two edges take byte stores
+      // aligned) and leaves as 16-byte stores; only the edges of a flushed range take byte stores
       char* buf = s_buf + wave * kStageBytes;
       unsigned long long w0 = s_base[r0] & ~15ull, lo = s_base[r0], hi = lo;
       auto flush = [&](unsigned long long f_lo, unsigned long long f_hi) {
@@ -396,26 +432,26 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       };
-      for (uint32_t lr = r0; lr < r1; ++lr) {
-        const uint32_t meta = s_meta[lr];
+      for (uint32_t q = r0; q < r1; ++q) {
+        const uint32_t meta = s_meta[q];
         const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
         if (stage >= a.p.n_stages || !ok) continue;
-        const uint32_t slot = s_slot[lr], cls = s_cls[lr];
-        const unsigned long long p = s_base[lr];
-        const unsigned long long end = p + rec_bytes(a, stage, ok, slot, cls);
+        const uint32_t slot = s_slot[q], cls = s_cls[q];
+        const unsigned long long p = s_base[q], end = s_base[q + 1];
         if (end - w0 > kStageBytes) {  // the window is full: out with everything before this record
           flush(lo, p);  // (the chunk holding p is finished by byte stores from both sides)
           w0 = p & ~15ull;
           lo = p;
           if (end - w0 > kStageBytes) {  // larger than the window: straight to global memory
-            put_record(a, stage, ok, slot, cls, p, lane, s_now, [&](unsigned long long g, char c) { a.out[g] = c; });
+            put_record(a, T, stage, ok, slot, cls, p, lane, s_now,
+                       [&](unsigned long long gp, char c) { a.out[gp] = c; });
             lo = hi = end;
             w0 = end & ~15ull;
             continue;
           }
         }
-        put_record(a, stage, ok, slot, cls, p, lane, s_now,
-                   [&](unsigned long long g, char c) { buf[(uint32_t)(g - w0)] = c; });
+        put_record(a, T, stage, ok, slot, cls, p, lane, s_now,
+                   [&](unsigned long long gp, char c) { buf[(uint32_t)(gp - w0)] = c; });
         hi = end;
       }
       if (hi > lo) flush(lo, hi);
@@ -511,6 +547,8 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->p.n_classes = g->n_classes;
   em->p.n_templates = g->n_templates;
   em->p.n_stages = g->n_stages;
+  em->p.n_pieces = g->n_pieces;
+  em->p.n_lits = (uint32_t)std::min<uint64_t>(g->n_lit_bytes, 0xFFFFFFFFu);
   const uint32_t n_st = g->stage_tpl_ptr[g->n_stages];
   if (kwk_status st = upload(em, const_cast<uint32_t**>(&em->p.stage_tpl_ptr), g->stage_tpl_ptr, g->n_stages + 1)) return st;
   if (kwk_status st = upload(em, const_cast<uint16_t**>(&em->p.stage_tpl), g->stage_tpl, n_st)) return st;
@@ -550,7 +588,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   HIP_TRY(hipMemset(d, 0, 4 * 8));
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, em->device));
-  em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 4u));
+  em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 8u));
   HIP_TRY(hipEventCreate(&em->ev0));
   HIP_TRY(hipEventCreate(&em->ev1));
   return KWK_OK;
@@ -686,14 +724,19 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   a.now_len = (uint32_t)now.size();
   // the list's count lives on the device: every tile loop reads it; the grid covers the capacity
   HIP_TRY(hipEventRecord(em->ev0, em->stream));
-  hipLaunchKernelGGL(emit_size_kernel, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  const bool lds = em->p.n_pieces <= kLdsPieces && em->p.n_lits <= kLdsLits;
+  if (lds)
+    hipLaunchKernelGGL(emit_size_kernel<true>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  else
+    hipLaunchKernelGGL(emit_size_kernel<false>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
-  if (source & KWK_EMIT_BYTE_STORES)
-    hipLaunchKernelGGL(emit_write_kernel<false>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
-  else
-    hipLaunchKernelGGL(emit_write_kernel<true>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
+  const bool bytes = (source & KWK_EMIT_BYTE_STORES) != 0;
+  const void* wk = bytes ? (lds ? (const void*)emit_write_kernel<false, true> : (const void*)emit_write_kernel<false, false>)
+                         : (lds ? (const void*)emit_write_kernel<true, true> : (const void*)emit_write_kernel<true, false>);
+  void* wargs[] = {&a};
+  HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(em->ev1, em->stream));
   em->emitted = true;

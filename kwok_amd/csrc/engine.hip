@@ -3821,7 +3821,10 @@ struct kwk_engine {
   uint32_t podv_n = 0;
   uint32_t usage_blocks = 0;      // KWK_TUNE_USAGE_BLOCKS (0: occupancy API)
   uint32_t compact_small = 8192;  // KWK_TUNE_COMPACT_SMALL (kSmallSegs)
-  bool compact_lb = true;         // KWK_TUNE_COMPACT_LB: the one-pass look-back hand-back
+  // KWK_TUNE_COMPACT_LB: the one-pass look-back hand-back.  Off by default: with four segments
+  // per workgroup the prefix frontier advances ~64 workgroups per look-back round trip, 73 us at
+  // C5 against 27 us for the scan pair (r4d)
+  bool compact_lb = false;
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)

@@ -96,6 +96,71 @@ def _run(cl, steps, dt_ns, seed):
         eng.close()
 
 
+def _big_stage_run(steps):
+    """Patches longer than the emitter's per-wave LDS window (6 KiB): the staged writer sends such a
+    record straight to global memory; a short second stage keeps the windows in use around it."""
+    from kwok_amd.host import emit
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.controller import KindController
+    from kwok_amd.host.encoder import NativeIngest
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import stage_from_v1alpha1
+    from tests.parity_util import NOW0
+    from tests.test_patch import FUNCS
+
+    def doc(name, key, op, vals, template):
+        sel = {"key": key, "operator": op}
+        if vals:
+            sel["values"] = vals
+        return stage_from_v1alpha1({
+            "apiVersion": "kwok.x-k8s.io/v1alpha1", "kind": "Stage", "metadata": {"name": name},
+            "spec": {"resourceRef": {"apiGroup": "v1", "kind": "Pod"}, "selector": {"matchExpressions": [sel]},
+                     "next": {"statusTemplate": template}}})
+    big = "x" * 7000
+    stages = [doc("big", ".status.phase", "DoesNotExist", None,
+                  "phase: Pending\nmessage: '" + big + " at {{ Now }}'\nhostIP: {{ NodeIPWith .spec.nodeName | Quote }}\n"),
+              doc("small", ".status.phase", "In", ["Pending"], "phase: Running\nreason: '{{ Now }}'\n")]
+    objs = [{"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": "d", "uid": f"u{i}"},
+             "spec": {"nodeName": f"n{i % 7}", "containers": [{"name": "c", "image": "i"}]}} for i in range(3000)]
+    prog = KindProgram(stages)
+    prog.explore(objs)
+    nat = NativeIngest(prog)
+    hot, dels, rec, cls = nat.columns(objs)
+    eng = Engine(prog, capacity=len(objs), max_records=len(nat.record_array()) + 64)
+    ctl = KindController(prog, eng, Ingest(prog), objs, funcs=FUNCS, native=True)
+    classes = [prog.class_of(o, register=False) for o in ctl.objs]
+    ep = emit.EmitProgram(prog.stages, ctl.patcher, {classes[0]: ctl.objs[0]}, len(prog.class_ids))
+    em = emit.Emitter(eng, len(objs), ep)
+    n_dev = 0
+    try:
+        w, cc = ep.rows(ctl.objs, classes)
+        em.set_rows(0, w, cc)
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, nat.record_array())
+        for k in range(steps):
+            now = NOW0 + k * 10**9
+            eng.step(now, 7, k)
+            eng.fired_compact(packed=True)
+            items, offs, out = em.run(now, packed=True)
+            fired = eng.fired()
+            ctl.handle(fired, now)
+            for n, it in enumerate(items):
+                slot = int(fired[int(it["rec"])]["slot"])
+                assert int(it["status"]) == emit.STATUS_OK, (k, slot)
+                assert out[int(offs[n]):int(offs[n + 1])] == ctl.last_patches[(slot, 0)], (k, slot)
+                n_dev += 1
+        return n_dev
+    finally:
+        em.close()
+        ctl.close()
+        nat.close()
+        eng.close()
+
+
+def test_gpu_emit_records_larger_than_the_window():
+    assert _big_stage_run(steps=4) >= 6000
+
+
 def test_gpu_emit_c2_pod_general_equals_native_render():
     cl = W.make_cluster("C2", 30, 400, seed=91)
     c = _run(cl, steps=30, dt_ns=500 * 10**6, seed=0x91)

@@ -116,7 +116,7 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
             e.close()
 
 
-HANDBACK_PATHS = ((1, 8192), (0, 8192), (0, 0))  # (KWK_TUNE_COMPACT_LB, KWK_TUNE_COMPACT_SMALL)
+HANDBACK_PATHS = ((0, 8192), (1, 8192), (0, 0))  # (KWK_TUNE_COMPACT_LB, KWK_TUNE_COMPACT_SMALL); [0] = default
 
 
 def _handback_path(eng, path):
@@ -126,9 +126,9 @@ def _handback_path(eng, path):
 
 
 def test_handback_pair_equals_one_launch_at_4m_pods():
-    """The fired hand-back's three paths over the same step's segments: the one-pass look-back
-    compaction (the default), the one-launch compaction that re-sums the counts (at most 8192
-    segments) and the scan + expansion pair (KWK_TUNE_COMPACT_LB 0, KWK_TUNE_COMPACT_SMALL 0)
+    """The fired hand-back's three paths over the same step's segments: the one-launch compaction
+    that re-sums the counts (at most 8192 segments, the default here), the one-pass look-back
+    compaction (KWK_TUNE_COMPACT_LB 1) and the scan + expansion pair (KWK_TUNE_COMPACT_SMALL 0)
     give the same dense list in the same order; every slot once."""
     prog, eng = _pods("auto")
     try:
