@@ -50,9 +50,11 @@ constexpr uint32_t kBlock = 256, kTile = kBlock;  // records per tile: one per t
 constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
 constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
 constexpr uint32_t kScanBlock = 1024;
-constexpr uint32_t kStageBytes = 4096;  // per-wave LDS window of the staged writes
-constexpr uint32_t kLdsPieces = 512;    // skeleton tables staged in LDS when they fit
-constexpr uint32_t kLdsLits = 12288;
+constexpr uint32_t kStageBytes = 3072;  // per-wave LDS window of the staged writes
+constexpr uint32_t kLdsPieces = 256;    // skeleton tables staged in LDS when they fit
+constexpr uint32_t kLdsLits = 8192;
+constexpr uint32_t kLdsSkels = 64;
+constexpr uint32_t kRecSk = 4;          // skeletons of a record's emitted items kept in LDS (more: looked up)
 
 struct Prog {
   const uint32_t* stage_tpl_ptr;
@@ -66,7 +68,7 @@ struct Prog {
   uint8_t* const* cols;
   const uint32_t* stride;
   uint32_t n_classes, n_templates, n_stages, n_pieces;
-  uint32_t n_lits;
+  uint32_t n_lits, n_cols, n_skels;
 };
 
 struct EmitArgs {
@@ -132,9 +134,21 @@ __device__ __forceinline__ Rec fetch(const EmitArgs& a, uint32_t r) {
   return x;
 }
 
+// where a record's call values are read: the value columns in global memory, or the rows the
+// write kernel staged in LDS for the tile (kLdsCols columns of 16 bytes)
+constexpr uint32_t kLdsCols = 2;
+struct Vals {
+  const uint8_t* lds;  // [kLdsCols][kTile][16] or null
+  uint32_t lr;         // the record's index in the tile
+  __device__ __forceinline__ const uint8_t* row(const EmitArgs& a, uint32_t c, uint32_t slot) const {
+    if (lds) return lds + ((uint64_t)c * kTile + lr) * 16u;
+    return a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
+  }
+};
+
 // bytes of one skeleton for this slot, or -1 when a value is unusable
 __device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S,
-                                                uint32_t slot) {
+                                                uint32_t slot, const Vals& V = Vals{nullptr, 0}) {
   long long b = 0;
   for (uint32_t q = 0; q < S.n_pieces; ++q) {
     const kwk_emit_piece P = T.pieces[S.first_piece + q];
@@ -142,8 +156,7 @@ __device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables&
     if (P.slot == 0) {
       b += a.now_len;
     } else if (P.slot != KWK_EMIT_NO_SLOT) {
-      const uint32_t c = P.slot - 1u;
-      const uint32_t len = a.p.cols[c][(uint64_t)slot * a.p.stride[c]];
+      const uint32_t len = V.row(a, P.slot - 1u, slot)[0];
       if (len == 0xFFu) return -1;
       b += len;
     }
@@ -165,7 +178,8 @@ struct Size {
   unsigned long long bytes;
 };
 
-__device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, const Rec& x, uint64_t w) {
+__device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, const Rec& x, uint64_t w,
+                                         const Vals& V = Vals{nullptr, 0}) {
   Size s{0u, 0u, 0ull};
   if (x.stage >= a.p.n_stages) return s;
   const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
@@ -173,7 +187,7 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, con
     ++s.items;
     const int k = x.valid ? skel_index(a, w, a.p.stage_tpl[j]) : -1;
     if (k < 0) continue;
-    const long long b = skel_bytes(a, T, a.p.skels[k], x.slot);
+    const long long b = skel_bytes(a, T, a.p.skels[k], x.slot, V);
     if (b < 0) continue;
     s.ok |= 1u << (j - t0);
     s.bytes += (unsigned long long)b;
@@ -181,16 +195,13 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, con
   return s;
 }
 
-// the bytes of a record's emitted items: put(global position, byte) for each, 64 lanes per run
-// (a value's length and bytes are loaded together)
+// the bytes of one emitted item: put(global position, byte) for each, 64 lanes per run (a value's
+// length and bytes are loaded together); returns the position after them
 template <typename Put>
-__device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, uint32_t stage, uint32_t ok,
-                                           uint32_t slot, uint32_t cls, unsigned long long p, uint32_t lane,
-                                           const char* s_now, Put put) {
-  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
-  for (uint32_t j = t0; j < t1; ++j) {
-    if (!((ok >> (j - t0)) & 1u)) continue;
-    const kwk_emit_skel S = a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]];
+__device__ __forceinline__ unsigned long long put_skel(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S,
+                                                       uint32_t slot, unsigned long long p, uint32_t lane,
+                                                       const char* s_now, const Vals& V, Put put) {
+  {
     for (uint32_t q = 0; q < S.n_pieces; ++q) {
       const kwk_emit_piece P = T.pieces[S.first_piece + q];
       const char* src = T.lits + P.lit_off;
@@ -200,8 +211,8 @@ __device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, u
         if (lane < a.now_len) put(p + lane, s_now[lane]);
         p += a.now_len;
       } else if (P.slot != KWK_EMIT_NO_SLOT) {
-        const uint32_t c = P.slot - 1u, sd = a.p.stride[c];
-        const uint8_t* v = a.p.cols[c] + (uint64_t)slot * sd;
+        const uint32_t c = P.slot - 1u, sd = V.lds ? 16u : a.p.stride[c];
+        const uint8_t* v = V.row(a, c, slot);
         const uint32_t len = v[0];
         const char b0 = lane + 1u < sd ? (char)v[1 + lane] : 0;
         if (lane < len) put(p + lane, b0);
@@ -210,6 +221,23 @@ __device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, u
       }
     }
   }
+  return p;
+}
+
+// every emitted item of a record: the skeletons listed in LDS (n_sk <= kRecSk), or looked up
+template <typename Put>
+__device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, const kwk_emit_skel* skels,
+                                           uint32_t stage, uint32_t ok, uint32_t n_sk, const int16_t* sk,
+                                           uint32_t slot, uint32_t cls, unsigned long long p, uint32_t lane,
+                                           const char* s_now, const Vals& V, Put put) {
+  if (n_sk <= kRecSk) {
+    for (uint32_t j = 0; j < n_sk; ++j) p = put_skel(a, T, skels[sk[j]], slot, p, lane, s_now, V, put);
+    return;
+  }
+  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
+  for (uint32_t j = t0; j < t1; ++j)
+    if ((ok >> (j - t0)) & 1u)
+      p = put_skel(a, T, a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]], slot, p, lane, s_now, V, put);
 }
 
 template <typename T>
@@ -329,9 +357,14 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
+// kLds: the skeleton tables and the records' call-value rows (at most kLdsCols columns of 16
+// bytes) staged in LDS
 template <bool kStaged, bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   __shared__ __attribute__((aligned(16))) char s_buf[kStaged ? kWaves * kStageBytes : 16];
+  __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
+  __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
+  __shared__ int16_t s_sk[kTile * kRecSk];
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
   __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
   __shared__ uint32_t s_slot[kTile];
@@ -344,7 +377,10 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const unsigned long long tot_i = a.totals[0], tot_b = a.totals[1];
   if (tot_i > a.cap_items || tot_b > a.cap_bytes || a.totals[2]) return;  // KWK_ECAP: nothing is written
-  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
+  if constexpr (kLds)
+    for (uint32_t j = threadIdx.x; j < a.p.n_skels; j += blockDim.x) s_skels[j] = a.p.skels[j];
+  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);  // (its barrier covers s_skels)
+  const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.offsets[tot_i] = tot_b;
   if (threadIdx.x < 40) s_now[threadIdx.x] = a.now[threadIdx.x];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -354,10 +390,18 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     Rec x{0u, 0xFFFFFFFFu, false};
     uint64_t w = 0;
     Size sz{0u, 0u, 0ull};
+    Vals V{nullptr, lr};
+    if constexpr (kLds) V.lds = reinterpret_cast<const uint8_t*>(s_vals);
     if (r < n) {
       x = fetch(a, r);
       w = x.valid ? a.words[x.slot] : 0ull;
-      sz = rec_size(a, T, x, w);
+      if constexpr (kLds) {  // the record's value rows, one 16-byte gather per column
+        for (uint32_t c = 0; c < kLdsCols; ++c)
+          s_vals[c * kTile + lr] = c < a.p.n_cols && x.valid
+                                       ? *reinterpret_cast<const uint4*>(a.p.cols[c] + (uint64_t)x.slot * 16u)
+                                       : make_uint4(0xFFu, 0u, 0u, 0u);
+      }
+      sz = rec_size(a, T, x, w, V);
     }
     n_ok += (uint32_t)__popc(sz.ok);
     // block-exclusive prefix of the records' items / bytes, plus the tile's base
@@ -375,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       pos += s_wb[v];
     }
     s_slot[lr] = x.slot;
-    s_meta[lr] = sz.ok | (r < n ? (x.stage & 0xFFu) << 16 : 0xFFu << 16);
+    uint32_t n_sk = 0;
     s_cls[lr] = (uint32_t)(w & 0xFFFFu);
     s_base[lr] = pos;
     if (lr == kTile - 1) s_base[kTile] = pos + sz.bytes;
@@ -388,9 +432,12 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         a.items[item] = kwk_emit_item{r, (uint16_t)tid, (uint8_t)(ok ? KWK_EMIT_OK : KWK_EMIT_HOST), 0};
         a.offsets[item] = pos;
         if (ok) {
-          const kwk_emit_skel& S = a.p.skels[skel_index(a, w, tid)];
-          pos += (unsigned long long)skel_bytes(a, T, S, x.slot);
+          const int k = skel_index(a, w, tid);
+          const kwk_emit_skel& S = skels[k];
+          pos += (unsigned long long)skel_bytes(a, T, S, x.slot, V);
           g = (g & S.keep) | S.set;
+          if (n_sk < kRecSk) s_sk[lr * kRecSk + n_sk] = (int16_t)k;
+          ++n_sk;
         }
       }
       // the object's guard bits after the patches (all items emitted here; else the host sets them)
@@ -402,6 +449,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         if (nw != w) a.words[x.slot] = nw;
       }
     }
+    s_meta[lr] = sz.ok | (r < n ? (x.stage & 0xFFu) << 16 : 0xFFu << 16) | min(n_sk, 15u) << 24;
     __syncthreads();
     // bytes: wave `wave` writes records [wave * 64, wave * 64 + 64) of the tile, whose output is
     // one contiguous span, 64 lanes per literal run / value
@@ -409,9 +457,10 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     if constexpr (!kStaged) {
       for (uint32_t q = r0; q < r1; ++q) {
         const uint32_t meta = s_meta[q];
-        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
+        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu, n_sk = meta >> 24;
         if (stage >= a.p.n_stages || !ok) continue;
-        put_record(a, T, stage, ok, s_slot[q], s_cls[q], s_base[q], lane, s_now,
+        const Vals Vq{kLds ? reinterpret_cast<const uint8_t*>(s_vals) : nullptr, q};
+        put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, s_slot[q], s_cls[q], s_base[q], lane, s_now, Vq,
                    [&](unsigned long long gp, char c) { a.out[gp] = c; });
       }
     } else {
@@ -434,23 +483,24 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       };
       for (uint32_t q = r0; q < r1; ++q) {
         const uint32_t meta = s_meta[q];
-        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu;
+        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu, n_sk = meta >> 24;
         if (stage >= a.p.n_stages || !ok) continue;
         const uint32_t slot = s_slot[q], cls = s_cls[q];
         const unsigned long long p = s_base[q], end = s_base[q + 1];
+        const Vals Vq{kLds ? reinterpret_cast<const uint8_t*>(s_vals) : nullptr, q};
         if (end - w0 > kStageBytes) {  // the window is full: out with everything before this record
           flush(lo, p);  // (the chunk holding p is finished by byte stores from both sides)
           w0 = p & ~15ull;
           lo = p;
           if (end - w0 > kStageBytes) {  // larger than the window: straight to global memory
-            put_record(a, T, stage, ok, slot, cls, p, lane, s_now,
+            put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, slot, cls, p, lane, s_now, Vq,
                        [&](unsigned long long gp, char c) { a.out[gp] = c; });
             lo = hi = end;
             w0 = end & ~15ull;
             continue;
           }
         }
-        put_record(a, T, stage, ok, slot, cls, p, lane, s_now,
+        put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, slot, cls, p, lane, s_now, Vq,
                    [&](unsigned long long gp, char c) { buf[(uint32_t)(gp - w0)] = c; });
         hi = end;
       }
@@ -549,6 +599,8 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->p.n_stages = g->n_stages;
   em->p.n_pieces = g->n_pieces;
   em->p.n_lits = (uint32_t)std::min<uint64_t>(g->n_lit_bytes, 0xFFFFFFFFu);
+  em->p.n_cols = g->n_columns;
+  em->p.n_skels = g->n_skels;
   const uint32_t n_st = g->stage_tpl_ptr[g->n_stages];
   if (kwk_status st = upload(em, const_cast<uint32_t**>(&em->p.stage_tpl_ptr), g->stage_tpl_ptr, g->n_stages + 1)) return st;
   if (kwk_status st = upload(em, const_cast<uint16_t**>(&em->p.stage_tpl), g->stage_tpl, n_st)) return st;
@@ -724,7 +776,9 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   a.now_len = (uint32_t)now.size();
   // the list's count lives on the device: every tile loop reads it; the grid covers the capacity
   HIP_TRY(hipEventRecord(em->ev0, em->stream));
-  const bool lds = em->p.n_pieces <= kLdsPieces && em->p.n_lits <= kLdsLits;
+  bool lds = em->p.n_pieces <= kLdsPieces && em->p.n_lits <= kLdsLits && em->p.n_skels <= kLdsSkels;
+  bool vals16 = em->n_columns <= kLdsCols;
+  for (uint32_t c = 0; c < em->n_columns; ++c) vals16 = vals16 && em->stride[c] == 16u;
   if (lds)
     hipLaunchKernelGGL(emit_size_kernel<true>, dim3(em->grid), dim3(kBlock), 0, em->stream, a);
   else
@@ -733,8 +787,9 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
   const bool bytes = (source & KWK_EMIT_BYTE_STORES) != 0;
-  const void* wk = bytes ? (lds ? (const void*)emit_write_kernel<false, true> : (const void*)emit_write_kernel<false, false>)
-                         : (lds ? (const void*)emit_write_kernel<true, true> : (const void*)emit_write_kernel<true, false>);
+  const bool wl = lds && vals16;  // the write kernel's LDS path also stages the value rows
+  const void* wk = bytes ? (wl ? (const void*)emit_write_kernel<false, true> : (const void*)emit_write_kernel<false, false>)
+                         : (wl ? (const void*)emit_write_kernel<true, true> : (const void*)emit_write_kernel<true, false>);
   void* wargs[] = {&a};
   HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());
