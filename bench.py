@@ -3,9 +3,10 @@
 One *step* = one reconciliation pass of the HIP engines over the whole resident cluster
 (pods + nodes): harness churn, match of changed objects, weighted pick + delay/jitter,
 firing of due objects, their next-state deltas, and the fired hand-back — each engine's
-fired list compacted into one dense device list every step (kwk_fired_compact_packed: 4-byte
-records, 27-bit slot | 5-bit stage; --handback rec: kwk_fired_compact's 8-byte kwk_fired_rec; the
-Go host would DMA it from there).  Every `--report-every` steps (the reporting interval) the cluster
+fired list compacted into one dense device list every step (pods: kwk_fired_compact_packed16, the
+1-byte sweep's 2-byte records {offset, stage, flags} grouped by 2048-slot segment; nodes:
+kwk_fired_compact_packed, 4-byte records, 27-bit slot | 5-bit stage; --handback packed / rec: 4-byte
+records / 8-byte kwk_fired_rec for both; the Go host would DMA it from there).  Every `--report-every` steps (the reporting interval) the cluster
 aggregates are computed on the device and summed over all GPUs with one RCCL all-reduce:
 per-stage transition counts, the pod / node phase histograms (kwk_count) and the cluster
 CPU / memory usage (kwk_usage over the default usage-from-annotation ClusterResourceUsage).
@@ -159,10 +160,14 @@ class Reporter:
 
 SWEEP_NAMES = {1: "sweep16_kernel", 2: "sweep16_fsm_kernel", 3: "sweepw_kernel<4>", 4: "sweepw_kernel<8>",
                5: "sweep8_kernel"}  # kwk_last_sweep kernel codes (KWK_SWEEP_*)
-EV_EVERY = 2  # HIP events bracket the pod sweep of every 2nd step: each marker idles the stream ~5 us (r2b)
+EV_EVERY = 4  # HIP events bracket the pod sweep of every 4th step (5 launches of 20): each marker pair idles
+              # the stream ~4.7 us (r4e trace), 1.2 us per step at this spacing instead of 2.4 us every 2nd step
 
 
-HANDBACK = {"packed": "packed", "rec": True}  # --handback: kwk_step_n's compaction (4-byte packed / kwk_fired_rec)
+# --handback: kwk_step_n's compaction (2-byte records where the sweep has them / 4-byte packed / kwk_fired_rec)
+HANDBACK = {"packed16": "packed16", "packed": "packed", "rec": True}
+HANDBACK_NAMES = {"packed16": "2-byte pod records + 4-byte packed node records", "packed": "packed 4-byte",
+                  "rec": "8-byte kwk_fired_rec"}
 
 
 def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None,
@@ -199,15 +204,20 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
         pods.step(now, seed, k)
         if timed:
             pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
-        packed = handback == "packed"
-        pods.fired_compact(packed)
+        packed = handback in ("packed", "packed16")
+        # the 1-byte sweep writes 2-byte records when the program has at most 4 stages
+        p16 = handback == "packed16" and pods.last_sweep()["kernel"] == 5 and len(pods.p.stages) <= 4
+        pods.fired_compact("16" if p16 else packed)
         nodes.step(now, seed, k)
         nodes.fired_compact(packed)
         if pinned is not None:  # PCIe-inclusive: every fired record copied to pinned host memory
-            if packed:
-                n_fired_host += len(pods.fired_packed(pinned[0])) + len(nodes.fired_packed(pinned[1]))
+            if p16:  # 2 bytes per transition + the records per 2048-slot segment
+                n_fired_host += len(pods.fired_packed16((pinned[0], pinned[2]))[0])
+            elif packed:
+                n_fired_host += len(pods.fired_packed(pinned[0]))
             else:
-                n_fired_host += len(pods.fired(pinned[0])) + len(nodes.fired(pinned[1]))
+                n_fired_host += len(pods.fired(pinned[0]))
+            n_fired_host += len(nodes.fired_packed(pinned[1])) if packed else len(nodes.fired(pinned[1]))
         if reporter is not None and report_every and (j + 1) % report_every == 0:
             last = reporter.collect(now)
     return last, n_fired_host
@@ -577,9 +587,11 @@ def main():
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
-    ap.add_argument("--handback", choices=("packed", "rec"), default="packed",
-                    help="fired hand-back per step: packed 4-byte records (kwk_fired_compact_packed, 27-bit slot | "
-                         "5-bit stage) or 8-byte kwk_fired_rec (kwk_fired_compact)")
+    ap.add_argument("--handback", choices=("packed16", "packed", "rec"), default="packed16",
+                    help="fired hand-back per step: 2-byte records where the sweep has them (kwk_fired_compact_packed16: "
+                         "the 1-byte sweep's {offset, stage, flags} + records per segment; other engines 4-byte), "
+                         "packed 4-byte records (kwk_fired_compact_packed, 27-bit slot | 5-bit stage) or 8-byte "
+                         "kwk_fired_rec (kwk_fired_compact)")
     ap.add_argument("--collective", choices=("torch", "native"), default="torch",
                     help="aggregate all-reduce: torch.distributed (default) or libkwok_comm (RCCL, no torch; N > 1)")
     args = ap.parse_args()
@@ -730,7 +742,8 @@ def main():
     pcie = None
     if args.pcie_steps > 0 and world == 1:
         from kwok_amd.host.engine import PinnedBuffer
-        pin = (PinnedBuffer(8 * pods.capacity), PinnedBuffer(8 * nodes.capacity))
+        pin = (PinnedBuffer(8 * pods.capacity), PinnedBuffer(8 * nodes.capacity),
+               PinnedBuffer(4 * (pods.capacity // 512 + 64)))
         k0 = args.warmup + args.steps
         s2p, s2n = pods.stats(), nodes.stats()
         t1 = time.perf_counter()
@@ -741,9 +754,11 @@ def main():
         assert n_host == nf, (n_host, nf)
         pcie = {"value": round(nf / wall, 1), "unit": "stage transitions/sec", "steps": args.pcie_steps,
                 "fired_records_to_host_per_step": nf / args.pcie_steps, "ms_per_step": round(wall / args.pcie_steps * 1e3, 4),
-                "note": "each step's fired lists copied into kwk_alloc_host buffers: " + (
-                    "kwk_fired_packed, 4 B per transition" if args.handback == "packed" else
-                    "kwk_fired, 8 B per transition")}
+                "note": "each step's fired lists copied into kwk_alloc_host buffers: " + {
+                    "packed16": "pods kwk_fired_packed16 (2 B per transition + 4 B per 2048-slot segment), nodes "
+                                "kwk_fired_packed (4 B)",
+                    "packed": "kwk_fired_packed, 4 B per transition",
+                    "rec": "kwk_fired, 8 B per transition"}[args.handback]}
         for p in pin:
             p.close()
     patch_emit = None
@@ -799,7 +814,7 @@ def main():
             "config": {"workload": f"C5: {total_nodes:,} nodes / {total_nodes * args.pods_per_node:,} pods in total "
                                    f"over {world} GPU(s), pod-fast + node-initialize/heartbeat, harness churn "
                                    "(Succeeded -> delete -> re-create), 10% Job-owned; per step: sweep + fired "
-                                   f"hand-back (device compaction into {'packed 4-byte' if args.handback == 'packed' else '8-byte kwk_fired_rec'}"
+                                   f"hand-back (device compaction into {HANDBACK_NAMES[args.handback]}"
                                    f" records); every {args.report_every} steps: phase "
                                    "histograms + cluster usage + per-stage counts all-reduced over RCCL",
                        "nodes": total_nodes, "pods": total_nodes * args.pods_per_node,

@@ -319,6 +319,23 @@ kwk_status kwk_fired_device(kwk_engine* eng, const kwk_fired_rec** recs, const u
 #define KWK_FIRED_PACKED_STAGE(r) ((uint32_t)(r) >> 27)
 #define KWK_FIRED_PACKED_SLOT(r) ((uint32_t)(r) & 0x7FFFFFFu)
 kwk_status kwk_fired_compact_packed(kwk_engine* eng);
+/* The hand-back at 2 bytes per transition, for engines on the 1-byte dictionary sweep with at most 4
+ * stages (the C1 / C5 pod-fast shape; KWK_ESTATE otherwise: use kwk_fired_packed): the sweep's
+ * own records {offset: 11, stage: 2, flags: 3} copied into one dense list, grouped by segment, plus
+ * the records per segment.  Segment s (in order) covers slots [s * region_slots, (s + 1) *
+ * region_slots); a record r of it is slot s * region_slots + KWK_FIRED16_SLOT(r), stage
+ * KWK_FIRED16_STAGE(r), flags KWK_FIRED16_FLAGS(r) (the KWK_FIRED_* bits).  Same (slot, stage)
+ * sequence as kwk_fired.  kwk_step_n(..., KWK_COMPACT_PACKED16, ...) enqueues it per step (an engine
+ * without 2-byte records then leaves the 4-byte packed list). */
+#define KWK_COMPACT_PACKED16 3u
+#define KWK_FIRED16_STAGE(r) (((uint32_t)(r) >> 11) & 3u)
+#define KWK_FIRED16_FLAGS(r) (((uint32_t)(r) >> 13) & 7u)
+#define KWK_FIRED16_SLOT(r)                                                                                   \
+  (((((uint32_t)(r) & 0x7FFu) >> 8) >> 2) * 1024u + (((((uint32_t)(r) & 0x7FFu) >> 2) & 63u) ^ (((uint32_t)(r) & 0x7FFu) >> 8)) * 16u + \
+   ((((uint32_t)(r) & 0x7FFu) >> 8) & 3u) * 4u + ((uint32_t)(r) & 3u))
+kwk_status kwk_fired_compact_packed16(kwk_engine* eng);
+kwk_status kwk_fired_packed16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint32_t* n_out, uint32_t* seg_counts,
+                              uint32_t seg_cap, uint32_t* n_segs, uint32_t* region_slots);
 kwk_status kwk_fired_packed(kwk_engine* eng, uint32_t* out, uint32_t cap, uint32_t* n_out);
 kwk_status kwk_fired_packed_device(kwk_engine* eng, const uint32_t** recs, const uint32_t** count);
 /* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */

@@ -50,7 +50,7 @@ constexpr uint32_t kBlock = 256, kTile = kBlock;  // records per tile: one per t
 constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
 constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
 constexpr uint32_t kScanBlock = 1024;
-constexpr uint32_t kStageBytes = 3072;  // per-wave LDS window of the staged writes
+constexpr uint32_t kStageBytes = 2048;  // per-wave LDS window of the staged writes
 constexpr uint32_t kLdsPieces = 256;    // skeleton tables staged in LDS when they fit
 constexpr uint32_t kLdsLits = 8192;
 constexpr uint32_t kLdsSkels = 64;

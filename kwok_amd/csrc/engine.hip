@@ -2161,34 +2161,88 @@ __device__ __forceinline__ void store_out(const CompactArgs& a, uint32_t at, uin
   else store_rec_nt(&a.out[at], slot, x);
 }
 
-// one wave per segment; the first 256 records are loaded together with the segment's count and
-// offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it).  kPacked:
-// 4-byte records (kwk_fired_packed) instead of kwk_fired_rec — half the bytes written
-template <int kRec, bool kPacked = false>
+// kSpw segments per wave; each segment's first 256 records are loaded together with its count
+// and offset (a segment holds at least 64 * 16 + 31 words, so the loads stay inside it), all the
+// wave's segments' loads in flight at once: at C5 (48k segments) one segment per wave ran six
+// dispatch rounds of a ~3.5 us load chain (21 us); four per wave keep every wave resident.
+// kPacked: 4-byte records (kwk_fired_packed) instead of kwk_fired_rec — half the bytes written
+constexpr uint32_t kCompactSpw = 4;
+template <int kRec, bool kPacked = false, uint32_t kSpw = 1>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
+  static_assert(kScanGroup % (kSpw * kWavesPerBlock) == 0, "a wave's segments lie in one scan group");
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t seg = blockIdx.x * kSegsPerBlock + wave;
-  if (seg >= a.n_segs) return;
-  const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
-  uint2 r[kPre];
+  const uint32_t seg0 = (blockIdx.x * kWavesPerBlock + wave) * kSpw;
+  if (seg0 >= a.n_segs) return;
+  uint2 r[kSpw][kPre];
+  uint32_t c[kSpw], o1[kSpw];
 #pragma unroll
-  for (int k = 0; k < kPre; ++k) r[k] = rec_at<kRec>(sp, lane + 64u * k);
-  const uint32_t c = a.counts[seg];
-  uint32_t gp = 0;  // records of the groups before this segment's
-  for (uint32_t g = lane; g < seg / kScanGroup; g += 64) gp += a.group_tot[g];
-  for (int o = 32; o > 0; o >>= 1) gp += __shfl_xor(gp, o);
-  const uint32_t off = gp + a.offsets[1 + seg];
-  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
-  const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
+  for (uint32_t s = 0; s < kSpw; ++s) {
+    const uint32_t seg = seg0 + s < a.n_segs ? seg0 + s : seg0;
+    const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
 #pragma unroll
-  for (int k = 0; k < kPre; ++k) {
-    const uint32_t j = lane + 64u * k;
-    if (j < c) store_out<kPacked>(a, off + j, base + r[k].x, r[k].y);
+    for (int k = 0; k < kPre; ++k) r[s][k] = rec_at<kRec>(sp, lane + 64u * k);
+    c[s] = seg0 + s < a.n_segs ? a.counts[seg] : 0u;
+    o1[s] = a.offsets[1 + seg];
   }
-  for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
-    const uint2 x = rec_at<kRec>(sp, j);
-    store_out<kPacked>(a, off + j, base + x.x, x.y);
+  uint32_t gp = 0;  // records of the groups before the wave's segments' group
+  for (uint32_t g = lane; g < seg0 / kScanGroup; g += 64) gp += a.group_tot[g];
+  for (int o = 32; o > 0; o >>= 1) gp += __shfl_xor(gp, o);
+#pragma unroll
+  for (uint32_t s = 0; s < kSpw; ++s) {
+    const uint32_t seg = seg0 + s;
+    if (seg >= a.n_segs) break;
+    const uint32_t off = gp + o1[s];
+    if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c[s];
+    const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const uint32_t j = lane + 64u * k;
+      if (j < c[s]) store_out<kPacked>(a, off + j, base + r[s][k].x, r[s][k].y);
+    }
+    const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
+    for (uint32_t j = lane + 64u * kPre; j < c[s]; j += 64) {
+      const uint2 x = rec_at<kRec>(sp, j);
+      store_out<kPacked>(a, off + j, base + x.x, x.y);
+    }
+  }
+}
+
+// The 2-byte hand-back (kwk_fired_compact_packed16): the 1-byte sweep's <= 4-stage records
+// {LDS offset: 11, stage: 2, flags: 3} copied as they are into one dense list at their segment's
+// offset; the host maps a record to its slot with its segment's region (KWK_FIRED16_SLOT)
+template <uint32_t kSpw>
+__global__ __launch_bounds__(kBlock) void compact16_kernel(CompactArgs a) {
+  static_assert(kScanGroup % (kSpw * kWavesPerBlock) == 0, "a wave's segments lie in one scan group");
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t seg0 = (blockIdx.x * kWavesPerBlock + wave) * kSpw;
+  if (seg0 >= a.n_segs) return;
+  uint32_t c[kSpw], o1[kSpw];
+  uint16_t r[kSpw][4];
+#pragma unroll
+  for (uint32_t s = 0; s < kSpw; ++s) {
+    const uint32_t seg = seg0 + s < a.n_segs ? seg0 + s : seg0;
+    const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) r[s][k] = sp[lane + 64u * k];
+    c[s] = seg0 + s < a.n_segs ? a.counts[seg] : 0u;
+    o1[s] = a.offsets[1 + seg];
+  }
+  uint32_t gp = 0;
+  for (uint32_t g = lane; g < seg0 / kScanGroup; g += 64) gp += a.group_tot[g];
+  for (int o = 32; o > 0; o >>= 1) gp += __shfl_xor(gp, o);
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+#pragma unroll
+  for (uint32_t s = 0; s < kSpw; ++s) {
+    const uint32_t seg = seg0 + s;
+    if (seg >= a.n_segs) break;
+    const uint32_t off = gp + o1[s];
+    if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c[s];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (lane + 64u * k < c[s]) __builtin_nontemporal_store(r[s][k], out + off + lane + 64u * k);
+    const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+    for (uint32_t j = lane + 256u; j < c[s]; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
   }
 }
 
@@ -3737,6 +3791,7 @@ struct kwk_engine {
   int last_rec = 0;                // record kind of the last sweep's segments (kRecSlot / kRecId8 / kRecId8Half)
   bool compacted = false;     // the last sweep's fired list is compacted on the device
   bool compacted_packed = false;  // ... as 4-byte packed records (kwk_fired_compact_packed)
+  bool compacted_16 = false;      // ... as the 1-byte sweep's 2-byte records (kwk_fired_compact_packed16)
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
@@ -4973,10 +5028,15 @@ kwk_status kwk_sync(kwk_engine* e) {
 
 // fired hand-back on the device: per-(tile, wave) counts -> exclusive scan -> dense list in
 // d_compact, total at d_wave_offsets[n_waves] (enqueue only)
-static kwk_status enqueue_compact(kwk_engine* e, bool packed = false) {
+// mode: 0 kwk_fired_rec, 1 packed 4-byte records, 2 the 2-byte records where the sweep wrote them
+// (else the 4-byte packed ones)
+static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (mode == 2 && e->last_rec != kRecId8Half) mode = 1;
+  const bool packed = mode == 1;
   e->compacted = true;
   e->compacted_packed = packed;
+  e->compacted_16 = mode == 2;
   if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
     HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), e->stream));
     return KWK_OK;
@@ -4993,7 +5053,7 @@ static kwk_status enqueue_compact(kwk_engine* e, bool packed = false) {
   a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
   const int rk = e->last_rec;
-  if (e->compact_lb) {  // one pass: the offsets by decoupled look-back
+  if (mode != 2 && e->compact_lb) {  // one pass: the offsets by decoupled look-back
     if (++e->lb_epoch >= (1u << 24)) e->lb_epoch = 1;
     unsigned long long* st = e->d_lb_status;
     uint32_t ep = e->lb_epoch;
@@ -5009,7 +5069,7 @@ static kwk_status enqueue_compact(kwk_engine* e, bool packed = false) {
     return KWK_OK;
   }
   void* args[] = {&a};
-  if (n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
+  if (mode != 2 && n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
     const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half, true>
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8, true>
                                                 : (const void*)compact_small_kernel<kRecSlot, true>)
@@ -5021,13 +5081,21 @@ static kwk_status enqueue_compact(kwk_engine* e, bool packed = false) {
   }
   hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
                      e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
-  const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, true>
-                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, true>
-                                              : (const void*)compact_kernel<kRecSlot, true>)
-                         : (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half>
-                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8>
-                                              : (const void*)compact_kernel<kRecSlot>);
-  HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
+  constexpr uint32_t W = kCompactSpw;
+  if (mode == 2) {
+    hipLaunchKernelGGL(compact16_kernel<W>, dim3((n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock)), dim3(kBlock),
+                       0, e->stream, a);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
+  const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, true, W>
+                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, true, W>
+                                              : (const void*)compact_kernel<kRecSlot, true, W>)
+                         : (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, false, W>
+                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, false, W>
+                                              : (const void*)compact_kernel<kRecSlot, false, W>);
+  const uint32_t eblocks = (n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock);
+  HIP_TRY(hipLaunchKernel(k, dim3(eblocks), dim3(kBlock), args, 0, e->stream));
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
@@ -5081,11 +5149,50 @@ kwk_status kwk_fired_packed(kwk_engine* e, uint32_t* out, uint32_t cap, uint32_t
   return KWK_OK;
 }
 
+static int compact_mode(uint32_t compact) {
+  return compact == KWK_COMPACT_PACKED16 ? 2 : compact == KWK_COMPACT_PACKED ? 1 : 0;
+}
+
+kwk_status kwk_fired_compact_packed16(kwk_engine* e) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  return enqueue_compact(e, 2);
+}
+
+kwk_status kwk_fired_packed16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32_t* n_out, uint32_t* seg_counts,
+                              uint32_t seg_cap, uint32_t* n_segs, uint32_t* region_slots) {
+  ErrScope es_(e);
+  if (!e || !n_out || !n_segs || !region_slots) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  *n_segs = n_waves;
+  *region_slots = 64u * e->last_objs << e->last_region_shift;
+  if (n_waves == 0) { *n_out = 0; return KWK_OK; }
+  if (!e->compacted || !e->compacted_16) {
+    if (e->last_rec != kRecId8Half)
+      return fail(KWK_ESTATE, "2-byte records are the 1-byte sweep's with at most 4 stages: use kwk_fired_packed");
+    if (kwk_status st = enqueue_compact(e, 2)) return st;
+  }
+  uint32_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_out = total;
+  if (!out && !seg_counts) return KWK_OK;
+  if (out && total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
+  if (seg_counts && n_waves > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(n_waves));
+  if (out && total) HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, e->stream));
+  if (seg_counts)
+    HIP_TRY(hipMemcpyAsync(seg_counts, e->d_wave_counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
   ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
-  if (compact == KWK_COMPACT_PACKED)
+  if (compact == KWK_COMPACT_PACKED || compact == KWK_COMPACT_PACKED16)
     if (kwk_status st = packed_ok(e)) return st;
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n; ++k) {
@@ -5097,7 +5204,7 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
     if (ev)
       if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
     if (compact)
-      if (kwk_status st = enqueue_compact(e, compact == KWK_COMPACT_PACKED)) return st;
+      if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
   }
   return KWK_OK;
 }
@@ -5108,7 +5215,7 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
   if (!e || !other) return fail(KWK_EINVAL, "null engine");
   if (e == other) return fail(KWK_EINVAL, "the two engines must differ");
   if (e->device != other->device) return fail(KWK_EINVAL, "the two engines are on different devices");
-  if (compact == KWK_COMPACT_PACKED) {
+  if (compact == KWK_COMPACT_PACKED || compact == KWK_COMPACT_PACKED16) {
     if (kwk_status st = packed_ok(e)) return st;
     if (other->capacity > kPackedSlots) return fail(KWK_ECAP, "packed fired records hold 27-bit slots: other engine > 2^27");
   }
@@ -5123,11 +5230,11 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
     if (ev)
       if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
     if (compact)
-      if (kwk_status st = enqueue_compact(e, compact == KWK_COMPACT_PACKED)) return st;
+      if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
     // the other engine's step right behind (its own stream): both chains start together
     if (kwk_status st = launch_sweep(other, now, seed, step0 + k, true)) return st;
     if (compact)
-      if (kwk_status st = enqueue_compact(other, compact == KWK_COMPACT_PACKED)) return st;
+      if (kwk_status st = enqueue_compact(other, compact_mode(compact))) return st;
   }
   return KWK_OK;
 }
@@ -5135,7 +5242,7 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
 kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
   ErrScope es_(e);
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
-  if (!e->compacted || e->compacted_packed) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
+  if (!e->compacted || e->compacted_packed || e->compacted_16) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
   *recs = e->d_compact;
   *count = e->d_wave_offsets;
   return KWK_OK;
@@ -5147,7 +5254,7 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (kwk_status st = set_dev(e)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
-  if (!e->compacted || e->compacted_packed)  // the segments are intact: expand them as kwk_fired_rec
+  if (!e->compacted || e->compacted_packed || e->compacted_16)  // the segments are intact: expand them as kwk_fired_rec
     if (kwk_status st = enqueue_compact(e)) return st;
   uint32_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));

@@ -170,11 +170,13 @@ EXPORTS = [
     "kwk_alloc_host", "kwk_free_host", "kwk_replace", "kwk_usage_mixed", "kwk_usage_read_containers",
     "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
-    "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device",
+    "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
+    "kwk_fired_packed16",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
 COMPACT_PACKED = 2  # kwk_step_n compact = KWK_COMPACT_PACKED
+COMPACT_PACKED16 = 3  # kwk_step_n compact = KWK_COMPACT_PACKED16 (2-byte records where the sweep has them)
 AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
 
 _lib = None
@@ -230,6 +232,9 @@ def lib():
     L.kwk_fired_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_fired_compact_packed.argtypes = [C.c_void_p]
     L.kwk_fired_packed.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_fired_compact_packed16.argtypes = [C.c_void_p]
+    L.kwk_fired_packed16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32), C.c_void_p, C.c_uint32,
+                                     _p(C.c_uint32), _p(C.c_uint32)]
     L.kwk_fired_packed_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
@@ -283,3 +288,16 @@ def check(status: int, what: str = "", eng=None):
 
 def ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def fired16_decode(recs: np.ndarray, seg_counts: np.ndarray, region_slots: int):
+    """(slot, stage, flags) arrays of a kwk_fired_packed16 list (KWK_FIRED16_* in kwok_engine.h)."""
+    r = recs.astype(np.uint32)
+    x = r & np.uint32(0x7FF)
+    jj = x >> np.uint32(8)
+    lane = ((x >> np.uint32(2)) & np.uint32(63)) ^ jj
+    within = (jj >> np.uint32(2)) * np.uint32(1024) + lane * np.uint32(16) + (jj & np.uint32(3)) * np.uint32(4) + \
+        (x & np.uint32(3))
+    seg = np.repeat(np.arange(len(seg_counts), dtype=np.int64), seg_counts.astype(np.int64))
+    slot = seg * int(region_slots) + within.astype(np.int64)
+    return slot, (r >> np.uint32(11)) & np.uint32(3), (r >> np.uint32(13)) & np.uint32(7)

@@ -132,6 +132,14 @@ class PinnedBuffer:
             pass
 
 
+def _compact_code(compact) -> int:
+    if compact == "packed16":
+        return abi.COMPACT_PACKED16
+    if compact == "packed":
+        return abi.COMPACT_PACKED
+    return 1 if compact else 0
+
+
 class Engine:
     """One kwk_engine (C ABI) for one KindProgram."""
 
@@ -240,20 +248,24 @@ class Engine:
     def step_n(self, n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact=True, ev_every: int = 0,
                ev_j0: int = 0):
         """kwk_step_n: n steps (+ device compaction after each) enqueued by one call; compact =
-        True (kwk_fired_rec), "packed" (4-byte records) or False."""
-        c = abi.COMPACT_PACKED if compact == "packed" else (1 if compact else 0)
+        True (kwk_fired_rec), "packed" (4-byte records), "packed16" (2-byte records where the sweep
+        has them, else 4-byte) or False."""
+        c = _compact_code(compact)
         self._check(abi.lib().kwk_step_n(self.h, n, now0_ns, dt_ns, seed, step0, c, ev_every, ev_j0), "kwk_step_n")
 
     def step_n_pair(self, other: "Engine", n: int, now0_ns: int, dt_ns: int, seed: int, step0: int, compact=True,
                     ev_every: int = 0, ev_j0: int = 0):
         """kwk_step_n_pair: this engine's and `other`'s steps enqueued in turn, step by step."""
-        c = abi.COMPACT_PACKED if compact == "packed" else (1 if compact else 0)
+        c = _compact_code(compact)
         self._check(abi.lib().kwk_step_n_pair(self.h, other.h, n, now0_ns, dt_ns, seed, step0, c, ev_every, ev_j0),
                     "kwk_step_n_pair")
 
-    def fired_compact(self, packed: bool = False):
-        """kwk_fired_compact (/ _packed): the last step's fired list compacted on the device (enqueue only)."""
-        if packed:
+    def fired_compact(self, packed=False):
+        """kwk_fired_compact (/ _packed, packed = True; / _packed16, packed = "16"): the last step's fired
+        list compacted on the device (enqueue only)."""
+        if packed == "16":
+            self._check(abi.lib().kwk_fired_compact_packed16(self.h), "kwk_fired_compact_packed16")
+        elif packed:
             self._check(abi.lib().kwk_fired_compact_packed(self.h), "kwk_fired_compact_packed")
         else:
             self._check(abi.lib().kwk_fired_compact(self.h), "kwk_fired_compact")
@@ -268,6 +280,23 @@ class Engine:
         if n.value:
             self._check(L.kwk_fired_packed(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_packed")
         return out
+
+    def fired_packed16(self, pinned=None):
+        """The last step's list as 2-byte records (kwk_fired_packed16) -> (records u16, records per
+        segment u32, region_slots); abi.EngineError (KWK_ESTATE) when the sweep has no 2-byte records.
+        pinned: (PinnedBuffer for the records, PinnedBuffer for the counts)."""
+        n, ns, rs = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        L = abi.lib()
+        self._check(L.kwk_fired_packed16(self.h, None, 0, C.byref(n), None, 0, C.byref(ns), C.byref(rs)),
+                    "kwk_fired_packed16")
+        if pinned is not None:
+            out, cnt = pinned[0].array(np.uint16, n.value), pinned[1].array(np.uint32, ns.value)
+        else:
+            out, cnt = np.zeros(n.value, dtype=np.uint16), np.zeros(ns.value, dtype=np.uint32)
+        self._check(L.kwk_fired_packed16(self.h, abi.ptr(out) if n.value else None, n.value, C.byref(n),
+                                         abi.ptr(cnt) if ns.value else None, ns.value, C.byref(ns), C.byref(rs)),
+                    "kwk_fired_packed16")
+        return out, cnt, int(rs.value)
 
     def set_tuning(self, key: int, value: int):
         """kwk_set_tuning: an explicit kernel choice (abi.TUNE_*)."""

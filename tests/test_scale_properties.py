@@ -155,7 +155,9 @@ def test_packed_handback_equals_records_at_4m_pods(state):
     compaction paths (look-back, one launch at <= 8192 segments, the scan + expansion pair above): the same
     (slot, stage) sequence; kwk_fired after a packed compaction re-expands the full records
     (flags included); kwk_step_n with KWK_COMPACT_PACKED leaves the same packed list as the
-    per-step calls.  1-byte ids (sweep8), 2-byte words, fused 8-byte records (C2 mix)."""
+    per-step calls.  1-byte ids (sweep8), 2-byte words, fused 8-byte records (C2 mix).  The 2-byte
+    hand-back (kwk_fired_packed16) of the 1-byte sweep decodes to the same (slot, stage, flags); the
+    other formats refuse it."""
     from kwok_amd.host import abi
     if state == "dw":
         from kwok_amd import workload as W
@@ -188,12 +190,31 @@ def test_packed_handback_equals_records_at_4m_pods(state):
                 assert len(pk) == len(full) > 0, (k, small)
                 assert np.array_equal(pk & np.uint32(0x7FFFFFF), full["slot"]), (k, small)
                 assert np.array_equal(pk >> np.uint32(27), full["stage"].astype(np.uint32)), (k, small)
+            # the 2-byte records (1-byte sweep, <= 4 stages): same slots, stages and flags
+            if state == "auto":
+                eng.fired_compact("16")
+                recs, cnt, rs = eng.fired_packed16()
+                full = eng.fired()
+                sl, sg, fl = abi.fired16_decode(recs, cnt, rs)
+                assert len(recs) == len(full) and int(cnt.sum()) == len(full), k
+                assert np.array_equal(sl, full["slot"].astype(np.int64)), k
+                assert np.array_equal(sg, full["stage"].astype(np.uint32)), k
+                assert np.array_equal(fl, full["flags"].astype(np.uint32)), k
+            else:
+                with pytest.raises(abi.EngineError):
+                    eng.fired_packed16()
         _handback_path(eng, HANDBACK_PATHS[0])
         ref = eng.fired_packed()
         eng.step_n(1, now0 + 4 * dt, dt, 0x6B776F6B, 4, "packed")
         a = eng.fired_packed()
         eng2_full = eng.fired()
         assert np.array_equal(a & np.uint32(0x7FFFFFF), eng2_full["slot"]) and len(a) > 0 and len(ref) > 0
+        if state == "auto":  # kwk_step_n leaves the 2-byte list itself
+            eng.step_n(1, now0 + 5 * dt, dt, 0x6B776F6B, 5, "packed16")
+            recs, cnt, rs = eng.fired_packed16()
+            full = eng.fired()
+            sl, sg, _ = abi.fired16_decode(recs, cnt, rs)
+            assert len(recs) > 0 and np.array_equal(sl, full["slot"].astype(np.int64))
     finally:
         eng.close()
 
