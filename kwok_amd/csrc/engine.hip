@@ -2246,6 +2246,34 @@ __global__ __launch_bounds__(kBlock) void compact16_kernel(CompactArgs a) {
   }
 }
 
+// the 2-byte hand-back in one launch for small sweeps (as compact_small_kernel below)
+__global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  __shared__ uint32_t s_seg[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t first = blockIdx.x * kSegsPerBlock;
+  const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(a.counts);
+  uint32_t sum = 0;
+#pragma unroll 8
+  for (uint32_t q = threadIdx.x; q < first / 4u; q += kBlock) {
+    const uint4 v = c4[q];
+    sum += (v.x + v.y) + (v.z + v.w);
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) s_part[wave] = sum;
+  if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < a.n_segs ? a.counts[first + threadIdx.x] : 0u;
+  __syncthreads();
+  const uint32_t seg = first + wave;
+  if (seg >= a.n_segs) return;
+  uint32_t off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
+  const uint32_t c = s_seg[wave];
+  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
+  const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
+}
+
 // Hand-back in one launch for small sweeps (at most kwk_engine::compact_small segments, 8192 by default: the node kinds, the
 // strong-scaling shards): each block sums the counts of every segment before its own (at most
 // 32 KB, L2-resident) instead of waiting for seg_scan_kernel, then expands its four segments as
@@ -5069,6 +5097,11 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
     return KWK_OK;
   }
   void* args[] = {&a};
+  if (mode == 2 && !e->compact_lb && n_waves <= e->compact_small) {
+    hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
   if (mode != 2 && n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
     const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half, true>
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8, true>
