@@ -81,9 +81,11 @@ typedef struct {
 
 #define KWK_EMIT_FROM_RECORDS 0u /* kwk_fired_device's list (kwk_fired_compact) */
 #define KWK_EMIT_FROM_PACKED 1u  /* kwk_fired_packed_device's list (kwk_fired_compact_packed) */
-#define KWK_EMIT_BYTE_STORES (1u << 8) /* or-ed into source: write the bytes straight to global memory, one
-                                          byte store per lane (diagnostic: the default stages each wave's
-                                          span in LDS and stores whole 16-byte chunks) */
+/* or-ed into source (diagnostics; the default: each record written by one lane, 16 bytes per store):
+ * one wave per record, 64 lanes per literal run, straight to global memory one byte per lane / through
+ * an LDS window of the wave's records leaving as 16-byte stores */
+#define KWK_EMIT_BYTE_STORES (1u << 8)
+#define KWK_EMIT_WAVE_WINDOW (1u << 9)
 
 const char* kwk_emit_last_error(const kwk_emitter* em);
 /* an emitter for `eng`'s fired lists over slots [0, capacity), on the engine's stream */

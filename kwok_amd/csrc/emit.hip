@@ -195,6 +195,51 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, con
   return s;
 }
 
+// one lane's output stream (a record written by the thread that sized it): byte stores up to the
+// first 16-byte boundary, then 16 bytes gathered in registers per store, the tail as bytes
+struct LaneOut {
+  char* out;
+  unsigned long long g;
+  uint64_t lo = 0, hi = 0;
+  uint32_t n = 0;
+  __device__ __forceinline__ void put(uint8_t c) {
+    if (n == 0 && (g & 15u)) {
+      out[g++] = (char)c;
+      return;
+    }
+    if (n < 8u) lo |= (uint64_t)c << (8u * n);
+    else hi |= (uint64_t)c << (8u * (n - 8u));
+    ++n;
+    ++g;
+    if (n == 16u) {
+      *reinterpret_cast<uint4*>(out + g - 16u) =
+          make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      n = 0;
+      lo = hi = 0;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    for (uint32_t k = 0; k < n; ++k) out[g - n + k] = (char)((k < 8u ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xFFu);
+  }
+};
+
+// one emitted item by one lane (the lane-per-record writer)
+__device__ __forceinline__ void lane_skel(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S, uint32_t slot,
+                                          const char* s_now, const Vals& V, LaneOut& o) {
+  for (uint32_t q = 0; q < S.n_pieces; ++q) {
+    const kwk_emit_piece P = T.pieces[S.first_piece + q];
+    const char* src = T.lits + P.lit_off;
+    for (uint32_t k = 0; k < P.lit_len; ++k) o.put((uint8_t)src[k]);
+    if (P.slot == 0) {
+      for (uint32_t k = 0; k < a.now_len; ++k) o.put((uint8_t)s_now[k]);
+    } else if (P.slot != KWK_EMIT_NO_SLOT) {
+      const uint8_t* v = V.row(a, P.slot - 1u, slot);
+      const uint32_t len = v[0];
+      for (uint32_t k = 0; k < len; ++k) o.put(v[1 + k]);
+    }
+  }
+}
+
 // the bytes of one emitted item: put(global position, byte) for each, 64 lanes per run (a value's
 // length and bytes are loaded together); returns the position after them
 template <typename Put>
@@ -357,10 +402,15 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
-// kLds: the skeleton tables and the records' call-value rows (at most kLdsCols columns of 16
-// bytes) staged in LDS
-template <bool kStaged, bool kLds>
+// kMode: kWriteLane (default) — each thread writes the record it sized, 16-byte stores from
+// registers; kWriteWindow — each wave writes its 64 records' contiguous span, 64 lanes per literal
+// run, through an LDS window leaving as 16-byte stores; kWriteBytes — the same straight to global
+// memory, one byte store per lane.  kLds: the skeleton tables and the records' call-value rows (at
+// most kLdsCols columns of 16 bytes) staged in LDS
+constexpr int kWriteBytes = 0, kWriteWindow = 1, kWriteLane = 2;
+template <int kMode, bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
+  constexpr bool kStaged = kMode == kWriteWindow;
   __shared__ __attribute__((aligned(16))) char s_buf[kStaged ? kWaves * kStageBytes : 16];
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
@@ -440,6 +490,18 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           ++n_sk;
         }
       }
+      if constexpr (kMode == kWriteLane) {  // this thread writes the record it just sized
+        if (n_sk) {
+          LaneOut o{a.out, s_base[lr]};
+          if (n_sk <= kRecSk) {
+            for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
+          } else {
+            for (uint32_t j = t0; j < t1; ++j)
+              if ((sz.ok >> (j - t0)) & 1u) lane_skel(a, T, skels[skel_index(a, w, a.p.stage_tpl[j])], x.slot, s_now, V, o);
+          }
+          o.finish();
+        }
+      }
       // the object's guard bits after the patches (all items emitted here; else the host sets them)
       const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
       if (x.valid && sz.ok == all) {
@@ -454,7 +516,9 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     // bytes: wave `wave` writes records [wave * 64, wave * 64 + 64) of the tile, whose output is
     // one contiguous span, 64 lanes per literal run / value
     const uint32_t r0 = wave * kWaveRecs, r1 = r0 + kWaveRecs;
-    if constexpr (!kStaged) {
+    if constexpr (kMode == kWriteLane) {
+      // written above
+    } else if constexpr (!kStaged) {
       for (uint32_t q = r0; q < r1; ++q) {
         const uint32_t meta = s_meta[q];
         const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu, n_sk = meta >> 24;
@@ -786,10 +850,12 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
-  const bool bytes = (source & KWK_EMIT_BYTE_STORES) != 0;
+  const int mode = (source & KWK_EMIT_BYTE_STORES) ? kWriteBytes : (source & KWK_EMIT_WAVE_WINDOW) ? kWriteWindow
+                                                                                                 : kWriteLane;
   const bool wl = lds && vals16;  // the write kernel's LDS path also stages the value rows
-  const void* wk = bytes ? (wl ? (const void*)emit_write_kernel<false, true> : (const void*)emit_write_kernel<false, false>)
-                         : (wl ? (const void*)emit_write_kernel<true, true> : (const void*)emit_write_kernel<true, false>);
+#define WK(M) (wl ? (const void*)emit_write_kernel<M, true> : (const void*)emit_write_kernel<M, false>)
+  const void* wk = mode == kWriteBytes ? WK(kWriteBytes) : mode == kWriteWindow ? WK(kWriteWindow) : WK(kWriteLane);
+#undef WK
   void* wargs[] = {&a};
   HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());
