@@ -2886,64 +2886,6 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
   }
 }
 
-// The C5 layout — every node holds the same number of pods, in node order (node_ptr[j] =
-// j * ppn, ppn a multiple of 4), 1-byte ids and the 1-byte key column — takes
-// usage_uniform_kernel: one thread per node summing its ppn pods in order from dword-aligned
-// 16-byte loads, no chunk descriptors, no node-boundary search, no segmented scan
-// (usage_fast_kernel: 108-150 us at C5, VALU- and latency-bound on the scan)
-__global__ __launch_bounds__(kBlock) void usage_uniform_kernel(UsageArgs a, uint32_t ppn, uint32_t n_nodes) {
-  __shared__ double2 s_kv[kUKeyDict];
-  __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
-  for (uint32_t j = threadIdx.x; j < a.kv_n; j += kBlock) s_kv[j] = a.kv[j];
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods);
-  const __amdgpu_buffer_rsrc_t uk_rs = make_rsrc(a.ukey8, a.n_pods);
-  double tot_c = 0.0, tot_m = 0.0;
-  for (uint32_t node = blockIdx.x * kBlock + threadIdx.x; node < n_nodes; node += gridDim.x * kBlock) {
-    const uint32_t p0 = node * ppn;
-    double c = 0.0, m = 0.0;
-    for (uint32_t i = 0; i < ppn; i += 16u) {
-      const auto sv = __builtin_amdgcn_raw_buffer_load_b128(st_rs, p0 + i, 0, 0);
-      const auto kq = __builtin_amdgcn_raw_buffer_load_b128(uk_rs, p0 + i, 0, 0);
-#pragma unroll
-      for (uint32_t b = 0; b < 16u; ++b) {
-        const uint32_t id = (sv[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
-        const uint32_t key = (kq[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
-        const bool live = i + b < ppn && (id & kIdAlive) != 0;
-        const double2 v = s_kv[key];
-        c += live ? v.x : 0.0;
-        m += live ? v.y : 0.0;
-      }
-    }
-    // NodeResourceUsage (:195-224) and its integrator (nodeResourceCumulativeUsage, :67-109)
-    double2 cm = reinterpret_cast<const double2*>(a.cum)[node];
-    const int64_t lt = a.last_t[node];
-    if (lt != INT64_MIN) {
-      const double dt = dur_seconds(a.now - lt);
-      cm.x += dt * c;
-      cm.y += dt * m;
-      reinterpret_cast<double2*>(a.cum)[node] = cm;
-    }
-    a.last_t[node] = a.now;
-    reinterpret_cast<double4*>(a.node_out)[node] = make_double4(c, m, cm.x, cm.y);
-    tot_c += c;
-    tot_m += m;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    tot_c += __shfl_xor(tot_c, o);
-    tot_m += __shfl_xor(tot_m, o);
-  }
-  if (lane == 0) { s_c[wave] = tot_c; s_m[wave] = tot_m; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tc = 0, tm = 0;
-    for (int i = 0; i < kWavesPerBlock; ++i) { tc += s_c[i]; tm += s_m[i]; }
-    a.block_part[blockIdx.x * 2 + 0] = tc;
-    a.block_part[blockIdx.x * 2 + 1] = tm;
-  }
-}
-
 // The common configuration — every pod's containers evaluate alike (no mixed table) and no
 // per-pod outputs — takes usage_fast_kernel: the same chunks, lanes and scan, but a pod's value
 // is one LDS lookup in `podv` (containers x value, summed on the host in spec order exactly as
@@ -3892,8 +3834,6 @@ struct kwk_engine {
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
-  uint32_t usage_ppn = 0;     // node_ptr[j] = j * usage_ppn for every node (usage_uniform_kernel), else 0
-  bool usage_uniform = true;  // KWK_TUNE_USAGE_UNIFORM
   uint32_t sweep_blocks = 0;  // persistent 2-byte sweep: resident blocks per CU (0: the occupancy)
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
@@ -4642,10 +4582,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
-      return KWK_OK;
-    case KWK_TUNE_USAGE_UNIFORM:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_UNIFORM: 0 or 1");
-      e->usage_uniform = value != 0;
       return KWK_OK;
     case KWK_TUNE_COMPACT_LB:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_LB: 0 or 1");
@@ -5433,12 +5369,6 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
     if (node_ptr[j + 1] < node_ptr[j]) return fail(KWK_EINVAL, "node_ptr must be non-decreasing");
   const uint32_t n_pods = node_ptr[n_nodes];
   if (n_pods > e->capacity) return fail(KWK_ECAP, "node_ptr covers more pods than capacity");
-  {  // the uniform layout of usage_uniform_kernel: node j's pods are [j * ppn, (j + 1) * ppn)
-    const uint32_t ppn = n_nodes ? node_ptr[1] : 0u;
-    bool uni = ppn > 0 && ppn % 4u == 0 && ppn <= 4096u;
-    for (uint32_t j = 0; uni && j <= n_nodes; ++j) uni = node_ptr[j] == (uint64_t)j * ppn;
-    e->usage_ppn = uni ? ppn : 0u;
-  }
   bool mixed_keys = false;
   for (uint32_t p = 0; p < n_pods; ++p) {
     if ((ukey[p] >> 28) == 0) {  // containers differ: index into kwk_usage_mixed's table
@@ -5961,13 +5891,6 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
                               : wb == 4 ? (const void*)K<4 __VA_ARGS__> : (const void*)K<8 __VA_ARGS__>)
   if (!e->has_mixed_keys && !e->d_pod_out && e->podv_n) {  // usage_fast_kernel
     const bool k8 = e->d_ukey8 != nullptr && e->usage_key8;
-    if (k8 && wb == 1 && e->usage_ppn && e->usage_uniform) {  // usage_uniform_kernel
-      const uint32_t grid = std::min((e->n_nodes + kBlock - 1) / kBlock, ublocks);
-      hipLaunchKernelGGL(usage_uniform_kernel, dim3(grid), dim3(kBlock), 0, e->stream, ua, e->usage_ppn, e->n_nodes);
-      hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
-      HIP_TRY(hipGetLastError());
-      return KWK_OK;
-    }
     const void* fk = k8 ? USAGE_KERNEL(usage_fast_kernel, , true) : USAGE_KERNEL(usage_fast_kernel);
     uint32_t grid = persist_grid(e, fk, ublocks);
     if (e->usage_blocks) grid = std::min(ublocks, (uint32_t)e->n_cus * e->usage_blocks);

@@ -336,57 +336,3 @@ def test_gpu_usage_key8_column_matches_4byte_keys(state):
     np.testing.assert_allclose(node[:, 2:], 2.0 * want, rtol=REL_TOL, atol=0)
     np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("ppn", [100, 12])
-def test_gpu_usage_uniform_layout_matches_chunked_kernel(ppn):
-    """The C5 layout (every node ppn pods in node order, 1-byte ids and keys) takes
-    usage_uniform_kernel: node sums, integrators and totals equal the chunked usage_fast_kernel's
-    (KWK_TUNE_USAGE_UNIFORM 0) within the usage tolerance, and numpy's."""
-    from kwok_amd.host import abi
-    from kwok_amd.host.compiler import KindProgram
-    from kwok_amd.host.engine import Engine, Ingest
-    from kwok_amd.host.stages import load_stage_files
-
-    cl, pods = _cluster(n_nodes=40, n_pods=6000, seed=31)
-    n_nodes = len(pods) // ppn
-    n = n_nodes * ppn
-    pods = pods[:n]
-    ptr = (np.arange(n_nodes + 1) * ppn).astype(np.uint32)
-    rng = np.random.default_rng(5)
-    cv, mv = rng.random(30) * 4, rng.random(30) * 2**32
-    ci, mi, nc = rng.integers(0, 30, 50), rng.integers(0, 30, 50), rng.integers(1, 6, 50)
-    dict_keys = (ci | (mi << 14) | (nc << 28)).astype(np.uint32)
-    pick = rng.integers(0, 50, n)
-    keys = dict_keys[pick]
-    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
-    kp.explore(pods)
-    ing = Ingest(kp)
-    cols = ing.columns(pods)
-    gone = np.arange(3, n, 13)
-    alive = np.ones(n, dtype=bool)
-    alive[gone] = False
-    t0 = 1_700_000_000 * 10**9
-    got = {}
-    for uni in (1, 0):
-        eng = Engine(kp, capacity=n)
-        try:
-            eng.set_tuning(abi.TUNE_USAGE_UNIFORM, uni)
-            eng.load_stages()
-            eng.load(*cols, ing.record_array())
-            eng.usage_config(ptr, keys, cv, mv)
-            eng.delete(gone)
-            eng.usage(t0)
-            eng.usage(t0 + 3 * 10**9)
-            got[uni] = eng.usage_read()
-        finally:
-            eng.close()
-    np.testing.assert_allclose(got[1][0], got[0][0], rtol=REL_TOL, atol=0)
-    np.testing.assert_allclose(got[1][1], got[0][1], rtol=REL_TOL)
-    node, total = got[1]
-    pod_c = np.where(alive, nc[pick] * cv[ci[pick]], 0.0)
-    pod_m = np.where(alive, nc[pick] * mv[mi[pick]], 0.0)
-    want = np.stack([pod_c.reshape(n_nodes, ppn).sum(axis=1), pod_m.reshape(n_nodes, ppn).sum(axis=1)], axis=1)
-    np.testing.assert_allclose(node[:, :2], want, rtol=REL_TOL, atol=0)
-    np.testing.assert_allclose(node[:, 2:], 3.0 * want, rtol=REL_TOL, atol=0)
-    np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)

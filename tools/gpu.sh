@@ -94,6 +94,16 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
           python -c "import json; d=json.load(open('$O/st_${l}_$i.json')); print('$l', $i, d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'])"
         done
       done ;;
+    ab2)  # same-box A/B of C5 bench variants by flags, alternating x2: "<label>:<bench args>;..."
+      IFS=';' read -ra V <<< "$arg"
+      for i in 1 2; do
+        for v in "${V[@]}"; do
+          l=${v%%:*}; x=${v#*:}
+          timeout -k 10 200 python -u bench.py $B1 --no-pmc --no-cpu-baseline --hbm-nodes 0 --pcie-steps 0 --emit-steps 0 $x \
+            > $O/ab_${l}_$i.json 2> $O/ab_${l}_$i.err || { tail -20 $O/ab_${l}_$i.err; exit 1; }
+          python -c "import json; d=json.load(open('$O/ab_${l}_$i.json')); print('$l', $i, d['value'], 'ms/step', d['ms_per_step'], 'sweep us', d['detail']['pod_sweep_us_mean'])"
+        done
+      done ;;
     dist)
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 \
         bench.py --gpus 2 --steps 6 --warmup 2 --nodes 200000 --dist-backend gloo --no-cpu-baseline --no-pmc --hbm-nodes 0 \
