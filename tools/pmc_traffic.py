@@ -1,4 +1,5 @@
-"""HBM traffic per pod-sweep launch from a tools/gpu_profile.sh run -> profiles/pmc_traffic.json.
+"""HBM traffic per pod-sweep launch from rocprofv3 --pmc passes (bench.py runs them itself as child
+processes; this script summarises such a run) -> profiles/pmc_traffic.json.
 
 FETCH_SIZE / WRITE_SIZE (KiB per dispatch) are summed over the PMC dimensions per dispatch.
 Only the pod engine's sweep launches count: in the churn run they are the harness
