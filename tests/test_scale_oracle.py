@@ -62,19 +62,22 @@ def _rows_at(eng, slots):
     return hot, dels
 
 
-@pytest.mark.parametrize("state", ["auto", "u16"])
+@pytest.mark.parametrize("state", ["auto", "u16", "auto-shard"])
 def test_c5_persistent_table_sweep_sampled_oracle(state):
     """C5 pod shape (pod-fast, 100 pods per node, 10 % Job-owned, harness churn) at the sizes
     where the sweeps run persistent with two tiles in flight: the 1-byte dictionary-id sweep
     (auto: sweep8_kernel, the bench's kernel; 8192-id tiles, 40M pods) and the 2-byte table-only
-    sweep (u16: sweep16_fsm_kernel, 20M pods), every ~10000th / 4999th slot checked each step."""
+    sweep (u16: sweep16_fsm_kernel, 20M pods), every ~10000th / 4999th slot checked each step;
+    auto-shard: the 12.5M-pod shard of N = 8 (1526 tiles: two per workgroup in one round,
+    KWK_TUNE_SWEEP_PAIRS)."""
     from bench import shard_pod_variants
     from kwok_amd import workload as W
     from kwok_amd.host import abi
     from kwok_amd.host.compiler import HarnessSpec, KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
-    n = 40_000_000 if state == "auto" else 20_000_000
+    n = {"auto": 40_000_000, "u16": 20_000_000, "auto-shard": 12_500_000}[state]
+    state = "auto" if state == "auto-shard" else state
     files = W.stage_paths(W.POD_FAST)
     pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
     prog = KindProgram(load_stage_files(*files), HarnessSpec())
