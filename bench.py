@@ -582,8 +582,6 @@ def main():
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
     ap.add_argument("--tune-sweep-blocks", type=int, default=0,
                     help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
-    ap.add_argument("--tune-sweep-pairs", type=int, default=-1,
-                    help="diagnostic: KWK_TUNE_SWEEP_PAIRS for the pod engine (1: two tiles per workgroup at shard sizes)")
     ap.add_argument("--tune-compact-lb", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_LB for both engines (1: one-pass look-back, the default)")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
@@ -670,9 +668,6 @@ def main():
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
-    if args.tune_sweep_pairs >= 0:
-        from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_SWEEP_PAIRS, args.tune_sweep_pairs)
     if args.tune_compact_lb >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_COMPACT_LB, args.tune_compact_lb)

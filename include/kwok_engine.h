@@ -227,9 +227,6 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1, or 0
                                   (default: the scan + expansion pair / the one-launch small compaction above;
                                   the look-back measured 73 us against 27 us at C5) */
-#define KWK_TUNE_SWEEP_PAIRS 12 /* 1-byte sweep with more tiles than one round of resident workgroups but at most
-                                   two: the persistent grid with two tiles per workgroup, 1 (default) or 0 (one tile
-                                   per workgroup, two rounds) */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */

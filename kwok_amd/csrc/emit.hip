@@ -218,6 +218,24 @@ struct LaneOut {
       lo = hi = 0;
     }
   }
+  // `cnt` (<= 4) bytes of w, low byte first: one register insert when they land on a whole dword
+  // of the 16-byte gather
+  __device__ __forceinline__ void put4(uint32_t w, uint32_t cnt) {
+    if (cnt == 4u && (n & 3u) == 0u && !(n == 0u && (g & 15u))) {
+      if (n < 8u) lo |= (uint64_t)w << (8u * n);
+      else hi |= (uint64_t)w << (8u * (n - 8u));
+      n += 4u;
+      g += 4u;
+      if (n == 16u) {
+        *reinterpret_cast<uint4*>(out + g - 16u) =
+            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        n = 0;
+        lo = hi = 0;
+      }
+      return;
+    }
+    for (uint32_t b = 0; b < cnt; ++b) put((uint8_t)(w >> (8u * b)));
+  }
   __device__ __forceinline__ void finish() {
     for (uint32_t k = 0; k < n; ++k) out[g - n + k] = (char)((k < 8u ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xFFu);
   }
@@ -228,8 +246,13 @@ __device__ __forceinline__ void lane_skel(const EmitArgs& a, const Tables& T, co
                                           const char* s_now, const Vals& V, LaneOut& o) {
   for (uint32_t q = 0; q < S.n_pieces; ++q) {
     const kwk_emit_piece P = T.pieces[S.first_piece + q];
-    const char* src = T.lits + P.lit_off;
-    for (uint32_t k = 0; k < P.lit_len; ++k) o.put((uint8_t)src[k]);
+    // the literal as aligned dword pairs (the tables carry 8 bytes of padding): four bytes per step
+    const uint32_t* L = reinterpret_cast<const uint32_t*>(T.lits);
+    for (uint32_t k = 0; k < P.lit_len; k += 4u) {
+      const uint32_t off = P.lit_off + k;
+      const uint64_t both = (uint64_t)L[off >> 2] | (uint64_t)L[(off >> 2) + 1u] << 32;
+      o.put4((uint32_t)(both >> (8u * (off & 3u))), min(4u, (uint32_t)P.lit_len - k));
+    }
     if (P.slot == 0) {
       for (uint32_t k = 0; k < a.now_len; ++k) o.put((uint8_t)s_now[k]);
     } else if (P.slot != KWK_EMIT_NO_SLOT) {
@@ -673,7 +696,11 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
     return st;
   if (kwk_status st = upload(em, const_cast<kwk_emit_skel**>(&em->p.skels), g->skels, g->n_skels)) return st;
   if (kwk_status st = upload(em, const_cast<kwk_emit_piece**>(&em->p.pieces), g->pieces, g->n_pieces)) return st;
-  if (kwk_status st = upload(em, const_cast<char**>(&em->p.lits), g->lits, g->n_lit_bytes)) return st;
+  {  // the literal runs with 16 bytes of zero padding (the writers read aligned dword pairs)
+    std::vector<char> lits(g->lits, g->lits + g->n_lit_bytes);
+    lits.resize(lits.size() + 16, 0);
+    if (kwk_status st = upload(em, const_cast<char**>(&em->p.lits), lits.data(), lits.size())) return st;
+  }
   if (kwk_status st = upload(em, const_cast<uint8_t**>(&em->p.fresh), g->fresh_guards, g->n_classes)) return st;
   em->n_columns = g->n_columns;
   em->stride.assign(g->column_stride, g->column_stride + g->n_columns);
@@ -840,7 +867,7 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   a.now_len = (uint32_t)now.size();
   // the list's count lives on the device: every tile loop reads it; the grid covers the capacity
   HIP_TRY(hipEventRecord(em->ev0, em->stream));
-  bool lds = em->p.n_pieces <= kLdsPieces && em->p.n_lits <= kLdsLits && em->p.n_skels <= kLdsSkels;
+  bool lds = em->p.n_pieces <= kLdsPieces && em->p.n_lits + 8u <= kLdsLits && em->p.n_skels <= kLdsSkels;
   bool vals16 = em->n_columns <= kLdsCols;
   for (uint32_t c = 0; c < em->n_columns; ++c) vals16 = vals16 && em->stride[c] == 16u;
   if (lds)

@@ -3908,7 +3908,6 @@ struct kwk_engine {
   // per workgroup the prefix frontier advances ~64 workgroups per look-back round trip, 73 us at
   // C5 against 27 us for the scan pair (r4d)
   bool compact_lb = false;
-  bool pair_small = true;  // KWK_TUNE_SWEEP_PAIRS: the 1-byte sweep's two-tiles-per-workgroup grid for shard sizes
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)
@@ -4584,10 +4583,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
       return KWK_OK;
-    case KWK_TUNE_SWEEP_PAIRS:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_SWEEP_PAIRS: 0 or 1");
-      e->pair_small = value != 0;
-      return KWK_OK;
     case KWK_TUNE_COMPACT_LB:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_LB: 0 or 1");
       e->compact_lb = value != 0;
@@ -4915,18 +4910,11 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
     if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);
-    // more tiles than one round of resident workgroups but at most two (a strong-scaling shard:
-    // 1526 tiles at 12.5M pods against 1280 resident): every workgroup takes two tiles, the second
-    // prefetched, in one round instead of two rounds of one tile each
-    bool pairs = false;
-    if (e->persist16 && !e->sweep_blocks && e->pair_small && tiles > pg && tiles <= 2 * pg) {
-      pg = (tiles + 1) / 2;
-      pairs = true;
-    }
+
     uint32_t blocks = tiles;
     e->last_sweep = kwk_sweep_info{KWK_SWEEP_8, (uint32_t)kQ8, 0, 1, tiles, tiles, a.harness.enable ? 1u : 0u, 0};
     const void* kern = K8(false, 1);
-    if (2 * pg <= tiles || pairs) {  // else the persistent loop would run about once: one block per tile
+    if (2 * pg <= tiles) {  // else the persistent loop would run about once: one block per tile
       blocks = pg;
       e->last_sweep.persistent = 1;
       e->last_sweep.grid = pg;

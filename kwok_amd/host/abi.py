@@ -98,7 +98,6 @@ TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_COMPACT_LB = 11
-TUNE_SWEEP_PAIRS = 12
 
 
 class Lease(C.Structure):

@@ -68,8 +68,7 @@ def test_c5_persistent_table_sweep_sampled_oracle(state):
     where the sweeps run persistent with two tiles in flight: the 1-byte dictionary-id sweep
     (auto: sweep8_kernel, the bench's kernel; 8192-id tiles, 40M pods) and the 2-byte table-only
     sweep (u16: sweep16_fsm_kernel, 20M pods), every ~10000th / 4999th slot checked each step;
-    auto-shard: the 12.5M-pod shard of N = 8 (1526 tiles: two per workgroup in one round,
-    KWK_TUNE_SWEEP_PAIRS)."""
+    auto-shard: the 12.5M-pod shard of N = 8 (1526 one-tile workgroups)."""
     from bench import shard_pod_variants
     from kwok_amd import workload as W
     from kwok_amd.host import abi
