@@ -583,7 +583,9 @@ def main():
     ap.add_argument("--tune-sweep-blocks", type=int, default=0,
                     help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
     ap.add_argument("--tune-compact-lb", type=int, default=-1,
-                    help="diagnostic: KWK_TUNE_COMPACT_LB for both engines (1: one-pass look-back, the default)")
+                    help="diagnostic: KWK_TUNE_COMPACT_LB for both engines (1: one-pass look-back; default 0)")
+    ap.add_argument("--tune-usage-rows", type=int, default=0,
+                    help="diagnostic: KWK_TUNE_USAGE_ROWS for the pod engine (0: the default, 4 rows per chunk)")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
@@ -655,6 +657,9 @@ def main():
     log(f"rank {rank}: nodes [{nlo}, {nhi}), pods [{nlo * args.pods_per_node}, {nhi * args.pods_per_node})")
     pods, nodes, (pvars, pidx) = build_engines(nlo, nhi, args.pods_per_node, local_rank, args.seed, args.job_frac,
                                                wide_state=args.wide_state)
+    if args.tune_usage_rows:
+        from kwok_amd.host import abi
+        pods.set_tuning(abi.TUNE_USAGE_ROWS, args.tune_usage_rows)
     configure_usage(pods, pvars, pidx, nhi - nlo, args.pods_per_node)
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:

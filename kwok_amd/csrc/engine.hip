@@ -2562,7 +2562,11 @@ __global__ void dw_unfold_kernel(const uint2* __restrict__ st, int64_t* __restri
 // and keeps its integrators (Go keys them by name, so a re-created pod continues them).
 constexpr uint32_t kURun = 16;                  // consecutive pods per lane
 constexpr uint32_t kURow = 64u * kURun;         // slots per wave row
-constexpr uint32_t kUChunkPods = kURow - 8u;    // a chunk fits one row even after rounding its start down to 8
+constexpr uint32_t kUChunkRows = 4;            // rows per chunk (KWK_TUNE_USAGE_ROWS): the per-chunk costs
+                                                // (descriptor, node boundaries, integrators, node stores) spread
+                                                // over up to 4 rows, whose loads run one row ahead
+constexpr uint32_t kUChunkPods = kURow - 8u;    // pods of a one-row chunk: it fits one row even after rounding its
+                                                // start down to 8; an R-row chunk holds R * kURow - 8
 constexpr uint32_t kUChunkNodes = 128;          // nodes per chunk: the wave's LDS copy of node_ptr
 constexpr uint32_t kULdsValues = 512;           // cpu + mem dictionary entries staged in LDS (else read via L1)
 struct UsageArgs {
@@ -2725,7 +2729,6 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the previous chunk is done with sp / ss
     for (uint32_t j = lane; j <= nk; j += 64) sp[j] = a.node_ptr[na + j];
-    if (nxt < a.n_chunks) load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     // a node's sum is final where it closes (in LDS); the integrators and outputs are written
     // after the rows, all lanes at once
@@ -2735,8 +2738,19 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
     }
     double carry_c = 0.0, carry_m = 0.0;  // the open node's sum from earlier rows
     uint32_t carry_k = 0xFFFFFFFFu;
+    if (r_first >= c1)  // no rows (a chunk of empty nodes): the next chunk's first row
+      load_row(nsv, nkv, nch.x & ~7u, nch.x, nxt < a.n_chunks ? nch.y : 0u);
     for (uint32_t r0 = r_first; r0 < c1; r0 += kURow) {  // wave-uniform
-      if (r0 != r_first) load_row(sv, kv, r0, c0, c1);  // nodes larger than a row
+      if (r0 != r_first) {  // the row loaded during the previous one
+#pragma unroll
+        for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) kv[q] = nkv[q];
+      }
+      {  // one row ahead: the chunk's next row, or after its last the next chunk's first
+        const bool more = r0 + kURow < c1;
+        load_row(nsv, nkv, more ? r0 + kURow : nch.x & ~7u, more ? c0 : nch.x, more ? c1 : nxt < a.n_chunks ? nch.y : 0u);
+      }
       const uint32_t lf = r0 + lane * kURun;
       const uint32_t p_lo = max(lf, c0), p_hi = min(lf + kURun, c1);
       const bool has = p_lo < p_hi;
@@ -2983,17 +2997,25 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
 #pragma unroll
     for (uint32_t t = 0; t < 3; ++t)
       if (lane + 64u * t <= nk) sp[lane + 64u * t] = cnp[t];
-    if (nxt < a.n_chunks) {
-      load_row(nsv, nkv, nch.x & ~7u, nch.x, nch.y);
-      load_meta(nch, nnp, npc, npl);
-    }
+    if (nxt < a.n_chunks) load_meta(nch, nnp, npc, npl);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t k = lane; k < nk; k += 64)  // nodes without pods
       if (sp[k] == sp[k + 1]) ss[k] = make_double2(0.0, 0.0);
     double carry_c = 0.0, carry_m = 0.0;
     uint32_t carry_k = 0xFFFFFFFFu;
+    if (r_first >= c1)  // no rows (a chunk of empty nodes): the next chunk's first row
+      load_row(nsv, nkv, nch.x & ~7u, nch.x, nxt < a.n_chunks ? nch.y : 0u);
     for (uint32_t r0 = r_first; r0 < c1; r0 += kURow) {  // wave-uniform
-      if (r0 != r_first) load_row(sv, kv, r0, c0, c1);
+      if (r0 != r_first) {  // the row loaded during the previous one
+#pragma unroll
+        for (uint32_t q = 0; q < WB; ++q) sv[q] = nsv[q];
+#pragma unroll
+        for (uint32_t q = 0; q < KQ; ++q) kv[q] = nkv[q];
+      }
+      {  // one row ahead: the chunk's next row, or after its last the next chunk's first
+        const bool more = r0 + kURow < c1;
+        load_row(nsv, nkv, more ? r0 + kURow : nch.x & ~7u, more ? c0 : nch.x, more ? c1 : nxt < a.n_chunks ? nch.y : 0u);
+      }
       const uint32_t lf = r0 + lane * kURun;
       const uint32_t p_lo = max(lf, c0), p_hi = min(lf + kURun, c1);
       const bool has = p_lo < p_hi;
@@ -3110,9 +3132,10 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   }
 }
 
-// cluster totals: the per-block partials summed in a fixed order (1024 threads)
-__global__ __launch_bounds__(1024) void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks,
-                                                           double* __restrict__ out) {
+// cluster totals: the per-block partials summed in a fixed order (1024 threads); thread 0 writes
+// out[0..1] and returns true
+__device__ __forceinline__ bool usage_total_block(const double* __restrict__ part, uint32_t n_blocks,
+                                                  double* __restrict__ out) {
   double c = 0, m = 0;
   for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) { c += part[b * 2]; m += part[b * 2 + 1]; }
   for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o); m += __shfl_xor(m, o); }
@@ -3124,7 +3147,13 @@ __global__ __launch_bounds__(1024) void usage_total_kernel(const double* __restr
     for (uint32_t i = 0; i < blockDim.x / 64; ++i) { tc += sc[i]; tm += sm[i]; }
     out[0] = tc;
     out[1] = tm;
+    return true;
   }
+  return false;
+}
+__global__ __launch_bounds__(1024) void usage_total_kernel(const double* __restrict__ part, uint32_t n_blocks,
+                                                           double* __restrict__ out) {
+  usage_total_block(part, n_blocks, out);
 }
 
 // ------------------------------------------------------------------ Metric CRD values
@@ -3565,10 +3594,11 @@ __global__ __launch_bounds__(kBlock) void count8_kernel(const void* __restrict__
     part[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < 4u * NG ? s_cnt[threadIdx.x] : 0u;
 }
 
-// out[m] = sum over the blocks' partial rows (1024 threads: 16 masks x 64 block strides)
-__global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
-                                                           uint32_t n_masks, unsigned long long* __restrict__ out) {
-  __shared__ unsigned long long s[1024];
+// out[m] = sum over the blocks' partial rows (1024 threads: 16 masks x 64 block strides); s[m]
+// holds the sum afterwards
+__device__ __forceinline__ void count_total_block(const uint32_t* __restrict__ part, uint32_t n_blocks,
+                                                  uint32_t n_masks, unsigned long long* __restrict__ out,
+                                                  unsigned long long* s) {
   const uint32_t m = threadIdx.x & (kMaxCountMasks - 1), r = threadIdx.x / kMaxCountMasks;
   unsigned long long c = 0;
   constexpr uint32_t kRows = 1024 / kMaxCountMasks;  // rows summed in parallel
@@ -3590,13 +3620,19 @@ __global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __res
   }
   if (threadIdx.x < n_masks) out[threadIdx.x] = s[threadIdx.x];
 }
+__global__ __launch_bounds__(1024) void count_total_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
+                                                           uint32_t n_masks, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s[1024];
+  count_total_block(part, n_blocks, n_masks, out, s);
+}
 
+// out = nullptr: the partial rows only (kwk_aggregate sums them in agg_final_kernel)
 static void launch_count8(uint32_t n_masks, dim3 g, hipStream_t s, const void* st, uint32_t n, const StateFmt& fmt,
                           const uint32_t* masks, uint32_t* part, unsigned long long* out) {
   if (n_masks <= 4) hipLaunchKernelGGL((count8_kernel<1>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
   else if (n_masks <= 8) hipLaunchKernelGGL((count8_kernel<2>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
   else hipLaunchKernelGGL((count8_kernel<4>), g, dim3(kBlock), 0, s, st, n, fmt, masks, n_masks, part);
-  hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
+  if (out) hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
 }
 
 template <uint32_t WB>
@@ -3609,17 +3645,35 @@ static void launch_count(uint32_t n_masks, dim3 g, hipStream_t s, const void* st
   else if (n_masks <= 4) hipLaunchKernelGGL((count_kernel<WB, 4>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
   else if (n_masks <= 8) hipLaunchKernelGGL((count_kernel<WB, 8>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
   else hipLaunchKernelGGL((count_kernel<WB, 16>), g, dim3(kBlock), 0, s, st, n, abit, pmask, masks, n_masks, part, px);
-  hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
+  if (out) hipLaunchKernelGGL(count_total_kernel, dim3(1), dim3(1024), 0, s, part, g.x, n_masks, out);
 }
 
-// kwk_aggregate's output: per-stage transitions, mask counts, cluster usage as float64
-__global__ void agg_pack_kernel(const unsigned long long* __restrict__ stats, uint32_t n_stages,
-                                const unsigned long long* __restrict__ counts, uint32_t n_masks,
-                                const double* __restrict__ cluster, uint32_t usage, double* __restrict__ out) {
+// kwk_aggregate's tail in one launch (was count_total + usage_total + agg_pack: two launch gaps
+// fewer per report): the mask counts' partial rows summed (n_cblocks = 0: counts already final),
+// the usage kernel's block partials summed into cluster (usage), then the packed output
+__global__ __launch_bounds__(1024) void agg_final_kernel(const uint32_t* __restrict__ cpart, uint32_t n_cblocks,
+                                                         uint32_t n_masks, unsigned long long* __restrict__ counts,
+                                                         const double* __restrict__ upart, uint32_t n_ublocks,
+                                                         double* __restrict__ cluster, uint32_t usage,
+                                                         const unsigned long long* __restrict__ stats, uint32_t n_stages,
+                                                         double* __restrict__ out) {
+  __shared__ unsigned long long s[1024];
+  __shared__ double s_clu[2];
   const uint32_t t = threadIdx.x;
+  if (n_cblocks) count_total_block(cpart, n_cblocks, n_masks, counts, s);
+  // usage: 1 = sum the usage kernel's partials, 2 = no usage kernel ran (no nodes): pack the
+  // cluster sums as they stand
+  if (usage == 1 && usage_total_block(upart, n_ublocks, cluster)) {
+    s_clu[0] = cluster[0];
+    s_clu[1] = cluster[1];
+  } else if (usage == 2 && t == 0) {
+    s_clu[0] = cluster[0];
+    s_clu[1] = cluster[1];
+  }
+  __syncthreads();
   if (t < n_stages) out[t] = (double)stats[3 + t];
-  else if (t < n_stages + n_masks) out[t] = (double)counts[t - n_stages];
-  else if (usage && t < n_stages + n_masks + 2) out[t] = cluster[t - n_stages - n_masks];
+  else if (t < n_stages + n_masks) out[t] = (double)(n_cblocks ? s[t - n_stages] : counts[t - n_stages]);
+  else if (usage && t < n_stages + n_masks + 2) out[t] = s_clu[t - n_stages - n_masks];
 }
 
 // ------------------------------------------------------------------ node leases
@@ -3834,6 +3888,7 @@ struct kwk_engine {
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
+  uint32_t usage_rows = kUChunkRows;  // KWK_TUNE_USAGE_ROWS: rows per usage chunk (set before kwk_usage_config)
   uint32_t sweep_blocks = 0;  // persistent 2-byte sweep: resident blocks per CU (0: the occupancy)
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
@@ -4568,6 +4623,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_USAGE_KEY8:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
       e->usage_key8 = value != 0;
+      return KWK_OK;
+    case KWK_TUNE_USAGE_ROWS:
+      if (value < 1 || value > 16) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_ROWS: 1..16");
+      e->usage_rows = value;
       return KWK_OK;
     case KWK_TUNE_USAGE_BLOCKS:
       if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
@@ -5384,14 +5443,15 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk};
   for (void* p : olds) if (p) hipFree(p);
-  // usage_kernel's chunks: whole nodes, at most kUChunkPods pods (one wave row) and kUChunkNodes
-  // nodes each; a node with more pods than a row gets a chunk of its own (the wave carries its
-  // sum from row to row)
+  // the usage kernels' chunks: whole nodes, at most usage_rows wave rows of pods (less the 8 of the
+  // rounded start) and kUChunkNodes nodes each; a node with more pods than that gets a chunk of its
+  // own (the wave carries its sum from row to row)
   std::vector<uint4> chunks;
+  const uint32_t chunk_pods = e->usage_rows * kURow - 8u;
   for (uint32_t n = 0; n < n_nodes;) {
     const uint32_t c0 = node_ptr[n];
     uint32_t nb = n + 1;
-    while (nb < n_nodes && nb - n < kUChunkNodes && node_ptr[nb + 1] - c0 <= kUChunkPods) ++nb;
+    while (nb < n_nodes && nb - n < kUChunkNodes && node_ptr[nb + 1] - c0 <= chunk_pods) ++nb;
     chunks.push_back(make_uint4(c0, node_ptr[nb], n, nb));
     n = nb;
   }
@@ -5875,13 +5935,10 @@ kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_firs
   return KWK_OK;
 }
 
-kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
-  ErrScope es_(e);
-  if (!e) return fail(KWK_EINVAL, "null engine");
-  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
-  if (e->n_nodes == 0) return KWK_OK;
+// the usage kernel alone (its block partials in d_usage_part, *n_blocks of them)
+static kwk_status enqueue_usage(kwk_engine* e, int64_t now_ns, uint32_t* n_blocks) {
+  *n_blocks = 0;
   const uint32_t ublocks = (e->n_uchunks + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
   UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, (uint32_t)e->h_cpu.size(),
                (uint32_t)e->h_mem.size(), e->d_uchunk, e->n_uchunks, e->n_usage_pods, e->d_node_out, e->d_node_cum,
                e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last, e->d_mixed,
@@ -5899,8 +5956,7 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
       void* args[] = {&ua};
       HIP_TRY(hipLaunchKernel(fk, dim3(grid), dim3(kBlock), args, 0, e->stream));
     }
-    hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
-    HIP_TRY(hipGetLastError());
+    *n_blocks = grid;
     return KWK_OK;
   }
   // persistent grid (every block slot the occupancy allows), at most one chunk per wave
@@ -5911,6 +5967,18 @@ kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
     void* args[] = {&ua};
     HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(kBlock), args, 0, e->stream));
   }
+  *n_blocks = grid;
+  return KWK_OK;
+}
+
+kwk_status kwk_usage(kwk_engine* e, int64_t now_ns) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
+  if (e->n_nodes == 0) return KWK_OK;
+  if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
+  uint32_t grid = 0;
+  if (kwk_status st = enqueue_usage(e, now_ns, &grid)) return st;
   hipLaunchKernelGGL(usage_total_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_usage_part, grid, e->d_cluster);
   HIP_TRY(hipGetLastError());
   return KWK_OK;
@@ -6022,6 +6090,7 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
   // masks go to the device only when they change (a pageable copy would stall the host, r3 trace)
   if (!(n_masks && e->n_active))
     HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
+  uint32_t n_cblocks = 0;  // count blocks whose partial rows agg_final_kernel sums
   if (n_masks) {
     if (n_masks != e->agg_n_masks || memcmp(masks, e->agg_masks, 4 * (size_t)n_masks) != 0) {
       // the previous masks' copy may still be queued on the stream (it reads e->agg_masks when
@@ -6042,18 +6111,26 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
       const dim3 g((uint32_t)blocks);
       if (kwk_status st = ensure_count_part(e)) return st;
       uint32_t* pp = e->d_count_part;
-      if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, e->d_agg_masks, pp, e->d_agg_counts);
-      else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
-      else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts);
-      else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, e->d_agg_counts,
+      // partial rows only: agg_final_kernel sums them
+      if (wb == 1) launch_count8(n_masks, g, e->stream, e->d_st, e->n_active, e->fmt, e->d_agg_masks, pp, nullptr);
+      else if (wb == 2) launch_count<2>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, nullptr);
+      else if (wb == 4) launch_count<4>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, nullptr);
+      else launch_count<8>(n_masks, g, e->stream, e->d_st, e->n_active, abit, pmask, e->d_agg_masks, pp, nullptr,
                            e->fmt.dw);
       HIP_TRY(hipGetLastError());
+      n_cblocks = g.x;
     }
   }
-  if (usage)
-    if (kwk_status st = kwk_usage(e, now_ns)) return st;
-  hipLaunchKernelGGL(agg_pack_kernel, dim3(1), dim3(64), 0, e->stream, e->d_stats, n_stages, e->d_agg_counts, n_masks,
-                     e->d_cluster, usage ? 1u : 0u, dst);
+  uint32_t n_ublocks = 0;
+  const bool run_usage = usage && e->n_nodes;
+  if (run_usage) {
+    if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
+    if (kwk_status st = enqueue_usage(e, now_ns, &n_ublocks)) return st;
+  }
+  // usage with no nodes: the cluster sums stay what the last kwk_usage left (as before)
+  hipLaunchKernelGGL(agg_final_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_count_part, n_cblocks, n_masks,
+                     e->d_agg_counts, e->d_usage_part, n_ublocks, e->d_cluster, usage ? (run_usage ? 1u : 2u) : 0u,
+                     e->d_stats, n_stages, dst);
   HIP_TRY(hipGetLastError());
   *n_out = n_stages + n_masks + (usage ? 2u : 0u);
   return KWK_OK;

@@ -98,6 +98,7 @@ TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_COMPACT_LB = 11
+TUNE_USAGE_ROWS = 12
 
 
 class Lease(C.Structure):

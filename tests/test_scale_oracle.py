@@ -65,7 +65,7 @@ def _rows_at(eng, slots):
 @pytest.mark.parametrize("state", ["auto", "u16", "auto-shard"])
 def test_c5_persistent_table_sweep_sampled_oracle(state):
     """C5 pod shape (pod-fast, 100 pods per node, 10 % Job-owned, harness churn) at the sizes
-    where the sweeps run persistent with two tiles in flight: the 1-byte dictionary-id sweep
+    where the sweeps run persistent with two tiles in flight (the shard: one tile per workgroup): the 1-byte dictionary-id sweep
     (auto: sweep8_kernel, the bench's kernel; 8192-id tiles, 40M pods) and the 2-byte table-only
     sweep (u16: sweep16_fsm_kernel, 20M pods), every ~10000th / 4999th slot checked each step;
     auto-shard: the 12.5M-pod shard of N = 8 (1526 one-tile workgroups)."""
@@ -76,6 +76,7 @@ def test_c5_persistent_table_sweep_sampled_oracle(state):
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
     n = {"auto": 40_000_000, "u16": 20_000_000, "auto-shard": 12_500_000}[state]
+    persistent = 0 if state == "auto-shard" else 1  # the shard's tiles fit one resident grid
     state = "auto" if state == "auto-shard" else state
     files = W.stage_paths(W.POD_FAST)
     pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
@@ -93,7 +94,7 @@ def test_c5_persistent_table_sweep_sampled_oracle(state):
         slots = list(range(3, n, 9973 if state == "auto" else 4999))
         assert int(np.sum(idx[slots])) > 100  # Job-owned pods (pod-complete) are in the sample
         kernel = abi.SWEEP_8 if state == "auto" else abi.SWEEP_16_FSM
-        total = _sampled_run(prog, eng, files, pvars, idx, slots, 10, 10**9, kernel, 1)
+        total = _sampled_run(prog, eng, files, pvars, idx, slots, 10, 10**9, kernel, persistent)
         assert total > len(slots)  # every pod became ready once, Job pods completed, deletions re-created
         assert eng.stats()["state_bytes"] == (1 if state == "auto" else 2)
     finally:

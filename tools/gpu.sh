@@ -7,6 +7,7 @@
 #   smoke                      __graft_entry__.smoke()
 #   bench[=<bench.py args>]    the driver's bench command (default --gpus 1 --steps 20 --warmup 5)
 #   prof                       kernel trace + stats of the driver's bench command (kernel_stats.csv)
+#   timeline[=<bench args>]    kernel trace of the C5 bench (timed steps only): 10 steps' dispatches and gaps
 #   configs                    bench.py --config C1..C4 lines (configs_C1_C4.jsonl)
 #   c2prof                     C2 working set: kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #   sq                         SQ counter passes over the C5 pod sweep and the C2 word sweep
@@ -14,7 +15,8 @@
 #                              125k / 250k / 500k nodes) + a kernel trace of the 125k-node shard
 #   dist                       2 ranks sharing the GPU over gloo (the N > 1 bench path) vs one rank
 #   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/ab/<so>, alternating x2
-#   variants=<args>            tools/variants.py run <args> (cost-isolation builds)
+#   abemit=<so>                same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>
+#   variants=<args>           tools/variants.py run <args> (cost-isolation builds)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; T=$1; shift; O=$R/gpurun_out/$T
 mkdir -p $O && cd $R
@@ -42,6 +44,12 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py $B1 --no-pmc --no-cpu-baseline \
         > $O/prof_bench.json 2> $O/prof_bench.err || { tail -30 $O/prof_bench.err; exit 1; }
       cd $R && python tools/rocpd_summary.py stats $(find $O/prof -name '*.db' | head -1) $O/kernel_stats.csv && cut -c1-150 $O/kernel_stats.csv | head -14 ;;
+    timeline)  # kernel trace of the C5 timed steps only; every dispatch of 10 steps with its gap
+      TRACE
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run -- python3 $R/bench.py $B1 --no-pmc --no-cpu-baseline \
+        --hbm-nodes 0 --pcie-steps 0 --emit-steps 0 $arg > $O/tl_bench.json 2> $O/tl_bench.err || { tail -30 $O/tl_bench.err; exit 1; }
+      cd $R && python tools/rocpd_summary.py timeline $(find $O/tl -name '*.db' | head -1) sweep8 10 10 > $O/timeline.txt \
+        && cat $O/timeline.txt ;;
     configs)
       for c in C1 C2 C3 C4; do
         timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 5 >> $O/configs_C1_C4.jsonl 2> $O/config_$c.err || { tail -30 $O/config_$c.err; exit 1; }
@@ -120,6 +128,17 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
         done
       done
       cp $O/cur.so kwok_amd/lib/libkwok_engine.so && rm -f $O/cur.so ;;
+    abemit)  # same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>, alternating x2
+      L=kwok_amd/lib/libkwok_emit.so; cp $L $O/cur_emit.so
+      for i in 1 2; do
+        for v in cur other; do
+          if [ $v = other ]; then cp tools/ab/$arg $L; else cp $O/cur_emit.so $L; fi
+          timeout -k 10 200 python -u bench.py --gpus 1 --steps 5 --warmup 3 --no-pmc --no-cpu-baseline --hbm-nodes 0 --pcie-steps 0 \
+            --emit-steps 8 > $O/emit_${v}_$i.json 2> $O/emit_${v}_$i.err || { cp $O/cur_emit.so $L; tail -20 $O/emit_${v}_$i.err; exit 1; }
+          python -c "import json; e=json.load(open('$O/emit_${v}_$i.json'))['patch_emit']; print('$v', $i, e['patches_per_s'], 'us', e['avg_emit_us'])"
+        done
+      done
+      cp $O/cur_emit.so $L && rm -f $O/cur_emit.so ;;
     variants)
       timeout -k 10 600 python -u tools/variants.py run $arg > $O/variants.jsonl 2> $O/variants.err || { tail -30 $O/variants.err; exit 1; }
       cut -c1-300 $O/variants.jsonl ;;

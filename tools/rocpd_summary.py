@@ -4,6 +4,9 @@
     python tools/rocpd_summary.py pmc <db> [kernel-substring]  # per-kernel counter means per dispatch
     python tools/rocpd_summary.py window <db> <kernel-substring> <first> <count> [stride]
                                                            # mean duration of dispatches first, first+stride, ...
+    python tools/rocpd_summary.py timeline <db> <kernel-substring> <nth> <span>
+                                                           # every dispatch from the nth launch of a kernel to
+                                                           # the (nth + span)th: offsets, durations, gaps
 
 `stats` reproduces rocprofv3's kernel_stats.csv columns (Name, Calls, TotalDurationNs,
 AverageNs, Percentage, MinNs, MaxNs).  `pmc` sums each counter over its dimensions
@@ -67,8 +70,35 @@ def window(db: str, kernel: str, first: int, count: int, stride: int = 1):
             "median_ns": statistics.median(sel), "min_ns": min(sel), "max_ns": max(sel), "durations_ns": sel}
 
 
+def _short(name: str) -> str:
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("((")[0].split("(")[0][:60] if "(" in n else n[:60]
+
+
+def timeline(db: str, kernel: str, nth: int, span: int):
+    """The dispatches from the nth dispatch of `kernel` to the (nth + span)th, in start order:
+    offset from the first start, duration and the idle gap before each (ns) — what one step's
+    kernels cost back to back, launch gaps included."""
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, \"end\" from kernels order by start").fetchall()
+    hits = [i for i, r in enumerate(rows) if kernel in r[0]]
+    i0, i1 = hits[nth], hits[min(nth + span, len(hits) - 1)]
+    t0, prev = rows[i0][1], rows[i0][1]
+    out = []
+    for name, s, e in rows[i0:i1 + 1]:
+        out.append((int(s - t0), int(e - s), int(max(0, s - prev)), _short(name)))
+        prev = max(prev, e)
+    busy = sum(d for _, d, _, _ in out[:-1])
+    return out, int(rows[i1][1] - t0), busy
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "window":
+    if sys.argv[1] == "timeline":
+        rows, wall, busy = timeline(sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))
+        for off, dur, gap, name in rows:
+            print(f"{off / 1e3:9.2f} us  dur {dur / 1e3:8.2f}  gap {gap / 1e3:6.2f}  {name}")
+        print(f"wall {wall / 1e3:.2f} us (first to last start), kernels busy {busy / 1e3:.2f} us")
+    elif sys.argv[1] == "window":
         import json
         print(json.dumps(window(sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]),
                                 int(sys.argv[6]) if len(sys.argv) > 6 else 1)))
