@@ -2598,7 +2598,9 @@ struct UsageArgs {
   const double2* __restrict__ kv;     // {cpu, mem} value of each distinct usage key (<= kUKeyDict)
   uint32_t kv_n;
 };
-constexpr uint32_t kUKeyDict = 256;  // distinct usage keys that take the 1-byte key column
+constexpr uint32_t kUKeyDict = 256;  // entries of the 1-byte key column's value table
+constexpr uint32_t kUKeyZero = 255;  // its entry {0, 0}: the key a dead / out-of-range pod reads, so at
+                                     // most 255 distinct keys take the 1-byte column
 
 // a pod's usage_key: containers (bits 28..31) x one interned value each, or 0 containers =
 // a pod whose containers differ: bits 0..27 index its {first, count} entry of the mixed table
@@ -2631,6 +2633,19 @@ __device__ __forceinline__ bool run_alive(const uint4 (&sv)[WB], int j, uint32_t
     // the sched word of {pred, sched}; px: the packed word of a fused record
     return ((px ? ((j & 1) ? c.z : c.x) : ((j & 1) ? c.w : c.y)) & abit) != 0;
   }
+}
+
+// the alive bits (kIdAlive) of a lane's 16 1-byte ids as a 16-bit mask, bit j = pod j of the run:
+// per dword the four bits at 0 / 8 / 16 / 24 meet at bits 21-24 of one multiply (no carries)
+__device__ __forceinline__ uint32_t alive16_ids(const uint4 c) {
+  const uint32_t dw[4] = {c.x, c.y, c.z, c.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t a = (dw[d] >> 5) & 0x01010101u;
+    m |= (((a * 0x204081u) >> 21) & 15u) << (4 * d);
+  }
+  return m;
 }
 
 // DPP helpers of the usage kernels' lane scans (GFX9 DPP: row_shr, row_bcast15/31, wave_shr);
@@ -2916,6 +2931,7 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   __shared__ double2 s_sum[kWavesPerBlock][kUChunkNodes];
   __shared__ double s_pv[kKey8 ? 1 : kUFastVals];
   __shared__ double2 s_kv[kKey8 ? kUKeyDict : 1];
+  __shared__ uint32_t s_nib[16];
   __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
@@ -2965,7 +2981,12 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   }
   if (chunk + n_waves < a.n_chunks) nch2 = a.chunks[chunk + n_waves];
   if (kKey8) {
-    for (uint32_t j = threadIdx.x; j < a.kv_n; j += kBlock) s_kv[j] = a.kv[j];
+    for (uint32_t j = threadIdx.x; j < kUKeyDict; j += kBlock) s_kv[j] = j < a.kv_n ? a.kv[j] : make_double2(0.0, 0.0);
+    if (threadIdx.x < 16) {  // s_nib[x]: byte i = 0xFF where bit i of x is clear (that pod reads kUKeyZero)
+      uint32_t m = 0;
+      for (uint32_t i = 0; i < 4; ++i) m |= ((threadIdx.x >> i) & 1u) ? 0u : 0xFFu << (8 * i);
+      s_nib[threadIdx.x] = m;
+    }
   } else {
     for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
   }
@@ -3035,6 +3056,60 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
       uint32_t head_k = 0;
       double acc_c = 0.0, acc_m = 0.0, head_c = 0.0, head_m = 0.0;
       uint32_t bnd = sp[k + 1];
+      bool done = false;  // the row's pods summed by the branch-free path below
+      if constexpr (kKey8 && WB == 1) {
+        // every lane's run crosses at most one node boundary (nodes of >= 16 pods, C5's 100): its
+        // pods before the boundary and from it are summed separately without branches — a pod
+        // that is dead, out of range or on the other side reads the zero entry kUKeyZero, so each
+        // sum is the in-order sum of its pods exactly as the per-pod loop adds them
+        uint32_t k2 = k, nb2 = bnd;
+        const bool has_b = has && bnd < p_hi;
+        if (has_b) {  // the node holding pod bnd (past nodes without pods)
+          k2 = k + 1;
+          while (sp[k2 + 1] <= bnd) ++k2;
+          nb2 = sp[k2 + 1];
+        }
+        if (!ballot(has_b && nb2 < p_hi)) {  // wave-uniform: no run crosses two boundaries
+          done = true;
+          const uint32_t lo = has ? p_lo - lf : 0u, hi = has ? p_hi - lf : 0u, jb = has_b ? bnd - lf : hi;
+          const uint32_t alive = alive16_ids(sv[0]);
+          const uint32_t m_a = alive & ((1u << jb) - 1u) & ~((1u << lo) - 1u);  // pods [lo, jb)
+          const uint32_t m_b = alive & ((1u << hi) - 1u) & ~((1u << jb) - 1u);  // pods [jb, hi)
+          uint4 kq = kv[0];  // one key dword (4 pods) per step, rotated: 8 values in flight, not 32
+          uint32_t qa = m_a, qb = m_b;
+          double ac = 0.0, am = 0.0, bc = 0.0, bm = 0.0;
+#pragma unroll 1
+          for (int d = 0; d < 4; ++d) {
+            const uint32_t ka = kq.x | s_nib[qa & 15u], kb = kq.x | s_nib[qb & 15u];
+            kq = make_uint4(kq.y, kq.z, kq.w, 0u);
+            qa >>= 4;
+            qb >>= 4;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const double2 va = s_kv[(ka >> (8 * b)) & 0xFFu], vb = s_kv[(kb >> (8 * b)) & 0xFFu];
+              ac += va.x;
+              am += va.y;
+              bc += vb.x;
+              bm += vb.y;
+            }
+          }
+          if (has_b) {  // node k closes at the boundary, node k2 goes on to the run's end
+            if (cont && !head) {
+              head = true; head_k = k; head_c = ac; head_m = am;
+            } else {
+              ss[k] = make_double2(ac, am);
+            }
+            k = k2;
+            bnd = nb2;
+            acc_c = bc;
+            acc_m = bm;
+          } else {
+            acc_c = ac;
+            acc_m = am;
+          }
+        }
+      }
+      if (!done) {
 #pragma unroll
       for (int j = 0; j < (int)kURun; ++j) {
         const uint32_t p = lf + (uint32_t)j;
@@ -3067,6 +3142,7 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
         }
         acc_c += live ? vc : 0.0;
         acc_m += live ? vm : 0.0;
+      }
       }
       // a node ending with the lane's last pod is closed here (the next lane starts a new
       // node); so is the chunk's last node
@@ -5499,7 +5575,7 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
       uint32_t d = 0;
       while (d < dict.size() && dict[d] != ukey[p]) ++d;  // few distinct keys: linear search
       if (d == dict.size()) {
-        if (dict.size() == kUKeyDict) { fits = false; break; }
+        if (dict.size() == kUKeyZero) { fits = false; break; }
         dict.push_back(ukey[p]);
       }
       k8[p] = (uint8_t)d;

@@ -8,6 +8,7 @@
 #   bench[=<bench.py args>]    the driver's bench command (default --gpus 1 --steps 20 --warmup 5)
 #   prof                       kernel trace + stats of the driver's bench command (kernel_stats.csv)
 #   timeline[=<bench args>]    kernel trace of the C5 bench (timed steps only): 10 steps' dispatches and gaps
+#   agg                        the reporting kernels alone at C5 (tools/agg_bench.py) + SQ passes over usage
 #   configs                    bench.py --config C1..C4 lines (configs_C1_C4.jsonl)
 #   c2prof                     C2 working set: kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #   sq                         SQ counter passes over the C5 pod sweep and the C2 word sweep
@@ -50,6 +51,19 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
         --hbm-nodes 0 --pcie-steps 0 --emit-steps 0 $arg > $O/tl_bench.json 2> $O/tl_bench.err || { tail -30 $O/tl_bench.err; exit 1; }
       cd $R && python tools/rocpd_summary.py timeline $(find $O/tl -name '*.db' | head -1) sweep8 10 10 > $O/timeline.txt \
         && cat $O/timeline.txt ;;
+    agg)  # the reporting kernels alone at C5 (tools/agg_bench.py) + SQ passes over them
+      timeout -k 10 300 python -u tools/agg_bench.py > $O/agg.json 2> $O/agg.err || { tail -30 $O/agg.err; exit 1; }
+      cat $O/agg.json
+      TRACE
+      S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
+      S2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+      for p in 1 2; do
+        S=S$p
+        timeout -s KILL 200 rocprofv3 --pmc ${!S} -d $O/aggsq$p -o run -- python3 $R/tools/agg_bench.py --reps 3 --usage-only > $O/aggsq$p.log 2>&1 || { tail -20 $O/aggsq$p.log; exit 1; }
+      done
+      cd $R
+      for d in aggsq1 aggsq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) usage_fast; done > $O/agg_sq.txt
+      cat $O/agg_sq.txt ;;
     configs)
       for c in C1 C2 C3 C4; do
         timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 5 >> $O/configs_C1_C4.jsonl 2> $O/config_$c.err || { tail -30 $O/config_$c.err; exit 1; }
