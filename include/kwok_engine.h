@@ -229,6 +229,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1, or 0
                                   (default: the scan + expansion pair / the one-launch small compaction above;
                                   the look-back measured 73 us against 27 us at C5) */
+#define KWK_TUNE_AGG_FUSED 13  /* kwk_aggregate with KWK_AGG_USAGE on 1-byte ids: the <= 4 mask counts taken inside the
+                                  usage kernel's pass over the id column, 1 (default), or 0 (a count pass of their own) */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */

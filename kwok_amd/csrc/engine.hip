@@ -2569,6 +2569,7 @@ constexpr uint32_t kUChunkPods = kURow - 8u;    // pods of a one-row chunk: it f
                                                 // start down to 8; an R-row chunk holds R * kURow - 8
 constexpr uint32_t kUChunkNodes = 128;          // nodes per chunk: the wave's LDS copy of node_ptr
 constexpr uint32_t kULdsValues = 512;           // cpu + mem dictionary entries staged in LDS (else read via L1)
+constexpr int kMaxCountMasks = 16;  // kwk_count / kwk_aggregate masks per call
 struct UsageArgs {
   const void* __restrict__ st;
   StateFmt fmt;
@@ -2597,6 +2598,11 @@ struct UsageArgs {
   const uint8_t* __restrict__ ukey8;  // usage_fast_kernel<WB, true>: per pod, an index into kv
   const double2* __restrict__ kv;     // {cpu, mem} value of each distinct usage key (<= kUKeyDict)
   uint32_t kv_n;
+  // usage_fast_kernel<1, true> with kwk_aggregate's mask counts folded in (n_cmasks 1..4, 0: none):
+  // count8_kernel's per-id table over the same id rows, partial rows per block into cpart
+  const uint32_t* __restrict__ cmasks;
+  uint32_t n_cmasks;
+  uint32_t* __restrict__ cpart;       // [grid][kMaxCountMasks]
 };
 constexpr uint32_t kUKeyDict = 256;  // entries of the 1-byte key column's value table
 constexpr uint32_t kUKeyZero = 255;  // its entry {0, 0}: the key a dead / out-of-range pod reads, so at
@@ -2687,7 +2693,10 @@ __global__ __launch_bounds__(kBlock) void usage_kernel(UsageArgs a) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
   uint32_t chunk = blockIdx.x * kWavesPerBlock + wave;
-  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods * WB);
+  // range-checked per dword: a size that ends inside a dword would zero the last pods' bytes of
+  // it (ids of 1-2 bytes), so the size is rounded up to whole 16-byte loads (the columns are
+  // padded; pods past the chunk's end are masked out by the lanes' ranges)
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, (a.n_pods * WB + 15u) & ~15u);
   const __amdgpu_buffer_rsrc_t uk_rs = make_rsrc(a.ukey, a.n_pods * 4u);
   // the next chunk: descriptor and first row in flight
   uint4 nch = make_uint4(0u, 0u, 0u, 0u);
@@ -2932,12 +2941,18 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   __shared__ double s_pv[kKey8 ? 1 : kUFastVals];
   __shared__ double2 s_kv[kKey8 ? kUKeyDict : 1];
   __shared__ uint32_t s_nib[16];
+  constexpr bool kCnt = kKey8 && WB == 1;  // mask counts can ride along (a.n_cmasks)
+  __shared__ uint32_t s_clut[kCnt ? 256 : 1];
+  __shared__ unsigned int s_ccnt[kCnt ? 4 : 1];
   __shared__ double s_c[kWavesPerBlock], s_m[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
   uint32_t chunk = blockIdx.x * kWavesPerBlock + wave;
-  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, a.n_pods * WB);
-  const __amdgpu_buffer_rsrc_t uk_rs = kKey8 ? make_rsrc(a.ukey8, a.n_pods) : make_rsrc(a.ukey, a.n_pods * 4u);
+  // range-checked per dword: a size that ends inside a dword would zero the last pods' bytes of
+  // it (ids of 1-2 bytes), so the size is rounded up to whole 16-byte loads (the columns are
+  // padded; pods past the chunk's end are masked out by the lanes' ranges)
+  const __amdgpu_buffer_rsrc_t st_rs = make_rsrc(a.st, (a.n_pods * WB + 15u) & ~15u);
+  const __amdgpu_buffer_rsrc_t uk_rs = kKey8 ? make_rsrc(a.ukey8, (a.n_pods + 15u) & ~15u) : make_rsrc(a.ukey, a.n_pods * 4u);
   uint4 nch = make_uint4(0u, 0u, 0u, 0u);
   uint4 nsv[WB], nkv[KQ];
   auto load_row = [&](uint4 (&dsv)[WB], uint4 (&dkv)[KQ], uint32_t r0, uint32_t c0, uint32_t c1) {
@@ -2987,6 +3002,19 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
       for (uint32_t i = 0; i < 4; ++i) m |= ((threadIdx.x >> i) & 1u) ? 0u : 0xFFu << (8 * i);
       s_nib[threadIdx.x] = m;
     }
+    if constexpr (kCnt) {
+      if (a.n_cmasks) {  // count8_kernel's table: byte m of entry id = 1 if the id counts for mask m
+        const uint2 v = fmt_unpack(a.fmt.id2w[threadIdx.x], a.fmt);
+        const uint32_t al = (v.y & KWK_F_ALIVE) ? 1u : 0u;
+        uint32_t x = 0;
+        for (uint32_t m = 0; m < a.n_cmasks; ++m) {
+          const uint32_t mk = a.cmasks[m];
+          x |= (al & ((mk == 0u || (v.x & mk) != 0u) ? 1u : 0u)) << (8 * m);
+        }
+        s_clut[threadIdx.x] = x;  // kBlock = 256 threads: one entry each
+        if (threadIdx.x < 4) s_ccnt[threadIdx.x] = 0;
+      }
+    }
   } else {
     for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
   }
@@ -2997,6 +3025,8 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   double tot_c = 0.0, tot_m = 0.0;
   uint32_t* __restrict__ sp = s_ptr[wave];
   double2* __restrict__ ss = s_sum[wave];
+  const bool cnt_on = kCnt && a.n_cmasks != 0;  // uniform
+  uint32_t ccnt[4] = {0u, 0u, 0u, 0u};          // per lane: pods counted for masks 0..3
   for (; chunk < a.n_chunks; chunk += n_waves) {  // wave-uniform
     const uint4 ch = nch;
     const uint32_t c0 = ch.x, c1 = ch.y, na = ch.z, nk = ch.w - ch.z;
@@ -3073,6 +3103,21 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
           done = true;
           const uint32_t lo = has ? p_lo - lf : 0u, hi = has ? p_hi - lf : 0u, jb = has_b ? bnd - lf : hi;
           const uint32_t alive = alive16_ids(sv[0]);
+          if constexpr (kCnt) {
+            if (cnt_on) {  // the row's pods [lo, hi) by id (an out-of-range pod reads id 0: counts nothing)
+              const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+              const uint32_t ids[4] = {sv[0].x, sv[0].y, sv[0].z, sv[0].w};
+              uint32_t acc = 0;  // four byte counters (<= 16 each)
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                const uint32_t q = ids[d] & ~s_nib[(rng >> (4 * d)) & 15u];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc += s_clut[(q >> (8 * b)) & 0xFFu];
+              }
+#pragma unroll
+              for (int m = 0; m < 4; ++m) ccnt[m] += (acc >> (8 * m)) & 0xFFu;
+            }
+          }
           const uint32_t m_a = alive & ((1u << jb) - 1u) & ~((1u << lo) - 1u);  // pods [lo, jb)
           const uint32_t m_b = alive & ((1u << hi) - 1u) & ~((1u << jb) - 1u);  // pods [jb, hi)
           uint4 kq = kv[0];  // one key dword (4 pods) per step, rotated: 8 values in flight, not 32
@@ -3126,6 +3171,14 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
           bnd = sp[k + 1];
         }
         const bool live = in && run_alive<WB>(sv, j, abit, a.fmt.dw != 0);
+        if constexpr (kCnt) {
+          if (cnt_on && in) {
+            const uint32_t e = s_clut[(((j >> 2) == 0 ? sv[0].x : (j >> 2) == 1 ? sv[0].y : (j >> 2) == 2 ? sv[0].z : sv[0].w) >>
+                                       (8 * (j & 3))) & 0xFFu];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) ccnt[m] += (e >> (8 * m)) & 0xFFu;
+          }
+        }
         double vc, vm;
         if constexpr (kKey8) {
           const uint4 kq = kv[0];
@@ -3199,12 +3252,26 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
     tot_m += __shfl_xor(tot_m, o);
   }
   if (lane == 0) { s_c[wave] = tot_c; s_m[wave] = tot_m; }
+  if constexpr (kCnt) {
+    if (cnt_on) {  // the block's partial row of mask counts (summed by agg_final_kernel)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint32_t c = ccnt[m];
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if (lane == 0 && c) atomicAdd(&s_ccnt[m], c);
+      }
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     double tc = 0, tm = 0;
     for (int i = 0; i < kWavesPerBlock; ++i) { tc += s_c[i]; tm += s_m[i]; }
     a.block_part[blockIdx.x * 2 + 0] = tc;
     a.block_part[blockIdx.x * 2 + 1] = tm;
+  }
+  if constexpr (kCnt) {
+    if (cnt_on && threadIdx.x < kMaxCountMasks)
+      a.cpart[(uint64_t)blockIdx.x * kMaxCountMasks + threadIdx.x] = threadIdx.x < 4u ? s_ccnt[threadIdx.x] : 0u;
   }
 }
 
@@ -3441,7 +3508,6 @@ __global__ __launch_bounds__(kBlock) void histogram_kernel(MetricArgs a, HistDes
 // state column (8, 4 or 2 words) and tests the raw words (pred bits, alive flag) against the
 // masks — only the n_masks masks asked for (a wave-uniform loop bound) — with per-lane
 // counters in registers, one 64-bit atomic per block and mask.
-constexpr int kMaxCountMasks = 16;
 template <uint32_t WB, int NM>  // NM >= n_masks masks tested (compile time); the rest count nothing used
 __global__ __launch_bounds__(kBlock) void count_kernel(const void* __restrict__ st, uint32_t n, uint32_t abit,
                                                        uint32_t pmask, const uint32_t* __restrict__ masks,
@@ -3964,6 +4030,7 @@ struct kwk_engine {
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
+  bool agg_fused = true;      // KWK_TUNE_AGG_FUSED: kwk_aggregate's mask counts inside the usage kernel
   uint32_t usage_rows = kUChunkRows;  // KWK_TUNE_USAGE_ROWS: rows per usage chunk (set before kwk_usage_config)
   uint32_t sweep_blocks = 0;  // persistent 2-byte sweep: resident blocks per CU (0: the occupancy)
   int n_cus = 256;
@@ -4699,6 +4766,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_USAGE_KEY8:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
       e->usage_key8 = value != 0;
+      return KWK_OK;
+    case KWK_TUNE_AGG_FUSED:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_AGG_FUSED: 0 or 1");
+      e->agg_fused = value != 0;
       return KWK_OK;
     case KWK_TUNE_USAGE_ROWS:
       if (value < 1 || value > 16) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_ROWS: 1..16");
@@ -6011,14 +6082,24 @@ kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_firs
   return KWK_OK;
 }
 
-// the usage kernel alone (its block partials in d_usage_part, *n_blocks of them)
-static kwk_status enqueue_usage(kwk_engine* e, int64_t now_ns, uint32_t* n_blocks) {
+// whether usage_fast_kernel<1, true> runs for this engine and covers every active slot, so that
+// kwk_aggregate's mask counts (<= 4) can ride along in it instead of a count8_kernel pass
+static bool usage_counts(const kwk_engine* e, uint32_t n_masks) {
+  return e->agg_fused && n_masks >= 1 && n_masks <= 4 && word_bytes(e->fmt) == 1 && !e->has_mixed_keys &&
+         !e->d_pod_out && e->podv_n && e->d_ukey8 && e->usage_key8 && e->n_nodes && e->n_usage_pods == e->n_active;
+}
+
+// the usage kernel alone (its block partials in d_usage_part, *n_blocks of them); cmasks: the
+// mask counts folded in (usage_counts), their partial rows in d_count_part
+static kwk_status enqueue_usage(kwk_engine* e, int64_t now_ns, uint32_t* n_blocks, const uint32_t* cmasks = nullptr,
+                                uint32_t n_cmasks = 0) {
   *n_blocks = 0;
   const uint32_t ublocks = (e->n_uchunks + kWavesPerBlock - 1) / kWavesPerBlock;
   UsageArgs ua{e->d_st, e->fmt, e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, (uint32_t)e->h_cpu.size(),
                (uint32_t)e->h_mem.size(), e->d_uchunk, e->n_uchunks, e->n_usage_pods, e->d_node_out, e->d_node_cum,
                e->d_node_last, now_ns, e->d_usage_part, e->d_pod_out, e->d_pod_cum, e->d_pod_last, e->d_mixed,
-               e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n, e->d_ukey8, e->d_kv, e->kv_n};
+               e->d_ckeys, e->d_mbase, e->d_ccum, e->d_podv, e->podv_n, e->d_ukey8, e->d_kv, e->kv_n,
+               cmasks, n_cmasks, e->d_count_part};
   const uint32_t wb = word_bytes(e->fmt);
   // the kernels are specialised on the state word's bytes (1: dictionary ids, 2, 4, 8)
 #define USAGE_KERNEL(K, ...) (wb == 1 ? (const void*)K<1 __VA_ARGS__> : wb == 2 ? (const void*)K<2 __VA_ARGS__>   \
@@ -6167,6 +6248,10 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
   if (!(n_masks && e->n_active))
     HIP_TRY(hipMemsetAsync(e->d_agg_counts, 0, sizeof(unsigned long long) * kMaxCountMasks, e->stream));
   uint32_t n_cblocks = 0;  // count blocks whose partial rows agg_final_kernel sums
+  // the counts ride along in the usage kernel (one pass over the id column instead of two)
+  const bool fused = usage && e->d_node_ptr && usage_counts(e, n_masks);
+  if (fused)
+    if (kwk_status st = ensure_count_part(e)) return st;
   if (n_masks) {
     if (n_masks != e->agg_n_masks || memcmp(masks, e->agg_masks, 4 * (size_t)n_masks) != 0) {
       // the previous masks' copy may still be queued on the stream (it reads e->agg_masks when
@@ -6176,7 +6261,7 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
       e->agg_n_masks = n_masks;
       HIP_TRY(hipMemcpyAsync(e->d_agg_masks, e->agg_masks, 4 * (size_t)n_masks, hipMemcpyHostToDevice, e->stream));
     }
-    if (e->n_active) {
+    if (e->n_active && !fused) {
       const uint32_t wb = (uint32_t)word_bytes(e->fmt);
       const uint64_t chunks = ((uint64_t)e->n_active * wb + 15u) / 16u;
       uint64_t blocks = (chunks + kBlock * 4 - 1) / (kBlock * 4);
@@ -6201,7 +6286,9 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
   const bool run_usage = usage && e->n_nodes;
   if (run_usage) {
     if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
-    if (kwk_status st = enqueue_usage(e, now_ns, &n_ublocks)) return st;
+    if (kwk_status st = enqueue_usage(e, now_ns, &n_ublocks, fused ? e->d_agg_masks : nullptr, fused ? n_masks : 0u))
+      return st;
+    if (fused) n_cblocks = n_ublocks;
   }
   // usage with no nodes: the cluster sums stay what the last kwk_usage left (as before)
   hipLaunchKernelGGL(agg_final_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_count_part, n_cblocks, n_masks,

@@ -99,6 +99,7 @@ TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_COMPACT_LB = 11
 TUNE_USAGE_ROWS = 12
+TUNE_AGG_FUSED = 13
 
 
 class Lease(C.Structure):

@@ -336,3 +336,39 @@ def test_gpu_usage_key8_column_matches_4byte_keys(state):
     np.testing.assert_allclose(node[:, 2:], 2.0 * want, rtol=REL_TOL, atol=0)
     np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pods_per_node", [100, 7])
+def test_gpu_aggregate_counts_in_usage_pass(pods_per_node):
+    """kwk_aggregate on 1-byte ids with usage: the mask counts taken inside the usage kernel's pass
+    (KWK_TUNE_AGG_FUSED 1, the default) equal a count pass of their own (0) and kwk_count, and the
+    usage sums are unchanged — 2M pods of the C5 shape after churn steps; 100 pods per node (the
+    branch-free rows) and 7 (runs crossing several node boundaries: the per-pod loop)."""
+    import bench
+    from kwok_amd.host import abi
+    from kwok_amd.host.cluster import phase_masks
+    n_nodes = 2_000_000 // pods_per_node
+    pods, nodes, (pvars, pidx) = bench.build_engines(0, n_nodes, pods_per_node, 0, 0x6B776F6B, 0.1)
+    try:
+        bench.configure_usage(pods, pvars, pidx, n_nodes, pods_per_node)
+        assert pods.stats()["state_bytes"] == 1
+        for k in range(5):
+            pods.step(bench.NOW0 + k * 10**9, 1, k)
+        pm = [0] + list(phase_masks(pods.p, values=("Running", "Succeeded", "Failed")).values())
+        pm = pm[:4]
+        now = bench.NOW0 + 10 * 10**9
+        outs = []
+        for fused in (1, 0):
+            pods.set_tuning(abi.TUNE_AGG_FUSED, fused)
+            n = pods.aggregate(pm, now, usage=True)
+            outs.append(pods.aggregate_read(n))
+        pods.set_tuning(abi.TUNE_AGG_FUSED, 1)
+        assert np.array_equal(outs[0], outs[1])
+        counts = pods.count(pm)
+        n_st = len(outs[0]) - len(pm) - 2
+        assert outs[0][n_st:n_st + len(pm)].astype(np.int64).tolist() == [int(c) for c in counts]
+        assert counts[0] > 0 and outs[0][-2] > 0
+    finally:
+        pods.close()
+        nodes.close()
