@@ -1425,9 +1425,8 @@ __device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, 
     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, seg_n));
     if constexpr (kStages4) {
       if (fire) wl[pos] = (uint16_t)((addr & 0x7FFu) | (e & kId8Rec16));
-      const uint32_t code = (e >> 11) & 3u;
-#pragma unroll
-      for (uint32_t st = 0; st < 4; ++st) stc[st] += (uint32_t)__popcll(ballot(code == st) & bal);
+      // per-lane byte counters, one per stage code (bits 11-12): no ballot / SALU chain per stage
+      stc[0] += (e >> 31) << ((e >> 8) & 0x18u);
     } else {
       __builtin_amdgcn_raw_buffer_store_b32((addr & 0x7FFu) | ((e >> 3) & 0x1FE000u), seg_rs, fire ? (1u + pos) * 4u : kOOB,
                                             0, 0);
@@ -1488,7 +1487,9 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   s_inv[wave][lane] = 0xFFFFFFFFu;
   __syncthreads();
 
-  uint32_t stc[4] = {0u, 0u, 0u, 0u};   // wave-uniform: fired records of stages 0-3 (kStages4)
+  // kStages4: stc[0] = this tile's fired records of stages 0-3 as byte counters (<= 32 items per lane
+  // and tile), folded after each tile into 16-bit counters stc[1] (stages 0, 2) and stc[2] (1, 3)
+  uint32_t stc[4] = {0u, 0u, 0u, 0u};
   uint32_t n_matched = 0, n_bytes = 0;  // per lane
   uint32_t n_lline = 0;                 // per lane: bytes of the phase-3 line stores
   uint32_t w_bytes = 0, w_line = 0;     // wave-uniform
@@ -1679,6 +1680,11 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
       w_bytes += 4u * seg_n + 4u;
     }
     wave_fired += seg_n;
+    if constexpr (kStages4) {
+      stc[1] += stc[0] & 0x00FF00FFu;
+      stc[2] += (stc[0] >> 8) & 0x00FF00FFu;
+      stc[0] = 0u;
+    }
     if (kPersist && kDepth == 2) issue_tile(v, tile + 2u * gridDim.x);
   };
   if constexpr (!kPersist) {
@@ -1692,16 +1698,27 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
     }
   }
 
+  uint32_t st4[4] = {0u, 0u, 0u, 0u};
+  if constexpr (kStages4) {  // the lanes' 16-bit counters summed per stage (32-bit sums)
+    st4[0] = stc[1] & 0xFFFFu;
+    st4[1] = stc[2] & 0xFFFFu;
+    st4[2] = stc[1] >> 16;
+    st4[3] = stc[2] >> 16;
+  }
   for (int off = 32; off > 0; off >>= 1) {
     n_matched += __shfl_xor(n_matched, off);
     n_bytes += __shfl_xor(n_bytes, off);
     n_lline += __shfl_xor(n_lline, off);
+    if constexpr (kStages4) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) st4[st] += __shfl_xor(st4[st], off);
+    }
   }
   if (lane == 0) {
     if constexpr (kStages4) {
 #pragma unroll
       for (int st = 0; st < 4; ++st)
-        if (stc[st]) atomicAdd(&s_stat[3 + st], stc[st]);
+        if (st4[st]) atomicAdd(&s_stat[3 + st], st4[st]);
     }
     atomicAdd(&s_stat[0], n_matched);
     atomicAdd(&s_stat[1], wave_fired);
@@ -2167,6 +2184,7 @@ __device__ __forceinline__ void store_out(const CompactArgs& a, uint32_t at, uin
 // dispatch rounds of a ~3.5 us load chain (21 us); four per wave keep every wave resident.
 // kPacked: 4-byte records (kwk_fired_packed) instead of kwk_fired_rec — half the bytes written
 constexpr uint32_t kCompactSpw = 4;
+constexpr uint32_t kCompact16Spw = 4;  // segments per wave of the 2-byte compaction
 template <int kRec, bool kPacked = false, uint32_t kSpw = 1>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
@@ -3797,11 +3815,22 @@ __global__ __launch_bounds__(1024) void agg_final_kernel(const uint32_t* __restr
                                                          uint32_t n_masks, unsigned long long* __restrict__ counts,
                                                          const double* __restrict__ upart, uint32_t n_ublocks,
                                                          double* __restrict__ cluster, uint32_t usage,
-                                                         const unsigned long long* __restrict__ stats, uint32_t n_stages,
-                                                         double* __restrict__ out) {
+                                                         const unsigned long long* __restrict__ cum, uint32_t cum_rows,
+                                                         uint32_t n_stages, double* __restrict__ out) {
   __shared__ unsigned long long s[1024];
   __shared__ double s_clu[2];
+  __shared__ unsigned long long s_st[KWK_MAX_STAGES];
   const uint32_t t = threadIdx.x;
+  // per-stage transitions: the sweeps' statistics rows summed here (reduce_stats_kernel's words
+  // 3 + stage, without its launch)
+  if (t < KWK_MAX_STAGES) s_st[t] = 0;
+  __syncthreads();
+  for (uint32_t st = 0; st < n_stages; ++st) {  // uniform
+    unsigned long long v = 0;
+    for (uint32_t r = t; r < cum_rows; r += blockDim.x) v += cum[(uint64_t)r * kStatWords + 3 + st];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((t & 63) == 0 && v) atomicAdd(&s_st[st], v);
+  }
   if (n_cblocks) count_total_block(cpart, n_cblocks, n_masks, counts, s);
   // usage: 1 = sum the usage kernel's partials, 2 = no usage kernel ran (no nodes): pack the
   // cluster sums as they stand
@@ -3813,7 +3842,7 @@ __global__ __launch_bounds__(1024) void agg_final_kernel(const uint32_t* __restr
     s_clu[1] = cluster[1];
   }
   __syncthreads();
-  if (t < n_stages) out[t] = (double)stats[3 + t];
+  if (t < n_stages) out[t] = (double)s_st[t];
   else if (t < n_stages + n_masks) out[t] = (double)(n_cblocks ? s[t - n_stages] : counts[t - n_stages]);
   else if (usage && t < n_stages + n_masks + 2) out[t] = s_clu[t - n_stages - n_masks];
 }
@@ -5323,8 +5352,9 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
                      e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
   constexpr uint32_t W = kCompactSpw;
   if (mode == 2) {
-    hipLaunchKernelGGL(compact16_kernel<W>, dim3((n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock)), dim3(kBlock),
-                       0, e->stream, a);
+    constexpr uint32_t W16 = kCompact16Spw;
+    hipLaunchKernelGGL(compact16_kernel<W16>, dim3((n_waves + W16 * kWavesPerBlock - 1) / (W16 * kWavesPerBlock)),
+                       dim3(kBlock), 0, e->stream, a);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
@@ -6241,8 +6271,6 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
     HIP_TRY(hipMalloc(&e->d_agg_masks, sizeof(uint32_t) * kMaxCountMasks));
   }
   double* dst = out ? out : e->d_agg;
-  hipLaunchKernelGGL(reduce_stats_kernel, dim3(kStatWords), dim3(kBlock), 0, e->stream, e->d_cum, e->cum_rows, e->d_stats);
-  HIP_TRY(hipGetLastError());
   // count_total_kernel overwrites the counts it produces: zeroed only when no count runs.  The
   // masks go to the device only when they change (a pageable copy would stall the host, r3 trace)
   if (!(n_masks && e->n_active))
@@ -6293,7 +6321,7 @@ kwk_status kwk_aggregate(kwk_engine* e, uint32_t n_masks, const uint32_t* masks,
   // usage with no nodes: the cluster sums stay what the last kwk_usage left (as before)
   hipLaunchKernelGGL(agg_final_kernel, dim3(1), dim3(1024), 0, e->stream, e->d_count_part, n_cblocks, n_masks,
                      e->d_agg_counts, e->d_usage_part, n_ublocks, e->d_cluster, usage ? (run_usage ? 1u : 2u) : 0u,
-                     e->d_stats, n_stages, dst);
+                     e->d_cum, e->cum_rows, n_stages, dst);
   HIP_TRY(hipGetLastError());
   *n_out = n_stages + n_masks + (usage ? 2u : 0u);
   return KWK_OK;
