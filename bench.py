@@ -160,8 +160,9 @@ class Reporter:
 
 SWEEP_NAMES = {1: "sweep16_kernel", 2: "sweep16_fsm_kernel", 3: "sweepw_kernel<4>", 4: "sweepw_kernel<8>",
                5: "sweep8_kernel"}  # kwk_last_sweep kernel codes (KWK_SWEEP_*)
-EV_EVERY = 4  # HIP events bracket the pod sweep of every 4th step (5 launches of 20): each marker pair idles
-              # the stream ~4.7 us (r4e trace), 1.2 us per step at this spacing instead of 2.4 us every 2nd step
+EV_EVERY = 10  # HIP events bracket the pod sweep of every 10th step (2 launches of 20, 5 of the default 50):
+               # each marker idles the stream ~4.6-7 us (r4e / r4w traces), ~0.9 us per step at this spacing
+               # (2.3 us every 4th step); the kernel trace of the same command cross-checks the mean
 
 
 # --handback: kwk_step_n's compaction (2-byte records where the sweep has them / 4-byte packed / kwk_fired_rec)
