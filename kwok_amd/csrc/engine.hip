@@ -1440,8 +1440,10 @@ __device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, 
   }
 }
 
+// one tile per workgroup (small engines, the strong-scaling shards): 6 workgroups per CU (<= 80
+// VGPRs, 26.8 KB of LDS) so that a 12.5M-id shard's 1526 tiles are one dispatch round, not two
 template <bool kPersist, int kDepth, bool kStages4>
-__global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist ? 1 : 6))) void sweep8_kernel(SweepArgs a) {
   constexpr int Q = kQ8;
   constexpr int K = 16 * Q;                // ids per lane
   constexpr uint32_t kWave = 64u * K;      // ids per wave region
@@ -1451,7 +1453,8 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   static_assert(kWave == 2048 && K == 32, "11-bit record offsets, 32-bit lane masks");
   __shared__ __attribute__((aligned(2048))) uint32_t s_tile[kWavesPerBlock][4 * Q][64];
   __shared__ __attribute__((aligned(16))) uint16_t s_work[kWavesPerBlock][kWave];
-  __shared__ uint32_t s_inv[kWavesPerBlock][64];  // kIdInvalid bytes: the inactive lanes' entries
+  __shared__ uint32_t s_inv[64];  // kIdInvalid bytes: the inactive lanes' entries (shared by the waves:
+                                  // they only ever write 0xFF back)
   __shared__ uint32_t s_fsm[512];
   __shared__ unsigned int s_stat[kStatWords];
   const uint32_t lane = threadIdx.x & 63;
@@ -1484,7 +1487,7 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
     s_fsm[threadIdx.x + kBlock] = t1;
   }
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
-  s_inv[wave][lane] = 0xFFFFFFFFu;
+  if (wave == 0) s_inv[lane] = 0xFFFFFFFFu;
   __syncthreads();
 
   // kStages4: stc[0] = this tile's fired records of stages 0-3 as byte counters (<= 32 items per lane
@@ -1499,7 +1502,7 @@ __global__ __launch_bounds__(kBlock) void sweep8_kernel(SweepArgs a) {
   const __amdgpu_buffer_rsrc_t gq_rs = make_rsrc(a.st, (a.n + 2047u) & ~2047u);  // whole lines of the padded column
   const uint32_t tile_lds = lds_addr(tw);  // 2 KiB aligned
   const uint32_t lane4 = lane * 4u;
-  const uint32_t inv_ent = lds_addr(&s_inv[wave][lane]);
+  const uint32_t inv_ent = lds_addr(&s_inv[lane]);
 
   // tile_body also runs for one tile past the last (the second half of the last pair of the
   // persistent loop, which has no exit in between: the in-order wait counts stay the same on

@@ -16,6 +16,7 @@
 #                              125k / 250k / 500k nodes) + a kernel trace of the 125k-node shard
 #   dist                       2 ranks sharing the GPU over gloo (the N > 1 bench path) vs one rank
 #   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/ab/<so>, alternating x2
+#   abshard=<so>               the same A/B at the N = 8 shard size (125k nodes / 12.5M pods)
 #   abemit=<so>                same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>
 #   variants=<args>           tools/variants.py run <args> (cost-isolation builds)
 set -o pipefail
@@ -139,6 +140,18 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
           timeout -k 10 200 python -u bench.py $B1 --no-pmc --no-cpu-baseline > $O/${v}_$i.json 2> $O/${v}_$i.err \
             || { cp $O/cur.so kwok_amd/lib/libkwok_engine.so; tail -20 $O/${v}_$i.err; exit 1; }
           python -c "import json; d=json.load(open('$O/${v}_$i.json')); print('$v', $i, d['value'], 'ms/step', d['ms_per_step'], 'sweep us', d['detail']['pod_sweep_us_mean'])"
+        done
+      done
+      cp $O/cur.so kwok_amd/lib/libkwok_engine.so && rm -f $O/cur.so ;;
+    abshard)  # same-box A/B at the N = 8 shard size (125k nodes): in-tree engine vs tools/ab/<so>, alternating x2
+      cp kwok_amd/lib/libkwok_engine.so $O/cur.so
+      S="--nodes 125000 --no-cpu-baseline --no-pmc --hbm-nodes 0 --pcie-steps 0 --emit-steps 0 --steps 40 --warmup 5"
+      for i in 1 2; do
+        for v in cur other; do
+          if [ $v = other ]; then cp tools/ab/$arg kwok_amd/lib/libkwok_engine.so; else cp $O/cur.so kwok_amd/lib/libkwok_engine.so; fi
+          timeout -k 10 200 python -u bench.py $S > $O/sh_${v}_$i.json 2> $O/sh_${v}_$i.err \
+            || { cp $O/cur.so kwok_amd/lib/libkwok_engine.so; tail -20 $O/sh_${v}_$i.err; exit 1; }
+          python -c "import json; d=json.load(open('$O/sh_${v}_$i.json')); print('$v', $i, d['value'], 'ms/step', d['ms_per_step'], 'sweep us', d['detail']['pod_sweep_us_mean'])"
         done
       done
       cp $O/cur.so kwok_amd/lib/libkwok_engine.so && rm -f $O/cur.so ;;
