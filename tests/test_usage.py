@@ -242,15 +242,18 @@ def test_gpu_usage_irregular_nodes(state):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_pods", [6000, 5997])
 @pytest.mark.parametrize("state", ["auto", "u32", "dw", "wide"])
-def test_gpu_usage_fast_path_irregular_nodes(state):
+def test_gpu_usage_fast_path_irregular_nodes(state, n_pods):
     """The uniform-container configuration (no mixed pods, no per-pod outputs) takes
-    usage_fast_kernel: same irregular node layout, node sums and integrators vs the oracle."""
+    usage_fast_kernel: same irregular node layout, node sums and integrators vs the oracle.
+    5997 pods: the state / key columns end inside a dword (the buffer resources' range check
+    works per dword: round 4 found the last pods read as dead there)."""
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
 
-    cl, pods = _cluster(n_nodes=40, n_pods=6000, seed=23)
+    cl, pods = _cluster(n_nodes=40, n_pods=n_pods, seed=23)
     ptr = _irregular_node_ptr(len(pods))
     text = open(GOLDEN).read()
     prog = UsageProgram(*load_usage_yaml(text))
