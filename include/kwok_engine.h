@@ -231,6 +231,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                   the look-back measured 73 us against 27 us at C5) */
 #define KWK_TUNE_AGG_FUSED 13  /* kwk_aggregate with KWK_AGG_USAGE on 1-byte ids: the <= 4 mask counts taken inside the
                                   usage kernel's pass over the id column, 1 (default), or 0 (a count pass of their own) */
+#define KWK_TUNE_STREAM_PRIORITY 15 /* the engine's stream: 0 (default priority), 1 (the device's greatest) or 2 (its
+                                       least); re-created after a synchronise, so set it between steps */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */

@@ -4803,6 +4803,18 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_AGG_FUSED: 0 or 1");
       e->agg_fused = value != 0;
       return KWK_OK;
+    case KWK_TUNE_STREAM_PRIORITY: {  // the engine's stream re-created at the HIP priority asked for
+      if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_STREAM_PRIORITY: 0 (default), 1 (greatest) or 2 (least)");
+      if (kwk_status st = set_dev(e)) return st;
+      int least = 0, greatest = 0;
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      hipStream_t ns = nullptr;
+      HIP_TRY(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, value == 1 ? greatest : value == 2 ? least : 0));
+      HIP_TRY(hipStreamDestroy(e->stream));
+      e->stream = ns;
+      return KWK_OK;
+    }
     case KWK_TUNE_USAGE_ROWS:
       if (value < 1 || value > 16) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_ROWS: 1..16");
       e->usage_rows = value;

@@ -100,6 +100,7 @@ TUNE_WORD_TILES = 10
 TUNE_COMPACT_LB = 11
 TUNE_USAGE_ROWS = 12
 TUNE_AGG_FUSED = 13
+TUNE_STREAM_PRIORITY = 15
 
 
 class Lease(C.Structure):
