@@ -603,8 +603,9 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
 
 struct kwk_emitter {
   std::string err;
-  kwk_engine* eng = nullptr;
-  hipStream_t stream = nullptr;
+  kwk_engine* eng = nullptr;  // must outlive the emitter
+  hipStream_t stream = nullptr;  // the engine's stream as of the current call (kwk_stream at every entry:
+                                 // KWK_TUNE_STREAM_PRIORITY re-creates it, so it is never cached across calls)
   int device = 0;
   uint32_t capacity = 0, n_columns = 0, max_tiles = 0, grid = 0;
   Prog p{};
@@ -624,7 +625,8 @@ struct kwk_emitter {
 
   ~kwk_emitter() {
     hipSetDevice(device);
-    if (stream) hipStreamSynchronize(stream);
+    void* s = nullptr;
+    if (eng && kwk_stream(eng, &s) == KWK_OK && s) hipStreamSynchronize(static_cast<hipStream_t>(s));
     for (void* x : allocs) hipFree(x);
     if (d_items) hipFree(d_items);
     if (d_offsets) hipFree(d_offsets);
@@ -636,12 +638,44 @@ struct kwk_emitter {
 
 namespace {
 
+// the engine's current stream and device (every entry point: the stream may have been re-created)
+kwk_status bind(kwk_emitter* em) {
+  void* s = nullptr;
+  if (kwk_stream(em->eng, &s) != KWK_OK || !s)
+    return fail(KWK_ESTATE, std::string("kwk_stream: ") + kwk_last_error(em->eng));
+  em->stream = static_cast<hipStream_t>(s);
+  HIP_TRY(hipSetDevice(em->device));
+  return KWK_OK;
+}
+
+// host -> device copy ordered on the engine's stream (a pageable hipMemcpy on the null stream can
+// return with its DMA in flight, and the engine's non-blocking stream would not wait for it)
+kwk_status copy_in(kwk_emitter* em, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return KWK_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, em->stream));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  return KWK_OK;
+}
+
+kwk_status copy_out(kwk_emitter* em, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return KWK_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, em->stream));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  return KWK_OK;
+}
+
+kwk_status fill(kwk_emitter* em, void* dst, int v, size_t bytes) {
+  HIP_TRY(hipMemsetAsync(dst, v, bytes, em->stream));
+  HIP_TRY(hipStreamSynchronize(em->stream));
+  return KWK_OK;
+}
+
 template <typename T>
 kwk_status upload(kwk_emitter* em, T** dst, const T* src, size_t n) {
   void* d = nullptr;
   HIP_TRY(hipMalloc(&d, std::max<size_t>(1, n) * sizeof(T)));
   em->allocs.push_back(d);
-  if (n) HIP_TRY(hipMemcpy(d, src, n * sizeof(T), hipMemcpyHostToDevice));
+  if (kwk_status st = copy_in(em, d, src, n * sizeof(T))) return st;
   *dst = static_cast<T*>(d);
   return KWK_OK;
 }
@@ -708,7 +742,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
     void* d = nullptr;
     HIP_TRY(hipMalloc(&d, (size_t)em->capacity * em->stride[c] + 1));
     em->allocs.push_back(d);
-    HIP_TRY(hipMemset(d, 0xFF, (size_t)em->capacity * em->stride[c] + 1));  // every value unusable until set
+    if (kwk_status st = fill(em, d, 0xFF, (size_t)em->capacity * em->stride[c] + 1)) return st;  // unusable until set
     em->cols.push_back(static_cast<uint8_t*>(d));
   }
   if (kwk_status st = upload(em, const_cast<uint8_t***>(&em->p.cols), em->cols.data(), em->cols.size())) return st;
@@ -716,7 +750,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   void* d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)std::max(1u, em->capacity) * 8));
   em->allocs.push_back(d);
-  HIP_TRY(hipMemset(d, 0, (size_t)std::max(1u, em->capacity) * 8));  // class 0, nothing accepted: all to the host
+  if (kwk_status st = fill(em, d, 0, (size_t)std::max(1u, em->capacity) * 8)) return st;  // class 0, nothing accepted: all to the host
   em->d_words = static_cast<uint64_t*>(d);
   em->max_tiles = (em->capacity + kTile - 1) / kTile + 1;
   HIP_TRY(hipMalloc(&d, (size_t)em->max_tiles * 4));
@@ -728,7 +762,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   HIP_TRY(hipMalloc(&d, 4 * 8));
   em->allocs.push_back(d);
   em->d_totals = static_cast<unsigned long long*>(d);
-  HIP_TRY(hipMemset(d, 0, 4 * 8));
+  if (kwk_status st = fill(em, d, 0, 4 * 8)) return st;
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, em->device));
   em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 8u));
@@ -759,8 +793,7 @@ kwk_status kwk_emitter_create(kwk_engine* eng, uint32_t capacity, const kwk_emit
     delete em;
     return fail(KWK_EHIP, std::string("hipStreamGetDevice: ") + hipGetErrorString(e));
   }
-  kwk_status st = KWK_OK;
-  if (hipSetDevice(em->device) != hipSuccess) st = fail(KWK_EHIP, "hipSetDevice");
+  kwk_status st = bind(em);
   if (!st) st = emitter_init(em, prog);
   if (st) {
     delete em;
@@ -779,20 +812,16 @@ kwk_status kwk_emit_set_words(kwk_emitter* em, uint32_t first, uint32_t n, const
   ErrScope es_(em ? &em->err : nullptr);
   if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
-  HIP_TRY(hipSetDevice(em->device));
-  HIP_TRY(hipStreamSynchronize(em->stream));
-  if (n) HIP_TRY(hipMemcpy(em->d_words + first, words, (size_t)n * 8, hipMemcpyHostToDevice));
-  return KWK_OK;
+  if (kwk_status st = bind(em)) return st;
+  return copy_in(em, em->d_words + first, words, (size_t)n * 8);
 }
 
 kwk_status kwk_emit_get_words(kwk_emitter* em, uint32_t first, uint32_t n, uint64_t* words) {
   ErrScope es_(em ? &em->err : nullptr);
   if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
-  HIP_TRY(hipSetDevice(em->device));
-  HIP_TRY(hipStreamSynchronize(em->stream));
-  if (n) HIP_TRY(hipMemcpy(words, em->d_words + first, (size_t)n * 8, hipMemcpyDeviceToHost));
-  return KWK_OK;
+  if (kwk_status st = bind(em)) return st;
+  return copy_out(em, words, em->d_words + first, (size_t)n * 8);
 }
 
 kwk_status kwk_emit_set_column(kwk_emitter* em, uint32_t c, uint32_t first, uint32_t n, const uint8_t* data) {
@@ -800,17 +829,14 @@ kwk_status kwk_emit_set_column(kwk_emitter* em, uint32_t c, uint32_t first, uint
   if (!em || (n && !data)) return fail(KWK_EINVAL, "null argument");
   if (c >= em->n_columns) return fail(KWK_EINVAL, "column out of range");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
-  HIP_TRY(hipSetDevice(em->device));
-  HIP_TRY(hipStreamSynchronize(em->stream));
-  if (n)
-    HIP_TRY(hipMemcpy(em->cols[c] + (size_t)first * em->stride[c], data, (size_t)n * em->stride[c], hipMemcpyHostToDevice));
-  return KWK_OK;
+  if (kwk_status st = bind(em)) return st;
+  return copy_in(em, em->cols[c] + (size_t)first * em->stride[c], data, (size_t)n * em->stride[c]);
 }
 
 kwk_status kwk_emit_reserve(kwk_emitter* em, uint32_t max_items, uint64_t max_bytes) {
   ErrScope es_(em ? &em->err : nullptr);
   if (!em) return fail(KWK_EINVAL, "null emitter");
-  HIP_TRY(hipSetDevice(em->device));
+  if (kwk_status st = bind(em)) return st;
   HIP_TRY(hipStreamSynchronize(em->stream));
   if (max_items > em->cap_items) {
     if (em->d_items) HIP_TRY(hipFree(em->d_items));
@@ -847,7 +873,7 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   } else {
     return fail(KWK_EINVAL, "source must be KWK_EMIT_FROM_RECORDS or KWK_EMIT_FROM_PACKED");
   }
-  HIP_TRY(hipSetDevice(em->device));
+  if (kwk_status st = bind(em)) return st;
   if (!em->d_offsets)
     if (kwk_status st = kwk_emit_reserve(em, 1, 1)) return st;
   a.words = em->d_words;
@@ -895,10 +921,9 @@ kwk_status kwk_emit_result(kwk_emitter* em, uint32_t* n_items, uint64_t* n_bytes
   ErrScope es_(em ? &em->err : nullptr);
   if (!em || !n_items || !n_bytes) return fail(KWK_EINVAL, "null argument");
   if (!em->emitted) return fail(KWK_ESTATE, "kwk_emit must come first");
-  HIP_TRY(hipSetDevice(em->device));
-  HIP_TRY(hipStreamSynchronize(em->stream));
+  if (kwk_status st = bind(em)) return st;
   unsigned long long t[3];
-  HIP_TRY(hipMemcpy(t, em->d_totals, sizeof t, hipMemcpyDeviceToHost));
+  if (kwk_status st = copy_out(em, t, em->d_totals, sizeof t)) return st;
   *n_items = (uint32_t)t[0];
   *n_bytes = t[1];
   if (t[2]) return fail(KWK_ECAP, "the fired list is longer than the emitter's capacity");
@@ -913,7 +938,7 @@ kwk_status kwk_emit_stats(kwk_emitter* em, uint32_t* n_items, uint32_t* n_emitte
   if (!em || !n_items || !n_emitted || !n_bytes) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = kwk_emit_result(em, n_items, n_bytes)) return st;
   unsigned long long t = 0;
-  HIP_TRY(hipMemcpy(&t, em->d_totals + 3, 8, hipMemcpyDeviceToHost));
+  if (kwk_status st = copy_out(em, &t, em->d_totals + 3, 8)) return st;
   *n_emitted = (uint32_t)t;
   return KWK_OK;
 }
@@ -933,10 +958,13 @@ kwk_status kwk_emit_copy(kwk_emitter* em, kwk_emit_item* items, uint64_t* offset
   uint64_t nb = 0;
   if (kwk_status st = kwk_emit_result(em, &ni, &nb)) return st;
   if ((ni && (!items || !offsets)) || (nb && !bytes) || !offsets) return fail(KWK_EINVAL, "null argument");
-  if (ni) HIP_TRY(hipMemcpy(items, em->d_items, (size_t)ni * sizeof(kwk_emit_item), hipMemcpyDeviceToHost));
-  if (ni) HIP_TRY(hipMemcpy(offsets, em->d_offsets, ((size_t)ni + 1) * 8, hipMemcpyDeviceToHost));
-  else offsets[0] = 0;
-  if (nb) HIP_TRY(hipMemcpy(bytes, em->d_out, (size_t)nb, hipMemcpyDeviceToHost));
+  if (ni) {
+    if (kwk_status st = copy_out(em, items, em->d_items, (size_t)ni * sizeof(kwk_emit_item))) return st;
+    if (kwk_status st = copy_out(em, offsets, em->d_offsets, ((size_t)ni + 1) * 8)) return st;
+  } else {
+    offsets[0] = 0;
+  }
+  if (kwk_status st = copy_out(em, bytes, em->d_out, (size_t)nb)) return st;
   return KWK_OK;
 }
 
@@ -944,7 +972,7 @@ kwk_status kwk_emit_elapsed(kwk_emitter* em, float* ms) {
   ErrScope es_(em ? &em->err : nullptr);
   if (!em || !ms) return fail(KWK_EINVAL, "null argument");
   if (!em->emitted) return fail(KWK_ESTATE, "kwk_emit must come first");
-  HIP_TRY(hipSetDevice(em->device));
+  if (kwk_status st = bind(em)) return st;
   HIP_TRY(hipEventSynchronize(em->ev1));
   HIP_TRY(hipEventElapsedTime(ms, em->ev0, em->ev1));
   return KWK_OK;

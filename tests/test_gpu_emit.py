@@ -172,3 +172,74 @@ def test_gpu_emit_c1_pod_fast_equals_native_render():
     cl = W.make_cluster("C1", 20, 300, seed=92)
     c = _run(cl, steps=8, dt_ns=10**9, seed=0x92)
     assert c["device"] >= 300 and c["host"] == 0, c
+
+
+def test_gpu_emit_after_stream_recreated_and_column_rewritten():
+    """Stream ordering: the emitter is created before KWK_TUNE_STREAM_PRIORITY re-creates
+    the engine's stream; its value columns are first filled with decoy call values, then rewritten
+    whole (a multi-MB upload) and the step is emitted at once.  Every device item must equal the
+    native render, so the emission ran on the live stream and after the rewrite landed."""
+    from kwok_amd.host import abi, emit
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.controller import KindController
+    from kwok_amd.host.encoder import NativeIngest
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    from tests.parity_util import NOW0
+    from tests.test_patch import FUNCS
+    cl = W.make_cluster("C1", 400, 40000, seed=93)
+    objs = cl.pods.materialize()
+    prog = KindProgram(load_stage_files(*cl.pod_stage_files))
+    prog.explore(objs)
+    nat = NativeIngest(prog)
+    hot, dels, rec, cls = nat.columns(objs)
+    eng = Engine(prog, capacity=len(objs), max_records=len(nat.record_array()) + 64)
+    ctl = KindController(prog, eng, Ingest(prog), objs, funcs=FUNCS, native=True)
+    classes = [prog.class_of(o, register=False) for o in ctl.objs]
+    reps = {}
+    for o, c in zip(ctl.objs, classes):
+        reps.setdefault(c, o)
+    ep = emit.EmitProgram(prog.stages, ctl.patcher, reps, len(prog.class_ids))
+    em = emit.Emitter(eng, len(objs), ep)
+    try:
+        words, cols = ep.rows(ctl.objs, classes)
+        assert ep.n_columns >= 1
+        decoy = {}
+        for c, rows in cols.items():
+            d = np.zeros_like(rows)
+            d[:, 0] = 7
+            d[:, 1:8] = np.frombuffer(b"9.9.9.9", dtype=np.uint8)
+            decoy[c] = d
+        em.set_rows(0, words, decoy)
+        eng.set_tuning(abi.TUNE_STREAM_PRIORITY, 1)   # the stream the emitter saw at create is gone
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, nat.record_array())
+        n_dev = 0
+        for k in range(3):
+            now = NOW0 + k * 10**9
+            if k == 1:
+                eng.set_tuning(abi.TUNE_STREAM_PRIORITY, 2)
+            for c, rows in cols.items():            # the real values, rewritten whole right before the emit
+                em.set_column(c, 0, rows)
+            eng.step(now, 0x93, k)
+            eng.fired_compact(packed=True)
+            items, offs, out = em.run(now, packed=True)
+            fired = eng.fired()
+            ctl.handle(fired, now)
+            pos = collections.Counter()
+            for n, it in enumerate(items):
+                r = int(it["rec"])
+                slot = int(fired[r]["slot"])
+                pi = pos[r]
+                pos[r] += 1
+                assert int(it["status"]) == emit.STATUS_OK, (k, slot)
+                assert out[int(offs[n]):int(offs[n + 1])] == ctl.last_patches[(slot, pi)], (k, slot)
+                n_dev += 1
+            for c in cols:                           # decoys again: a later emit must not see them
+                em.set_column(c, 0, decoy[c])
+        assert n_dev >= 40000, n_dev
+    finally:
+        em.close()
+        ctl.close()
+        nat.close()
+        eng.close()

@@ -448,3 +448,108 @@ def test_c3_config_size_tick_n_sampled_oracle():
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.gpu
+def test_tick_disregarded_nodes_are_not_managed():
+    """a node need() rejects (node_controller.go:186-200) never gets putNodeInfo /
+    onNodeManagedFunc, so kwok never calls TryHold for its Lease and its pods are never managed
+    (nodeGetFunc fails, pod_controller.go:393-395).  The host duty: such a node's
+    lease record goes to kwk_lease_set without HOLD / QUEUED, and its pods are upserted with
+    KWK_F_MANAGED clear.  A third of 3000 nodes carry pool=frozen (the disregard label selector);
+    kwk_tick_n over 40 ticks: no lease write, fire or MANAGED bit ever touches them or their pods,
+    while every other node's leases, nodes and pods stay bit-exact against the oracle
+    (lease_ref.LeaseSim + OracleSim with the same filter)."""
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.labelsel import DisregardSpec
+    from kwok_amd.host.stages import load_stage_files
+    from oracle.next_ref import load_stage_docs
+    from oracle.sim import OracleSim
+    from tests.parity_util import NOW0, compare_state
+    n_nodes, ppn, me = 3000, 2, 1
+    n_pods = n_nodes * ppn
+    rng = np.random.default_rng(37)
+    frozen = np.arange(n_nodes) % 3 == 0
+    leases = c3_leases(n_nodes, NOW0, rng)
+    for i in np.flatnonzero(frozen):  # no TryHold: not in holdLeaseSet, nothing queued
+        leases[i].flags &= ~(LR.HOLD | LR.QUEUED)
+        leases[i].next_try_ns = 0
+    nfiles, pfiles = W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), W.stage_paths(W.POD_FAST)
+    nodes = [W.node_object(f"node-{i}", labels={"pool": "frozen"} if frozen[i] else None) for i in range(n_nodes)]
+    pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+    pidx = (np.arange(n_pods) % 10 == 3).astype(np.int32)
+    pods = [pvars[int(k)] for k in pidx]
+    node_ptr = np.arange(0, n_pods + 1, ppn, dtype=np.uint32)
+    held0 = np.array([LR.held(L, me) for L in leases])
+    dg = DisregardSpec(label_selector="pool=frozen")
+    engines = []
+    try:
+        nprog = KindProgram(load_stage_files(*nfiles), None, disregard=dg)
+        nprog.explore(nodes)
+        ning = Ingest(nprog)
+        nhot, ndels, nrec, ncls = ning.columns(nodes)
+        nhot["sched"][~held0] &= ~np.uint32(abi.F_MANAGED)
+        pprog = KindProgram(load_stage_files(*pfiles), HarnessSpec())
+        pprog.explore(pvars)
+        ping = Ingest(pprog)
+        phot, pdels, prec, pcls = ping.variant_columns(pvars, pidx)
+        pod_node = np.arange(n_pods) // ppn
+        phot["sched"][~held0[pod_node] | frozen[pod_node]] &= ~np.uint32(abi.F_MANAGED)
+        neng = Engine(nprog, capacity=n_nodes, kind_salt=1)
+        engines.append(neng)
+        peng = Engine(pprog, capacity=n_pods)
+        engines.append(peng)
+        neng.load_stages()
+        neng.load(nhot, ndels, nrec, ncls, ning.record_array())
+        peng.load_stages()
+        peng.set_harness(True)
+        peng.load(phot, pdels, prec, pcls, ping.record_array())
+        neng.lease_config(me, 40, 10 * 10**9, 0.04)
+        neng.lease_set(to_array(leases))
+        peng.tick_bind(neng, node_ptr)
+        lsim = LR.LeaseSim(leases, me, 40, 10 * 10**9, 0.04, kind_salt=1)
+        nsim = OracleSim(load_stage_docs(*nfiles), nodes, kind_salt=1,
+                         disregard=(dg.annotation_selector, dg.label_selector))
+        psim = OracleSim(load_stage_docs(*pfiles), pods, harness=True)
+        for i in range(n_nodes):
+            nsim.managed[i] = bool(held0[i])
+            for q in range(ppn):
+                psim.managed[i * ppn + q] = bool(held0[i]) and not frozen[i]
+        frozen_pods = set(np.flatnonzero(frozen[pod_node]).tolist())
+        frozen_nodes = set(np.flatnonzero(frozen).tolist())
+        seed, dt = 0x7B, 250 * 10**6
+        counts = {"ops": 0, "node": 0, "pod": 0}
+        for k in range(40):
+            now = NOW0 + k * dt
+            neng.tick_n(peng, 1, now, dt, seed, k, compact=True)
+            ops = lsim.step(now, seed, k)
+            for j, op in ops:
+                h = LR.held(lsim.leases[j], me)
+                nsim.set_managed(j, h, op != LR.OP_BUSY)
+                for q in range(ppn):
+                    psim.set_managed(j * ppn + q, h, op != LR.OP_BUSY)
+            nexp, pexp = nsim.step(now, seed, k), psim.step(now, seed, k)
+            got_ops = neng.lease_ops()
+            assert sorted((int(r["slot"]), int(r["stage"])) for r in got_ops) == sorted(ops), f"tick {k}: lease ops"
+            assert not {int(r["slot"]) for r in got_ops} & frozen_nodes, k
+            assert_leases_equal(neng.lease_read(), lsim.leases, k)
+            for eng, sim, prog, exp, name, frz in ((neng, nsim, nprog, nexp, "node", frozen_nodes),
+                                                  (peng, psim, pprog, pexp, "pod", frozen_pods)):
+                f = eng.fired()
+                got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in f)
+                assert got == sorted(exp), f"tick {k}: {name} fired"
+                assert not {g[0] for g in got} & frz, (k, name)
+                compare_state(prog, eng, sim, k)
+                hot, _ = eng.read()
+                managed = (hot["sched"] & np.uint32(abi.F_MANAGED)) != 0
+                assert managed.tolist() == list(sim.managed), f"tick {k}: {name} managed"
+                if name == "pod":
+                    assert not managed[sorted(frz)].any(), k
+                counts[name] += len(exp)
+            counts["ops"] += len(ops)
+        assert counts["ops"] > 0 and counts["node"] > 0 and counts["pod"] > 0, counts
+    finally:
+        for e in engines:
+            e.close()
