@@ -23,9 +23,11 @@ PATCH_SRC = [os.path.join(PKG, "csrc", "patch.cpp")]
 PATCH_HDR = [os.path.join(ROOT, "include", "kwok_patch.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR,
              os.path.join(PKG, "csrc", "timefmt.hpp")]
 PATCH_OUT = os.path.join(PKG, "lib", "libkwok_patch.so")
-COMPILER_SRC = [os.path.join(PKG, "csrc", "compiler.cpp")]
-COMPILER_HDR = [os.path.join(ROOT, "include", "kwok_compiler.h"), os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR] + \
-    [os.path.join(PKG, "csrc", h) for h in ("host_common.hpp", "gotpl.hpp", "patchtpl.hpp", "nextstate.hpp", "labelsel.hpp")]
+COMPILER_SRC = [os.path.join(PKG, "csrc", "compiler.cpp"), os.path.join(PKG, "csrc", "metrics_compiler.cpp")]
+COMPILER_HDR = [os.path.join(ROOT, "include", "kwok_compiler.h"), os.path.join(ROOT, "include", "kwok_metrics.h"),
+                os.path.join(ROOT, "include", "kwok_engine.h"), DOM_HDR] + \
+    [os.path.join(PKG, "csrc", h) for h in ("host_common.hpp", "gotpl.hpp", "patchtpl.hpp", "nextstate.hpp", "labelsel.hpp",
+                                            "celc.hpp")]
 COMPILER_OUT = os.path.join(PKG, "lib", "libkwok_compiler.so")
 COMM_SRC = [os.path.join(PKG, "csrc", "comm.cpp")]
 COMM_HDR = [os.path.join(ROOT, "include", "kwok_comm.h"), os.path.join(ROOT, "include", "kwok_engine.h")]
@@ -64,7 +66,8 @@ def build_encoder(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_compiler(force: bool = False, verbose: bool = False) -> str:
-    """The native Stage compiler (lifecycle.NewLifecycle behind the C ABI)."""
+    """The native Stage compiler (lifecycle.NewLifecycle behind the C ABI) and Metric CR compiler
+    (kwok_metrics.h)."""
     return _host_lib(COMPILER_OUT, COMPILER_SRC, COMPILER_HDR, force, verbose)
 
 

@@ -405,32 +405,20 @@ class Engine:
     # Metric CRD values (kwok_amd/host/metrics.py)
     def metrics_load(self, programs):
         """programs: [(dimension name, [(op, arg), ...])] from cel.lower()."""
-        from . import cel
-        descs = (abi.MetricDesc * max(1, len(programs)))()
-        flat = []
-        for i, (dim, prog) in enumerate(programs):
-            descs[i] = abi.MetricDesc(abi.METRIC_DIM[dim], len(flat), len(prog), 0)
-            flat += prog
-        ops = (abi.MetricOp * max(1, len(flat)))()
-        for i, (op, x) in enumerate(flat):
-            ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
-        self._check(abi.lib().kwk_metrics_load(self.h, len(programs), descs, len(flat), ops), "kwk_metrics_load")
+        n, descs, n_ops, ops = pack_metric_programs(programs)
+        self.metrics_load_arrays(n, descs, n_ops, ops)
+
+    def metrics_load_arrays(self, n, descs, n_ops, ops):
+        """kwk_metrics_load over packed kwk_metric_desc / kwk_metric_op arrays (pointers or ctypes
+        arrays: pack_metric_programs, or the native compiler's kwk_metric_set_programs)."""
+        self._check(abi.lib().kwk_metrics_load(self.h, n, descs, n_ops, ops), "kwk_metrics_load")
 
     def histograms_load(self, histograms):
         """histograms: [(dimension name, [(le, hidden, [(op, arg), ...]), ...])] (cel.lower per bucket)."""
-        from . import cel
-        descs = (abi.HistogramDesc * max(1, len(histograms)))()
-        buckets, flat = [], []
-        for i, (dim, bks) in enumerate(histograms):
-            descs[i] = abi.HistogramDesc(abi.METRIC_DIM[dim], len(buckets), len(bks), 0)
-            for le, hidden, prog in bks:
-                buckets.append(abi.MetricBucket(float(le), 1 if hidden else 0, len(flat), len(prog), 0))
-                flat += prog
-        barr = (abi.MetricBucket * max(1, len(buckets)))(*buckets)
-        ops = (abi.MetricOp * max(1, len(flat)))()
-        for i, (op, x) in enumerate(flat):
-            ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
-        self._check(abi.lib().kwk_histograms_load(self.h, len(histograms), descs, len(buckets), barr, len(flat), ops),
+        self.histograms_load_arrays(*pack_histogram_programs(histograms))
+
+    def histograms_load_arrays(self, n, descs, n_buckets, buckets, n_ops, ops):
+        self._check(abi.lib().kwk_histograms_load(self.h, n, descs, n_buckets, buckets, n_ops, ops),
                     "kwk_histograms_load")
 
     def histograms_eval(self, now_ns: int, node_first: int, n_nodes: int) -> np.ndarray:
@@ -568,3 +556,36 @@ class Engine:
         ms = C.c_float()
         self._check(abi.lib().kwk_event_elapsed(self.h, a, b, C.byref(ms)), "kwk_event_elapsed")
         return float(ms.value)
+
+
+def _pack_ops(flat):
+    from . import cel
+    ops = (abi.MetricOp * max(1, len(flat)))()
+    for i, (op, x) in enumerate(flat):
+        ops[i] = abi.MetricOp(op, int(x) if op == cel.OP_LOAD else 0, float(x) if op == cel.OP_CONST else 0.0)
+    return ops
+
+
+def pack_metric_programs(programs):
+    """[(dimension name, [(op, arg), ...])] -> (n, kwk_metric_desc array, n_ops, kwk_metric_op array),
+    the arrays kwk_metrics_load takes."""
+    descs = (abi.MetricDesc * max(1, len(programs)))()
+    flat = []
+    for i, (dim, prog) in enumerate(programs):
+        descs[i] = abi.MetricDesc(abi.METRIC_DIM[dim], len(flat), len(prog), 0)
+        flat += prog
+    return len(programs), descs, len(flat), _pack_ops(flat)
+
+
+def pack_histogram_programs(histograms):
+    """[(dimension name, [(le, hidden, [(op, arg), ...]), ...])] -> the six kwk_histograms_load
+    arguments after the engine."""
+    descs = (abi.HistogramDesc * max(1, len(histograms)))()
+    buckets, flat = [], []
+    for i, (dim, bks) in enumerate(histograms):
+        descs[i] = abi.HistogramDesc(abi.METRIC_DIM[dim], len(buckets), len(bks), 0)
+        for le, hidden, prog in bks:
+            buckets.append(abi.MetricBucket(float(le), 1 if hidden else 0, len(flat), len(prog), 0))
+            flat += prog
+    barr = (abi.MetricBucket * max(1, len(buckets)))(*buckets)
+    return len(histograms), descs, len(buckets), barr, len(flat), _pack_ops(flat)

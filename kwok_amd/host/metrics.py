@@ -130,12 +130,29 @@ def histogram_write(buckets: Sequence[Tuple[float, bool]], values: Sequence[int]
             "sum": total}
 
 
+def load_metric_doc(text: str) -> dict:
+    """The Metric document of a YAML text (what the Go host has decoded and hands the native
+    compiler as JSON)."""
+    for doc in yaml.safe_load_all(text):
+        if doc and doc.get("kind") == "Metric":
+            return doc
+    raise ValueError("no Metric document")
+
+
 class MetricsProgram:
-    def __init__(self, configs: Sequence[MetricConfig]):
+    def __init__(self, configs: Sequence[MetricConfig], native=None):
+        """native: a native_metrics.NativeMetricSet compiled from the same CR: the device programs
+        come from libkwok_compiler (kwk_compile_metrics) instead of cel.lower, and so does the list
+        of host-evaluated metrics."""
         self.configs = list(configs)
         self.programs = []          # gauges / counters, in config order
         self.hist_programs = []     # histograms, in config order: (dimension, [(le, hidden, program)])
         self.host_metrics: List[str] = []
+        self.native = native
+        if native is not None:
+            self.host_metrics = list(native.host_metrics)
+            self.hist_programs = [(m.dimension, None) for m in self.configs if m.kind == "histogram"]
+            return
         for m in self.configs:
             if m.kind == "histogram":
                 try:
@@ -152,7 +169,17 @@ class MetricsProgram:
                 self.host_metrics.append(m.name)
                 self.programs.append((m.dimension, [(cel.OP_CONST, math.nan)]))
 
+    @classmethod
+    def from_native(cls, text: str) -> "MetricsProgram":
+        """The Metric CR of a YAML text compiled by the native compiler (kwk_compile_metrics)."""
+        from .native_metrics import NativeMetricSet
+        _, configs = load_metric_yaml(text)
+        return cls(configs, native=NativeMetricSet(load_metric_doc(text)))
+
     def load(self, pods_engine):
+        if self.native is not None:
+            self.native.load(pods_engine)
+            return
         pods_engine.metrics_load(self.programs)
         if self.hist_programs:
             pods_engine.histograms_load(self.hist_programs)

@@ -31,7 +31,9 @@ def _header_functions():
 
 
 @pytest.mark.parametrize("header,lib", [("kwok_engine.h", "libkwok_engine.so"), ("kwok_encoder.h", "libkwok_encoder.so"),
-                                        ("kwok_patch.h", "libkwok_patch.so"), ("kwok_comm.h", "libkwok_comm.so")])
+                                        ("kwok_patch.h", "libkwok_patch.so"), ("kwok_comm.h", "libkwok_comm.so"),
+                                        ("kwok_compiler.h", "libkwok_compiler.so"), ("kwok_metrics.h", "libkwok_compiler.so"),
+                                        ("kwok_emit.h", "libkwok_emit.so")])
 def test_every_header_declaration_is_exported(header, lib):
     """Each C-ABI library loads (no GPU needed) and defines every function its include/*.h
     declares (a header's own declarations, not the engine types it includes)."""

@@ -92,11 +92,14 @@ def test_gauge_counter_exposition_matches_reference_text():
 
 
 @pytest.mark.gpu
-def test_gpu_metric_cr_reference_vectors():
+@pytest.mark.parametrize("compiler", ["native", "python"])
+def test_gpu_metric_cr_reference_vectors(compiler):
     """The gauge / counter / histogram CR above through kwk_metrics_eval / kwk_histograms_eval on
     every node of a small cluster: histogram bounds, cumulative counts and sample count exactly as
     histogram_test.go, the sum equal to Write's ascending accumulation; gauge and counter series
-    exposed exactly as gauge_test.go / counter_test.go expect after their last Set."""
+    exposed exactly as gauge_test.go / counter_test.go expect after their last Set.  The device
+    programs come from the native Metric CR compiler (kwk_compile_metrics, the Go host's path) or
+    from the Python lowering."""
     from kwok_amd import workload as W
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.engine import Engine, Ingest
@@ -117,8 +120,11 @@ def test_gpu_metric_cr_reference_vectors():
         eng.load(*ing.columns(pods), ing.record_array())
         eng.usage_config(cl.node_ptr, *cols)
         eng.usage_pods(True)
-        _, configs = load_metric_yaml(_metric_yaml())
-        mp = MetricsProgram(configs)
+        if compiler == "native":
+            mp = MetricsProgram.from_native(_metric_yaml())
+            assert mp.native is not None
+        else:
+            mp = MetricsProgram(load_metric_yaml(_metric_yaml())[1])
         assert mp.host_metrics == []
         mp.load(eng)
         eng.metrics_inputs(np.full(len(pods), np.iinfo(np.int64).min, dtype=np.int64),

@@ -105,7 +105,8 @@ def test_mixed_containers_get_mixed_entries():
 
 
 @pytest.mark.gpu
-def test_gpu_container_usage_and_metric_scrape():
+@pytest.mark.parametrize("compiler", ["native", "python"])
+def test_gpu_container_usage_and_metric_scrape(compiler):
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.engine import Engine, Ingest
     from kwok_amd.host.stages import load_stage_files
@@ -124,8 +125,8 @@ def test_gpu_container_usage_and_metric_scrape():
         eng.load(*ing.columns(pods), ing.record_array())
         eng.usage_config(cl.node_ptr, *cols)
         eng.usage_pods(True)
-        _, configs = load_metric_yaml(open(METRICS).read())
-        mp = MetricsProgram(configs)
+        text_cr = open(METRICS).read()
+        mp = MetricsProgram.from_native(text_cr) if compiler == "native" else MetricsProgram(load_metric_yaml(text_cr)[1])
         mp.load(eng)
         created = np.array([_ns(p["metadata"]["creationTimestamp"]) if "creationTimestamp" in p["metadata"]
                             else np.iinfo(np.int64).min for p in pods], dtype=np.int64)
@@ -276,7 +277,8 @@ def test_histogram_metric_yaml_lowers():
 
 
 @pytest.mark.gpu
-def test_gpu_histogram_metrics_scrape():
+@pytest.mark.parametrize("compiler", ["native", "python"])
+def test_gpu_histogram_metrics_scrape(compiler):
     """Histogram Metric CRs evaluated on the device (kwk_histograms_eval) against the oracle's
     restatement of updateHistogram + histogram.Write (oracle/metrics_ref.py), node by node over
     two evaluations with dead pods: bucket counts, sample counts exactly; sample sums within
@@ -299,8 +301,7 @@ def test_gpu_histogram_metrics_scrape():
         eng.load(*ing.columns(pods), ing.record_array())
         eng.usage_config(cl.node_ptr, *cols)
         eng.usage_pods(True)
-        _, configs = load_metric_yaml(HIST_YAML)
-        mp = MetricsProgram(configs)
+        mp = MetricsProgram.from_native(HIST_YAML) if compiler == "native" else MetricsProgram(load_metric_yaml(HIST_YAML)[1])
         mp.load(eng)
         alive = np.ones(len(pods), dtype=bool)
         t = 1_700_000_000 * 10**9
