@@ -375,3 +375,88 @@ def test_gpu_aggregate_counts_in_usage_pass(pods_per_node):
     finally:
         pods.close()
         nodes.close()
+
+
+def _mixed_usage_doc(name):
+    """A namespaced ResourceUsage named like the pod: container-1 evaluates apart from the others
+    (findUsageInUsages, metrics_resource_usage.go:226-264), so the pod takes kwk_usage_mixed."""
+    return {"apiVersion": "kwok.x-k8s.io/v1alpha1", "kind": "ResourceUsage",
+            "metadata": {"name": name, "namespace": "default"},
+            "spec": {"usages": [{"containers": ["container-1"],
+                                 "usage": {"cpu": {"value": "300m"}, "memory": {"value": "32Mi"}}},
+                                {"usage": {"cpu": {"value": "2"}, "memory": {"expression": 'Quantity("1Gi")'}}}]}}
+
+
+@pytest.mark.gpu
+def test_c4_config_size_sampled_oracle():
+    """C4 at its configuration size: 10k nodes / 1M pods, 1-4 containers per
+    pod, half of the pods annotated from the workload's usage values (usage-from-annotation), and
+    ~250 pods whose containers differ (a pod-named ResourceUsage: kwk_usage_mixed).  Over three
+    evaluations (pods deleted before the second), every 97th node's usage and cumulative usage
+    against the oracle's nodeResourceUsage / nodeResourceCumulativeUsage restatement (usage_ref)
+    within 1e-6 relative, and the cluster totals against the per-variant values summed exactly.
+    Reference: pkg/kwok/server/metrics_resource_usage.go:36-224."""
+    from kwok_amd.host.compiler import KindProgram
+    from kwok_amd.host.engine import Engine, Ingest
+    from kwok_amd.host.stages import load_stage_files
+    n_nodes, n_pods = 10_000, 1_000_000
+    cl = W.make_cluster("C4", n_nodes, n_pods, seed=44)
+    ptr = cl.node_ptr
+    pvars, pidx = cl.pods.variants, cl.pods.index
+    sample = list(range(3, n_nodes, 97))
+    mixed = sorted(set(range(17, n_pods, 4999)) | {int(ptr[j]) + 1 for j in sample[::2] if ptr[j + 1] - ptr[j] > 1})
+    mixed_objs = [cl.pods.materialize(i, i + 1)[0] for i in mixed]
+    text = open(GOLDEN).read()
+    extra = [_mixed_usage_doc(o["metadata"]["name"]) for o in mixed_objs]
+    docs = [d for d in yaml.safe_load_all(text) if d] + extra
+    prog = UsageProgram(*load_usage_yaml(text, yaml.safe_dump_all(extra)))
+    keys_all, cv, mv, mx, ck = usage_columns(prog, list(pvars) + mixed_objs)
+    keys = keys_all[:len(pvars)][pidx]
+    keys[mixed] = keys_all[len(pvars):]
+    assert mx is not None and len(mx) >= 2 and np.count_nonzero((keys >> 28) == 0) >= len(mixed) // 2
+    kp = KindProgram(load_stage_files(*cl.pod_stage_files))
+    kp.explore(pvars)
+    ing = Ingest(kp)
+    hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+    eng = Engine(kp, capacity=n_pods)
+    try:
+        eng.load_stages()
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        eng.usage_config(ptr, keys, cv, mv, mx, ck)
+        # the sampled nodes' pods, materialised once (the mixed ones carry their real names)
+        pods_of = {}
+        for j in sample:
+            objs = cl.pods.materialize(int(ptr[j]), int(ptr[j + 1]))
+            pods_of[j] = objs
+        val = {}  # (pod index, resource) -> the pod's usage (the oracle, once)
+        for j in sample:
+            for k, p in enumerate(pods_of[j]):
+                for r in ("cpu", "memory"):
+                    val[(int(ptr[j]) + k, r)] = usage_ref.node_usage(docs, [p], r)
+        # exact cluster totals from the per-variant values (+ the mixed pods)
+        var_val = {r: np.array([usage_ref.node_usage(docs[:1], [v], r) for v in pvars]) for r in ("cpu", "memory")}
+        mix_val = {r: np.array([usage_ref.node_usage(docs, [o], r) for o in mixed_objs]) for r in ("cpu", "memory")}
+        alive = np.ones(n_pods, dtype=bool)
+        cum = usage_ref.Cumulative()
+        t = 1_700_000_000 * 10**9
+        for k in range(3):
+            if k == 1:
+                gone = np.arange(11, n_pods, 13)
+                eng.delete(gone)
+                alive[gone] = False
+            eng.usage(t)
+            node, total = eng.usage_read()
+            for j in sample:
+                lo, hi = int(ptr[j]), int(ptr[j + 1])
+                want = [sum(val[(i, r)] for i in range(lo, hi) if alive[i]) for r in ("cpu", "memory")]
+                wc = [cum.advance((j, r), want[q], t) for q, r in enumerate(("cpu", "memory"))]
+                np.testing.assert_allclose(node[j], want + wc, rtol=REL_TOL, atol=0, err_msg=f"evaluation {k}, node {j}")
+            plain = alive.copy()
+            plain[mixed] = False
+            for q, r in enumerate(("cpu", "memory")):
+                exact = float(np.bincount(pidx[plain], minlength=len(pvars)) @ var_val[r]) + \
+                    float(mix_val[r][alive[mixed]].sum())
+                assert total[q] == pytest.approx(exact, rel=REL_TOL), (k, r)
+            t += 2_500_000_000 + 123_457 * k
+    finally:
+        eng.close()
