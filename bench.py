@@ -583,8 +583,6 @@ def main():
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
     ap.add_argument("--tune-sweep-blocks", type=int, default=0,
                     help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
-    ap.add_argument("--tune-compact-lb", type=int, default=-1,
-                    help="diagnostic: KWK_TUNE_COMPACT_LB for both engines (1: one-pass look-back; default 0)")
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
@@ -677,10 +675,6 @@ def main():
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
-    if args.tune_compact_lb >= 0:
-        from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_COMPACT_LB, args.tune_compact_lb)
-        nodes.set_tuning(abi.TUNE_COMPACT_LB, args.tune_compact_lb)
     if args.tune_priority:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_STREAM_PRIORITY, 1)

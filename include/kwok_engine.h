@@ -226,9 +226,7 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
-#define KWK_TUNE_COMPACT_LB 11 /* fired hand-back: one pass with the offsets by decoupled look-back, 1, or 0
-                                  (default: the scan + expansion pair / the one-launch small compaction above;
-                                  the look-back measured 73 us against 27 us at C5) */
+/* 11: retired (the one-pass look-back hand-back, measured slower: 73 vs 27 us at C5) */
 #define KWK_TUNE_AGG_FUSED 13  /* kwk_aggregate with KWK_AGG_USAGE on 1-byte ids: the <= 4 mask counts taken inside the
                                   usage kernel's pass over the id column, 1 (default), or 0 (a count pass of their own) */
 #define KWK_TUNE_STREAM_PRIORITY 15 /* the engine's stream: 0 (default priority), 1 (the device's greatest) or 2 (its

@@ -2334,84 +2334,6 @@ __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   }
 }
 
-// Hand-back in one pass (the default): each workgroup expands four segments at the offset a
-// decoupled look-back gives it — the workgroup publishes its record count (flag "aggregate") as
-// soon as it has read its counts, then sums its predecessors' published values 64 at a time,
-// back to the nearest one that holds its inclusive prefix (flag "prefix"), and publishes its own.
-// No scan kernel, no group totals, no launch between them.  Status words carry the launch's epoch
-// (24 bits) so the array is never cleared.  Progress: workgroup b waits only for workgroups < b,
-// which the dispatcher started earlier (in order per queue; the lowest unfinished one never waits).
-constexpr uint64_t kLbAgg = 1ull << 38, kLbPrefix = 2ull << 38, kLbValue = (1ull << 38) - 1ull;
-__device__ __forceinline__ uint64_t lb_load(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long* p, uint64_t v) {
-  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int kRec, bool kPacked = false>
-__global__ __launch_bounds__(kBlock) void compact_lb_kernel(CompactArgs a, unsigned long long* __restrict__ status,
-                                                            uint32_t epoch) {
-  constexpr int kPre = 4;
-  __shared__ uint32_t s_cnt[kWavesPerBlock];
-  __shared__ uint32_t s_base;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t b = blockIdx.x;
-  const uint32_t seg = b * kSegsPerBlock + wave;
-  const bool have = seg < a.n_segs;
-  const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)(have ? seg : 0u) * a.stride;
-  uint2 r[kPre];
-#pragma unroll
-  for (int k = 0; k < kPre; ++k) r[k] = rec_at<kRec>(sp, lane + 64u * k);  // overlap the look-back
-  const uint32_t c = have ? a.counts[seg] : 0u;
-  if (lane == 0) s_cnt[wave] = c;
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-    const uint64_t tag = (uint64_t)epoch << 40;
-    if (lane == 0) lb_store(&status[b], tag | (b == 0 ? kLbPrefix : kLbAgg) | tot);
-    uint64_t excl = 0;
-    for (int64_t top = (int64_t)b - 1; top >= 0; top -= 64) {  // wave-uniform
-      const int64_t me = top - (int64_t)lane;
-      uint64_t s = kLbPrefix;  // before block 0: prefix 0
-      bool ok = me < 0;
-      for (;;) {
-        if (!ok) {
-          s = lb_load(&status[me]);
-          ok = (s >> 40) == epoch && (s & (kLbAgg | kLbPrefix));
-        }
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const unsigned long long pm = __ballot((s & kLbPrefix) != 0);
-      const uint32_t first = pm ? (uint32_t)__ffsll((long long)pm) - 1u : 64u;  // the nearest prefix
-      uint64_t v = lane <= first ? (s & kLbValue) : 0ull;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      excl += v;
-      if (pm) break;
-    }
-    if (lane == 0) {
-      if (b > 0) lb_store(&status[b], tag | kLbPrefix | (excl + tot));
-      s_base = (uint32_t)excl;
-    }
-  }
-  __syncthreads();
-  if (!have) return;
-  uint32_t off = s_base;
-  for (uint32_t w = 0; w < wave; ++w) off += s_cnt[w];
-  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
-  const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
-#pragma unroll
-  for (int k = 0; k < kPre; ++k) {
-    const uint32_t j = lane + 64u * k;
-    if (j < c) store_out<kPacked>(a, off + j, base + r[k].x, r[k].y);
-  }
-  for (uint32_t j = lane + 64u * kPre; j < c; j += 64) {
-    const uint2 x = rec_at<kRec>(sp, j);
-    store_out<kPacked>(a, off + j, base + x.x, x.y);
-  }
-}
-
 // sums the per-block statistics rows [0, n_blocks) (the rows any sweep grid has used)
 __global__ void reduce_stats_kernel(const unsigned long long* __restrict__ cum, uint32_t n_blocks,
                                     unsigned long long* __restrict__ out) {
@@ -4101,8 +4023,6 @@ struct kwk_engine {
   uint32_t* d_wave_counts = nullptr;
   uint32_t* d_wave_offsets = nullptr;
   uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
-  unsigned long long* d_lb_status = nullptr;  // compact_lb_kernel's per-workgroup look-back words
-  uint32_t lb_epoch = 0;                      // its launch epoch (24 bits, never 0)
   unsigned long long* d_cum = nullptr;
   unsigned long long* d_stats = nullptr;
   uint64_t steps = 0;
@@ -4134,10 +4054,6 @@ struct kwk_engine {
   uint32_t podv_n = 0;
   uint32_t usage_blocks = 0;      // KWK_TUNE_USAGE_BLOCKS (0: occupancy API)
   uint32_t compact_small = 8192;  // KWK_TUNE_COMPACT_SMALL (kSmallSegs)
-  // KWK_TUNE_COMPACT_LB: the one-pass look-back hand-back.  Off by default: with four segments
-  // per workgroup the prefix frontier advances ~64 workgroups per look-back round trip, 73 us at
-  // C5 against 27 us for the scan pair (r4d)
-  bool compact_lb = false;
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
   // host copies of the usage configuration (per-container reads, metric scrapes)
@@ -4612,7 +4528,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
-  ALLOC(e->d_lb_status, sizeof(unsigned long long) * (n_waves / kSegsPerBlock + 2));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   ALLOC(e->d_id2w, sizeof(uint16_t) * 256);
@@ -4626,7 +4541,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
   hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
-  hipMemsetAsync(e->d_lb_status, 0, sizeof(unsigned long long) * (n_waves / kSegsPerBlock + 2), e->stream);
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
@@ -4653,7 +4567,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_lb_status, e->d_cum, e->d_stats,
+                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
@@ -4832,10 +4746,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
-      return KWK_OK;
-    case KWK_TUNE_COMPACT_LB:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_LB: 0 or 1");
-      e->compact_lb = value != 0;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -5332,23 +5242,8 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
   a.region_slots = 64u * e->last_objs << e->last_region_shift;
   a.stride = 64u * e->last_objs + 32u;
   const int rk = e->last_rec;
-  if (mode != 2 && e->compact_lb) {  // one pass: the offsets by decoupled look-back
-    if (++e->lb_epoch >= (1u << 24)) e->lb_epoch = 1;
-    unsigned long long* st = e->d_lb_status;
-    uint32_t ep = e->lb_epoch;
-    void* largs[] = {&a, &st, &ep};
-    const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_lb_kernel<kRecId8Half, true>
-                              : rk == kRecId8   ? (const void*)compact_lb_kernel<kRecId8, true>
-                                                : (const void*)compact_lb_kernel<kRecSlot, true>)
-                           : (rk == kRecId8Half ? (const void*)compact_lb_kernel<kRecId8Half>
-                              : rk == kRecId8   ? (const void*)compact_lb_kernel<kRecId8>
-                                                : (const void*)compact_lb_kernel<kRecSlot>);
-    HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), largs, 0, e->stream));
-    HIP_TRY(hipGetLastError());
-    return KWK_OK;
-  }
   void* args[] = {&a};
-  if (mode == 2 && !e->compact_lb && n_waves <= e->compact_small) {
+  if (mode == 2 && n_waves <= e->compact_small) {
     hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
     HIP_TRY(hipGetLastError());
     return KWK_OK;

@@ -97,7 +97,6 @@ TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_USAGE_BLOCKS, TUNE_FSM_KERNEL, TUNE_USA
 TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
-TUNE_COMPACT_LB = 11
 TUNE_USAGE_ROWS = 12
 TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15

@@ -24,8 +24,7 @@ def test_pod_fast_c1_mini(state):
     sweep16_kernel with its transition table (auto-gen: leaves the 1-byte format) and without it
     (auto-nofsm); dw = the 8-byte records of a packed word fused with its relative due time;
     auto-pair hands the fired list back through the scan + expansion pair (KWK_TUNE_COMPACT_SMALL
-    0), u16-pair through the one-pass look-back compaction (KWK_TUNE_COMPACT_LB 1), instead of the
-    one-launch compaction."""
+    0), u16-pair the 2-byte words through the same pair, instead of the one-launch compaction."""
     tuning, kernel = {}, {"auto": abi.SWEEP_8, "u16": abi.SWEEP_16_FSM, "u32": abi.SWEEP_W4, "dw": abi.SWEEP_WD,
                           "wide": abi.SWEEP_W8}.get(state)
     if state == "auto-nofsm":
@@ -35,7 +34,7 @@ def test_pod_fast_c1_mini(state):
     elif state == "auto-pair":
         tuning, kernel, state = {abi.TUNE_COMPACT_SMALL: 0}, abi.SWEEP_8, "auto"
     elif state == "u16-pair":
-        tuning, kernel, state = {abi.TUNE_COMPACT_LB: 1}, abi.SWEEP_16_FSM, "u16"
+        tuning, kernel, state = {abi.TUNE_COMPACT_SMALL: 0}, abi.SWEEP_16_FSM, "u16"
     cl = W.make_cluster("C1", 40, 400, seed=11)
     objs = cl.pods.materialize()
     total, per = run(cl.pod_stage_files, objs, steps=12, dt_ns=10**9, harness=True, state=state, tuning=tuning,

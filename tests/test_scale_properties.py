@@ -116,20 +116,18 @@ def test_sweep16_tile_shapes_agree_at_17m_pods():
             e.close()
 
 
-HANDBACK_PATHS = ((0, 8192), (1, 8192), (0, 0))  # (KWK_TUNE_COMPACT_LB, KWK_TUNE_COMPACT_SMALL); [0] = default
+HANDBACK_PATHS = (8192, 0)  # KWK_TUNE_COMPACT_SMALL; [0] = default
 
 
 def _handback_path(eng, path):
     from kwok_amd.host import abi
-    eng.set_tuning(abi.TUNE_COMPACT_LB, path[0])
-    eng.set_tuning(abi.TUNE_COMPACT_SMALL, path[1])
+    eng.set_tuning(abi.TUNE_COMPACT_SMALL, path)
 
 
 def test_handback_pair_equals_one_launch_at_4m_pods():
-    """The fired hand-back's three paths over the same step's segments: the one-launch compaction
-    that re-sums the counts (at most 8192 segments, the default here), the one-pass look-back
-    compaction (KWK_TUNE_COMPACT_LB 1) and the scan + expansion pair (KWK_TUNE_COMPACT_SMALL 0)
-    give the same dense list in the same order; every slot once."""
+    """The fired hand-back's two paths over the same step's segments: the one-launch compaction
+    that re-sums the counts (at most 8192 segments, the default here) and the scan + expansion pair
+    (KWK_TUNE_COMPACT_SMALL 0) give the same dense list in the same order; every slot once."""
     prog, eng = _pods("auto")
     try:
         now0 = 1_700_000_000 * 10**9
@@ -152,7 +150,7 @@ def test_handback_pair_equals_one_launch_at_4m_pods():
 def test_packed_handback_equals_records_at_4m_pods(state):
     """The packed hand-back (kwk_fired_compact_packed / kwk_fired_packed: 4-byte records, stage in
     bits 31-27, slot in 26-0) over the same step's segments as the 8-byte list, through both
-    compaction paths (look-back, one launch at <= 8192 segments, the scan + expansion pair above): the same
+    compaction paths (one launch at <= 8192 segments, the scan + expansion pair above): the same
     (slot, stage) sequence; kwk_fired after a packed compaction re-expands the full records
     (flags included); kwk_step_n with KWK_COMPACT_PACKED leaves the same packed list as the
     per-step calls.  1-byte ids (sweep8), 2-byte words, fused 8-byte records (C2 mix).  The 2-byte
