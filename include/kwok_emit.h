@@ -63,7 +63,8 @@ typedef struct {
   const kwk_emit_piece* pieces;
   const char* lits;
   const uint8_t* fresh_guards;    /* n_classes: guard bits of an object created from its spec */
-  const uint32_t* column_stride;  /* n_columns: bytes per slot, [length][text] (length 0xFF = unusable) */
+  const uint32_t* column_stride;  /* n_columns: bytes per slot, a multiple of 4 in 4..256: [length][text]
+                                   (length 0xFF = unusable) */
 } kwk_emit_program;
 
 /* per slot: bits 0-15 class, 16-23 guard bits, 32-63 template accepted (bit tid) */
@@ -81,11 +82,8 @@ typedef struct {
 
 #define KWK_EMIT_FROM_RECORDS 0u /* kwk_fired_device's list (kwk_fired_compact) */
 #define KWK_EMIT_FROM_PACKED 1u  /* kwk_fired_packed_device's list (kwk_fired_compact_packed) */
-/* or-ed into source (diagnostics; the default: each record written by one lane, 16 bytes per store):
- * one wave per record, 64 lanes per literal run, straight to global memory one byte per lane / through
- * an LDS window of the wave's records leaving as 16-byte stores */
-#define KWK_EMIT_BYTE_STORES (1u << 8)
-#define KWK_EMIT_WAVE_WINDOW (1u << 9)
+/* (round 5: the wave-per-record writers selected by bits 8 / 9 are retired — measured slower than
+ * the lane-per-record writer; any other bit of source is KWK_EINVAL) */
 
 const char* kwk_emit_last_error(const kwk_emitter* em);
 /* an emitter for `eng`'s fired lists over slots [0, capacity), on the engine's stream */

@@ -50,7 +50,7 @@ constexpr uint32_t kBlock = 256, kTile = kBlock;  // records per tile: one per t
 constexpr uint32_t kWaves = kBlock / 64, kWaveRecs = kTile / kWaves;
 constexpr uint32_t kMaxStageTpl = 16;  // templates of one stage (an item mask per record)
 constexpr uint32_t kScanBlock = 1024;
-constexpr uint32_t kStageBytes = 2048;  // per-wave LDS window of the staged writes
+constexpr uint32_t kNowWords = 10;      // Now() text (< 40 bytes) as dwords in LDS
 constexpr uint32_t kLdsPieces = 256;    // skeleton tables staged in LDS when they fit
 constexpr uint32_t kLdsLits = 8192;
 constexpr uint32_t kLdsSkels = 64;
@@ -195,117 +195,102 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, con
   return s;
 }
 
-// one lane's output stream (a record written by the thread that sized it): byte stores up to the
-// first 16-byte boundary, then 16 bytes gathered in registers per store, the tail as bytes
-struct LaneOut {
+// One lane's output stream (a record written by the thread that sized it), assembled four bytes
+// at a time in a 16-byte register window {lo, hi}: every append is one shifted OR at the window's
+// byte position (no per-byte work), a full window leaves as one 16-byte store.  The stream starts
+// at global byte g0: the window starts with g0 & 15 phantom bytes, so that every store is 16-byte
+// aligned; the first window (it shares its 16 bytes with the record before) and the last one (the
+// record after) are written with dword and byte stores covering exactly the record's bytes.
+struct Acc {
   char* out;
-  unsigned long long g;
-  uint64_t lo = 0, hi = 0;
-  uint32_t n = 0;
-  __device__ __forceinline__ void put(uint8_t c) {
-    if (n == 0 && (g & 15u)) {
-      out[g++] = (char)c;
-      return;
-    }
-    if (n < 8u) lo |= (uint64_t)c << (8u * n);
-    else hi |= (uint64_t)c << (8u * (n - 8u));
-    ++n;
-    ++g;
-    if (n == 16u) {
-      *reinterpret_cast<uint4*>(out + g - 16u) =
-          make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-      n = 0;
-      lo = hi = 0;
-    }
-  }
-  // `cnt` (<= 4) bytes of w, low byte first: one register insert when they land on a whole dword
-  // of the 16-byte gather
-  __device__ __forceinline__ void put4(uint32_t w, uint32_t cnt) {
-    if (cnt == 4u && (n & 3u) == 0u && !(n == 0u && (g & 15u))) {
-      if (n < 8u) lo |= (uint64_t)w << (8u * n);
-      else hi |= (uint64_t)w << (8u * (n - 8u));
-      n += 4u;
-      g += 4u;
-      if (n == 16u) {
-        *reinterpret_cast<uint4*>(out + g - 16u) =
-            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-        n = 0;
-        lo = hi = 0;
+  unsigned long long w0;  // global position of the window's byte 0 (16-byte aligned)
+  uint64_t lo, hi;
+  uint32_t n;             // bytes in the window (incl. the phantom head)
+  uint32_t head;          // phantom bytes of the first window (0 once it has left)
+  __device__ __forceinline__ Acc(char* o, unsigned long long g0)
+      : out(o), w0(g0 & ~15ull), lo(0), hi(0), n((uint32_t)(g0 & 15u)), head((uint32_t)(g0 & 15u)) {}
+  // bytes [b0, b1) of the window at w0, for a window shared with a neighbouring record
+  __device__ __forceinline__ void partial(uint32_t b0, uint32_t b1) const {
+    for (uint32_t b = b0; b < b1;) {
+      const uint64_t v = b < 8u ? lo : hi;
+      const uint32_t sh = 8u * (b & 7u);
+      if ((b & 3u) == 0u && b + 4u <= b1) {
+        *reinterpret_cast<uint32_t*>(out + w0 + b) = (uint32_t)(v >> sh);
+        b += 4u;
+      } else {
+        out[w0 + b] = (char)((v >> sh) & 0xFFu);
+        ++b;
       }
-      return;
     }
-    for (uint32_t b = 0; b < cnt; ++b) put((uint8_t)(w >> (8u * b)));
   }
-  __device__ __forceinline__ void finish() {
-    for (uint32_t k = 0; k < n; ++k) out[g - n + k] = (char)((k < 8u ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xFFu);
+  __device__ __forceinline__ void flush_full() {
+    if (head) {
+      partial(head, 16u);
+      head = 0;
+    } else {
+      *reinterpret_cast<uint4*>(out + w0) = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+    }
   }
+  // `cnt` (1..4) bytes, low byte first; w's bytes above cnt are zero
+  __device__ __forceinline__ void put(uint32_t w, uint32_t cnt) {
+    const uint64_t x = (uint64_t)w;
+    const uint32_t sh = 8u * n;  // 0..120
+    if (sh < 64u) {
+      lo |= x << sh;
+      hi |= sh > 32u ? x >> (64u - sh) : 0ull;
+    } else {
+      hi |= x << (sh - 64u);
+    }
+    const uint64_t spill = sh > 96u ? x >> (128u - sh) : 0ull;  // bytes past the window
+    n += cnt;
+    if (n >= 16u) {
+      flush_full();
+      w0 += 16u;
+      lo = spill;
+      hi = 0;
+      n -= 16u;
+    }
+  }
+  __device__ __forceinline__ void finish() const { partial(head, n); }
 };
 
-// one emitted item by one lane (the lane-per-record writer)
+__device__ __forceinline__ uint32_t low_bytes(uint32_t w, uint32_t cnt) {
+  return cnt >= 4u ? w : w & ((1u << (8u * cnt)) - 1u);
+}
+
+// `len` bytes starting at byte `off` of a dword array (aligned dword reads, one per step, joined by
+// alignbyte): the literal runs (LDS or global, 16 bytes of zero padding after them), Now (LDS) and
+// a value row's text (byte 1 on)
+__device__ __forceinline__ void put_run(Acc& o, const uint32_t* __restrict__ src, uint32_t off, uint32_t len) {
+  if (!len) return;
+  uint32_t d = off >> 2;
+  const uint32_t sh = off & 3u;
+  uint32_t cur = src[d];
+  for (uint32_t k = 0; k < len; k += 4u) {
+    const uint32_t nxt = src[d + 1u];
+    const uint32_t w = sh ? __builtin_amdgcn_alignbyte(nxt, cur, sh) : cur;
+    const uint32_t cnt = min(4u, len - k);
+    o.put(low_bytes(w, cnt), cnt);
+    cur = nxt;
+    ++d;
+  }
+}
+
+// one emitted item by one lane
 __device__ __forceinline__ void lane_skel(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S, uint32_t slot,
-                                          const char* s_now, const Vals& V, LaneOut& o) {
+                                          const uint32_t* s_now, const Vals& V, Acc& o) {
+  const uint32_t* L = reinterpret_cast<const uint32_t*>(T.lits);
   for (uint32_t q = 0; q < S.n_pieces; ++q) {
     const kwk_emit_piece P = T.pieces[S.first_piece + q];
-    // the literal as aligned dword pairs (the tables carry 8 bytes of padding): four bytes per step
-    const uint32_t* L = reinterpret_cast<const uint32_t*>(T.lits);
-    for (uint32_t k = 0; k < P.lit_len; k += 4u) {
-      const uint32_t off = P.lit_off + k;
-      const uint64_t both = (uint64_t)L[off >> 2] | (uint64_t)L[(off >> 2) + 1u] << 32;
-      o.put4((uint32_t)(both >> (8u * (off & 3u))), min(4u, (uint32_t)P.lit_len - k));
-    }
+    put_run(o, L, P.lit_off, P.lit_len);
     if (P.slot == 0) {
-      for (uint32_t k = 0; k < a.now_len; ++k) o.put((uint8_t)s_now[k]);
+      put_run(o, s_now, 0u, a.now_len);
     } else if (P.slot != KWK_EMIT_NO_SLOT) {
-      const uint8_t* v = V.row(a, P.slot - 1u, slot);
-      const uint32_t len = v[0];
-      for (uint32_t k = 0; k < len; ++k) o.put(v[1 + k]);
+      const uint8_t* v = V.row(a, P.slot - 1u, slot);  // [length][text]: rows 16-byte aligned in LDS, 4 in global
+      const uint32_t* v32 = reinterpret_cast<const uint32_t*>(v);
+      put_run(o, v32, 1u, (uint32_t)(v32[0] & 0xFFu));
     }
   }
-}
-
-// the bytes of one emitted item: put(global position, byte) for each, 64 lanes per run (a value's
-// length and bytes are loaded together); returns the position after them
-template <typename Put>
-__device__ __forceinline__ unsigned long long put_skel(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S,
-                                                       uint32_t slot, unsigned long long p, uint32_t lane,
-                                                       const char* s_now, const Vals& V, Put put) {
-  {
-    for (uint32_t q = 0; q < S.n_pieces; ++q) {
-      const kwk_emit_piece P = T.pieces[S.first_piece + q];
-      const char* src = T.lits + P.lit_off;
-      for (uint32_t o = lane; o < P.lit_len; o += 64u) put(p + o, src[o]);
-      p += P.lit_len;
-      if (P.slot == 0) {
-        if (lane < a.now_len) put(p + lane, s_now[lane]);
-        p += a.now_len;
-      } else if (P.slot != KWK_EMIT_NO_SLOT) {
-        const uint32_t c = P.slot - 1u, sd = V.lds ? 16u : a.p.stride[c];
-        const uint8_t* v = V.row(a, c, slot);
-        const uint32_t len = v[0];
-        const char b0 = lane + 1u < sd ? (char)v[1 + lane] : 0;
-        if (lane < len) put(p + lane, b0);
-        for (uint32_t o = lane + 64u; o < len; o += 64u) put(p + o, (char)v[1 + o]);
-        p += len;
-      }
-    }
-  }
-  return p;
-}
-
-// every emitted item of a record: the skeletons listed in LDS (n_sk <= kRecSk), or looked up
-template <typename Put>
-__device__ __forceinline__ void put_record(const EmitArgs& a, const Tables& T, const kwk_emit_skel* skels,
-                                           uint32_t stage, uint32_t ok, uint32_t n_sk, const int16_t* sk,
-                                           uint32_t slot, uint32_t cls, unsigned long long p, uint32_t lane,
-                                           const char* s_now, const Vals& V, Put put) {
-  if (n_sk <= kRecSk) {
-    for (uint32_t j = 0; j < n_sk; ++j) p = put_skel(a, T, skels[sk[j]], slot, p, lane, s_now, V, put);
-    return;
-  }
-  const uint32_t t0 = a.p.stage_tpl_ptr[stage], t1 = a.p.stage_tpl_ptr[stage + 1];
-  for (uint32_t j = t0; j < t1; ++j)
-    if ((ok >> (j - t0)) & 1u)
-      p = put_skel(a, T, a.p.skels[a.p.skel_of[cls * a.p.n_templates + a.p.stage_tpl[j]]], slot, p, lane, s_now, V, put);
 }
 
 template <typename T>
@@ -425,37 +410,33 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
-// kMode: kWriteLane (default) — each thread writes the record it sized, 16-byte stores from
-// registers; kWriteWindow — each wave writes its 64 records' contiguous span, 64 lanes per literal
-// run, through an LDS window leaving as 16-byte stores; kWriteBytes — the same straight to global
-// memory, one byte store per lane.  kLds: the skeleton tables and the records' call-value rows (at
-// most kLdsCols columns of 16 bytes) staged in LDS
-constexpr int kWriteBytes = 0, kWriteWindow = 1, kWriteLane = 2;
-template <int kMode, bool kLds>
+// Each thread writes the record it sized (Acc: a 16-byte register window, four bytes per append).
+// kLds: the skeleton tables and the records' call-value rows (at most kLdsCols columns of 16 bytes)
+// staged in LDS
+template <bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
-  constexpr bool kStaged = kMode == kWriteWindow;
-  __shared__ __attribute__((aligned(16))) char s_buf[kStaged ? kWaves * kStageBytes : 16];
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
   __shared__ int16_t s_sk[kTile * kRecSk];
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
   __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
-  __shared__ uint32_t s_slot[kTile];
-  __shared__ uint32_t s_meta[kTile];  // ok mask [15:0] | stage [23:16]
-  __shared__ uint32_t s_cls[kTile];
-  __shared__ unsigned long long s_base[kTile + 1];  // [r] = record r's first byte, [r + 1] its end
   __shared__ uint32_t s_wi[kWaves];
   __shared__ unsigned long long s_wb[kWaves];
-  __shared__ char s_now[40];
+  __shared__ uint32_t s_now[kNowWords];
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const unsigned long long tot_i = a.totals[0], tot_b = a.totals[1];
   if (tot_i > a.cap_items || tot_b > a.cap_bytes || a.totals[2]) return;  // KWK_ECAP: nothing is written
   if constexpr (kLds)
     for (uint32_t j = threadIdx.x; j < a.p.n_skels; j += blockDim.x) s_skels[j] = a.p.skels[j];
-  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);  // (its barrier covers s_skels)
+  if (threadIdx.x < kNowWords) {
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 4u; ++b) w |= (uint32_t)(uint8_t)a.now[4u * threadIdx.x + b] << (8u * b);
+    s_now[threadIdx.x] = w;
+  }
+  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
+  __syncthreads();  // s_skels, s_now
   const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.offsets[tot_i] = tot_b;
-  if (threadIdx.x < 40) s_now[threadIdx.x] = a.now[threadIdx.x];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint32_t n_ok = 0;
   for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -491,11 +472,8 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       item += s_wi[v];
       pos += s_wb[v];
     }
-    s_slot[lr] = x.slot;
+    const unsigned long long rec_base = pos;
     uint32_t n_sk = 0;
-    s_cls[lr] = (uint32_t)(w & 0xFFFFu);
-    s_base[lr] = pos;
-    if (lr == kTile - 1) s_base[kTile] = pos + sz.bytes;
     if (r < n && x.stage < a.p.n_stages) {
       const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
       uint32_t g = (uint32_t)(w >> 16) & 0xFFu;
@@ -513,17 +491,15 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           ++n_sk;
         }
       }
-      if constexpr (kMode == kWriteLane) {  // this thread writes the record it just sized
-        if (n_sk) {
-          LaneOut o{a.out, s_base[lr]};
-          if (n_sk <= kRecSk) {
-            for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
-          } else {
-            for (uint32_t j = t0; j < t1; ++j)
-              if ((sz.ok >> (j - t0)) & 1u) lane_skel(a, T, skels[skel_index(a, w, a.p.stage_tpl[j])], x.slot, s_now, V, o);
-          }
-          o.finish();
+      if (n_sk) {  // this thread writes the record it just sized
+        Acc o(a.out, rec_base);
+        if (n_sk <= kRecSk) {
+          for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
+        } else {
+          for (uint32_t j = t0; j < t1; ++j)
+            if ((sz.ok >> (j - t0)) & 1u) lane_skel(a, T, skels[skel_index(a, w, a.p.stage_tpl[j])], x.slot, s_now, V, o);
         }
+        o.finish();
       }
       // the object's guard bits after the patches (all items emitted here; else the host sets them)
       const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
@@ -534,66 +510,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         if (nw != w) a.words[x.slot] = nw;
       }
     }
-    s_meta[lr] = sz.ok | (r < n ? (x.stage & 0xFFu) << 16 : 0xFFu << 16) | min(n_sk, 15u) << 24;
-    __syncthreads();
-    // bytes: wave `wave` writes records [wave * 64, wave * 64 + 64) of the tile, whose output is
-    // one contiguous span, 64 lanes per literal run / value
-    const uint32_t r0 = wave * kWaveRecs, r1 = r0 + kWaveRecs;
-    if constexpr (kMode == kWriteLane) {
-      // written above
-    } else if constexpr (!kStaged) {
-      for (uint32_t q = r0; q < r1; ++q) {
-        const uint32_t meta = s_meta[q];
-        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu, n_sk = meta >> 24;
-        if (stage >= a.p.n_stages || !ok) continue;
-        const Vals Vq{kLds ? reinterpret_cast<const uint8_t*>(s_vals) : nullptr, q};
-        put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, s_slot[q], s_cls[q], s_base[q], lane, s_now, Vq,
-                   [&](unsigned long long gp, char c) { a.out[gp] = c; });
-      }
-    } else {
-      // staged: the span goes through a per-wave LDS window [w0, w0 + kStageBytes) (w0 16-byte
-      // aligned) and leaves as 16-byte stores; only the edges of a flushed range take byte stores
-      char* buf = s_buf + wave * kStageBytes;
-      unsigned long long w0 = s_base[r0] & ~15ull, lo = s_base[r0], hi = lo;
-      auto flush = [&](unsigned long long f_lo, unsigned long long f_hi) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (unsigned long long A = (f_lo & ~15ull) + lane * 16ull; A < f_hi; A += 1024ull) {
-          const uint32_t li = (uint32_t)(A - w0);
-          if (A >= f_lo && A + 16u <= f_hi) {
-            *reinterpret_cast<uint4*>(a.out + A) = *reinterpret_cast<const uint4*>(buf + li);
-          } else {
-            for (uint32_t b = 0; b < 16u; ++b)
-              if (A + b >= f_lo && A + b < f_hi) a.out[A + b] = buf[li + b];
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      };
-      for (uint32_t q = r0; q < r1; ++q) {
-        const uint32_t meta = s_meta[q];
-        const uint32_t stage = (meta >> 16) & 0xFFu, ok = meta & 0xFFFFu, n_sk = meta >> 24;
-        if (stage >= a.p.n_stages || !ok) continue;
-        const uint32_t slot = s_slot[q], cls = s_cls[q];
-        const unsigned long long p = s_base[q], end = s_base[q + 1];
-        const Vals Vq{kLds ? reinterpret_cast<const uint8_t*>(s_vals) : nullptr, q};
-        if (end - w0 > kStageBytes) {  // the window is full: out with everything before this record
-          flush(lo, p);  // (the chunk holding p is finished by byte stores from both sides)
-          w0 = p & ~15ull;
-          lo = p;
-          if (end - w0 > kStageBytes) {  // larger than the window: straight to global memory
-            put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, slot, cls, p, lane, s_now, Vq,
-                       [&](unsigned long long gp, char c) { a.out[gp] = c; });
-            lo = hi = end;
-            w0 = end & ~15ull;
-            continue;
-          }
-        }
-        put_record(a, T, skels, stage, ok, n_sk, s_sk + q * kRecSk, slot, cls, p, lane, s_now, Vq,
-                   [&](unsigned long long gp, char c) { buf[(uint32_t)(gp - w0)] = c; });
-        hi = end;
-      }
-      if (hi > lo) flush(lo, hi);
-    }
-    __syncthreads();
+    __syncthreads();  // s_wi / s_wb are rewritten by the next tile
   }
   n_ok = wave_sum(n_ok);
   if (lane == 0 && n_ok) atomicAdd(&a.totals[3], (unsigned long long)n_ok);
@@ -710,7 +627,8 @@ kwk_status check_program(const kwk_emit_program* g) {
     if (P.slot != KWK_EMIT_NO_SLOT && P.slot > g->n_columns) return fail(KWK_EINVAL, "emit program: slot out of range");
   }
   for (uint32_t c = 0; c < g->n_columns; ++c)
-    if (g->column_stride[c] < 2 || g->column_stride[c] > 256) return fail(KWK_EINVAL, "emit program: column stride 2..256");
+    if (g->column_stride[c] < 4 || g->column_stride[c] > 256 || (g->column_stride[c] & 3u))
+      return fail(KWK_EINVAL, "emit program: column stride 4..256, a multiple of 4");
   return KWK_OK;
 }
 
@@ -740,9 +658,9 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->stride.assign(g->column_stride, g->column_stride + g->n_columns);
   for (uint32_t c = 0; c < g->n_columns; ++c) {
     void* d = nullptr;
-    HIP_TRY(hipMalloc(&d, (size_t)em->capacity * em->stride[c] + 1));
+    HIP_TRY(hipMalloc(&d, (size_t)em->capacity * em->stride[c] + 16));  // + the dword a row's last read may touch
     em->allocs.push_back(d);
-    if (kwk_status st = fill(em, d, 0xFF, (size_t)em->capacity * em->stride[c] + 1)) return st;  // unusable until set
+    if (kwk_status st = fill(em, d, 0xFF, (size_t)em->capacity * em->stride[c] + 16)) return st;  // unusable until set
     em->cols.push_back(static_cast<uint8_t*>(d));
   }
   if (kwk_status st = upload(em, const_cast<uint8_t***>(&em->p.cols), em->cols.data(), em->cols.size())) return st;
@@ -873,6 +791,7 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   } else {
     return fail(KWK_EINVAL, "source must be KWK_EMIT_FROM_RECORDS or KWK_EMIT_FROM_PACKED");
   }
+  if (source & ~0xFFu) return fail(KWK_EINVAL, "unknown source flags");
   if (kwk_status st = bind(em)) return st;
   if (!em->d_offsets)
     if (kwk_status st = kwk_emit_reserve(em, 1, 1)) return st;
@@ -903,12 +822,8 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
-  const int mode = (source & KWK_EMIT_BYTE_STORES) ? kWriteBytes : (source & KWK_EMIT_WAVE_WINDOW) ? kWriteWindow
-                                                                                                 : kWriteLane;
   const bool wl = lds && vals16;  // the write kernel's LDS path also stages the value rows
-#define WK(M) (wl ? (const void*)emit_write_kernel<M, true> : (const void*)emit_write_kernel<M, false>)
-  const void* wk = mode == kWriteBytes ? WK(kWriteBytes) : mode == kWriteWindow ? WK(kWriteWindow) : WK(kWriteLane);
-#undef WK
+  const void* wk = wl ? (const void*)emit_write_kernel<true> : (const void*)emit_write_kernel<false>;
   void* wargs[] = {&a};
   HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());

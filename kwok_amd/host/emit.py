@@ -30,9 +30,6 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 NO_SLOT = 0xFFFF
 STATUS_OK, STATUS_HOST = 0, 1
 FROM_RECORDS, FROM_PACKED = 0, 1
-BYTE_STORES = 1 << 8  # or-ed into the source (diagnostics): a wave per record, byte stores
-WAVE_WINDOW = 1 << 9  # ... a wave per record through an LDS window (default: a lane per record)
-WRITERS = {"lane": 0, "window": WAVE_WINDOW, "bytes": BYTE_STORES}
 MAX_GUARDS = 8
 MARKER = "\U0010FFFD"
 
@@ -354,9 +351,9 @@ class Emitter:
     def reserve(self, items: int, nbytes: int):
         self._check(lib().kwk_emit_reserve(self.h, int(items), int(nbytes)), "kwk_emit_reserve")
 
-    def emit(self, now_ns: int, packed: bool = True, writer: str = "lane"):
-        """Enqueue the emission of the engine's last compacted list (writer: WRITERS)."""
-        src = (FROM_PACKED if packed else FROM_RECORDS) | WRITERS[writer]
+    def emit(self, now_ns: int, packed: bool = True):
+        """Enqueue the emission of the engine's last compacted list."""
+        src = FROM_PACKED if packed else FROM_RECORDS
         self._check(lib().kwk_emit(self.h, int(now_ns), src), "kwk_emit")
 
     def result(self) -> Tuple[int, int]:
@@ -374,13 +371,13 @@ class Emitter:
         self._check(lib().kwk_emit_stats(self.h, C.byref(ni), C.byref(ne), C.byref(nb)), "kwk_emit_stats")
         return int(ni.value), int(ne.value), int(nb.value)
 
-    def run(self, now_ns: int, packed: bool = True, writer: str = "lane"):
+    def run(self, now_ns: int, packed: bool = True):
         """Emit (re-emitting once with enough room) -> (items structured array, offsets, bytes)."""
-        self.emit(now_ns, packed, writer)
+        self.emit(now_ns, packed)
         ni, nb = self.result()
         if ni < 0:
             self.reserve(-ni - 1, max(nb, 1))
-            self.emit(now_ns, packed, writer)
+            self.emit(now_ns, packed)
             ni, nb = self.result()
             if ni < 0:
                 raise abi.EngineError("kwk_emit: reservation still too small")

@@ -1,8 +1,8 @@
 """Device patch emission on the GPU (include/kwok_emit.h): the native controller loop of
 tests/test_controller_native.py with libkwok_emit beside it.  Every step, kwk_emit expands the
-engine's fired list (kwk_fired records on even steps, 4-byte packed records on odd ones; the
-writers in turn: a lane per record, a wave per record through an LDS window, a wave per record
-with byte stores) on the device; each item it emits equals, byte for byte, the patch the controller rendered for that
+engine's fired list (kwk_fired records on even steps, 4-byte packed records on odd ones) on the
+device (each record written by one lane through a 16-byte register window: records sharing a
+16-byte window at both ends of every record, patches of every length); each item it emits equals, byte for byte, the patch the controller rendered for that
 object with kwk_patch_render (itself checked against the oracle's next state there), and each
 item it leaves to the host is one the skeleton cannot stand for (status guard not met, template
 ineligible for the class).  After the host's hand-back, the guard bits the device carried equal
@@ -53,7 +53,7 @@ def _run(cl, steps, dt_ns, seed):
             packed = k % 2 == 1
             eng.step(now, seed, k)
             eng.fired_compact(packed=packed)
-            items, offs, out = em.run(now, packed=packed, writer=("lane", "window", "bytes")[k % 3])
+            items, offs, out = em.run(now, packed=packed)
             fired = eng.fired()
             pre = {int(r["slot"]): ctl.objs[int(r["slot"])] for r in fired}
             ctl.handle(fired, now)
@@ -142,7 +142,7 @@ def _big_stage_run(steps):
             now = NOW0 + k * 10**9
             eng.step(now, 7, k)
             eng.fired_compact(packed=True)
-            items, offs, out = em.run(now, packed=True, writer=("lane", "window", "bytes")[k % 3])
+            items, offs, out = em.run(now, packed=True)
             fired = eng.fired()
             ctl.handle(fired, now)
             for n, it in enumerate(items):
