@@ -3,7 +3,7 @@
 # time limit and the steps are chained: the first failing step ends the call.
 #
 # Usage: bash tools/gpu.sh <tag> <step> [<step> ...]      outputs under gpurun_out/<tag>/
-#   tests[=<pytest -k expr>]   GPU test suite (or a selection)
+#   tests[=<pytest -k expr>]   GPU test suite (or a selection; '+' between names: any of them)
 #   smoke                      __graft_entry__.smoke()
 #   bench[=<bench.py args>]    the driver's bench command (default --gpus 1 --steps 20 --warmup 5)
 #   prof                       kernel trace + stats of the driver's bench command (kernel_stats.csv)
@@ -29,7 +29,7 @@ for step in "$@"; do
   echo "== $name $arg"
   case $name in
     tests)
-      K=(); [ -n "$arg" ] && K=(-k "$arg")
+      K=(); [ -n "$arg" ] && K=(-k "${arg//+/ or }")  # tests=a+b selects a or b
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
         > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
       tail -2 $O/pytest_gpu.log ;;
