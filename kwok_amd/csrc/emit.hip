@@ -410,11 +410,137 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
   }
 }
 
-// Each thread writes the record it sized (Acc: a 16-byte register window, four bytes per append).
+// ---- the chunk writer (the default when the program's tables fit in LDS) ----
+// Per call, every block renders each skeleton once into an LDS template with Now filled in:
+// consecutive literal runs and Now slots merge into one template run, so a skeleton is a short
+// list of segments (template run | value column c).  A record's bytes are the concatenation of its
+// items' segments; the thread that sized the record writes it as aligned 16-byte chunks: each chunk
+// gathers the bytes of the segments overlapping it (16 unaligned bytes from LDS: five aligned dword
+// reads joined by alignbyte, merged under a byte mask), and leaves as one 16-byte store.  The first
+// and the last chunk of a record share their 16 bytes with the neighbouring records: they are
+// written at the end with dword / byte stores covering exactly the record's bytes.  Every store
+// goes through a buffer resource with the offset out of range where a lane has nothing to store,
+// so no store sits under a divergent branch.
+constexpr uint32_t kTplBytes = 12288;                    // rendered templates in LDS
+constexpr uint32_t kMaxSegs = 2 * kLdsPieces + kLdsSkels;  // segments of every skeleton
+constexpr uint32_t kSegValue = 1u << 24;                 // segment kind: value column (y >> 24) - 1
+constexpr uint32_t kOOB = 0x80000000u;                   // buffer offset past the resource: no store
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+__device__ __forceinline__ uint32_t lds_rd(uint32_t a) { return *(const lds_u32*)(size_t)a; }
+
+// the 16 bytes at LDS byte address A (any alignment; bytes outside the arrays are don't-care)
+__device__ __forceinline__ void lds_load16(uint32_t A, uint32_t (&y)[4]) {
+  const uint32_t d = A & ~3u, sh = A & 3u;
+  const uint32_t w0 = lds_rd(d), w1 = lds_rd(d + 4u), w2 = lds_rd(d + 8u), w3 = lds_rd(d + 12u), w4 = lds_rd(d + 16u);
+  y[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  y[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  y[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  y[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+
+// byte mask of [lo, hi) (0 <= lo <= hi <= 16) as two 64-bit halves
+__device__ __forceinline__ uint64_t ones_bytes(uint32_t n) { return n >= 8u ? ~0ull : (1ull << (8u * n)) - 1ull; }
+__device__ __forceinline__ void merge16(uint32_t (&x)[4], const uint32_t (&y)[4], uint32_t lo, uint32_t hi) {
+  const uint64_t ml = ones_bytes(min(hi, 8u)) & ~ones_bytes(min(lo, 8u));
+  const uint64_t mh = ones_bytes(hi > 8u ? hi - 8u : 0u) & ~ones_bytes(lo > 8u ? lo - 8u : 0u);
+  x[0] = (y[0] & (uint32_t)ml) | (x[0] & ~(uint32_t)ml);
+  x[1] = (y[1] & (uint32_t)(ml >> 32)) | (x[1] & ~(uint32_t)(ml >> 32));
+  x[2] = (y[2] & (uint32_t)mh) | (x[2] & ~(uint32_t)mh);
+  x[3] = (y[3] & (uint32_t)(mh >> 32)) | (x[3] & ~(uint32_t)(mh >> 32));
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// bytes [b0, b1) of the chunk x stored at offset `at` of the resource (dword stores where whole
+// dwords lie inside, byte stores for the rest; all with out-of-range offsets where not needed)
+__device__ __forceinline__ void store_part(const __amdgpu_buffer_rsrc_t r, uint32_t at, const uint32_t (&x)[4], uint32_t b0,
+                                           uint32_t b1, bool live) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    const bool whole = live && 4u * k >= b0 && 4u * k + 4u <= b1;
+    __builtin_amdgcn_raw_buffer_store_b32(x[k], r, whole ? at + 4u * k : kOOB, 0, 0);
+  }
+  // the partial dword at the front (bytes b0 .. its dword's end) and at the back (its dword's start .. b1)
+  const uint32_t f0 = b0, f1 = min(b1, (b0 + 3u) & ~3u);
+  const uint32_t e0 = max(b0, b1 & ~3u), e1 = b1;
+  const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+  auto byte_at = [=](uint32_t b) __attribute__((always_inline)) {  // selects, not an indexed register array
+    const uint32_t d01 = (b & 4u) ? x1 : x0;
+    const uint32_t d23 = (b & 4u) ? x3 : x2;
+    return (((b & 8u) ? d23 : d01) >> (8u * (b & 3u))) & 0xFFu;
+  };
+#pragma unroll
+  for (uint32_t j = 0; j < 3u; ++j) {
+    const uint32_t bf = f0 + j, be = e0 + j;
+    const uint32_t vf = byte_at(bf), ve = byte_at(be);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)vf, r, live && bf < f1 ? at + bf : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ve, r, live && be < e1 && (be & 3u) < (e1 & 3u) ? at + be : kOOB, 0, 0);
+  }
+}
+
+// one record's bytes [g0, g1) (g relative to the resource base) from its items' segments
+struct ChunkOut {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t g0, g1;          // the record's byte range
+  uint32_t P;               // the chunk being filled (16-byte aligned)
+  uint32_t cur;             // output position of the next segment
+  uint32_t x[4];            // the chunk's bytes so far
+  uint32_t f[4];            // the first chunk (shared with the record before), kept for the end
+  bool first_open;          // the first chunk has not left yet
+  __device__ __forceinline__ ChunkOut(__amdgpu_buffer_rsrc_t rs, uint32_t start, uint32_t end)
+      : r(rs), g0(start), g1(end), P(start & ~15u), cur(start), first_open(true) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = f[k] = 0u;
+  }
+  // segment: `len` bytes at LDS byte address `src`
+  __device__ __forceinline__ void segment(uint32_t src, uint32_t len) {
+    const uint32_t a = cur, b = cur + len;
+    cur = b;
+    while (len) {
+      uint32_t y[4];
+      lds_load16(src + P - a, y);  // (P - a wraps below the segment: those bytes are masked out)
+      merge16(x, y, a > P ? a - P : 0u, min(b - P, 16u));
+      if (b < P + 16u) break;  // the segment ends inside the chunk
+      // the chunk is complete: a whole 16-byte store unless it is the record's first (shared) chunk
+      const bool shared = first_open && (g0 & 15u);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], x[1], x[2], x[3]}, r, shared ? kOOB : P, 0, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f[k] = shared ? x[k] : f[k];
+        x[k] = 0u;
+      }
+      first_open = false;
+      P += 16u;
+      if (b <= P) break;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    const bool had_first = !first_open && (g0 & 15u);
+    const uint32_t fb = had_first ? (g0 & ~15u) : 0u;
+    store_part(r, fb, f, g0 & 15u, 16u, had_first);                   // the first chunk, if it left the loop
+    store_part(r, P, x, first_open ? (g0 & 15u) : 0u, cur - P, cur > P);  // the last one (maybe also the first)
+  }
+};
+
+// Each thread writes the record it sized.  kChunk: the chunk writer above (the tables, the value
+// rows and the templates in LDS); else Acc, a 16-byte register window filled four bytes per append.
 // kLds: the skeleton tables and the records' call-value rows (at most kLdsCols columns of 16 bytes)
 // staged in LDS
-template <bool kLds>
+template <bool kLds, bool kChunk>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
+  static_assert(kLds || !kChunk, "the chunk writer reads its tables from LDS");
+  __shared__ __attribute__((aligned(16))) uint32_t s_tpl[kChunk ? kTplBytes / 4 + 8 : 1];
+  __shared__ uint2 s_seg[kChunk ? kMaxSegs : 1];
+  __shared__ uint2 s_skseg[kChunk ? kLdsSkels : 1];
+  __shared__ uint32_t s_pofs[kChunk ? kLdsPieces : 1];
+  __shared__ uint2 s_tsz[kChunk ? kLdsSkels : 1];
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
   __shared__ int16_t s_sk[kTile * kRecSk];
@@ -436,6 +562,60 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
   __syncthreads();  // s_skels, s_now
   const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
+  if constexpr (kChunk) {  // render every skeleton into its template (Now filled in) and its segment list
+    const uint32_t ns = a.p.n_skels;
+    for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) s_pofs[q] = 0xFFFFFFFFu;  // pieces of no skeleton
+    if (threadIdx.x < ns) {
+      const kwk_emit_skel S = s_skels[threadIdx.x];
+      uint32_t sz = 0;
+      for (uint32_t q = 0; q < S.n_pieces; ++q) {
+        const kwk_emit_piece P = s_pieces[S.first_piece + q];
+        sz += P.lit_len + (P.slot == 0 ? a.now_len : 0u);
+      }
+      s_tsz[threadIdx.x] = make_uint2(sz, 2u * S.n_pieces + 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive bases: template bytes, segment slots
+      uint32_t tb = 0, sb = 0;
+      for (uint32_t k = 0; k < ns; ++k) {
+        const uint2 v = s_tsz[k];
+        s_tsz[k] = make_uint2(tb, sb);
+        tb += v.x;
+        sb += v.y;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < ns) {
+      const kwk_emit_skel S = s_skels[threadIdx.x];
+      const uint32_t tpl = lds_addr(s_tpl);
+      uint32_t pos = s_tsz[threadIdx.x].x, run = pos, sb = s_tsz[threadIdx.x].y, n = 0;
+      for (uint32_t q = 0; q < S.n_pieces; ++q) {
+        const kwk_emit_piece P = s_pieces[S.first_piece + q];
+        s_pofs[S.first_piece + q] = pos;
+        pos += P.lit_len;
+        if (P.slot == 0) {
+          pos += a.now_len;
+        } else if (P.slot != KWK_EMIT_NO_SLOT) {
+          if (pos > run) s_seg[sb + n++] = make_uint2(tpl + run, pos - run);
+          s_seg[sb + n++] = make_uint2(P.slot - 1u, (uint32_t)P.slot * kSegValue);
+          run = pos;
+        }
+      }
+      if (pos > run) s_seg[sb + n++] = make_uint2(tpl + run, pos - run);
+      s_skseg[threadIdx.x] = make_uint2(sb, n);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) {  // the bytes: one piece per thread
+      if (s_pofs[q] == 0xFFFFFFFFu) continue;
+      const kwk_emit_piece P = s_pieces[q];
+      lds_u8* d = (lds_u8*)(size_t)(lds_addr(s_tpl) + s_pofs[q]);
+      const char* src = T.lits + P.lit_off;
+      for (uint32_t k = 0; k < P.lit_len; ++k) d[k] = (uint8_t)src[k];
+      if (P.slot == 0)
+        for (uint32_t k = 0; k < a.now_len; ++k) d[P.lit_len + k] = (uint8_t)(s_now[k >> 2] >> (8u * (k & 3u)));
+    }
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) a.offsets[tot_i] = tot_b;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint32_t n_ok = 0;
@@ -491,7 +671,23 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           ++n_sk;
         }
       }
-      if (n_sk) {  // this thread writes the record it just sized
+      if (kChunk && n_sk && n_sk <= kRecSk) {  // this thread writes the record it just sized
+        const unsigned long long tb = a.tile_bytes[t] & ~15ull;  // the tile's bytes: < 2 GiB past tb
+        ChunkOut o(make_rsrc(a.out + tb, 0x7FFFFFFFu), (uint32_t)(rec_base - tb), (uint32_t)(pos - tb));
+        for (uint32_t j = 0; j < n_sk; ++j) {
+          const uint2 ss = s_skseg[s_sk[lr * kRecSk + j]];
+          for (uint32_t q = 0; q < ss.y; ++q) {
+            const uint2 sg = s_seg[ss.x + q];
+            if (sg.y >= kSegValue) {
+              const uint32_t row = lds_addr(&s_vals[sg.x * kTile + lr]);
+              o.segment(row + 1u, lds_rd(row) & 0xFFu);
+            } else {
+              o.segment(sg.x, sg.y);
+            }
+          }
+        }
+        o.finish();
+      } else if (n_sk) {  // this thread writes the record it just sized
         Acc o(a.out, rec_base);
         if (n_sk <= kRecSk) {
           for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
@@ -539,6 +735,9 @@ struct kwk_emitter {
   uint64_t cap_items = 0, cap_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool emitted = false;
+  bool chunk_ok = false;          // skeletons own consecutive, disjoint piece ranges (the chunk writer's templates)
+  uint64_t tpl_lits = 0;          // literal bytes of every skeleton's pieces
+  uint32_t tpl_now_slots = 0;     // Now slots of every skeleton's pieces
 
   ~kwk_emitter() {
     hipSetDevice(device);
@@ -640,6 +839,21 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->p.n_lits = (uint32_t)std::min<uint64_t>(g->n_lit_bytes, 0xFFFFFFFFu);
   em->p.n_cols = g->n_columns;
   em->p.n_skels = g->n_skels;
+  {  // the chunk writer's templates: pieces owned by one skeleton each, in skeleton order
+    bool ok = true;
+    uint32_t next = 0;
+    for (uint32_t k = 0; k < g->n_skels && ok; ++k) {
+      const kwk_emit_skel& S = g->skels[k];
+      ok = S.first_piece >= next;
+      next = S.first_piece + S.n_pieces;
+      for (uint32_t q = 0; q < S.n_pieces; ++q) {
+        const kwk_emit_piece& P = g->pieces[S.first_piece + q];
+        em->tpl_lits += P.lit_len;
+        em->tpl_now_slots += P.slot == 0 ? 1u : 0u;
+      }
+    }
+    em->chunk_ok = ok;
+  }
   const uint32_t n_st = g->stage_tpl_ptr[g->n_stages];
   if (kwk_status st = upload(em, const_cast<uint32_t**>(&em->p.stage_tpl_ptr), g->stage_tpl_ptr, g->n_stages + 1)) return st;
   if (kwk_status st = upload(em, const_cast<uint16_t**>(&em->p.stage_tpl), g->stage_tpl, n_st)) return st;
@@ -823,7 +1037,11 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   hipLaunchKernelGGL(emit_scan_kernel, dim3(1), dim3(kScanBlock), 0, em->stream, a);
   HIP_TRY(hipGetLastError());
   const bool wl = lds && vals16;  // the write kernel's LDS path also stages the value rows
-  const void* wk = wl ? (const void*)emit_write_kernel<true> : (const void*)emit_write_kernel<false>;
+  // the chunk writer: templates (literals + Now per slot) within kTplBytes, pieces in skeleton order
+  const bool chunk = wl && em->chunk_ok && em->tpl_lits + (uint64_t)em->tpl_now_slots * a.now_len + 16u <= kTplBytes;
+  const void* wk = chunk ? (const void*)emit_write_kernel<true, true>
+                   : wl  ? (const void*)emit_write_kernel<true, false>
+                         : (const void*)emit_write_kernel<false, false>;
   void* wargs[] = {&a};
   HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());

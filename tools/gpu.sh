@@ -18,6 +18,7 @@
 #   ab=<so>                    same-box A/B of the bench: in-tree engine vs tools/ab/<so>, alternating x2
 #   abshard=<so>               the same A/B at the N = 8 shard size (125k nodes / 12.5M pods)
 #   abemit=<so>                same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>
+#   emitprof                   the patch emitter alone: kernel trace + SQ / TA counter passes over its write kernel
 #   variants=<args>           tools/variants.py run <args> (cost-isolation builds)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; T=$1; shift; O=$R/gpurun_out/$T
@@ -96,6 +97,22 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
       for d in c5sq1 c5sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweep8; done > $O/c5_sq.txt
       for d in c2sq1 c2sq2; do python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) sweepw; done > $O/c2_sq.txt
       cat $O/c5_sq.txt $O/c2_sq.txt ;;
+    emitprof)  # the patch emitter alone: kernel trace (size / scan / write split) + SQ and TA passes over emit_write
+      TRACE
+      E="$R/bench.py --gpus 1 --steps 2 --warmup 2 --no-pmc --no-cpu-baseline --hbm-nodes 0 --pcie-steps 0 --emit-steps 3"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/emit_trace -o run -- python3 $E > $O/emit_trace.json 2> $O/emit_trace.err \
+        || { tail -20 $O/emit_trace.err; exit 1; }
+      S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
+      S2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+      S3="TA_BUSY_avr TA_FLAT_WRITE_WAVEFRONTS_sum"
+      for p in 1 2 3; do
+        S=S$p
+        timeout -s KILL 150 rocprofv3 --pmc ${!S} -d $O/emsq$p -o run -- python3 $E > $O/emsq$p.log 2>&1 || { tail -20 $O/emsq$p.log; break; }
+      done
+      cd $R && python tools/rocpd_summary.py stats $(find $O/emit_trace -name '*.db' | head -1) $O/emit_kernel_stats.csv \
+        && cut -c1-150 $O/emit_kernel_stats.csv | grep -i emit
+      for d in emsq1 emsq2 emsq3; do [ -d $O/$d ] && python tools/rocpd_summary.py pmc $(find $O/$d -name '*.db' | head -1) emit_write; done \
+        > $O/emit_sq.txt; cat $O/emit_sq.txt ;;
     shards)
       S="--no-cpu-baseline --no-pmc --hbm-nodes 0 --pcie-steps 0 --steps 40 --warmup 5"
       for n in 125000 250000 500000; do
