@@ -96,10 +96,14 @@ struct Tables {
   const char* lits;
 };
 
-template <bool kLds>
+template <bool kLds, bool kLits = true>
 __device__ __forceinline__ Tables stage_tables(const EmitArgs& a, kwk_emit_piece* s_pieces, uint32_t* s_lits) {
   if constexpr (kLds) {
     for (uint32_t j = threadIdx.x; j < a.p.n_pieces; j += blockDim.x) s_pieces[j] = a.p.pieces[j];
+    if constexpr (!kLits) {  // the literal runs stay in global memory
+      __syncthreads();
+      return Tables{s_pieces, a.p.lits};
+    }
     const uint32_t nw = (a.p.n_lits + 3u) / 4u;
     for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
       uint32_t w = 0;
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(kScanBlock) void emit_scan_kernel(EmitArgs a) {
 // written at the end with dword / byte stores covering exactly the record's bytes.  Every store
 // goes through a buffer resource with the offset out of range where a lane has nothing to store,
 // so no store sits under a divergent branch.
-constexpr uint32_t kTplBytes = 12288;                    // rendered templates in LDS
+constexpr uint32_t kTplBytes = 8192;                     // rendered templates in LDS
 constexpr uint32_t kMaxSegs = 2 * kLdsPieces + kLdsSkels;  // segments of every skeleton
 constexpr uint32_t kSegValue = 1u << 24;                 // segment kind: value column (y >> 24) - 1
 constexpr uint32_t kOOB = 0x80000000u;                   // buffer offset past the resource: no store
@@ -529,23 +533,54 @@ struct ChunkOut {
   }
 };
 
-// Each thread writes the record it sized.  kChunk: the chunk writer above (the tables, the value
-// rows and the templates in LDS); else Acc, a 16-byte register window filled four bytes per append.
-// kLds: the skeleton tables and the records' call-value rows (at most kLdsCols columns of 16 bytes)
-// staged in LDS
+__device__ __forceinline__ unsigned long long ballot(const bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+// inclusive prefix maximum over the wave's lanes (DPP row shifts and broadcasts; 0 is the identity)
+template <int C, int RM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, C, RM, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, dpp_u32<0x111, 0xF>(v));
+  v = max(v, dpp_u32<0x112, 0xF>(v));
+  v = max(v, dpp_u32<0x114, 0xF>(v));
+  v = max(v, dpp_u32<0x118, 0xF>(v));
+  v = max(v, dpp_u32<0x142, 0xA>(v));
+  v = max(v, dpp_u32<0x143, 0xC>(v));
+  return v;
+}
+
+constexpr uint32_t kRecSegs = 12;  // segments of a record the cooperative writer tables (more: per-lane writers)
+
+// kChunk (the default when the program's tables fit in LDS): each wave writes its 64 records'
+// bytes — one contiguous span — together, lane L taking the span's aligned 16-byte chunks L, L + 64,
+// ...: every store instruction writes 1 KiB of whole lines.  The records' segments (template runs of
+// the skeletons rendered above, value rows) are tabled in LDS by their owner lanes; a chunk finds its
+// record by a prefix maximum over the lanes of "the last record starting at or before me", its
+// segment by a binary search in the record's table, and gathers its bytes from LDS.  (Lanes each
+// writing their own record scatter 16-byte stores over 64 lines: the L2 then writes half-filled lines
+// back and refills them — r5e: 2x the patch bytes written, 0.6x read.)  A wave with a record beyond
+// the tables (> kRecSk items, > kRecSegs segments) writes per lane (ChunkOut; Acc past kRecSk items).
+// !kChunk: per lane, Acc.  kLds: the skeleton tables and the records' call-value rows (at most
+// kLdsCols columns of 16 bytes) staged in LDS
 template <bool kLds, bool kChunk>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   static_assert(kLds || !kChunk, "the chunk writer reads its tables from LDS");
   __shared__ __attribute__((aligned(16))) uint32_t s_tpl[kChunk ? kTplBytes / 4 + 8 : 1];
   __shared__ uint2 s_seg[kChunk ? kMaxSegs : 1];
   __shared__ uint2 s_skseg[kChunk ? kLdsSkels : 1];
-  __shared__ uint32_t s_pofs[kChunk ? kLdsPieces : 1];
+  __shared__ uint16_t s_pofs[kChunk ? kLdsPieces : 1];
   __shared__ uint2 s_tsz[kChunk ? kLdsSkels : 1];
+  __shared__ uint16_t s_rend[kChunk ? kTile * kRecSegs : 1];  // per record: its segments' end offsets
+  __shared__ uint16_t s_rsrc[kChunk ? kTile * kRecSegs : 1];  // ... and LDS source addresses (< 64 KiB)
+  __shared__ uint32_t s_rb[kChunk ? kTile : 1], s_re[kChunk ? kTile : 1];
+  __shared__ uint8_t s_rn[kChunk ? kTile : 1];
+  __shared__ uint32_t s_map[kChunk ? kTile : 1];              // per wave: chunk -> 1 + last record starting there
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
   __shared__ int16_t s_sk[kTile * kRecSk];
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
-  __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
+  __shared__ uint32_t s_lits[kLds && !kChunk ? kLdsLits / 4 : 1];
   __shared__ uint32_t s_wi[kWaves];
   __shared__ unsigned long long s_wb[kWaves];
   __shared__ uint32_t s_now[kNowWords];
@@ -559,12 +594,12 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     for (uint32_t b = 0; b < 4u; ++b) w |= (uint32_t)(uint8_t)a.now[4u * threadIdx.x + b] << (8u * b);
     s_now[threadIdx.x] = w;
   }
-  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
+  const Tables T = stage_tables<kLds, !kChunk>(a, s_pieces, s_lits);
   __syncthreads();  // s_skels, s_now
   const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
   if constexpr (kChunk) {  // render every skeleton into its template (Now filled in) and its segment list
     const uint32_t ns = a.p.n_skels;
-    for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) s_pofs[q] = 0xFFFFFFFFu;  // pieces of no skeleton
+    for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) s_pofs[q] = 0xFFFFu;  // pieces of no skeleton
     if (threadIdx.x < ns) {
       const kwk_emit_skel S = s_skels[threadIdx.x];
       uint32_t sz = 0;
@@ -591,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       uint32_t pos = s_tsz[threadIdx.x].x, run = pos, sb = s_tsz[threadIdx.x].y, n = 0;
       for (uint32_t q = 0; q < S.n_pieces; ++q) {
         const kwk_emit_piece P = s_pieces[S.first_piece + q];
-        s_pofs[S.first_piece + q] = pos;
+        s_pofs[S.first_piece + q] = (uint16_t)pos;
         pos += P.lit_len;
         if (P.slot == 0) {
           pos += a.now_len;
@@ -606,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) {  // the bytes: one piece per thread
-      if (s_pofs[q] == 0xFFFFFFFFu) continue;
+      if (s_pofs[q] == 0xFFFFu) continue;
       const kwk_emit_piece P = s_pieces[q];
       lds_u8* d = (lds_u8*)(size_t)(lds_addr(s_tpl) + s_pofs[q]);
       const char* src = T.lits + P.lit_off;
@@ -653,9 +688,10 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       pos += s_wb[v];
     }
     const unsigned long long rec_base = pos;
-    uint32_t n_sk = 0;
+    uint32_t n_sk = 0, t0 = 0, t1 = 0;
     if (r < n && x.stage < a.p.n_stages) {
-      const uint32_t t0 = a.p.stage_tpl_ptr[x.stage], t1 = a.p.stage_tpl_ptr[x.stage + 1];
+      t0 = a.p.stage_tpl_ptr[x.stage];
+      t1 = a.p.stage_tpl_ptr[x.stage + 1];
       uint32_t g = (uint32_t)(w >> 16) & 0xFFu;
       for (uint32_t j = t0; j < t1; ++j, ++item) {
         const uint32_t tid = a.p.stage_tpl[j];
@@ -671,9 +707,101 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           ++n_sk;
         }
       }
-      if (kChunk && n_sk && n_sk <= kRecSk) {  // this thread writes the record it just sized
-        const unsigned long long tb = a.tile_bytes[t] & ~15ull;  // the tile's bytes: < 2 GiB past tb
-        ChunkOut o(make_rsrc(a.out + tb, 0x7FFFFFFFu), (uint32_t)(rec_base - tb), (uint32_t)(pos - tb));
+      // the object's guard bits after the patches (all items emitted here; else the host sets them)
+      const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
+      if (x.valid && sz.ok == all) {
+        const uint32_t cls = (uint32_t)(w & 0xFFFFu);
+        if (a.p.stage_delete[x.stage] && cls < a.p.n_classes) g = a.p.fresh[cls];
+        const uint64_t nw = (w & ~(0xFFull << 16)) | (uint64_t)g << 16;
+        if (nw != w) a.words[x.slot] = nw;
+      }
+    }
+    // ---- the bytes
+    bool lane_writes = n_sk != 0;  // this lane writes its own record (per-lane writers)
+    if constexpr (kChunk) {
+      const unsigned long long tb = a.tile_bytes[t] & ~15ull;  // the tile's bytes: < 2 GiB past tb
+      const uint32_t rb = (uint32_t)(rec_base - tb), re = (uint32_t)(pos - tb);
+      bool over = n_sk > kRecSk;
+      uint32_t ns = 0;
+      if (n_sk && !over) {  // table this record's segments: end offsets and LDS sources
+        uint32_t off = 0;
+        for (uint32_t j = 0; j < n_sk && !over; ++j) {
+          const uint2 ss = s_skseg[s_sk[lr * kRecSk + j]];
+          for (uint32_t q = 0; q < ss.y; ++q) {
+            const uint2 sg = s_seg[ss.x + q];
+            uint32_t src = sg.x, len = sg.y;
+            if (sg.y >= kSegValue) {
+              const uint32_t row = lds_addr(&s_vals[sg.x * kTile + lr]);
+              src = row + 1u;
+              len = lds_rd(row) & 0xFFu;
+            }
+            if (!len) continue;
+            if (ns == kRecSegs) {
+              over = true;
+              break;
+            }
+            off += len;
+            s_rend[lr * kRecSegs + ns] = (uint16_t)off;
+            s_rsrc[lr * kRecSegs + ns] = (uint16_t)src;
+            ++ns;
+          }
+        }
+        over = over || off > 0xFFFFu;
+      }
+      s_rb[lr] = rb;
+      s_re[lr] = re;
+      s_rn[lr] = (uint8_t)ns;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      lane_writes = false;
+      if (ballot(over)) {  // wave-uniform: a record the tables cannot hold
+        lane_writes = n_sk != 0;
+      } else {
+        const uint32_t w0 = wave * kWaveRecs;
+        const uint32_t S0 = s_rb[w0], S1 = s_re[w0 + kWaveRecs - 1];
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.out + tb, 0x7FFFFFFFu);
+        const uint32_t mc = (rb + 15u) >> 4;  // the first chunk starting inside or after this record's start
+        uint32_t carry = 0;                   // 1 + the last record started before this round's chunks
+        for (uint32_t cb = S0 >> 4; cb < ((S1 + 15u) >> 4); cb += 64u) {  // wave-uniform
+          s_map[w0 + lane] = 0u;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          if (re > rb && mc >= cb && mc < cb + 64u) atomicMax(&s_map[w0 + mc - cb], lane + 1u);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          const uint32_t m = max(wave_incl_max(s_map[w0 + lane]), carry);
+          carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+          const uint32_t P = (cb + lane) << 4;
+          uint32_t xb[4] = {0u, 0u, 0u, 0u};
+          const bool live = P < S1;
+          if (live) {
+            for (uint32_t q = m ? m - 1u : 0u; q < kWaveRecs; ++q) {  // the records overlapping [P, P + 16)
+              const uint32_t b0 = s_rb[w0 + q];
+              if (b0 >= P + 16u) break;
+              const uint32_t e0 = s_re[w0 + q];
+              if (e0 <= P) continue;
+              const uint32_t lo = (P > b0 ? P - b0 : 0u), hi = min(P + 16u, e0) - b0;
+              const uint32_t R = (w0 + q) * kRecSegs, nsq = s_rn[w0 + q];
+              uint32_t j = 0;  // the first segment ending after lo
+#pragma unroll
+              for (uint32_t step = 8; step; step >>= 1)
+                if (j + step <= nsq && s_rend[R + j + step - 1u] <= lo) j += step;
+              uint32_t sa = j ? s_rend[R + j - 1u] : 0u;
+              for (; j < nsq && sa < hi; ++j) {
+                const uint32_t sb = s_rend[R + j];
+                const uint32_t A = b0 + sa;  // the segment's first byte (tile-relative)
+                uint32_t y[4];
+                lds_load16(s_rsrc[R + j] + P - A, y);
+                merge16(xb, y, A > P ? A - P : 0u, min(b0 + sb - P, 16u));
+                sa = sb;
+              }
+            }
+          }
+          const uint32_t lo_b = S0 > P ? S0 - P : 0u, hi_b = S1 < P + 16u ? S1 - P : 16u;
+          const bool full = live && lo_b == 0u && hi_b == 16u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{xb[0], xb[1], xb[2], xb[3]}, rs, full ? P : kOOB, 0, 0);
+          store_part(rs, P, xb, lo_b, hi_b, live && !full);
+        }
+      }
+      if (lane_writes && n_sk <= kRecSk) {  // per lane, this record
+        ChunkOut o(make_rsrc(a.out + tb, 0x7FFFFFFFu), rb, re);
         for (uint32_t j = 0; j < n_sk; ++j) {
           const uint2 ss = s_skseg[s_sk[lr * kRecSk + j]];
           for (uint32_t q = 0; q < ss.y; ++q) {
@@ -687,26 +815,20 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           }
         }
         o.finish();
-      } else if (n_sk) {  // this thread writes the record it just sized
-        Acc o(a.out, rec_base);
-        if (n_sk <= kRecSk) {
-          for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
-        } else {
-          for (uint32_t j = t0; j < t1; ++j)
-            if ((sz.ok >> (j - t0)) & 1u) lane_skel(a, T, skels[skel_index(a, w, a.p.stage_tpl[j])], x.slot, s_now, V, o);
-        }
-        o.finish();
-      }
-      // the object's guard bits after the patches (all items emitted here; else the host sets them)
-      const uint32_t all = t1 - t0 >= 32 ? 0xFFFFFFFFu : (1u << (t1 - t0)) - 1u;
-      if (x.valid && sz.ok == all) {
-        const uint32_t cls = (uint32_t)(w & 0xFFFFu);
-        if (a.p.stage_delete[x.stage] && cls < a.p.n_classes) g = a.p.fresh[cls];
-        const uint64_t nw = (w & ~(0xFFull << 16)) | (uint64_t)g << 16;
-        if (nw != w) a.words[x.slot] = nw;
+        lane_writes = false;
       }
     }
-    __syncthreads();  // s_wi / s_wb are rewritten by the next tile
+    if (lane_writes) {  // per lane, Acc (four bytes per append)
+      Acc o(a.out, rec_base);
+      if (n_sk <= kRecSk) {
+        for (uint32_t j = 0; j < n_sk; ++j) lane_skel(a, T, skels[s_sk[lr * kRecSk + j]], x.slot, s_now, V, o);
+      } else {
+        for (uint32_t j = t0; j < t1; ++j)
+          if ((sz.ok >> (j - t0)) & 1u) lane_skel(a, T, skels[skel_index(a, w, a.p.stage_tpl[j])], x.slot, s_now, V, o);
+      }
+      o.finish();
+    }
+    __syncthreads();  // s_wi / s_wb and the tables are rewritten by the next tile
   }
   n_ok = wave_sum(n_ok);
   if (lane == 0 && n_ok) atomicAdd(&a.totals[3], (unsigned long long)n_ok);
