@@ -447,6 +447,9 @@ __device__ __forceinline__ void lds_load16(uint32_t A, uint32_t (&y)[4]) {
   y[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
 
+// a if bit is 0, b if 1 (bit: 0 or 1)
+__device__ __forceinline__ uint32_t blend(uint32_t a, uint32_t b, uint32_t bit) { return a ^ ((a ^ b) & (0u - bit)); }
+
 // byte mask of [lo, hi) (0 <= lo <= hi <= 16) as two 64-bit halves
 __device__ __forceinline__ uint64_t ones_bytes(uint32_t n) { return n >= 8u ? ~0ull : (1ull << (8u * n)) - 1ull; }
 __device__ __forceinline__ void merge16(uint32_t (&x)[4], const uint32_t (&y)[4], uint32_t lo, uint32_t hi) {
@@ -475,10 +478,9 @@ __device__ __forceinline__ void store_part(const __amdgpu_buffer_rsrc_t r, uint3
   const uint32_t f0 = b0, f1 = min(b1, (b0 + 3u) & ~3u);
   const uint32_t e0 = max(b0, b1 & ~3u), e1 = b1;
   const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
-  auto byte_at = [=](uint32_t b) __attribute__((always_inline)) {  // selects, not an indexed register array
-    const uint32_t d01 = (b & 4u) ? x1 : x0;
-    const uint32_t d23 = (b & 4u) ? x3 : x2;
-    return (((b & 8u) ? d23 : d01) >> (8u * (b & 3u))) & 0xFFu;
+  auto byte_at = [=](uint32_t b) __attribute__((always_inline)) {  // mask blends, not an indexed register array
+    const uint32_t d = blend(blend(x0, x1, (b >> 2) & 1u), blend(x2, x3, (b >> 2) & 1u), (b >> 3) & 1u);
+    return (d >> (8u * (b & 3u))) & 0xFFu;
   };
 #pragma unroll
   for (uint32_t j = 0; j < 3u; ++j) {
@@ -489,80 +491,116 @@ __device__ __forceinline__ void store_part(const __amdgpu_buffer_rsrc_t r, uint3
   }
 }
 
-// one record's bytes [g0, g1) (g relative to the resource base) from its items' segments
-struct ChunkOut {
-  __amdgpu_buffer_rsrc_t r;
-  uint32_t g0, g1;          // the record's byte range
-  uint32_t P;               // the chunk being filled (16-byte aligned)
-  uint32_t cur;             // output position of the next segment
-  uint32_t x[4];            // the chunk's bytes so far
-  uint32_t f[4];            // the first chunk (shared with the record before), kept for the end
-  bool first_open;          // the first chunk has not left yet
-  __device__ __forceinline__ ChunkOut(__amdgpu_buffer_rsrc_t rs, uint32_t start, uint32_t end)
-      : r(rs), g0(start), g1(end), P(start & ~15u), cur(start), first_open(true) {
+// chunk idx (0..7, per lane) of a 128-byte line buffer: mask blends (a select of two array elements
+// would be folded into an indexed load, and the buffer would leave the registers for scratch)
+__device__ __forceinline__ void pick_chunk(const uint32_t (&buf)[8][4], uint32_t idx, uint32_t (&x)[4]) {
+  const uint32_t b0 = idx & 1u, b1 = (idx >> 1) & 1u, b2 = (idx >> 2) & 1u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = f[k] = 0u;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t0 = blend(buf[0][k], buf[1][k], b0), t1 = blend(buf[2][k], buf[3][k], b0);
+    const uint32_t t2 = blend(buf[4][k], buf[5][k], b0), t3 = blend(buf[6][k], buf[7][k], b0);
+    x[k] = blend(blend(t0, t1, b1), blend(t2, t3, b1), b2);
   }
-  // segment: `len` bytes at LDS byte address `src`
-  __device__ __forceinline__ void segment(uint32_t src, uint32_t len) {
-    const uint32_t a = cur, b = cur + len;
-    cur = b;
-    while (len) {
-      uint32_t y[4];
-      lds_load16(src + P - a, y);  // (P - a wraps below the segment: those bytes are masked out)
-      merge16(x, y, a > P ? a - P : 0u, min(b - P, 16u));
-      if (b < P + 16u) break;  // the segment ends inside the chunk
-      // the chunk is complete: a whole 16-byte store unless it is the record's first (shared) chunk
-      const bool shared = first_open && (g0 & 15u);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], x[1], x[2], x[3]}, r, shared ? kOOB : P, 0, 0);
+}
+
+// bytes [lo, hi) (0 <= lo < hi <= 128) of a 128-byte line buffer at resource offset L: whole chunks
+// as 16-byte stores, the (at most two) chunks cut by lo / hi with dword and byte stores
+__device__ __forceinline__ void store_line_part(const __amdgpu_buffer_rsrc_t r, uint32_t L, const uint32_t (&buf)[8][4],
+                                                uint32_t lo, uint32_t hi, bool live) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        f[k] = shared ? x[k] : f[k];
-        x[k] = 0u;
+  for (uint32_t i = 0; i < 8u; ++i) {
+    const bool whole = live && 16u * i >= lo && 16u * i + 16u <= hi;
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, r, whole ? L + 16u * i : kOOB,
+                                           0, 0);
+  }
+  const uint32_t il = lo >> 4, ih = (hi - 1u) >> 4;
+  uint32_t x[4];
+  pick_chunk(buf, il, x);
+  const bool cut_lo = (lo & 15u) || (il == ih && (hi & 15u));
+  store_part(r, L + 16u * il, x, lo - 16u * il, min(hi - 16u * il, 16u), live && cut_lo);
+  pick_chunk(buf, ih, x);
+  const bool cut_hi = (hi & 15u) && ih != il;
+  store_part(r, L + 16u * ih, x, 0u, hi - 16u * ih, live && cut_hi);
+}
+
+
+// a record's segments in output order: its items' skeleton segment lists (template runs in LDS,
+// value rows of the record in LDS: column c at row0 + c * kTile * 16)
+struct SegIter {
+  const uint2* skseg;
+  const uint2* seg;
+  const int16_t* sk;       // the record's skeleton ids
+  uint32_t row0;           // LDS address of the record's row of value column 0
+  uint32_t n_sk, j, q, n, f;
+  uint32_t sa, sb;         // the current segment's output range [sa, sb) ...
+  uint32_t src;            // ... and the LDS address of its first byte
+  __device__ __forceinline__ void next() {  // the next non-empty segment (sa = sb = ~0 past the last)
+    uint32_t a0 = sb, b0 = 0xFFFFFFFFu, s0 = src;
+    bool found = false;
+    while (!found && (q < n || j < n_sk)) {
+      if (q == n) {
+        const uint2 ss = skseg[sk[j]];
+        f = ss.x;
+        n = ss.y;
+        q = 0;
+        ++j;
+        continue;
       }
-      first_open = false;
-      P += 16u;
-      if (b <= P) break;
+      const uint2 sg = seg[f + q];
+      ++q;
+      uint32_t so = sg.x, len = sg.y;
+      if (sg.y >= kSegValue) {
+        const uint32_t row = row0 + sg.x * kTile * 16u;
+        so = row + 1u;
+        len = lds_rd(row) & 0xFFu;
+      }
+      if (len) {
+        b0 = a0 + len;
+        s0 = so;
+        found = true;
+      }
     }
-  }
-  __device__ __forceinline__ void finish() {
-    const bool had_first = !first_open && (g0 & 15u);
-    const uint32_t fb = had_first ? (g0 & ~15u) : 0u;
-    store_part(r, fb, f, g0 & 15u, 16u, had_first);                   // the first chunk, if it left the loop
-    store_part(r, P, x, first_open ? (g0 & 15u) : 0u, cur - P, cur > P);  // the last one (maybe also the first)
+    sa = found ? a0 : 0xFFFFFFFFu;
+    sb = b0;
+    src = s0;
   }
 };
 
-__device__ __forceinline__ unsigned long long ballot(const bool b) { return __builtin_amdgcn_ballot_w64(b); }
-
-// inclusive prefix maximum over the wave's lanes (DPP row shifts and broadcasts; 0 is the identity)
-template <int C, int RM>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, C, RM, 0xF, false);
+// the eight 16-byte chunks of the line at L, gathered from the segments overlapping them
+__device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (&buf)[8][4]) {
+#pragma unroll
+  for (uint32_t i = 0; i < 8u; ++i) {
+    const uint32_t P = L + 16u * i;
+    uint32_t x0 = 0u, x1 = 0u, x2 = 0u, x3 = 0u;
+    while (it.sa < P + 16u) {
+      if (it.sb > P) {
+        uint32_t y[4], x[4] = {x0, x1, x2, x3};
+        lds_load16(it.src + P - it.sa, y);  // (bytes before the segment are masked out)
+        merge16(x, y, it.sa > P ? it.sa - P : 0u, min(it.sb - P, 16u));
+        x0 = x[0];
+        x1 = x[1];
+        x2 = x[2];
+        x3 = x[3];
+      }
+      if (it.sb > P + 16u) break;  // the segment continues into the next chunk
+      it.next();
+    }
+    buf[i][0] = x0;
+    buf[i][1] = x1;
+    buf[i][2] = x2;
+    buf[i][3] = x3;
+  }
 }
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  v = max(v, dpp_u32<0x111, 0xF>(v));
-  v = max(v, dpp_u32<0x112, 0xF>(v));
-  v = max(v, dpp_u32<0x114, 0xF>(v));
-  v = max(v, dpp_u32<0x118, 0xF>(v));
-  v = max(v, dpp_u32<0x142, 0xA>(v));
-  v = max(v, dpp_u32<0x143, 0xC>(v));
-  return v;
-}
 
-constexpr uint32_t kRecSegs = 12;  // segments of a record the cooperative writer tables (more: per-lane writers)
-
-// kChunk (the default when the program's tables fit in LDS): each wave writes its 64 records'
-// bytes — one contiguous span — together, lane L taking the span's aligned 16-byte chunks L, L + 64,
-// ...: every store instruction writes 1 KiB of whole lines.  The records' segments (template runs of
-// the skeletons rendered above, value rows) are tabled in LDS by their owner lanes; a chunk finds its
-// record by a prefix maximum over the lanes of "the last record starting at or before me", its
-// segment by a binary search in the record's table, and gathers its bytes from LDS.  (Lanes each
-// writing their own record scatter 16-byte stores over 64 lines: the L2 then writes half-filled lines
-// back and refills them — r5e: 2x the patch bytes written, 0.6x read.)  A wave with a record beyond
-// the tables (> kRecSk items, > kRecSegs segments) writes per lane (ChunkOut; Acc past kRecSk items).
-// !kChunk: per lane, Acc.  kLds: the skeleton tables and the records' call-value rows (at most
-// kLdsCols columns of 16 bytes) staged in LDS
+// Each thread writes the record it sized.  kChunk (the default when the program's tables fit in
+// LDS): the line writer above — the record's bytes gathered 16 at a time from its items' segments
+// (the skeletons' rendered templates and its value rows, all in LDS) and stored a 128-byte line at a
+// time.  (The first version, 16-byte stores as each chunk filled, left the L2 writing half-filled
+// lines back and refilling them: r5e, 2x the patch bytes written; a wave writing its records'
+// span together, lane L taking chunks L, L + 64, ..., stored whole lines but spent ~4x the VALU
+// finding each chunk's record and segment: r5f, 3.1 vs 2.4 ms.)  Records of more than kRecSk items
+// and !kChunk: Acc, four bytes per append.  kLds: the skeleton tables and the records' call-value
+// rows (at most kLdsCols columns of 16 bytes) staged in LDS
 template <bool kLds, bool kChunk>
 __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   static_assert(kLds || !kChunk, "the chunk writer reads its tables from LDS");
@@ -571,11 +609,6 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   __shared__ uint2 s_skseg[kChunk ? kLdsSkels : 1];
   __shared__ uint16_t s_pofs[kChunk ? kLdsPieces : 1];
   __shared__ uint2 s_tsz[kChunk ? kLdsSkels : 1];
-  __shared__ uint16_t s_rend[kChunk ? kTile * kRecSegs : 1];  // per record: its segments' end offsets
-  __shared__ uint16_t s_rsrc[kChunk ? kTile * kRecSegs : 1];  // ... and LDS source addresses (< 64 KiB)
-  __shared__ uint32_t s_rb[kChunk ? kTile : 1], s_re[kChunk ? kTile : 1];
-  __shared__ uint8_t s_rn[kChunk ? kTile : 1];
-  __shared__ uint32_t s_map[kChunk ? kTile : 1];              // per wave: chunk -> 1 + last record starting there
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
   __shared__ int16_t s_sk[kTile * kRecSk];
@@ -717,105 +750,33 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
       }
     }
     // ---- the bytes
-    bool lane_writes = n_sk != 0;  // this lane writes its own record (per-lane writers)
+    bool lane_writes = n_sk != 0;  // this lane writes its own record with Acc
     if constexpr (kChunk) {
       const unsigned long long tb = a.tile_bytes[t] & ~15ull;  // the tile's bytes: < 2 GiB past tb
-      const uint32_t rb = (uint32_t)(rec_base - tb), re = (uint32_t)(pos - tb);
-      bool over = n_sk > kRecSk;
-      uint32_t ns = 0;
-      if (n_sk && !over) {  // table this record's segments: end offsets and LDS sources
-        uint32_t off = 0;
-        for (uint32_t j = 0; j < n_sk && !over; ++j) {
-          const uint2 ss = s_skseg[s_sk[lr * kRecSk + j]];
-          for (uint32_t q = 0; q < ss.y; ++q) {
-            const uint2 sg = s_seg[ss.x + q];
-            uint32_t src = sg.x, len = sg.y;
-            if (sg.y >= kSegValue) {
-              const uint32_t row = lds_addr(&s_vals[sg.x * kTile + lr]);
-              src = row + 1u;
-              len = lds_rd(row) & 0xFFu;
-            }
-            if (!len) continue;
-            if (ns == kRecSegs) {
-              over = true;
-              break;
-            }
-            off += len;
-            s_rend[lr * kRecSegs + ns] = (uint16_t)off;
-            s_rsrc[lr * kRecSegs + ns] = (uint16_t)src;
-            ++ns;
-          }
-        }
-        over = over || off > 0xFFFFu;
-      }
-      s_rb[lr] = rb;
-      s_re[lr] = re;
-      s_rn[lr] = (uint8_t)ns;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      lane_writes = false;
-      if (ballot(over)) {  // wave-uniform: a record the tables cannot hold
-        lane_writes = n_sk != 0;
-      } else {
-        const uint32_t w0 = wave * kWaveRecs;
-        const uint32_t S0 = s_rb[w0], S1 = s_re[w0 + kWaveRecs - 1];
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.out + tb, 0x7FFFFFFFu);
-        const uint32_t mc = (rb + 15u) >> 4;  // the first chunk starting inside or after this record's start
-        uint32_t carry = 0;                   // 1 + the last record started before this round's chunks
-        for (uint32_t cb = S0 >> 4; cb < ((S1 + 15u) >> 4); cb += 64u) {  // wave-uniform
-          s_map[w0 + lane] = 0u;
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          if (re > rb && mc >= cb && mc < cb + 64u) atomicMax(&s_map[w0 + mc - cb], lane + 1u);
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          const uint32_t m = max(wave_incl_max(s_map[w0 + lane]), carry);
-          carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
-          const uint32_t P = (cb + lane) << 4;
-          uint32_t xb[4] = {0u, 0u, 0u, 0u};
-          const bool live = P < S1;
-          if (live) {
-            for (uint32_t q = m ? m - 1u : 0u; q < kWaveRecs; ++q) {  // the records overlapping [P, P + 16)
-              const uint32_t b0 = s_rb[w0 + q];
-              if (b0 >= P + 16u) break;
-              const uint32_t e0 = s_re[w0 + q];
-              if (e0 <= P) continue;
-              const uint32_t lo = (P > b0 ? P - b0 : 0u), hi = min(P + 16u, e0) - b0;
-              const uint32_t R = (w0 + q) * kRecSegs, nsq = s_rn[w0 + q];
-              uint32_t j = 0;  // the first segment ending after lo
-#pragma unroll
-              for (uint32_t step = 8; step; step >>= 1)
-                if (j + step <= nsq && s_rend[R + j + step - 1u] <= lo) j += step;
-              uint32_t sa = j ? s_rend[R + j - 1u] : 0u;
-              for (; j < nsq && sa < hi; ++j) {
-                const uint32_t sb = s_rend[R + j];
-                const uint32_t A = b0 + sa;  // the segment's first byte (tile-relative)
-                uint32_t y[4];
-                lds_load16(s_rsrc[R + j] + P - A, y);
-                merge16(xb, y, A > P ? A - P : 0u, min(b0 + sb - P, 16u));
-                sa = sb;
-              }
-            }
-          }
-          const uint32_t lo_b = S0 > P ? S0 - P : 0u, hi_b = S1 < P + 16u ? S1 - P : 16u;
-          const bool full = live && lo_b == 0u && hi_b == 16u;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{xb[0], xb[1], xb[2], xb[3]}, rs, full ? P : kOOB, 0, 0);
-          store_part(rs, P, xb, lo_b, hi_b, live && !full);
-        }
-      }
-      if (lane_writes && n_sk <= kRecSk) {  // per lane, this record
-        ChunkOut o(make_rsrc(a.out + tb, 0x7FFFFFFFu), rb, re);
-        for (uint32_t j = 0; j < n_sk; ++j) {
-          const uint2 ss = s_skseg[s_sk[lr * kRecSk + j]];
-          for (uint32_t q = 0; q < ss.y; ++q) {
-            const uint2 sg = s_seg[ss.x + q];
-            if (sg.y >= kSegValue) {
-              const uint32_t row = lds_addr(&s_vals[sg.x * kTile + lr]);
-              o.segment(row + 1u, lds_rd(row) & 0xFFu);
-            } else {
-              o.segment(sg.x, sg.y);
-            }
-          }
-        }
-        o.finish();
+      const uint32_t g0 = (uint32_t)(rec_base - tb), g1 = (uint32_t)(pos - tb);
+      if (n_sk && n_sk <= kRecSk) {
         lane_writes = false;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.out + tb, 0x7FFFFFFFu);
+        SegIter it{s_skseg, s_seg, s_sk + lr * kRecSk, lds_addr(&s_vals[lr]), n_sk, 0u, 0u, 0u, 0u, g0, g0, 0u};
+        it.next();
+        if (g1 > g0) {
+          // the first and the last line share bytes with the neighbouring records: both are stored
+          // at the end, when the neighbours' lanes store theirs (the same instructions: the L2 gets
+          // each shared line whole); the lines between leave as eight 16-byte stores each
+          const uint32_t Lf = g0 & ~127u, Ll = (g1 - 1u) & ~127u;
+          uint32_t fl[8][4], buf[8][4];
+          produce_line(it, Lf, fl);
+          for (uint32_t L = Lf + 128u; L < Ll; L += 128u) {
+            produce_line(it, L, buf);
+#pragma unroll
+            for (uint32_t i = 0; i < 8u; ++i)
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, rs, L + 16u * i, 0,
+                                                     0);
+          }
+          if (Ll != Lf) produce_line(it, Ll, buf);
+          store_line_part(rs, Lf, fl, g0 - Lf, min(g1 - Lf, 128u), true);
+          store_line_part(rs, Ll, buf, 0u, g1 - Ll, Ll != Lf);
+        }
       }
     }
     if (lane_writes) {  // per lane, Acc (four bytes per append)
