@@ -493,22 +493,22 @@ __device__ __forceinline__ void store_part(const __amdgpu_buffer_rsrc_t r, uint3
 
 // chunk idx (0..7, per lane) of a 128-byte line buffer: mask blends (a select of two array elements
 // would be folded into an indexed load, and the buffer would leave the registers for scratch)
-__device__ __forceinline__ void pick_chunk(const uint32_t (&buf)[8][4], uint32_t idx, uint32_t (&x)[4]) {
-  const uint32_t b0 = idx & 1u, b1 = (idx >> 1) & 1u, b2 = (idx >> 2) & 1u;
+constexpr uint32_t kLine = 64;             // bytes per burst of the line writer (a 64-byte half line: the
+constexpr uint32_t kLineChunks = kLine / 16;  // HBM burst; 128 held twice the registers, 3 vs 5 waves per SIMD)
+__device__ __forceinline__ void pick_chunk(const uint32_t (&buf)[kLineChunks][4], uint32_t idx, uint32_t (&x)[4]) {
+  static_assert(kLineChunks == 4, "a two-level blend tree");
+  const uint32_t b0 = idx & 1u, b1 = (idx >> 1) & 1u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t t0 = blend(buf[0][k], buf[1][k], b0), t1 = blend(buf[2][k], buf[3][k], b0);
-    const uint32_t t2 = blend(buf[4][k], buf[5][k], b0), t3 = blend(buf[6][k], buf[7][k], b0);
-    x[k] = blend(blend(t0, t1, b1), blend(t2, t3, b1), b2);
-  }
+  for (int k = 0; k < 4; ++k)
+    x[k] = blend(blend(buf[0][k], buf[1][k], b0), blend(buf[2][k], buf[3][k], b0), b1);
 }
 
-// bytes [lo, hi) (0 <= lo < hi <= 128) of a 128-byte line buffer at resource offset L: whole chunks
+// bytes [lo, hi) (0 <= lo < hi <= kLine) of a line buffer at resource offset L: whole chunks
 // as 16-byte stores, the (at most two) chunks cut by lo / hi with dword and byte stores
-__device__ __forceinline__ void store_line_part(const __amdgpu_buffer_rsrc_t r, uint32_t L, const uint32_t (&buf)[8][4],
+__device__ __forceinline__ void store_line_part(const __amdgpu_buffer_rsrc_t r, uint32_t L, const uint32_t (&buf)[kLineChunks][4],
                                                 uint32_t lo, uint32_t hi, bool live) {
 #pragma unroll
-  for (uint32_t i = 0; i < 8u; ++i) {
+  for (uint32_t i = 0; i < kLineChunks; ++i) {
     const bool whole = live && 16u * i >= lo && 16u * i + 16u <= hi;
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, r, whole ? L + 16u * i : kOOB,
                                            0, 0);
@@ -566,10 +566,10 @@ struct SegIter {
   }
 };
 
-// the eight 16-byte chunks of the line at L, gathered from the segments overlapping them
-__device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (&buf)[8][4]) {
+// the 16-byte chunks of the line at L, gathered from the segments overlapping them
+__device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (&buf)[kLineChunks][4]) {
 #pragma unroll
-  for (uint32_t i = 0; i < 8u; ++i) {
+  for (uint32_t i = 0; i < kLineChunks; ++i) {
     const uint32_t P = L + 16u * i;
     uint32_t x0 = 0u, x1 = 0u, x2 = 0u, x3 = 0u;
     while (it.sa < P + 16u) {
@@ -594,7 +594,7 @@ __device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (
 
 // Each thread writes the record it sized.  kChunk (the default when the program's tables fit in
 // LDS): the line writer above — the record's bytes gathered 16 at a time from its items' segments
-// (the skeletons' rendered templates and its value rows, all in LDS) and stored a 128-byte line at a
+// (the skeletons' rendered templates and its value rows, all in LDS) and stored kLine bytes at a
 // time.  (The first version, 16-byte stores as each chunk filled, left the L2 writing half-filled
 // lines back and refilling them: r5e, 2x the patch bytes written; a wave writing its records'
 // span together, lane L taking chunks L, L + 64, ..., stored whole lines but spent ~4x the VALU
@@ -697,9 +697,10 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     if (r < n) {
       x = fetch(a, r);
       w = x.valid ? a.words[x.slot] : 0ull;
-      if constexpr (kLds) {  // the record's value rows, one 16-byte gather per column
+      if constexpr (kLds) {  // the record's value rows, one 16-byte gather per column (stages with patches only)
+        const bool any = x.valid && x.stage < a.p.n_stages && a.p.stage_tpl_ptr[x.stage + 1] > a.p.stage_tpl_ptr[x.stage];
         for (uint32_t c = 0; c < kLdsCols; ++c)
-          s_vals[c * kTile + lr] = c < a.p.n_cols && x.valid
+          s_vals[c * kTile + lr] = c < a.p.n_cols && any
                                        ? *reinterpret_cast<const uint4*>(a.p.cols[c] + (uint64_t)x.slot * 16u)
                                        : make_uint4(0xFFu, 0u, 0u, 0u);
       }
@@ -763,18 +764,18 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
           // the first and the last line share bytes with the neighbouring records: both are stored
           // at the end, when the neighbours' lanes store theirs (the same instructions: the L2 gets
           // each shared line whole); the lines between leave as eight 16-byte stores each
-          const uint32_t Lf = g0 & ~127u, Ll = (g1 - 1u) & ~127u;
-          uint32_t fl[8][4], buf[8][4];
+          const uint32_t Lf = g0 & ~(kLine - 1u), Ll = (g1 - 1u) & ~(kLine - 1u);
+          uint32_t fl[kLineChunks][4], buf[kLineChunks][4];
           produce_line(it, Lf, fl);
-          for (uint32_t L = Lf + 128u; L < Ll; L += 128u) {
+          for (uint32_t L = Lf + kLine; L < Ll; L += kLine) {
             produce_line(it, L, buf);
 #pragma unroll
-            for (uint32_t i = 0; i < 8u; ++i)
+            for (uint32_t i = 0; i < kLineChunks; ++i)
               __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, rs, L + 16u * i, 0,
                                                      0);
           }
           if (Ll != Lf) produce_line(it, Ll, buf);
-          store_line_part(rs, Lf, fl, g0 - Lf, min(g1 - Lf, 128u), true);
+          store_line_part(rs, Lf, fl, g0 - Lf, min(g1 - Lf, kLine), true);
           store_line_part(rs, Ll, buf, 0u, g1 - Ll, Ll != Lf);
         }
       }
@@ -803,7 +804,8 @@ struct kwk_emitter {
   hipStream_t stream = nullptr;  // the engine's stream as of the current call (kwk_stream at every entry:
                                  // KWK_TUNE_STREAM_PRIORITY re-creates it, so it is never cached across calls)
   int device = 0;
-  uint32_t capacity = 0, n_columns = 0, max_tiles = 0, grid = 0;
+  uint32_t capacity = 0, n_columns = 0, max_tiles = 0, grid = 0, cus = 1;
+  int write_occ[3] = {0, 0, 0};   // resident blocks per CU of each write kernel variant (0: not asked yet)
   Prog p{};
   std::vector<void*> allocs;
   std::vector<uint32_t> stride;
@@ -981,6 +983,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, em->device));
   em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 8u));
+  em->cus = (uint32_t)std::max(1, cus);
   HIP_TRY(hipEventCreate(&em->ev0));
   HIP_TRY(hipEventCreate(&em->ev1));
   return KWK_OK;
@@ -1126,7 +1129,15 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
                    : wl  ? (const void*)emit_write_kernel<true, false>
                          : (const void*)emit_write_kernel<false, false>;
   void* wargs[] = {&a};
-  HIP_TRY(hipLaunchKernel(wk, dim3(em->grid), dim3(kBlock), wargs, 0, em->stream));
+  // the write kernel's grid: every block resident at once (one round; its tile loop does the rest)
+  const int vi = chunk ? 0 : wl ? 1 : 2;
+  if (!em->write_occ[vi]) {
+    int occ = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wk, kBlock, 0));
+    em->write_occ[vi] = std::max(1, occ);
+  }
+  const uint32_t wgrid = std::max(1u, std::min(em->max_tiles, em->cus * (uint32_t)em->write_occ[vi]));
+  HIP_TRY(hipLaunchKernel(wk, dim3(wgrid), dim3(kBlock), wargs, 0, em->stream));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(em->ev1, em->stream));
   em->emitted = true;
