@@ -493,14 +493,17 @@ __device__ __forceinline__ void store_part(const __amdgpu_buffer_rsrc_t r, uint3
 
 // chunk idx (0..7, per lane) of a 128-byte line buffer: mask blends (a select of two array elements
 // would be folded into an indexed load, and the buffer would leave the registers for scratch)
-constexpr uint32_t kLine = 64;             // bytes per burst of the line writer (a 64-byte half line: the
-constexpr uint32_t kLineChunks = kLine / 16;  // HBM burst; 128 held twice the registers, 3 vs 5 waves per SIMD)
+constexpr uint32_t kLine = 128;            // bytes per burst of the line writer: one L2 line (64-byte bursts
+constexpr uint32_t kLineChunks = kLine / 16;  // left the L2 writing half lines back: r5h, 1.35x the bytes)
 __device__ __forceinline__ void pick_chunk(const uint32_t (&buf)[kLineChunks][4], uint32_t idx, uint32_t (&x)[4]) {
-  static_assert(kLineChunks == 4, "a two-level blend tree");
-  const uint32_t b0 = idx & 1u, b1 = (idx >> 1) & 1u;
+  static_assert(kLineChunks == 8, "a three-level blend tree");
+  const uint32_t b0 = idx & 1u, b1 = (idx >> 1) & 1u, b2 = (idx >> 2) & 1u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    x[k] = blend(blend(buf[0][k], buf[1][k], b0), blend(buf[2][k], buf[3][k], b0), b1);
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t0 = blend(buf[0][k], buf[1][k], b0), t1 = blend(buf[2][k], buf[3][k], b0);
+    const uint32_t t2 = blend(buf[4][k], buf[5][k], b0), t3 = blend(buf[6][k], buf[7][k], b0);
+    x[k] = blend(blend(t0, t1, b1), blend(t2, t3, b1), b2);
+  }
 }
 
 // bytes [lo, hi) (0 <= lo < hi <= kLine) of a line buffer at resource offset L: whole chunks
@@ -524,40 +527,48 @@ __device__ __forceinline__ void store_line_part(const __amdgpu_buffer_rsrc_t r, 
 }
 
 
-// a record's segments in output order: its items' skeleton segment lists (template runs in LDS,
-// value rows of the record in LDS: column c at row0 + c * kTile * 16)
+// the tile's bytes from record `rec` on, segment by segment in output order: each record's items'
+// skeleton segment lists (template runs in LDS; value column c of record r at vals0 + (c * kTile +
+// r) * 16), records of no bytes skipped
 struct SegIter {
   const uint2* skseg;
   const uint2* seg;
-  const int16_t* sk;       // the record's skeleton ids
-  uint32_t row0;           // LDS address of the record's row of value column 0
-  uint32_t n_sk, j, q, n, f;
+  const int16_t* sk;       // per record: its skeleton ids (kRecSk each)
+  const uint8_t* nsk;      // per record: its items
+  uint32_t vals0;
+  uint32_t rec, n_sk, j, q, n, f;
   uint32_t sa, sb;         // the current segment's output range [sa, sb) ...
   uint32_t src;            // ... and the LDS address of its first byte
-  __device__ __forceinline__ void next() {  // the next non-empty segment (sa = sb = ~0 past the last)
+  __device__ __forceinline__ void next() {  // the next non-empty segment (sa = ~0 past the tile's last)
     uint32_t a0 = sb, b0 = 0xFFFFFFFFu, s0 = src;
     bool found = false;
-    while (!found && (q < n || j < n_sk)) {
-      if (q == n) {
-        const uint2 ss = skseg[sk[j]];
+    while (!found) {
+      if (q < n) {
+        const uint2 sg = seg[f + q];
+        ++q;
+        uint32_t so = sg.x, len = sg.y;
+        if (sg.y >= kSegValue) {
+          const uint32_t row = vals0 + (sg.x * kTile + rec) * 16u;
+          so = row + 1u;
+          len = lds_rd(row) & 0xFFu;
+        }
+        if (len) {
+          b0 = a0 + len;
+          s0 = so;
+          found = true;
+        }
+      } else if (j < n_sk) {
+        const uint2 ss = skseg[sk[rec * kRecSk + j]];
         f = ss.x;
         n = ss.y;
         q = 0;
         ++j;
-        continue;
-      }
-      const uint2 sg = seg[f + q];
-      ++q;
-      uint32_t so = sg.x, len = sg.y;
-      if (sg.y >= kSegValue) {
-        const uint32_t row = row0 + sg.x * kTile * 16u;
-        so = row + 1u;
-        len = lds_rd(row) & 0xFFu;
-      }
-      if (len) {
-        b0 = a0 + len;
-        s0 = so;
-        found = true;
+      } else if (rec + 1u < kTile) {  // the next record: its bytes follow these
+        ++rec;
+        n_sk = nsk[rec];
+        j = q = n = 0;
+      } else {
+        break;
       }
     }
     sa = found ? a0 : 0xFFFFFFFFu;
@@ -612,6 +623,8 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 s_vals[kLds ? kLdsCols * kTile : 1];
   __shared__ kwk_emit_skel s_skels[kLds ? kLdsSkels : 1];
   __shared__ int16_t s_sk[kTile * kRecSk];
+  __shared__ uint8_t s_nsk[kChunk ? kTile : 1];  // items per record (the line writer's iterator)
+  __shared__ uint32_t s_tend;                    // the tile's bytes end (relative to its 16-byte aligned base)
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
   __shared__ uint32_t s_lits[kLds && !kChunk ? kLdsLits / 4 : 1];
   __shared__ uint32_t s_wi[kWaves];
@@ -755,28 +768,33 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     if constexpr (kChunk) {
       const unsigned long long tb = a.tile_bytes[t] & ~15ull;  // the tile's bytes: < 2 GiB past tb
       const uint32_t g0 = (uint32_t)(rec_base - tb), g1 = (uint32_t)(pos - tb);
-      if (n_sk && n_sk <= kRecSk) {
+      s_nsk[lr] = (uint8_t)min(n_sk, kRecSk);
+      if (lr == kTile - 1u) s_tend = g1;
+      // a record of more than kRecSk items: the whole tile per lane (Acc)
+      if (!__syncthreads_or(n_sk > kRecSk)) {
         lane_writes = false;
+        // lane r writes the 128-byte lines that start inside its record, their bytes past it
+        // from the records after it: every line of the tile leaves whole, once (lane 0 also
+        // writes its part of the line the tile shares with the tile before, and the tile's last
+        // line is cut at its end)
+        const uint32_t tend = s_tend;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.out + tb, 0x7FFFFFFFu);
-        SegIter it{s_skseg, s_seg, s_sk + lr * kRecSk, lds_addr(&s_vals[lr]), n_sk, 0u, 0u, 0u, 0u, g0, g0, 0u};
+        SegIter it{s_skseg, s_seg, s_sk, s_nsk, lds_addr(s_vals), lr, s_nsk[lr], 0u, 0u, 0u, 0u, g0, g0, 0u};
         it.next();
-        if (g1 > g0) {
-          // the first and the last line share bytes with the neighbouring records: both are stored
-          // at the end, when the neighbours' lanes store theirs (the same instructions: the L2 gets
-          // each shared line whole); the lines between leave as eight 16-byte stores each
-          const uint32_t Lf = g0 & ~(kLine - 1u), Ll = (g1 - 1u) & ~(kLine - 1u);
-          uint32_t fl[kLineChunks][4], buf[kLineChunks][4];
-          produce_line(it, Lf, fl);
-          for (uint32_t L = Lf + kLine; L < Ll; L += kLine) {
-            produce_line(it, L, buf);
+        uint32_t buf[kLineChunks][4];
+        const uint32_t L0 = g0 & ~(kLine - 1u);
+        if (lr == 0 && L0 != g0 && tend > g0) {  // the tile's head line
+          produce_line(it, L0, buf);
+          store_line_part(rs, L0, buf, g0 - L0, min(tend - L0, kLine), true);
+        }
+        for (uint32_t L = (g0 + kLine - 1u) & ~(kLine - 1u); L < g1; L += kLine) {
+          produce_line(it, L, buf);
+          const bool whole = L + kLine <= tend;
 #pragma unroll
-            for (uint32_t i = 0; i < kLineChunks; ++i)
-              __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, rs, L + 16u * i, 0,
-                                                     0);
-          }
-          if (Ll != Lf) produce_line(it, Ll, buf);
-          store_line_part(rs, Lf, fl, g0 - Lf, min(g1 - Lf, kLine), true);
-          store_line_part(rs, Ll, buf, 0u, g1 - Ll, Ll != Lf);
+          for (uint32_t i = 0; i < kLineChunks; ++i)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, rs,
+                                                   whole ? L + 16u * i : kOOB, 0, 0);
+          store_line_part(rs, L, buf, 0u, min(tend - L, kLine), !whole);
         }
       }
     }
