@@ -779,15 +779,16 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         // line is cut at its end)
         const uint32_t tend = s_tend;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.out + tb, 0x7FFFFFFFu);
+        const uint32_t L0 = g0 & ~(kLine - 1u), L1 = (g0 + kLine - 1u) & ~(kLine - 1u);
+        const bool head = lr == 0 && L0 != g0 && tend > g0;  // the tile's head line
         SegIter it{s_skseg, s_seg, s_sk, s_nsk, lds_addr(s_vals), lr, s_nsk[lr], 0u, 0u, 0u, 0u, g0, g0, 0u};
-        it.next();
+        if (head || L1 < g1) it.next();  // (a lane with no line to write never walks the records after it)
         uint32_t buf[kLineChunks][4];
-        const uint32_t L0 = g0 & ~(kLine - 1u);
-        if (lr == 0 && L0 != g0 && tend > g0) {  // the tile's head line
+        if (head) {
           produce_line(it, L0, buf);
           store_line_part(rs, L0, buf, g0 - L0, min(tend - L0, kLine), true);
         }
-        for (uint32_t L = (g0 + kLine - 1u) & ~(kLine - 1u); L < g1; L += kLine) {
+        for (uint32_t L = L1; L < g1; L += kLine) {
           produce_line(it, L, buf);
           const bool whole = L + kLine <= tend;
 #pragma unroll
