@@ -90,19 +90,42 @@ struct EmitArgs {
   char now[40];
 };
 
+// per skeleton (LDS, built per block for this call's Now length): x = its fixed bytes (literal runs
+// and Now) | value slots << 24 (kSkszPieces: more than 4, count them piece by piece), y = the slots'
+// value columns, a byte each
+constexpr uint32_t kSkszPieces = 0xFFu;
+__device__ __forceinline__ void build_sksz(const EmitArgs& a, const kwk_emit_piece* pieces, uint2* sksz) {
+  for (uint32_t k = threadIdx.x; k < a.p.n_skels && k < kLdsSkels; k += blockDim.x) {
+    const kwk_emit_skel S = a.p.skels[k];
+    uint32_t fixed = 0, nv = 0, cols = 0;
+    for (uint32_t q = 0; q < S.n_pieces; ++q) {
+      const kwk_emit_piece P = pieces[S.first_piece + q];
+      fixed += P.lit_len + (P.slot == 0 ? a.now_len : 0u);
+      if (P.slot != 0 && P.slot != KWK_EMIT_NO_SLOT) {
+        if (nv < 4u) cols |= (uint32_t)(P.slot - 1u) << (8u * nv);
+        ++nv;
+      }
+    }
+    sksz[k] = make_uint2(nv > 4u || fixed >= (1u << 24) ? kSkszPieces << 24 : fixed | nv << 24, cols);
+  }
+}
+
 // the skeleton pieces and literal runs a kernel reads: LDS copies when the program's fit
 struct Tables {
   const kwk_emit_piece* pieces;
   const char* lits;
+  const uint2* sksz = nullptr;  // per-skeleton sizes (build_sksz), when staged
 };
 
 template <bool kLds, bool kLits = true>
-__device__ __forceinline__ Tables stage_tables(const EmitArgs& a, kwk_emit_piece* s_pieces, uint32_t* s_lits) {
+__device__ __forceinline__ Tables stage_tables(const EmitArgs& a, kwk_emit_piece* s_pieces, uint32_t* s_lits,
+                                               uint2* s_sksz) {
   if constexpr (kLds) {
     for (uint32_t j = threadIdx.x; j < a.p.n_pieces; j += blockDim.x) s_pieces[j] = a.p.pieces[j];
+    build_sksz(a, a.p.pieces, s_sksz);
     if constexpr (!kLits) {  // the literal runs stay in global memory
       __syncthreads();
-      return Tables{s_pieces, a.p.lits};
+      return Tables{s_pieces, a.p.lits, s_sksz};
     }
     const uint32_t nw = (a.p.n_lits + 3u) / 4u;
     for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
@@ -112,9 +135,9 @@ __device__ __forceinline__ Tables stage_tables(const EmitArgs& a, kwk_emit_piece
       s_lits[j] = w;
     }
     __syncthreads();
-    return Tables{s_pieces, reinterpret_cast<const char*>(s_lits)};
+    return Tables{s_pieces, reinterpret_cast<const char*>(s_lits), s_sksz};
   } else {
-    return Tables{a.p.pieces, a.p.lits};
+    return Tables{a.p.pieces, a.p.lits, nullptr};
   }
 }
 
@@ -150,9 +173,23 @@ struct Vals {
   }
 };
 
-// bytes of one skeleton for this slot, or -1 when a value is unusable
-__device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables& T, const kwk_emit_skel& S,
-                                                uint32_t slot, const Vals& V = Vals{nullptr, 0}) {
+// bytes of skeleton k for this slot, or -1 when a value is unusable
+__device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables& T, uint32_t k, uint32_t slot,
+                                                const Vals& V = Vals{nullptr, 0}) {
+  if (T.sksz) {
+    const uint2 z = T.sksz[k];
+    const uint32_t nv = z.x >> 24;
+    if (nv != kSkszPieces) {
+      long long b = z.x & 0xFFFFFFu;
+      for (uint32_t i = 0; i < nv; ++i) {
+        const uint32_t len = V.row(a, (z.y >> (8u * i)) & 0xFFu, slot)[0];
+        if (len == 0xFFu) return -1;
+        b += len;
+      }
+      return b;
+    }
+  }
+  const kwk_emit_skel S = a.p.skels[k];
   long long b = 0;
   for (uint32_t q = 0; q < S.n_pieces; ++q) {
     const kwk_emit_piece P = T.pieces[S.first_piece + q];
@@ -191,7 +228,7 @@ __device__ __forceinline__ Size rec_size(const EmitArgs& a, const Tables& T, con
     ++s.items;
     const int k = x.valid ? skel_index(a, w, a.p.stage_tpl[j]) : -1;
     if (k < 0) continue;
-    const long long b = skel_bytes(a, T, a.p.skels[k], x.slot, V);
+    const long long b = skel_bytes(a, T, (uint32_t)k, x.slot, V);
     if (b < 0) continue;
     s.ok |= 1u << (j - t0);
     s.bytes += (unsigned long long)b;
@@ -316,9 +353,10 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock) void emit_size_kernel(EmitArgs a) {
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
   __shared__ uint32_t s_lits[kLds ? kLdsLits / 4 : 1];
+  __shared__ uint2 s_sksz[kLds ? kLdsSkels : 1];
   __shared__ uint32_t s_i[kWaves];
   __shared__ unsigned long long s_b[kWaves];
-  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits);
+  const Tables T = stage_tables<kLds>(a, s_pieces, s_lits, s_sksz);
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -613,7 +651,7 @@ __device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (
 // and !kChunk: Acc, four bytes per append.  kLds: the skeleton tables and the records' call-value
 // rows (at most kLdsCols columns of 16 bytes) staged in LDS
 template <bool kLds, bool kChunk>
-__global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kChunk ? 5 : 1))) void emit_write_kernel(EmitArgs a) {
   static_assert(kLds || !kChunk, "the chunk writer reads its tables from LDS");
   __shared__ __attribute__((aligned(16))) uint32_t s_tpl[kChunk ? kTplBytes / 4 + 8 : 1];
   __shared__ uint2 s_seg[kChunk ? kMaxSegs : 1];
@@ -627,6 +665,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
   __shared__ uint32_t s_tend;                    // the tile's bytes end (relative to its 16-byte aligned base)
   __shared__ kwk_emit_piece s_pieces[kLds ? kLdsPieces : 1];
   __shared__ uint32_t s_lits[kLds && !kChunk ? kLdsLits / 4 : 1];
+  __shared__ uint2 s_sksz[kLds ? kLdsSkels : 1];
   __shared__ uint32_t s_wi[kWaves];
   __shared__ unsigned long long s_wb[kWaves];
   __shared__ uint32_t s_now[kNowWords];
@@ -640,7 +679,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
     for (uint32_t b = 0; b < 4u; ++b) w |= (uint32_t)(uint8_t)a.now[4u * threadIdx.x + b] << (8u * b);
     s_now[threadIdx.x] = w;
   }
-  const Tables T = stage_tables<kLds, !kChunk>(a, s_pieces, s_lits);
+  const Tables T = stage_tables<kLds, !kChunk>(a, s_pieces, s_lits, s_sksz);
   __syncthreads();  // s_skels, s_now
   const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
   if constexpr (kChunk) {  // render every skeleton into its template (Now filled in) and its segment list
@@ -748,7 +787,7 @@ __global__ __launch_bounds__(kBlock) void emit_write_kernel(EmitArgs a) {
         if (ok) {
           const int k = skel_index(a, w, tid);
           const kwk_emit_skel& S = skels[k];
-          pos += (unsigned long long)skel_bytes(a, T, S, x.slot, V);
+          pos += (unsigned long long)skel_bytes(a, T, (uint32_t)k, x.slot, V);
           g = (g & S.keep) | S.set;
           if (n_sk < kRecSk) s_sk[lr * kRecSk + n_sk] = (int16_t)k;
           ++n_sk;
