@@ -19,7 +19,7 @@
 #   abshard=<so>               the same A/B at the N = 8 shard size (125k nodes / 12.5M pods)
 #   abemit=<so>                same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>
 #   emitprof                   the patch emitter alone: kernel trace + SQ / TA counter passes over its write kernel
-#   variants=<args>           tools/variants.py run <args> (cost-isolation builds)
+#   variants=<a,b,...>         tools/variants.py build + run of those variants (cost-isolation builds, built on the box)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; T=$1; shift; O=$R/gpurun_out/$T
 mkdir -p $O && cd $R
@@ -184,7 +184,9 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
       done
       cp $O/cur_emit.so $L && rm -f $O/cur_emit.so ;;
     variants)
-      timeout -k 10 600 python -u tools/variants.py run $arg > $O/variants.jsonl 2> $O/variants.err || { tail -30 $O/variants.err; exit 1; }
+      V=$(echo $arg | tr ',' ' ')
+      timeout -k 10 600 python -u tools/variants.py build ${V//--*/} > $O/variants_build.log 2>&1 || { tail -30 $O/variants_build.log; exit 1; }
+      timeout -k 10 900 python -u tools/variants.py run $V > $O/variants.jsonl 2> $O/variants.err || { tail -30 $O/variants.err; exit 1; }
       cut -c1-300 $O/variants.jsonl ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac

@@ -111,6 +111,15 @@ VARIANTS = {
     # ... the next tile's stream issued after phase 2 (its registers not live across process_object)
     "tpb4_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 4;"), _PF_EARLY, _PF_LATE],
     "tpb8_late": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 8;"), _PF_EARLY, _PF_LATE],
+    # the word sweep's per-stage fired counts are not kept (the fired records still are)
+    "w_nostat": [("  unsigned long long rest = bal;  // one LDS add per distinct fired stage\n  while (rest) {",
+                  "  unsigned long long rest = 0;  // one LDS add per distinct fired stage\n  while (rest) {")],
+    # a multi-match takes its first matched stage: no weight getters, no pick draw
+    "w_nopick": [("  if (cnt == 1) {\n    pick = __ffs(m) - 1;\n  } else {",
+                  "  if (cnt >= 1) {\n    pick = __ffs(m) - 1;\n  } else {")],
+    # Philox replaced by a 64-bit multiply hash (every draw: pick, jitter)
+    "w_nophilox": [("  philox10(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32));\n  return (uint64_t)c0 | ((uint64_t)c1 << 32);",
+                    "  (void)c2; (void)c3;\n  return (gslot * 0x9E3779B97F4A7C15ull) ^ (step * 0xBF58476D1CE4E5B9ull) ^ key ^ site;")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
@@ -139,7 +148,7 @@ def build(names):
         subprocess.run(cmd, check=True)
         return so
 
-    with ThreadPoolExecutor(4) as ex:
+    with ThreadPoolExecutor(8) as ex:
         for so in ex.map(one, names):
             print(so, flush=True)
 
