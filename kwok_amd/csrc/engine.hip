@@ -99,16 +99,16 @@ __device__ __forceinline__ uint64_t philox_u64(uint64_t gslot, uint64_t step, ui
 }
 
 // rand.Intn / rand.Int63n replacement: floor(u64 * n / 2^64), n > 0
-__device__ __forceinline__ int64_t rng_below(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key, int64_t n) {
-  return (int64_t)__umul64hi(philox_u64(gslot, step, site, key), (uint64_t)n);
-}
+__device__ __forceinline__ int64_t below_u64(uint64_t u, int64_t n) { return (int64_t)__umul64hi(u, (uint64_t)n); }
 
 // rand.Float64 replacement: (u64 >> 11) * 2^-53, in [0, 1)
 __device__ __forceinline__ double rng_float64(uint64_t gslot, uint64_t step, uint32_t site, uint64_t key) {
   return (double)(philox_u64(gslot, step, site, key) >> 11) * 0x1.0p-53;
 }
 
-constexpr uint32_t kSitePick = 1, kSiteJitter = 2, kSiteLeaseJitter = 3, kSiteRetryJitter = 4;
+// site 1's block carries both draws of a matched object: words 0-1 the pick, words 2-3 the Delay
+// jitter ("site 2"), so an object that needs both runs one Philox (r5: C2 phase 2 is VALU-bound)
+constexpr uint32_t kSitePick = 1, kSiteLeaseJitter = 3, kSiteRetryJitter = 4;
 
 __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
   int64_t r;
@@ -127,8 +127,10 @@ __device__ __forceinline__ int64_t abs_time_sub(int64_t sec, int32_t nsec, int64
   // move one second into dn so that ds' and dn' share a sign: overflow of ds'*1e9 then implies
   // overflow of the total
   if (ds > 0) { ds -= 1; dn += 1000000000; } else { ds += 1; dn -= 1000000000; }
-  int64_t p, d;
-  if (__builtin_mul_overflow(ds, (int64_t)1000000000, &p)) return ds > 0 ? INT64_MAX : INT64_MIN;
+  // ds * 1e9 overflows int64 iff |ds| > 9223372036 (a range test, not a 64 x 64 overflow multiply)
+  if (ds > 9223372036ll || ds < -9223372036ll) return ds > 0 ? INT64_MAX : INT64_MIN;
+  const int64_t p = ds * 1000000000ll;
+  int64_t d;
   if (__builtin_add_overflow(p, dn, &d)) return dn > 0 ? INT64_MAX : INT64_MIN;
   return d;
 }
@@ -373,6 +375,15 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
   const uint64_t gslot = a.slot_base + i;
   int pick;
   const int cnt = __popc(m);
+  // the object's draws: one Philox block when it may need the pick or a jitter (T->reserved[0]:
+  // the stages with a Delay jitter, kwk_load_stages)
+  uint64_t u_pick = 0, u_jit = 0;
+  if (!kProbe && (cnt > 1 || (m & T->reserved[0]))) {
+    uint32_t c0 = (uint32_t)gslot, c1 = (uint32_t)a.step, c2 = (uint32_t)(a.step >> 32), c3 = kSitePick;
+    philox10(c0, c1, c2, c3, (uint32_t)a.key, (uint32_t)(a.key >> 32));
+    u_pick = (uint64_t)c0 | ((uint64_t)c1 << 32);
+    u_jit = (uint64_t)c2 | ((uint64_t)c3 << 32);
+  }
   if (cnt == 1) {
     pick = __ffs(m) - 1;
   } else {
@@ -389,9 +400,9 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
       }
     }
     if (nerr == cnt || (total == 0 && nerr == 0)) {
-      pick = nth_bit(m, rng_below(gslot, a.step, kSitePick, a.key, cnt));          // lifecycle.go:157,163
+      pick = nth_bit(m, below_u64(u_pick, cnt));                                    // lifecycle.go:157,163
     } else if (total == 0) {
-      int64_t want = rng_below(gslot, a.step, kSitePick, a.key, nge0);            // lifecycle.go:175
+      int64_t want = below_u64(u_pick, nge0);                                     // lifecycle.go:175
       pick = -1;
       for (uint32_t mm = m; mm; mm &= mm - 1) {
         const int s = __ffs(mm) - 1;
@@ -405,7 +416,7 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
       sched |= KWK_F_MATCHERR;  // rand.Int63n panics on n <= 0 in the reference
       return false;
     } else {
-      int64_t off = rng_below(gslot, a.step, kSitePick, a.key, total);            // lifecycle.go:180
+      int64_t off = below_u64(u_pick, total);                                     // lifecycle.go:180
       pick = 31 - __clz(m);  // fallback: last matched stage (lifecycle.go:190)
       for (uint32_t mm = m; mm; mm &= mm - 1) {
         const int s = __ffs(mm) - 1;
@@ -442,7 +453,7 @@ __device__ __forceinline__ bool match_object(const SweepArgs& a, const kwk_stage
               if (jit > 0) { gen = 1; return false; }
             }
             if (jit > 0)
-              delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));
+              delay = (int64_t)((uint64_t)delay + (uint64_t)below_u64(u_jit, jit));
           }
         }
       }
@@ -4622,7 +4633,13 @@ kwk_status kwk_load_stages(kwk_engine* e, const kwk_stage_table* t, const kwk_de
     }
     e->fmt = nf;
   }
-  HIP_TRY(upload(e, e->d_table, t, sizeof(kwk_stage_table)));
+  {  // the device copy carries the stages with a Delay jitter in reserved[0] (match_object's draw test)
+    kwk_stage_table dt = *t;
+    dt.reserved[0] = 0;
+    for (uint32_t s = 0; s < t->n_stages; ++s)
+      if (t->stages[s].has_delay && t->stages[s].has_jitter) dt.reserved[0] |= 1u << s;
+    HIP_TRY(upload(e, e->d_table, &dt, sizeof(kwk_stage_table)));
+  }
   // the match set of every pred value, when pred_bits is small (Lifecycle.match, lifecycle.go:51-63)
   // match-mask tables (match_mask): one exact table up to 8 pred bits, else one per pred byte
   // for the stages whose clauses each lie within one byte
@@ -5219,7 +5236,8 @@ kwk_status kwk_sync(kwk_engine* e) {
 // d_compact, total at d_wave_offsets[n_waves] (enqueue only)
 // mode: 0 kwk_fired_rec, 1 packed 4-byte records, 2 the 2-byte records where the sweep wrote them
 // (else the 4-byte packed ones)
-static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
+static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t stream = nullptr) {
+  if (!stream) stream = e->stream;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (mode == 2 && e->last_rec != kRecId8Half) mode = 1;
   const bool packed = mode == 1;
@@ -5227,7 +5245,7 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
   e->compacted_packed = packed;
   e->compacted_16 = mode == 2;
   if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
-    HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), stream));
     return KWK_OK;
   }
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
@@ -5244,7 +5262,7 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
   const int rk = e->last_rec;
   void* args[] = {&a};
   if (mode == 2 && n_waves <= e->compact_small) {
-    hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, e->stream, a);
+    hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
@@ -5255,16 +5273,16 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
                            : (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half>
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8>
                                                 : (const void*)compact_small_kernel<kRecSlot>);
-    HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, e->stream));
+    HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, stream));
     return KWK_OK;
   }
-  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, e->stream,
+  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, stream,
                      e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
   constexpr uint32_t W = kCompactSpw;
   if (mode == 2) {
     constexpr uint32_t W16 = kCompact16Spw;
     hipLaunchKernelGGL(compact16_kernel<W16>, dim3((n_waves + W16 * kWavesPerBlock - 1) / (W16 * kWavesPerBlock)),
-                       dim3(kBlock), 0, e->stream, a);
+                       dim3(kBlock), 0, stream, a);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
@@ -5275,7 +5293,7 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0) {
                             : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, false, W>
                                               : (const void*)compact_kernel<kRecSlot, false, W>);
   const uint32_t eblocks = (n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock);
-  HIP_TRY(hipLaunchKernel(k, dim3(eblocks), dim3(kBlock), args, 0, e->stream));
+  HIP_TRY(hipLaunchKernel(k, dim3(eblocks), dim3(kBlock), args, 0, stream));
   HIP_TRY(hipGetLastError());
   return KWK_OK;
 }
@@ -5368,6 +5386,20 @@ kwk_status kwk_fired_packed16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32
   return KWK_OK;
 }
 
+// one step of kwk_step_n / _pair: the sweep (bracketed by events ev_a, ev_a + 1 when ev_a >= 0),
+// then the hand-back.  (The hand-back of step k on a side stream overlapping the sweep of step
+// k + 1, segments double-buffered, measured slower: 80.1-80.8 vs 78.4-78.7 us per C5 step, the
+// persistent sweep holding the CUs the two latency-bound launches then wait for; r5p / r5r)
+static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1) {
+  if (ev_a >= 0)
+    if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
+  if (kwk_status st = launch_sweep(e, now, seed, step, true)) return st;
+  if (ev_a >= 0)
+    if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
+  if (!compact) return KWK_OK;
+  return enqueue_compact(e, compact_mode(compact));
+}
+
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
   ErrScope es_(e);
@@ -5377,14 +5409,8 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t j = ev_j0 + k;
-    const bool ev = ev_every && j % ev_every == 0;
-    if (ev)
-      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every))) return st;
-    if (kwk_status st = launch_sweep(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, true)) return st;
-    if (ev)
-      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
-    if (compact)
-      if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+    const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
+    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev)) return st;
   }
   return KWK_OK;
 }
@@ -5402,19 +5428,11 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t j = ev_j0 + k;
-    const bool ev = ev_every && j % ev_every == 0;
+    const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
     const int64_t now = now0_ns + (int64_t)k * dt_ns;
-    if (ev)
-      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every))) return st;
-    if (kwk_status st = launch_sweep(e, now, seed, step0 + k, true)) return st;
-    if (ev)
-      if (kwk_status st = kwk_event_record(e, 2u * (j / ev_every) + 1u)) return st;
-    if (compact)
-      if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+    if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev)) return st;
     // the other engine's step right behind (its own stream): both chains start together
-    if (kwk_status st = launch_sweep(other, now, seed, step0 + k, true)) return st;
-    if (compact)
-      if (kwk_status st = enqueue_compact(other, compact_mode(compact))) return st;
+    if (kwk_status st = step_one(other, now, seed, step0 + k, compact)) return st;
   }
   return KWK_OK;
 }

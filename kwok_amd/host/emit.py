@@ -142,8 +142,13 @@ class EmitProgram:
                 sk["need"] = bits
                 sk["guard_list"] = gs
                 self.skel[(cls, tid)] = sk
-        for (cls, tid), sk in self.skel.items():  # every guard known: each patch's effect on each
-            sk["keep"], sk["set"] = self._effect(self.reps[cls], tid, sk, sk["guard_list"])
+        for key in list(self.skel):  # every guard known: each patch's effect on each
+            sk = self.skel[key]
+            try:
+                sk["keep"], sk["set"] = self._effect(self.reps[key[0]], key[1], sk, sk["guard_list"])
+            except ValueError:  # a Now / call-value slot outside a JSON string: no stand-in text parses
+                del self.skel[key]
+                self.reasons[key] = "a value slot outside a JSON string"
         # value columns: one per (template, call site)
         self.col_base: Dict[int, int] = {}
         n_cols = 0

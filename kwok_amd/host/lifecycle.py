@@ -35,8 +35,10 @@ _M = (1 << 32) - 1
 
 
 def philox_u64(key: int, slot: int, step: int, site: int) -> int:
-    """Philox4x32-10 (key = seed ^ kind_salt << 32, counter = (slot, step lo, step hi, site))."""
-    c0, c1, c2, c3 = slot & _M, step & _M, (step >> 32) & _M, site & _M
+    """Philox4x32-10 (key = seed ^ kind_salt << 32, counter = (slot, step lo, step hi, site)); the
+    pick (site 1) and the jitter (site 2) share the block of counter site 1: words 0-1 / 2-3."""
+    jit = site == SITE_JITTER
+    c0, c1, c2, c3 = slot & _M, step & _M, (step >> 32) & _M, (SITE_PICK if jit else site) & _M
     k0, k1 = key & _M, (key >> 32) & _M
     for _ in range(10):
         p0 = 0xD2511F53 * c0
@@ -44,7 +46,7 @@ def philox_u64(key: int, slot: int, step: int, site: int) -> int:
         c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & _M, p1 & _M, ((p0 >> 32) ^ c3 ^ k1) & _M, p0 & _M
         k0 = (k0 + 0x9E3779B9) & _M
         k1 = (k1 + 0xBB67AE85) & _M
-    return c0 | (c1 << 32)
+    return (c2 | (c3 << 32)) if jit else (c0 | (c1 << 32))
 
 
 def rng_below(key: int, slot: int, step: int, site: int, n: int) -> int:

@@ -57,10 +57,13 @@ struct Rng {
   uint64_t seed = 0;
   uint64_t slot = 0;
   uint64_t step = 0;
+  // sites 1 (pick) and 2 (jitter) share the block of counter site 1: words 0-1 / 2-3
+  // (DESIGN.md §RNG); sites 3, 4 take words 0-1 of their own block
   uint64_t u64(uint32_t site) const {
-    uint32_t c[4] = {(uint32_t)slot, (uint32_t)step, (uint32_t)(step >> 32), site};
+    const bool jit = site == SITE_JITTER;
+    uint32_t c[4] = {(uint32_t)slot, (uint32_t)step, (uint32_t)(step >> 32), jit ? (uint32_t)SITE_PICK : site};
     philox4x32_10(c, seed);
-    return (uint64_t)c[0] | ((uint64_t)c[1] << 32);
+    return jit ? (uint64_t)c[2] | ((uint64_t)c[3] << 32) : (uint64_t)c[0] | ((uint64_t)c[1] << 32);
   }
   // rand.Intn / rand.Int63n replacement: floor(u64 * n / 2^64), n > 0
   int64_t below(uint32_t site, int64_t n) const {

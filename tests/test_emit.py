@@ -63,6 +63,38 @@ def test_skeleton_fill_equals_native_render(config):
     assert ep.guards and ep.guards[0] == (("status", "containerStatuses"), ("spec", "containers"))
 
 
+def test_unquoted_value_slot_is_ineligible():
+    """a skeleton whose Now / call-value slot sits outside a JSON string (a template
+    rendering a number or bool there) cannot be analysed with stand-in text; EmitProgram marks
+    that (class, template) ineligible with a reason instead of raising."""
+    _, states = _workload_states("C2", 10, 100, seed=75)
+    stages, pp = _pod_program()
+    pods = [o for o in states if o.get("kind", "Pod") == "Pod"]
+    cls, reps = _classes(pods)
+    first = emit.EmitProgram(stages, pp, reps, len(reps))
+    (c0, t0), sk0 = sorted(first.skel.items())[0]
+
+    class Unquoted:  # the native program, with one skeleton's first slot moved out of its string
+        def __init__(self, inner):
+            self.inner = inner
+
+        def __getattr__(self, name):
+            return getattr(self.inner, name)
+
+        def skeleton(self, tid, rep):
+            sk = self.inner.skeleton(tid, rep)
+            if tid == t0 and sk["eligible"] and sk["slots"]:
+                sk = dict(sk, lits=['{"n": '] + ['0, "m": "'] * (len(sk["slots"]) - 1) + ['"}'] if len(sk["slots"]) > 1
+                          else ['{"n": ', '}'])
+            return sk
+
+    ep = emit.EmitProgram(stages, Unquoted(pp), reps, len(reps))
+    bad = [k for k in first.skel if k[1] == t0 and first.skel[k]["slots"]]
+    assert bad and all(k not in ep.skel for k in bad)
+    assert all(ep.reasons[k] == "a value slot outside a JSON string" for k in bad)
+    assert set(ep.skel) == set(first.skel) - set(bad)
+
+
 def test_emit_program_guard_effects():
     _, states = _workload_states("C2", 10, 400, seed=74)
     stages, pp = _pod_program()

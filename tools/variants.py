@@ -3,8 +3,9 @@ bench.py).  Each variant is engine.hip with a few source replacements — most o
 WRONG results on purpose (a phase skipped, a draw replaced) and exist only to time what the
 removed work costs on the C2-mix HBM working set.
 
-    python tools/variants.py build [names...]      # -> tools/build/libkwok_engine_<name>.so
+    python tools/variants.py build [names...]      # -> tools/build/libkwok_engine_<name>.so ("a+b": b applied to a)
     python tools/variants.py run [names...]        # one child process per variant, JSON lines
+    python tools/variants.py snap                  # HEAD's engine.hip -> tools/ab/ (the "head" variant on the box)
 """
 from __future__ import annotations
 
@@ -120,6 +121,8 @@ VARIANTS = {
     # Philox replaced by a 64-bit multiply hash (every draw: pick, jitter)
     "w_nophilox": [("  philox10(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32));\n  return (uint64_t)c0 | ((uint64_t)c1 << 32);",
                     "  (void)c2; (void)c3;\n  return (gslot * 0x9E3779B97F4A7C15ull) ^ (step * 0xBF58476D1CE4E5B9ull) ^ key ^ site;")],
+    # fused: fired records stored per phase-2 pass (not staged in LDS)
+    "w_nolds": [("constexpr bool kDwLdsRecs = true;", "constexpr bool kDwLdsRecs = false;")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
@@ -132,13 +135,20 @@ def build(names):
 
     def one(name):
         s = src
-        if name == "head":  # the committed engine.hip: same-box A/B against the working tree ("base")
-            s = subprocess.run(["git", "show", "HEAD:kwok_amd/csrc/engine.hip"], cwd=ROOT, check=True,
-                               capture_output=True, text=True).stdout
-        for old, new in VARIANTS[name]:
-            if old not in s:
-                raise SystemExit(f"variant {name}: pattern not found: {old[:60]!r}")
-            s = s.replace(old, new)
+        parts = name.split("+")  # "a+b": variant b's replacements applied to variant a's source
+        if parts[0] == "head":  # the committed engine.hip: same-box A/B against the working tree ("base");
+            # the GPU box has no .git: `variants.py snap` leaves HEAD's source in tools/ab/ first
+            snap = os.path.join(ROOT, "tools", "ab", "engine_head.hip")
+            if os.path.exists(snap):
+                s = open(snap).read()
+            else:
+                s = subprocess.run(["git", "show", "HEAD:kwok_amd/csrc/engine.hip"], cwd=ROOT, check=True,
+                                   capture_output=True, text=True).stdout
+        for part in parts:
+            for old, new in VARIANTS[part]:
+                if old not in s:
+                    raise SystemExit(f"variant {name}: pattern not found: {old[:60]!r}")
+                s = s.replace(old, new)
         path = os.path.join(OUT, f"engine_{name}.hip")
         open(path, "w").write(s)
         so = os.path.join(OUT, f"libkwok_engine_{name}.so")
@@ -177,7 +187,7 @@ def child_c5(name, steps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=("build", "run", "child"))
+    ap.add_argument("cmd", choices=("build", "run", "child", "snap"))
     ap.add_argument("names", nargs="*")
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
@@ -185,7 +195,12 @@ def main():
     ap.add_argument("--state", default="auto", help="C2 pod state format (auto: fused records, u32: split due)")
     a = ap.parse_args()
     names = a.names or list(VARIANTS)
-    if a.cmd == "build":
+    if a.cmd == "snap":
+        os.makedirs(os.path.join(ROOT, "tools", "ab"), exist_ok=True)
+        src = subprocess.run(["git", "show", "HEAD:kwok_amd/csrc/engine.hip"], cwd=ROOT, check=True,
+                             capture_output=True, text=True).stdout
+        open(os.path.join(ROOT, "tools", "ab", "engine_head.hip"), "w").write(src)
+    elif a.cmd == "build":
         build(names)
     elif a.cmd == "child":
         if a.c5:
