@@ -75,6 +75,12 @@ kwk_status fail(kwk_status code, const std::string& msg) {
 // ------------------------------------------------------------------ Philox4x32-10
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
                                          uint32_t k1) {
+  // the round keys are wave-uniform (a kernel argument): the empty asm re-defines the key here so
+  // that the round keys are scalar adds at the call instead of 20 values hoisted out of the word
+  // sweep's loops into SGPRs it does not have (spilled to VGPR lanes, reloaded lane by lane; r5)
+  k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+  k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // one 32 x 32 -> 64-bit multiply per product (v_mad_u64_u32) instead of separate lo / hi
@@ -1763,8 +1769,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
 //           (tile, wave) segment;
 //  phase 3  aligned 8-lane groups (one 128-byte line) holding a changed word are stored whole.
 constexpr int kQW = 4;                 // 16-byte chunks per lane: 16 (4-byte) / 8 (8-byte) words per lane
-constexpr int kDwMinBlocks = 6;        // fused word sweep: resident workgroups per CU the VGPR cap allows
-                                       // (80 VGPRs + 24 B of scratch; 467-470 vs 477-479 us at 5, r3w)
+constexpr int kDwMinBlocks = 5;        // fused word sweep: resident workgroups per CU the VGPR cap allows
+                                       // (96 VGPRs, no scratch: 470-482 vs 485-524 us at 6 on the same boxes,
+                                       // r5t / r5v; at 6 the round-5 kernel spills 28-48 B of VGPRs, r3w had
+                                       // 467-470 at 6 vs 477-479 at 5)
 constexpr int kQWD = 4;                // fused records: 8 per lane, 2048-object tiles (16 per lane: 129 VGPRs,
                                        // 3 waves per SIMD, 630 vs 541 us at C2, r3p)
 constexpr int kLdsDeltasW = 128;       // (class, stage) deltas staged in LDS by the word sweep
@@ -1789,9 +1797,9 @@ __device__ __forceinline__ void set_chunk_word(uint4& c, int j, uint2 w) {
 __device__ __forceinline__ uint32_t pred_word(uint32_t w) { return w; }  // word holding pred
 __device__ __forceinline__ uint32_t pred_word(uint2 w) { return w.x; }
 
-// fused records: a VGPR cap for 6 waves per SIMD (the next tile in flight pushed the kernel to
-// 108 VGPRs / 4 waves: 528 -> 481 us at 5 waves, r3v, -> 467-470 us at 6, r3w; the LDS tile
-// allows 6 workgroups per CU); the 4-byte words lose with a cap (522 -> 579 us at 5)
+// fused records: a VGPR cap (the next tile in flight pushed the kernel to 108 VGPRs / 4 waves:
+// 528 -> 481 us at 5 waves, r3v; round 5: 5 waves per SIMD, kDwMinBlocks); the 4-byte words
+// lose with a cap (522 -> 579 us at 5)
 template <bool kHarness, uint32_t kWB, bool kDW = false>
 __global__ __launch_bounds__(kBlock, kDW ? kDwMinBlocks : 1) void sweepw_kernel(SweepArgs a) {
   static_assert(!kDW || kWB == 8, "fused records are 8 bytes");
