@@ -581,13 +581,9 @@ def main():
     ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
     ap.add_argument("--tune-fsm-kernel", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
-    ap.add_argument("--tune-sweep-blocks", type=int, default=0,
-                    help="diagnostic: KWK_TUNE_SWEEP_BLOCKS for the pod engine (0: the occupancy)")
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
-    ap.add_argument("--tune-usage-rows", type=int, default=0,
-                    help="diagnostic: KWK_TUNE_USAGE_ROWS for the pod engine (0: the default, 4 rows per chunk)")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
@@ -659,9 +655,6 @@ def main():
     log(f"rank {rank}: nodes [{nlo}, {nhi}), pods [{nlo * args.pods_per_node}, {nhi * args.pods_per_node})")
     pods, nodes, (pvars, pidx) = build_engines(nlo, nhi, args.pods_per_node, local_rank, args.seed, args.job_frac,
                                                wide_state=args.wide_state)
-    if args.tune_usage_rows:
-        from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_USAGE_ROWS, args.tune_usage_rows)
     configure_usage(pods, pvars, pidx, nhi - nlo, args.pods_per_node)
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
@@ -669,9 +662,6 @@ def main():
     if args.tune_q16:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_Q16, args.tune_q16)
-    if args.tune_sweep_blocks:
-        from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_SWEEP_BLOCKS, args.tune_sweep_blocks)
     if args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)

@@ -215,12 +215,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    prefetched, or 0 = the general sweep16 kernel */
 #define KWK_TUNE_USAGE_KEY8 6  /* usage fast path: 1-byte usage-key column when at most 256 distinct keys occur,
                                    1 (default) or 0 (the 4-byte keys) */
-#define KWK_TUNE_SWEEP_BLOCKS 7 /* persistent 2-byte sweep: blocks per CU of its grid, 0 (default: the occupancy
-                                   the HIP runtime reports) or 1..8 (fewer than the occupancy: an experiment knob) */
-#define KWK_TUNE_USAGE_ROWS 12  /* usage kernels: wave rows (1024 pods) per chunk of whole nodes, 1..16 (default 4);
-                                   read by kwk_usage_config, so set it before that call */
-#define KWK_TUNE_USAGE_BLOCKS 4 /* usage kernels: resident blocks per CU of the persistent grid, 0 (default:
-                                   the occupancy the HIP runtime reports) or 1..8 */
+/* 4, 7, 12: retired experiment knobs (usage grid, sweep grid, usage chunk rows: tools/variants.py
+ * patches the constants for such measurements) */
 #define KWK_TUNE_COMPACT_SMALL 8 /* fired hand-back: the most segments compacted in one launch (each block sums
                                    the counts before its own), 0..8192 (default 8192); more use the scan +
                                    expansion pair; 0 = always the pair */

@@ -2524,7 +2524,7 @@ __global__ void dw_unfold_kernel(const uint2* __restrict__ st, int64_t* __restri
 // and keeps its integrators (Go keys them by name, so a re-created pod continues them).
 constexpr uint32_t kURun = 16;                  // consecutive pods per lane
 constexpr uint32_t kURow = 64u * kURun;         // slots per wave row
-constexpr uint32_t kUChunkRows = 4;            // rows per chunk (KWK_TUNE_USAGE_ROWS): the per-chunk costs
+constexpr uint32_t kUChunkRows = 4;            // rows per chunk: the per-chunk costs
                                                 // (descriptor, node boundaries, integrators, node stores) spread
                                                 // over up to 4 rows, whose loads run one row ahead
 constexpr uint32_t kUChunkPods = kURow - 8u;    // pods of a one-row chunk: it fits one row even after rounding its
@@ -4004,8 +4004,6 @@ struct kwk_engine {
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
   bool agg_fused = true;      // KWK_TUNE_AGG_FUSED: kwk_aggregate's mask counts inside the usage kernel
-  uint32_t usage_rows = kUChunkRows;  // KWK_TUNE_USAGE_ROWS: rows per usage chunk (set before kwk_usage_config)
-  uint32_t sweep_blocks = 0;  // persistent 2-byte sweep: resident blocks per CU (0: the occupancy)
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
   uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
@@ -4071,7 +4069,6 @@ struct kwk_engine {
   uint32_t* d_agg_masks = nullptr;
   double* d_podv = nullptr;       // usage_fast_kernel's pod values per (containers, value id)
   uint32_t podv_n = 0;
-  uint32_t usage_blocks = 0;      // KWK_TUNE_USAGE_BLOCKS (0: occupancy API)
   uint32_t compact_small = 8192;  // KWK_TUNE_COMPACT_SMALL (kSmallSegs)
   uint4* d_uchunk = nullptr;      // usage_kernel's chunks of whole nodes {first pod, end pod, first node, end node}
   uint32_t n_uchunks = 0;
@@ -4730,10 +4727,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
       e->fsm_kernel = value;
       return refresh_format(e);
-    case KWK_TUNE_SWEEP_BLOCKS:
-      if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_SWEEP_BLOCKS: 0..8");
-      e->sweep_blocks = value;
-      return KWK_OK;
     case KWK_TUNE_USAGE_KEY8:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
       e->usage_key8 = value != 0;
@@ -4754,14 +4747,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       e->stream = ns;
       return KWK_OK;
     }
-    case KWK_TUNE_USAGE_ROWS:
-      if (value < 1 || value > 16) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_ROWS: 1..16");
-      e->usage_rows = value;
-      return KWK_OK;
-    case KWK_TUNE_USAGE_BLOCKS:
-      if (value > 8) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_BLOCKS: 0..8");
-      e->usage_blocks = value;
-      return KWK_OK;
     case KWK_TUNE_WORD_TILES:
       if (value > 16) return fail(KWK_EINVAL, "KWK_TUNE_WORD_TILES: 0 (per format) or 1..16");
       e->word_tpb = value;
@@ -5094,7 +5079,6 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
 #define K8(P, D) (s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
-    if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);
 
     uint32_t blocks = tiles;
     e->last_sweep = kwk_sweep_info{KWK_SWEEP_8, (uint32_t)kQ8, 0, 1, tiles, tiles, a.harness.enable ? 1u : 0u, 0};
@@ -5134,7 +5118,6 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
                                                 : (const void*)sweep16_fsm_kernel<HV, QV, true, 1>)             \
                           : (const void*)sweep16_kernel<HV, QV, true>;                                          \
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;                                            \
-    if (e->persist16 && e->sweep_blocks) pg = std::min(tiles, (uint32_t)e->n_cus * e->sweep_blocks);           \
     e->last_sweep = kwk_sweep_info{lean ? (uint32_t)KWK_SWEEP_16_FSM : (uint32_t)KWK_SWEEP_16, QV, 0, 1, tiles,    \
                                    tiles, HV ? 1u : 0u, 0};                                                     \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
@@ -5556,11 +5539,11 @@ kwk_status kwk_usage_config(kwk_engine* e, uint32_t n_nodes, const uint32_t* nod
   void* olds[] = {e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk};
   for (void* p : olds) if (p) hipFree(p);
-  // the usage kernels' chunks: whole nodes, at most usage_rows wave rows of pods (less the 8 of the
+  // the usage kernels' chunks: whole nodes, at most kUChunkRows wave rows of pods (less the 8 of the
   // rounded start) and kUChunkNodes nodes each; a node with more pods than that gets a chunk of its
   // own (the wave carries its sum from row to row)
   std::vector<uint4> chunks;
-  const uint32_t chunk_pods = e->usage_rows * kURow - 8u;
+  const uint32_t chunk_pods = kUChunkRows * kURow - 8u;
   for (uint32_t n = 0; n < n_nodes;) {
     const uint32_t c0 = node_ptr[n];
     uint32_t nb = n + 1;
@@ -6075,7 +6058,7 @@ static kwk_status enqueue_usage(kwk_engine* e, int64_t now_ns, uint32_t* n_block
     const void* fk = k8 ? USAGE_KERNEL(usage_fast_kernel, , true) : USAGE_KERNEL(usage_fast_kernel);
     // 8 workgroups per CU by default, twice what is resident: the last chunks start as the first
     // workgroups finish, so the tail is shorter (C5: 91-93 vs 97-99 us with the occupancy grid, r4 agg)
-    const uint32_t per_cu = e->usage_blocks ? e->usage_blocks : 8u;
+    const uint32_t per_cu = 8u;
     const uint32_t grid = std::min(ublocks, (uint32_t)e->n_cus * per_cu);
     if (grid) {
       void* args[] = {&ua};

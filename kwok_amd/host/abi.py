@@ -93,11 +93,10 @@ ENGINE_WIDE_STATE = 1
 ENGINE_STATE32 = 2
 ENGINE_STATE16 = 4   # never the 1-byte dictionary format
 ENGINE_SPLIT_DUE = 8  # never the fused 8-byte record {packed word, relative due}
-TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_USAGE_BLOCKS, TUNE_FSM_KERNEL, TUNE_USAGE_KEY8, TUNE_SWEEP_BLOCKS = 1, 2, 3, 4, 5, 6, 7
+TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_FSM_KERNEL, TUNE_USAGE_KEY8 = 1, 2, 3, 5, 6
 TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
-TUNE_USAGE_ROWS = 12
 TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15
 

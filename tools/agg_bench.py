@@ -57,15 +57,6 @@ def main():
         pods.close()
         nodes.close()
         return
-    from kwok_amd.host import abi
-    for b in (2, 3, 4, 5, 6, 8):  # resident blocks per CU of the usage kernel's persistent grid
-        pods.set_tuning(abi.TUNE_USAGE_BLOCKS, b)
-        res[f"usage_blocks{b}"] = timed(pods, usage, args.reps)
-    pods.set_tuning(abi.TUNE_USAGE_BLOCKS, 0)
-    for r in (1, 2, 8, 4):  # wave rows per usage chunk (KWK_TUNE_USAGE_ROWS; read by kwk_usage_config), default last
-        pods.set_tuning(abi.TUNE_USAGE_ROWS, r)
-        bench.configure_usage(pods, pvars, pidx, args.nodes, args.pods_per_node)
-        res[f"usage_rows{r}"] = timed(pods, usage, args.reps)
     res["count"] = timed(pods, lambda: pods.count(pm), args.reps)
     res["fired_compact"] = timed(pods, pods.fired_compact, args.reps)
     res["aggregate"] = timed(pods, lambda: pods.aggregate(pm, t[0], usage=True), args.reps)

@@ -100,8 +100,8 @@ VARIANTS = {
     # sweep8: 1 / 2 id passes per loop step instead of 4 (run with --c5)
     "id8b1": [("constexpr uint32_t kId8Batch = 4;", "constexpr uint32_t kId8Batch = 1;")],
     "id8b2": [("constexpr uint32_t kId8Batch = 4;", "constexpr uint32_t kId8Batch = 2;")],
-    # fused word sweep capped at 5 waves per SIMD instead of 6
-    "lb5": [("constexpr int kDwMinBlocks = 6;", "constexpr int kDwMinBlocks = 5;")],
+    # fused word sweep capped at 6 waves per SIMD instead of 5 (the round-4 default)
+    "lb6": [("constexpr int kDwMinBlocks = 5;", "constexpr int kDwMinBlocks = 6;")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
     # set-up once, the next tile's stream in flight)
     "tpb1": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 1;")],
