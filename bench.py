@@ -194,8 +194,12 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
             if reporter is not None and report_every and (k - k0) % report_every == 0:
                 last = reporter.collect(NOW0 + (k - 1) * dt)
         return last, 0
+    # every step's fired lists to pinned host memory, overlapped (kwk_fired_fetch_async): the copies of
+    # step k run on the engines' copy streams while step k + 1 sweeps; step k + 1's compaction waits
+    # for them on the device; the host buffers alternate between steps
     last = None
     n_fired_host = 0
+    packed = handback in ("packed", "packed16")
     for k in range(k0, k1):
         now = NOW0 + k * dt
         j = k - k0
@@ -205,22 +209,18 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
         pods.step(now, seed, k)
         if timed:
             pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
-        packed = handback in ("packed", "packed16")
         # the 1-byte sweep writes 2-byte records when the program has at most 4 stages
         p16 = handback == "packed16" and pods.last_sweep()["kernel"] == 5 and len(pods.p.stages) <= 4
         pods.fired_compact("16" if p16 else packed)
         nodes.step(now, seed, k)
         nodes.fired_compact(packed)
-        if pinned is not None:  # PCIe-inclusive: every fired record copied to pinned host memory
-            if p16:  # 2 bytes per transition + the records per 2048-slot segment
-                n_fired_host += len(pods.fired_packed16((pinned[0], pinned[2]))[0])
-            elif packed:
-                n_fired_host += len(pods.fired_packed(pinned[0]))
-            else:
-                n_fired_host += len(pods.fired(pinned[0]))
-            n_fired_host += len(nodes.fired_packed(pinned[1])) if packed else len(nodes.fired(pinned[1]))
+        b = 3 * (j % 2)
+        n_fired_host += pods.fetch_async(pinned[b], pinned[b + 2])["n_records"]
+        n_fired_host += nodes.fetch_async(pinned[b + 1])["n_records"]
         if reporter is not None and report_every and (j + 1) % report_every == 0:
             last = reporter.collect(now)
+    pods.fetch_wait()
+    nodes.fetch_wait()
     return last, n_fired_host
 
 
@@ -574,7 +574,7 @@ def main():
     ap.add_argument("--hbm-steps", type=int, default=10)
     ap.add_argument("--hbm-only", action="store_true", help="diagnostic: only the C2-mix HBM working-set run")
     ap.add_argument("--hbm-warmup", type=int, default=12)
-    ap.add_argument("--pcie-steps", type=int, default=5)
+    ap.add_argument("--pcie-steps", type=int, default=10)
     ap.add_argument("--emit-steps", type=int, default=5, help="device patch emission steps after the timed run (0: off)")
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
@@ -739,9 +739,13 @@ def main():
     pcie = None
     if args.pcie_steps > 0 and world == 1:
         from kwok_amd.host.engine import PinnedBuffer
-        pin = (PinnedBuffer(8 * pods.capacity), PinnedBuffer(8 * nodes.capacity),
-               PinnedBuffer(4 * (pods.capacity // 512 + 64)))
+        pin = tuple(PinnedBuffer(n) for _ in range(2)  # two sets: step k's copy runs while step k + 1 is enqueued
+                    for n in (8 * pods.capacity, 8 * nodes.capacity, 4 * (pods.capacity // 512 + 64)))
         k0 = args.warmup + args.steps
+        # one untimed step first: the copy streams, events and snapshot buffers are created at the
+        # engines' first fetch
+        run_steps(pods, nodes, args.seed, dt, k0, k0 + 1, pinned=pin, handback=args.handback)
+        k0 += 1
         s2p, s2n = pods.stats(), nodes.stats()
         t1 = time.perf_counter()
         _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin, handback=args.handback)
@@ -751,17 +755,18 @@ def main():
         assert n_host == nf, (n_host, nf)
         pcie = {"value": round(nf / wall, 1), "unit": "stage transitions/sec", "steps": args.pcie_steps,
                 "fired_records_to_host_per_step": nf / args.pcie_steps, "ms_per_step": round(wall / args.pcie_steps * 1e3, 4),
-                "note": "each step's fired lists copied into kwk_alloc_host buffers: " + {
-                    "packed16": "pods kwk_fired_packed16 (2 B per transition + 4 B per 2048-slot segment), nodes "
-                                "kwk_fired_packed (4 B)",
-                    "packed": "kwk_fired_packed, 4 B per transition",
-                    "rec": "kwk_fired, 8 B per transition"}[args.handback]}
+                "note": "each step's fired lists copied into kwk_alloc_host buffers by kwk_fired_fetch_async (the "
+                        "copy of step k overlaps the sweep of step k + 1): " + {
+                    "packed16": "pods' 2-byte records (2 B per transition + 4 B per 2048-slot segment), nodes' "
+                                "4-byte packed records",
+                    "packed": "4-byte packed records",
+                    "rec": "kwk_fired_rec, 8 B per transition"}[args.handback]}
         for p in pin:
             p.close()
     patch_emit = None
     if args.emit_steps > 0 and world == 1:
         log("device patch emission run")
-        patch_emit = measure_patch_emit(pods, pvars, pidx, args, dt, args.warmup + args.steps + max(0, args.pcie_steps))
+        patch_emit = measure_patch_emit(pods, pvars, pidx, args, dt, args.warmup + args.steps + (args.pcie_steps + 1 if pcie else 0))
     del pidx
     if reporter.comm is not None:
         reporter.comm.close()

@@ -338,6 +338,24 @@ kwk_status kwk_fired_packed16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint
                               uint32_t seg_cap, uint32_t* n_segs, uint32_t* region_slots);
 kwk_status kwk_fired_packed(kwk_engine* eng, uint32_t* out, uint32_t cap, uint32_t* n_out);
 kwk_status kwk_fired_packed_device(kwk_engine* eng, const uint32_t** recs, const uint32_t** count);
+/* Overlapped hand-back to the host (the playStage workers' input, pod_controller.go:257-290): the
+ * last step's compacted list (whatever kwk_fired_compact* / kwk_step_n left: 2-, 4- or 8-byte
+ * records) and, for the 2-byte records, the records per segment, copied by the engine's copy
+ * stream while the device goes on.  The call waits for the list's length only (the compaction of
+ * that step), enqueues the copies and returns: call it after enqueuing the NEXT step's sweep and
+ * the copy overlaps that sweep.  The engine's next compaction waits for the copy on the device
+ * (the list is rewritten in place); the host buffers hold the copy after kwk_fired_fetch_wait (or
+ * the engine's next fetch).  Buffers from kwk_alloc_host make the copies DMA; double-buffer them
+ * to read one step's records while the next step's copy runs.  seg_counts may be NULL. */
+typedef struct {
+  uint32_t n_records;      /* records in the list (the bytes copied: n_records * record_bytes) */
+  uint32_t record_bytes;   /* 2 (KWK_COMPACT_PACKED16), 4 (KWK_COMPACT_PACKED) or 8 (kwk_fired_rec) */
+  uint32_t n_segs;         /* 2-byte records: segments (seg_counts entries copied), else 0 */
+  uint32_t region_slots;   /* 2-byte records: slots per segment (KWK_FIRED16_SLOT), else 0 */
+} kwk_fetch_info;
+kwk_status kwk_fired_fetch_async(kwk_engine* eng, void* out, uint64_t cap_bytes, uint32_t* seg_counts, uint32_t seg_cap,
+                                 kwk_fetch_info* info);
+kwk_status kwk_fired_fetch_wait(kwk_engine* eng);
 /* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */
 kwk_status kwk_alloc_host(uint64_t bytes, void** out);
 kwk_status kwk_free_host(void* p);

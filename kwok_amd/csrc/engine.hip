@@ -3989,6 +3989,14 @@ struct kwk_engine {
   bool compacted = false;     // the last sweep's fired list is compacted on the device
   bool compacted_packed = false;  // ... as 4-byte packed records (kwk_fired_compact_packed)
   bool compacted_16 = false;      // ... as the 1-byte sweep's 2-byte records (kwk_fired_compact_packed16)
+  // kwk_fired_fetch_async: the copy stream, the list length's pinned word, a snapshot of the
+  // segment counts (the next sweep rewrites d_wave_counts while the copy reads the snapshot)
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_count = nullptr, ev_copied = nullptr;
+  uint32_t* h_count = nullptr;
+  uint32_t* d_counts_snap = nullptr;
+  bool copy_pending = false;   // the next compaction waits for ev_copied
+  bool copy_recorded = false;  // ev_copied was recorded (kwk_fired_fetch_wait)
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
@@ -4594,6 +4602,12 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (e->d_tick_ptr) hipFree(e->d_tick_ptr);
   if (e->ev_lease) hipEventDestroy(e->ev_lease);
   if (e->ev_podsync) hipEventDestroy(e->ev_podsync);
+  if (e->copy_stream) hipStreamSynchronize(e->copy_stream);
+  for (hipEvent_t ev : {e->ev_count, e->ev_copied})
+    if (ev) hipEventDestroy(ev);
+  if (e->h_count) hipHostFree(e->h_count);
+  if (e->d_counts_snap) hipFree(e->d_counts_snap);
+  if (e->copy_stream) hipStreamDestroy(e->copy_stream);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
@@ -5232,6 +5246,10 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (mode == 2 && e->last_rec != kRecId8Half) mode = 1;
   const bool packed = mode == 1;
+  if (e->copy_pending) {  // kwk_fired_fetch_async is still copying the list this rewrites
+    HIP_TRY(hipStreamWaitEvent(stream, e->ev_copied, 0));
+    e->copy_pending = false;
+  }
   e->compacted = true;
   e->compacted_packed = packed;
   e->compacted_16 = mode == 2;
@@ -5453,6 +5471,64 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
   HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_fetch_async(kwk_engine* e, void* out, uint64_t cap_bytes, uint32_t* seg_counts, uint32_t seg_cap,
+                                 kwk_fetch_info* info) {
+  ErrScope es_(e);
+  if (!e || !info) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  memset(info, 0, sizeof(*info));
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (n_waves == 0) return KWK_OK;
+  if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_fetch_async needs the step's list compacted (kwk_fired_compact*)");
+  if (!e->copy_stream) {
+    int prio = 0;
+    HIP_TRY(hipStreamGetPriority(e->stream, &prio));
+    HIP_TRY(hipStreamCreateWithPriority(&e->copy_stream, hipStreamNonBlocking, prio));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_count, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_copied, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&e->h_count, 64, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&e->d_counts_snap, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
+  }
+  const uint32_t rb = e->compacted_16 ? 2u : e->compacted_packed ? 4u : (uint32_t)sizeof(kwk_fired_rec);
+  const bool segs = e->compacted_16 && seg_counts;
+  if (segs && n_waves > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(n_waves));
+  // the length (and the segment counts) behind the compaction on the engine's stream; only the
+  // length is waited for here
+  HIP_TRY(hipMemcpyAsync(e->h_count, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  if (segs)
+    HIP_TRY(hipMemcpyAsync(e->d_counts_snap, e->d_wave_counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToDevice,
+                           e->stream));
+  HIP_TRY(hipEventRecord(e->ev_count, e->stream));
+  HIP_TRY(hipEventSynchronize(e->ev_count));
+  const uint32_t total = *e->h_count;
+  info->n_records = total;
+  info->record_bytes = rb;
+  if (e->compacted_16) {
+    info->n_segs = n_waves;
+    info->region_slots = 64u * e->last_objs << e->last_region_shift;
+  }
+  if (out && (uint64_t)total * rb > cap_bytes)
+    return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string((uint64_t)total * rb) + " bytes");
+  HIP_TRY(hipStreamWaitEvent(e->copy_stream, e->ev_count, 0));
+  if (out && total)
+    HIP_TRY(hipMemcpyAsync(out, e->d_compact, (size_t)total * rb, hipMemcpyDeviceToHost, e->copy_stream));
+  if (segs)
+    HIP_TRY(hipMemcpyAsync(seg_counts, e->d_counts_snap, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToHost,
+                           e->copy_stream));
+  HIP_TRY(hipEventRecord(e->ev_copied, e->copy_stream));
+  e->copy_pending = true;
+  e->copy_recorded = true;
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_fetch_wait(kwk_engine* e) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  if (e->copy_recorded) HIP_TRY(hipEventSynchronize(e->ev_copied));
   return KWK_OK;
 }
 

@@ -76,6 +76,12 @@ class StepStats(C.Structure):
                 ("line_bytes", C.c_uint64)]
 
 
+class FetchInfo(C.Structure):
+    """kwk_fetch_info (kwk_fired_fetch_async)."""
+    _fields_ = [("n_records", C.c_uint32), ("record_bytes", C.c_uint32), ("n_segs", C.c_uint32),
+                ("region_slots", C.c_uint32)]
+
+
 class SweepInfo(C.Structure):
     _fields_ = [(k, C.c_uint32) for k in ("kernel", "q", "persistent", "depth", "grid", "tiles", "harness", "reserved")]
 
@@ -172,7 +178,7 @@ EXPORTS = [
     "kwk_metrics_load", "kwk_metrics_inputs", "kwk_metrics_eval", "kwk_aggregate", "kwk_aggregate_read",
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
     "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
-    "kwk_fired_packed16",
+    "kwk_fired_packed16", "kwk_fired_fetch_async", "kwk_fired_fetch_wait",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
@@ -237,6 +243,8 @@ def lib():
     L.kwk_fired_packed16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32), C.c_void_p, C.c_uint32,
                                      _p(C.c_uint32), _p(C.c_uint32)]
     L.kwk_fired_packed_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
+    L.kwk_fired_fetch_async.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, _p(FetchInfo)]
+    L.kwk_fired_fetch_wait.argtypes = [C.c_void_p]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
     L.kwk_set_tuning.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]

@@ -281,6 +281,21 @@ class Engine:
             self._check(L.kwk_fired_packed(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_packed")
         return out
 
+    def fetch_async(self, out: "PinnedBuffer", counts: Optional["PinnedBuffer"] = None) -> dict:
+        """kwk_fired_fetch_async: the last step's compacted list (and, for 2-byte records, the records per
+        segment) copied into `out` / `counts` on the engine's copy stream; returns the list's shape
+        at once ({n_records, record_bytes, n_segs, region_slots}).  The buffers hold the copy after
+        fetch_wait() (or the next fetch)."""
+        info = abi.FetchInfo()
+        self._check(abi.lib().kwk_fired_fetch_async(self.h, out.p, out.nbytes, counts.p if counts is not None else None,
+                                                   counts.nbytes // 4 if counts is not None else 0, C.byref(info)),
+                    "kwk_fired_fetch_async")
+        return {k: getattr(info, k) for k, _ in abi.FetchInfo._fields_}
+
+    def fetch_wait(self):
+        """kwk_fired_fetch_wait: the last fetch's copies are in the host buffers."""
+        self._check(abi.lib().kwk_fired_fetch_wait(self.h), "kwk_fired_fetch_wait")
+
     def fired_packed16(self, pinned=None):
         """The last step's list as 2-byte records (kwk_fired_packed16) -> (records u16, records per
         segment u32, region_slots); abi.EngineError (KWK_ESTATE) when the sweep has no 2-byte records.

@@ -376,6 +376,56 @@ def test_step_n_equals_per_step_calls():
             e.close()
 
 
+def test_fetch_async_equals_sync_readback():
+    """kwk_fired_fetch_async (the overlapped host hand-back): each step's list copied on the copy
+    stream while the next step is enqueued and compacted (the compaction waits for the copy on the
+    device), buffers alternating, equals the synchronous kwk_fired_packed16 / kwk_fired_packed /
+    kwk_fired of a twin engine stepped alike — 2-byte records with their per-segment counts,
+    4-byte packed and 8-byte records."""
+    from kwok_amd.host import abi
+    from kwok_amd.host.engine import PinnedBuffer
+    now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
+    for mode in ("16", True, False):
+        (_, a), (_, b) = _pods("auto", n_nodes=20_000), _pods("auto", n_nodes=20_000)
+        bufs = [(PinnedBuffer(8 * a.capacity), PinnedBuffer(4 * (a.capacity // 512 + 64))) for _ in range(2)]
+        try:
+            for k in range(6):
+                for e in (a, b):
+                    e.step(now0 + k * dt, seed, k)
+                    e.fired_compact(mode)
+                out, cnt = bufs[k % 2]
+                info = b.fetch_async(out, cnt)
+                if mode == "16":
+                    recs, segc, rs = a.fired_packed16()
+                    b.fetch_wait()
+                    assert info["record_bytes"] == 2 and info["n_segs"] == len(segc) and info["region_slots"] == rs
+                    got = out.array(np.uint16, info["n_records"])
+                    assert np.array_equal(got, recs), k
+                    assert np.array_equal(cnt.array(np.uint32, info["n_segs"]), segc), k
+                elif mode:
+                    ref = a.fired_packed()
+                    b.fetch_wait()
+                    assert info["record_bytes"] == 4 and np.array_equal(out.array(np.uint32, info["n_records"]), ref), k
+                else:
+                    ref = a.fired()
+                    b.fetch_wait()
+                    got = out.array(abi.FIRED_DTYPE, info["n_records"])
+                    assert info["record_bytes"] == 8 and np.array_equal(got, ref), k
+                assert info["n_records"] > 0
+            # an un-waited fetch, then a step: the engine's own compaction orders after the copy
+            info = b.fetch_async(bufs[0][0], bufs[0][1])
+            for e in (a, b):
+                e.step(now0 + 6 * dt, seed, 6)
+                e.fired_compact(mode)
+            assert np.array_equal(_fired_key(a.fired()), _fired_key(b.fired()))
+        finally:
+            for e in (a, b):
+                e.close()
+            for x in bufs:
+                for p in x:
+                    p.close()
+
+
 def test_fused_records_load_read_step_at_4m_pods():
     """The fused records' due times at scale: 4M C2 pods loaded with a queued stage on every third
     pod, its due time inside the 68.7 s window of the first step's epoch, years before it, or
