@@ -189,3 +189,66 @@ def test_gpu_disregarded_nodes_never_fire():
     total, per = run(W.stage_paths(W.NODE_FAST + W.NODE_HEARTBEAT), objs, steps=20, dt_ns=2 * 10**9, kind_salt=1,
                      compiler="native", disregard=DisregardSpec(label_selector="pool=frozen"))
     assert per["node-initialize"] == 40 and per["node-heartbeat"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_queued_pod_relabelled_disregarded_and_back():
+    """pods with a queued stage whose labels change to match the disregard selector (a
+    Modified event need() skips, pod_controller.go:397-407) still fire the queued stage and are
+    not re-matched while disregarded; when the label is removed again, re-matching resumes.  The
+    host re-encodes the changed objects and upserts them with the device's queued stage and due
+    time kept (the informer's event); the oracle gets the same label edits.  Fired sets and
+    states against the oracle every step."""
+    from kwok_amd.host.engine import Ingest
+    from tests.parity_util import NOW0, build, compare_state
+    cl, objs = _disregard_cluster(83)
+    d = DisregardSpec(annotation_selector="fake=custom", label_selector="tier in (batch)")
+    prog, eng, sim = build(cl.pod_stage_files, objs, harness=True, disregard=d)
+    try:
+        _, _, rec0, _ = Ingest(prog).columns(objs)  # the record index each slot was loaded with
+        ing = Ingest(prog)
+        moved, fired_moved = [], {"off": set(), "on": set()}
+
+        def relabel(on):
+            for i in moved:
+                for o in (sim.objs[i], sim.orig[i]):  # the re-created object keeps its labels too
+                    if o is None:
+                        continue
+                    labels = o.setdefault("metadata", {}).setdefault("labels", {})
+                    if on:
+                        labels["tier"] = "batch"
+                    else:
+                        labels.pop("tier", None)
+                if sim.objs[i] is not None:
+                    sim.dirty[i] = True
+            hot, dels = eng.read()
+            cur = [sim.objs[i] if sim.objs[i] is not None else sim.orig[i] for i in moved]
+            nh, _, _, nc = ing.columns(cur)
+            rows = hot[moved].copy()
+            rows["pred"] = nh["pred"]
+            alive = (rows["sched"] & np.uint32(abi.F_ALIVE)) != 0
+            rows["sched"] = np.where(alive, rows["sched"] | np.uint32(abi.F_DIRTY), rows["sched"])
+            eng.replace(np.asarray(moved), rows, dels[moved], rec0[moved], nc)
+
+        for k in range(40):
+            now = NOW0 + k * 500 * 10**6
+            if k == 8:  # needed pods with a queued stage not yet due
+                moved = [i for i in range(len(objs)) if i % 5 in (0, 3, 4) and sim.objs[i] is not None
+                         and sim.pending[i] is not None and sim.due[i] > now][:24]
+                assert len(moved) >= 8
+                relabel(True)
+            if k == 24:
+                relabel(False)
+            eng.step(now, 0x83, k)
+            got = sorted((int(r["slot"]), int(r["stage"]), int(r["flags"])) for r in eng.fired())
+            assert got == sorted(sim.step(now, 0x83, k)), f"step {k}"
+            compare_state(prog, eng, sim, k)
+            mv = {g[0] for g in got} & set(moved)
+            if 8 <= k < 24:
+                fired_moved["off"] |= mv
+            elif k >= 24:
+                fired_moved["on"] |= mv
+        assert fired_moved["off"], "queued stages of relabelled pods fire"
+        assert fired_moved["on"], "re-matching resumes once the label is gone"
+    finally:
+        eng.close()
