@@ -42,7 +42,7 @@ VARIANTS = {
     # phase 2 of the word sweep does nothing (no state change, no fires)
     "w_nophase2": [(_P2, "const uint2 nv = s; (void)due; (void)i;")],
     # jitter without its Philox draw
-    "nojitter": [("delay = (int64_t)((uint64_t)delay + (uint64_t)rng_below(gslot, a.step, kSiteJitter, a.key, jit));",
+    "nojitter": [("delay = (int64_t)((uint64_t)delay + (uint64_t)below_u64(u_jit, jit));",
                   "delay = (int64_t)((uint64_t)delay + (uint64_t)(jit >> 1));")],
     # the word sweep's fired records / per-stage counts are not written
     "w_noemit": [("      emit_fired<true>(f, off, lane, seg, seg_n, s_stat, n_bytes);\n", "      (void)f;\n")],
@@ -118,9 +118,9 @@ VARIANTS = {
     # a multi-match takes its first matched stage: no weight getters, no pick draw
     "w_nopick": [("  if (cnt == 1) {\n    pick = __ffs(m) - 1;\n  } else {",
                   "  if (cnt >= 1) {\n    pick = __ffs(m) - 1;\n  } else {")],
-    # Philox replaced by a 64-bit multiply hash (every draw: pick, jitter)
-    "w_nophilox": [("  philox10(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32));\n  return (uint64_t)c0 | ((uint64_t)c1 << 32);",
-                    "  (void)c2; (void)c3;\n  return (gslot * 0x9E3779B97F4A7C15ull) ^ (step * 0xBF58476D1CE4E5B9ull) ^ key ^ site;")],
+    # the matcher's Philox block replaced by a few multiplies (the pick and jitter draws)
+    "w_nophilox": [("    philox10(c0, c1, c2, c3, (uint32_t)a.key, (uint32_t)(a.key >> 32));",
+                    "    c0 ^= c1 * 0x9E3779B9u; c1 ^= c0 * 0x85EBCA6Bu; c2 ^= c1 * 0xC2B2AE35u; c3 ^= c2 * 0x27D4EB2Fu;")],
     # fused: fired records stored per phase-2 pass (not staged in LDS)
     "w_nolds": [("constexpr bool kDwLdsRecs = true;", "constexpr bool kDwLdsRecs = false;")],
     # the word sweep's phase 3 stores no state lines
