@@ -123,6 +123,19 @@ VARIANTS = {
                     "    c0 ^= c1 * 0x9E3779B9u; c1 ^= c0 * 0x85EBCA6Bu; c2 ^= c1 * 0xC2B2AE35u; c3 ^= c2 * 0x27D4EB2Fu;")],
     # fused: fired records stored per phase-2 pass (not staged in LDS)
     "w_nolds": [("constexpr bool kDwLdsRecs = true;", "constexpr bool kDwLdsRecs = false;")],
+    # fused word sweep: each wave touches the 32 lines of its region of the tile after next (one dword
+    # load per line, into L2), so the next tile's prefetch issued before phase 2 — which phase 2's
+    # loads wait behind in the in-order vmcnt queue — hits L2
+    "w_touch": [("  const uint32_t tbase = tile * kTile;\n",
+                 "  const uint32_t tbase = tile * kTile;\n"
+                 "  if (kDW && tile + 2u * gridDim.x < n_tiles)\n"
+                 "    touch_sink ^= __builtin_amdgcn_raw_buffer_load_b32(st_rs, lane < 32u ? ((tile + 2u * gridDim.x) * kTile + "
+                 "wave * kWave) * kWB + lane * 128u : kOOB, 0, 0);\n"),
+                ("  load_tile(tile);  // the first tile's stream is issued before the LDS set-up so its latency overlaps it\n",
+                 "  load_tile(tile);  // the first tile's stream is issued before the LDS set-up so its latency overlaps it\n"
+                 "  uint32_t touch_sink = 0;\n"),
+                ("  for (int o = 32; o > 0; o >>= 1) {\n    n_matched += __shfl_xor(n_matched, o);\n    n_bytes += __shfl_xor(n_bytes, o);\n    n_line += __shfl_xor(n_line, o);\n  }\n  if (lane == 0) {\n    atomicAdd(&s_stat[0], n_matched);",
+                 "  for (int o = 32; o > 0; o >>= 1) {\n    n_matched += __shfl_xor(n_matched, o);\n    n_bytes += __shfl_xor(n_bytes, o);\n    n_line += __shfl_xor(n_line, o);\n  }\n  if (touch_sink == 0x9E3779B9u && a.n == 1u) n_line += 1u;\n  if (lane == 0) {\n    atomicAdd(&s_stat[0], n_matched);")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
