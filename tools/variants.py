@@ -187,14 +187,15 @@ def child(name, hbm_nodes, steps, state="auto"):
     print(json.dumps({"variant": name, "state": state, **r}), flush=True)
 
 
-def child_c5(name, steps):
-    """The C5 bench line (pod sweep timing) with the variant library."""
+def child_c5(name, steps, nodes=0):
+    """The C5 bench line (pod sweep timing) with the variant library (nodes > 0: that many nodes, e.g.
+    the N = 8 shard's 125000)."""
     sys.path.insert(0, ROOT)
     from kwok_amd.host import abi
     abi.LIB_PATH = os.path.join(OUT, f"libkwok_engine_{name}.so")
     import bench
     sys.argv = ["bench.py", "--steps", str(steps), "--warmup", "5", "--no-pmc", "--no-cpu-baseline", "--hbm-nodes", "0",
-                "--pcie-steps", "0"]
+                "--pcie-steps", "0", "--emit-steps", "0"] + (["--nodes", str(nodes)] if nodes else [])
     bench.main()
 
 
@@ -205,6 +206,7 @@ def main():
     ap.add_argument("--hbm-nodes", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--c5", action="store_true", help="time the C5 pod sweep instead of the C2 working set")
+    ap.add_argument("--c5-nodes", type=int, default=0, help="with --c5: the bench's --nodes (0: the default 1M)")
     ap.add_argument("--state", default="auto", help="C2 pod state format (auto: fused records, u32: split due)")
     a = ap.parse_args()
     names = a.names or list(VARIANTS)
@@ -217,13 +219,14 @@ def main():
         build(names)
     elif a.cmd == "child":
         if a.c5:
-            child_c5(names[0], a.steps)
+            child_c5(names[0], a.steps, a.c5_nodes)
         else:
             child(names[0], a.hbm_nodes, a.steps, a.state)
     else:
         for n in names:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "child", n, "--hbm-nodes", str(a.hbm_nodes),
-                                "--steps", str(a.steps), "--state", a.state] + (["--c5"] if a.c5 else []), timeout=300)
+                                "--steps", str(a.steps), "--state", a.state, "--c5-nodes", str(a.c5_nodes)] +
+                               (["--c5"] if a.c5 else []), timeout=300)
             if r.returncode != 0:
                 raise SystemExit(f"variant {n}: rc {r.returncode}")
 
