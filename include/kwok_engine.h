@@ -230,6 +230,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */
+#define KWK_TUNE_FOLD_HB 16    /* kwk_step_n / _pair with KWK_COMPACT_PACKED16 on small 1-byte engines: a step's
+                                  2-byte hand-back copied by the next step's sweep (kwk_fired_fold16), 1
+                                  (default) or 0 (the hand-back launched after every step) */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
 
 /* stage table + per-(class, stage) deltas; replaces the previous table (version bump) */
@@ -356,6 +359,15 @@ typedef struct {
 kwk_status kwk_fired_fetch_async(kwk_engine* eng, void* out, uint64_t cap_bytes, uint32_t* seg_counts, uint32_t seg_cap,
                                  kwk_fetch_info* info);
 kwk_status kwk_fired_fetch_wait(kwk_engine* eng);
+
+/* The folded hand-back (no reference counterpart: an observation point for tests).  Inside one
+ * kwk_step_n / kwk_step_n_pair call with KWK_COMPACT_PACKED16, an engine whose 1-byte sweep runs
+ * one tile per workgroup (small engines: the strong-scaling shards) does not launch the hand-back
+ * for steps before the call's last: the next step's sweep copies the step's 2-byte list (the
+ * kwk_fired_compact_packed16 list, same order) while it rewrites the segments.  The call's last
+ * step is compacted as before.  This returns the list of the step before the last (n_out: its
+ * records; out may be NULL to ask for the count), KWK_ESTATE when the last call did not fold. */
+kwk_status kwk_fired_fold16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint32_t* n_out);
 /* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */
 kwk_status kwk_alloc_host(uint64_t bytes, void** out);
 kwk_status kwk_free_host(void* p);

@@ -309,6 +309,16 @@ struct SweepArgs {
   uint32_t fsm_bits;
   int64_t dw_epoch_old;          // fused format: the epoch the records hold (fmt.epoch: the one written)
   uint32_t dw_rebase;            // fused format: the epoch moves this sweep (every pending record re-encoded)
+  // folded hand-back (one-tile-per-workgroup sweep8 with 2-byte records: the N = 8 shard's size):
+  // the sweep copies the PREVIOUS step's records of each (tile, wave) segment into fold_out before
+  // this step's replace them; fold_counts = that step's segment counts (this step writes
+  // wave_counts, the other buffer); fold_n <- the list's length
+  uint16_t* __restrict__ fold_out;
+  const uint32_t* __restrict__ fold_counts;
+  uint32_t* __restrict__ fold_n;
+  uint32_t fold_prev;
+  uint32_t* __restrict__ btot_out;          // one-tile sweep8 with 2-byte records: records per workgroup
+  const uint32_t* __restrict__ fold_btot;   // ... the previous step's (the fold's prefix)
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -1474,6 +1484,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
                                   // they only ever write 0xFF back)
   __shared__ uint32_t s_fsm[512];
   __shared__ unsigned int s_stat[kStatWords];
+  __shared__ uint32_t s_fold[2 * kWavesPerBlock];  // fold: per wave the records before the block / its count
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
@@ -1481,6 +1492,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
   const __amdgpu_buffer_rsrc_t cnt_rs = make_rsrc(a.wave_counts, n_tiles * kWavesPerBlock * 4u);
+  const __amdgpu_buffer_rsrc_t fold_rs = make_rsrc(a.fold_out, 0x7FFFFFF0u);
   uint4 va[kDepth][Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
     const uint32_t off = t < n_tiles ? t * kTile + wave * kWave + lane * 16u : kOOB - 2048u;
@@ -1505,6 +1517,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   }
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   if (wave == 0) s_inv[lane] = 0xFFFFFFFFu;
+  const bool fold = !kPersist && kStages4 && a.fold_prev && blockIdx.x < n_tiles;  // block-uniform
+  if (fold) {  // the previous step's records before this block: its per-workgroup totals (16-byte loads)
+    const uint32_t nb = blockIdx.x;
+    const uint4* __restrict__ b4 = reinterpret_cast<const uint4*>(a.fold_btot);
+    uint32_t sum = 0;
+#pragma unroll 2
+    for (uint32_t q = threadIdx.x; q < nb / 4u; q += kBlock) {
+      const uint4 v = b4[q];
+      sum += (v.x + v.y) + (v.z + v.w);
+    }
+    if (threadIdx.x < (nb & 3u)) sum += a.fold_btot[(nb & ~3u) + threadIdx.x];
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0) s_fold[wave] = sum;
+    if (threadIdx.x < kWavesPerBlock) s_fold[kWavesPerBlock + threadIdx.x] = a.fold_counts[nb * kWavesPerBlock + threadIdx.x];
+  }
   __syncthreads();
 
   // kStages4: stc[0] = this tile's fired records of stages 0-3 as byte counters (<= 32 items per lane
@@ -1532,6 +1559,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const uint32_t seg_id = tile * kWavesPerBlock + wave;
     uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + (uint64_t)seg_id * kSeg8;
     const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg8 * 4u);
+    // folded hand-back: this segment's records of the previous step, two per lane and dword,
+    // records 2 * lane + 128 * j (+1), loaded now and stored after this step's fixed store set;
+    // past 512 records (rare) copied here, before this step's records overwrite the segment
+    uint32_t f_o = 0, f_c = 0, f_v[4] = {0u, 0u, 0u, 0u};
+    if (fold) {
+      f_o = s_fold[0] + s_fold[1] + s_fold[2] + s_fold[3];
+      for (uint32_t w = 0; w < wave; ++w) f_o += s_fold[kWavesPerBlock + w];
+      f_c = s_fold[kWavesPerBlock + wave];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t r = 2u * lane + 128u * j;
+        f_v[j] = __builtin_amdgcn_raw_buffer_load_b32(seg_rs, r < f_c ? kRec16Header + r * 2u : kOOB, 0, 0);
+      }
+      if (f_c > 512u) {
+        const uint16_t* old = reinterpret_cast<const uint16_t*>(seg32 + kRec16Header / 4u);
+        for (uint32_t j = 512u + lane; j < f_c; j += 64u) a.fold_out[f_o + j] = old[j];
+      }
+      if (seg_id + 1u == n_tiles * kWavesPerBlock && lane == 0) *a.fold_n = f_o + f_c;
+    }
     uint4 cur_copy[Q];
     if (kDepth == 1) {
 #pragma unroll
@@ -1673,6 +1719,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       // records: seg_n 2-byte records from the work list, as 16-byte chunks of whole 128-byte
       // lines (the tail of the last line is padding)
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (fold)  // the previous records are in registers before this step's overwrite them
+        asm volatile("" ::"v"(f_v[0]), "v"(f_v[1]), "v"(f_v[2]), "v"(f_v[3]));
       const uint32_t n_chunks = ((seg_n * 2u + 127u) & ~127u) / 16u;
       const uint4* wq = reinterpret_cast<const uint4*>(wl);
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1685,6 +1733,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       }
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{seg_n, 0u, 0u, 0u}, seg_rs, lane == 0 && real ? 0u : kOOB, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(seg_n, cnt_rs, lane == 0 && real ? seg_id * 4u : kOOB, 0, 0);
+      if (fold) {  // the previous step's records (a fixed set of eight 2-byte stores)
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+          const uint32_t r = 2u * lane + 128u * j;
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f_v[j], fold_rs, r < f_c ? (f_o + r) * 2u : kOOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(f_v[j] >> 16), fold_rs, r + 1u < f_c ? (f_o + r + 1u) * 2u : kOOB,
+                                                0, 0);
+        }
+      }
       if (real) {
         w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
         w_bytes += 2u * seg_n + 4u;
@@ -1750,6 +1807,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const unsigned int val = s_stat[threadIdx.x];
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
   }
+  if (!kPersist && kStages4 && threadIdx.x == 0) a.btot_out[blockIdx.x] = s_stat[1];  // the next step's fold prefix
 }
 
 // ------------------------------------------------------------------ 4- and 8-byte state sweep
@@ -4045,6 +4103,20 @@ struct kwk_engine {
   kwk_delta* d_deltas = nullptr;
   kwk_fired_rec* d_fired = nullptr;
   kwk_fired_rec* d_compact = nullptr;
+  // folded hand-back (kwk_step_n / _pair with KWK_COMPACT_PACKED16 when the 1-byte sweep runs one
+  // tile per workgroup and the hand-back would be one launch: the strong-scaling shards): a step's
+  // 2-byte list is copied by the NEXT step's sweep into d_fold; the call's last step is compacted
+  // as usual.  fold_pending: the last sweep's list awaits the next sweep (its counts in
+  // d_wave_counts, swapped into d_counts_prev when that sweep starts)
+  bool fold_hb = true;  // KWK_TUNE_FOLD_HB
+  bool fold_now = false;
+  bool fold_pending = false;
+  bool fold_valid = false;     // d_fold holds the list of the step before the last (kwk_fired_fold16)
+  uint16_t* d_fold = nullptr;
+  uint32_t* d_fold_n = nullptr;
+  uint32_t* d_counts_prev = nullptr;
+  uint32_t* d_btot = nullptr;       // records per workgroup of the last one-tile sweep8 (2-byte records)
+  uint32_t* d_btot_prev = nullptr;  // ... of the one before (swapped with d_btot as the counts)
   uint32_t* d_wave_counts = nullptr;
   uint32_t* d_wave_offsets = nullptr;
   uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
@@ -4551,6 +4623,8 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
+  ALLOC(e->d_btot, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
+  ALLOC(e->d_btot_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
   ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
@@ -4590,7 +4664,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -4770,6 +4844,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
+      return KWK_OK;
+    case KWK_TUNE_FOLD_HB:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FOLD_HB: 0 or 1");
+      e->fold_hb = value != 0;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -5024,6 +5102,12 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
   a.fsm_bits = 0;
   a.dw_epoch_old = e->fmt.epoch;
   a.dw_rebase = 0;
+  a.fold_out = e->d_fold;
+  a.fold_counts = e->d_counts_prev;
+  a.fold_n = e->d_fold_n;
+  a.fold_prev = e->fold_now ? 1u : 0u;
+  a.btot_out = e->d_btot;
+  a.fold_btot = e->d_btot_prev;
   return a;
 }
 
@@ -5069,6 +5153,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   e->compacted = false;
   e->last_sweep = kwk_sweep_info{};
+  if (!e->fold_now) e->fold_valid = false;  // d_fold no longer holds the list before the last
   if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
@@ -5399,13 +5484,37 @@ kwk_status kwk_fired_packed16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32
 // then the hand-back.  (The hand-back of step k on a side stream overlapping the sweep of step
 // k + 1, segments double-buffered, measured slower: 80.1-80.8 vs 78.4-78.7 us per C5 step, the
 // persistent sweep holding the CUs the two latency-bound launches then wait for; r5p / r5r)
-static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1) {
+// fold: the call may fold its steps' hand-backs; last: the call's last step (always compacted)
+static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1,
+                           bool fold = false, bool last = true) {
+  if (e->fold_pending) {  // this sweep copies the previous step's list; it writes its counts to the other buffer
+    std::swap(e->d_wave_counts, e->d_counts_prev);
+    std::swap(e->d_btot, e->d_btot_prev);
+    e->fold_now = true;
+  }
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
-  if (kwk_status st = launch_sweep(e, now, seed, step, true)) return st;
+  const kwk_status sst = launch_sweep(e, now, seed, step, true);
+  const bool folded = e->fold_now && e->fmt.byte && e->last_sweep.persistent == 0 && e->last_rec == kRecId8Half;
+  e->fold_now = false;
+  e->fold_pending = false;
+  if (sst) return sst;
+  if (folded) e->fold_valid = true;
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
   if (!compact) return KWK_OK;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (fold && !last && e->fold_hb && compact == KWK_COMPACT_PACKED16 && e->fmt.byte && e->last_rec == kRecId8Half &&
+      e->last_sweep.persistent == 0 && n_waves > 0 && n_waves <= e->compact_small) {
+    if (!e->d_fold) {
+      HIP_TRY(hipMalloc((void**)&e->d_fold, sizeof(uint16_t) * (size_t)e->capacity + 64));
+      HIP_TRY(hipMalloc((void**)&e->d_fold_n, 64));
+      HIP_TRY(hipMalloc((void**)&e->d_counts_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 4)));
+    }
+    e->compacted = false;  // this step's list: copied by the next sweep
+    e->fold_pending = true;
+    return KWK_OK;
+  }
   return enqueue_compact(e, compact_mode(compact));
 }
 
@@ -5419,7 +5528,8 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t j = ev_j0 + k;
     const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
-    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev)) return st;
+    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev, true, k + 1 == n))
+      return st;
   }
   return KWK_OK;
 }
@@ -5439,9 +5549,9 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
     const uint32_t j = ev_j0 + k;
     const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
     const int64_t now = now0_ns + (int64_t)k * dt_ns;
-    if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev)) return st;
+    if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev, true, k + 1 == n)) return st;
     // the other engine's step right behind (its own stream): both chains start together
-    if (kwk_status st = step_one(other, now, seed, step0 + k, compact)) return st;
+    if (kwk_status st = step_one(other, now, seed, step0 + k, compact, -1, true, k + 1 == n)) return st;
   }
   return KWK_OK;
 }
@@ -5521,6 +5631,22 @@ kwk_status kwk_fired_fetch_async(kwk_engine* e, void* out, uint64_t cap_bytes, u
   HIP_TRY(hipEventRecord(e->ev_copied, e->copy_stream));
   e->copy_pending = true;
   e->copy_recorded = true;
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_fold16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  if (!e->fold_valid || !e->d_fold) return fail(KWK_ESTATE, "no folded list: the last kwk_step_n did not fold");
+  uint32_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, e->d_fold_n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
+  HIP_TRY(hipMemcpyAsync(out, e->d_fold, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 

@@ -105,6 +105,7 @@ TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15
+TUNE_FOLD_HB = 16
 
 
 class Lease(C.Structure):
@@ -179,6 +180,7 @@ EXPORTS = [
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
     "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
     "kwk_fired_packed16", "kwk_fired_fetch_async", "kwk_fired_fetch_wait",
+    "kwk_fired_fold16",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
@@ -245,6 +247,7 @@ def lib():
     L.kwk_fired_packed_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_fired_fetch_async.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, _p(FetchInfo)]
     L.kwk_fired_fetch_wait.argtypes = [C.c_void_p]
+    L.kwk_fired_fold16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
     L.kwk_set_tuning.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]

@@ -296,6 +296,17 @@ class Engine:
         """kwk_fired_fetch_wait: the last fetch's copies are in the host buffers."""
         self._check(abi.lib().kwk_fired_fetch_wait(self.h), "kwk_fired_fetch_wait")
 
+    def fired_fold16(self) -> np.ndarray:
+        """kwk_fired_fold16: the 2-byte list of the step before the last of the last kwk_step_n, as
+        the next step's sweep copied it (abi.EngineError KWK_ESTATE when that call did not fold)."""
+        n = C.c_uint32()
+        L = abi.lib()
+        self._check(L.kwk_fired_fold16(self.h, None, 0, C.byref(n)), "kwk_fired_fold16")
+        out = np.zeros(n.value, dtype=np.uint16)
+        if n.value:
+            self._check(L.kwk_fired_fold16(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_fold16")
+        return out
+
     def fired_packed16(self, pinned=None):
         """The last step's list as 2-byte records (kwk_fired_packed16) -> (records u16, records per
         segment u32, region_slots); abi.EngineError (KWK_ESTATE) when the sweep has no 2-byte records.

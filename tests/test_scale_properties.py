@@ -426,6 +426,42 @@ def test_fetch_async_equals_sync_readback():
                     p.close()
 
 
+def test_folded_handback_equals_compacted_list():
+    """kwk_step_n with KWK_COMPACT_PACKED16 on a small 1-byte engine (one tile per workgroup): the
+    steps before the call's last are not compacted, the next sweep copies their 2-byte lists
+    (kwk_fired_fold16).  That list equals kwk_fired_packed16 of a twin engine stepped one step per
+    call — step 0 (every pod fires: segments past 512 records, the copy's tail loop) and a later
+    step — and the call's last step is compacted as before; no fold after a one-step call or with
+    KWK_TUNE_FOLD_HB = 0."""
+    from kwok_amd.host import abi
+    now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
+    (_, a), (_, b), (_, c) = (_pods("auto", n_nodes=20_000), _pods("auto", n_nodes=20_000),
+                              _pods("auto", n_nodes=20_000, tuning={abi.TUNE_FOLD_HB: 0}))
+    try:
+        ref = []
+        for k in range(5):
+            a.step_n(1, now0 + k * dt, dt, seed, k, "packed16")
+            recs, segc, _ = a.fired_packed16()
+            ref.append(recs)
+            if k == 0:
+                assert segc.max() > 512, segc.max()
+        assert a.last_sweep()["persistent"] == 0
+        b.step_n(2, now0, dt, seed, 0, "packed16")
+        assert np.array_equal(b.fired_fold16(), ref[0])
+        assert np.array_equal(b.fired_packed16()[0], ref[1])
+        b.step_n(3, now0 + 2 * dt, dt, seed, 2, "packed16")
+        assert np.array_equal(b.fired_fold16(), ref[3])
+        assert np.array_equal(b.fired_packed16()[0], ref[4])
+        assert np.array_equal(b.read()[0]["pred"], a.read()[0]["pred"])
+        for e, n in ((b, 1), (c, 2)):
+            e.step_n(n, now0 + 5 * dt, dt, seed, 5, "packed16")
+            with pytest.raises(abi.EngineError, match="did not fold"):
+                e.fired_fold16()
+    finally:
+        for e in (a, b, c):
+            e.close()
+
+
 def test_fused_records_load_read_step_at_4m_pods():
     """The fused records' due times at scale: 4M C2 pods loaded with a queued stage on every third
     pod, its due time inside the 68.7 s window of the first step's epoch, years before it, or
