@@ -1643,19 +1643,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
       const bool slow = rdy || any_due;          // ... or due times may be written
       {
+        // entry = tile_lds | lds_id8(k, lane4) = ent0 ^ lds_id8(k, 0) (lane4 has no bits in
+        // lds_id8's k fields): three ops per item on the per-lane loop, whose trip count is the
+        // most items of any lane
         uint32_t m = need;
         uint16_t* wp = wl + pos;
+        const uint32_t ent0 = tile_lds | lane4;
         if (rdy) {
           while (m) {
             const uint32_t k = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            *wp++ = (uint16_t)((tile_lds | lds_id8(k, lane4)) | ((ready >> k) & 1u) << 15);
+            *wp++ = (uint16_t)((ent0 ^ ((k & 7u) * 0x104u | k >> 3)) | ((ready >> k) & 1u) << 15);
           }
         } else {
           while (m) {
             const uint32_t k = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            *wp++ = (uint16_t)(tile_lds | lds_id8(k, lane4));
+            *wp++ = (uint16_t)(ent0 ^ ((k & 7u) * 0x104u | k >> 3));
           }
         }
       }
@@ -1704,12 +1708,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     // in-order wait for the next prefetched tile counts exactly the stores issued after it
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      uint4 nv = cur[q];
-      if (n_work)
+      // without work the tile is unchanged: nothing stored (the data is then never written)
+      uint4 nv = make_uint4(0u, 0u, 0u, 0u);
+      unsigned long long chm = 0;
+      if (n_work) {
         nv = make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)], tw[lds_col8(q * 4 + 2, lane)],
                         tw[lds_col8(q * 4 + 3, lane)]);
-      const bool ch = (nv.x ^ cur[q].x) | (nv.y ^ cur[q].y) | (nv.z ^ cur[q].z) | (nv.w ^ cur[q].w);
-      const bool st = (ballot(ch) >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);
+        chm = ballot(nv.x != cur[q].x) | ballot(nv.y != cur[q].y) | ballot(nv.z != cur[q].z) | ballot(nv.w != cur[q].w);
+      }
+      const bool st = (chm >> (lane & ~(kStoreLanes - 1u))) & ((1ull << kStoreLanes) - 1ull);
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{nv.x, nv.y, nv.z, nv.w}, gq_rs,
                                              st ? wbase + (uint32_t)q * 1024u + lane * 16u : kOOB, 0, 2 /* nt */);
