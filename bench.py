@@ -166,9 +166,10 @@ EV_EVERY = 10  # HIP events bracket the pod sweep of every 10th step (2 launches
 
 
 # --handback: kwk_step_n's compaction (2-byte records where the sweep has them / 4-byte packed / kwk_fired_rec)
-HANDBACK = {"packed16": "packed16", "packed": "packed", "rec": True}
-HANDBACK_NAMES = {"packed16": "2-byte pod records + 4-byte packed node records", "packed": "packed 4-byte",
-                  "rec": "8-byte kwk_fired_rec"}
+HANDBACK = {"packed16": "packed16", "bits": "bits", "packed": "packed", "rec": True}
+HANDBACK_NAMES = {"packed16": "2-byte pod records + 4-byte packed node records",
+                  "bits": "per-segment pod fired maps + 2-bit stage codes + 4-byte packed node records",
+                  "packed": "packed 4-byte", "rec": "8-byte kwk_fired_rec"}
 
 
 def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report_every=0, pinned=None,
@@ -199,7 +200,7 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
     # for them on the device; the host buffers alternate between steps
     last = None
     n_fired_host = 0
-    packed = handback in ("packed", "packed16")
+    packed = handback in ("packed", "packed16", "bits")
     for k in range(k0, k1):
         now = NOW0 + k * dt
         j = k - k0
@@ -210,8 +211,8 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
         if timed:
             pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
         # the 1-byte sweep writes 2-byte records when the program has at most 4 stages
-        p16 = handback == "packed16" and pods.last_sweep()["kernel"] == 5 and len(pods.p.stages) <= 4
-        pods.fired_compact("16" if p16 else packed)
+        p16 = handback in ("packed16", "bits") and pods.last_sweep()["kernel"] == 5 and len(pods.p.stages) <= 4
+        pods.fired_compact(("16" if handback == "packed16" else "bits") if p16 else packed)
         nodes.step(now, seed, k)
         nodes.fired_compact(packed)
         b = 3 * (j % 2)
@@ -587,7 +588,9 @@ def main():
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
-    ap.add_argument("--handback", choices=("packed16", "packed", "rec"), default="packed16",
+    ap.add_argument("--pcie-handback", choices=("bits", "packed16", "packed", "rec"), default="bits",
+                    help="the PCIe-inclusive leg's hand-back format (default: the fewest bytes per transition)")
+    ap.add_argument("--handback", choices=("packed16", "bits", "packed", "rec"), default="packed16",
                     help="fired hand-back per step: 2-byte records where the sweep has them (kwk_fired_compact_packed16: "
                          "the 1-byte sweep's {offset, stage, flags} + records per segment; other engines 4-byte), "
                          "packed 4-byte records (kwk_fired_compact_packed, 27-bit slot | 5-bit stage) or 8-byte "
@@ -744,11 +747,12 @@ def main():
         k0 = args.warmup + args.steps
         # one untimed step first: the copy streams, events and snapshot buffers are created at the
         # engines' first fetch
-        run_steps(pods, nodes, args.seed, dt, k0, k0 + 1, pinned=pin, handback=args.handback)
+        run_steps(pods, nodes, args.seed, dt, k0, k0 + 1, pinned=pin, handback=args.pcie_handback)
         k0 += 1
         s2p, s2n = pods.stats(), nodes.stats()
         t1 = time.perf_counter()
-        _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin, handback=args.handback)
+        _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin,
+                              handback=args.pcie_handback)
         wall = time.perf_counter() - t1
         s3p, s3n = pods.stats(), nodes.stats()
         nf = (s3p["fired"] - s2p["fired"]) + (s3n["fired"] - s2n["fired"])
@@ -759,8 +763,10 @@ def main():
                         "copy of step k overlaps the sweep of step k + 1): " + {
                     "packed16": "pods' 2-byte records (2 B per transition + 4 B per 2048-slot segment), nodes' "
                                 "4-byte packed records",
+                    "bits": "pods' fired maps (256 B per 2048-slot segment) + 2-bit stage codes "
+                            "(kwk_fired_compact_bits, ~1.5 B per transition at 10 % firing), nodes' 4-byte packed records",
                     "packed": "4-byte packed records",
-                    "rec": "kwk_fired_rec, 8 B per transition"}[args.handback]}
+                    "rec": "kwk_fired_rec, 8 B per transition"}[args.pcie_handback]}
         for p in pin:
             p.close()
     patch_emit = None

@@ -339,6 +339,20 @@ kwk_status kwk_fired_compact_packed(kwk_engine* eng);
 kwk_status kwk_fired_compact_packed16(kwk_engine* eng);
 kwk_status kwk_fired_packed16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint32_t* n_out, uint32_t* seg_counts,
                               uint32_t seg_cap, uint32_t* n_segs, uint32_t* region_slots);
+/* The hand-back at ~1.5 bytes per transition (C5's 10 % firing), for the same engines as the 2-byte
+ * records: per segment s of n (slots [s * region_slots, (s + 1) * region_slots)) a 2048-bit map
+ * at words [64 s, 64 s + 64), bit i set when the object of KWK_BITS_SLOT(i) fired, then every
+ * segment's stage codes from word 64 n on, 2 bits each (code j at bits 2 (j % 16) of the segment's
+ * word j / 16), one per set bit in bit order, each segment's codes padded to a whole word:
+ * segment s's codes start after sum_{t<s} ceil(popcount(map t) / 16) words.  Same (slot, stage)
+ * sequence as kwk_fired; the flags are not carried (as KWK_COMPACT_PACKED).  n_words: the list's
+ * words, n_records: its transitions.  kwk_step_n(..., KWK_COMPACT_BITS, ...) enqueues it per step
+ * (an engine without 2-byte records then leaves the 4-byte packed list). */
+#define KWK_COMPACT_BITS 4u
+#define KWK_BITS_SLOT(i) KWK_FIRED16_SLOT(((((uint32_t)(i) & 7u) << 8) | ((((uint32_t)(i) >> 5) & 63u) << 2 ^ (((uint32_t)(i) & 7u) << 2)) | (((uint32_t)(i) >> 3) & 3u)))
+kwk_status kwk_fired_compact_bits(kwk_engine* eng);
+kwk_status kwk_fired_bits(kwk_engine* eng, uint32_t* out, uint64_t cap_words, uint64_t* n_words, uint32_t* n_records,
+                          uint32_t* n_segs, uint32_t* region_slots);
 kwk_status kwk_fired_packed(kwk_engine* eng, uint32_t* out, uint32_t cap, uint32_t* n_out);
 kwk_status kwk_fired_packed_device(kwk_engine* eng, const uint32_t** recs, const uint32_t** count);
 /* Overlapped hand-back to the host (the playStage workers' input, pod_controller.go:257-290): the
@@ -351,10 +365,13 @@ kwk_status kwk_fired_packed_device(kwk_engine* eng, const uint32_t** recs, const
  * the engine's next fetch).  Buffers from kwk_alloc_host make the copies DMA; double-buffer them
  * to read one step's records while the next step's copy runs.  seg_counts may be NULL. */
 typedef struct {
-  uint32_t n_records;      /* records in the list (the bytes copied: n_records * record_bytes) */
-  uint32_t record_bytes;   /* 2 (KWK_COMPACT_PACKED16), 4 (KWK_COMPACT_PACKED) or 8 (kwk_fired_rec) */
-  uint32_t n_segs;         /* 2-byte records: segments (seg_counts entries copied), else 0 */
-  uint32_t region_slots;   /* 2-byte records: slots per segment (KWK_FIRED16_SLOT), else 0 */
+  uint32_t n_records;      /* transitions in the list (records; the bitmap hand-back: its set bits) */
+  uint32_t record_bytes;   /* 2 (KWK_COMPACT_PACKED16), 4 (KWK_COMPACT_PACKED), 8 (kwk_fired_rec), 0 (KWK_COMPACT_BITS) */
+  uint32_t n_segs;         /* 2-byte records / bitmap hand-back: segments (seg_counts entries copied), else 0 */
+  uint32_t region_slots;   /* 2-byte records / bitmap hand-back: slots per segment, else 0 */
+  uint32_t format;         /* KWK_COMPACT_PACKED16, _PACKED, _BITS or 1 (kwk_fired_rec) */
+  uint32_t reserved;
+  uint64_t bytes;          /* bytes copied into out */
 } kwk_fetch_info;
 kwk_status kwk_fired_fetch_async(kwk_engine* eng, void* out, uint64_t cap_bytes, uint32_t* seg_counts, uint32_t seg_cap,
                                  kwk_fetch_info* info);

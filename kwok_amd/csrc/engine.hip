@@ -2173,11 +2173,15 @@ constexpr uint32_t kScanPer = 16;                         // counts per thread
 constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 4096 counts per group (one workgroup)
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
 
-// offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records
+// offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records.
+// kWords (the bitmap hand-back): the same over ceil(records / 16) (its 32-bit code words), and
+// group_tot[gridDim.x + g] = the group's records
+template <bool kWords = false>
 __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
                                                          uint32_t* __restrict__ offsets,
                                                          uint32_t* __restrict__ group_tot) {
   __shared__ uint32_t s_wave[kWavesPerBlock];
+  __shared__ uint32_t s_rec[kWavesPerBlock];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t i0 = blockIdx.x * kScanGroup + t * kScanPer;
   uint32_t v[kScanPer];
@@ -2193,6 +2197,16 @@ __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __rest
       if (i + 2 < n) c.z = counts[i + 2];
     }
     v[4 * q] = c.x; v[4 * q + 1] = c.y; v[4 * q + 2] = c.z; v[4 * q + 3] = c.w;
+  }
+  uint32_t rsum = 0;
+  if constexpr (kWords) {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+      rsum += v[j];
+      v[j] = (v[j] + 15u) >> 4;
+    }
+    for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
+    if (lane == 0) s_rec[wave] = rsum;
   }
   uint32_t sum = 0;
 #pragma unroll
@@ -2215,6 +2229,7 @@ __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __rest
     run += v[j];
   }
   if (t == kBlock - 1) group_tot[blockIdx.x] = run;
+  if (kWords && t == 0) group_tot[gridDim.x + blockIdx.x] = s_rec[0] + s_rec[1] + s_rec[2] + s_rec[3];
 }
 
 struct CompactArgs {
@@ -2377,6 +2392,105 @@ __global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) 
   const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
   for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
+}
+
+// The bitmap hand-back (kwk_fired_compact_bits): the 1-byte sweep's <= 4-stage records as one
+// 2048-bit map per segment — bit i = lane * 32 + k for the id at lds_id8(k, lane * 4), the order
+// the sweep's work list (lane-major, k ascending) writes its records in — plus their 2-bit stage
+// codes in that same order, 16 per 32-bit word, each segment's codes padded to a whole word:
+//   words [64 s, 64 s + 64)                 segment s's map
+//   words [64 n + W(s), 64 n + W(s + 1))    its codes, W(s) = sum over t < s of ceil(records_t / 16)
+// 1.25 bytes per transition at C5's 10 % firing for the maps + 0.25 for the codes, against 2 (+ the
+// records per segment) for the 2-byte records.  tot <- {words, records}.  kSmall: one launch, each
+// block summing the counts before its own (as compact16_small); else after seg_scan_kernel<true>.
+template <bool kSmall>
+__global__ __launch_bounds__(kBlock) void bits_kernel(CompactArgs a, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s_map[kWavesPerBlock][64];
+  __shared__ uint32_t s_part[2][kWavesPerBlock];
+  __shared__ uint32_t s_seg[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t first = blockIdx.x * kSegsPerBlock;
+  const uint32_t seg = first + wave;
+  const uint32_t n = a.n_segs;
+  uint32_t wpre = 0, rpre = 0, c = 0;  // code words / records before the segment, its records
+  if constexpr (kSmall) {
+    const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(a.counts);
+    uint32_t ws = 0, rs = 0;
+#pragma unroll 8
+    for (uint32_t q = threadIdx.x; q < first / 4u; q += kBlock) {
+      const uint4 v = c4[q];
+      rs += (v.x + v.y) + (v.z + v.w);
+      ws += ((v.x + 15u) >> 4) + ((v.y + 15u) >> 4) + ((v.z + 15u) >> 4) + ((v.w + 15u) >> 4);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      ws += __shfl_xor(ws, o);
+      rs += __shfl_xor(rs, o);
+    }
+    if (lane == 0) {
+      s_part[0][wave] = ws;
+      s_part[1][wave] = rs;
+    }
+    if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < n ? a.counts[first + threadIdx.x] : 0u;
+    __syncthreads();
+    if (seg >= n) return;
+    wpre = s_part[0][0] + s_part[0][1] + s_part[0][2] + s_part[0][3];
+    rpre = s_part[1][0] + s_part[1][1] + s_part[1][2] + s_part[1][3];
+    for (uint32_t w = 0; w < wave; ++w) {
+      wpre += (s_seg[w] + 15u) >> 4;
+      rpre += s_seg[w];
+    }
+    c = s_seg[wave];
+  } else {
+    if (seg >= n) return;
+    const uint32_t g = seg / kScanGroup;
+    for (uint32_t x = lane; x < g; x += 64) wpre += a.group_tot[x];
+    for (int o = 32; o > 0; o >>= 1) wpre += __shfl_xor(wpre, o);
+    wpre += a.offsets[1 + seg];
+    c = a.counts[seg];
+    if (seg == n - 1) {  // the records of every group
+      const uint32_t groups = (n + kScanGroup - 1) / kScanGroup;
+      for (uint32_t x = lane; x < groups; x += 64) rpre += a.group_tot[groups + x];
+      for (int o = 32; o > 0; o >>= 1) rpre += __shfl_xor(rpre, o);
+      rpre -= c;
+    }
+  }
+  const uint16_t* __restrict__ rp =
+      reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+  uint32_t* __restrict__ map = s_map[wave];
+  map[lane] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t j = lane; j < c; j += 64u) {
+    const uint32_t x = rp[j] & 0x7FFu, jj = x >> 8;
+    atomicOr(&map[((x >> 2) & 63u) ^ jj], 1u << ((x & 3u) * 8u + jj));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(a.out);
+  __builtin_nontemporal_store(map[lane], out + 64u * seg + lane);
+  uint32_t* __restrict__ codes = out + 64u * n + wpre;
+  for (uint32_t base = 0; base < c; base += 1024u) {  // 16 records (two 16-byte loads) per lane and word
+    const uint32_t i = base + 16u * lane;
+    if (i < c) {
+      const uint4* q = reinterpret_cast<const uint4*>(rp + i);
+      const uint4 r0 = q[0], r1 = q[1];
+      const uint32_t d[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      uint32_t w = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < 8; ++t) {
+        w |= ((d[t] >> 11) & 3u) << (4u * t);
+        w |= ((d[t] >> 27) & 3u) << (4u * t + 2u);
+      }
+      const uint32_t left = c - i;  // codes past the segment's records: zero
+      if (left < 16u) w &= (1u << (2u * left)) - 1u;
+      __builtin_nontemporal_store(w, codes + i / 16u);
+    }
+  }
+  if (seg == n - 1 && lane == 0) {
+    tot[0] = 64u * n + wpre + ((c + 15u) >> 4);
+    tot[1] = rpre + c;
+    a.offsets[0] = tot[0];
+  }
 }
 
 // Hand-back in one launch for small sweeps (at most kwk_engine::compact_small segments, 8192 by default: the node kinds, the
@@ -4054,6 +4168,7 @@ struct kwk_engine {
   bool compacted = false;     // the last sweep's fired list is compacted on the device
   bool compacted_packed = false;  // ... as 4-byte packed records (kwk_fired_compact_packed)
   bool compacted_16 = false;      // ... as the 1-byte sweep's 2-byte records (kwk_fired_compact_packed16)
+  bool compacted_bits = false;    // ... as its per-segment maps + stage codes (kwk_fired_compact_bits)
   // kwk_fired_fetch_async: the copy stream, the list length's pinned word, a snapshot of the
   // segment counts (the next sweep rewrites d_wave_counts while the copy reads the snapshot)
   hipStream_t copy_stream = nullptr;
@@ -4126,7 +4241,8 @@ struct kwk_engine {
   uint32_t* d_btot_prev = nullptr;  // ... of the one before (swapped with d_btot as the counts)
   uint32_t* d_wave_counts = nullptr;
   uint32_t* d_wave_offsets = nullptr;
-  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
+  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals (x2: the bitmap hand-back's records)
+  uint32_t* d_hb_tot = nullptr;       // the bitmap hand-back's {words, records}
   unsigned long long* d_cum = nullptr;
   unsigned long long* d_stats = nullptr;
   uint64_t steps = 0;
@@ -4632,7 +4748,8 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_btot, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
   ALLOC(e->d_btot_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
-  ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
+  ALLOC(e->d_seg_groups, sizeof(uint32_t) * 2 * (n_waves / kScanGroup + 2));
+  ALLOC(e->d_hb_tot, 64);
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   ALLOC(e->d_id2w, sizeof(uint16_t) * 256);
@@ -4671,7 +4788,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_hb_tot, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -5336,7 +5453,7 @@ kwk_status kwk_sync(kwk_engine* e) {
 static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t stream = nullptr) {
   if (!stream) stream = e->stream;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
-  if (mode == 2 && e->last_rec != kRecId8Half) mode = 1;
+  if ((mode == 2 || mode == 3) && e->last_rec != kRecId8Half) mode = 1;
   const bool packed = mode == 1;
   if (e->copy_pending) {  // kwk_fired_fetch_async is still copying the list this rewrites
     HIP_TRY(hipStreamWaitEvent(stream, e->ev_copied, 0));
@@ -5345,8 +5462,10 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
   e->compacted = true;
   e->compacted_packed = packed;
   e->compacted_16 = mode == 2;
+  e->compacted_bits = mode == 3;
   if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
     HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), stream));
+    HIP_TRY(hipMemsetAsync(e->d_hb_tot, 0, 2 * sizeof(uint32_t), stream));
     return KWK_OK;
   }
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
@@ -5367,6 +5486,11 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
+  if (mode == 3 && n_waves <= e->compact_small) {
+    hipLaunchKernelGGL(bits_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_hb_tot);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
   if (mode != 2 && n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
     const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half, true>
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8, true>
@@ -5377,8 +5501,16 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
     HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, stream));
     return KWK_OK;
   }
-  hipLaunchKernelGGL(seg_scan_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup), dim3(kBlock), 0, stream,
-                     e->d_wave_counts, n_waves, e->d_wave_offsets, e->d_seg_groups);
+  const uint32_t groups = (n_waves + kScanGroup - 1) / kScanGroup;
+  if (mode == 3) {
+    hipLaunchKernelGGL(seg_scan_kernel<true>, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
+                       e->d_wave_offsets, e->d_seg_groups);
+    hipLaunchKernelGGL(bits_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_hb_tot);
+    HIP_TRY(hipGetLastError());
+    return KWK_OK;
+  }
+  hipLaunchKernelGGL(seg_scan_kernel<false>, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
+                     e->d_wave_offsets, e->d_seg_groups);
   constexpr uint32_t W = kCompactSpw;
   if (mode == 2) {
     constexpr uint32_t W16 = kCompact16Spw;
@@ -5449,7 +5581,42 @@ kwk_status kwk_fired_packed(kwk_engine* e, uint32_t* out, uint32_t cap, uint32_t
 }
 
 static int compact_mode(uint32_t compact) {
-  return compact == KWK_COMPACT_PACKED16 ? 2 : compact == KWK_COMPACT_PACKED ? 1 : 0;
+  return compact == KWK_COMPACT_BITS ? 3 : compact == KWK_COMPACT_PACKED16 ? 2 : compact == KWK_COMPACT_PACKED ? 1 : 0;
+}
+
+kwk_status kwk_fired_compact_bits(kwk_engine* e) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (kwk_status st = set_dev(e)) return st;
+  return enqueue_compact(e, 3);
+}
+
+kwk_status kwk_fired_bits(kwk_engine* e, uint32_t* out, uint64_t cap_words, uint64_t* n_words, uint32_t* n_records,
+                          uint32_t* n_segs, uint32_t* region_slots) {
+  ErrScope es_(e);
+  if (!e || !n_words || !n_records || !n_segs || !region_slots) return fail(KWK_EINVAL, "null argument");
+  if (kwk_status st = set_dev(e)) return st;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  *n_segs = n_waves;
+  *region_slots = 64u * e->last_objs << e->last_region_shift;
+  *n_words = 0;
+  *n_records = 0;
+  if (n_waves == 0) return KWK_OK;
+  if (!e->compacted || !e->compacted_bits) {
+    if (e->last_rec != kRecId8Half)
+      return fail(KWK_ESTATE, "the bitmap hand-back is the 1-byte sweep's with at most 4 stages: use kwk_fired_packed");
+    if (kwk_status st = enqueue_compact(e, 3)) return st;
+  }
+  uint32_t t[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(t, e->d_hb_tot, sizeof(t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_words = t[0];
+  *n_records = t[1];
+  if (!out) return KWK_OK;
+  if (t[0] > cap_words) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(t[0]) + " words");
+  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint32_t) * (size_t)t[0], hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
 }
 
 kwk_status kwk_fired_compact_packed16(kwk_engine* e) {
@@ -5566,7 +5733,8 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
 kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uint32_t** count) {
   ErrScope es_(e);
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
-  if (!e->compacted || e->compacted_packed || e->compacted_16) return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
+  if (!e->compacted || e->compacted_packed || e->compacted_16 || e->compacted_bits)
+    return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
   *recs = e->d_compact;
   *count = e->d_wave_offsets;
   return KWK_OK;
@@ -5578,7 +5746,7 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (kwk_status st = set_dev(e)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
-  if (!e->compacted || e->compacted_packed || e->compacted_16)  // the segments are intact: expand them as kwk_fired_rec
+  if (!e->compacted || e->compacted_packed || e->compacted_16 || e->compacted_bits)  // the segments are intact: expand them
     if (kwk_status st = enqueue_compact(e)) return st;
   uint32_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -5609,21 +5777,25 @@ kwk_status kwk_fired_fetch_async(kwk_engine* e, void* out, uint64_t cap_bytes, u
     HIP_TRY(hipHostMalloc((void**)&e->h_count, 64, hipHostMallocDefault));
     HIP_TRY(hipMalloc((void**)&e->d_counts_snap, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
   }
-  const uint32_t rb = e->compacted_16 ? 2u : e->compacted_packed ? 4u : (uint32_t)sizeof(kwk_fired_rec);
+  const bool bits = e->compacted_bits;
+  const uint32_t rb = bits ? 4u : e->compacted_16 ? 2u : e->compacted_packed ? 4u : (uint32_t)sizeof(kwk_fired_rec);
   const bool segs = e->compacted_16 && seg_counts;
   if (segs && n_waves > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(n_waves));
   // the length (and the segment counts) behind the compaction on the engine's stream; only the
   // length is waited for here
-  HIP_TRY(hipMemcpyAsync(e->h_count, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->h_count, bits ? e->d_hb_tot : e->d_wave_offsets, 2 * sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, e->stream));
   if (segs)
     HIP_TRY(hipMemcpyAsync(e->d_counts_snap, e->d_wave_counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToDevice,
                            e->stream));
   HIP_TRY(hipEventRecord(e->ev_count, e->stream));
   HIP_TRY(hipEventSynchronize(e->ev_count));
-  const uint32_t total = *e->h_count;
-  info->n_records = total;
-  info->record_bytes = rb;
-  if (e->compacted_16) {
+  const uint32_t total = e->h_count[0];  // records, or the bitmap hand-back's 32-bit words
+  info->n_records = bits ? e->h_count[1] : total;
+  info->record_bytes = bits ? 0u : rb;
+  info->format = bits ? KWK_COMPACT_BITS : e->compacted_16 ? KWK_COMPACT_PACKED16 : e->compacted_packed ? KWK_COMPACT_PACKED : 1u;
+  info->bytes = (uint64_t)total * rb;
+  if (e->compacted_16 || bits) {
     info->n_segs = n_waves;
     info->region_slots = 64u * e->last_objs << e->last_region_shift;
   }

@@ -79,7 +79,7 @@ class StepStats(C.Structure):
 class FetchInfo(C.Structure):
     """kwk_fetch_info (kwk_fired_fetch_async)."""
     _fields_ = [("n_records", C.c_uint32), ("record_bytes", C.c_uint32), ("n_segs", C.c_uint32),
-                ("region_slots", C.c_uint32)]
+                ("region_slots", C.c_uint32), ("format", C.c_uint32), ("reserved", C.c_uint32), ("bytes", C.c_uint64)]
 
 
 class SweepInfo(C.Structure):
@@ -180,12 +180,13 @@ EXPORTS = [
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
     "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
     "kwk_fired_packed16", "kwk_fired_fetch_async", "kwk_fired_fetch_wait",
-    "kwk_fired_fold16",
+    "kwk_fired_fold16", "kwk_fired_compact_bits", "kwk_fired_bits",
 ]
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
 COMPACT_PACKED = 2  # kwk_step_n compact = KWK_COMPACT_PACKED
 COMPACT_PACKED16 = 3  # kwk_step_n compact = KWK_COMPACT_PACKED16 (2-byte records where the sweep has them)
+COMPACT_BITS = 4  # kwk_step_n compact = KWK_COMPACT_BITS (per-segment fired maps + 2-bit stage codes, same engines)
 AGG_USAGE = 1 << 0  # KWK_AGG_USAGE
 
 _lib = None
@@ -247,6 +248,9 @@ def lib():
     L.kwk_fired_packed_device.argtypes = [C.c_void_p, _p(C.c_void_p), _p(C.c_void_p)]
     L.kwk_fired_fetch_async.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, _p(FetchInfo)]
     L.kwk_fired_fetch_wait.argtypes = [C.c_void_p]
+    L.kwk_fired_compact_bits.argtypes = [C.c_void_p]
+    L.kwk_fired_bits.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, _p(C.c_uint64), _p(C.c_uint32), _p(C.c_uint32),
+                                 _p(C.c_uint32)]
     L.kwk_fired_fold16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
@@ -300,6 +304,31 @@ def check(status: int, what: str = "", eng=None):
 
 def ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def bits_slot(i: np.ndarray) -> np.ndarray:
+    """KWK_BITS_SLOT: the slot within its segment of map bit i (lane i >> 5, phase-1 bit k = i & 31 of
+    that lane, i.e. byte k >> 3 of its dword k & 7)."""
+    i = i.astype(np.uint32)
+    jj, lane, b = i & np.uint32(7), (i >> np.uint32(5)) & np.uint32(63), (i >> np.uint32(3)) & np.uint32(3)
+    return (jj >> np.uint32(2)) * np.uint32(1024) + lane * np.uint32(16) + (jj & np.uint32(3)) * np.uint32(4) + b
+
+
+def bits_decode(words: np.ndarray, n_segs: int, region_slots: int):
+    """(slot, stage) arrays of a kwk_fired_bits list (KWK_COMPACT_BITS in kwok_engine.h): the maps
+    (64 words per segment) give the slots in bit order, the codes after them the stages."""
+    words = np.asarray(words, dtype=np.uint32)
+    maps = words[:64 * n_segs]
+    bits = np.unpackbits(maps.view(np.uint8), bitorder="little").reshape(n_segs, 2048)
+    seg, i = np.nonzero(bits)
+    counts = bits.sum(axis=1, dtype=np.int64)
+    wstart = np.concatenate(([0], np.cumsum((counts + 15) // 16)))[:-1]
+    rank = np.arange(len(seg), dtype=np.int64) - np.repeat(np.concatenate(([0], np.cumsum(counts)))[:-1], counts)
+    code_words = words[64 * n_segs:]
+    w = code_words[wstart[seg] + rank // 16]
+    stage = (w >> (2 * (rank % 16)).astype(np.uint32)) & np.uint32(3)
+    slot = seg.astype(np.int64) * int(region_slots) + bits_slot(i).astype(np.int64)
+    return slot, stage
 
 
 def fired16_decode(recs: np.ndarray, seg_counts: np.ndarray, region_slots: int):

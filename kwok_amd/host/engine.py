@@ -135,6 +135,8 @@ class PinnedBuffer:
 def _compact_code(compact) -> int:
     if compact == "packed16":
         return abi.COMPACT_PACKED16
+    if compact == "bits":
+        return abi.COMPACT_BITS
     if compact == "packed":
         return abi.COMPACT_PACKED
     return 1 if compact else 0
@@ -265,6 +267,8 @@ class Engine:
         list compacted on the device (enqueue only)."""
         if packed == "16":
             self._check(abi.lib().kwk_fired_compact_packed16(self.h), "kwk_fired_compact_packed16")
+        elif packed == "bits":
+            self._check(abi.lib().kwk_fired_compact_bits(self.h), "kwk_fired_compact_bits")
         elif packed:
             self._check(abi.lib().kwk_fired_compact_packed(self.h), "kwk_fired_compact_packed")
         else:
@@ -306,6 +310,18 @@ class Engine:
         if n.value:
             self._check(L.kwk_fired_fold16(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_fold16")
         return out
+
+    def fired_bits(self):
+        """The last step's list as per-segment fired maps + 2-bit stage codes (kwk_fired_bits) ->
+        (words u32, transitions, segments, region_slots); abi.bits_decode gives (slot, stage)."""
+        nw, nr, ns, rs = C.c_uint64(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        L = abi.lib()
+        self._check(L.kwk_fired_bits(self.h, None, 0, C.byref(nw), C.byref(nr), C.byref(ns), C.byref(rs)), "kwk_fired_bits")
+        out = np.zeros(nw.value, dtype=np.uint32)
+        if nw.value:
+            self._check(L.kwk_fired_bits(self.h, abi.ptr(out), nw.value, C.byref(nw), C.byref(nr), C.byref(ns), C.byref(rs)),
+                        "kwk_fired_bits")
+        return out, nr.value, ns.value, rs.value
 
     def fired_packed16(self, pinned=None):
         """The last step's list as 2-byte records (kwk_fired_packed16) -> (records u16, records per

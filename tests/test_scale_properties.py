@@ -198,9 +198,22 @@ def test_packed_handback_equals_records_at_4m_pods(state):
                 assert np.array_equal(sl, full["slot"].astype(np.int64)), k
                 assert np.array_equal(sg, full["stage"].astype(np.uint32)), k
                 assert np.array_equal(fl, full["flags"].astype(np.uint32)), k
+                # the bitmap hand-back (maps + 2-bit codes), both paths: same (slot, stage) sequence
+                for small in HANDBACK_PATHS:
+                    _handback_path(eng, small)
+                    eng.fired_compact("bits")
+                    words, n_tr, ns, rs2 = eng.fired_bits()
+                    assert n_tr == len(full) and ns == len(cnt) and rs2 == rs, (k, small)
+                    bsl, bsg = abi.bits_decode(words, ns, rs2)
+                    assert len(words) == 64 * ns + int(((cnt.astype(np.int64) + 15) // 16).sum()), (k, small)
+                    assert np.array_equal(bsl, full["slot"].astype(np.int64)), (k, small)
+                    assert np.array_equal(bsg, full["stage"].astype(np.uint32)), (k, small)
+                _handback_path(eng, HANDBACK_PATHS[0])
             else:
                 with pytest.raises(abi.EngineError):
                     eng.fired_packed16()
+                with pytest.raises(abi.EngineError):
+                    eng.fired_bits()
         _handback_path(eng, HANDBACK_PATHS[0])
         ref = eng.fired_packed()
         eng.step_n(1, now0 + 4 * dt, dt, 0x6B776F6B, 4, "packed")
@@ -213,6 +226,12 @@ def test_packed_handback_equals_records_at_4m_pods(state):
             full = eng.fired()
             sl, sg, _ = abi.fired16_decode(recs, cnt, rs)
             assert len(recs) > 0 and np.array_equal(sl, full["slot"].astype(np.int64))
+            eng.step_n(1, now0 + 6 * dt, dt, 0x6B776F6B, 6, "bits")
+            words, n_tr, ns, rs = eng.fired_bits()
+            full = eng.fired()
+            bsl, bsg = abi.bits_decode(words, ns, rs)
+            assert n_tr == len(full) > 0 and np.array_equal(bsl, full["slot"].astype(np.int64))
+            assert np.array_equal(bsg, full["stage"].astype(np.uint32))
     finally:
         eng.close()
 
@@ -380,12 +399,12 @@ def test_fetch_async_equals_sync_readback():
     """kwk_fired_fetch_async (the overlapped host hand-back): each step's list copied on the copy
     stream while the next step is enqueued and compacted (the compaction waits for the copy on the
     device), buffers alternating, equals the synchronous kwk_fired_packed16 / kwk_fired_packed /
-    kwk_fired of a twin engine stepped alike — 2-byte records with their per-segment counts,
-    4-byte packed and 8-byte records."""
+    kwk_fired of a twin engine stepped alike — the bitmap hand-back (maps + stage codes), 2-byte
+    records with their per-segment counts, 4-byte packed and 8-byte records."""
     from kwok_amd.host import abi
     from kwok_amd.host.engine import PinnedBuffer
     now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
-    for mode in ("16", True, False):
+    for mode in ("bits", "16", True, False):
         (_, a), (_, b) = _pods("auto", n_nodes=20_000), _pods("auto", n_nodes=20_000)
         bufs = [(PinnedBuffer(8 * a.capacity), PinnedBuffer(4 * (a.capacity // 512 + 64))) for _ in range(2)]
         try:
@@ -395,7 +414,13 @@ def test_fetch_async_equals_sync_readback():
                     e.fired_compact(mode)
                 out, cnt = bufs[k % 2]
                 info = b.fetch_async(out, cnt)
-                if mode == "16":
+                if mode == "bits":
+                    words, n_tr, ns, rs = a.fired_bits()
+                    b.fetch_wait()
+                    assert info["format"] == abi.COMPACT_BITS and info["record_bytes"] == 0
+                    assert info["n_records"] == n_tr and info["n_segs"] == ns and info["bytes"] == 4 * len(words)
+                    assert np.array_equal(out.array(np.uint32, len(words)), words), k
+                elif mode == "16":
                     recs, segc, rs = a.fired_packed16()
                     b.fetch_wait()
                     assert info["record_bytes"] == 2 and info["n_segs"] == len(segc) and info["region_slots"] == rs
