@@ -339,15 +339,18 @@ kwk_status kwk_fired_compact_packed(kwk_engine* eng);
 kwk_status kwk_fired_compact_packed16(kwk_engine* eng);
 kwk_status kwk_fired_packed16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint32_t* n_out, uint32_t* seg_counts,
                               uint32_t seg_cap, uint32_t* n_segs, uint32_t* region_slots);
-/* The hand-back at ~1.5 bytes per transition (C5's 10 % firing), for the same engines as the 2-byte
- * records: per segment s of n (slots [s * region_slots, (s + 1) * region_slots)) a 2048-bit map
- * at words [64 s, 64 s + 64), bit i set when the object of KWK_BITS_SLOT(i) fired, then every
- * segment's stage codes from word 64 n on, 2 bits each (code j at bits 2 (j % 16) of the segment's
- * word j / 16), one per set bit in bit order, each segment's codes padded to a whole word:
- * segment s's codes start after sum_{t<s} ceil(popcount(map t) / 16) words.  Same (slot, stage)
- * sequence as kwk_fired; the flags are not carried (as KWK_COMPACT_PACKED).  n_words: the list's
- * words, n_records: its transitions.  kwk_step_n(..., KWK_COMPACT_BITS, ...) enqueues it per step
- * (an engine without 2-byte records then leaves the 4-byte packed list). */
+/* The hand-back at ~1.1 bytes per transition (C5's 10 % firing), for the same engines as the 2-byte
+ * records: per segment s of n (slots [s * region_slots, (s + 1) * region_slots)) a 2048-bit fired
+ * map, bit i set when the object of KWK_BITS_SLOT(i) fired, kept byte-sparse, and the 2-bit stage
+ * codes of its set bits in bit order.  Words:
+ *   s < n                 segment s: records c (bits 0-15), nonzero map bytes z (bits 16-31)
+ *   n + P(s) ...          segment s: 8 summary words (bit t of word w: map byte 32 w + t is
+ *                         nonzero), its z nonzero map bytes in order (padded to a word), its c
+ *                         codes, 16 per word (code j at bits 2 (j % 16) of word j / 16; padded)
+ * with P(s) = sum over t < s of (8 + ceil(z_t / 4) + ceil(c_t / 16)).  Same (slot, stage) sequence
+ * as kwk_fired; the flags are not carried (as KWK_COMPACT_PACKED).  n_words: the list's words,
+ * n_records: its transitions.  kwk_step_n(..., KWK_COMPACT_BITS, ...) enqueues it per step (an
+ * engine without 2-byte records then leaves the 4-byte packed list). */
 #define KWK_COMPACT_BITS 4u
 #define KWK_BITS_SLOT(i) KWK_FIRED16_SLOT(((((uint32_t)(i) & 7u) << 8) | ((((uint32_t)(i) >> 5) & 63u) << 2 ^ (((uint32_t)(i) & 7u) << 2)) | (((uint32_t)(i) >> 3) & 3u)))
 kwk_status kwk_fired_compact_bits(kwk_engine* eng);

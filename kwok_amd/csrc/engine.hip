@@ -2173,15 +2173,11 @@ constexpr uint32_t kScanPer = 16;                         // counts per thread
 constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 4096 counts per group (one workgroup)
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
 
-// offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records.
-// kWords (the bitmap hand-back): the same over ceil(records / 16) (its 32-bit code words), and
-// group_tot[gridDim.x + g] = the group's records
-template <bool kWords = false>
+// offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records
 __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
                                                          uint32_t* __restrict__ offsets,
                                                          uint32_t* __restrict__ group_tot) {
   __shared__ uint32_t s_wave[kWavesPerBlock];
-  __shared__ uint32_t s_rec[kWavesPerBlock];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t i0 = blockIdx.x * kScanGroup + t * kScanPer;
   uint32_t v[kScanPer];
@@ -2197,16 +2193,6 @@ __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __rest
       if (i + 2 < n) c.z = counts[i + 2];
     }
     v[4 * q] = c.x; v[4 * q + 1] = c.y; v[4 * q + 2] = c.z; v[4 * q + 3] = c.w;
-  }
-  uint32_t rsum = 0;
-  if constexpr (kWords) {
-#pragma unroll
-    for (uint32_t j = 0; j < kScanPer; ++j) {
-      rsum += v[j];
-      v[j] = (v[j] + 15u) >> 4;
-    }
-    for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
-    if (lane == 0) s_rec[wave] = rsum;
   }
   uint32_t sum = 0;
 #pragma unroll
@@ -2229,7 +2215,6 @@ __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __rest
     run += v[j];
   }
   if (t == kBlock - 1) group_tot[blockIdx.x] = run;
-  if (kWords && t == 0) group_tot[gridDim.x + blockIdx.x] = s_rec[0] + s_rec[1] + s_rec[2] + s_rec[3];
 }
 
 struct CompactArgs {
@@ -2396,67 +2381,22 @@ __global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) 
 
 // The bitmap hand-back (kwk_fired_compact_bits): the 1-byte sweep's <= 4-stage records as one
 // 2048-bit map per segment — bit i = lane * 32 + k for the id at lds_id8(k, lane * 4), the order
-// the sweep's work list (lane-major, k ascending) writes its records in — plus their 2-bit stage
-// codes in that same order, 16 per 32-bit word, each segment's codes padded to a whole word:
-//   words [64 s, 64 s + 64)                 segment s's map
-//   words [64 n + W(s), 64 n + W(s + 1))    its codes, W(s) = sum over t < s of ceil(records_t / 16)
-// 1.25 bytes per transition at C5's 10 % firing for the maps + 0.25 for the codes, against 2 (+ the
-// records per segment) for the 2-byte records.  tot <- {words, records}.  kSmall: one launch, each
-// block summing the counts before its own (as compact16_small); else after seg_scan_kernel<true>.
-template <bool kSmall>
-__global__ __launch_bounds__(kBlock) void bits_kernel(CompactArgs a, uint32_t* __restrict__ tot) {
-  __shared__ uint32_t s_map[kWavesPerBlock][64];
-  __shared__ uint32_t s_part[2][kWavesPerBlock];
-  __shared__ uint32_t s_seg[kWavesPerBlock];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t first = blockIdx.x * kSegsPerBlock;
-  const uint32_t seg = first + wave;
-  const uint32_t n = a.n_segs;
-  uint32_t wpre = 0, rpre = 0, c = 0;  // code words / records before the segment, its records
-  if constexpr (kSmall) {
-    const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(a.counts);
-    uint32_t ws = 0, rs = 0;
-#pragma unroll 8
-    for (uint32_t q = threadIdx.x; q < first / 4u; q += kBlock) {
-      const uint4 v = c4[q];
-      rs += (v.x + v.y) + (v.z + v.w);
-      ws += ((v.x + 15u) >> 4) + ((v.y + 15u) >> 4) + ((v.z + 15u) >> 4) + ((v.w + 15u) >> 4);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      ws += __shfl_xor(ws, o);
-      rs += __shfl_xor(rs, o);
-    }
-    if (lane == 0) {
-      s_part[0][wave] = ws;
-      s_part[1][wave] = rs;
-    }
-    if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < n ? a.counts[first + threadIdx.x] : 0u;
-    __syncthreads();
-    if (seg >= n) return;
-    wpre = s_part[0][0] + s_part[0][1] + s_part[0][2] + s_part[0][3];
-    rpre = s_part[1][0] + s_part[1][1] + s_part[1][2] + s_part[1][3];
-    for (uint32_t w = 0; w < wave; ++w) {
-      wpre += (s_seg[w] + 15u) >> 4;
-      rpre += s_seg[w];
-    }
-    c = s_seg[wave];
-  } else {
-    if (seg >= n) return;
-    const uint32_t g = seg / kScanGroup;
-    for (uint32_t x = lane; x < g; x += 64) wpre += a.group_tot[x];
-    for (int o = 32; o > 0; o >>= 1) wpre += __shfl_xor(wpre, o);
-    wpre += a.offsets[1 + seg];
-    c = a.counts[seg];
-    if (seg == n - 1) {  // the records of every group
-      const uint32_t groups = (n + kScanGroup - 1) / kScanGroup;
-      for (uint32_t x = lane; x < groups; x += 64) rpre += a.group_tot[groups + x];
-      for (int o = 32; o > 0; o >>= 1) rpre += __shfl_xor(rpre, o);
-      rpre -= c;
-    }
-  }
+// the sweep's work list (lane-major, k ascending) writes its records in — kept byte-sparse, plus
+// the records' 2-bit stage codes in that same order.  For n segments:
+//   word s < n                {records c: 16, nonzero map bytes z: 16} of segment s
+//   from word n + P(s)        segment s: 8 summary words (bit t of word w: map byte 32 w + t is
+//                             nonzero), its z nonzero map bytes in order (padded to a word), its c
+//                             codes, 16 per word (code j at bits 2 (j % 16) of word j / 16)
+// with P(s) = sum over t < s of (8 + ceil(z_t / 4) + ceil(c_t / 16)).  ~1.1 bytes per transition at
+// C5's 10 % firing (43 % of the map bytes are zero), against 2 (+ 4 per segment) for the 2-byte
+// records.  Two kernels over one wave per segment: bits_size_kernel (the map in LDS -> {c, z}, the
+// segment's words, its workgroup's records) and, after the prefix of those words (in-kernel up to
+// compact_small segments, else seg_scan_kernel), bits_write_kernel (the map again -> the words at
+// P(s)); tot <- {words, records}.
+__device__ __forceinline__ void bits_map(const CompactArgs& a, uint32_t seg, uint32_t c, uint32_t* __restrict__ map,
+                                         uint32_t lane) {
   const uint16_t* __restrict__ rp =
       reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
-  uint32_t* __restrict__ map = s_map[wave];
   map[lane] = 0u;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -2466,30 +2406,129 @@ __global__ __launch_bounds__(kBlock) void bits_kernel(CompactArgs a, uint32_t* _
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t d) {
+  return (uint32_t)((d & 0xFFu) != 0) + (uint32_t)((d & 0xFF00u) != 0) + (uint32_t)((d & 0xFF0000u) != 0) +
+         (uint32_t)((d >> 24) != 0);
+}
+
+__global__ __launch_bounds__(kBlock) void bits_size_kernel(CompactArgs a, uint32_t* __restrict__ wc,
+                                                           uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s_map[kWavesPerBlock][64];
+  __shared__ uint32_t s_c[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t seg = blockIdx.x * kSegsPerBlock + wave;
+  uint32_t c = 0;
+  if (seg < a.n_segs) {
+    c = a.counts[seg];
+    bits_map(a, seg, c, s_map[wave], lane);
+    uint32_t z = nz_bytes(s_map[wave][lane]);
+    for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
+    if (lane == 0) {
+      reinterpret_cast<uint32_t*>(a.out)[seg] = c | z << 16;
+      wc[seg] = 8u + ((z + 3u) >> 2) + ((c + 15u) >> 4);
+    }
+  }
+  if (lane == 0) s_c[wave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+}
+
+template <bool kSmall>
+__global__ __launch_bounds__(kBlock) void bits_write_kernel(CompactArgs a, const uint32_t* __restrict__ wc,
+                                                            const uint32_t* __restrict__ bsum, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s_map[kWavesPerBlock][64];
+  __shared__ uint32_t s_stage[kWavesPerBlock][64];  // the nonzero map bytes, in order
+  __shared__ uint32_t s_sum[kWavesPerBlock][8];
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  __shared__ uint32_t s_seg[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t first = blockIdx.x * kSegsPerBlock;
+  const uint32_t seg = first + wave;
+  const uint32_t n = a.n_segs;
+  uint32_t pre = 0;  // P(seg)
+  if constexpr (kSmall) {
+    const uint4* __restrict__ w4 = reinterpret_cast<const uint4*>(wc);
+    uint32_t ws = 0;
+#pragma unroll 8
+    for (uint32_t q = threadIdx.x; q < first / 4u; q += kBlock) {
+      const uint4 v = w4[q];
+      ws += (v.x + v.y) + (v.z + v.w);
+    }
+    for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o);
+    if (lane == 0) s_part[wave] = ws;
+    if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < n ? wc[first + threadIdx.x] : 0u;
+    __syncthreads();
+    if (seg >= n) return;
+    pre = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    for (uint32_t w = 0; w < wave; ++w) pre += s_seg[w];
+  } else {
+    if (seg >= n) return;
+    for (uint32_t x = lane; x < seg / kScanGroup; x += 64) pre += a.group_tot[x];
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    pre += a.offsets[1 + seg];
+  }
   uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(a.out);
-  __builtin_nontemporal_store(map[lane], out + 64u * seg + lane);
-  uint32_t* __restrict__ codes = out + 64u * n + wpre;
+  const uint32_t cz = out[seg];  // bits_size_kernel's {c, z}
+  const uint32_t c = cz & 0xFFFFu, z = cz >> 16;
+  uint32_t* __restrict__ map = s_map[wave];
+  bits_map(a, seg, c, map, lane);
+  uint32_t* __restrict__ dst = out + n + pre;
+  // summary: lane L's four map bytes are bits 4 (L % 8) .. + 3 of word L / 8; the nonzero bytes
+  // staged in LDS at their rank
+  const uint32_t d = map[lane];
+  const uint32_t f4 = (uint32_t)((d & 0xFFu) != 0) | (uint32_t)((d & 0xFF00u) != 0) << 1 |
+                      (uint32_t)((d & 0xFF0000u) != 0) << 2 | (uint32_t)((d >> 24) != 0) << 3;
+  uint32_t* __restrict__ sm = s_sum[wave];
+  uint32_t* __restrict__ st = s_stage[wave];
+  if (lane < 8) sm[lane] = 0u;
+  st[lane] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (f4) atomicOr(&sm[lane >> 3], f4 << (4u * (lane & 7u)));
+  const uint32_t cnt = (uint32_t)__popc(f4);
+  const uint32_t incl = wave_incl_scan(cnt);
+  uint32_t pb = incl - cnt;
+  uint8_t* __restrict__ sb = reinterpret_cast<uint8_t*>(st);
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    if ((f4 >> j) & 1u) sb[pb++] = (uint8_t)(d >> (8u * j));
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 8) __builtin_nontemporal_store(sm[lane], dst + lane);
+  const uint32_t zw = (z + 3u) >> 2;
+  if (lane < zw) __builtin_nontemporal_store(st[lane], dst + 8u + lane);
+  uint32_t* __restrict__ codes = dst + 8u + zw;
+  const uint16_t* __restrict__ rp =
+      reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
   for (uint32_t base = 0; base < c; base += 1024u) {  // 16 records (two 16-byte loads) per lane and word
     const uint32_t i = base + 16u * lane;
     if (i < c) {
       const uint4* q = reinterpret_cast<const uint4*>(rp + i);
       const uint4 r0 = q[0], r1 = q[1];
-      const uint32_t d[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      const uint32_t dd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
       uint32_t w = 0;
 #pragma unroll
       for (uint32_t t = 0; t < 8; ++t) {
-        w |= ((d[t] >> 11) & 3u) << (4u * t);
-        w |= ((d[t] >> 27) & 3u) << (4u * t + 2u);
+        w |= ((dd[t] >> 11) & 3u) << (4u * t);
+        w |= ((dd[t] >> 27) & 3u) << (4u * t + 2u);
       }
       const uint32_t left = c - i;  // codes past the segment's records: zero
       if (left < 16u) w &= (1u << (2u * left)) - 1u;
       __builtin_nontemporal_store(w, codes + i / 16u);
     }
   }
-  if (seg == n - 1 && lane == 0) {
-    tot[0] = 64u * n + wpre + ((c + 15u) >> 4);
-    tot[1] = rpre + c;
-    a.offsets[0] = tot[0];
+  if (seg == n - 1) {  // the list's words and records
+    const uint32_t nb = (n + kSegsPerBlock - 1) / kSegsPerBlock;
+    uint32_t r = 0;
+    for (uint32_t x = lane; x < nb; x += 64) r += bsum[x];
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    if (lane == 0) {
+      tot[0] = n + pre + 8u + zw + ((c + 15u) >> 4);
+      tot[1] = r;
+      a.offsets[0] = tot[0];
+    }
   }
 }
 
@@ -4176,6 +4215,13 @@ struct kwk_engine {
   uint32_t* h_count = nullptr;
   uint32_t* d_counts_snap = nullptr;
   bool copy_pending = false;   // the next compaction waits for ev_copied
+  // the list buffer double-buffered once fetched: a compaction whose buffer is still being copied
+  // moves to the other (waiting only for that one's copy), so step k + 1's compaction does not
+  // wait for step k's copy; the *_alt fields swap with their current counterparts
+  kwk_fired_rec* d_compact_alt = nullptr;
+  uint32_t* d_counts_snap_alt = nullptr;
+  hipEvent_t ev_copied_alt = nullptr;
+  bool copy_pending_alt = false;
   bool copy_recorded = false;  // ev_copied was recorded (kwk_fired_fetch_wait)
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
@@ -4241,8 +4287,10 @@ struct kwk_engine {
   uint32_t* d_btot_prev = nullptr;  // ... of the one before (swapped with d_btot as the counts)
   uint32_t* d_wave_counts = nullptr;
   uint32_t* d_wave_offsets = nullptr;
-  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals (x2: the bitmap hand-back's records)
+  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
   uint32_t* d_hb_tot = nullptr;       // the bitmap hand-back's {words, records}
+  uint32_t* d_bits_wc = nullptr;      // ... its words per segment
+  uint32_t* d_bits_bsum = nullptr;    // ... its records per workgroup of bits_size_kernel
   unsigned long long* d_cum = nullptr;
   unsigned long long* d_stats = nullptr;
   uint64_t steps = 0;
@@ -4748,8 +4796,10 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
   ALLOC(e->d_btot, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
   ALLOC(e->d_btot_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
-  ALLOC(e->d_seg_groups, sizeof(uint32_t) * 2 * (n_waves / kScanGroup + 2));
+  ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
   ALLOC(e->d_hb_tot, 64);
+  ALLOC(e->d_bits_wc, sizeof(uint32_t) * (n_waves + 4));
+  ALLOC(e->d_bits_bsum, sizeof(uint32_t) * (n_waves / kSegsPerBlock + 4));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
   ALLOC(e->d_stats, sizeof(unsigned long long) * kStatWords);
   ALLOC(e->d_id2w, sizeof(uint16_t) * 256);
@@ -4788,7 +4838,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_hb_tot, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -4801,10 +4851,11 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (e->ev_lease) hipEventDestroy(e->ev_lease);
   if (e->ev_podsync) hipEventDestroy(e->ev_podsync);
   if (e->copy_stream) hipStreamSynchronize(e->copy_stream);
-  for (hipEvent_t ev : {e->ev_count, e->ev_copied})
+  for (hipEvent_t ev : {e->ev_count, e->ev_copied, e->ev_copied_alt})
     if (ev) hipEventDestroy(ev);
   if (e->h_count) hipHostFree(e->h_count);
-  if (e->d_counts_snap) hipFree(e->d_counts_snap);
+  for (void* p : {(void*)e->d_counts_snap, (void*)e->d_counts_snap_alt, (void*)e->d_compact_alt})
+    if (p) hipFree(p);
   if (e->copy_stream) hipStreamDestroy(e->copy_stream);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
@@ -5455,7 +5506,13 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if ((mode == 2 || mode == 3) && e->last_rec != kRecId8Half) mode = 1;
   const bool packed = mode == 1;
-  if (e->copy_pending) {  // kwk_fired_fetch_async is still copying the list this rewrites
+  if (e->copy_pending && e->d_compact_alt) {  // kwk_fired_fetch_async is copying this buffer: the other one
+    std::swap(e->d_compact, e->d_compact_alt);
+    std::swap(e->d_counts_snap, e->d_counts_snap_alt);
+    std::swap(e->ev_copied, e->ev_copied_alt);
+    std::swap(e->copy_pending, e->copy_pending_alt);
+  }
+  if (e->copy_pending) {  // ... still copying the list this rewrites
     HIP_TRY(hipStreamWaitEvent(stream, e->ev_copied, 0));
     e->copy_pending = false;
   }
@@ -5487,7 +5544,9 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
     return KWK_OK;
   }
   if (mode == 3 && n_waves <= e->compact_small) {
-    hipLaunchKernelGGL(bits_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_hb_tot);
+    hipLaunchKernelGGL(bits_size_kernel, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum);
+    hipLaunchKernelGGL(bits_write_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum,
+                       e->d_hb_tot);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
@@ -5503,13 +5562,15 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
   }
   const uint32_t groups = (n_waves + kScanGroup - 1) / kScanGroup;
   if (mode == 3) {
-    hipLaunchKernelGGL(seg_scan_kernel<true>, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
-                       e->d_wave_offsets, e->d_seg_groups);
-    hipLaunchKernelGGL(bits_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_hb_tot);
+    hipLaunchKernelGGL(bits_size_kernel, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum);
+    hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_bits_wc, n_waves, e->d_wave_offsets,
+                       e->d_seg_groups);
+    hipLaunchKernelGGL(bits_write_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum,
+                       e->d_hb_tot);
     HIP_TRY(hipGetLastError());
     return KWK_OK;
   }
-  hipLaunchKernelGGL(seg_scan_kernel<false>, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
                      e->d_wave_offsets, e->d_seg_groups);
   constexpr uint32_t W = kCompactSpw;
   if (mode == 2) {
@@ -5774,6 +5835,9 @@ kwk_status kwk_fired_fetch_async(kwk_engine* e, void* out, uint64_t cap_bytes, u
     HIP_TRY(hipStreamCreateWithPriority(&e->copy_stream, hipStreamNonBlocking, prio));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_count, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_copied, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_copied_alt, hipEventDisableTiming));
+    HIP_TRY(hipMalloc((void**)&e->d_compact_alt, sizeof(kwk_fired_rec) * (size_t)e->capacity));
+    HIP_TRY(hipMalloc((void**)&e->d_counts_snap_alt, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
     HIP_TRY(hipHostMalloc((void**)&e->h_count, 64, hipHostMallocDefault));
     HIP_TRY(hipMalloc((void**)&e->d_counts_snap, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
   }
@@ -5833,7 +5897,7 @@ kwk_status kwk_fired_fetch_wait(kwk_engine* e) {
   ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
-  if (e->copy_recorded) HIP_TRY(hipEventSynchronize(e->ev_copied));
+  if (e->copy_recorded) HIP_TRY(hipStreamSynchronize(e->copy_stream));  // both buffers' copies
   return KWK_OK;
 }
 

@@ -315,19 +315,33 @@ def bits_slot(i: np.ndarray) -> np.ndarray:
 
 
 def bits_decode(words: np.ndarray, n_segs: int, region_slots: int):
-    """(slot, stage) arrays of a kwk_fired_bits list (KWK_COMPACT_BITS in kwok_engine.h): the maps
-    (64 words per segment) give the slots in bit order, the codes after them the stages."""
+    """(slot, stage) arrays of a kwk_fired_bits list (KWK_COMPACT_BITS in kwok_engine.h): per segment
+    {records c, nonzero map bytes z} up front, then its 8 summary words, its z nonzero map bytes
+    and its c stage codes at the running offset."""
     words = np.asarray(words, dtype=np.uint32)
-    maps = words[:64 * n_segs]
-    bits = np.unpackbits(maps.view(np.uint8), bitorder="little").reshape(n_segs, 2048)
-    seg, i = np.nonzero(bits)
-    counts = bits.sum(axis=1, dtype=np.int64)
-    wstart = np.concatenate(([0], np.cumsum((counts + 15) // 16)))[:-1]
-    rank = np.arange(len(seg), dtype=np.int64) - np.repeat(np.concatenate(([0], np.cumsum(counts)))[:-1], counts)
-    code_words = words[64 * n_segs:]
-    w = code_words[wstart[seg] + rank // 16]
-    stage = (w >> (2 * (rank % 16)).astype(np.uint32)) & np.uint32(3)
-    slot = seg.astype(np.int64) * int(region_slots) + bits_slot(i).astype(np.int64)
+    n = int(n_segs)
+    head = words[:n]
+    c = (head & np.uint32(0xFFFF)).astype(np.int64)
+    z = (head >> np.uint32(16)).astype(np.int64)
+    zw = (z + 3) // 4
+    size = 8 + zw + (c + 15) // 16
+    base = n + np.concatenate(([0], np.cumsum(size)))[:-1]
+    summ = words[base[:, None] + np.arange(8)]  # n x 8
+    nzb = np.unpackbits(np.ascontiguousarray(summ).view(np.uint8), bitorder="little").reshape(n, 256)
+    seg, m = np.nonzero(nzb)  # the nonzero map bytes, in order
+    assert np.array_equal(np.bincount(seg, minlength=n), z), "summary / byte count mismatch"
+    rank = np.arange(len(seg), dtype=np.int64) - np.repeat(np.concatenate(([0], np.cumsum(z)))[:-1], z)
+    byte_view = words.view(np.uint8)
+    mb = byte_view[4 * (base[seg] + 8) + rank]
+    bits = np.unpackbits(mb[:, None], axis=1, bitorder="little")  # one row per nonzero byte
+    row, b = np.nonzero(bits)
+    seg_b = seg[row]
+    i = m[row] * 8 + b
+    assert np.array_equal(np.bincount(seg_b, minlength=n), c), "map / record count mismatch"
+    rank2 = np.arange(len(seg_b), dtype=np.int64) - np.repeat(np.concatenate(([0], np.cumsum(c)))[:-1], c)
+    w = words[base[seg_b] + 8 + zw[seg_b] + rank2 // 16]
+    stage = (w >> (2 * (rank2 % 16)).astype(np.uint32)) & np.uint32(3)
+    slot = seg_b.astype(np.int64) * int(region_slots) + bits_slot(i).astype(np.int64)
     return slot, stage
 
 

@@ -37,17 +37,24 @@ def test_header_bits_slot_macro(tmp_path):
 
 
 def _encode(segs):
-    """bits_kernel's layout: 64 map words per segment, then each segment's codes padded to words."""
-    maps, codes = [], []
+    """bits_size_kernel + bits_write_kernel's layout: {c, z} per segment, then per segment the 8
+    summary words, the nonzero map bytes (padded to a word) and the stage codes (padded)."""
+    head, body = [], []
     for bits, stages in segs:
         m = np.zeros(2048, dtype=np.uint8)
         m[bits] = 1
-        maps.append(np.packbits(m, bitorder="little").view(np.uint32))
+        mb = np.packbits(m, bitorder="little")  # 256 map bytes
+        nz = mb != 0
+        head.append(len(bits) | int(nz.sum()) << 16)
+        body.append(np.packbits(nz.astype(np.uint8), bitorder="little").view(np.uint32))
+        zb = np.zeros(4 * ((int(nz.sum()) + 3) // 4), dtype=np.uint8)
+        zb[:int(nz.sum())] = mb[nz]
+        body.append(zb.view(np.uint32))
         w = np.zeros((len(bits) + 15) // 16, dtype=np.uint32)
         for j, st in enumerate(stages):
             w[j // 16] |= np.uint32(int(st) << (2 * (j % 16)))
-        codes.append(w)
-    return np.concatenate(maps + codes)
+        body.append(w)
+    return np.concatenate([np.array(head, dtype=np.uint32)] + body)
 
 
 def test_bits_decode_round_trip():
@@ -58,7 +65,6 @@ def test_bits_decode_round_trip():
         bits = np.flatnonzero(rng.random(2048) < density).astype(np.int64)
         segs.append((bits, rng.integers(0, 4, len(bits))))
     words = _encode(segs)
-    assert len(words) == 64 * len(segs) + sum((len(b) + 15) // 16 for b, _ in segs)
     slot, stage = abi.bits_decode(words, len(segs), 2048)
     want_slot = np.concatenate([s * 2048 + abi.bits_slot(b).astype(np.int64) for s, (b, _) in enumerate(segs)])
     want_stage = np.concatenate([st for _, st in segs]).astype(np.uint32)
