@@ -2787,6 +2787,7 @@ struct UsageArgs {
 constexpr uint32_t kUKeyDict = 256;  // entries of the 1-byte key column's value table
 constexpr uint32_t kUKeyZero = 255;  // its entry {0, 0}: the key a dead / out-of-range pod reads, so at
                                      // most 255 distinct keys take the 1-byte column
+constexpr uint32_t kUSeqKeys = 16;   // keys whose in-order sums of 0..16 pods usage_fast_kernel keeps in LDS
 
 // a pod's usage_key: containers (bits 28..31) x one interned value each, or 0 containers =
 // a pod whose containers differ: bits 0..27 index its {first, count} entry of the mixed table
@@ -3121,6 +3122,10 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
   __shared__ double s_pv[kKey8 ? 1 : kUFastVals];
   __shared__ double2 s_kv[kKey8 ? kUKeyDict : 1];
   __shared__ uint32_t s_nib[16];
+  // s_seq[k][n]: the in-order sum of n pods of key k (0.0 + v + v + ..., n adds), keys < kUSeqKeys:
+  // a lane's run whose 16 keys are one key sums to the entry of its live-pod count, bit for bit
+  // the per-pod sums below (a masked pod adds the zero entry, and s + 0.0 == s)
+  __shared__ double2 s_seq[kKey8 && WB == 1 ? kUSeqKeys : 1][kURun + 1];
   constexpr bool kCnt = kKey8 && WB == 1;  // mask counts can ride along (a.n_cmasks)
   __shared__ uint32_t s_clut[kCnt ? 256 : 1];
   __shared__ unsigned int s_ccnt[kCnt ? 4 : 1];
@@ -3199,6 +3204,20 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
     for (uint32_t j = threadIdx.x; j < a.podv_n; j += kBlock) s_pv[j] = a.podv[j];
   }
   __syncthreads();
+  if constexpr (kKey8 && WB == 1) {  // s_seq: one thread per (key, cpu | memory), n = 0..kURun in order
+    if (threadIdx.x < 2 * kUSeqKeys) {
+      const uint32_t k = threadIdx.x >> 1;
+      const double v = (threadIdx.x & 1) ? s_kv[k].y : s_kv[k].x;
+      double* col = reinterpret_cast<double*>(&s_seq[k][0]) + (threadIdx.x & 1);
+      double s = 0.0;
+      col[0] = s;
+      for (uint32_t n = 1; n <= kURun; ++n) {
+        s += v;
+        col[2 * n] = s;
+      }
+    }
+    __syncthreads();
+  }
   const uint32_t nv = a.n_cpu + a.n_mem;  // podv row: cpu values then memory values
   const uint32_t abit = WB == 1 ? kIdAlive : (WB == 8 && !a.fmt.dw) ? (uint32_t)KWK_F_ALIVE
                                                                    : (uint32_t)(KWK_F_ALIVE >> 8) << a.fmt.fshift;
@@ -3250,10 +3269,17 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
       const uint32_t lf = r0 + lane * kURun;
       const uint32_t p_lo = max(lf, c0), p_hi = min(lf + kURun, c1);
       const bool has = p_lo < p_hi;
-      // the non-empty node holding the lane's first pod
+      // the non-empty node holding the lane's first pod (the last k with sp[k] <= p_lo): from the
+      // chunk's mean node size: the guess's own bounds decide it for equal-sized nodes, else a
+      // binary search over the side of the guess that holds it
       uint32_t k = 0;
       if (has) {
-        uint32_t lo = 0, hi = nk;
+        const float f = (float)(p_lo - c0) * ((float)nk / (float)(c1 - c0));
+        const uint32_t g = min((uint32_t)f, nk - 1u);
+        uint32_t lo = 0, hi = nk;  // the node is in [lo, hi)
+        if (sp[g] > p_lo) hi = g;
+        else if (sp[g + 1u] <= p_lo) lo = g + 1u;
+        else { lo = g; hi = g + 1u; }
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
           if (sp[mid] <= p_lo) lo = mid; else hi = mid;
@@ -3303,8 +3329,21 @@ __global__ __launch_bounds__(kBlock) void usage_fast_kernel(UsageArgs a) {
           uint4 kq = kv[0];  // one key dword (4 pods) per step, rotated: 8 values in flight, not 32
           uint32_t qa = m_a, qb = m_b;
           double ac = 0.0, am = 0.0, bc = 0.0, bm = 0.0;
+          // one key over the lane's 16 pods (a lane without pods reads the n = 0 entries): the sums
+          // are s_seq entries; the wave takes the per-pod loop if any lane's keys differ
+          const uint32_t k0 = kq.x & 0xFFu, rep = k0 * 0x01010101u;
+          const bool one = !has || (kq.x == rep && kq.y == rep && kq.z == rep && kq.w == rep && k0 < kUSeqKeys);
+          const int d_end = ballot(!one) ? 4 : 0;  // wave-uniform
+          if (d_end == 0) {
+            const uint32_t ks = has ? k0 : 0u;
+            const double2 sa = s_seq[ks][__popc(m_a)], sb = s_seq[ks][__popc(m_b)];
+            ac = sa.x;
+            am = sa.y;
+            bc = sb.x;
+            bm = sb.y;
+          }
 #pragma unroll 1
-          for (int d = 0; d < 4; ++d) {
+          for (int d = 0; d < d_end; ++d) {
             const uint32_t ka = kq.x | s_nib[qa & 15u], kb = kq.x | s_nib[qb & 15u];
             kq = make_uint4(kq.y, kq.z, kq.w, 0u);
             qa >>= 4;

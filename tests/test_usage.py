@@ -340,6 +340,53 @@ def test_gpu_usage_key8_column_matches_4byte_keys(state):
     np.testing.assert_allclose(total, want.sum(axis=0), rtol=REL_TOL)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("pods_per_node", [100, 37])
+def test_gpu_usage_one_key_runs_match_per_pod_sums(pods_per_node):
+    """usage_fast_kernel<1, true> (1-byte ids, 1-byte keys): where every lane's 16 pods carry one
+    key (< 16 keys, the C5 case) a lane's sums are read from the in-order sums of 0..16 pods of
+    that key, and a lane's first node is found from the chunk's mean node size.  Both must give
+    node sums and integrators bit-identical to the per-pod loop of the 4-byte-key kernel
+    (KWK_TUNE_USAGE_KEY8 0): one column with waves of one-key runs, a mixed stretch, keys >= 16,
+    dead pods and churned ids, 100 pods per node (the C5 shape) and 37 (irregular last node)."""
+    import bench
+    from kwok_amd.host import abi
+    n_nodes = 200_000 // pods_per_node
+    n = n_nodes * pods_per_node
+    ptr = (np.arange(n_nodes + 1, dtype=np.int64) * pods_per_node).astype(np.uint32)
+    ptr[-2] = ptr[-1] - 3  # a short last-but-one node
+    rng = np.random.default_rng(5)
+    cv, mv = rng.random(30) * 3, rng.random(30) * 2**30
+    ci, mi, nc = rng.integers(0, 30, 24), rng.integers(0, 30, 24), rng.integers(1, 5, 24)
+    dict_keys = (ci | (mi << 14) | (nc << 28)).astype(np.uint32)  # 24 distinct keys
+    # blocks of 1024 pods of one key (keys 0..3), a mixed stretch, a stretch of key 20 (>= 16)
+    pick = np.repeat(np.arange(n // 1024 + 1) % 4, 1024)[:n]
+    pick[40_000:42_000] = rng.integers(0, 24, 2000)
+    pick[60_000:70_000] = 20
+    keys = dict_keys[pick]
+    gone = np.arange(3, n, 17)
+    t0 = bench.NOW0 + 10 * 10**9
+    got = {}
+    for key8 in (1, 0):
+        pods, nodes, _ = bench.build_engines(0, n_nodes, pods_per_node, 0, 0x6B776F6B, 0.1)
+        try:
+            assert pods.stats()["state_bytes"] == 1
+            pods.set_tuning(abi.TUNE_USAGE_KEY8, key8)
+            pods.usage_config(ptr, keys, cv, mv)
+            for k in range(3):  # churned ids (pods deleted by the harness read as dead)
+                pods.step(bench.NOW0 + k * 10**9, 1, k)
+            pods.delete(gone)
+            pods.usage(t0)
+            pods.usage(t0 + 2 * 10**9)
+            got[key8] = pods.usage_read()
+        finally:
+            pods.close()
+            nodes.close()
+    assert np.array_equal(got[1][0], got[0][0]) and np.array_equal(got[1][1], got[0][1])
+    node, total = got[1]
+    assert node[:, 0].max() > 0
+    np.testing.assert_allclose(total, node[:, :2].sum(axis=0), rtol=REL_TOL)
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pods_per_node", [100, 7])

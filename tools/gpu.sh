@@ -172,6 +172,15 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
         done
       done
       cp $O/cur.so kwok_amd/lib/libkwok_engine.so && rm -f $O/cur.so ;;
+    abusage)  # same-box A/B of the C5 usage kernel alone (tools/agg_bench.py --usage-only): in-tree engine vs tools/ab/<so>
+      for i in 1 2; do
+        for v in cur other; do
+          L=kwok_amd/lib/libkwok_engine.so; [ $v = other ] && L=tools/ab/$arg
+          timeout -k 10 200 python -u tools/agg_bench.py --usage-only --reps 10 --lib $L > $O/usage_${v}_$i.json 2> $O/usage_${v}_$i.err \
+            || { tail -20 $O/usage_${v}_$i.err; exit 1; }
+          echo "$v $i $(cat $O/usage_${v}_$i.json)"
+        done
+      done ;;
     abemit)  # same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>, alternating x2
       L=kwok_amd/lib/libkwok_emit.so; cp $L $O/cur_emit.so
       for i in 1 2; do
