@@ -308,6 +308,17 @@ def measure_patch_emit(pods, pvars, pidx, args, dt, k0):
                     "HIP events; call values synthetic IPv4 text; parity: tests/test_gpu_emit.py"}
 
 
+def sweep_launches(n_steps, report_every, steps_per_launch):
+    """Pod sweep launches of run_steps' kwk_step_n_pair calls (one per reporting interval): with
+    fused steps (KWK_TUNE_FUSE_STEPS, kwk_sweep_info.steps == 2) a call of n steps launches
+    n // 2 pairs and, for odd n, one single step."""
+    if steps_per_launch < 2:
+        return n_steps
+    sizes = [report_every] * (n_steps // report_every) + ([n_steps % report_every] if n_steps % report_every else []) \
+        if report_every else [n_steps]
+    return sum(n - n // 2 for n in sizes)
+
+
 def sweep_bytes(s0, s1):
     return s1["bytes"] - s0["bytes"], s1["line_bytes"] - s0["line_bytes"]
 
@@ -585,6 +596,9 @@ def main():
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
+    ap.add_argument("--fuse-steps", type=int, default=1, choices=(0, 1),
+                    help="KWK_TUNE_FUSE_STEPS for the pod engine: 1 (default) two steps per 1-byte sweep launch, "
+                         "0 one step per launch")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
@@ -672,6 +686,8 @@ def main():
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_STREAM_PRIORITY, 1)
         nodes.set_tuning(abi.TUNE_STREAM_PRIORITY, 2)
+    from kwok_amd.host import abi
+    pods.set_tuning(abi.TUNE_FUSE_STEPS, args.fuse_steps)
     if args.tune_compact_small >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_COMPACT_SMALL, args.tune_compact_small)
@@ -789,7 +805,9 @@ def main():
     if rank == 0:
         value = total_fired / max_s
         pod_kernel_s = statistics.mean(sweep_ms) / 1e3
-        achieved = (pbytes / args.steps) / pod_kernel_s / 1e9
+        spl = max(1, int(pod_kernel.get("steps", 1)))  # steps per pod sweep launch (2: fused pairs)
+        launches = sweep_launches(args.steps, report_every, spl)
+        achieved = (pbytes / launches) / pod_kernel_s / 1e9
         sb = int(s1p["state_bytes"])
         tr = None if traffic is None else traffic["read"] + traffic["write"]
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -799,11 +817,12 @@ def main():
                                  "per launch" if traffic else f"null: {pmc_err}"),
                 "kernel": SWEEP_NAMES.get(pod_kernel["kernel"], "?") + (" persistent" if pod_kernel["persistent"] else "")
                           + " (pods)",
-                "bytes_per_launch": int(pbytes / args.steps), "state_bytes_per_object": sb,
+                "bytes_per_launch": int(pbytes / launches), "state_bytes_per_object": sb,
+                "steps_per_launch": spl, "launches": launches,
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
-                "line_bytes_per_launch": int(plines / args.steps),
-                "line_frac": round(plines / args.steps / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
+                "line_bytes_per_launch": int(plines / launches),
+                "line_frac": round(plines / launches / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
         if tr:
             roof["traffic_GBps"] = round(tr / pod_kernel_s / 1e9, 1)
         cpu = None

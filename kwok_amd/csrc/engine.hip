@@ -319,6 +319,10 @@ struct SweepArgs {
   uint32_t fold_prev;
   uint32_t* __restrict__ btot_out;          // one-tile sweep8 with 2-byte records: records per workgroup
   const uint32_t* __restrict__ fold_btot;   // ... the previous step's (the fold's prefix)
+  // sweep8_kernel<..., kFuse>: the second step of the launch (its time, segments and counts)
+  kwk_fired_rec* __restrict__ fired2;
+  uint32_t* __restrict__ wave_counts2;
+  int64_t now2;
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -1469,7 +1473,10 @@ __device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, 
 
 // one tile per workgroup (small engines, the strong-scaling shards): 6 workgroups per CU (<= 80
 // VGPRs, 26.8 KB of LDS) so that a 12.5M-id shard's 1526 tiles are one dispatch round, not two
-template <bool kPersist, int kDepth, bool kStages4>
+// kFuse: two steps per launch (a.now, a.now2) for tables without delayed stages — each id is read
+// once, stepped twice in LDS and written once; the first step's records go to a.fired /
+// a.wave_counts, the second's to a.fired2 / a.wave_counts2 (launch_sweep_pair)
+template <bool kPersist, int kDepth, bool kStages4, bool kFuse = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist ? 1 : 6))) void sweep8_kernel(SweepArgs a) {
   constexpr int Q = kQ8;
   constexpr int K = 16 * Q;                // ids per lane
@@ -1478,6 +1485,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   constexpr uint32_t kSeg8 = 64u * K + 32u;
   static_assert(kDepth >= 1 && kDepth <= 2 && (kPersist || kDepth == 1), "prefetch depth");
   static_assert(kWave == 2048 && K == 32, "11-bit record offsets, 32-bit lane masks");
+  static_assert(!kFuse || kStages4, "fused steps hand back 2-byte records");
   __shared__ __attribute__((aligned(2048))) uint32_t s_tile[kWavesPerBlock][4 * Q][64];
   __shared__ __attribute__((aligned(16))) uint16_t s_work[kWavesPerBlock][kWave];
   __shared__ uint32_t s_inv[64];  // kIdInvalid bytes: the inactive lanes' entries (shared by the waves:
@@ -1492,6 +1500,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
   const __amdgpu_buffer_rsrc_t cnt_rs = make_rsrc(a.wave_counts, n_tiles * kWavesPerBlock * 4u);
+  const __amdgpu_buffer_rsrc_t cnt2_rs = make_rsrc(kFuse ? a.wave_counts2 : a.wave_counts, n_tiles * kWavesPerBlock * 4u);
   const __amdgpu_buffer_rsrc_t fold_rs = make_rsrc(a.fold_out, 0x7FFFFFF0u);
   uint4 va[kDepth][Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
@@ -1555,7 +1564,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const bool real = tile < n_tiles;  // wave-uniform
     const uint32_t wbase = tile * kTile + wave * kWave;
     const bool full = (uint64_t)(tile + 1) * kTile <= a.n;
-    uint32_t seg_n = 0;  // wave-uniform
     const uint32_t seg_id = tile * kWavesPerBlock + wave;
     uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + (uint64_t)seg_id * kSeg8;
     const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg8 * 4u);
@@ -1599,108 +1607,180 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
           for (uint32_t b = 0; b < 4; ++b) in_range |= (j * 4u + b < c ? 1u : 0u) << (b * 8u + (uint32_t)q * 4u + j);
       }
     }
-    uint32_t need = 0, pend = 0, ready = 0;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const uint32_t dw[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t jj = (uint32_t)(q * 4 + j);
-        need |= (dw[j] & 0x80808080u) >> (7u - jj);
-        pend |= ((dw[j] << 1) & 0x80808080u) >> (7u - jj);
-      }
-    }
-    need &= in_range;
-    pend &= in_range;
-    if (ballot(pend != 0)) {  // a queued stage: is it due? (4 loads in flight: registers stay low)
-#pragma unroll 4
-      for (int k = 0; k < K; ++k) {
-        const uint32_t p = (pend >> k) & 1u;
-        const uint32_t slot = id8_slot(lds_id8((uint32_t)k, lane4));
-        const int64_t d = buf_load_i64(due_rs, p ? (wbase + slot) * 8u : kOOB);
-        ready |= (p & (uint32_t)(d <= a.now)) << k;
-      }
-      need |= ready;
-    }
-    n_bytes += (uint32_t)__popc(in_range) + 8u * (uint32_t)__popc(pend);
-    uint32_t n_work = 0, pos = 0;
-    {  // exclusive prefix of the lanes' item counts (DPP scan) and the wave's total
-      const uint32_t cnt = (uint32_t)__popc(need);
-      const uint32_t incl = wave_incl_scan(cnt);
-      pos = incl - cnt;
-      n_work = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    }
-    if (n_work) {  // wave-uniform
-      // ---- phase 2: the ids to the LDS tile, the work list (absolute LDS addresses of the ids in
-      // slot order per lane), then one lookup in the id table per item, 64 items per pass
-#pragma unroll
+    // phases 1 and 2 of one step over the wave's ids (registers): the need / pend bits, the due
+    // test at `now`, the work list and the table passes; the step's records staged at the work
+    // list's front (seg_n).  Returns the items worked: the tile is in LDS iff nonzero.  first: the
+    // step that read the ids from HBM (a fused pair's second step adds no read bytes)
+    auto phase12 = [&](const uint4 (&ids)[Q], const int64_t now, const bool first, uint32_t& seg_n)
+                       __attribute__((always_inline)) -> uint32_t {
+      uint32_t need = 0, pend = 0, ready = 0;
+  #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        tw[lds_col8(q * 4 + 0, lane)] = cur[q].x;
-        tw[lds_col8(q * 4 + 1, lane)] = cur[q].y;
-        tw[lds_col8(q * 4 + 2, lane)] = cur[q].z;
-        tw[lds_col8(q * 4 + 3, lane)] = cur[q].w;
-      }
-      const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
-      const bool slow = rdy || any_due;          // ... or due times may be written
-      {
-        // entry = tile_lds | lds_id8(k, lane4) = ent0 ^ lds_id8(k, 0) (lane4 has no bits in
-        // lds_id8's k fields): three ops per item on the per-lane loop, whose trip count is the
-        // most items of any lane
-        uint32_t m = need;
-        uint16_t* wp = wl + pos;
-        const uint32_t ent0 = tile_lds | lane4;
-        if (rdy) {
-          while (m) {
-            const uint32_t k = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            *wp++ = (uint16_t)((ent0 ^ ((k & 7u) * 0x104u | k >> 3)) | ((ready >> k) & 1u) << 15);
-          }
-        } else {
-          while (m) {
-            const uint32_t k = (uint32_t)__builtin_ctz(m);
-            m &= m - 1u;
-            *wp++ = (uint16_t)(ent0 ^ ((k & 7u) * 0x104u | k >> 3));
-          }
+        const uint32_t dw[4] = {ids[q].x, ids[q].y, ids[q].z, ids[q].w};
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t jj = (uint32_t)(q * 4 + j);
+          need |= (dw[j] & 0x80808080u) >> (7u - jj);
+          pend |= ((dw[j] << 1) & 0x80808080u) >> (7u - jj);
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      // the next pass's entries are read while this pass works (an entry past the list: the
-      // lane's kIdInvalid byte)
-      if (slow) {
-        uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : inv_ent;
-        for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
-          const uint32_t we = nwe;
-          if (c + 64u < n_work) {
-            const uint32_t x = (uint32_t)wl[(c + 64u + lane) & (kWave - 1u)];
-            nwe = c + 64u + lane < n_work ? x : inv_ent;
-          }
-          id8_pass<true, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
-                                   fdue_rs, due_rs, wbase, a.now);
+      need &= in_range;
+      pend &= in_range;
+      if (ballot(pend != 0)) {  // a queued stage: is it due? (4 loads in flight: registers stay low)
+  #pragma unroll 4
+        for (int k = 0; k < K; ++k) {
+          const uint32_t p = (pend >> k) & 1u;
+          const uint32_t slot = id8_slot(lds_id8((uint32_t)k, lane4));
+          const int64_t d = buf_load_i64(due_rs, p ? (wbase + slot) * 8u : kOOB);
+          ready |= (p & (uint32_t)(d <= now)) << k;
         }
-      } else {
-        // kId8Batch passes per step (their LDS round trips overlap); the next step's entries are
-        // read while these work (records of passes < c + 64 * kId8Batch land below it)
-        constexpr uint32_t kB = kId8Batch;
-        uint32_t nw[kB];
-#pragma unroll
-        for (uint32_t j = 0; j < kB; ++j) nw[j] = 64u * j + lane < n_work ? (uint32_t)wl[64u * j + lane] : inv_ent;
-        for (uint32_t c = 0; c < n_work; c += 64u * kB) {  // wave-uniform
-          uint32_t we[kB];
-#pragma unroll
-          for (uint32_t j = 0; j < kB; ++j) we[j] = nw[j];
-          if (c + 64u * kB < n_work) {
-#pragma unroll
-            for (uint32_t j = 0; j < kB; ++j) {
-              const uint32_t i = c + 64u * (kB + j) + lane;
-              const uint32_t x = (uint32_t)wl[i & (kWave - 1u)];
-              nw[j] = i < n_work ? x : inv_ent;
+        need |= ready;
+      }
+      n_bytes += (first ? (uint32_t)__popc(in_range) : 0u) + 8u * (uint32_t)__popc(pend);
+      uint32_t n_work = 0, pos = 0;
+      {  // exclusive prefix of the lanes' item counts (DPP scan) and the wave's total
+        const uint32_t cnt = (uint32_t)__popc(need);
+        const uint32_t incl = wave_incl_scan(cnt);
+        pos = incl - cnt;
+        n_work = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+      if (n_work) {  // wave-uniform
+        // ---- phase 2: the ids to the LDS tile, the work list (absolute LDS addresses of the ids in
+        // slot order per lane), then one lookup in the id table per item, 64 items per pass
+  #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          tw[lds_col8(q * 4 + 0, lane)] = ids[q].x;
+          tw[lds_col8(q * 4 + 1, lane)] = ids[q].y;
+          tw[lds_col8(q * 4 + 2, lane)] = ids[q].z;
+          tw[lds_col8(q * 4 + 3, lane)] = ids[q].w;
+        }
+        const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
+        const bool slow = rdy || any_due;          // ... or due times may be written
+        {
+          // entry = tile_lds | lds_id8(k, lane4) = ent0 ^ lds_id8(k, 0) (lane4 has no bits in
+          // lds_id8's k fields): three ops per item on the per-lane loop, whose trip count is the
+          // most items of any lane
+          uint32_t m = need;
+          uint16_t* wp = wl + pos;
+          const uint32_t ent0 = tile_lds | lane4;
+          if (rdy) {
+            while (m) {
+              const uint32_t k = (uint32_t)__builtin_ctz(m);
+              m &= m - 1u;
+              *wp++ = (uint16_t)((ent0 ^ ((k & 7u) * 0x104u | k >> 3)) | ((ready >> k) & 1u) << 15);
+            }
+          } else {
+            while (m) {
+              const uint32_t k = (uint32_t)__builtin_ctz(m);
+              m &= m - 1u;
+              *wp++ = (uint16_t)(ent0 ^ ((k & 7u) * 0x104u | k >> 3));
             }
           }
-          id8_passn<kStages4, kB>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane);
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // the next pass's entries are read while this pass works (an entry past the list: the
+        // lane's kIdInvalid byte)
+        if (slow) {
+          uint32_t nwe = lane < n_work ? (uint32_t)wl[lane] : inv_ent;
+          for (uint32_t c = 0; c < n_work; c += 64u) {  // wave-uniform
+            const uint32_t we = nwe;
+            if (c + 64u < n_work) {
+              const uint32_t x = (uint32_t)wl[(c + 64u + lane) & (kWave - 1u)];
+              nwe = c + 64u + lane < n_work ? x : inv_ent;
+            }
+            id8_pass<true, kStages4>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane, any_due,
+                                     fdue_rs, due_rs, wbase, now);
+          }
+        } else {
+          // kId8Batch passes per step (their LDS round trips overlap); the next step's entries are
+          // read while these work (records of passes < c + 64 * kId8Batch land below it)
+          constexpr uint32_t kB = kId8Batch;
+          uint32_t nw[kB];
+  #pragma unroll
+          for (uint32_t j = 0; j < kB; ++j) nw[j] = 64u * j + lane < n_work ? (uint32_t)wl[64u * j + lane] : inv_ent;
+          for (uint32_t c = 0; c < n_work; c += 64u * kB) {  // wave-uniform
+            uint32_t we[kB];
+  #pragma unroll
+            for (uint32_t j = 0; j < kB; ++j) we[j] = nw[j];
+            if (c + 64u * kB < n_work) {
+  #pragma unroll
+              for (uint32_t j = 0; j < kB; ++j) {
+                const uint32_t i = c + 64u * (kB + j) + lane;
+                const uint32_t x = (uint32_t)wl[i & (kWave - 1u)];
+                nw[j] = i < n_work ? x : inv_ent;
+              }
+            }
+            id8_passn<kStages4, kB>(we, s_fsm, wl, seg_rs, seg_n, n_bytes, n_matched, stc, s_stat, n_stages, lane);
+          }
+        }
+        n_lline -= (uint32_t)__popc(need);  // the ids' own writes are replaced by the line stores below
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       }
-      n_lline -= (uint32_t)__popc(need);  // the ids' own writes are replaced by the line stores below
+      return n_work;
+    };
+    // the step's staged records to its segment (kStages4), the header and the count
+    auto store_records = [&](const __amdgpu_buffer_rsrc_t seg_rs, const __amdgpu_buffer_rsrc_t cnt_rs,
+                             const uint32_t seg_n) __attribute__((always_inline)) {
+      if constexpr (kStages4) {
+        // records: seg_n 2-byte records from the work list, as 16-byte chunks of whole 128-byte
+        // lines (the tail of the last line is padding)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (fold)  // the previous records are in registers before this step's overwrite them
+          asm volatile("" ::"v"(f_v[0]), "v"(f_v[1]), "v"(f_v[2]), "v"(f_v[3]));
+        const uint32_t n_chunks = ((seg_n * 2u + 127u) & ~127u) / 16u;
+        const uint4* wq = reinterpret_cast<const uint4*>(wl);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  #pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+          const uint32_t ci = r * 64u + lane;
+          const uint4 x = wq[ci];
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{x.x, x.y, x.z, x.w}, seg_rs,
+                                                 ci < n_chunks ? kRec16Header + ci * 16u : kOOB, 0, 0);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{seg_n, 0u, 0u, 0u}, seg_rs, lane == 0 && real ? 0u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(seg_n, cnt_rs, lane == 0 && real ? seg_id * 4u : kOOB, 0, 0);
+        if (fold) {  // the previous step's records (a fixed set of eight 2-byte stores)
+  #pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t r = 2u * lane + 128u * j;
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f_v[j], fold_rs, r < f_c ? (f_o + r) * 2u : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(f_v[j] >> 16), fold_rs, r + 1u < f_c ? (f_o + r + 1u) * 2u : kOOB,
+                                                  0, 0);
+          }
+        }
+        if (real) {
+          w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
+          w_bytes += 2u * seg_n + 4u;
+        }
+      } else if (real) {
+        const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
+        for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
+        if (lane == 0) {
+          seg32[0] = seg_n;
+          a.wave_counts[seg_id] = seg_n;
+        }
+        w_line += 4u * (end - used);
+        w_bytes += 4u * seg_n + 4u;
+      }
+      wave_fired += seg_n;
+    };
+    uint32_t seg_n = 0;  // wave-uniform
+    const uint32_t n_work = phase12(cur, a.now, true, seg_n);
+    uint32_t any_work = n_work;
+    uint32_t seg_last = seg_n;
+    if constexpr (kFuse) {
+      // the pair's second step (a.now2) on the ids the first left: its records go to the second
+      // segment set once the first's are out of the work list
+      store_records(seg_rs, cnt_rs, seg_n);
+      uint4 mid[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        mid[q] = n_work ? make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)],
+                                     tw[lds_col8(q * 4 + 2, lane)], tw[lds_col8(q * 4 + 3, lane)])
+                        : cur[q];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      seg_last = 0;
+      any_work |= phase12(mid, a.now2, false, seg_last);
     }
     // ---- phase 3 and the hand-back segment: a fixed set of stores per tile (whole 128-byte lines
     // wherever an id changed, the staged records, the header), each lane's offset out of range
@@ -1711,7 +1791,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       // without work the tile is unchanged: nothing stored (the data is then never written)
       uint4 nv = make_uint4(0u, 0u, 0u, 0u);
       unsigned long long chm = 0;
-      if (n_work) {
+      if (any_work) {
         nv = make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)], tw[lds_col8(q * 4 + 2, lane)],
                         tw[lds_col8(q * 4 + 3, lane)]);
         chm = ballot(nv.x != cur[q].x) | ballot(nv.y != cur[q].y) | ballot(nv.z != cur[q].z) | ballot(nv.w != cur[q].w);
@@ -1722,48 +1802,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
                                              st ? wbase + (uint32_t)q * 1024u + lane * 16u : kOOB, 0, 2 /* nt */);
       n_lline += st ? 16u : 0u;
     }
-    if constexpr (kStages4) {
-      // records: seg_n 2-byte records from the work list, as 16-byte chunks of whole 128-byte
-      // lines (the tail of the last line is padding)
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (fold)  // the previous records are in registers before this step's overwrite them
-        asm volatile("" ::"v"(f_v[0]), "v"(f_v[1]), "v"(f_v[2]), "v"(f_v[3]));
-      const uint32_t n_chunks = ((seg_n * 2u + 127u) & ~127u) / 16u;
-      const uint4* wq = reinterpret_cast<const uint4*>(wl);
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-      for (uint32_t r = 0; r < 4; ++r) {
-        const uint32_t ci = r * 64u + lane;
-        const uint4 x = wq[ci];
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{x.x, x.y, x.z, x.w}, seg_rs,
-                                               ci < n_chunks ? kRec16Header + ci * 16u : kOOB, 0, 0);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{seg_n, 0u, 0u, 0u}, seg_rs, lane == 0 && real ? 0u : kOOB, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(seg_n, cnt_rs, lane == 0 && real ? seg_id * 4u : kOOB, 0, 0);
-      if (fold) {  // the previous step's records (a fixed set of eight 2-byte stores)
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-          const uint32_t r = 2u * lane + 128u * j;
-          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f_v[j], fold_rs, r < f_c ? (f_o + r) * 2u : kOOB, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(f_v[j] >> 16), fold_rs, r + 1u < f_c ? (f_o + r + 1u) * 2u : kOOB,
-                                                0, 0);
-        }
-      }
-      if (real) {
-        w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
-        w_bytes += 2u * seg_n + 4u;
-      }
-    } else if (real) {
-      const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
-      for (uint32_t x = used + lane; x < end; x += 64) seg32[x] = 0u;
-      if (lane == 0) {
-        seg32[0] = seg_n;
-        a.wave_counts[seg_id] = seg_n;
-      }
-      w_line += 4u * (end - used);
-      w_bytes += 4u * seg_n + 4u;
-    }
-    wave_fired += seg_n;
+    if constexpr (kFuse)
+      store_records(make_rsrc(reinterpret_cast<uint32_t*>(a.fired2) + (uint64_t)seg_id * kSeg8, kSeg8 * 4u), cnt2_rs, seg_last);
+    else
+      store_records(seg_rs, cnt_rs, seg_last);
     if constexpr (kStages4) {
       stc[1] += stc[0] & 0x00FF00FFu;
       stc[2] += (stc[0] >> 8) & 0x00FF00FFu;
@@ -2169,8 +2211,9 @@ __global__ __launch_bounds__(kBlock, kDW ? kDwMinBlocks : 1) void sweepw_kernel(
 // look-back was measured slower here: with ~12k tiny blocks the look-back chains, not the bytes,
 // set the time — 165 us vs the ~30 us the bytes need.)
 constexpr uint32_t kPackedSlots = 1u << 27;                // packed fired records: 27-bit slots
-constexpr uint32_t kScanPer = 16;                         // counts per thread
-constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 4096 counts per group (one workgroup)
+constexpr uint32_t kScanPer = 4;                          // counts per thread (16: 4096-count groups, 12 workgroups
+                                                          // at C5 for ~5 us; 4: 48 shorter ones)
+constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 1024 counts per group (one workgroup)
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
 
 // offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records
@@ -4026,11 +4069,20 @@ __global__ __launch_bounds__(1024) void agg_final_kernel(const uint32_t* __restr
   // 3 + stage, without its launch)
   if (t < KWK_MAX_STAGES) s_st[t] = 0;
   __syncthreads();
-  for (uint32_t st = 0; st < n_stages; ++st) {  // uniform
-    unsigned long long v = 0;
-    for (uint32_t r = t; r < cum_rows; r += blockDim.x) v += cum[(uint64_t)r * kStatWords + 3 + st];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((t & 63) == 0 && v) atomicAdd(&s_st[st], v);
+  for (uint32_t s0 = 0; s0 < n_stages; s0 += 8) {  // uniform: up to 8 stages' words of a row in one pass
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t r = t; r < cum_rows; r += blockDim.x) {
+      const unsigned long long* __restrict__ row = cum + (uint64_t)r * kStatWords + 3 + s0;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j)
+        if (s0 + j < n_stages) v[j] += row[j];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      if (s0 + j >= n_stages) break;
+      for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
+      if ((t & 63) == 0 && v[j]) atomicAdd(&s_st[s0 + j], v[j]);
+    }
   }
   if (n_cblocks) count_total_block(cpart, n_cblocks, n_masks, counts, s);
   // usage: 1 = sum the usage kernel's partials, 2 = no usage kernel ran (no nodes): pack the
@@ -4320,6 +4372,11 @@ struct kwk_engine {
   bool fold_pending = false;
   bool fold_valid = false;     // d_fold holds the list of the step before the last (kwk_fired_fold16)
   uint16_t* d_fold = nullptr;
+  // two steps per sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kFuse>): the second step's
+  // segments and counts, swapped with d_fired / d_wave_counts after the first step's hand-back
+  bool fuse_steps = true;
+  kwk_fired_rec* d_fired2 = nullptr;
+  uint32_t* d_wave_counts2 = nullptr;
   uint32_t* d_fold_n = nullptr;
   uint32_t* d_counts_prev = nullptr;
   uint32_t* d_btot = nullptr;       // records per workgroup of the last one-tile sweep8 (2-byte records)
@@ -4877,7 +4934,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_fired2, e->d_wave_counts2, e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -5062,6 +5119,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
     case KWK_TUNE_FOLD_HB:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FOLD_HB: 0 or 1");
       e->fold_hb = value != 0;
+      return KWK_OK;
+    case KWK_TUNE_FUSE_STEPS:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 or 1");
+      e->fuse_steps = value != 0;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -5362,13 +5423,16 @@ static kwk_status build_fsm(kwk_engine* e) {
   return KWK_OK;
 }
 
-static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire) {
+// fuse: the 1-byte sweep takes two steps (now_ns, now2_ns) in one launch (fusable(); the second
+// step's segments and counts go to d_fired2 / d_wave_counts2)
+static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire,
+                               bool fuse = false, int64_t now2_ns = 0) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   e->compacted = false;
   e->last_sweep = kwk_sweep_info{};
   if (!e->fold_now) e->fold_valid = false;  // d_fold no longer holds the list before the last
-  if (e->n_active == 0) { e->last_blocks = 0; ++e->steps; return KWK_OK; }
+  if (e->n_active == 0) { e->last_blocks = 0; e->steps += fuse ? 2u : 1u; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
   const bool h = a.harness.enable != 0;
@@ -5389,7 +5453,15 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const uint32_t tiles = (e->n_active + tile - 1) / tile;
     const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
 
-#define K8(P, D) (s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
+    if (fuse) {
+      if (!s4 || !e->d_fired2) return fail(KWK_ESTATE, "fused steps: 1-byte sweep with <= 4 stages and its buffers");
+      a.fired2 = e->d_fired2;
+      a.wave_counts2 = e->d_wave_counts2;
+      a.now2 = now2_ns;
+    }
+#define K8(P, D)                                                                                        \
+  (fuse ? (const void*)sweep8_kernel<P, D, true, true>                                                 \
+        : s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
 
@@ -5413,7 +5485,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     e->last_blocks = tiles;
     e->last_grid = blocks;
     e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
-    ++e->steps;
+    e->last_sweep.steps = fuse ? 2u : 1u;
+    e->steps += fuse ? 2u : 1u;
     return KWK_OK;
   }
   if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
@@ -5792,6 +5865,45 @@ static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t s
   return enqueue_compact(e, compact_mode(compact));
 }
 
+// two steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no due
+// time (objects then step independently of the clock except through due times already queued,
+// which the second step tests at its own now) and whose records are the 2-byte ones
+static bool fusable(const kwk_engine* e, uint32_t ev_every) {
+  return e->fuse_steps && e->fmt.byte && e->n_stages <= 4 && !e->fsm8_due_any && e->loaded_table && !e->fold_pending &&
+         ev_every != 1;
+}
+
+// steps k (now) and k + 1 (now + dt) of kwk_step_n / _pair in one launch, then each step's
+// hand-back in turn: the first step's from d_fired, then (buffers swapped) the second's, which
+// stays the engine's last step; ev_a brackets the launch (the sample of either step)
+static kwk_status step_pair(kwk_engine* e, int64_t now, int64_t dt, uint64_t seed, uint64_t step, uint32_t compact,
+                            int ev_a) {
+  if (!e->d_fired2) {
+    const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
+    HIP_TRY(hipMalloc((void**)&e->d_fired2, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
+                                                                      (size_t)kBlock * kMaxObjPerThread)));
+    HIP_TRY(hipMalloc((void**)&e->d_wave_counts2, sizeof(uint32_t) * (n_waves + 4)));
+  }
+  if (ev_a >= 0)
+    if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
+  if (kwk_status st = launch_sweep(e, now, seed, step, true, true, now + dt)) return st;
+  if (ev_a >= 0)
+    if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
+  if (compact)
+    if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+  std::swap(e->d_fired, e->d_fired2);
+  std::swap(e->d_wave_counts, e->d_wave_counts2);
+  e->compacted = false;
+  if (compact)
+    if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+  return KWK_OK;
+}
+
+// the event sample of step j (ev_every > 0), or -1
+static int ev_of(uint32_t ev_every, uint32_t j) {
+  return ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
+}
+
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0) {
   ErrScope es_(e);
@@ -5799,11 +5911,18 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
   if (compact == KWK_COMPACT_PACKED || compact == KWK_COMPACT_PACKED16)
     if (kwk_status st = packed_ok(e)) return st;
   if (kwk_status st = set_dev(e)) return st;
-  for (uint32_t k = 0; k < n; ++k) {
+  for (uint32_t k = 0; k < n;) {
     const uint32_t j = ev_j0 + k;
-    const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
-    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev, true, k + 1 == n))
+    if (k + 1 < n && fusable(e, ev_every)) {
+      const int ev = ev_of(ev_every, j) >= 0 ? ev_of(ev_every, j) : ev_of(ev_every, j + 1);
+      if (kwk_status st = step_pair(e, now0_ns + (int64_t)k * dt_ns, dt_ns, seed, step0 + k, compact, ev)) return st;
+      k += 2;
+      continue;
+    }
+    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev_of(ev_every, j), true,
+                                 k + 1 == n))
       return st;
+    ++k;
   }
   return KWK_OK;
 }
@@ -5819,13 +5938,22 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
     if (other->capacity > kPackedSlots) return fail(KWK_ECAP, "packed fired records hold 27-bit slots: other engine > 2^27");
   }
   if (kwk_status st = set_dev(e)) return st;
-  for (uint32_t k = 0; k < n; ++k) {
+  for (uint32_t k = 0; k < n;) {
     const uint32_t j = ev_j0 + k;
-    const int ev = ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
     const int64_t now = now0_ns + (int64_t)k * dt_ns;
-    if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev, true, k + 1 == n)) return st;
-    // the other engine's step right behind (its own stream): both chains start together
-    if (kwk_status st = step_one(other, now, seed, step0 + k, compact, -1, true, k + 1 == n)) return st;
+    // a fused pair of the first engine, the other's two steps right behind (its own stream)
+    const uint32_t m = k + 1 < n && fusable(e, ev_every) ? 2u : 1u;
+    if (m == 2) {
+      const int ev = ev_of(ev_every, j) >= 0 ? ev_of(ev_every, j) : ev_of(ev_every, j + 1);
+      if (kwk_status st = step_pair(e, now, dt_ns, seed, step0 + k, compact, ev)) return st;
+    } else if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev_of(ev_every, j), true, k + 1 == n)) {
+      return st;
+    }
+    // the other engine's step(s) right behind (its own stream): both chains start together
+    for (uint32_t i = 0; i < m; ++i)
+      if (kwk_status st = step_one(other, now + (int64_t)i * dt_ns, seed, step0 + k + i, compact, -1, true, k + i + 1 == n))
+        return st;
+    k += m;
   }
   return KWK_OK;
 }

@@ -83,7 +83,7 @@ class FetchInfo(C.Structure):
 
 
 class SweepInfo(C.Structure):
-    _fields_ = [(k, C.c_uint32) for k in ("kernel", "q", "persistent", "depth", "grid", "tiles", "harness", "reserved")]
+    _fields_ = [(k, C.c_uint32) for k in ("kernel", "q", "persistent", "depth", "grid", "tiles", "harness", "steps")]
 
 
 SWEEP_16, SWEEP_16_FSM, SWEEP_W4, SWEEP_W8, SWEEP_8, SWEEP_WD = 1, 2, 3, 4, 5, 6  # KWK_SWEEP_*
@@ -106,6 +106,7 @@ TUNE_WORD_TILES = 10
 TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15
 TUNE_FOLD_HB = 16
+TUNE_FUSE_STEPS = 17
 
 
 class Lease(C.Structure):

@@ -368,7 +368,10 @@ def test_step_n_equals_per_step_calls():
     """kwk_step_n (the bench's per-interval call) enqueues exactly the per-tick kwk_step +
     kwk_fired_compact sequence: same states, statistics and last fired list, with and without
     the event samples."""
-    engines = {name: _pods("auto", n_nodes=20_000)[1] for name in ("calls", "n", "n_ev")}
+    from kwok_amd.host import abi
+    unfused = {abi.TUNE_FUSE_STEPS: 0}  # one step per launch (the fused pairs: the test below)
+    engines = {name: _pods("auto", n_nodes=20_000, tuning=None if name == "calls" else unfused)[1]
+               for name in ("calls", "n", "n_ev")}
     try:
         now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
         for k in range(7):
@@ -393,6 +396,93 @@ def test_step_n_equals_per_step_calls():
     finally:
         for e in engines.values():
             e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes", [20_000, 250_000])
+def test_fused_step_pairs_equal_per_step_calls(n_nodes):
+    """KWK_TUNE_FUSE_STEPS (default on): kwk_step_n sweeps the 1-byte ids two steps per launch
+    (sweep8_kernel<..., kFuse>: each id read once, stepped twice in LDS, written once; each step's
+    records to its own segments, each hand-back in turn).  States, the last fired list, the fired /
+    matched / per-stage counts and the step count must equal the per-step kwk_step +
+    kwk_fired_compact calls — one-tile grid (2M pods) and persistent grid (25M pods), pairs and a
+    trailing single step, with event samples; the fused launch reads and writes the ids once."""
+    from kwok_amd.host import abi
+    engines = {"calls": _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 0})[1]}
+    engines["fused"] = _pods("auto", n_nodes=n_nodes)[1]
+    engines["fused_ev"] = _pods("auto", n_nodes=n_nodes)[1]
+    try:
+        now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
+        ref = engines["calls"]
+        for k in range(7):
+            ref.step(now0 + k * dt, seed, k)
+            ref.fired_compact()
+        assert ref.last_sweep()["kernel"] == abi.SWEEP_8
+        f = engines["fused"]
+        f.step_n(3, now0, dt, seed, 0)
+        f.step_n(4, now0 + 3 * dt, dt, seed, 3)
+        assert f.last_sweep()["steps"] == 2  # the call's last two steps: one launch
+        engines["fused_ev"].step_n(7, now0, dt, seed, 0, True, 2, 0)
+        assert engines["fused_ev"].last_sweep()["steps"] == 1  # 3 pairs, then step 6 alone
+        r_hot, _ = ref.read()
+        r_fired = _fired_key(ref.fired())
+        r_st = ref.stats()
+        assert len(r_fired) > 0
+        for name in ("fused", "fused_ev"):
+            e = engines[name]
+            hot, _ = e.read()
+            for col in ("pred", "sched"):
+                assert np.array_equal(hot[col], r_hot[col]), (name, col)
+            assert np.array_equal(_fired_key(e.fired()), r_fired), name
+            st = e.stats()
+            for key in ("fired", "matched", "steps", "fired_per_stage"):
+                assert st[key] == r_st[key], (name, key)
+            assert st["bytes"] < r_st["bytes"]  # the pairs read and write each id once
+        assert engines["fused_ev"].event_elapsed_ms(4, 5) > 0.0  # sample 2 = the launch of steps 4-5
+    finally:
+        for e in engines.values():
+            e.close()
+
+
+@pytest.mark.gpu
+def test_fused_step_n_pair_equals_per_step_calls():
+    """The bench's call, kwk_step_n_pair, with the pod engine's steps fused in pairs and the node
+    engine's stepped one by one behind each pair: both engines' states, last fired lists (2-byte
+    pod records with their segment counts, 4-byte node records) and counts equal the per-step
+    calls, for an odd step count (a trailing single pod step)."""
+    import bench
+    from kwok_amd.host import abi
+    now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
+    runs = {}
+    for mode in ("calls", "pair"):
+        pods, nodes, _ = bench.build_engines(0, 20_000, PPN, 0, seed, 0.1)
+        try:
+            assert pods.stats()["state_bytes"] == 1
+            if mode == "calls":
+                pods.set_tuning(abi.TUNE_FUSE_STEPS, 0)
+                for k in range(9):
+                    pods.step(now0 + k * dt, seed, k)
+                    pods.fired_compact("16")
+                    nodes.step(now0 + k * dt, seed, k)
+                    nodes.fired_compact(True)
+            else:
+                pods.step_n_pair(nodes, 4, now0, dt, seed, 0, "packed16")
+                pods.step_n_pair(nodes, 5, now0 + 4 * dt, dt, seed, 4, "packed16")
+                assert pods.last_sweep()["steps"] == 1
+            recs, segc, _ = pods.fired_packed16()
+            runs[mode] = (pods.read()[0], nodes.read()[0], recs, segc, nodes.fired_packed(), pods.stats(), nodes.stats())
+        finally:
+            pods.close()
+            nodes.close()
+    a, b = runs["calls"], runs["pair"]
+    for i in (0, 1):
+        for col in ("pred", "sched"):
+            assert np.array_equal(a[i][col], b[i][col]), (i, col)
+    assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3]) and len(a[2]) > 0
+    assert np.array_equal(np.sort(a[4]), np.sort(b[4]))
+    for i in (5, 6):
+        for key in ("fired", "matched", "steps", "fired_per_stage"):
+            assert a[i][key] == b[i][key], (i, key)
 
 
 def test_fetch_async_equals_sync_readback():
@@ -460,8 +550,9 @@ def test_folded_handback_equals_compacted_list():
     KWK_TUNE_FOLD_HB = 0."""
     from kwok_amd.host import abi
     now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
-    (_, a), (_, b), (_, c) = (_pods("auto", n_nodes=20_000), _pods("auto", n_nodes=20_000),
-                              _pods("auto", n_nodes=20_000, tuning={abi.TUNE_FOLD_HB: 0}))
+    one = {abi.TUNE_FUSE_STEPS: 0}  # one step per launch: the fold is the unfused steps' hand-back
+    (_, a), (_, b), (_, c) = (_pods("auto", n_nodes=20_000, tuning=one), _pods("auto", n_nodes=20_000, tuning=one),
+                              _pods("auto", n_nodes=20_000, tuning={abi.TUNE_FOLD_HB: 0, **one}))
     try:
         ref = []
         for k in range(5):
