@@ -308,15 +308,22 @@ def measure_patch_emit(pods, pvars, pidx, args, dt, k0):
                     "HIP events; call values synthetic IPv4 text; parity: tests/test_gpu_emit.py"}
 
 
-def sweep_launches(n_steps, report_every, steps_per_launch):
+def sweep_launches(n_steps, report_every, fuse_max):
     """Pod sweep launches of run_steps' kwk_step_n_pair calls (one per reporting interval): with
-    fused steps (KWK_TUNE_FUSE_STEPS, kwk_sweep_info.steps == 2) a call of n steps launches
-    n // 2 pairs and, for odd n, one single step."""
-    if steps_per_launch < 2:
-        return n_steps
+    fused steps (KWK_TUNE_FUSE_STEPS) the host takes 4, 2 or 1 steps per launch, the most the
+    call's steps left allow (the HIP event samples, every EV_EVERY >= 4 steps, are never two in
+    one launch)."""
     sizes = [report_every] * (n_steps // report_every) + ([n_steps % report_every] if n_steps % report_every else []) \
         if report_every else [n_steps]
-    return sum(n - n // 2 for n in sizes)
+    launches = 0
+    for n in sizes:
+        while n:
+            m = fuse_max if fuse_max >= 2 else 1
+            while m > n:
+                m >>= 1
+            launches += 1
+            n -= m
+    return launches
 
 
 def sweep_bytes(s0, s1):
@@ -596,9 +603,9 @@ def main():
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
-    ap.add_argument("--fuse-steps", type=int, default=1, choices=(0, 1),
-                    help="KWK_TUNE_FUSE_STEPS for the pod engine: 1 (default) two steps per 1-byte sweep launch, "
-                         "0 one step per launch")
+    ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4),
+                    help="KWK_TUNE_FUSE_STEPS for the pod engine: up to 4 (default) or 2 steps per 1-byte sweep "
+                         "launch, 0 / 1 one step per launch")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
@@ -805,8 +812,9 @@ def main():
     if rank == 0:
         value = total_fired / max_s
         pod_kernel_s = statistics.mean(sweep_ms) / 1e3
-        spl = max(1, int(pod_kernel.get("steps", 1)))  # steps per pod sweep launch (2: fused pairs)
-        launches = sweep_launches(args.steps, report_every, spl)
+        fuse_max = args.fuse_steps if pod_kernel["steps"] > 1 else 1  # the last launch fused: the engine fuses
+        launches = sweep_launches(args.steps, report_every, fuse_max)
+        spl = args.steps / launches  # steps per pod sweep launch (mean)
         achieved = (pbytes / launches) / pod_kernel_s / 1e9
         sb = int(s1p["state_bytes"])
         tr = None if traffic is None else traffic["read"] + traffic["write"]
@@ -818,7 +826,10 @@ def main():
                 "kernel": SWEEP_NAMES.get(pod_kernel["kernel"], "?") + (" persistent" if pod_kernel["persistent"] else "")
                           + " (pods)",
                 "bytes_per_launch": int(pbytes / launches), "state_bytes_per_object": sb,
-                "steps_per_launch": spl, "launches": launches,
+                "steps_per_launch": round(spl, 3), "launches": launches,
+                "launch_note": "bytes per launch = the timed region's pod sweep bytes / its launches (fused launches of "
+                               "4 and 2 steps averaged); avg_launch_us = the sampled launches (the first of each "
+                               "reporting interval: 4 steps when fused), so `achieved` understates a 4-step launch's",
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
                 "line_bytes_per_launch": int(plines / launches),

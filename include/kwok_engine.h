@@ -233,9 +233,9 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_FOLD_HB 16    /* kwk_step_n / _pair with KWK_COMPACT_PACKED16 on small 1-byte engines: a step's
                                   2-byte hand-back copied by the next step's sweep (kwk_fired_fold16), 1
                                   (default) or 0 (the hand-back launched after every step) */
-#define KWK_TUNE_FUSE_STEPS 17 /* kwk_step_n / _pair on 1-byte engines with <= 4 stages and no delayed stage: two
-                                  steps per sweep launch (each id read once, stepped twice in LDS, written once;
-                                  each step's fired records and hand-back kept apart), 1 (default) or 0 (one step
+#define KWK_TUNE_FUSE_STEPS 17 /* kwk_step_n / _pair on 1-byte engines with <= 4 stages and no delayed stage: up to
+                                  4 (default) or 2 steps per sweep launch (each id read once, stepped in LDS,
+                                  written once; each step's fired records and hand-back kept apart), or 0 / 1 (one step
                                   per launch).  Results are bit-identical; kwk_step_stats.bytes / line_bytes count
                                   the fused launch's own reads and writes */
 kwk_status kwk_set_tuning(kwk_engine* eng, uint32_t key, uint32_t value);
@@ -648,7 +648,7 @@ typedef struct {
   uint32_t grid;         /* workgroups launched */
   uint32_t tiles;        /* tiles swept */
   uint32_t harness;      /* 1: the harness variant */
-  uint32_t steps;        /* steps the launch swept: 2 for a fused pair (KWK_TUNE_FUSE_STEPS), else 1 (0: unset) */
+  uint32_t steps;        /* steps the launch swept: 2 or 4 when fused (KWK_TUNE_FUSE_STEPS), else 1 (0: unset) */
 } kwk_sweep_info;
 kwk_status kwk_last_sweep(kwk_engine* eng, kwk_sweep_info* out);
 uint32_t kwk_abi_version(void);

@@ -279,6 +279,7 @@ struct RawTest {
   uint32_t term, del;  // harness: terminal phase bits / deletionTimestamp bit (pred)
 };
 
+constexpr uint32_t kMaxFuseSteps = 4;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS)
 struct SweepArgs {
   void* __restrict__ st;         // per object state word (StateFmt: uint2 {pred, sched} or packed u32)
   int64_t* __restrict__ due;     // per object due time (read only for objects with a pending stage)
@@ -319,10 +320,10 @@ struct SweepArgs {
   uint32_t fold_prev;
   uint32_t* __restrict__ btot_out;          // one-tile sweep8 with 2-byte records: records per workgroup
   const uint32_t* __restrict__ fold_btot;   // ... the previous step's (the fold's prefix)
-  // sweep8_kernel<..., kFuse>: the second step of the launch (its time, segments and counts)
-  kwk_fired_rec* __restrict__ fired2;
-  uint32_t* __restrict__ wave_counts2;
-  int64_t now2;
+  // sweep8_kernel<..., kSteps>: steps 1 .. kSteps - 1 of the launch (their times, segments and counts)
+  kwk_fired_rec* __restrict__ firedx[kMaxFuseSteps - 1];
+  uint32_t* __restrict__ countsx[kMaxFuseSteps - 1];
+  int64_t nowx[kMaxFuseSteps - 1];
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -1473,10 +1474,10 @@ __device__ __forceinline__ void id8_fire(const uint32_t addr, const uint32_t e, 
 
 // one tile per workgroup (small engines, the strong-scaling shards): 6 workgroups per CU (<= 80
 // VGPRs, 26.8 KB of LDS) so that a 12.5M-id shard's 1526 tiles are one dispatch round, not two
-// kFuse: two steps per launch (a.now, a.now2) for tables without delayed stages — each id is read
-// once, stepped twice in LDS and written once; the first step's records go to a.fired /
-// a.wave_counts, the second's to a.fired2 / a.wave_counts2 (launch_sweep_pair)
-template <bool kPersist, int kDepth, bool kStages4, bool kFuse = false>
+// kSteps > 1: fused steps (a.now, then a.nowx[s - 1] for step s) for tables without delayed
+// stages — each id is read once, stepped kSteps times in LDS and written once; step 0's records go
+// to a.fired / a.wave_counts, step s's to a.firedx / a.countsx[s - 1] (step_group)
+template <bool kPersist, int kDepth, bool kStages4, int kSteps = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist ? 1 : 6))) void sweep8_kernel(SweepArgs a) {
   constexpr int Q = kQ8;
   constexpr int K = 16 * Q;                // ids per lane
@@ -1485,7 +1486,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   constexpr uint32_t kSeg8 = 64u * K + 32u;
   static_assert(kDepth >= 1 && kDepth <= 2 && (kPersist || kDepth == 1), "prefetch depth");
   static_assert(kWave == 2048 && K == 32, "11-bit record offsets, 32-bit lane masks");
-  static_assert(!kFuse || kStages4, "fused steps hand back 2-byte records");
+  static_assert((kSteps == 1 || kStages4) && kSteps >= 1 && kSteps <= (int)kMaxFuseSteps,
+                "fused steps hand back 2-byte records");
   __shared__ __attribute__((aligned(2048))) uint32_t s_tile[kWavesPerBlock][4 * Q][64];
   __shared__ __attribute__((aligned(16))) uint16_t s_work[kWavesPerBlock][kWave];
   __shared__ uint32_t s_inv[64];  // kIdInvalid bytes: the inactive lanes' entries (shared by the waves:
@@ -1500,7 +1502,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
   const __amdgpu_buffer_rsrc_t cnt_rs = make_rsrc(a.wave_counts, n_tiles * kWavesPerBlock * 4u);
-  const __amdgpu_buffer_rsrc_t cnt2_rs = make_rsrc(kFuse ? a.wave_counts2 : a.wave_counts, n_tiles * kWavesPerBlock * 4u);
   const __amdgpu_buffer_rsrc_t fold_rs = make_rsrc(a.fold_out, 0x7FFFFFF0u);
   uint4 va[kDepth][Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
@@ -1768,19 +1769,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const uint32_t n_work = phase12(cur, a.now, true, seg_n);
     uint32_t any_work = n_work;
     uint32_t seg_last = seg_n;
-    if constexpr (kFuse) {
-      // the pair's second step (a.now2) on the ids the first left: its records go to the second
-      // segment set once the first's are out of the work list
-      store_records(seg_rs, cnt_rs, seg_n);
+#pragma unroll
+    for (int st = 1; st < kSteps; ++st) {
+      // step st (a.nowx[st - 1]) on the ids the steps before left: the previous step's records go
+      // to its segment first (they sit in the work list the next list overwrites)
+      const uint32_t* px = reinterpret_cast<const uint32_t*>(st == 1 ? a.fired : a.firedx[st - 2]);
+      store_records(make_rsrc(px + (uint64_t)seg_id * kSeg8, kSeg8 * 4u),
+                    make_rsrc(st == 1 ? a.wave_counts : a.countsx[st - 2], n_tiles * kWavesPerBlock * 4u), seg_last);
       uint4 mid[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        mid[q] = n_work ? make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)],
-                                     tw[lds_col8(q * 4 + 2, lane)], tw[lds_col8(q * 4 + 3, lane)])
-                        : cur[q];
+        mid[q] = any_work ? make_uint4(tw[lds_col8(q * 4 + 0, lane)], tw[lds_col8(q * 4 + 1, lane)],
+                                       tw[lds_col8(q * 4 + 2, lane)], tw[lds_col8(q * 4 + 3, lane)])
+                          : cur[q];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       seg_last = 0;
-      any_work |= phase12(mid, a.now2, false, seg_last);
+      any_work |= phase12(mid, a.nowx[st - 1], false, seg_last);
     }
     // ---- phase 3 and the hand-back segment: a fixed set of stores per tile (whole 128-byte lines
     // wherever an id changed, the staged records, the header), each lane's offset out of range
@@ -1802,8 +1806,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
                                              st ? wbase + (uint32_t)q * 1024u + lane * 16u : kOOB, 0, 2 /* nt */);
       n_lline += st ? 16u : 0u;
     }
-    if constexpr (kFuse)
-      store_records(make_rsrc(reinterpret_cast<uint32_t*>(a.fired2) + (uint64_t)seg_id * kSeg8, kSeg8 * 4u), cnt2_rs, seg_last);
+    if constexpr (kSteps > 1)
+      store_records(make_rsrc(reinterpret_cast<const uint32_t*>(a.firedx[kSteps - 2]) + (uint64_t)seg_id * kSeg8, kSeg8 * 4u),
+                    make_rsrc(a.countsx[kSteps - 2], n_tiles * kWavesPerBlock * 4u), seg_last);
     else
       store_records(seg_rs, cnt_rs, seg_last);
     if constexpr (kStages4) {
@@ -2217,12 +2222,12 @@ constexpr uint32_t kScanGroup = kBlock * kScanPer;        // 1024 counts per gro
 constexpr uint32_t kSegsPerBlock = kWavesPerBlock;        // one wave per segment
 
 // offsets[1 + i] = records before segment i within its group, group_tot[g] = the group's records
-__global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
-                                                         uint32_t* __restrict__ offsets,
-                                                         uint32_t* __restrict__ group_tot) {
+__device__ __forceinline__ void seg_scan_block(const uint32_t* __restrict__ counts, uint32_t n,
+                                               uint32_t* __restrict__ offsets, uint32_t* __restrict__ group_tot,
+                                               const uint32_t block) {
   __shared__ uint32_t s_wave[kWavesPerBlock];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint32_t i0 = blockIdx.x * kScanGroup + t * kScanPer;
+  const uint32_t i0 = block * kScanGroup + t * kScanPer;
   uint32_t v[kScanPer];
 #pragma unroll
   for (uint32_t q = 0; q < kScanPer / 4; ++q) {
@@ -2257,7 +2262,12 @@ __global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __rest
     if (i0 + j < n) offsets[1 + i0 + j] = run;
     run += v[j];
   }
-  if (t == kBlock - 1) group_tot[blockIdx.x] = run;
+  if (t == kBlock - 1) group_tot[block] = run;
+}
+__global__ __launch_bounds__(kBlock) void seg_scan_kernel(const uint32_t* __restrict__ counts, uint32_t n,
+                                                         uint32_t* __restrict__ offsets,
+                                                         uint32_t* __restrict__ group_tot) {
+  seg_scan_block(counts, n, offsets, group_tot, blockIdx.x);
 }
 
 struct CompactArgs {
@@ -2271,6 +2281,14 @@ struct CompactArgs {
   uint32_t region_slots;                  // object slots per region (wave / tile)
   uint32_t stride;
 };
+// the hand-backs of a fused launch's steps in one launch each (blockIdx.y = the step)
+struct CompactArgs4 {
+  CompactArgs a[kMaxFuseSteps];
+};
+__global__ __launch_bounds__(kBlock) void seg_scan_multi_kernel(CompactArgs4 m) {
+  const CompactArgs& a = m.a[blockIdx.y];
+  seg_scan_block(a.counts, a.n_segs, a.offsets, const_cast<uint32_t*>(a.group_tot), blockIdx.x);
+}
 
 // record kinds: 4-byte {slot within the region: 13, stage: 5, flags: 3} after the count word;
 // the 1-byte sweep's 4-byte records with an LDS offset in the slot field (id8_slot); its 2-byte
@@ -2360,10 +2378,10 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // {LDS offset: 11, stage: 2, flags: 3} copied as they are into one dense list at their segment's
 // offset; the host maps a record to its slot with its segment's region (KWK_FIRED16_SLOT)
 template <uint32_t kSpw>
-__global__ __launch_bounds__(kBlock) void compact16_kernel(CompactArgs a) {
+__device__ __forceinline__ void compact16_block(const CompactArgs& a, const uint32_t block) {
   static_assert(kScanGroup % (kSpw * kWavesPerBlock) == 0, "a wave's segments lie in one scan group");
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t seg0 = (blockIdx.x * kWavesPerBlock + wave) * kSpw;
+  const uint32_t seg0 = (block * kWavesPerBlock + wave) * kSpw;
   if (seg0 >= a.n_segs) return;
   uint32_t c[kSpw], o1[kSpw];
   uint16_t r[kSpw][4];
@@ -2393,13 +2411,21 @@ __global__ __launch_bounds__(kBlock) void compact16_kernel(CompactArgs a) {
     for (uint32_t j = lane + 256u; j < c[s]; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
   }
 }
+template <uint32_t kSpw>
+__global__ __launch_bounds__(kBlock) void compact16_kernel(CompactArgs a) {
+  compact16_block<kSpw>(a, blockIdx.x);
+}
+template <uint32_t kSpw>
+__global__ __launch_bounds__(kBlock) void compact16_multi_kernel(CompactArgs4 m) {
+  compact16_block<kSpw>(m.a[blockIdx.y], blockIdx.x);
+}
 
 // the 2-byte hand-back in one launch for small sweeps (as compact_small_kernel below)
-__global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) {
+__device__ __forceinline__ void compact16_small_block(const CompactArgs& a, const uint32_t block) {
   __shared__ uint32_t s_part[kWavesPerBlock];
   __shared__ uint32_t s_seg[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t first = blockIdx.x * kSegsPerBlock;
+  const uint32_t first = block * kSegsPerBlock;
   const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(a.counts);
   uint32_t sum = 0;
 #pragma unroll 8
@@ -2420,6 +2446,10 @@ __global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) 
   const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
   for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
+}
+__global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) { compact16_small_block(a, blockIdx.x); }
+__global__ __launch_bounds__(kBlock) void compact16_small_multi_kernel(CompactArgs4 m) {
+  compact16_small_block(m.a[blockIdx.y], blockIdx.x);
 }
 
 // The bitmap hand-back (kwk_fired_compact_bits): the 1-byte sweep's <= 4-stage records as one
@@ -4372,11 +4402,16 @@ struct kwk_engine {
   bool fold_pending = false;
   bool fold_valid = false;     // d_fold holds the list of the step before the last (kwk_fired_fold16)
   uint16_t* d_fold = nullptr;
-  // two steps per sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kFuse>): the second step's
-  // segments and counts, swapped with d_fired / d_wave_counts after the first step's hand-back
-  bool fuse_steps = true;
-  kwk_fired_rec* d_fired2 = nullptr;
-  uint32_t* d_wave_counts2 = nullptr;
+  // up to fuse_steps steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kSteps>):
+  // steps 1.. segments and counts, rotated with d_fired / d_wave_counts by the steps' hand-backs
+  uint32_t fuse_steps = kMaxFuseSteps;
+  kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
+  uint32_t* d_countsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
+  // ... and the 2-byte hand-backs of all but the group's last step (one launch for the group):
+  // their lists, offsets and scan-group totals
+  uint16_t* d_listx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
+  uint32_t* d_offsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
+  uint32_t* d_groupsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
   uint32_t* d_fold_n = nullptr;
   uint32_t* d_counts_prev = nullptr;
   uint32_t* d_btot = nullptr;       // records per workgroup of the last one-tile sweep8 (2-byte records)
@@ -4934,7 +4969,10 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  void* ptrs[] = {e->d_fired2, e->d_wave_counts2, e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  void* ptrs[] = {e->d_firedx[0], e->d_firedx[1], e->d_firedx[2], e->d_countsx[0], e->d_countsx[1], e->d_countsx[2],
+                  e->d_listx[0], e->d_listx[1], e->d_listx[2], e->d_offsx[0], e->d_offsx[1], e->d_offsx[2],
+                  e->d_groupsx[0], e->d_groupsx[1], e->d_groupsx[2],
+                  e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -5121,8 +5159,8 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       e->fold_hb = value != 0;
       return KWK_OK;
     case KWK_TUNE_FUSE_STEPS:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 or 1");
-      e->fuse_steps = value != 0;
+      if (value > kMaxFuseSteps || value == 3) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2 or 4");
+      e->fuse_steps = value < 2 ? 1u : value;
       return KWK_OK;
     default:
       return fail(KWK_EINVAL, "unknown tuning key " + std::to_string(key));
@@ -5423,16 +5461,17 @@ static kwk_status build_fsm(kwk_engine* e) {
   return KWK_OK;
 }
 
-// fuse: the 1-byte sweep takes two steps (now_ns, now2_ns) in one launch (fusable(); the second
-// step's segments and counts go to d_fired2 / d_wave_counts2)
+// steps > 1: the 1-byte sweep takes that many steps (now_ns + s * dt_ns) in one launch (step_group;
+// step s's segments and counts go to d_firedx / d_countsx[s - 1])
 static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire,
-                               bool fuse = false, int64_t now2_ns = 0) {
+                               uint32_t steps = 1, int64_t dt_ns = 0) {
+  const bool fuse = steps > 1;
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   e->compacted = false;
   e->last_sweep = kwk_sweep_info{};
   if (!e->fold_now) e->fold_valid = false;  // d_fold no longer holds the list before the last
-  if (e->n_active == 0) { e->last_blocks = 0; e->steps += fuse ? 2u : 1u; return KWK_OK; }
+  if (e->n_active == 0) { e->last_blocks = 0; e->steps += steps; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
   const bool h = a.harness.enable != 0;
@@ -5454,14 +5493,18 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
 
     if (fuse) {
-      if (!s4 || !e->d_fired2) return fail(KWK_ESTATE, "fused steps: 1-byte sweep with <= 4 stages and its buffers");
-      a.fired2 = e->d_fired2;
-      a.wave_counts2 = e->d_wave_counts2;
-      a.now2 = now2_ns;
+      if (!s4 || (steps != 2 && steps != 4)) return fail(KWK_ESTATE, "fused steps: 2 or 4, 1-byte sweep with <= 4 stages");
+      for (uint32_t i = 0; i + 1 < steps; ++i) {
+        if (!e->d_firedx[i]) return fail(KWK_ESTATE, "fused steps: buffers not allocated");
+        a.firedx[i] = e->d_firedx[i];
+        a.countsx[i] = e->d_countsx[i];
+        a.nowx[i] = now_ns + (int64_t)(i + 1) * dt_ns;
+      }
     }
 #define K8(P, D)                                                                                        \
-  (fuse ? (const void*)sweep8_kernel<P, D, true, true>                                                 \
-        : s4 ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
+  (steps == 4   ? (const void*)sweep8_kernel<P, D, true, 4>                                            \
+   : steps == 2 ? (const void*)sweep8_kernel<P, D, true, 2>                                            \
+   : s4         ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
     uint32_t pg = e->persist16 ? persist_grid(e, pk, tiles) : tiles;
 
@@ -5485,8 +5528,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     e->last_blocks = tiles;
     e->last_grid = blocks;
     e->cum_rows = blocks > e->cum_rows ? blocks : e->cum_rows;
-    e->last_sweep.steps = fuse ? 2u : 1u;
-    e->steps += fuse ? 2u : 1u;
+    e->last_sweep.steps = steps;
+    e->steps += steps;
     return KWK_OK;
   }
   if (e->fmt.half) {  // 2-byte words: whole-line write-back sweep
@@ -5865,43 +5908,102 @@ static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t s
   return enqueue_compact(e, compact_mode(compact));
 }
 
-// two steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no due
-// time (objects then step independently of the clock except through due times already queued,
-// which the second step tests at its own now) and whose records are the 2-byte ones
-static bool fusable(const kwk_engine* e, uint32_t ev_every) {
-  return e->fuse_steps && e->fmt.byte && e->n_stages <= 4 && !e->fsm8_due_any && e->loaded_table && !e->fold_pending &&
-         ev_every != 1;
+// several steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no
+// due time (objects then step independently of the clock except through due times already
+// queued, which each step tests at its own now) and whose records are the 2-byte ones.  The steps
+// a launch takes: 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
+// sample per launch (ev_every 2 or 3: pairs; 1: none fused)
+static uint32_t fuse_group(const kwk_engine* e, uint32_t left, uint32_t ev_every) {
+  if (e->fuse_steps < 2 || !e->fmt.byte || e->n_stages > 4 || e->fsm8_due_any || !e->loaded_table || e->fold_pending ||
+      ev_every == 1)
+    return 1;
+  uint32_t m = e->fuse_steps;
+  if (ev_every && ev_every < 4) m = 2;
+  while (m > left) m >>= 1;
+  return m ? m : 1;
 }
 
-// steps k (now) and k + 1 (now + dt) of kwk_step_n / _pair in one launch, then each step's
-// hand-back in turn: the first step's from d_fired, then (buffers swapped) the second's, which
-// stays the engine's last step; ev_a brackets the launch (the sample of either step)
-static kwk_status step_pair(kwk_engine* e, int64_t now, int64_t dt, uint64_t seed, uint64_t step, uint32_t compact,
-                            int ev_a) {
-  if (!e->d_fired2) {
+// steps k .. k + m - 1 of kwk_step_n / _pair (now, now + dt, ...) in one launch, then each step's
+// hand-back in turn: step 0's from d_fired, then each next step's, its segments rotated into
+// d_fired / d_wave_counts (the last step's stay there: the engine's last step); ev_a brackets the
+// launch (the sample of whichever step it is)
+static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt, uint64_t seed, uint64_t step,
+                             uint32_t compact, int ev_a) {
+  for (uint32_t i = 0; i + 1 < m; ++i) {
+    if (e->d_firedx[i]) continue;
     const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
-    HIP_TRY(hipMalloc((void**)&e->d_fired2, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
-                                                                      (size_t)kBlock * kMaxObjPerThread)));
-    HIP_TRY(hipMalloc((void**)&e->d_wave_counts2, sizeof(uint32_t) * (n_waves + 4)));
+    HIP_TRY(hipMalloc((void**)&e->d_firedx[i], sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
+                                                                         (size_t)kBlock * kMaxObjPerThread)));
+    HIP_TRY(hipMalloc((void**)&e->d_countsx[i], sizeof(uint32_t) * (n_waves + 4)));
+    HIP_TRY(hipMalloc((void**)&e->d_listx[i], sizeof(uint16_t) * (size_t)e->capacity + 64));
+    HIP_TRY(hipMalloc((void**)&e->d_offsx[i], sizeof(uint32_t) * (n_waves + 4)));
+    HIP_TRY(hipMalloc((void**)&e->d_groupsx[i], sizeof(uint32_t) * (n_waves / kScanGroup + 4)));
   }
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
-  if (kwk_status st = launch_sweep(e, now, seed, step, true, true, now + dt)) return st;
+  if (kwk_status st = launch_sweep(e, now, seed, step, true, m, dt)) return st;
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
-  if (compact)
-    if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
-  std::swap(e->d_fired, e->d_fired2);
-  std::swap(e->d_wave_counts, e->d_wave_counts2);
-  e->compacted = false;
-  if (compact)
-    if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
+  if (compact == KWK_COMPACT_PACKED16 && e->last_rec == kRecId8Half && n_waves && !e->copy_pending) {
+    // the steps' 2-byte hand-backs in one launch (two: scan + expansion, past compact_small
+    // segments), blockIdx.y = the step: all but the last into the group's own lists, the last into
+    // the engine's (kwk_fired_packed16 reads it), each step's segments and counts as it swept them
+    CompactArgs4 c4;
+    for (uint32_t i = 0; i < m; ++i) {
+      CompactArgs& a = c4.a[i];
+      const bool last = i + 1 == m;
+      a.fired32 = reinterpret_cast<const uint32_t*>(i ? e->d_firedx[i - 1] : e->d_fired);
+      a.counts = i ? e->d_countsx[i - 1] : e->d_wave_counts;
+      a.offsets = last ? e->d_wave_offsets : e->d_offsx[i];
+      a.group_tot = last ? e->d_seg_groups : e->d_groupsx[i];
+      a.out = last ? e->d_compact : reinterpret_cast<kwk_fired_rec*>(e->d_listx[i]);
+      a.n_segs = n_waves;
+      a.seg_region_shift = e->last_region_shift;
+      a.region_slots = 64u * e->last_objs << e->last_region_shift;
+      a.stride = 64u * e->last_objs + 32u;
+    }
+    const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
+    if (n_waves <= e->compact_small) {
+      hipLaunchKernelGGL(compact16_small_multi_kernel, dim3(blocks, m), dim3(kBlock), 0, e->stream, c4);
+    } else {
+      constexpr uint32_t W16 = kCompact16Spw;
+      hipLaunchKernelGGL(seg_scan_multi_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup, m), dim3(kBlock), 0,
+                         e->stream, c4);
+      hipLaunchKernelGGL(compact16_multi_kernel<W16>, dim3((n_waves + W16 * kWavesPerBlock - 1) / (W16 * kWavesPerBlock), m),
+                         dim3(kBlock), 0, e->stream, c4);
+    }
+    HIP_TRY(hipGetLastError());
+    for (uint32_t i = 1; i < m; ++i) {  // the last step's segments and counts where the engine reads them
+      std::swap(e->d_fired, e->d_firedx[i - 1]);
+      std::swap(e->d_wave_counts, e->d_countsx[i - 1]);
+    }
+    e->compacted = true;
+    e->compacted_packed = false;
+    e->compacted_16 = true;
+    e->compacted_bits = false;
+    return KWK_OK;
+  }
+  for (uint32_t i = 0; i < m; ++i) {
+    if (i) {
+      std::swap(e->d_fired, e->d_firedx[i - 1]);
+      std::swap(e->d_wave_counts, e->d_countsx[i - 1]);
+      e->compacted = false;
+    }
+    if (compact)
+      if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+  }
   return KWK_OK;
 }
 
-// the event sample of step j (ev_every > 0), or -1
+// the event sample of step j (ev_every > 0), or -1; of a launch of steps j .. j + m - 1: the first
 static int ev_of(uint32_t ev_every, uint32_t j) {
   return ev_every && j % ev_every == 0 ? (int)(2u * (j / ev_every)) : -1;
+}
+static int ev_of_group(uint32_t ev_every, uint32_t j, uint32_t m) {
+  for (uint32_t i = 0; i < m; ++i)
+    if (ev_of(ev_every, j + i) >= 0) return ev_of(ev_every, j + i);
+  return -1;
 }
 
 kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
@@ -5913,10 +6015,12 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
   if (kwk_status st = set_dev(e)) return st;
   for (uint32_t k = 0; k < n;) {
     const uint32_t j = ev_j0 + k;
-    if (k + 1 < n && fusable(e, ev_every)) {
-      const int ev = ev_of(ev_every, j) >= 0 ? ev_of(ev_every, j) : ev_of(ev_every, j + 1);
-      if (kwk_status st = step_pair(e, now0_ns + (int64_t)k * dt_ns, dt_ns, seed, step0 + k, compact, ev)) return st;
-      k += 2;
+    const uint32_t m = fuse_group(e, n - k, ev_every);
+    if (m > 1) {
+      if (kwk_status st = step_group(e, m, now0_ns + (int64_t)k * dt_ns, dt_ns, seed, step0 + k, compact,
+                                     ev_of_group(ev_every, j, m)))
+        return st;
+      k += m;
       continue;
     }
     if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev_of(ev_every, j), true,
@@ -5941,11 +6045,10 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
   for (uint32_t k = 0; k < n;) {
     const uint32_t j = ev_j0 + k;
     const int64_t now = now0_ns + (int64_t)k * dt_ns;
-    // a fused pair of the first engine, the other's two steps right behind (its own stream)
-    const uint32_t m = k + 1 < n && fusable(e, ev_every) ? 2u : 1u;
-    if (m == 2) {
-      const int ev = ev_of(ev_every, j) >= 0 ? ev_of(ev_every, j) : ev_of(ev_every, j + 1);
-      if (kwk_status st = step_pair(e, now, dt_ns, seed, step0 + k, compact, ev)) return st;
+    // the first engine's fused steps (or one), the other's as many right behind (its own stream)
+    const uint32_t m = fuse_group(e, n - k, ev_every);
+    if (m > 1) {
+      if (kwk_status st = step_group(e, m, now, dt_ns, seed, step0 + k, compact, ev_of_group(ev_every, j, m))) return st;
     } else if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev_of(ev_every, j), true, k + 1 == n)) {
       return st;
     }

@@ -401,12 +401,13 @@ def test_step_n_equals_per_step_calls():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_nodes", [20_000, 250_000])
 def test_fused_step_pairs_equal_per_step_calls(n_nodes):
-    """KWK_TUNE_FUSE_STEPS (default on): kwk_step_n sweeps the 1-byte ids two steps per launch
-    (sweep8_kernel<..., kFuse>: each id read once, stepped twice in LDS, written once; each step's
+    """KWK_TUNE_FUSE_STEPS (default 4): kwk_step_n sweeps the 1-byte ids up to four steps per launch
+    (sweep8_kernel<..., kSteps>: each id read once, stepped in LDS, written once; each step's
     records to its own segments, each hand-back in turn).  States, the last fired list, the fired /
     matched / per-stage counts and the step count must equal the per-step kwk_step +
-    kwk_fired_compact calls — one-tile grid (2M pods) and persistent grid (25M pods), pairs and a
-    trailing single step, with event samples; the fused launch reads and writes the ids once."""
+    kwk_fired_compact calls — one-tile grid (2M pods) and persistent grid (25M pods); groups of
+    four, pairs (event samples every 2nd step cap a launch at two steps) and single steps; the
+    fused launches read and write the ids once."""
     from kwok_amd.host import abi
     engines = {"calls": _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 0})[1]}
     engines["fused"] = _pods("auto", n_nodes=n_nodes)[1]
@@ -421,9 +422,9 @@ def test_fused_step_pairs_equal_per_step_calls(n_nodes):
         f = engines["fused"]
         f.step_n(3, now0, dt, seed, 0)
         f.step_n(4, now0 + 3 * dt, dt, seed, 3)
-        assert f.last_sweep()["steps"] == 2  # the call's last two steps: one launch
+        assert f.last_sweep()["steps"] == 4  # the second call's four steps: one launch
         engines["fused_ev"].step_n(7, now0, dt, seed, 0, True, 2, 0)
-        assert engines["fused_ev"].last_sweep()["steps"] == 1  # 3 pairs, then step 6 alone
+        assert engines["fused_ev"].last_sweep()["steps"] == 1  # samples every 2nd step: 3 pairs, then step 6
         r_hot, _ = ref.read()
         r_fired = _fired_key(ref.fired())
         r_st = ref.stats()
@@ -445,11 +446,13 @@ def test_fused_step_pairs_equal_per_step_calls(n_nodes):
 
 
 @pytest.mark.gpu
-def test_fused_step_n_pair_equals_per_step_calls():
-    """The bench's call, kwk_step_n_pair, with the pod engine's steps fused in pairs and the node
-    engine's stepped one by one behind each pair: both engines' states, last fired lists (2-byte
-    pod records with their segment counts, 4-byte node records) and counts equal the per-step
-    calls, for an odd step count (a trailing single pod step)."""
+@pytest.mark.parametrize("compact_small", [-1, 0])
+def test_fused_step_n_pair_equals_per_step_calls(compact_small):
+    """The bench's call, kwk_step_n_pair with 2-byte hand-backs: the pod engine's steps fused in
+    groups of four and two, each group's hand-backs in one launch (one-launch prefix, or with
+    KWK_TUNE_COMPACT_SMALL 0 the scan + expansion pair, blockIdx.y = the step), the node engine
+    stepped one by one behind each group.  Both engines' states, last fired lists (2-byte pod
+    records with their segment counts, 4-byte node records) and counts equal the per-step calls."""
     import bench
     from kwok_amd.host import abi
     now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
@@ -458,17 +461,19 @@ def test_fused_step_n_pair_equals_per_step_calls():
         pods, nodes, _ = bench.build_engines(0, 20_000, PPN, 0, seed, 0.1)
         try:
             assert pods.stats()["state_bytes"] == 1
+            if compact_small >= 0:
+                pods.set_tuning(abi.TUNE_COMPACT_SMALL, compact_small)
             if mode == "calls":
                 pods.set_tuning(abi.TUNE_FUSE_STEPS, 0)
-                for k in range(9):
+                for k in range(10):
                     pods.step(now0 + k * dt, seed, k)
                     pods.fired_compact("16")
                     nodes.step(now0 + k * dt, seed, k)
                     nodes.fired_compact(True)
             else:
                 pods.step_n_pair(nodes, 4, now0, dt, seed, 0, "packed16")
-                pods.step_n_pair(nodes, 5, now0 + 4 * dt, dt, seed, 4, "packed16")
-                assert pods.last_sweep()["steps"] == 1
+                pods.step_n_pair(nodes, 6, now0 + 4 * dt, dt, seed, 4, "packed16")
+                assert pods.last_sweep()["steps"] == 2  # groups 4 | 4, 2
             recs, segc, _ = pods.fired_packed16()
             runs[mode] = (pods.read()[0], nodes.read()[0], recs, segc, nodes.fired_packed(), pods.stats(), nodes.stats())
         finally:
