@@ -382,8 +382,8 @@ def _pmc_pass(counter, args, outdir):
     process has not touched the GPU).  -> mean counter value per pod-sweep launch (KiB)."""
     d = os.path.join(outdir, counter.lower())
     cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
-           "--pmc-child", "--steps", "6", "--warmup", "4", "--nodes", str(args.nodes),
-           "--pods-per-node", str(args.pods_per_node), "--seed", str(args.seed)]
+           "--pmc-child", "--steps", "8", "--warmup", "4", "--nodes", str(args.nodes),
+           "--pods-per-node", str(args.pods_per_node), "--seed", str(args.seed), "--fuse-steps", str(args.fuse_steps)]
     env = dict(os.environ, TMPDIR=outdir)
     r = subprocess.run(cmd, cwd=outdir, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150)
     if r.returncode != 0:
@@ -396,7 +396,12 @@ def _pmc_pass(counter, args, outdir):
     for disp, name, cn, v in c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection"):
         if "sweep" in name and "<true" in name and cn == counter:  # the pod engine (harness) only
             per[disp] = per.get(disp, 0.0) + float(v)
-    vals = [per[k] for k in sorted(per)][4:]  # past the warm-up launches
+    # past the warm-up launches: 4 steps, then 8 timed — one launch per step, or with fused steps
+    # (KWK_TUNE_FUSE_STEPS 4) one 4-step launch, then two
+    f = args.fuse_steps
+    fused = f >= 2 and len(per) == sweep_launches(4, 0, f) + sweep_launches(8, 0, f)
+    timed = sweep_launches(8, 0, f) if fused else 8
+    vals = [per[k] for k in sorted(per)][len(per) - timed:]
     if not vals:
         raise RuntimeError(f"rocprofv3 {counter}: no pod sweep dispatches")
     return statistics.mean(vals), len(vals)
