@@ -1612,7 +1612,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     // test at `now`, the work list and the table passes; the step's records staged at the work
     // list's front (seg_n).  Returns the items worked: the tile is in LDS iff nonzero.  first: the
     // step that read the ids from HBM (a fused pair's second step adds no read bytes)
-    auto phase12 = [&](const uint4 (&ids)[Q], const int64_t now, const bool first, uint32_t& seg_n)
+    auto phase12 = [&](const uint4 (&ids)[Q], const int64_t now, const bool first, const bool in_lds, uint32_t& seg_n)
                        __attribute__((always_inline)) -> uint32_t {
       uint32_t need = 0, pend = 0, ready = 0;
   #pragma unroll
@@ -1648,12 +1648,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       if (n_work) {  // wave-uniform
         // ---- phase 2: the ids to the LDS tile, the work list (absolute LDS addresses of the ids in
         // slot order per lane), then one lookup in the id table per item, 64 items per pass
+        if (!in_lds) {  // (a fused step after one with work: the tile is there already)
   #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          tw[lds_col8(q * 4 + 0, lane)] = ids[q].x;
-          tw[lds_col8(q * 4 + 1, lane)] = ids[q].y;
-          tw[lds_col8(q * 4 + 2, lane)] = ids[q].z;
-          tw[lds_col8(q * 4 + 3, lane)] = ids[q].w;
+          for (int q = 0; q < Q; ++q) {
+            tw[lds_col8(q * 4 + 0, lane)] = ids[q].x;
+            tw[lds_col8(q * 4 + 1, lane)] = ids[q].y;
+            tw[lds_col8(q * 4 + 2, lane)] = ids[q].z;
+            tw[lds_col8(q * 4 + 3, lane)] = ids[q].w;
+          }
         }
         const bool rdy = ballot(ready != 0) != 0;  // wave-uniform: entries carry the ready bit
         const bool slow = rdy || any_due;          // ... or due times may be written
@@ -1766,7 +1768,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
       wave_fired += seg_n;
     };
     uint32_t seg_n = 0;  // wave-uniform
-    const uint32_t n_work = phase12(cur, a.now, true, seg_n);
+    const uint32_t n_work = phase12(cur, a.now, true, false, seg_n);
     uint32_t any_work = n_work;
     uint32_t seg_last = seg_n;
 #pragma unroll
@@ -1784,7 +1786,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
                           : cur[q];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       seg_last = 0;
-      any_work |= phase12(mid, a.nowx[st - 1], false, seg_last);
+      any_work |= phase12(mid, a.nowx[st - 1], false, any_work != 0, seg_last);
     }
     // ---- phase 3 and the hand-back segment: a fixed set of stores per tile (whole 128-byte lines
     // wherever an id changed, the staged records, the header), each lane's offset out of range
