@@ -7,7 +7,8 @@
 #   smoke                      __graft_entry__.smoke()
 #   bench[=<bench.py args>]    the driver's bench command (default --gpus 1 --steps 20 --warmup 5)
 #   prof                       kernel trace + stats of the driver's bench command (kernel_stats.csv)
-#   timeline[=<bench args>]    kernel trace of the C5 bench (timed steps only): 10 steps' dispatches and gaps
+#   timeline[=<bench args>]    kernel trace of the C5 bench (timed steps only): one reporting interval's dispatches and
+#                              gaps (from pod sweep launch TL_N, 2, for TL_SPAN, 3, launches: fused groups 4 + 4 + 2)
 #   agg                        the reporting kernels alone at C5 (tools/agg_bench.py) + SQ passes over usage
 #   configs                    bench.py --config C1..C4 lines (configs_C1_C4.jsonl)
 #   c2prof                     C2 working set: kernel trace + FETCH_SIZE / WRITE_SIZE passes
@@ -51,7 +52,7 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
       TRACE
       timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run -- python3 $R/bench.py $B1 --no-pmc --no-cpu-baseline \
         --hbm-nodes 0 --pcie-steps 0 --emit-steps 0 $arg > $O/tl_bench.json 2> $O/tl_bench.err || { tail -30 $O/tl_bench.err; exit 1; }
-      cd $R && python tools/rocpd_summary.py timeline $(find $O/tl -name '*.db' | head -1) sweep8 10 10 > $O/timeline.txt \
+      cd $R && python tools/rocpd_summary.py timeline $(find $O/tl -name '*.db' | head -1) sweep8 ${TL_N:-2} ${TL_SPAN:-3} > $O/timeline.txt \
         && cat $O/timeline.txt ;;
     agg)  # the reporting kernels alone at C5 (tools/agg_bench.py) + SQ passes over them
       timeout -k 10 300 python -u tools/agg_bench.py > $O/agg.json 2> $O/agg.err || { tail -30 $O/agg.err; exit 1; }
