@@ -195,34 +195,21 @@ def run_steps(pods, nodes, seed, dt, k0, k1, ev_base=None, reporter=None, report
             if reporter is not None and report_every and (k - k0) % report_every == 0:
                 last = reporter.collect(NOW0 + (k - 1) * dt)
         return last, 0
-    # every step's fired lists to pinned host memory, overlapped (kwk_fired_fetch_async): the copies of
-    # step k run on the engines' copy streams while step k + 1 sweeps; step k + 1's compaction waits
-    # for them on the device; the host buffers alternate between steps
-    last = None
+    # every step's fired lists to pinned host memory on the fused path: one kwk_step_n_pair call for
+    # the steps (pod launches of 4 + 4 + 2 steps, each launch's hand-backs in one launch), every
+    # step's list kept in the engines' hand-back rings (kwk_fired_keep) and fetched by step
+    # (kwk_fired_fetch_step: waits for that step's compaction only, the copy runs on the copy stream
+    # while the later steps sweep); pinned[j] = step j's (pod list, node list, pod segment counts)
+    n = k1 - k0
+    assert len(pinned) >= n
+    pods.step_n_pair(nodes, n, NOW0 + k0 * dt, dt, seed, k0, HANDBACK[handback])
     n_fired_host = 0
-    packed = handback in ("packed", "packed16", "bits")
-    for k in range(k0, k1):
-        now = NOW0 + k * dt
-        j = k - k0
-        timed = ev_base is not None and j % EV_EVERY == 0
-        if timed:
-            pods.event_record(ev_base + 2 * (j // EV_EVERY))
-        pods.step(now, seed, k)
-        if timed:
-            pods.event_record(ev_base + 2 * (j // EV_EVERY) + 1)
-        # the 1-byte sweep writes 2-byte records when the program has at most 4 stages
-        p16 = handback in ("packed16", "bits") and pods.last_sweep()["kernel"] == 5 and len(pods.p.stages) <= 4
-        pods.fired_compact(("16" if handback == "packed16" else "bits") if p16 else packed)
-        nodes.step(now, seed, k)
-        nodes.fired_compact(packed)
-        b = 3 * (j % 2)
-        n_fired_host += pods.fetch_async(pinned[b], pinned[b + 2])["n_records"]
-        n_fired_host += nodes.fetch_async(pinned[b + 1])["n_records"]
-        if reporter is not None and report_every and (j + 1) % report_every == 0:
-            last = reporter.collect(now)
+    for j in range(n):
+        n_fired_host += pods.fetch_step(k0 + j, pinned[j][0], pinned[j][2])["n_records"]
+        n_fired_host += nodes.fetch_step(k0 + j, pinned[j][1])["n_records"]
     pods.fetch_wait()
     nodes.fetch_wait()
-    return last, n_fired_host
+    return None, n_fired_host
 
 
 def synth_ipv4(first: int, n: int, lead: int, stride: int) -> np.ndarray:
@@ -739,6 +726,7 @@ def main():
     agg_dict = agg.result().as_dict() if agg is not None else None  # the last interval's all-reduced aggregates
     s1p, s1n = pods.stats(), nodes.stats()
     pod_kernel = pods.last_sweep()
+    pod_n_stages = len(pods.p.stages)
     n_ev = (args.steps + EV_EVERY - 1) // EV_EVERY
     if world > 1:  # sampled after the timed region (the same steps continued)
         k0 = args.warmup + args.steps
@@ -770,13 +758,18 @@ def main():
     pcie = None
     if args.pcie_steps > 0 and world == 1:
         from kwok_amd.host.engine import PinnedBuffer
-        pin = tuple(PinnedBuffer(n) for _ in range(2)  # two sets: step k's copy runs while step k + 1 is enqueued
-                    for n in (8 * pods.capacity, 8 * nodes.capacity, 4 * (pods.capacity // 512 + 64)))
+        pod_list = {"bits": 2, "packed16": 2, "packed": 4, "rec": 8}[args.pcie_handback] * pods.capacity + 64
+        node_list = (8 if args.pcie_handback == "rec" else 4) * nodes.capacity + 64
+        pin = [tuple(PinnedBuffer(n) for n in (pod_list, node_list, 4 * (pods.capacity // 512 + 64)))
+               for _ in range(args.pcie_steps)]
+        pods.fired_keep(args.pcie_steps)
+        nodes.fired_keep(args.pcie_steps)
         k0 = args.warmup + args.steps
-        # one untimed step first: the copy streams, events and snapshot buffers are created at the
-        # engines' first fetch
-        run_steps(pods, nodes, args.seed, dt, k0, k0 + 1, pinned=pin, handback=args.pcie_handback)
-        k0 += 1
+        # one untimed call first: the copy streams, events and ring slots are created at the first use
+        run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin, handback=args.pcie_handback)
+        k0 += args.pcie_steps
+        pods.sync()
+        nodes.sync()
         s2p, s2n = pods.stats(), nodes.stats()
         t1 = time.perf_counter()
         _, n_host = run_steps(pods, nodes, args.seed, dt, k0, k0 + args.pcie_steps, pinned=pin,
@@ -787,20 +780,28 @@ def main():
         assert n_host == nf, (n_host, nf)
         pcie = {"value": round(nf / wall, 1), "unit": "stage transitions/sec", "steps": args.pcie_steps,
                 "fired_records_to_host_per_step": nf / args.pcie_steps, "ms_per_step": round(wall / args.pcie_steps * 1e3, 4),
-                "note": "each step's fired lists copied into kwk_alloc_host buffers by kwk_fired_fetch_async (the "
-                        "copy of step k overlaps the sweep of step k + 1): " + {
+                "n_host_equals_fired": True,
+                "note": "one kwk_step_n_pair call on the fused path (pod launches of up to 4 steps), then every "
+                        "step's fired lists copied into kwk_alloc_host buffers by kwk_fired_fetch_step from the "
+                        "engines' hand-back rings (each copy overlaps the later steps): " + {
                     "packed16": "pods' 2-byte records (2 B per transition + 4 B per 2048-slot segment), nodes' "
                                 "4-byte packed records",
-                    "bits": "pods' fired maps (256 B per 2048-slot segment) + 2-bit stage codes "
-                            "(kwk_fired_compact_bits, ~1.5 B per transition at 10 % firing), nodes' 4-byte packed records",
+                    "bits": "pods' byte-sparse fired maps + 2-bit stage codes (kwk_fired_compact_bits, ~1.1 B per "
+                            "transition at 10 % firing), nodes' 4-byte packed records",
                     "packed": "4-byte packed records",
                     "rec": "kwk_fired_rec, 8 B per transition"}[args.pcie_handback]}
-        for p in pin:
-            p.close()
+        pods.fired_keep(0)
+        nodes.fired_keep(0)
+        for x in pin:
+            for p in x:
+                p.close()
+        k_after = k0 + args.pcie_steps
+    else:
+        k_after = args.warmup + args.steps
     patch_emit = None
     if args.emit_steps > 0 and world == 1:
         log("device patch emission run")
-        patch_emit = measure_patch_emit(pods, pvars, pidx, args, dt, args.warmup + args.steps + (args.pcie_steps + 1 if pcie else 0))
+        patch_emit = measure_patch_emit(pods, pvars, pidx, args, dt, k_after)
     del pidx
     if reporter.comm is not None:
         reporter.comm.close()
@@ -817,7 +818,10 @@ def main():
     if rank == 0:
         value = total_fired / max_s
         pod_kernel_s = statistics.mean(sweep_ms) / 1e3
-        fuse_max = args.fuse_steps if pod_kernel["steps"] > 1 else 1  # the last launch fused: the engine fuses
+        # the engine fuses the 1-byte pod sweep when its program allows (pod-fast: <= 4 stages, no delayed
+        # stage) — decided from the engine, not from the last launch's steps (a 1-step tail launch)
+        fuse_max = (args.fuse_steps if (args.fuse_steps >= 2 and int(s1p["state_bytes"]) == 1 and pod_n_stages <= 4)
+                    else 1)
         launches = sweep_launches(args.steps, report_every, fuse_max)
         spl = args.steps / launches  # steps per pod sweep launch (mean)
         achieved = (pbytes / launches) / pod_kernel_s / 1e9

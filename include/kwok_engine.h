@@ -230,9 +230,7 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */
-#define KWK_TUNE_FOLD_HB 16    /* kwk_step_n / _pair with KWK_COMPACT_PACKED16 on small 1-byte engines: a step's
-                                  2-byte hand-back copied by the next step's sweep (kwk_fired_fold16), 1
-                                  (default) or 0 (the hand-back launched after every step) */
+/* 16: retired in round 6 (the folded hand-back, superseded by fused steps at the shard size) */
 #define KWK_TUNE_FUSE_STEPS 17 /* kwk_step_n / _pair on 1-byte engines with <= 4 stages and no delayed stage: up to
                                   4 (default) or 2 steps per sweep launch (each id read once, stepped in LDS,
                                   written once; each step's fired records and hand-back kept apart), or 0 / 1 (one step
@@ -300,17 +298,31 @@ kwk_status kwk_match(kwk_engine* eng, int64_t now_ns, uint64_t seed, uint64_t st
  * direct DMA — and synchronises.  Records are grouped by sweep region (ascending regions: a
  * wave's 512-2048 slots in the 2-byte sweeps, a tile's 2048 / 4096 slots in the 8- / 4-byte word
  * sweep), unordered within a region; each fired slot appears once.  A step that swept nothing
- * (no active slots) leaves an empty list. */
+ * (no active slots) leaves an empty list.
+ * Every compaction writes a list of its own in a ring of device lists tagged with the step it
+ * compacted (DESIGN.md §5 "Hand-back"): the last one is the engine's list the readers below
+ * return, and the lists of the last kwk_fired_keep() compactions stay readable by step number
+ * through kwk_fired_fetch_step — every step of a kwk_step_n / _pair call, fused or not. */
 kwk_status kwk_fired_compact(kwk_engine* eng);
-/* n steps (now0 + k * dt, step0 + k for k < n), each followed by kwk_fired_compact when compact != 0:
- * the per-tick loop of kwk_step / kwk_fired_compact enqueued by one call (enqueue only).  With
- * ev_every > 0, events 2i / 2i + 1 (kwk_event_record) bracket the sweep of every step whose
- * index j = ev_j0 + k is a multiple of ev_every (i = j / ev_every). */
+/* n steps (now0 + k * dt, step0 + k for k < n), each with its hand-back in the given format when
+ * compact != 0 (enqueue only): the per-tick loop of kwk_step / kwk_fired_compact in one call.
+ * On 1-byte engines with <= 4 stages and no delayed stage (KWK_TUNE_FUSE_STEPS) the steps are swept
+ * in launches of up to 4 steps (each id read and written once per launch) and the launch's
+ * hand-backs run as one launch: results are those of the per-step calls, and every step's list is
+ * compacted into its own ring slot (tag step0 + k), so kwk_fired_fetch_step(eng, step0 + k, ...)
+ * reads it while the ring holds it.  The engine's readers (kwk_fired*, kwk_fired_fetch_async) return
+ * the call's last step.  With ev_every > 0, events 2i / 2i + 1 (kwk_event_record) bracket the sweep
+ * LAUNCH containing the first step j = ev_j0 + k that is a multiple of ev_every (i = j / ev_every):
+ * that launch sweeps kwk_last_sweep().steps steps (1, 2 or 4; ev_every 2 or 3 caps launches at 2
+ * steps, 1 disables the fusion), so a caller turning an event pair into per-step time divides by
+ * the steps of that launch. */
 kwk_status kwk_step_n(kwk_engine* eng, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed, uint64_t step0,
                       uint32_t compact, uint32_t ev_every, uint32_t ev_j0);
-/* kwk_step_n over two engines of one shard (the pod and node kinds), enqueued step by step in turn —
- * eng's sweep (+ events) and hand-back, then other's — so that neither stream waits for the host
- * to finish enqueuing the other's n steps; events go on eng's stream only.  Messages: eng's handle. */
+/* kwk_step_n over two engines of one shard (the pod and node kinds), enqueued launch by launch in
+ * turn — eng's sweep launch (+ events) and hand-back, then as many of other's steps — so that
+ * neither stream waits for the host to finish enqueuing the other's n steps; events go on eng's
+ * stream only, as in kwk_step_n.  Both engines' steps are tagged step0 + k in their rings.
+ * Messages: eng's handle. */
 kwk_status kwk_step_n_pair(kwk_engine* eng, kwk_engine* other, uint32_t n, int64_t now0_ns, int64_t dt_ns, uint64_t seed,
                            uint64_t step0, uint32_t compact, uint32_t ev_every, uint32_t ev_j0);
 kwk_status kwk_fired(kwk_engine* eng, kwk_fired_rec* out, uint32_t cap, uint32_t* n_out);
@@ -380,19 +392,26 @@ typedef struct {
   uint32_t format;         /* KWK_COMPACT_PACKED16, _PACKED, _BITS or 1 (kwk_fired_rec) */
   uint32_t reserved;
   uint64_t bytes;          /* bytes copied into out */
+  uint64_t step;           /* the step whose list was copied */
 } kwk_fetch_info;
 kwk_status kwk_fired_fetch_async(kwk_engine* eng, void* out, uint64_t cap_bytes, uint32_t* seg_counts, uint32_t seg_cap,
                                  kwk_fetch_info* info);
 kwk_status kwk_fired_fetch_wait(kwk_engine* eng);
 
-/* The folded hand-back (no reference counterpart: an observation point for tests).  Inside one
- * kwk_step_n / kwk_step_n_pair call with KWK_COMPACT_PACKED16, an engine whose 1-byte sweep runs
- * one tile per workgroup (small engines: the strong-scaling shards) does not launch the hand-back
- * for steps before the call's last: the next step's sweep copies the step's 2-byte list (the
- * kwk_fired_compact_packed16 list, same order) while it rewrites the segments.  The call's last
- * step is compacted as before.  This returns the list of the step before the last (n_out: its
- * records; out may be NULL to ask for the count), KWK_ESTATE when the last call did not fold. */
-kwk_status kwk_fired_fold16(kwk_engine* eng, uint16_t* out, uint32_t cap, uint32_t* n_out);
+/* Every step's hand-back to the host, fused steps included (the playStage workers' input for each
+ * step, pod_controller.go:257-290).  kwk_fired_keep(eng, depth) keeps the lists of the last `depth`
+ * compactions (1..64; 0 = the default: the last few, no per-step completion signal) in the device
+ * ring and makes every compaction signal its own completion and write its length to pinned host
+ * memory.  kwk_fired_fetch_step(eng, step, ...) is kwk_fired_fetch_async for the list of step
+ * `step` (the step argument of kwk_step / kwk_step_n's step0 + k): it waits for THAT step's
+ * compaction only (later steps go on running), enqueues the copies on the copy stream and returns;
+ * the ring slot is rewritten only after its copy (the compaction waits on the device).  So a host
+ * calls kwk_step_n(eng, n, ...) and then kwk_fired_fetch_step for step0 .. step0 + n - 1, each copy
+ * overlapping the later steps' sweeps, and reads the buffers after kwk_fired_fetch_wait.  KWK_ESTATE
+ * when the ring no longer holds that step. */
+kwk_status kwk_fired_keep(kwk_engine* eng, uint32_t depth);
+kwk_status kwk_fired_fetch_step(kwk_engine* eng, uint64_t step, void* out, uint64_t cap_bytes, uint32_t* seg_counts,
+                                uint32_t seg_cap, kwk_fetch_info* info);
 /* pinned (page-locked) host buffers for kwk_fired / kwk_read / usage outputs, reused across steps */
 kwk_status kwk_alloc_host(uint64_t bytes, void** out);
 kwk_status kwk_free_host(void* p);
@@ -651,6 +670,9 @@ typedef struct {
   uint32_t steps;        /* steps the launch swept: 2 or 4 when fused (KWK_TUNE_FUSE_STEPS), else 1 (0: unset) */
 } kwk_sweep_info;
 kwk_status kwk_last_sweep(kwk_engine* eng, kwk_sweep_info* out);
+/* 2 since round 6: the hand-back ring (kwk_fired_keep / kwk_fired_fetch_step, kwk_fetch_info.step),
+ * KWK_TUNE_FOLD_HB and kwk_fired_fold16 retired, kwk_sweep_info.steps (was reserved) */
+#define KWK_ABI_VERSION 2u
 uint32_t kwk_abi_version(void);
 uint32_t kwk_tile_objects(void); /* objects per sweep workgroup */
 

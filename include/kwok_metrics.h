@@ -42,7 +42,8 @@ extern "C" {
 
 typedef struct kwk_metric_set kwk_metric_set;
 
-/* message of the last failing call on m; m = NULL: the calling thread's last message */
+/* message of the calling thread's last failing call (m may be NULL: the messages are kept per
+ * thread, whichever set the call named) */
 const char* kwk_metric_set_last_error(const kwk_metric_set* m);
 
 /* metric_json: one v1alpha1 Metric object (JSON; {"kind": "Metric", "spec": {"path", "metrics":

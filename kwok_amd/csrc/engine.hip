@@ -280,6 +280,8 @@ struct RawTest {
 };
 
 constexpr uint32_t kMaxFuseSteps = 4;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS)
+constexpr uint32_t kHbMin = 4;         // hand-back ring slots: at least a fused launch's steps (kwk_fired_keep)
+constexpr uint32_t kHbMax = 64;
 struct SweepArgs {
   void* __restrict__ st;         // per object state word (StateFmt: uint2 {pred, sched} or packed u32)
   int64_t* __restrict__ due;     // per object due time (read only for objects with a pending stage)
@@ -310,16 +312,6 @@ struct SweepArgs {
   uint32_t fsm_bits;
   int64_t dw_epoch_old;          // fused format: the epoch the records hold (fmt.epoch: the one written)
   uint32_t dw_rebase;            // fused format: the epoch moves this sweep (every pending record re-encoded)
-  // folded hand-back (one-tile-per-workgroup sweep8 with 2-byte records: the N = 8 shard's size):
-  // the sweep copies the PREVIOUS step's records of each (tile, wave) segment into fold_out before
-  // this step's replace them; fold_counts = that step's segment counts (this step writes
-  // wave_counts, the other buffer); fold_n <- the list's length
-  uint16_t* __restrict__ fold_out;
-  const uint32_t* __restrict__ fold_counts;
-  uint32_t* __restrict__ fold_n;
-  uint32_t fold_prev;
-  uint32_t* __restrict__ btot_out;          // one-tile sweep8 with 2-byte records: records per workgroup
-  const uint32_t* __restrict__ fold_btot;   // ... the previous step's (the fold's prefix)
   // sweep8_kernel<..., kSteps>: steps 1 .. kSteps - 1 of the launch (their times, segments and counts)
   kwk_fired_rec* __restrict__ firedx[kMaxFuseSteps - 1];
   uint32_t* __restrict__ countsx[kMaxFuseSteps - 1];
@@ -1494,7 +1486,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
                                   // they only ever write 0xFF back)
   __shared__ uint32_t s_fsm[512];
   __shared__ unsigned int s_stat[kStatWords];
-  __shared__ uint32_t s_fold[2 * kWavesPerBlock];  // fold: per wave the records before the block / its count
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);
@@ -1502,7 +1493,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   const __amdgpu_buffer_rsrc_t due_rs = make_rsrc(a.due, a.n * 8u);
   const __amdgpu_buffer_rsrc_t fdue_rs = make_rsrc(a.fsm_due, 8u * 512u);
   const __amdgpu_buffer_rsrc_t cnt_rs = make_rsrc(a.wave_counts, n_tiles * kWavesPerBlock * 4u);
-  const __amdgpu_buffer_rsrc_t fold_rs = make_rsrc(a.fold_out, 0x7FFFFFF0u);
   uint4 va[kDepth][Q];
   auto issue_tile = [&](uint4 (&dst)[Q], const uint32_t t) __attribute__((always_inline)) {
     const uint32_t off = t < n_tiles ? t * kTile + wave * kWave + lane * 16u : kOOB - 2048u;
@@ -1527,21 +1517,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
   }
   if (threadIdx.x < kStatWords) s_stat[threadIdx.x] = 0;
   if (wave == 0) s_inv[lane] = 0xFFFFFFFFu;
-  const bool fold = !kPersist && kStages4 && a.fold_prev && blockIdx.x < n_tiles;  // block-uniform
-  if (fold) {  // the previous step's records before this block: its per-workgroup totals (16-byte loads)
-    const uint32_t nb = blockIdx.x;
-    const uint4* __restrict__ b4 = reinterpret_cast<const uint4*>(a.fold_btot);
-    uint32_t sum = 0;
-#pragma unroll 2
-    for (uint32_t q = threadIdx.x; q < nb / 4u; q += kBlock) {
-      const uint4 v = b4[q];
-      sum += (v.x + v.y) + (v.z + v.w);
-    }
-    if (threadIdx.x < (nb & 3u)) sum += a.fold_btot[(nb & ~3u) + threadIdx.x];
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    if (lane == 0) s_fold[wave] = sum;
-    if (threadIdx.x < kWavesPerBlock) s_fold[kWavesPerBlock + threadIdx.x] = a.fold_counts[nb * kWavesPerBlock + threadIdx.x];
-  }
   __syncthreads();
 
   // kStages4: stc[0] = this tile's fired records of stages 0-3 as byte counters (<= 32 items per lane
@@ -1568,25 +1543,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const uint32_t seg_id = tile * kWavesPerBlock + wave;
     uint32_t* __restrict__ seg32 = reinterpret_cast<uint32_t*>(a.fired) + (uint64_t)seg_id * kSeg8;
     const __amdgpu_buffer_rsrc_t seg_rs = make_rsrc(seg32, kSeg8 * 4u);
-    // folded hand-back: this segment's records of the previous step, two per lane and dword,
-    // records 2 * lane + 128 * j (+1), loaded now and stored after this step's fixed store set;
-    // past 512 records (rare) copied here, before this step's records overwrite the segment
-    uint32_t f_o = 0, f_c = 0, f_v[4] = {0u, 0u, 0u, 0u};
-    if (fold) {
-      f_o = s_fold[0] + s_fold[1] + s_fold[2] + s_fold[3];
-      for (uint32_t w = 0; w < wave; ++w) f_o += s_fold[kWavesPerBlock + w];
-      f_c = s_fold[kWavesPerBlock + wave];
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t r = 2u * lane + 128u * j;
-        f_v[j] = __builtin_amdgcn_raw_buffer_load_b32(seg_rs, r < f_c ? kRec16Header + r * 2u : kOOB, 0, 0);
-      }
-      if (f_c > 512u) {
-        const uint16_t* old = reinterpret_cast<const uint16_t*>(seg32 + kRec16Header / 4u);
-        for (uint32_t j = 512u + lane; j < f_c; j += 64u) a.fold_out[f_o + j] = old[j];
-      }
-      if (seg_id + 1u == n_tiles * kWavesPerBlock && lane == 0) *a.fold_n = f_o + f_c;
-    }
     uint4 cur_copy[Q];
     if (kDepth == 1) {
 #pragma unroll
@@ -1728,8 +1684,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
         // records: seg_n 2-byte records from the work list, as 16-byte chunks of whole 128-byte
         // lines (the tail of the last line is padding)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (fold)  // the previous records are in registers before this step's overwrite them
-          asm volatile("" ::"v"(f_v[0]), "v"(f_v[1]), "v"(f_v[2]), "v"(f_v[3]));
         const uint32_t n_chunks = ((seg_n * 2u + 127u) & ~127u) / 16u;
         const uint4* wq = reinterpret_cast<const uint4*>(wl);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1742,15 +1696,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
         }
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{seg_n, 0u, 0u, 0u}, seg_rs, lane == 0 && real ? 0u : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(seg_n, cnt_rs, lane == 0 && real ? seg_id * 4u : kOOB, 0, 0);
-        if (fold) {  // the previous step's records (a fixed set of eight 2-byte stores)
-  #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t r = 2u * lane + 128u * j;
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f_v[j], fold_rs, r < f_c ? (f_o + r) * 2u : kOOB, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(f_v[j] >> 16), fold_rs, r + 1u < f_c ? (f_o + r + 1u) * 2u : kOOB,
-                                                  0, 0);
-          }
-        }
         if (real) {
           w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
           w_bytes += 2u * seg_n + 4u;
@@ -1863,7 +1808,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
     const unsigned int val = s_stat[threadIdx.x];
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
   }
-  if (!kPersist && kStages4 && threadIdx.x == 0) a.btot_out[blockIdx.x] = s_stat[1];  // the next step's fold prefix
 }
 
 // ------------------------------------------------------------------ 4- and 8-byte state sweep
@@ -2278,6 +2222,10 @@ struct CompactArgs {
   uint32_t* __restrict__ offsets;         // seg_scan_kernel's output; [0] <- the list length
   const uint32_t* __restrict__ group_tot;
   kwk_fired_rec* __restrict__ out;
+  uint32_t* __restrict__ counts_out;      // 2-byte / bitmap lists: the step's records per segment, kept with
+                                          // the list (the next sweep rewrites `counts`), or null
+  uint32_t* __restrict__ host_len;        // kwk_fired_keep: pinned host words <- the list length (bitmap:
+                                          // {words, records}), or null
   uint32_t n_segs;
   uint32_t seg_region_shift;              // segments per sweep region = 1 << shift
   uint32_t region_slots;                  // object slots per region (wave / tile)
@@ -2361,7 +2309,10 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     const uint32_t seg = seg0 + s;
     if (seg >= a.n_segs) break;
     const uint32_t off = gp + o1[s];
-    if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c[s];
+    if (seg == a.n_segs - 1 && lane == 0) {
+      a.offsets[0] = off + c[s];
+      if (a.host_len) a.host_len[0] = off + c[s];
+    }
     const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
@@ -2396,6 +2347,11 @@ __device__ __forceinline__ void compact16_block(const CompactArgs& a, const uint
     c[s] = seg0 + s < a.n_segs ? a.counts[seg] : 0u;
     o1[s] = a.offsets[1 + seg];
   }
+  if (a.counts_out) {
+#pragma unroll
+    for (uint32_t s = 0; s < kSpw; ++s)
+      if (lane == s && seg0 + s < a.n_segs) a.counts_out[seg0 + s] = c[s];
+  }
   uint32_t gp = 0;
   for (uint32_t g = lane; g < seg0 / kScanGroup; g += 64) gp += a.group_tot[g];
   for (int o = 32; o > 0; o >>= 1) gp += __shfl_xor(gp, o);
@@ -2405,7 +2361,10 @@ __device__ __forceinline__ void compact16_block(const CompactArgs& a, const uint
     const uint32_t seg = seg0 + s;
     if (seg >= a.n_segs) break;
     const uint32_t off = gp + o1[s];
-    if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c[s];
+    if (seg == a.n_segs - 1 && lane == 0) {
+      a.offsets[0] = off + c[s];
+      if (a.host_len) a.host_len[0] = off + c[s];
+    }
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
       if (lane + 64u * k < c[s]) __builtin_nontemporal_store(r[s][k], out + off + lane + 64u * k);
@@ -2437,14 +2396,21 @@ __device__ __forceinline__ void compact16_small_block(const CompactArgs& a, cons
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
   if (lane == 0) s_part[wave] = sum;
-  if (threadIdx.x < kSegsPerBlock) s_seg[threadIdx.x] = first + threadIdx.x < a.n_segs ? a.counts[first + threadIdx.x] : 0u;
+  if (threadIdx.x < kSegsPerBlock) {
+    const uint32_t c = first + threadIdx.x < a.n_segs ? a.counts[first + threadIdx.x] : 0u;
+    s_seg[threadIdx.x] = c;
+    if (a.counts_out && first + threadIdx.x < a.n_segs) a.counts_out[first + threadIdx.x] = c;
+  }
   __syncthreads();
   const uint32_t seg = first + wave;
   if (seg >= a.n_segs) return;
   uint32_t off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
   for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
   const uint32_t c = s_seg[wave];
-  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
+  if (seg == a.n_segs - 1 && lane == 0) {
+    a.offsets[0] = off + c;
+    if (a.host_len) a.host_len[0] = off + c;
+  }
   const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
   for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
@@ -2603,6 +2569,10 @@ __global__ __launch_bounds__(kBlock) void bits_write_kernel(CompactArgs a, const
       tot[0] = n + pre + 8u + zw + ((c + 15u) >> 4);
       tot[1] = r;
       a.offsets[0] = tot[0];
+      if (a.host_len) {
+        a.host_len[0] = tot[0];
+        a.host_len[1] = r;
+      }
     }
   }
 }
@@ -2637,7 +2607,10 @@ __global__ __launch_bounds__(kBlock) void compact_small_kernel(CompactArgs a) {
   uint32_t off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
   for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
   const uint32_t c = s_seg[wave];
-  if (seg == a.n_segs - 1 && lane == 0) a.offsets[0] = off + c;
+  if (seg == a.n_segs - 1 && lane == 0) {
+    a.offsets[0] = off + c;
+    if (a.host_len) a.host_len[0] = off + c;
+  }
   const uint32_t* __restrict__ sp = a.fired32 + (uint64_t)seg * a.stride;
   const uint32_t base = (seg >> a.seg_region_shift) * a.region_slots;
   for (uint32_t j = lane; j < c; j += 64) {
@@ -4331,21 +4304,39 @@ struct kwk_engine {
   bool compacted_packed = false;  // ... as 4-byte packed records (kwk_fired_compact_packed)
   bool compacted_16 = false;      // ... as the 1-byte sweep's 2-byte records (kwk_fired_compact_packed16)
   bool compacted_bits = false;    // ... as its per-segment maps + stage codes (kwk_fired_compact_bits)
-  // kwk_fired_fetch_async: the copy stream, the list length's pinned word, a snapshot of the
-  // segment counts (the next sweep rewrites d_wave_counts while the copy reads the snapshot)
+  // The hand-back ring (DESIGN.md §5 "Hand-back"): every compaction writes a slot of its own, in
+  // turn — the step's dense list, its scan offsets ([0] = the length) and group totals, the bitmap
+  // hand-back's {words, records} and, for 2-byte / bitmap lists, the step's records per segment
+  // (the next sweep rewrites d_wave_counts) — tagged with the step it compacted.  So the lists of
+  // the last hb.size() compactions stay readable by step (kwk_fired_fetch_step: every step of a
+  // kwk_step_n call, fused or not), hb[hb_cur] is the engine's last list (kwk_fired*), and a
+  // compaction waits on the device only for the copy of the slot it rewrites.
+  struct HbSlot {
+    void* list = nullptr;
+    size_t list_bytes = 0;
+    uint32_t* offsets = nullptr;
+    uint32_t* groups = nullptr;
+    uint32_t* tot = nullptr;
+    uint32_t* counts = nullptr;
+    hipEvent_t ev_copied = nullptr;  // the copy stream's last copy out of this slot
+    hipEvent_t ev_done = nullptr;    // kwk_fired_keep: recorded after the compaction that wrote the slot
+    int done_slot = -1;              // ... the slot whose ev_done marks it (a fused group's last step)
+    bool copy_pending = false;       // ev_copied recorded and not yet waited for by a compaction
+    bool valid = false;
+    uint64_t step = 0;               // the step whose list the slot holds
+    int mode = 0;                    // enqueue_compact's mode
+    uint32_t n_segs = 0, region_slots = 0;
+  };
+  std::vector<HbSlot> hb = std::vector<HbSlot>(kHbMin);
+  uint32_t hb_cur = 0;
+  bool hb_track = false;       // kwk_fired_keep: compactions record ev_done and write their length to h_len
+  uint32_t* h_len = nullptr;   // pinned, 2 words per slot (the kernels write them: host_len)
+  uint32_t* h_len_dev = nullptr;
+  uint64_t last_step_no = 0;   // the step number of the last sweep's (last) step
   hipStream_t copy_stream = nullptr;
-  hipEvent_t ev_count = nullptr, ev_copied = nullptr;
+  hipEvent_t ev_count = nullptr;  // kwk_fired_fetch_async without kwk_fired_keep: the length's copy
   uint32_t* h_count = nullptr;
-  uint32_t* d_counts_snap = nullptr;
-  bool copy_pending = false;   // the next compaction waits for ev_copied
-  // the list buffer double-buffered once fetched: a compaction whose buffer is still being copied
-  // moves to the other (waiting only for that one's copy), so step k + 1's compaction does not
-  // wait for step k's copy; the *_alt fields swap with their current counterparts
-  kwk_fired_rec* d_compact_alt = nullptr;
-  uint32_t* d_counts_snap_alt = nullptr;
-  hipEvent_t ev_copied_alt = nullptr;
-  bool copy_pending_alt = false;
-  bool copy_recorded = false;  // ev_copied was recorded (kwk_fired_fetch_wait)
+  bool copy_recorded = false;  // a copy was enqueued (kwk_fired_fetch_wait)
   kwk_sweep_info last_sweep{};  // kwk_last_sweep
   bool loaded_table = false;
   uint32_t n_stages = 0, n_classes = 0;
@@ -4393,35 +4384,12 @@ struct kwk_engine {
   uint32_t lut_n = 0, lut_bytes = 0, lut_rest = 0;
   kwk_delta* d_deltas = nullptr;
   kwk_fired_rec* d_fired = nullptr;
-  kwk_fired_rec* d_compact = nullptr;
-  // folded hand-back (kwk_step_n / _pair with KWK_COMPACT_PACKED16 when the 1-byte sweep runs one
-  // tile per workgroup and the hand-back would be one launch: the strong-scaling shards): a step's
-  // 2-byte list is copied by the NEXT step's sweep into d_fold; the call's last step is compacted
-  // as usual.  fold_pending: the last sweep's list awaits the next sweep (its counts in
-  // d_wave_counts, swapped into d_counts_prev when that sweep starts)
-  bool fold_hb = true;  // KWK_TUNE_FOLD_HB
-  bool fold_now = false;
-  bool fold_pending = false;
-  bool fold_valid = false;     // d_fold holds the list of the step before the last (kwk_fired_fold16)
-  uint16_t* d_fold = nullptr;
   // up to fuse_steps steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kSteps>):
   // steps 1.. segments and counts, rotated with d_fired / d_wave_counts by the steps' hand-backs
   uint32_t fuse_steps = kMaxFuseSteps;
   kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
   uint32_t* d_countsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
-  // ... and the 2-byte hand-backs of all but the group's last step (one launch for the group):
-  // their lists, offsets and scan-group totals
-  uint16_t* d_listx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
-  uint32_t* d_offsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
-  uint32_t* d_groupsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
-  uint32_t* d_fold_n = nullptr;
-  uint32_t* d_counts_prev = nullptr;
-  uint32_t* d_btot = nullptr;       // records per workgroup of the last one-tile sweep8 (2-byte records)
-  uint32_t* d_btot_prev = nullptr;  // ... of the one before (swapped with d_btot as the counts)
   uint32_t* d_wave_counts = nullptr;
-  uint32_t* d_wave_offsets = nullptr;
-  uint32_t* d_seg_groups = nullptr;   // seg_scan_kernel's per-group totals
-  uint32_t* d_hb_tot = nullptr;       // the bitmap hand-back's {words, records}
   uint32_t* d_bits_wc = nullptr;      // ... its words per segment
   uint32_t* d_bits_bsum = nullptr;    // ... its records per workgroup of bits_size_kernel
   unsigned long long* d_cum = nullptr;
@@ -4878,6 +4846,15 @@ extern "C" {
 
 const char* kwk_last_error(const kwk_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
 
+// ------------------------------------------------------------------ hand-back ring
+static void hb_free(kwk_engine::HbSlot& h) {
+  for (void* p : {h.list, (void*)h.offsets, (void*)h.groups, (void*)h.tot, (void*)h.counts})
+    if (p) hipFree(p);
+  for (hipEvent_t ev : {h.ev_copied, h.ev_done})
+    if (ev) hipEventDestroy(ev);
+  h = kwk_engine::HbSlot{};
+}
+
 kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   if (!d || !out) return fail(KWK_EINVAL, "null argument");
   if (d->capacity == 0) return fail(KWK_EINVAL, "capacity must be > 0");
@@ -4924,13 +4901,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_lut, sizeof(uint32_t) * kLutTables);
   ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
                                               (size_t)kBlock * kMaxObjPerThread));
-  ALLOC(e->d_compact, sizeof(kwk_fired_rec) * (size_t)e->capacity);
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
-  ALLOC(e->d_wave_offsets, sizeof(uint32_t) * (n_waves + 1));
-  ALLOC(e->d_btot, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
-  ALLOC(e->d_btot_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap + 4));
-  ALLOC(e->d_seg_groups, sizeof(uint32_t) * (n_waves / kScanGroup + 2));
-  ALLOC(e->d_hb_tot, 64);
   ALLOC(e->d_bits_wc, sizeof(uint32_t) * (n_waves + 4));
   ALLOC(e->d_bits_bsum, sizeof(uint32_t) * (n_waves / kSegsPerBlock + 4));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
@@ -4945,7 +4916,6 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   hipMemsetAsync(e->d_due, 0, sizeof(int64_t) * (size_t)e->capacity, e->stream);
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
-  hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
@@ -4971,11 +4941,11 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   }
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
+  if (e->copy_stream) hipStreamSynchronize(e->copy_stream);
+  for (kwk_engine::HbSlot& h : e->hb) hb_free(h);
   void* ptrs[] = {e->d_firedx[0], e->d_firedx[1], e->d_firedx[2], e->d_countsx[0], e->d_countsx[1], e->d_countsx[2],
-                  e->d_listx[0], e->d_listx[1], e->d_listx[2], e->d_offsx[0], e->d_offsx[1], e->d_offsx[2],
-                  e->d_groupsx[0], e->d_groupsx[1], e->d_groupsx[2],
-                  e->d_hb_tot, e->d_bits_wc, e->d_bits_bsum, e->d_fold, e->d_fold_n, e->d_counts_prev, e->d_btot, e->d_btot_prev, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_compact, e->d_wave_counts, e->d_wave_offsets, e->d_seg_groups, e->d_cum, e->d_stats,
+                  e->d_bits_wc, e->d_bits_bsum, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+                  e->d_wave_counts, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
@@ -4986,12 +4956,9 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (e->d_tick_ptr) hipFree(e->d_tick_ptr);
   if (e->ev_lease) hipEventDestroy(e->ev_lease);
   if (e->ev_podsync) hipEventDestroy(e->ev_podsync);
-  if (e->copy_stream) hipStreamSynchronize(e->copy_stream);
-  for (hipEvent_t ev : {e->ev_count, e->ev_copied, e->ev_copied_alt})
-    if (ev) hipEventDestroy(ev);
+  if (e->ev_count) hipEventDestroy(e->ev_count);
   if (e->h_count) hipHostFree(e->h_count);
-  for (void* p : {(void*)e->d_counts_snap, (void*)e->d_counts_snap_alt, (void*)e->d_compact_alt})
-    if (p) hipFree(p);
+  if (e->h_len) hipHostFree(e->h_len);
   if (e->copy_stream) hipStreamDestroy(e->copy_stream);
   for (auto ev : e->events) hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
@@ -5155,10 +5122,6 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
-      return KWK_OK;
-    case KWK_TUNE_FOLD_HB:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FOLD_HB: 0 or 1");
-      e->fold_hb = value != 0;
       return KWK_OK;
     case KWK_TUNE_FUSE_STEPS:
       if (value > kMaxFuseSteps || value == 3) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2 or 4");
@@ -5417,12 +5380,6 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
   a.fsm_bits = 0;
   a.dw_epoch_old = e->fmt.epoch;
   a.dw_rebase = 0;
-  a.fold_out = e->d_fold;
-  a.fold_counts = e->d_counts_prev;
-  a.fold_n = e->d_fold_n;
-  a.fold_prev = e->fold_now ? 1u : 0u;
-  a.btot_out = e->d_btot;
-  a.fold_btot = e->d_btot_prev;
   return a;
 }
 
@@ -5472,7 +5429,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
   e->compacted = false;
   e->last_sweep = kwk_sweep_info{};
-  if (!e->fold_now) e->fold_valid = false;  // d_fold no longer holds the list before the last
+  e->last_step_no = step + (steps ? steps - 1 : 0);
   if (e->n_active == 0) { e->last_blocks = 0; e->steps += steps; return KWK_OK; }
   SweepArgs a = sweep_args(e, now_ns, seed, step, fire);
   const bool nar = e->fmt.narrow != 0;
@@ -5654,60 +5611,110 @@ kwk_status kwk_sync(kwk_engine* e) {
   return KWK_OK;
 }
 
-// fired hand-back on the device: per-(tile, wave) counts -> exclusive scan -> dense list in
-// d_compact, total at d_wave_offsets[n_waves] (enqueue only)
+// fired hand-back on the device: per-(tile, wave) counts -> exclusive scan -> dense list in the
+// next ring slot, its length at the slot's offsets[0] (enqueue only)
 // mode: 0 kwk_fired_rec, 1 packed 4-byte records, 2 the 2-byte records where the sweep wrote them
-// (else the 4-byte packed ones)
+// (else the 4-byte packed ones), 3 the bitmap hand-back (likewise)
+
+// the ring slot `k` compactions after the engine's last list
+static uint32_t hb_next(const kwk_engine* e, uint32_t k = 1) { return (e->hb_cur + k) % (uint32_t)e->hb.size(); }
+
+// bytes of a slot's list in `mode` at the engine's capacity (the bitmap hand-back: at most
+// 1 + 8 + 64 + 128 words per 2048-slot segment)
+static size_t hb_list_bytes(const kwk_engine* e, int mode) {
+  if (mode == 3) return 4u * ((size_t)e->n_blocks_cap * kWavesPerBlock * 201u + 64u);
+  const size_t rb = mode == 2 ? 2u : mode == 1 ? 4u : sizeof(kwk_fired_rec);
+  return rb * (size_t)e->capacity + 64u;
+}
+
+// slot i made ready for a compaction in `mode` on `stream`: the copy stream's last copy out of it
+// waited for on the device, its buffers (re)sized
+static kwk_status hb_prepare(kwk_engine* e, uint32_t i, int mode, hipStream_t stream) {
+  kwk_engine::HbSlot& h = e->hb[i];
+  if (h.copy_pending) {
+    HIP_TRY(hipStreamWaitEvent(stream, h.ev_copied, 0));
+    h.copy_pending = false;
+  }
+  const size_t need = hb_list_bytes(e, mode);
+  if (h.list_bytes < need) {
+    if (h.list) HIP_TRY(hipFree(h.list));  // (synchronises the device: no copy or kernel still reads it)
+    h.list = nullptr;
+    h.list_bytes = 0;
+    HIP_TRY(hipMalloc(&h.list, need));
+    h.list_bytes = need;
+  }
+  if (!h.offsets) {
+    const size_t n_waves = (size_t)e->n_blocks_cap * kWavesPerBlock;
+    HIP_TRY(hipMalloc((void**)&h.offsets, sizeof(uint32_t) * (n_waves + 4)));
+    HIP_TRY(hipMalloc((void**)&h.groups, sizeof(uint32_t) * (n_waves / kScanGroup + 4)));
+    HIP_TRY(hipMalloc((void**)&h.tot, 64));
+    HIP_TRY(hipMalloc((void**)&h.counts, sizeof(uint32_t) * (n_waves + 4)));
+  }
+  if (e->hb_track && !h.ev_done) HIP_TRY(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming));
+  return KWK_OK;
+}
+
+// slot i now holds step `step`'s list (written by the compaction just enqueued on `stream`)
+static kwk_status hb_commit(kwk_engine* e, uint32_t i, uint64_t step, int mode, uint32_t n_segs, int done_slot,
+                            hipStream_t stream, bool record) {
+  kwk_engine::HbSlot& h = e->hb[i];
+  h.valid = true;
+  h.step = step;
+  h.mode = mode;
+  h.n_segs = n_segs;
+  h.region_slots = n_segs ? 64u * e->last_objs << e->last_region_shift : 0u;
+  h.done_slot = done_slot;
+  e->hb_cur = i;
+  if (e->hb_track && record) HIP_TRY(hipEventRecord(h.ev_done, stream));
+  return KWK_OK;
+}
+
+static void hb_args(const kwk_engine* e, uint32_t i, int mode, CompactArgs& a) {
+  const kwk_engine::HbSlot& h = e->hb[i];
+  a.out = reinterpret_cast<kwk_fired_rec*>(h.list);
+  a.offsets = h.offsets;
+  a.group_tot = h.groups;
+  a.counts_out = mode == 2 ? h.counts : nullptr;
+  a.host_len = e->hb_track ? e->h_len_dev + 2u * i : nullptr;
+  a.n_segs = e->last_blocks * kWavesPerBlock;
+  a.seg_region_shift = e->last_region_shift;
+  a.region_slots = 64u * e->last_objs << e->last_region_shift;
+  a.stride = 64u * e->last_objs + 32u;
+}
+
 static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t stream = nullptr) {
   if (!stream) stream = e->stream;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if ((mode == 2 || mode == 3) && e->last_rec != kRecId8Half) mode = 1;
   const bool packed = mode == 1;
-  if (e->copy_pending && e->d_compact_alt) {  // kwk_fired_fetch_async is copying this buffer: the other one
-    std::swap(e->d_compact, e->d_compact_alt);
-    std::swap(e->d_counts_snap, e->d_counts_snap_alt);
-    std::swap(e->ev_copied, e->ev_copied_alt);
-    std::swap(e->copy_pending, e->copy_pending_alt);
-  }
-  if (e->copy_pending) {  // ... still copying the list this rewrites
-    HIP_TRY(hipStreamWaitEvent(stream, e->ev_copied, 0));
-    e->copy_pending = false;
-  }
+  const uint32_t i = hb_next(e);
+  if (kwk_status st = hb_prepare(e, i, mode, stream)) return st;
+  kwk_engine::HbSlot& h = e->hb[i];
   e->compacted = true;
   e->compacted_packed = packed;
   e->compacted_16 = mode == 2;
   e->compacted_bits = mode == 3;
   if (n_waves == 0) {  // nothing swept: the device list is empty (never the previous step's count)
-    HIP_TRY(hipMemsetAsync(e->d_wave_offsets, 0, sizeof(uint32_t), stream));
-    HIP_TRY(hipMemsetAsync(e->d_hb_tot, 0, 2 * sizeof(uint32_t), stream));
-    return KWK_OK;
+    HIP_TRY(hipMemsetAsync(h.offsets, 0, sizeof(uint32_t), stream));
+    HIP_TRY(hipMemsetAsync(h.tot, 0, 2 * sizeof(uint32_t), stream));
+    if (e->hb_track) HIP_TRY(hipMemsetAsync(e->h_len_dev + 2u * i, 0, 2 * sizeof(uint32_t), stream));
+    return hb_commit(e, i, e->last_step_no, mode, 0, (int)i, stream, true);
   }
   const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
   CompactArgs a;
   a.fired32 = reinterpret_cast<const uint32_t*>(e->d_fired);
   a.counts = e->d_wave_counts;
-  a.offsets = e->d_wave_offsets;
-  a.group_tot = e->d_seg_groups;
-  a.out = e->d_compact;
-  a.n_segs = n_waves;
-  a.seg_region_shift = e->last_region_shift;
-  a.region_slots = 64u * e->last_objs << e->last_region_shift;
-  a.stride = 64u * e->last_objs + 32u;
+  hb_args(e, i, mode, a);
   const int rk = e->last_rec;
   void* args[] = {&a};
+  const uint32_t groups = (n_waves + kScanGroup - 1) / kScanGroup;
   if (mode == 2 && n_waves <= e->compact_small) {
     hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, stream, a);
-    HIP_TRY(hipGetLastError());
-    return KWK_OK;
-  }
-  if (mode == 3 && n_waves <= e->compact_small) {
+  } else if (mode == 3 && n_waves <= e->compact_small) {
     hipLaunchKernelGGL(bits_size_kernel, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum);
     hipLaunchKernelGGL(bits_write_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum,
-                       e->d_hb_tot);
-    HIP_TRY(hipGetLastError());
-    return KWK_OK;
-  }
-  if (mode != 2 && n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
+                       h.tot);
+  } else if (mode != 2 && mode != 3 && n_waves <= e->compact_small) {  // one launch: prefix sums inside the expansion
     const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_small_kernel<kRecId8Half, true>
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8, true>
                                                 : (const void*)compact_small_kernel<kRecSlot, true>)
@@ -5715,38 +5722,32 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
                               : rk == kRecId8   ? (const void*)compact_small_kernel<kRecId8>
                                                 : (const void*)compact_small_kernel<kRecSlot>);
     HIP_TRY(hipLaunchKernel(k, dim3(blocks), dim3(kBlock), args, 0, stream));
-    return KWK_OK;
-  }
-  const uint32_t groups = (n_waves + kScanGroup - 1) / kScanGroup;
-  if (mode == 3) {
+  } else if (mode == 3) {
     hipLaunchKernelGGL(bits_size_kernel, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum);
-    hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_bits_wc, n_waves, e->d_wave_offsets,
-                       e->d_seg_groups);
+    hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_bits_wc, n_waves, h.offsets, h.groups);
     hipLaunchKernelGGL(bits_write_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum,
-                       e->d_hb_tot);
-    HIP_TRY(hipGetLastError());
-    return KWK_OK;
+                       h.tot);
+  } else {
+    hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves, h.offsets,
+                       h.groups);
+    if (mode == 2) {
+      constexpr uint32_t W16 = kCompact16Spw;
+      hipLaunchKernelGGL(compact16_kernel<W16>, dim3((n_waves + W16 * kWavesPerBlock - 1) / (W16 * kWavesPerBlock)),
+                         dim3(kBlock), 0, stream, a);
+    } else {
+      constexpr uint32_t W = kCompactSpw;
+      const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, true, W>
+                                : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, true, W>
+                                                  : (const void*)compact_kernel<kRecSlot, true, W>)
+                             : (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, false, W>
+                                : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, false, W>
+                                                  : (const void*)compact_kernel<kRecSlot, false, W>);
+      const uint32_t eblocks = (n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock);
+      HIP_TRY(hipLaunchKernel(k, dim3(eblocks), dim3(kBlock), args, 0, stream));
+    }
   }
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(groups), dim3(kBlock), 0, stream, e->d_wave_counts, n_waves,
-                     e->d_wave_offsets, e->d_seg_groups);
-  constexpr uint32_t W = kCompactSpw;
-  if (mode == 2) {
-    constexpr uint32_t W16 = kCompact16Spw;
-    hipLaunchKernelGGL(compact16_kernel<W16>, dim3((n_waves + W16 * kWavesPerBlock - 1) / (W16 * kWavesPerBlock)),
-                       dim3(kBlock), 0, stream, a);
-    HIP_TRY(hipGetLastError());
-    return KWK_OK;
-  }
-  const void* k = packed ? (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, true, W>
-                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, true, W>
-                                              : (const void*)compact_kernel<kRecSlot, true, W>)
-                         : (rk == kRecId8Half ? (const void*)compact_kernel<kRecId8Half, false, W>
-                            : rk == kRecId8   ? (const void*)compact_kernel<kRecId8, false, W>
-                                              : (const void*)compact_kernel<kRecSlot, false, W>);
-  const uint32_t eblocks = (n_waves + W * kWavesPerBlock - 1) / (W * kWavesPerBlock);
-  HIP_TRY(hipLaunchKernel(k, dim3(eblocks), dim3(kBlock), args, 0, stream));
   HIP_TRY(hipGetLastError());
-  return KWK_OK;
+  return hb_commit(e, i, e->last_step_no, mode, n_waves, (int)i, stream, true);
 }
 
 kwk_status kwk_fired_compact(kwk_engine* e) {
@@ -5766,15 +5767,24 @@ kwk_status kwk_fired_compact_packed(kwk_engine* e) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = packed_ok(e)) return st;
   if (kwk_status st = set_dev(e)) return st;
-  return enqueue_compact(e, true);
+  return enqueue_compact(e, 1);
 }
 
 kwk_status kwk_fired_packed_device(kwk_engine* e, const uint32_t** recs, const uint32_t** count) {
   ErrScope es_(e);
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
   if (!e->compacted || !e->compacted_packed) return fail(KWK_ESTATE, "kwk_fired_compact_packed must follow kwk_step");
-  *recs = reinterpret_cast<const uint32_t*>(e->d_compact);
-  *count = e->d_wave_offsets;
+  *recs = reinterpret_cast<const uint32_t*>(e->hb[e->hb_cur].list);
+  *count = e->hb[e->hb_cur].offsets;
+  return KWK_OK;
+}
+
+// the length (or the bitmap hand-back's {words, records}) of the engine's last list (synchronises)
+static kwk_status hb_len(kwk_engine* e, uint32_t* t) {
+  const kwk_engine::HbSlot& h = e->hb[e->hb_cur];
+  HIP_TRY(hipMemcpyAsync(t, h.mode == 3 ? h.tot : h.offsets, h.mode == 3 ? 2 * sizeof(uint32_t) : sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 
@@ -5786,14 +5796,13 @@ kwk_status kwk_fired_packed(kwk_engine* e, uint32_t* out, uint32_t cap, uint32_t
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) { *n_out = 0; return KWK_OK; }
   if (!e->compacted || !e->compacted_packed)
-    if (kwk_status st = enqueue_compact(e, true)) return st;
+    if (kwk_status st = enqueue_compact(e, 1)) return st;
   uint32_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (kwk_status st = hb_len(e, &total)) return st;
   *n_out = total;
   if (!out || total == 0) return KWK_OK;
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
-  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out, e->hb[e->hb_cur].list, sizeof(uint32_t) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
@@ -5826,13 +5835,12 @@ kwk_status kwk_fired_bits(kwk_engine* e, uint32_t* out, uint64_t cap_words, uint
     if (kwk_status st = enqueue_compact(e, 3)) return st;
   }
   uint32_t t[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(t, e->d_hb_tot, sizeof(t), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (kwk_status st = hb_len(e, t)) return st;
   *n_words = t[0];
   *n_records = t[1];
   if (!out) return KWK_OK;
   if (t[0] > cap_words) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(t[0]) + " words");
-  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint32_t) * (size_t)t[0], hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out, e->hb[e->hb_cur].list, sizeof(uint32_t) * (size_t)t[0], hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
@@ -5859,54 +5867,32 @@ kwk_status kwk_fired_packed16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32
     if (kwk_status st = enqueue_compact(e, 2)) return st;
   }
   uint32_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (kwk_status st = hb_len(e, &total)) return st;
   *n_out = total;
   if (!out && !seg_counts) return KWK_OK;
   if (out && total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
   if (seg_counts && n_waves > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(n_waves));
-  if (out && total) HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, e->stream));
+  const kwk_engine::HbSlot& h = e->hb[e->hb_cur];
+  if (out && total) HIP_TRY(hipMemcpyAsync(out, h.list, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, e->stream));
   if (seg_counts)
-    HIP_TRY(hipMemcpyAsync(seg_counts, e->d_wave_counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(seg_counts, h.counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return KWK_OK;
 }
 
 // one step of kwk_step_n / _pair: the sweep (bracketed by events ev_a, ev_a + 1 when ev_a >= 0),
-// then the hand-back.  (The hand-back of step k on a side stream overlapping the sweep of step
-// k + 1, segments double-buffered, measured slower: 80.1-80.8 vs 78.4-78.7 us per C5 step, the
-// persistent sweep holding the CUs the two latency-bound launches then wait for; r5p / r5r)
-// fold: the call may fold its steps' hand-backs; last: the call's last step (always compacted)
-static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1,
-                           bool fold = false, bool last = true) {
-  if (e->fold_pending) {  // this sweep copies the previous step's list; it writes its counts to the other buffer
-    std::swap(e->d_wave_counts, e->d_counts_prev);
-    std::swap(e->d_btot, e->d_btot_prev);
-    e->fold_now = true;
-  }
+// then the hand-back into the next ring slot.  (The hand-back of step k on a side stream
+// overlapping the sweep of step k + 1, segments double-buffered, measured slower: 80.1-80.8 vs
+// 78.4-78.7 us per C5 step, the persistent sweep holding the CUs the two latency-bound launches
+// then wait for; r5p / r5r.  Round 5's folded hand-back — the next sweep copying a step's 2-byte
+// list — is superseded by fused steps at the shard size and was removed in round 6.)
+static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1) {
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
-  const kwk_status sst = launch_sweep(e, now, seed, step, true);
-  const bool folded = e->fold_now && e->fmt.byte && e->last_sweep.persistent == 0 && e->last_rec == kRecId8Half;
-  e->fold_now = false;
-  e->fold_pending = false;
-  if (sst) return sst;
-  if (folded) e->fold_valid = true;
+  if (kwk_status st = launch_sweep(e, now, seed, step, true)) return st;
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
   if (!compact) return KWK_OK;
-  const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
-  if (fold && !last && e->fold_hb && compact == KWK_COMPACT_PACKED16 && e->fmt.byte && e->last_rec == kRecId8Half &&
-      e->last_sweep.persistent == 0 && n_waves > 0 && n_waves <= e->compact_small) {
-    if (!e->d_fold) {
-      HIP_TRY(hipMalloc((void**)&e->d_fold, sizeof(uint16_t) * (size_t)e->capacity + 64));
-      HIP_TRY(hipMalloc((void**)&e->d_fold_n, 64));
-      HIP_TRY(hipMalloc((void**)&e->d_counts_prev, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 4)));
-    }
-    e->compacted = false;  // this step's list: copied by the next sweep
-    e->fold_pending = true;
-    return KWK_OK;
-  }
   return enqueue_compact(e, compact_mode(compact));
 }
 
@@ -5916,8 +5902,7 @@ static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t s
 // a launch takes: 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
 // sample per launch (ev_every 2 or 3: pairs; 1: none fused)
 static uint32_t fuse_group(const kwk_engine* e, uint32_t left, uint32_t ev_every) {
-  if (e->fuse_steps < 2 || !e->fmt.byte || e->n_stages > 4 || e->fsm8_due_any || !e->loaded_table || e->fold_pending ||
-      ev_every == 1)
+  if (e->fuse_steps < 2 || !e->fmt.byte || e->n_stages > 4 || e->fsm8_due_any || !e->loaded_table || ev_every == 1)
     return 1;
   uint32_t m = e->fuse_steps;
   if (ev_every && ev_every < 4) m = 2;
@@ -5925,10 +5910,11 @@ static uint32_t fuse_group(const kwk_engine* e, uint32_t left, uint32_t ev_every
   return m ? m : 1;
 }
 
-// steps k .. k + m - 1 of kwk_step_n / _pair (now, now + dt, ...) in one launch, then each step's
-// hand-back in turn: step 0's from d_fired, then each next step's, its segments rotated into
-// d_fired / d_wave_counts (the last step's stay there: the engine's last step); ev_a brackets the
-// launch (the sample of whichever step it is)
+// steps k .. k + m - 1 of kwk_step_n / _pair (now, now + dt, ...) in one launch, then every step's
+// hand-back into a ring slot of its own (the next m slots, in step order, so each step's list stays
+// readable by kwk_fired_fetch_step): step 0's segments in d_fired, step s's in d_firedx[s - 1],
+// rotated so that the last step's stay in d_fired / d_wave_counts (the engine's last step); ev_a
+// brackets the launch (the sample of whichever step it is)
 static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt, uint64_t seed, uint64_t step,
                              uint32_t compact, int ev_a) {
   for (uint32_t i = 0; i + 1 < m; ++i) {
@@ -5937,9 +5923,6 @@ static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt,
     HIP_TRY(hipMalloc((void**)&e->d_firedx[i], sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
                                                                          (size_t)kBlock * kMaxObjPerThread)));
     HIP_TRY(hipMalloc((void**)&e->d_countsx[i], sizeof(uint32_t) * (n_waves + 4)));
-    HIP_TRY(hipMalloc((void**)&e->d_listx[i], sizeof(uint16_t) * (size_t)e->capacity + 64));
-    HIP_TRY(hipMalloc((void**)&e->d_offsx[i], sizeof(uint32_t) * (n_waves + 4)));
-    HIP_TRY(hipMalloc((void**)&e->d_groupsx[i], sizeof(uint32_t) * (n_waves / kScanGroup + 4)));
   }
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
@@ -5947,23 +5930,17 @@ static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt,
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
-  if (compact == KWK_COMPACT_PACKED16 && e->last_rec == kRecId8Half && n_waves && !e->copy_pending) {
+  if (compact == KWK_COMPACT_PACKED16 && e->last_rec == kRecId8Half && n_waves) {
     // the steps' 2-byte hand-backs in one launch (two: scan + expansion, past compact_small
-    // segments), blockIdx.y = the step: all but the last into the group's own lists, the last into
-    // the engine's (kwk_fired_packed16 reads it), each step's segments and counts as it swept them
+    // segments), blockIdx.y = the step, step i's list into ring slot hb_next(i + 1)
     CompactArgs4 c4;
+    for (uint32_t i = 0; i < m; ++i)
+      if (kwk_status st = hb_prepare(e, hb_next(e, i + 1), 2, e->stream)) return st;
     for (uint32_t i = 0; i < m; ++i) {
       CompactArgs& a = c4.a[i];
-      const bool last = i + 1 == m;
       a.fired32 = reinterpret_cast<const uint32_t*>(i ? e->d_firedx[i - 1] : e->d_fired);
       a.counts = i ? e->d_countsx[i - 1] : e->d_wave_counts;
-      a.offsets = last ? e->d_wave_offsets : e->d_offsx[i];
-      a.group_tot = last ? e->d_seg_groups : e->d_groupsx[i];
-      a.out = last ? e->d_compact : reinterpret_cast<kwk_fired_rec*>(e->d_listx[i]);
-      a.n_segs = n_waves;
-      a.seg_region_shift = e->last_region_shift;
-      a.region_slots = 64u * e->last_objs << e->last_region_shift;
-      a.stride = 64u * e->last_objs + 32u;
+      hb_args(e, hb_next(e, i + 1), 2, a);
     }
     const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
     if (n_waves <= e->compact_small) {
@@ -5980,6 +5957,11 @@ static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt,
       std::swap(e->d_fired, e->d_firedx[i - 1]);
       std::swap(e->d_wave_counts, e->d_countsx[i - 1]);
     }
+    const uint32_t last = hb_next(e, m);
+    for (uint32_t i = 0; i < m; ++i) {
+      const uint32_t slot = hb_next(e, 1);  // hb_commit advances hb_cur: slots in step order
+      if (kwk_status st = hb_commit(e, slot, step + i, 2, n_waves, (int)last, e->stream, i + 1 == m)) return st;
+    }
     e->compacted = true;
     e->compacted_packed = false;
     e->compacted_16 = true;
@@ -5992,9 +5974,12 @@ static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt,
       std::swap(e->d_wave_counts, e->d_countsx[i - 1]);
       e->compacted = false;
     }
-    if (compact)
+    if (compact) {
+      e->last_step_no = step + i;  // the tag of this step's list
       if (kwk_status st = enqueue_compact(e, compact_mode(compact))) return st;
+    }
   }
+  e->last_step_no = step + m - 1;
   return KWK_OK;
 }
 
@@ -6025,8 +6010,7 @@ kwk_status kwk_step_n(kwk_engine* e, uint32_t n, int64_t now0_ns, int64_t dt_ns,
       k += m;
       continue;
     }
-    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev_of(ev_every, j), true,
-                                 k + 1 == n))
+    if (kwk_status st = step_one(e, now0_ns + (int64_t)k * dt_ns, seed, step0 + k, compact, ev_of(ev_every, j)))
       return st;
     ++k;
   }
@@ -6051,13 +6035,12 @@ kwk_status kwk_step_n_pair(kwk_engine* e, kwk_engine* other, uint32_t n, int64_t
     const uint32_t m = fuse_group(e, n - k, ev_every);
     if (m > 1) {
       if (kwk_status st = step_group(e, m, now, dt_ns, seed, step0 + k, compact, ev_of_group(ev_every, j, m))) return st;
-    } else if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev_of(ev_every, j), true, k + 1 == n)) {
+    } else if (kwk_status st = step_one(e, now, seed, step0 + k, compact, ev_of(ev_every, j))) {
       return st;
     }
     // the other engine's step(s) right behind (its own stream): both chains start together
     for (uint32_t i = 0; i < m; ++i)
-      if (kwk_status st = step_one(other, now + (int64_t)i * dt_ns, seed, step0 + k + i, compact, -1, true, k + i + 1 == n))
-        return st;
+      if (kwk_status st = step_one(other, now + (int64_t)i * dt_ns, seed, step0 + k + i, compact, -1)) return st;
     k += m;
   }
   return KWK_OK;
@@ -6068,8 +6051,8 @@ kwk_status kwk_fired_device(kwk_engine* e, const kwk_fired_rec** recs, const uin
   if (!e || !recs || !count) return fail(KWK_EINVAL, "null argument");
   if (!e->compacted || e->compacted_packed || e->compacted_16 || e->compacted_bits)
     return fail(KWK_ESTATE, "kwk_fired_compact must follow kwk_step");
-  *recs = e->d_compact;
-  *count = e->d_wave_offsets;
+  *recs = reinterpret_cast<const kwk_fired_rec*>(e->hb[e->hb_cur].list);
+  *count = e->hb[e->hb_cur].offsets;
   return KWK_OK;
 }
 
@@ -6082,13 +6065,102 @@ kwk_status kwk_fired(kwk_engine* e, kwk_fired_rec* out, uint32_t cap, uint32_t* 
   if (!e->compacted || e->compacted_packed || e->compacted_16 || e->compacted_bits)  // the segments are intact: expand them
     if (kwk_status st = enqueue_compact(e)) return st;
   uint32_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, e->d_wave_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (kwk_status st = hb_len(e, &total)) return st;
   *n_out = total;
   if (!out || total == 0) return KWK_OK;
   if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
-  HIP_TRY(hipMemcpyAsync(out, e->d_compact, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out, e->hb[e->hb_cur].list, sizeof(kwk_fired_rec) * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_fired_keep(kwk_engine* e, uint32_t depth) {
+  ErrScope es_(e);
+  if (!e) return fail(KWK_EINVAL, "null engine");
+  if (depth > kHbMax) return fail(KWK_EINVAL, "kwk_fired_keep: depth 0.." + std::to_string(kHbMax));
+  if (kwk_status st = set_dev(e)) return st;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->copy_stream) HIP_TRY(hipStreamSynchronize(e->copy_stream));
+  const uint32_t slots = depth > kHbMin ? depth : kHbMin;
+  // the engine's last list stays the last (moved to slot 0 of the new ring)
+  kwk_engine::HbSlot cur = e->hb[e->hb_cur];
+  e->hb[e->hb_cur] = kwk_engine::HbSlot{};
+  for (kwk_engine::HbSlot& h : e->hb) hb_free(h);
+  e->hb.assign(slots, kwk_engine::HbSlot{});
+  cur.copy_pending = false;
+  e->hb[0] = cur;
+  e->hb_cur = 0;
+  e->hb_track = depth > 0;
+  if (e->hb_track && !e->h_len) {
+    HIP_TRY(hipHostMalloc((void**)&e->h_len, 2 * sizeof(uint32_t) * kHbMax, hipHostMallocDefault));
+    memset(e->h_len, 0, 2 * sizeof(uint32_t) * kHbMax);
+    HIP_TRY(hipHostGetDevicePointer((void**)&e->h_len_dev, e->h_len, 0));
+  }
+  e->hb[0].done_slot = 0;
+  if (e->hb_track && e->hb[0].offsets) {  // the current list's length where a fetch reads it
+    if (!e->hb[0].ev_done) HIP_TRY(hipEventCreateWithFlags(&e->hb[0].ev_done, hipEventDisableTiming));
+    const bool bits = e->hb[0].mode == 3;
+    e->h_len[1] = 0u;
+    HIP_TRY(hipMemcpy(e->h_len, bits ? e->hb[0].tot : e->hb[0].offsets, (bits ? 2 : 1) * sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+    HIP_TRY(hipEventRecord(e->hb[0].ev_done, e->stream));
+  }
+  return KWK_OK;
+}
+
+// slot i's list to host memory on the copy stream (kwk_fired_fetch_async / _step)
+static kwk_status hb_fetch(kwk_engine* e, uint32_t i, void* out, uint64_t cap_bytes, uint32_t* seg_counts,
+                           uint32_t seg_cap, kwk_fetch_info* info) {
+  kwk_engine::HbSlot& h = e->hb[i];
+  if (!e->copy_stream) {
+    int prio = 0;
+    HIP_TRY(hipStreamGetPriority(e->stream, &prio));
+    HIP_TRY(hipStreamCreateWithPriority(&e->copy_stream, hipStreamNonBlocking, prio));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_count, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&e->h_count, 64, hipHostMallocDefault));
+  }
+  if (!h.ev_copied) HIP_TRY(hipEventCreateWithFlags(&h.ev_copied, hipEventDisableTiming));
+  const bool bits = h.mode == 3, b16 = h.mode == 2;
+  const uint32_t rb = bits ? 4u : b16 ? 2u : h.mode == 1 ? 4u : (uint32_t)sizeof(kwk_fired_rec);
+  const bool segs = b16 && seg_counts && h.n_segs;
+  if (segs && h.n_segs > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(h.n_segs));
+  uint32_t t[2] = {0u, 0u};
+  hipEvent_t done = nullptr;
+  if (e->hb_track && h.done_slot >= 0 && e->hb[h.done_slot].ev_done) {
+    // the compaction that wrote the slot signals its own end; its kernels wrote the length here
+    done = e->hb[h.done_slot].ev_done;
+    HIP_TRY(hipEventSynchronize(done));
+    t[0] = e->h_len[2u * i];
+    t[1] = e->h_len[2u * i + 1u];
+  } else {
+    // the length behind everything enqueued on the engine's stream so far
+    HIP_TRY(hipMemcpyAsync(e->h_count, bits ? h.tot : h.offsets, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipEventRecord(e->ev_count, e->stream));
+    HIP_TRY(hipEventSynchronize(e->ev_count));
+    done = e->ev_count;
+    t[0] = e->h_count[0];
+    t[1] = e->h_count[1];
+  }
+  if (!h.n_segs) t[0] = t[1] = 0u;
+  const uint32_t total = t[0];  // records, or the bitmap hand-back's 32-bit words
+  info->n_records = bits ? t[1] : total;
+  info->record_bytes = bits ? 0u : rb;
+  info->format = bits ? KWK_COMPACT_BITS : b16 ? KWK_COMPACT_PACKED16 : h.mode == 1 ? KWK_COMPACT_PACKED : 1u;
+  info->bytes = (uint64_t)total * rb;
+  info->step = h.step;
+  if (b16 || bits) {
+    info->n_segs = h.n_segs;
+    info->region_slots = h.region_slots;
+  }
+  if (out && (uint64_t)total * rb > cap_bytes)
+    return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string((uint64_t)total * rb) + " bytes");
+  HIP_TRY(hipStreamWaitEvent(e->copy_stream, done, 0));
+  if (out && total) HIP_TRY(hipMemcpyAsync(out, h.list, (size_t)total * rb, hipMemcpyDeviceToHost, e->copy_stream));
+  if (segs)
+    HIP_TRY(hipMemcpyAsync(seg_counts, h.counts, sizeof(uint32_t) * h.n_segs, hipMemcpyDeviceToHost, e->copy_stream));
+  HIP_TRY(hipEventRecord(h.ev_copied, e->copy_stream));
+  h.copy_pending = true;
+  e->copy_recorded = true;
   return KWK_OK;
 }
 
@@ -6101,75 +6173,29 @@ kwk_status kwk_fired_fetch_async(kwk_engine* e, void* out, uint64_t cap_bytes, u
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
   if (n_waves == 0) return KWK_OK;
   if (!e->compacted) return fail(KWK_ESTATE, "kwk_fired_fetch_async needs the step's list compacted (kwk_fired_compact*)");
-  if (!e->copy_stream) {
-    int prio = 0;
-    HIP_TRY(hipStreamGetPriority(e->stream, &prio));
-    HIP_TRY(hipStreamCreateWithPriority(&e->copy_stream, hipStreamNonBlocking, prio));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_count, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_copied, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_copied_alt, hipEventDisableTiming));
-    HIP_TRY(hipMalloc((void**)&e->d_compact_alt, sizeof(kwk_fired_rec) * (size_t)e->capacity));
-    HIP_TRY(hipMalloc((void**)&e->d_counts_snap_alt, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
-    HIP_TRY(hipHostMalloc((void**)&e->h_count, 64, hipHostMallocDefault));
-    HIP_TRY(hipMalloc((void**)&e->d_counts_snap, sizeof(uint32_t) * ((size_t)e->n_blocks_cap * kWavesPerBlock + 1)));
-  }
-  const bool bits = e->compacted_bits;
-  const uint32_t rb = bits ? 4u : e->compacted_16 ? 2u : e->compacted_packed ? 4u : (uint32_t)sizeof(kwk_fired_rec);
-  const bool segs = e->compacted_16 && seg_counts;
-  if (segs && n_waves > seg_cap) return fail(KWK_ECAP, "segment buffer too small: need " + std::to_string(n_waves));
-  // the length (and the segment counts) behind the compaction on the engine's stream; only the
-  // length is waited for here
-  HIP_TRY(hipMemcpyAsync(e->h_count, bits ? e->d_hb_tot : e->d_wave_offsets, 2 * sizeof(uint32_t),
-                         hipMemcpyDeviceToHost, e->stream));
-  if (segs)
-    HIP_TRY(hipMemcpyAsync(e->d_counts_snap, e->d_wave_counts, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToDevice,
-                           e->stream));
-  HIP_TRY(hipEventRecord(e->ev_count, e->stream));
-  HIP_TRY(hipEventSynchronize(e->ev_count));
-  const uint32_t total = e->h_count[0];  // records, or the bitmap hand-back's 32-bit words
-  info->n_records = bits ? e->h_count[1] : total;
-  info->record_bytes = bits ? 0u : rb;
-  info->format = bits ? KWK_COMPACT_BITS : e->compacted_16 ? KWK_COMPACT_PACKED16 : e->compacted_packed ? KWK_COMPACT_PACKED : 1u;
-  info->bytes = (uint64_t)total * rb;
-  if (e->compacted_16 || bits) {
-    info->n_segs = n_waves;
-    info->region_slots = 64u * e->last_objs << e->last_region_shift;
-  }
-  if (out && (uint64_t)total * rb > cap_bytes)
-    return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string((uint64_t)total * rb) + " bytes");
-  HIP_TRY(hipStreamWaitEvent(e->copy_stream, e->ev_count, 0));
-  if (out && total)
-    HIP_TRY(hipMemcpyAsync(out, e->d_compact, (size_t)total * rb, hipMemcpyDeviceToHost, e->copy_stream));
-  if (segs)
-    HIP_TRY(hipMemcpyAsync(seg_counts, e->d_counts_snap, sizeof(uint32_t) * n_waves, hipMemcpyDeviceToHost,
-                           e->copy_stream));
-  HIP_TRY(hipEventRecord(e->ev_copied, e->copy_stream));
-  e->copy_pending = true;
-  e->copy_recorded = true;
-  return KWK_OK;
+  return hb_fetch(e, e->hb_cur, out, cap_bytes, seg_counts, seg_cap, info);
 }
 
-kwk_status kwk_fired_fold16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32_t* n_out) {
+kwk_status kwk_fired_fetch_step(kwk_engine* e, uint64_t step, void* out, uint64_t cap_bytes, uint32_t* seg_counts,
+                                uint32_t seg_cap, kwk_fetch_info* info) {
   ErrScope es_(e);
-  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  if (!e || !info) return fail(KWK_EINVAL, "null argument");
   if (kwk_status st = set_dev(e)) return st;
-  if (!e->fold_valid || !e->d_fold) return fail(KWK_ESTATE, "no folded list: the last kwk_step_n did not fold");
-  uint32_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, e->d_fold_n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  *n_out = total;
-  if (!out || total == 0) return KWK_OK;
-  if (total > cap) return fail(KWK_ECAP, "fired buffer too small: need " + std::to_string(total));
-  HIP_TRY(hipMemcpyAsync(out, e->d_fold, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  return KWK_OK;
+  memset(info, 0, sizeof(*info));
+  const uint32_t n = (uint32_t)e->hb.size();
+  for (uint32_t k = 0; k < n; ++k) {  // newest first
+    const uint32_t i = (e->hb_cur + n - k) % n;
+    if (e->hb[i].valid && e->hb[i].step == step) return hb_fetch(e, i, out, cap_bytes, seg_counts, seg_cap, info);
+  }
+  return fail(KWK_ESTATE, "no kept list of step " + std::to_string(step) + " (the ring holds the last " +
+                              std::to_string(n) + " compactions: kwk_fired_keep)");
 }
 
 kwk_status kwk_fired_fetch_wait(kwk_engine* e) {
   ErrScope es_(e);
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
-  if (e->copy_recorded) HIP_TRY(hipStreamSynchronize(e->copy_stream));  // both buffers' copies
+  if (e->copy_recorded) HIP_TRY(hipStreamSynchronize(e->copy_stream));  // every slot's copies
   return KWK_OK;
 }
 
@@ -7276,7 +7302,7 @@ kwk_status kwk_event_elapsed(kwk_engine* e, uint32_t a, uint32_t b, float* ms) {
   return KWK_OK;
 }
 
-uint32_t kwk_abi_version(void) { return 1u; }
+uint32_t kwk_abi_version(void) { return KWK_ABI_VERSION; }
 uint32_t kwk_tile_objects(void) { return (uint32_t)(kBlock * kMinObjPerThread); }
 
 }  // extern "C"

@@ -19,7 +19,6 @@
 using kwkjson::JV;
 
 struct kwk_metric_set {
-  std::string err;
   std::vector<kwk_metric_desc> metrics;
   std::vector<kwk_metric_op> ops;
   std::vector<kwk_histogram_desc> hists;
@@ -221,7 +220,12 @@ void compile(kwk_metric_set& M, const JV& cr) {
 
 extern "C" {
 
-const char* kwk_metric_set_last_error(const kwk_metric_set* m) { return m ? m->err.c_str() : g_err.c_str(); }
+// every failing entry point records its message in the calling thread's g_err (a set's own calls
+// never fail after it is built), so the message is g_err whatever `m` is
+const char* kwk_metric_set_last_error(const kwk_metric_set* m) {
+  (void)m;
+  return g_err.c_str();
+}
 
 kwk_status kwk_compile_metrics(const char* metric_json, kwk_metric_set** out) {
   if (!metric_json || !out) return fail(KWK_EINVAL, "null argument");

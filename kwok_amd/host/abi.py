@@ -77,9 +77,10 @@ class StepStats(C.Structure):
 
 
 class FetchInfo(C.Structure):
-    """kwk_fetch_info (kwk_fired_fetch_async)."""
+    """kwk_fetch_info (kwk_fired_fetch_async / kwk_fired_fetch_step)."""
     _fields_ = [("n_records", C.c_uint32), ("record_bytes", C.c_uint32), ("n_segs", C.c_uint32),
-                ("region_slots", C.c_uint32), ("format", C.c_uint32), ("reserved", C.c_uint32), ("bytes", C.c_uint64)]
+                ("region_slots", C.c_uint32), ("format", C.c_uint32), ("reserved", C.c_uint32), ("bytes", C.c_uint64),
+                ("step", C.c_uint64)]
 
 
 class SweepInfo(C.Structure):
@@ -105,7 +106,6 @@ TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15
-TUNE_FOLD_HB = 16
 TUNE_FUSE_STEPS = 17
 
 
@@ -181,8 +181,9 @@ EXPORTS = [
     "kwk_last_sweep", "kwk_tick_bind", "kwk_tick", "kwk_tick_n", "kwk_histograms_load", "kwk_histograms_eval",
     "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
     "kwk_fired_packed16", "kwk_fired_fetch_async", "kwk_fired_fetch_wait",
-    "kwk_fired_fold16", "kwk_fired_compact_bits", "kwk_fired_bits",
+    "kwk_fired_compact_bits", "kwk_fired_bits", "kwk_fired_keep", "kwk_fired_fetch_step",
 ]
+ABI_VERSION = 2  # KWK_ABI_VERSION of include/kwok_engine.h: the library must match the structs above
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
 TICK_COMPACT_PACKED = 1 << 1  # KWK_TICK_COMPACT_PACKED
 COMPACT_PACKED = 2  # kwk_step_n compact = KWK_COMPACT_PACKED
@@ -252,7 +253,9 @@ def lib():
     L.kwk_fired_compact_bits.argtypes = [C.c_void_p]
     L.kwk_fired_bits.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, _p(C.c_uint64), _p(C.c_uint32), _p(C.c_uint32),
                                  _p(C.c_uint32)]
-    L.kwk_fired_fold16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, _p(C.c_uint32)]
+    L.kwk_fired_keep.argtypes = [C.c_void_p, C.c_uint32]
+    L.kwk_fired_fetch_step.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                       _p(FetchInfo)]
     L.kwk_alloc_host.argtypes = [C.c_uint64, _p(C.c_void_p)]
     L.kwk_free_host.argtypes = [C.c_void_p]
     L.kwk_set_tuning.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
@@ -291,6 +294,9 @@ def lib():
         fn = getattr(L, name)
         if name not in ("kwk_last_error", "kwk_abi_version", "kwk_tile_objects"):
             fn.restype = s
+    if L.kwk_abi_version() != ABI_VERSION:
+        raise EngineError(f"{LIB_PATH}: ABI version {L.kwk_abi_version()}, this binding needs {ABI_VERSION} "
+                          "(rebuild: python -m kwok_amd.build)")
     _lib = L
     return L
 

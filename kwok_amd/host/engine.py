@@ -300,16 +300,21 @@ class Engine:
         """kwk_fired_fetch_wait: the last fetch's copies are in the host buffers."""
         self._check(abi.lib().kwk_fired_fetch_wait(self.h), "kwk_fired_fetch_wait")
 
-    def fired_fold16(self) -> np.ndarray:
-        """kwk_fired_fold16: the 2-byte list of the step before the last of the last kwk_step_n, as
-        the next step's sweep copied it (abi.EngineError KWK_ESTATE when that call did not fold)."""
-        n = C.c_uint32()
-        L = abi.lib()
-        self._check(L.kwk_fired_fold16(self.h, None, 0, C.byref(n)), "kwk_fired_fold16")
-        out = np.zeros(n.value, dtype=np.uint16)
-        if n.value:
-            self._check(L.kwk_fired_fold16(self.h, abi.ptr(out), n.value, C.byref(n)), "kwk_fired_fold16")
-        return out
+    def fired_keep(self, depth: int):
+        """kwk_fired_keep: keep the lists of the last `depth` compactions readable by step
+        (fetch_step), each compaction signalling its own completion."""
+        self._check(abi.lib().kwk_fired_keep(self.h, depth), "kwk_fired_keep")
+
+    def fetch_step(self, step: int, out: "PinnedBuffer", counts: Optional["PinnedBuffer"] = None) -> dict:
+        """kwk_fired_fetch_step: step `step`'s list (any step of a kwk_step_n call still in the ring)
+        copied into `out` / `counts` on the copy stream, as fetch_async; the buffers hold it after
+        fetch_wait()."""
+        info = abi.FetchInfo()
+        self._check(abi.lib().kwk_fired_fetch_step(self.h, step, out.p, out.nbytes,
+                                                  counts.p if counts is not None else None,
+                                                  counts.nbytes // 4 if counts is not None else 0, C.byref(info)),
+                    "kwk_fired_fetch_step")
+        return {k: getattr(info, k) for k, _ in abi.FetchInfo._fields_}
 
     def fired_bits(self):
         """The last step's list as per-segment fired maps + 2-bit stage codes (kwk_fired_bits) ->

@@ -58,6 +58,10 @@ def cel_lower(expr: str, dimension: str) -> List[Tuple[int, float]]:
     cap = 256
     ops = (abi.MetricOp * cap)()
     st = L.kwk_cel_lower(expr.encode(), DIMS.get(dimension, 3), ops, cap, C.byref(n))
+    if st == abi.KWK_ECAP and n.value > cap:  # a longer program: *n_ops = the length it needs
+        cap = n.value
+        ops = (abi.MetricOp * cap)()
+        st = L.kwk_cel_lower(expr.encode(), DIMS.get(dimension, 3), ops, cap, C.byref(n))
     if st == KWK_ENOLOWER:
         raise cel.LowerError(L.kwk_metric_set_last_error(None).decode(errors="replace"))
     if st != 0:

@@ -101,6 +101,71 @@ def test_c5_persistent_table_sweep_sampled_oracle(state):
         eng.close()
 
 
+@pytest.mark.parametrize("n", [40_000_000, 12_500_000])
+def test_c5_fused_steps_every_step_sampled_oracle(n):
+    """The headline kernel as the bench runs it: `sweep8_kernel<..., 4>`, four
+    steps per launch over the C5 pod shape — 40M pods on the persistent grid, 12.5M (the N = 8
+    shard) one tile per workgroup — stepped by kwk_step_n calls of 10 steps (launches of 4 + 4 + 2
+    steps, each launch's 2-byte hand-backs in one launch), and EVERY step's list read by step
+    through the hand-back ring (kwk_fired_keep + kwk_fired_fetch_step) and decoded on the host: the
+    fired records of every ~9973rd slot must equal `OracleSim` stepped one step at a time, at each
+    of the 20 steps; after each call the sampled objects' states equal the oracle's."""
+    from bench import shard_pod_variants
+    from kwok_amd import workload as W
+    from kwok_amd.host import abi
+    from kwok_amd.host.compiler import HarnessSpec, KindProgram
+    from kwok_amd.host.engine import Engine, Ingest, PinnedBuffer
+    from kwok_amd.host.stages import load_stage_files
+    from oracle.next_ref import load_stage_docs
+    from oracle.sim import OracleSim
+    files = W.stage_paths(W.POD_FAST)
+    pvars = [W.pod_object("p", "n"), W.pod_object("p", "n", job=True)]
+    prog = KindProgram(load_stage_files(*files), HarnessSpec())
+    prog.explore(pvars)
+    ing = Ingest(prog)
+    idx = shard_pod_variants(0, n, SEED, 0.1)
+    hot, dels, rec, cls = ing.variant_columns(pvars, idx)
+    eng = Engine(prog, capacity=n, state="auto")
+    bufs = [(PinnedBuffer(2 * n + 64), PinnedBuffer(4 * (n // 2048 + 64))) for _ in range(10)]
+    try:
+        eng.load_stages()
+        eng.set_harness(True)
+        eng.load(hot, dels, rec, cls, ing.record_array())
+        del hot, dels, rec, cls
+        eng.fired_keep(10)
+        slots = list(range(3, n, 9973))
+        sample = np.asarray(slots, dtype=np.int64)
+        sim = OracleSim(load_stage_docs(*files), [pvars[int(idx[s])] for s in slots], harness=True, slots=slots)
+        total = 0
+        for call in range(2):
+            k0 = 10 * call
+            eng.step_n(10, NOW0 + k0 * 10**9, 10**9, SEED, k0, "packed16")
+            info = eng.last_sweep()
+            assert info["kernel"] == abi.SWEEP_8 and info["steps"] == 2, info
+            assert info["persistent"] == (1 if n == 40_000_000 else 0), info
+            infos = [eng.fetch_step(k0 + j, *bufs[j]) for j in range(10)]
+            eng.fetch_wait()
+            for j, fi in enumerate(infos):
+                k = k0 + j
+                out, cnt = bufs[j]
+                slot, stage, flags = abi.fired16_decode(out.array(np.uint16, fi["n_records"]),
+                                                        cnt.array(np.uint32, fi["n_segs"]), fi["region_slots"])
+                assert len(np.unique(slot)) == len(slot), f"step {k}: a slot fired twice"
+                sel = np.isin(slot.astype(np.int64), sample)
+                got = sorted(zip(slot[sel].tolist(), stage[sel].tolist(), flags[sel].tolist()))
+                exp = sorted(sim.step(NOW0 + k * 10**9, SEED, k))
+                assert got == exp, f"step {k}: device-only {sorted(set(got) - set(exp))[:6]} oracle-only " \
+                                   f"{sorted(set(exp) - set(got))[:6]}"
+                total += len(exp)
+            compare_state(prog, eng, sim, k0 + 9, rows=_rows_at(eng, slots))
+        assert total > len(slots)
+    finally:
+        eng.close()
+        for x in bufs:
+            for p in x:
+                p.close()
+
+
 @pytest.mark.parametrize("state", ["u32", "auto"])
 def test_c2_word_sweep_sampled_oracle(state):
     """C2 stage mix (pod-general + chaos: weighted picks, jitter draws, value records, the

@@ -546,41 +546,68 @@ def test_fetch_async_equals_sync_readback():
                     p.close()
 
 
-def test_folded_handback_equals_compacted_list():
-    """kwk_step_n with KWK_COMPACT_PACKED16 on a small 1-byte engine (one tile per workgroup): the
-    steps before the call's last are not compacted, the next sweep copies their 2-byte lists
-    (kwk_fired_fold16).  That list equals kwk_fired_packed16 of a twin engine stepped one step per
-    call — step 0 (every pod fires: segments past 512 records, the copy's tail loop) and a later
-    step — and the call's last step is compacted as before; no fold after a one-step call or with
-    KWK_TUNE_FOLD_HB = 0."""
+@pytest.mark.parametrize("n_nodes,mode", [(250_000, "16"), (250_000, "bits"), (20_000, "16")])
+def test_fused_call_every_step_list_equals_per_step_calls(n_nodes, mode):
+    """Every step's hand-back of a fused kwk_step_n call: 10 steps in one call
+    sweep as launches of 4 + 4 + 2 steps, each launch's hand-backs in one launch, and every step's
+    list lands in a ring slot of its own (kwk_fired_keep).  kwk_fired_fetch_step(k) for each of the
+    10 steps — all fetched before one wait, the copies overlapping the later steps — must equal the
+    list of the same step from per-step kwk_step + compaction calls of an unfused twin: the 2-byte
+    records with their per-segment counts (25M pods: persistent grid, scan + expansion pair; 2M:
+    one-tile grid, one-launch prefix) and the bitmap hand-back (25M).  The lists' transitions add up
+    to the fired count (n_host == fired), a step the ring no longer holds is refused, and the
+    call's last list is still the engine's (kwk_fired_packed16)."""
     from kwok_amd.host import abi
+    from kwok_amd.host.engine import PinnedBuffer
     now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
-    one = {abi.TUNE_FUSE_STEPS: 0}  # one step per launch: the fold is the unfused steps' hand-back
-    (_, a), (_, b), (_, c) = (_pods("auto", n_nodes=20_000, tuning=one), _pods("auto", n_nodes=20_000, tuning=one),
-                              _pods("auto", n_nodes=20_000, tuning={abi.TUNE_FOLD_HB: 0, **one}))
+    compact = "packed16" if mode == "16" else "bits"
+    (_, ref), (_, f) = _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 0}), _pods("auto", n_nodes=n_nodes)
+    cap = f.capacity
+    bufs = [(PinnedBuffer(2 * cap + 64), PinnedBuffer(4 * (cap // 2048 + 64))) for _ in range(10)]
     try:
-        ref = []
-        for k in range(5):
-            a.step_n(1, now0 + k * dt, dt, seed, k, "packed16")
-            recs, segc, _ = a.fired_packed16()
-            ref.append(recs)
-            if k == 0:
-                assert segc.max() > 512, segc.max()
-        assert a.last_sweep()["persistent"] == 0
-        b.step_n(2, now0, dt, seed, 0, "packed16")
-        assert np.array_equal(b.fired_fold16(), ref[0])
-        assert np.array_equal(b.fired_packed16()[0], ref[1])
-        b.step_n(3, now0 + 2 * dt, dt, seed, 2, "packed16")
-        assert np.array_equal(b.fired_fold16(), ref[3])
-        assert np.array_equal(b.fired_packed16()[0], ref[4])
-        assert np.array_equal(b.read()[0]["pred"], a.read()[0]["pred"])
-        for e, n in ((b, 1), (c, 2)):
-            e.step_n(n, now0 + 5 * dt, dt, seed, 5, "packed16")
-            with pytest.raises(abi.EngineError, match="did not fold"):
-                e.fired_fold16()
+        exp = []
+        for k in range(10):
+            ref.step(now0 + k * dt, seed, k)
+            ref.fired_compact(mode)
+            exp.append(ref.fired_packed16()[:2] if mode == "16" else ref.fired_bits())
+        f.fired_keep(16)
+        fired0 = f.stats()["fired"]
+        f.step_n(10, now0, dt, seed, 0, compact)
+        assert f.last_sweep()["steps"] == 2  # groups 4 | 4 | 2
+        infos = [f.fetch_step(k, *bufs[k]) for k in range(10)]
+        f.fetch_wait()
+        n_host = 0
+        for k, info in enumerate(infos):
+            out, cnt = bufs[k]
+            assert info["step"] == k
+            if mode == "16":
+                recs, segc = exp[k]
+                assert info["format"] == abi.COMPACT_PACKED16 and info["n_records"] == len(recs), k
+                assert np.array_equal(out.array(np.uint16, info["n_records"]), recs), k
+                assert np.array_equal(cnt.array(np.uint32, info["n_segs"]), segc), k
+            else:
+                words, n_tr, ns, _ = exp[k]
+                assert info["format"] == abi.COMPACT_BITS and info["n_records"] == n_tr and info["n_segs"] == ns, k
+                assert np.array_equal(out.array(np.uint32, info["bytes"] // 4), words), k
+            n_host += info["n_records"]
+        assert n_host == f.stats()["fired"] - fired0 and n_host > 0
+        assert f.stats()["fired"] == ref.stats()["fired"]
+        if mode == "16":
+            assert np.array_equal(f.fired_packed16()[0], exp[9][0])
+        # a 4-deep ring holds the last 4 compactions only
+        f.fired_keep(4)
+        f.step_n(10, now0 + 10 * dt, dt, seed, 10, compact)
+        for k in (16, 17, 18, 19):
+            f.fetch_step(k, *bufs[k - 16])
+        f.fetch_wait()
+        with pytest.raises(abi.EngineError, match="no kept list of step 15"):
+            f.fetch_step(15, *bufs[4])
     finally:
-        for e in (a, b, c):
+        for e in (ref, f):
             e.close()
+        for x in bufs:
+            for p in x:
+                p.close()
 
 
 def test_fused_records_load_read_step_at_4m_pods():

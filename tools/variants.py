@@ -102,19 +102,19 @@ VARIANTS = {
     "id8b2": [("constexpr uint32_t kId8Batch = 4;", "constexpr uint32_t kId8Batch = 2;")],
     # fused word sweep capped at 6 waves per SIMD instead of 5 (the round-4 default)
     "lb6": [("constexpr int kDwMinBlocks = 5;", "constexpr int kDwMinBlocks = 6;")],
-    # the hand-back launched after every step of kwk_step_n (no fold into the next sweep)
-    "nofoldhb": [("  bool fold_hb = true;", "  bool fold_hb = false;")],
     # sweep8 cost isolation (the shard-size step, --c5 --c5-nodes 125000): no phase 2 (no LDS passes,
     # no fires) / no statistics atomics at the end / no phase-3 line stores / an empty kernel
     "s8_nop2": [("    if (n_work) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile",
                  "    if (n_work && a.n == 0u) {  // wave-uniform\n      // ---- phase 2: the ids to the LDS tile")],
     "s8_nostat": [("    if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);\n"
-                   "  }\n  if (!kPersist && kStages4",
+                   "  }\n}\n\n// ------------------------------------------------------------------ 4- and 8-byte state sweep",
                    "    if (val && a.n == 0u) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], "
-                   "(unsigned long long)val);\n  }\n  if (!kPersist && kStages4")],
+                   "(unsigned long long)val);\n  }\n}\n\n// ------------------------------------------------------------------ 4- and 8-byte state sweep")],
     "s8_nop3": [("st ? wbase + (uint32_t)q * 1024u + lane * 16u : kOOB, 0, 2 /* nt */);", "kOOB, 0, 2 /* nt */);")],
-    "s8_empty": [("  __shared__ uint32_t s_fold[2 * kWavesPerBlock];  // fold: per wave the records before the block / its count\n",
-                  "  __shared__ uint32_t s_fold[2 * kWavesPerBlock];\n  if (a.n != 0xFFFFFFFFu) return;\n")],
+    "s8_empty": [("  __shared__ unsigned int s_stat[kStatWords];\n  const uint32_t lane = threadIdx.x & 63;\n"
+                  "  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);",
+                  "  __shared__ unsigned int s_stat[kStatWords];\n  if (a.n != 0xFFFFFFFFu) return;\n  const uint32_t lane = threadIdx.x & 63;\n"
+                  "  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n  const uint32_t n_tiles = (uint32_t)(((uint64_t)a.n + kTile - 1) / kTile);")],
     # word sweep: one workgroup per tile / 2 / 4 / 8 tiles per workgroup (a loop over tiles, the LDS
     # set-up once, the next tile's stream in flight)
     "tpb1": [("  uint32_t word_tpb = 0;", "  uint32_t word_tpb = 1;")],
