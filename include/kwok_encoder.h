@@ -52,6 +52,17 @@ kwk_status kwk_encoder_add_classes(kwk_encoder* enc, const char* classes_json);
 /* the interned records so far: n_records x (slots) kwk_value, for kwk_load / kwk_set_records */
 kwk_status kwk_encoder_records(kwk_encoder* enc, kwk_value* out, uint32_t cap, uint32_t* n_records);
 
+/* expression.NewQuery + Query.Execute (pkg/utils/expression/query.go:33-69) of one jq query on one
+ * JSON document (taken as ToJSONStandard would hand it over: no presence rewriting), with the
+ * native jq subset the encoder runs for Stage selector keys and *From getters (kwok_amd/csrc/jqc.hpp:
+ * paths, pipes, comma, `//`, and / or / not, comparisons, arithmetic, literals, [..], {..}, if, try,
+ * assignments, length / has / keys / select / map / ... ).  out <- the outputs as a JSON array
+ * (nulls dropped; gojq ints as integers, float64 numbers as gojq encodes them) or `null` for the nil
+ * result of a runtime error; NUL-terminated, *n_out = its length (KWK_ECAP: cap too small).
+ * KWK_EINVAL: the query is outside the subset (the message names the construct) — the Go host then
+ * keeps the reference lifecycle for that resourceRef. */
+kwk_status kwk_jq_eval(const char* query, const char* json, char* out, uint32_t cap, uint32_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -221,8 +221,10 @@ Stage stage_from_v1alpha1(const JV& obj) {
   return st;
 }
 
-// ------------------------------------------------------------------ jq step programs
-// kwok_amd/host/encoder.py query_steps (_SEG / _SELECT): field / iter / select_eq joined by |
+// ------------------------------------------------------------------ jq queries
+// Selector keys and *From getters compile with the native jq subset (jqc.hpp, through
+// kwkhost::compile_query); the encoder spec carries each query's source, which the encoder
+// compiles the same way.
 bool sp(char c) { return kwktpl::is_space(c); }
 
 std::string strip(const std::string& s) { return kwktpl::py_strip(s); }
@@ -234,186 +236,6 @@ std::string json_body(const std::string& body) {
   kwkjson::Parser P{q.data(), q.data() + q.size()};
   if (!P.value(v) || v.t != JV::STR) throw CompileError("bad string in query: " + body);
   return v.s;
-}
-
-// _SEG at i: \.?\[\s*"(...)"\s*\] | \.(ident) | \.?\[\s*\] | \.(?=\s*$)
-bool seg_at(const std::string& s, size_t i, size_t& end, int& kind, std::string& val) {
-  size_t j = i;
-  // alternative 1 / 3: \.?\[ ...
-  {
-    size_t k = j;
-    if (k < s.size() && s[k] == '.') ++k;
-    if (k < s.size() && s[k] == '[') {
-      size_t q = k + 1;
-      while (q < s.size() && sp(s[q])) ++q;
-      if (q < s.size() && s[q] == '"') {
-        size_t r = q + 1;
-        while (r < s.size() && s[r] != '"') r += s[r] == '\\' ? 2 : 1;
-        if (r < s.size()) {
-          size_t t = r + 1;
-          while (t < s.size() && sp(s[t])) ++t;
-          if (t < s.size() && s[t] == ']') {
-            kind = 1;
-            val = json_body(s.substr(q + 1, r - q - 1));
-            end = t + 1;
-            return true;
-          }
-        }
-      }
-    }
-  }
-  if (j < s.size() && s[j] == '.' && j + 1 < s.size() && kwktpl::is_alpha_(s[j + 1])) {
-    size_t k = j + 2;
-    while (k < s.size() && kwktpl::is_alnum_(s[k])) ++k;
-    kind = 2;
-    val = s.substr(j + 1, k - j - 1);
-    end = k;
-    return true;
-  }
-  {
-    size_t k = j;
-    if (k < s.size() && s[k] == '.') ++k;
-    if (k < s.size() && s[k] == '[') {
-      size_t q = k + 1;
-      while (q < s.size() && sp(s[q])) ++q;
-      if (q < s.size() && s[q] == ']') {
-        kind = 3;
-        end = q + 1;
-        return true;
-      }
-    }
-  }
-  if (j < s.size() && s[j] == '.') {
-    size_t k = j + 1;
-    while (k < s.size() && sp(s[k])) ++k;
-    if (k == s.size()) {
-      kind = 4;
-      end = j + 1;
-      return true;
-    }
-  }
-  return false;
-}
-
-struct QStep {
-  std::string op;  // field / iter / select_eq
-  std::string key;
-  std::vector<std::string> path;
-  JV lit;
-};
-
-std::vector<QStep> q_path(const std::string& src0, const std::string& whole) {
-  std::vector<QStep> steps;
-  const std::string s = strip(src0);
-  if (s == ".") return steps;
-  size_t i = 0;
-  while (i < s.size()) {
-    size_t end;
-    int kind;
-    std::string val;
-    if (!seg_at(s, i, end, kind, val) || end == i) throw CompileError("jq construct not supported natively: '" + whole + "'");
-    if (kind == 1 || kind == 2) steps.push_back({"field", val, {}, JV()});
-    else if (kind == 3) steps.push_back({"iter", "", {}, JV()});
-    i = end;
-    while (i < s.size() && s[i] == ' ') ++i;
-  }
-  return steps;
-}
-
-bool q_select(const std::string& part, std::string& path, JV& lit) {
-  // ^select\s*\(\s*(?P<path>[^=]+?)\s*==\s*(?P<lit>"..."|true|false|null|-?\d+(?:\.\d+)?)\s*\)$
-  if (part.rfind("select", 0) != 0) return false;
-  size_t i = 6;
-  while (i < part.size() && sp(part[i])) ++i;
-  if (i >= part.size() || part[i] != '(') return false;
-  ++i;
-  while (i < part.size() && sp(part[i])) ++i;
-  const size_t eq = part.find('=', i);
-  if (eq == std::string::npos || eq == i || eq + 1 >= part.size() || part[eq + 1] != '=') return false;
-  path = kwktpl::py_rstrip(part.substr(i, eq - i));
-  if (path.empty()) return false;
-  size_t j = eq + 2;
-  while (j < part.size() && sp(part[j])) ++j;
-  size_t e = j;
-  if (j < part.size() && part[j] == '"') {
-    e = j + 1;
-    while (e < part.size() && part[e] != '"') e += part[e] == '\\' ? 2 : 1;
-    if (e >= part.size()) return false;
-    ++e;
-  } else if (part.compare(j, 4, "true") == 0 || part.compare(j, 4, "null") == 0) {
-    e = j + 4;
-  } else if (part.compare(j, 5, "false") == 0) {
-    e = j + 5;
-  } else {
-    if (e < part.size() && part[e] == '-') ++e;
-    const size_t d0 = e;
-    while (e < part.size() && kwktpl::is_digit(part[e])) ++e;
-    if (e == d0) return false;
-    if (e + 1 < part.size() && part[e] == '.' && kwktpl::is_digit(part[e + 1])) {
-      ++e;
-      while (e < part.size() && kwktpl::is_digit(part[e])) ++e;
-    }
-  }
-  const std::string lt = part.substr(j, e - j);
-  size_t k = e;
-  while (k < part.size() && sp(part[k])) ++k;
-  if (k >= part.size() || part[k] != ')' || k + 1 != part.size()) return false;
-  kwkjson::Parser P{lt.data(), lt.data() + lt.size()};
-  if (!P.value(lit)) throw CompileError("bad literal in select: " + lt);
-  return true;
-}
-
-std::vector<QStep> query_steps(const std::string& src) {
-  std::vector<QStep> steps;
-  size_t p = 0;
-  for (;;) {
-    const size_t bar = src.find('|', p);
-    const std::string part = strip(src.substr(p, bar == std::string::npos ? std::string::npos : bar - p));
-    std::string path;
-    JV lit;
-    if (q_select(part, path, lit)) {
-      std::vector<QStep> sub = q_path(path, src);
-      QStep s{"select_eq", "", {}, lit};
-      for (const QStep& x : sub) {
-        if (x.op != "field") throw CompileError("select over a non-path: '" + src + "'");
-        s.path.push_back(x.key);
-      }
-      steps.push_back(std::move(s));
-    } else if (!part.empty() && part[0] == '.') {
-      for (QStep& x : q_path(part, src)) steps.push_back(std::move(x));
-    } else {
-      throw CompileError("jq construct not supported natively: '" + src + "'");
-    }
-    if (bar == std::string::npos) break;
-    p = bar + 1;
-  }
-  return steps;
-}
-
-kwkhost::Query to_query(const std::vector<QStep>& steps) {
-  kwkhost::Query q;
-  for (const QStep& s : steps) {
-    kwkhost::Step st;
-    if (s.op == "field") { st.op = 'F'; st.key = s.key; }
-    else if (s.op == "iter") st.op = 'I';
-    else { st.op = 'S'; st.path = s.path; st.lit = s.lit; }
-    q.steps.push_back(std::move(st));
-  }
-  return q;
-}
-
-PJ steps_pj(const std::vector<QStep>& steps) {
-  PJ l = PJ::list();
-  for (const QStep& s : steps) {
-    if (s.op == "field") l.push(PJ::list({PJ::str("field"), PJ::str(s.key)}));
-    else if (s.op == "iter") l.push(PJ::list({PJ::str("iter")}));
-    else {
-      PJ path = PJ::list();
-      for (const std::string& k : s.path) path.push(PJ::str(k));
-      l.push(PJ::list({PJ::str("select_eq"), path, kwkpatch::pj_of(s.lit)}));
-    }
-  }
-  return l;
 }
 
 // compiler.path_prefix: the leading static path of a query
@@ -462,10 +284,23 @@ std::vector<std::string> path_prefix(const std::string& src) {
   return out;
 }
 
+// compiler._norm: the query without whitespace outside its string literals (the feature / slot key)
 std::string norm(const std::string& s) {
   std::string o;
-  for (char c : s)
-    if (!sp(c)) o += c;
+  bool in_str = false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    const char c = s[i];
+    if (in_str) {
+      o += c;
+      if (c == '\\' && i + 1 < s.size()) o += s[++i];
+      else if (c == '"') in_str = false;
+    } else if (c == '"') {
+      in_str = true;
+      o += c;
+    } else if (!sp(c)) {
+      o += c;
+    }
+  }
   return o;
 }
 
@@ -588,8 +423,7 @@ struct kwk_program {
 
   struct Feature {
     std::string src;
-    std::vector<QStep> steps;
-    kwkhost::Query q;
+    kwkhost::CQuery q;
     int present_bit = -1;
     std::vector<std::pair<std::string, int>> lit_bits;
     uint32_t mask() const {
@@ -604,7 +438,6 @@ struct kwk_program {
   std::vector<std::pair<std::string, int>> fin_bits;
   int fin_other_bit = -1;
   std::vector<std::pair<std::string, std::string>> slots;  // (type, src)
-  std::vector<std::vector<QStep>> slot_steps;
   std::map<std::pair<std::string, std::string>, int> slot_index;
   std::vector<kwk_stage_desc> desc;
 
@@ -638,8 +471,11 @@ struct kwk_program {
     if (it != features.end()) return it->second;
     Feature f;
     f.src = src;
-    f.steps = query_steps(src);
-    f.q = to_query(f.steps);
+    try {
+      f.q = kwkhost::compile_query(src);
+    } catch (const kwkjq::Unsupported& e) {
+      throw CompileError(e.what());
+    }
     feature_order.push_back(key);
     return features.emplace(key, std::move(f)).first->second;
   }
@@ -690,8 +526,12 @@ struct kwk_program {
     if (it != slot_index.end()) return it->second;
     const int id = (int)slots.size();
     slot_index[key] = id;
+    try {
+      kwkhost::compile_query(src);
+    } catch (const kwkjq::Unsupported& e) {
+      throw CompileError(e.what());
+    }
     slots.emplace_back(typ, src);
-    slot_steps.push_back(query_steps(src));
     return id;
   }
 
@@ -845,14 +685,14 @@ struct kwk_program {
 
   uint32_t pred_of(const JV& obj) {
     uint32_t pred = 0;
-    std::vector<const JV*> out;
+    std::vector<kwkjq::Val> out;
     for (const std::string& key : feature_order) {
       const Feature& f = features.at(key);
-      if (!kwkhost::run_query(f.q, &obj, out) || out.empty()) continue;
+      if (!kwkhost::exec_query(f.q, obj, out) || out.empty()) continue;
       if (f.present_bit >= 0) pred |= 1u << f.present_bit;
       for (const auto& lb : f.lit_bits)
-        for (const JV* d : out)
-          if ((d->t == JV::BOOL && (d->b ? "true" : "false") == lb.first) || (d->t == JV::STR && d->s == lb.first)) {
+        for (const kwkjq::Val& d : out)
+          if (kwkjq::has_value(*d.p, lb.first)) {
             pred |= 1u << lb.second;
             break;
           }
@@ -1084,7 +924,7 @@ struct kwk_program {
       PJ lit = PJ::dict();
       for (const auto& lb : f.lit_bits) lit.set(lb.first, PJ::integer(lb.second));
       feats.push(PJ::dict()
-                     .set("steps", steps_pj(f.steps))
+                     .set("query", PJ::str(f.src))
                      .set("present_bit", f.present_bit < 0 ? PJ::null() : PJ::integer(f.present_bit))
                      .set("literals", lit));
     }
@@ -1092,7 +932,7 @@ struct kwk_program {
     for (const auto& fb : fin_bits) fins.set(fb.first, PJ::integer(fb.second));
     PJ sl = PJ::list();
     for (size_t i = 0; i < slots.size(); ++i)
-      sl.push(PJ::dict().set("type", PJ::str(slots[i].first)).set("steps", steps_pj(slot_steps[i])));
+      sl.push(PJ::dict().set("type", PJ::str(slots[i].first)).set("query", PJ::str(slots[i].second)));
     PJ cls = PJ::dict();
     for (size_t i = 0; i < class_keys.size(); ++i) cls.set(class_keys[i], PJ::integer((long long)i));
     PJ im = PJ::list();

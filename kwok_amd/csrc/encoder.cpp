@@ -316,13 +316,13 @@ int64_t f64_to_i64(double x) {
 struct kwk_encoder {
   std::string err;  // message of the last failing call on this handle
   struct Feature {
-    Query q;
+    CQuery q;
     int32_t present_bit = -1;
     std::vector<std::pair<std::string, uint32_t>> lits;
   };
   struct Slot {
     bool duration = false;
-    Query q;
+    CQuery q;
   };
   std::vector<Feature> features;
   std::vector<std::pair<std::string, uint32_t>> fin_bits;
@@ -361,16 +361,16 @@ void encode_one(const kwk_encoder& E, const char* text, uint32_t len, Row& r, kw
   Parser P{text, text + len};
   if (!P.value(obj) || obj.t != JV::OBJ) { r.err = "invalid JSON object"; return; }
   typed_presence(obj);
-  std::vector<const JV*> out;
+  std::vector<kwkjq::Val> out;
   // feature bits (KindProgram.pred_of)
   for (const auto& f : E.features) {
-    if (!run_query(f.q, &obj, out) || out.empty()) continue;
+    if (!exec_query(f.q, obj, out) || out.empty()) continue;
     if (f.present_bit >= 0) r.pred |= 1u << f.present_bit;
     for (const auto& lit : f.lits) {
-      for (const JV* d : out) {
-        // selector.go hasValue: strings, bools via FormatBool; JSON numbers never match
-        if ((d->t == JV::STR && d->s == lit.first) ||
-            (d->t == JV::BOOL && (d->b ? "true" : "false") == lit.first)) {
+      for (const kwkjq::Val& d : out) {
+        // selector.go hasValue: strings, bools via FormatBool, gojq ints via FormatInt; JSON
+        // numbers (float64) never match
+        if (kwkjq::has_value(*d.p, lit.first)) {
           r.pred |= 1u << lit.second;
           break;
         }
@@ -396,15 +396,15 @@ void encode_one(const kwk_encoder& E, const char* text, uint32_t len, Row& r, kw
   bool any = false;
   r.rec.assign(E.slots.size(), kwk_value{0, 0, KWK_V_DEFAULT});
   for (size_t s = 0; s < E.slots.size(); ++s) {
-    if (!run_query(E.slots[s].q, &obj, out) || out.empty()) continue;
-    const JV* t = out[0];
+    if (!exec_query(E.slots[s].q, obj, out) || out.empty()) continue;
+    const JV* t = out[0].p;
     kwk_value& v = r.rec[s];
     if (!E.slots[s].duration) {  // int64From.Get (value_int_from.go:53-81)
       if (t->t == JV::STR) {
         int64_t n;
         if (t->s.empty() || !parse_int(t->s, n)) v = kwk_value{0, 0, KWK_V_NOTOK};
         else v = kwk_value{n, 0, KWK_V_OK};
-      } else if (t->t == JV::NUM) {
+      } else if (t->t == JV::NUM && !kwkjq::is_gint(*t)) {  // float64 (a gojq int: the default)
         v = kwk_value{f64_to_i64(strtod(t->s.c_str(), nullptr)), 0, KWK_V_OK};
       }
     } else {  // durationFrom.Get (value_duration_from.go:53-79)
@@ -453,8 +453,13 @@ kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out) {
   if (!feats || feats->t != JV::ARR) return fail(KWK_EINVAL, "encoder spec: features");
   for (const JV& f : feats->a) {
     kwk_encoder::Feature F;
-    const JV* steps = f.get("steps");
-    if (!steps || !load_query(*steps, F.q)) return fail(KWK_EINVAL, "encoder spec: feature query steps");
+    const JV* src = f.get("query");
+    if (!src || src->t != JV::STR) return fail(KWK_EINVAL, "encoder spec: feature query");
+    try {
+      F.q = compile_query(src->s);
+    } catch (const kwkjq::Unsupported& e) {
+      return fail(KWK_EINVAL, std::string("encoder spec: ") + e.what());
+    }
     const JV* pb = f.get("present_bit");
     F.present_bit = (pb && pb->t == JV::NUM) ? atoi(pb->s.c_str()) : -1;
     if (const JV* lits = f.get("literals"))
@@ -469,8 +474,13 @@ kwk_status kwk_encoder_create(const char* spec_json, kwk_encoder** out) {
       kwk_encoder::Slot S;
       const JV* typ = s.get("type");
       S.duration = typ && typ->t == JV::STR && typ->s == "duration";
-      const JV* steps = s.get("steps");
-      if (!steps || !load_query(*steps, S.q)) return fail(KWK_EINVAL, "encoder spec: slot query steps");
+      const JV* src = s.get("query");
+      if (!src || src->t != JV::STR) return fail(KWK_EINVAL, "encoder spec: slot query");
+      try {
+        S.q = compile_query(src->s);
+      } catch (const kwkjq::Unsupported& e) {
+        return fail(KWK_EINVAL, std::string("encoder spec: ") + e.what());
+      }
       E->slots.push_back(std::move(S));
     }
   if (const JV* cls = spec.get("classes"))
@@ -602,6 +612,35 @@ kwk_status kwk_encoder_records(kwk_encoder* E, kwk_value* out, uint32_t cap, uin
   if (!out || !n) return KWK_OK;
   if (n > cap) return fail(KWK_ECAP, "record buffer too small");
   memcpy(out, E->records.data(), sizeof(kwk_value) * E->records.size());
+  return KWK_OK;
+}
+
+kwk_status kwk_jq_eval(const char* query, const char* json, char* out, uint32_t cap, uint32_t* n_out) {
+  ErrScope es_(nullptr);
+  if (!query || !json || !n_out || (cap && !out)) return fail(KWK_EINVAL, "null argument");
+  JV doc;
+  Parser P{json, json + strlen(json)};
+  if (!P.value(doc)) return fail(KWK_EINVAL, "invalid JSON input");
+  std::string text;
+  try {
+    const CQuery q = compile_query(query);
+    std::vector<kwkjq::Val> res;
+    if (!exec_query(q, doc, res)) {
+      text = "null";
+    } else {
+      text = "[";
+      for (size_t i = 0; i < res.size(); ++i) {
+        if (i) text += ',';
+        kwkjq::encode(text, *res[i].p);
+      }
+      text += "]";
+    }
+  } catch (const kwkjq::Unsupported& e) {
+    return fail(KWK_EINVAL, e.what());
+  }
+  *n_out = (uint32_t)text.size();
+  if (text.size() + 1 > cap) return fail(KWK_ECAP, "output buffer too small: need " + std::to_string(text.size() + 1));
+  memcpy(out, text.c_str(), text.size() + 1);
   return KWK_OK;
 }
 

@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "jqc.hpp"
 #include "json_dom.hpp"
 
 namespace kwkhost {
@@ -137,9 +138,10 @@ inline void canon(std::string& o, const JV& v) {
 }
 
 // ------------------------------------------------------------------ query step programs
-// A query is a list of steps over a stream of values (nullptr = null):
+// The fast path of the jq queries the shipped Stage CRs use (a lowering of the jqc.hpp syntax
+// tree, compile_query below): a list of steps over a stream of values (nullptr = null):
 //   F <key>   .key (null -> null; a non-object -> error)
-//   I         .[] (array items / object values; anything else -> error)
+//   I         .[] (array items / object values in gojq's sorted key order; else -> error)
 //   S <path> <lit>   select(<path> == <lit>) with <path> a list of keys
 // Query.Execute semantics (query.go:48-69): an error makes the result nil; nulls are dropped.
 struct Step {
@@ -177,8 +179,10 @@ inline bool run_query(const Query& q, const JV* root, std::vector<const JV*>& ou
         nxt.push_back(v->get(s.key));
       } else if (s.op == 'I') {
         if (!v) return false;
-        if (v->t == JV::ARR || v->t == JV::OBJ) {
+        if (v->t == JV::ARR) {
           for (const JV& x : v->a) nxt.push_back(&x);
+        } else if (v->t == JV::OBJ) {
+          for (const auto& kv : kwkjq::entries(*v)) nxt.push_back(kv.second);
         } else {
           return false;
         }
@@ -199,6 +203,76 @@ inline bool run_query(const Query& q, const JV* root, std::vector<const JV*>& ou
   out.clear();
   for (const JV* v : cur)
     if (v && v->t != JV::NUL) out.push_back(v);
+  return true;
+}
+
+// A compiled selector key / getter query (expression.NewQuery): the step program when the query
+// lowers to one (path steps and select(path == literal), the forms of kustomize/stage/**), else the
+// jq evaluator (jqc.hpp).  kwkjq::Unsupported for a query outside the native subset.
+struct CQuery {
+  std::shared_ptr<kwkjq::Query> jq;
+  Query steps;
+  bool fast = false;
+};
+
+// a path of fields from `.` (for select's operand)
+inline bool lower_path(const kwkjq::Node& n, std::vector<std::string>& keys) {
+  if (n.k == kwkjq::Node::IDENT) return true;
+  if (n.k != kwkjq::Node::FIELD || !lower_path(*n.a, keys)) return false;
+  keys.push_back(n.name);
+  return true;
+}
+inline bool lower_steps(const kwkjq::Node& n, Query& q) {
+  using K = kwkjq::Node;
+  switch (n.k) {
+    case K::IDENT: return true;
+    case K::FIELD: {
+      if (!lower_steps(*n.a, q)) return false;
+      Step s;
+      s.op = 'F';
+      s.key = n.name;
+      q.steps.push_back(std::move(s));
+      return true;
+    }
+    case K::ITER: {
+      if (!lower_steps(*n.a, q)) return false;
+      Step s;
+      s.op = 'I';
+      q.steps.push_back(std::move(s));
+      return true;
+    }
+    case K::PIPE: return lower_steps(*n.a, q) && lower_steps(*n.b, q);
+    case K::FUNC: {
+      if (n.name != "select" || n.args.size() != 1 || n.args[0]->k != K::CMP || n.args[0]->name != "==") return false;
+      const K& c = *n.args[0];
+      const K* path = c.a.get();
+      const K* lit = c.b.get();
+      if (path->k == K::LIT) std::swap(path, lit);
+      Step s;
+      s.op = 'S';
+      if (lit->k != K::LIT || lit->lit.t == JV::ARR || lit->lit.t == JV::OBJ || !lower_path(*path, s.path)) return false;
+      s.lit = lit->lit;
+      q.steps.push_back(std::move(s));
+      return true;
+    }
+    default: return false;
+  }
+}
+
+inline CQuery compile_query(const std::string& src) {
+  CQuery q;
+  q.jq = std::make_shared<kwkjq::Query>(src);
+  q.fast = lower_steps(*q.jq->root, q.steps);
+  return q;
+}
+
+// Query.Execute on a document (outputs borrow from `doc` or hold computed values)
+inline bool exec_query(const CQuery& q, const JV& doc, std::vector<kwkjq::Val>& out) {
+  if (!q.fast) return q.jq->execute(doc, out);
+  thread_local std::vector<const JV*> raw;
+  out.clear();
+  if (!run_query(q.steps, &doc, raw)) return false;
+  for (const JV* v : raw) out.push_back(kwkjq::Val{v, nullptr});
   return true;
 }
 
@@ -299,35 +373,15 @@ inline void typed_presence(JV& obj, const char* type) {
   }
 }
 
+// Pods and nodes reach the reference's matcher as typed objects (PodController / NodeController);
+// every other kind through the StageController as *unstructured.Unstructured
+// (stage_controller.go:174-232), whose json.Marshal writes the object map as it holds it: every
+// field, zero values and nulls included — so those objects are left as they are.
 inline void typed_presence(JV& obj) {
   const JV* kind = obj.t == JV::OBJ ? obj.get("kind") : nullptr;
   const bool known = kind && kind->t == JV::STR && (kind->s == "Pod" || kind->s == "Node");
-  typed_presence(obj, known ? kind->s.c_str() : "");
+  if (known) typed_presence(obj, kind->s.c_str());
 }
-
-inline bool load_query(const JV& steps, Query& q) {
-  if (steps.t != JV::ARR) return false;
-  for (const JV& s : steps.a) {
-    if (s.t != JV::ARR || s.a.empty() || s.a[0].t != JV::STR) return false;
-    Step st;
-    const std::string& op = s.a[0].s;
-    if (op == "field" && s.a.size() == 2 && s.a[1].t == JV::STR) { st.op = 'F'; st.key = s.a[1].s; }
-    else if (op == "iter" && s.a.size() == 1) { st.op = 'I'; }
-    else if (op == "select_eq" && s.a.size() == 3 && s.a[1].t == JV::ARR) {
-      st.op = 'S';
-      for (const JV& k : s.a[1].a) {
-        if (k.t != JV::STR) return false;
-        st.path.push_back(k.s);
-      }
-      st.lit = s.a[2];
-    } else {
-      return false;
-    }
-    q.steps.push_back(std::move(st));
-  }
-  return true;
-}
-
 
 // compiler.class_key: the spec shape without status, identity metadata, node placement;
 // ownerReferences reduced to their sorted kinds (kwok_amd/host/compiler.py class_key)

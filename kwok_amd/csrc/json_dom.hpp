@@ -11,6 +11,7 @@ struct JV {
   enum T : uint8_t { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
   bool b = false;
   bool is_int = false;     // a JSON number literal without fraction / exponent
+  bool gint = false;       // a gojq int computed by a jq query (jqc.hpp); JSON input numbers are float64
   std::string s;           // STR: the string; NUM: the literal text
   std::vector<JV> a;       // ARR items / OBJ values
   std::vector<std::string> k;  // OBJ keys (input order; duplicate keys: the last wins on lookup)

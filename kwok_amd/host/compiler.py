@@ -47,8 +47,12 @@ class CompileError(ValueError):
     pass
 
 
+_NORM = re.compile(r'"(?:[^"\\]|\\.)*"|\s+')
+
+
 def _norm(src: str) -> str:
-    return re.sub(r"\s+", "", src)
+    """The query without whitespace outside its string literals (the feature / slot key)."""
+    return _NORM.sub(lambda m: m.group(0) if m.group(0).startswith('"') else "", src)
 
 
 _SEG = re.compile(r'\.(?:([A-Za-z_][A-Za-z0-9_]*)|\[\s*"((?:[^"\\]|\\.)*)"\s*\]|"((?:[^"\\]|\\.)*)")')
@@ -417,8 +421,8 @@ class KindProgram:
                     else:
                         n = parse_int(t)
                         e = (abi.V_NOTOK, 0, 0) if n is None else (abi.V_OK, n, 0)
-                elif isinstance(t, float) or (isinstance(t, int) and not isinstance(t, bool)):
-                    e = (abi.V_OK, f64_to_i64(float(t)), 0)
+                elif isinstance(t, float):  # float64 (a gojq int falls to the default, as Go's switch)
+                    e = (abi.V_OK, f64_to_i64(t), 0)
                 else:
                     e = (abi.V_DEFAULT, 0, 0)
             else:  # durationFrom.Get (value_duration_from.go:53-79)

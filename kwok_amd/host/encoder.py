@@ -3,11 +3,11 @@ spec for libkwok_encoder.so (kwok_amd/csrc/encoder.cpp, include/kwok_encoder.h),
 ``NativeIngest``, a drop-in for ``engine.Ingest`` that encodes JSON bytes without per-object
 Python (a Go host hands the informer's bytes straight to kwk_encode).
 
-Feature and *From queries compile to step programs the encoder interprets: ``field`` (.k,
-.["k"]), ``iter`` (.[]) and ``select_eq`` (select(.a.b == literal)) joined by ``|`` — the forms
-kwok's Stage CRs use (kustomize/stage/**).  A program using any other jq construct, or
-"patch already applied" features (which need the template renderer), is rejected at
-``encoder_spec`` time with an explicit error; such a kind keeps the Python Ingest.
+Feature and *From queries travel as their jq source; the encoder compiles them with the native
+jq subset (kwok_amd/csrc/jqc.hpp; the Python mirror is jq.py): path steps and select(path ==
+literal) — the forms of kustomize/stage/** — run as step programs, everything else (length, not,
+comparisons, //, has, arithmetic, ...) through the evaluator.  A query outside the subset is
+rejected at ``encoder_spec`` time with the construct named.
 """
 from __future__ import annotations
 
@@ -21,6 +21,7 @@ import numpy as np
 
 from . import abi
 from .compiler import _IDENTITY_META, KindProgram
+from .jq import JqError, Query
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libkwok_encoder.so")
 CLASS_UNKNOWN = 0xFFFF
@@ -30,45 +31,14 @@ class EncoderUnsupported(ValueError):
     pass
 
 
-_SEG = re.compile(r'\.?\[\s*"((?:[^"\\]|\\.)*)"\s*\]|\.([A-Za-z_][A-Za-z0-9_]*)|\.?\[\s*\]|\.(?=\s*$)')
-_SELECT = re.compile(r'^select\s*\(\s*(?P<path>[^=]+?)\s*==\s*(?P<lit>"(?:[^"\\]|\\.)*"|true|false|null|-?\d+(?:\.\d+)?)\s*\)$')
-
-
-def _path(src: str) -> List[list]:
-    steps, i, s = [], 0, src.strip()
-    if s == ".":
-        return steps
-    while i < len(s):
-        m = _SEG.match(s, i)
-        if not m or m.end() == i:
-            raise EncoderUnsupported(f"jq construct not supported natively: {src!r}")
-        if m.group(1) is not None:
-            steps.append(["field", json.loads('"%s"' % m.group(1))])
-        elif m.group(2) is not None:
-            steps.append(["field", m.group(2)])
-        elif m.group(0).strip().endswith("]"):
-            steps.append(["iter"])
-        i = m.end()
-        while i < len(s) and s[i] == " ":
-            i += 1
-    return steps
-
-
-def query_steps(src: str) -> List[list]:
-    """jq query -> step program (field / iter / select_eq), or EncoderUnsupported."""
-    steps: List[list] = []
-    for part in (p.strip() for p in src.split("|")):
-        m = _SELECT.match(part)
-        if m:
-            sub = _path(m.group("path"))
-            if any(s[0] != "field" for s in sub):
-                raise EncoderUnsupported(f"select over a non-path: {src!r}")
-            steps.append(["select_eq", [s[1] for s in sub], json.loads(m.group("lit"))])
-        elif part.startswith("."):
-            steps += _path(part)
-        else:
-            raise EncoderUnsupported(f"jq construct not supported natively: {src!r}")
-    return steps
+def check_query(src: str) -> str:
+    """A selector key / getter query the native encoder compiles (kwok_amd/csrc/jqc.hpp, mirrored
+    by jq.py), or EncoderUnsupported naming the construct."""
+    try:
+        Query(src)
+    except JqError as e:
+        raise EncoderUnsupported(str(e)) from None
+    return src
 
 
 def encoder_spec(program: KindProgram) -> str:
@@ -76,9 +46,9 @@ def encoder_spec(program: KindProgram) -> str:
         return program.encoder_spec()
     if program.applied_bits:
         raise EncoderUnsupported("'patch already applied' features need the host renderer")
-    feats = [{"steps": query_steps(f.src), "present_bit": f.present_bit, "literals": dict(f.lit_bits)}
+    feats = [{"query": check_query(f.src), "present_bit": f.present_bit, "literals": dict(f.lit_bits)}
              for f in program.features.values()]
-    slots = [{"type": typ, "steps": query_steps(src)} for typ, src in program.slots]
+    slots = [{"type": typ, "query": check_query(src)} for typ, src in program.slots]
     spec = {"features": feats, "finalizers": dict(program.fin_bits), "finalizer_other_bit": program.fin_other_bit,
             "slots": slots, "classes": dict(program.class_ids), "identity_meta": list(_IDENTITY_META)}
     if program.disregard is not None:  # need()'s selectors, evaluated by the encoder into one bit
@@ -102,8 +72,9 @@ def lib():
         L.kwk_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
         L.kwk_encoder_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.kwk_jq_eval.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32)]
         L.kwk_encoder_add_classes.argtypes = [C.c_void_p, C.c_char_p]
-        for n in ("kwk_encoder_create", "kwk_encoder_destroy", "kwk_encode", "kwk_encoder_records",
+        for n in ("kwk_encoder_create", "kwk_encoder_destroy", "kwk_encode", "kwk_encoder_records", "kwk_jq_eval",
                   "kwk_encoder_add_classes"):
             getattr(L, n).restype = C.c_int32
         _lib = L
@@ -123,6 +94,25 @@ def pack_json(objs: Sequence) -> tuple:
     offs = np.zeros(len(parts) + 1, dtype=np.uint64)
     np.cumsum([len(p) for p in parts], out=offs[1:])
     return b"".join(parts), offs
+
+
+def jq_eval(query: str, doc) -> Optional[list]:
+    """kwk_jq_eval: Query.Execute of `query` on `doc` (a dict or JSON text) with the native jq subset
+    -> the outputs (nulls dropped) or None for the nil result; EncoderUnsupported outside the subset."""
+    text = doc if isinstance(doc, (str, bytes)) else json.dumps(doc)
+    text = text.encode() if isinstance(text, str) else text
+    n = C.c_uint32()
+    cap = 4096
+    while True:
+        buf = C.create_string_buffer(cap)
+        st = lib().kwk_jq_eval(query.encode(), text, buf, cap, C.byref(n))
+        if st == abi.KWK_ECAP:
+            cap = n.value + 1
+            continue
+        if st == abi.KWK_EINVAL:
+            raise EncoderUnsupported(lib().kwk_encoder_last_error(None).decode(errors="replace"))
+        _check(st, "kwk_jq_eval")
+        return json.loads(buf.value.decode())
 
 
 class NativeIngest:

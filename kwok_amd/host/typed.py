@@ -14,6 +14,8 @@ rewrite matters for hand-written objects (`"podIP": ""`, `"finalizers": []`, `"r
 `"labels": {}`), and after a patch (the apiserver round trip drops what a patch emptied)."""
 from __future__ import annotations
 
+import copy
+
 from typing import Optional
 
 # kinds: "keep" (no omitempty), "struct" / "ptr" (recurse into the named type), "list" (omitempty
@@ -88,9 +90,13 @@ def _rewrite(obj: dict, tname: str) -> dict:
 
 
 def typed_presence(obj: Optional[dict]) -> Optional[dict]:
-    """A new dict with the presence a typed Pod / Node round trip gives (other kinds: nulls and
-    empty values removed at the top level)."""
+    """A new dict with the presence a typed Pod / Node round trip gives.  Other kinds reach the
+    reference's matcher through the StageController as *unstructured.Unstructured
+    (stage_controller.go:174-232), whose json.Marshal writes the object map as it is — every field,
+    zero values and nulls included — so they are returned unchanged (a copy)."""
     if obj is None:
         return None
     k = obj.get("kind")
-    return _rewrite(obj, k if k in ("Pod", "Node") else "")
+    if k not in ("Pod", "Node"):
+        return copy.deepcopy(obj)
+    return _rewrite(obj, k)

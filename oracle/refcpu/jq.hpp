@@ -4,11 +4,16 @@
 // query forms KWOK's Stage CRs and tests use:
 //   paths `.a.b`, `.a["k"]`, `."k"`, `.a.[]`, `.a[]`, `.[n]`, pipes `|`, `,`,
 //   `select(f)`, comparisons, `and`/`or`/`not`, `//`, literals, `[...]`, `{...}`,
-//   `length`, `empty`, and the update forms `p = v`, `p += v` exercised by
-//   pkg/utils/expression/query_test.go:127-166.
+//   `length`, `empty`, `has(k)`, `keys`, `type`, `if-then-elif-else-end`, unary `-`, and the
+//   update forms `p = v`, `p += v` exercised by pkg/utils/expression/query_test.go:127-166.
+// gojq's value model: JSON input numbers are float64, number literals / `length` / int
+// arithmetic give ints (JV::integer) — selector.go hasValue matches ints (FormatInt), never
+// float64s; objects iterate and list their keys sorted (gojq holds them in Go maps).
 // Call sites restated: Query.Execute (pkg/utils/expression/query.go:48-69): a runtime error
 // makes the whole result nil; null outputs are dropped.
 #pragma once
+#include <algorithm>
+#include <climits>
 #include <functional>
 #include <map>
 
@@ -25,12 +30,14 @@ struct JqNode {
     INDEX,     // <sub>[expr]
     ITER,      // <sub>[]
     PIPE, COMMA, ALT, OR, AND, NOT_FN, CMP, ADD, SUB,
-    LIT, ARRAY, OBJECT, SELECT, LENGTH, EMPTY, ASSIGN, UPDATE_ADD, TRY
+    LIT, ARRAY, OBJECT, SELECT, LENGTH, EMPTY, ASSIGN, UPDATE_ADD, TRY,
+    HAS, KEYS, TYPE, IF, NEG
   } k;
   std::string name;  // FIELD name / CMP op
   JVP lit;
   std::shared_ptr<JqNode> a, b;  // operands (a = sub-expression / lhs)
   std::vector<std::pair<std::shared_ptr<JqNode>, std::shared_ptr<JqNode>>> obj;  // OBJECT entries
+  std::vector<std::shared_ptr<JqNode>> branches;  // IF: cond, then, cond, then, ..., [else]
 };
 using JqNodeP = std::shared_ptr<JqNode>;
 
@@ -83,24 +90,25 @@ class JqParser {
     }
     return l;
   }
+  // jq precedence, loosest first: '|', ',', '//' (right), '=' / '+=' (non-assoc), or, and, comparisons
   JqNodeP comma() {
-    JqNodeP l = assign();
+    JqNodeP l = alt();
     while (true) {
       ws();
-      if (i_ < s_.size() && s_[i_] == ',') { ++i_; auto n = mk(JqNode::COMMA); n->a = l; n->b = assign(); l = n; }
+      if (i_ < s_.size() && s_[i_] == ',') { ++i_; auto n = mk(JqNode::COMMA); n->a = l; n->b = alt(); l = n; }
       else return l;
     }
   }
-  JqNodeP assign() {
-    JqNodeP l = alt();
-    ws();
-    if (s_.compare(i_, 2, "+=") == 0) { i_ += 2; auto n = mk(JqNode::UPDATE_ADD); n->a = l; n->b = alt(); return n; }
-    if (i_ < s_.size() && s_[i_] == '=' && s_.compare(i_, 2, "==") != 0) { ++i_; auto n = mk(JqNode::ASSIGN); n->a = l; n->b = alt(); return n; }
+  JqNodeP alt() {
+    JqNodeP l = assign();
+    if (eat("//")) { auto n = mk(JqNode::ALT); n->a = l; n->b = alt(); return n; }
     return l;
   }
-  JqNodeP alt() {
+  JqNodeP assign() {
     JqNodeP l = orx();
-    if (eat("//")) { auto n = mk(JqNode::ALT); n->a = l; n->b = alt(); return n; }
+    ws();
+    if (s_.compare(i_, 2, "+=") == 0) { i_ += 2; auto n = mk(JqNode::UPDATE_ADD); n->a = l; n->b = orx(); return n; }
+    if (i_ < s_.size() && s_[i_] == '=' && s_.compare(i_, 2, "==") != 0) { ++i_; auto n = mk(JqNode::ASSIGN); n->a = l; n->b = orx(); return n; }
     return l;
   }
   JqNodeP orx() {
@@ -160,7 +168,14 @@ class JqParser {
       return base;
     }
   }
-  JqNodeP postfix() { return suffixes(term()); }
+  JqNodeP postfix() {
+    ws();
+    if (i_ < s_.size() && s_[i_] == '-' && !(i_ + 1 < s_.size() && isdigit((unsigned char)s_[i_ + 1]))) {
+      ++i_;
+      auto n = mk(JqNode::NEG); n->a = postfix(); return n;
+    }
+    return suffixes(term());
+  }
   JqNodeP term() {
     ws();
     if (i_ >= s_.size()) throw JqError("unexpected end in " + s_);
@@ -176,8 +191,16 @@ class JqParser {
     if (isdigit((unsigned char)c) || (c == '-' && i_ + 1 < s_.size() && isdigit((unsigned char)s_[i_ + 1]))) {
       size_t st = i_;
       ++i_;
-      while (i_ < s_.size() && (isdigit((unsigned char)s_[i_]) || s_[i_] == '.' || s_[i_] == 'e' || s_[i_] == 'E')) ++i_;
-      auto n = mk(JqNode::LIT); n->lit = JV::number(strtod(s_.substr(st, i_ - st).c_str(), nullptr)); return n;
+      bool frac = false;
+      while (i_ < s_.size() && (isdigit((unsigned char)s_[i_]) || s_[i_] == '.' || s_[i_] == 'e' || s_[i_] == 'E')) {
+        frac |= !isdigit((unsigned char)s_[i_]);
+        ++i_;
+      }
+      const std::string t = s_.substr(st, i_ - st);
+      auto n = mk(JqNode::LIT);
+      // gojq: a literal that fits an int is an int
+      n->lit = !frac && t.size() < 19 ? JV::integer(strtoll(t.c_str(), nullptr, 10)) : JV::number(strtod(t.c_str(), nullptr));
+      return n;
     }
     if (c == '(') { ++i_; JqNodeP n = pipe(); if (!eat(")")) throw JqError("expected )"); return n; }
     if (c == '[') {
@@ -216,6 +239,26 @@ class JqParser {
     if (eat_kw("not")) return mk(JqNode::NOT_FN);
     if (eat_kw("length")) return mk(JqNode::LENGTH);
     if (eat_kw("empty")) return mk(JqNode::EMPTY);
+    if (eat_kw("keys")) return mk(JqNode::KEYS);
+    if (eat_kw("type")) return mk(JqNode::TYPE);
+    if (eat_kw("has")) {
+      if (!eat("(")) throw JqError("expected ( after has");
+      auto n = mk(JqNode::HAS); n->a = pipe();
+      if (!eat(")")) throw JqError("expected )");
+      return n;
+    }
+    if (eat_kw("if")) {
+      auto n = mk(JqNode::IF);
+      while (true) {
+        n->branches.push_back(pipe());
+        if (!eat_kw("then")) throw JqError("expected then");
+        n->branches.push_back(pipe());
+        if (eat_kw("elif")) continue;
+        if (eat_kw("else")) n->branches.push_back(pipe());
+        if (!eat_kw("end")) throw JqError("expected end");
+        return n;
+      }
+    }
     throw JqError("unsupported jq syntax at " + std::to_string(i_) + " in " + s_);
   }
 };
@@ -234,6 +277,18 @@ inline const char* jq_type(const JVP& v) {
     case JV::OBJ: return "object";
   }
   return "?";
+}
+
+// an object's entries as a Go map holds them: the last duplicate key wins, keys sorted
+inline std::vector<std::pair<std::string, JVP>> jq_entries(const JVP& v) {
+  std::vector<std::pair<std::string, JVP>> e;
+  for (size_t i = 0; i < v->o.size(); ++i) {
+    bool later = false;
+    for (size_t j = i + 1; j < v->o.size(); ++j) later |= v->o[j].first == v->o[i].first;
+    if (!later) e.push_back(v->o[i]);
+  }
+  std::sort(e.begin(), e.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  return e;
 }
 
 inline JVP jq_index(const JVP& v, const JVP& key) {
@@ -268,7 +323,10 @@ inline int jq_order(const JVP& v) {
 inline int jq_compare(const JVP& x, const JVP& y) {
   int ox = jq_order(x), oy = jq_order(y);
   if (ox != oy) return ox < oy ? -1 : 1;
-  if (x->t == JV::NUM) return x->n < y->n ? -1 : (x->n > y->n ? 1 : 0);
+  if (x->t == JV::NUM) {
+    if (x->gint && y->gint) return x->i < y->i ? -1 : (x->i > y->i ? 1 : 0);
+    return x->n < y->n ? -1 : (x->n > y->n ? 1 : 0);
+  }
   if (x->t == JV::STR) return x->s < y->s ? -1 : (x->s > y->s ? 1 : 0);
   if (x->t == JV::ARR) {
     for (size_t i = 0; i < x->a.size() && i < y->a.size(); ++i) {
@@ -277,14 +335,28 @@ inline int jq_compare(const JVP& x, const JVP& y) {
     }
     return x->a.size() < y->a.size() ? -1 : (x->a.size() > y->a.size() ? 1 : 0);
   }
-  if (x->t == JV::OBJ) return jv_equal(x, y) ? 0 : (dumps(x) < dumps(y) ? -1 : 1);
+  if (x->t == JV::OBJ) {  // sorted key lists first, then the values key by key
+    const auto ex = jq_entries(x), ey = jq_entries(y);
+    for (size_t i = 0; i < ex.size() && i < ey.size(); ++i)
+      if (ex[i].first != ey[i].first) return ex[i].first < ey[i].first ? -1 : 1;
+    if (ex.size() != ey.size()) return ex.size() < ey.size() ? -1 : 1;
+    for (size_t i = 0; i < ex.size(); ++i) {
+      int c = jq_compare(ex[i].second, ey[i].second);
+      if (c) return c;
+    }
+    return 0;
+  }
   return 0;
 }
 
 inline JVP jq_add(const JVP& x, const JVP& y) {
   if (x->t == JV::NUL) return y;
   if (y->t == JV::NUL) return x;
-  if (x->t == JV::NUM && y->t == JV::NUM) return JV::number(x->n + y->n);
+  if (x->t == JV::NUM && y->t == JV::NUM) {
+    long long z;
+    if (x->gint && y->gint && !__builtin_add_overflow(x->i, y->i, &z)) return JV::integer(z);
+    return JV::number(x->n + y->n);
+  }
   if (x->t == JV::STR && y->t == JV::STR) return JV::str(x->s + y->s);
   if (x->t == JV::ARR && y->t == JV::ARR) {
     auto v = std::make_shared<JV>(*x);
@@ -358,7 +430,7 @@ inline void jq_paths(const JqNode* n, const JVP& in, const Path& base, const Emi
         if (v->t == JV::ARR) {
           for (size_t i = 0; i < v->a.size(); ++i) { Path q = p; q.push_back(JV::number((double)i)); emit(q, v->a[i]); }
         } else if (v->t == JV::OBJ) {
-          for (auto& kv : v->o) { Path q = p; q.push_back(JV::str(kv.first)); emit(q, kv.second); }
+          for (auto& kv : jq_entries(v)) { Path q = p; q.push_back(JV::str(kv.first)); emit(q, kv.second); }
         } else if (v->t != JV::NUL) {
           throw JqError(std::string("cannot iterate over: ") + jq_type(v));
         }
@@ -392,13 +464,16 @@ inline void jq_eval(const JqNode* n, const JVP& in, const Emit& emit) {
       jq_eval(n->a.get(), in, [&](const JVP& v) {
         // gojq: `.[]` over null is an error ("cannot iterate over: null")
         if (v->t == JV::ARR) { for (auto& e : v->a) emit(e); }
-        else if (v->t == JV::OBJ) { for (auto& kv : v->o) emit(kv.second); }
+        else if (v->t == JV::OBJ) { for (auto& kv : jq_entries(v)) emit(kv.second); }
         else throw JqError(std::string("cannot iterate over: ") + jq_type(v));
       });
       return;
-    case JqNode::TRY:
-      try { jq_eval(n->a.get(), in, emit); } catch (const JqError&) {}
+    case JqNode::TRY: {  // the outputs before an error; errors of the consumer are not caught here
+      std::vector<JVP> got;
+      try { jq_eval(n->a.get(), in, [&](const JVP& v) { got.push_back(v); }); } catch (const JqError&) {}
+      for (auto& v : got) emit(v);
       return;
+    }
     case JqNode::PIPE:
       jq_eval(n->a.get(), in, [&](const JVP& v) { jq_eval(n->b.get(), v, emit); });
       return;
@@ -407,11 +482,12 @@ inline void jq_eval(const JqNode* n, const JVP& in, const Emit& emit) {
       jq_eval(n->b.get(), in, emit);
       return;
     case JqNode::ALT: {
-      bool any = false;
+      std::vector<JVP> got;
       try {
-        jq_eval(n->a.get(), in, [&](const JVP& v) { if (jv_truthy(v)) { any = true; emit(v); } });
+        jq_eval(n->a.get(), in, [&](const JVP& v) { if (jv_truthy(v)) got.push_back(v); });
       } catch (const JqError&) {}
-      if (!any) jq_eval(n->b.get(), in, emit);
+      if (got.empty()) jq_eval(n->b.get(), in, emit);
+      for (auto& v : got) emit(v);
       return;
     }
     case JqNode::OR:
@@ -446,7 +522,10 @@ inline void jq_eval(const JqNode* n, const JVP& in, const Emit& emit) {
     case JqNode::SUB:
       jq_eval(n->b.get(), in, [&](const JVP& r) {
         jq_eval(n->a.get(), in, [&](const JVP& l) {
-          if (l->t == JV::NUM && r->t == JV::NUM) emit(JV::number(l->n - r->n));
+          long long z;
+          if (l->t == JV::NUM && r->t == JV::NUM && l->gint && r->gint && !__builtin_sub_overflow(l->i, r->i, &z))
+            emit(JV::integer(z));
+          else if (l->t == JV::NUM && r->t == JV::NUM) emit(JV::number(l->n - r->n));
           else throw JqError("cannot subtract");
         });
       });
@@ -491,20 +570,67 @@ inline void jq_eval(const JqNode* n, const JVP& in, const Emit& emit) {
       return;
     case JqNode::LENGTH:
       switch (in->t) {
-        case JV::NUL: emit(JV::number(0)); return;
+        case JV::NUL: emit(JV::integer(0)); return;
         case JV::BOOL: throw JqError("boolean has no length");
-        case JV::NUM: emit(JV::number(std::fabs(in->n))); return;
+        case JV::NUM:
+          if (in->gint && in->i != LLONG_MIN) emit(JV::integer(in->i < 0 ? -in->i : in->i));
+          else emit(JV::number(std::fabs(in->n)));
+          return;
         case JV::STR: {
-          size_t cps = 0;
+          long long cps = 0;
           for (unsigned char c : in->s) if ((c & 0xC0) != 0x80) ++cps;
-          emit(JV::number((double)cps));
+          emit(JV::integer(cps));
           return;
         }
-        case JV::ARR: emit(JV::number((double)in->a.size())); return;
-        case JV::OBJ: emit(JV::number((double)in->o.size())); return;
+        case JV::ARR: emit(JV::integer((long long)in->a.size())); return;
+        case JV::OBJ: emit(JV::integer((long long)jq_entries(in).size())); return;
       }
       return;
     case JqNode::EMPTY: return;
+    case JqNode::KEYS: {
+      auto v = std::make_shared<JV>();
+      v->t = JV::ARR;
+      if (in->t == JV::OBJ) for (auto& kv : jq_entries(in)) v->a.push_back(JV::str(kv.first));
+      else if (in->t == JV::ARR) for (size_t i = 0; i < in->a.size(); ++i) v->a.push_back(JV::integer((long long)i));
+      else throw JqError("keys cannot be applied to: " + std::string(jq_type(in)));
+      emit(v);
+      return;
+    }
+    case JqNode::TYPE: emit(JV::str(jq_type(in))); return;
+    case JqNode::HAS:
+      jq_eval(n->a.get(), in, [&](const JVP& k) {
+        if (in->t == JV::OBJ && k->t == JV::STR) { emit(JV::boolean(in->get(k->s) != nullptr)); return; }
+        if (in->t == JV::ARR && k->t == JV::NUM) {
+          const long long i = k->gint ? k->i : (long long)k->n;
+          emit(JV::boolean(i >= 0 && i < (long long)in->a.size()));
+          return;
+        }
+        throw JqError("has cannot be applied");
+      });
+      return;
+    case JqNode::NEG:
+      jq_eval(n->a.get(), in, [&](const JVP& v) {
+        if (v->t != JV::NUM) throw JqError("cannot negate");
+        if (v->gint && v->i != LLONG_MIN) emit(JV::integer(-v->i));
+        else emit(JV::number(-v->n));
+      });
+      return;
+    case JqNode::IF: {
+      const size_t nc = n->branches.size() / 2;
+      std::function<void(size_t)> branch = [&](size_t i) {
+        if (i == nc) {
+          if (n->branches.size() % 2) jq_eval(n->branches.back().get(), in, emit);
+          else emit(in);
+          return;
+        }
+        jq_eval(n->branches[2 * i].get(), in, [&](const JVP& c) {
+          if (jv_truthy(c)) jq_eval(n->branches[2 * i + 1].get(), in, emit);
+          else branch(i + 1);
+        });
+      };
+      branch(0);
+      return;
+    }
     case JqNode::ASSIGN:
       jq_eval(n->b.get(), in, [&](const JVP& val) {
         JVP out = in;

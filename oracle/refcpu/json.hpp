@@ -25,6 +25,8 @@ struct JV {
   enum Type { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
   bool b = false;
   double n = 0;
+  bool gint = false;  // gojq int (value in i)
+  long long i = 0;
   std::string s;
   std::vector<JVP> a;
   std::vector<std::pair<std::string, JVP>> o;  // insertion order kept; lookups linear
@@ -32,6 +34,10 @@ struct JV {
   static JVP null() { static JVP v = std::make_shared<JV>(); return v; }
   static JVP boolean(bool x) { auto v = std::make_shared<JV>(); v->t = BOOL; v->b = x; return v; }
   static JVP number(double x) { auto v = std::make_shared<JV>(); v->t = NUM; v->n = x; return v; }
+  // a gojq int (number literals, length, int arithmetic); JSON input numbers are float64
+  static JVP integer(long long x) {
+    auto v = std::make_shared<JV>(); v->t = NUM; v->n = (double)x; v->gint = true; v->i = x; return v;
+  }
   static JVP str(std::string x) { auto v = std::make_shared<JV>(); v->t = STR; v->s = std::move(x); return v; }
 
   const JVP* get(const std::string& k) const {
@@ -196,7 +202,8 @@ inline void dump(std::string& out, const JVP& v) {
     case JV::BOOL: out += v->b ? "true" : "false"; break;
     case JV::NUM: {
       char b[40];
-      if (std::floor(v->n) == v->n && std::fabs(v->n) < 1e17) snprintf(b, sizeof b, "%.0f", v->n);
+      if (v->gint) snprintf(b, sizeof b, "%lld", v->i);
+      else if (std::floor(v->n) == v->n && std::fabs(v->n) < 1e17) snprintf(b, sizeof b, "%.0f", v->n);
       else snprintf(b, sizeof b, "%.17g", v->n);
       out += b;
       break;

@@ -85,7 +85,11 @@ struct Requirement {
     switch (d->t) {
       case JV::STR: s = d->s; break;
       case JV::BOOL: s = d->b ? "true" : "false"; break;
-      default: return false;  // gojq yields float64 for JSON numbers: never matches (selector.go:101-111)
+      case JV::NUM:  // a gojq int (length, literals) matches FormatInt; float64 JSON numbers never do
+        if (!d->gint) return false;
+        s = std::to_string(d->i);
+        break;
+      default: return false;  // selector.go:101-111
     }
     for (auto& v : vs) if (v == s) return true;
     return false;
@@ -123,8 +127,8 @@ struct IntGetter {
       if (go_parse_int(t->s, n)) { out = n; return true; }
       return false;
     }
-    if (t->t == JV::NUM) { out = go_f64_to_i64(t->n); return true; }
-    if (has_value) { out = value; return true; }
+    if (t->t == JV::NUM && !t->gint) { out = go_f64_to_i64(t->n); return true; }  // float64 only: a gojq int
+    if (has_value) { out = value; return true; }                                    // falls to the default
     return false;
   }
 };

@@ -24,6 +24,8 @@ and non-omitempty fields are kept.  Fields the typed decode does not know are ke
 """
 from __future__ import annotations
 
+import copy
+
 from typing import Any, Dict, Optional
 
 # field kinds: K keep (no omitempty: always written), S struct (always written, recurse with the
@@ -98,9 +100,13 @@ def _struct(obj: dict, schema: Optional[str]) -> dict:
 
 
 def to_json_standard(obj: Optional[dict]) -> Optional[dict]:
-    """The presence the reference's queries see for a Pod / Node (other kinds: nulls removed and
-    empty values of fields the oracle does not know dropped, as omitempty would)."""
+    """The presence the reference's queries see: a typed Pod / Node round trip
+    (PodController / NodeController), or, for every other kind, the object as the StageController
+    holds it — *unstructured.Unstructured, whose json.Marshal writes the map as it is, zero values and
+    nulls included (pkg/kwok/controllers/stage_controller.go:174-232)."""
     if obj is None:
         return None
     kind = obj.get("kind")
-    return _struct(obj, kind if kind in ("Pod", "Node") else None)
+    if kind not in ("Pod", "Node"):
+        return copy.deepcopy(obj)
+    return _struct(obj, kind)

@@ -12,7 +12,7 @@ import pytest
 
 from kwok_amd import workload as W
 from kwok_amd.host.compiler import HarnessSpec, KindProgram
-from kwok_amd.host.encoder import EncoderUnsupported, NativeIngest, pack_json, query_steps
+from kwok_amd.host.encoder import EncoderUnsupported, NativeIngest, check_query, pack_json
 from kwok_amd.host.engine import Ingest
 from kwok_amd.host.stages import load_stage_files
 
@@ -93,12 +93,18 @@ def test_unknown_class_reported():
     assert np.all(cls[job] == 0xFFFF) and np.all(cls[~job] != 0xFFFF) and nat.unknown_classes == job.sum()
 
 
-def test_query_step_forms():
-    assert query_steps('.status.conditions.[] | select( .type == "Ready" ) | .status') == [
-        ["field", "status"], ["field", "conditions"], ["iter"], ["select_eq", ["type"], "Ready"], ["field", "status"]]
-    assert query_steps('.metadata.labels["a/b"]') == [["field", "metadata"], ["field", "labels"], ["field", "a/b"]]
-    with pytest.raises(EncoderUnsupported):
-        query_steps(".a | length")
+def test_query_forms():
+    """The encoder spec carries each query's source; the native jq subset (jqc.hpp / jq.py) accepts
+    the shipped forms and the gojq constructs Stage CRs may use, and refuses the rest with the
+    construct named."""
+    for q in ('.status.conditions.[] | select( .type == "Ready" ) | .status', '.metadata.labels["a/b"]',
+              ".status.conditions | length", '.status.phase != "Running"', ".a // .b", 'has("x")',
+              ".spec.containers | map(.name) | length > 1", "if .a then 1 else 2 end", ".a.b? | not"):
+        assert check_query(q) == q
+    for q, what in ((". as $x | $x", "'as'"), ("reduce .[] as $x (0; . + $x)", "'reduce'"), ('test("a")', "test/1"),
+                    (".a[1:2]", "slices"), ('"\\(.a)"', "interpolation"), ("..", "'..'"), ("@base64", "formats")):
+        with pytest.raises(EncoderUnsupported, match=what):
+            check_query(q)
 
 
 def test_native_encoder_throughput_report(capsys):

@@ -127,8 +127,11 @@ def test_native_compiler_errors_and_drops():
     with pytest.raises(CompileError, match="resourceRef"):
         NativeProgram(docs + node)
     jq = json.loads(json.dumps(docs[0]))
-    jq["spec"]["selector"]["matchExpressions"][0]["key"] = ".status.conditions | length"
-    with pytest.raises(CompileError, match="jq construct"):
+    jq["spec"]["selector"]["matchExpressions"][0]["key"] = ".status.conditions | .[] as $c | $c.type"
+    with pytest.raises(CompileError, match="jq construct not supported natively: 'as'"):
+        NativeProgram([jq])
+    jq["spec"]["selector"]["matchExpressions"][0]["key"] = '.metadata.name | test("^a")'
+    with pytest.raises(CompileError, match="function test/1"):
         NativeProgram([jq])
 
 
