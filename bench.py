@@ -586,12 +586,16 @@ def main():
     ap.add_argument("--hbm-only", action="store_true", help="diagnostic: only the C2-mix HBM working-set run")
     ap.add_argument("--hbm-warmup", type=int, default=12)
     ap.add_argument("--pcie-steps", type=int, default=10)
+    ap.add_argument("--metrics-pods", type=int, default=0,
+                    help="diagnostic: only the Metric-CR evaluation leg at this many pods (100 per node; C4 shape, "
+                         "metrics-resource.yaml), e.g. 100000000 for the single-GPU C5 size")
     ap.add_argument("--emit-steps", type=int, default=5, help="device patch emission steps after the timed run (0: off)")
     ap.add_argument("--no-harness", action="store_true", help="diagnostic: no churn (steady state is an idle sweep)")
     ap.add_argument("--wide-state", action="store_true", help="diagnostic: force the 8-byte device state format")
-    ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: KWK_TUNE_Q16 for the pod engine (0: default)")
+    ap.add_argument("--tune-q16", type=int, default=0, help="diagnostic: the 2-byte sweep's q (KWK_TUNE_SWEEP16) for the "
+                    "pod engine (0: default)")
     ap.add_argument("--tune-fsm-kernel", type=int, default=-1,
-                    help="diagnostic: KWK_TUNE_FSM_KERNEL for the pod engine (-1: default)")
+                    help="diagnostic: the table-only kernel field of KWK_TUNE_SWEEP16 for the pod engine (-1: default)")
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
@@ -618,6 +622,8 @@ def main():
         if not os.path.exists(kbuild.OUT):
             kbuild.build()
         r = configs.run(args.config, args.steps, args.warmup, args.seed)
+        if args.config == "C4":  # the Metric CR on the same cluster size
+            r["metric_cr"] = configs.run_metrics(10_000, 1_000_000, scrapes=10, warmup=3, seed=args.seed)
         roof = r.pop("roofline", None)
         cpu = None
         if not args.no_cpu_baseline:
@@ -633,6 +639,17 @@ def main():
                 "data": "synthetic (seeded kwokctl-shaped objects), cache-resident working set",
                 "config": {"workload": r.pop("workload")}, "roofline": roof, "cpu_baseline": cpu, "detail": r}
         print(json.dumps(line), flush=True)
+        return
+
+    if args.metrics_pods:
+        from kwok_amd import build as kbuild
+        from kwok_amd import configs
+        if not os.path.exists(kbuild.OUT):
+            kbuild.build()
+        n = args.metrics_pods
+        print(json.dumps(configs.run_metrics(max(1, n // args.pods_per_node), n, scrapes=5, warmup=2, seed=args.seed,
+                                             sample_every=9973 if n > 10_000_000 else 97, copy=n <= 10_000_000)),
+              flush=True)
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -675,12 +692,10 @@ def main():
     setup_s = time.perf_counter() - t_setup
     if args.no_harness:
         pods.set_harness(False)
-    if args.tune_q16:
+    if args.tune_q16 or args.tune_fsm_kernel >= 0:
         from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_Q16, args.tune_q16)
-    if args.tune_fsm_kernel >= 0:
-        from kwok_amd.host import abi
-        pods.set_tuning(abi.TUNE_FSM_KERNEL, args.tune_fsm_kernel)
+        pods.set_tuning(abi.TUNE_SWEEP16, abi.sweep16_shape(q=args.tune_q16 or 4,
+                                                            kernel=2 if args.tune_fsm_kernel < 0 else args.tune_fsm_kernel))
     if args.tune_priority:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_STREAM_PRIORITY, 1)

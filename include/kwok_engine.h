@@ -207,30 +207,33 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 
 /* Explicit kernel choices (defaults = the measured best; tests use them to check
  * that every kernel shape gives the same results).  Nothing is read from the environment. */
-#define KWK_TUNE_FSM 1        /* 2-byte sweep: precomputed transition table, 1 (default) or 0 */
-#define KWK_TUNE_Q16 2        /* 2-byte sweep: 16-byte chunks per lane, 4 (default), 2 or 1 */
-#define KWK_TUNE_PERSIST16 3  /* 2-byte sweep: persistent grid for large engines, 1 (default) or 0 */
-#define KWK_TUNE_FSM_KERNEL 5  /* 2-byte sweep with a transition table: the table-only kernel (general
-                                   entries deferred to its cold loop) with 2 (default) or 1 tiles
-                                   prefetched, or 0 = the general sweep16 kernel */
-#define KWK_TUNE_USAGE_KEY8 6  /* usage fast path: 1-byte usage-key column when at most 256 distinct keys occur,
-                                   1 (default) or 0 (the 4-byte keys) */
-/* 4, 7, 12: retired experiment knobs (usage grid, sweep grid, usage chunk rows: tools/variants.py
- * patches the constants for such measurements) */
+/* 1, 2, 3, 5 (round 6: merged into KWK_TUNE_SWEEP16), 4, 7, 12 (round 5: experiment knobs; tools/variants.py
+ * patches the constants for such measurements), 6, 13 (round 6: merged into KWK_TUNE_USAGE), 11 (the
+ * one-pass look-back hand-back, measured slower: 73 vs 27 us at C5), 16 (round 6: the folded hand-back,
+ * superseded by fused steps): retired */
+#define KWK_TUNE_SWEEP16 18   /* the table-driven sweeps' shape, KWK_SWEEP16_SHAPE(q, persistent, kernel, table):
+                                 q = 16-byte chunks per lane of the 2-byte sweep (4 default, 2 or 1), persistent = a
+                                 persistent grid for large engines (1 default), kernel = the table-only kernel with 2
+                                 (default) or 1 tiles prefetched (the 2-byte and the 1-byte sweeps), or 0 = the general
+                                 sweep16_kernel; table = the precomputed transition table (1 default) or 0 */
+#define KWK_SWEEP16_SHAPE(q, persistent, kernel, table) \
+  ((uint32_t)(q) | (uint32_t)(persistent) << 4 | (uint32_t)(kernel) << 8 | (uint32_t)(table) << 12)
+#define KWK_SWEEP16_DEFAULT KWK_SWEEP16_SHAPE(4, 1, 2, 1)
+#define KWK_TUNE_USAGE 19     /* the usage path: KWK_USAGE_KEY8 (the 1-byte usage-key column when at most 256
+                                 distinct keys occur) | KWK_USAGE_AGG_FUSED (kwk_aggregate with KWK_AGG_USAGE on 1-byte
+                                 ids: the <= 4 mask counts inside the usage kernel's pass); default both */
+#define KWK_USAGE_KEY8 1u
+#define KWK_USAGE_AGG_FUSED 2u
 #define KWK_TUNE_COMPACT_SMALL 8 /* fired hand-back: the most segments compacted in one launch (each block sums
                                    the counts before its own), 0..8192 (default 8192); more use the scan +
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
-/* 11: retired (the one-pass look-back hand-back, measured slower: 73 vs 27 us at C5) */
-#define KWK_TUNE_AGG_FUSED 13  /* kwk_aggregate with KWK_AGG_USAGE on 1-byte ids: the <= 4 mask counts taken inside the
-                                  usage kernel's pass over the id column, 1 (default), or 0 (a count pass of their own) */
 #define KWK_TUNE_STREAM_PRIORITY 15 /* the engine's stream: 0 (default priority), 1 (the device's greatest) or 2 (its
                                        least); re-created after a synchronise, so set it between steps */
 #define KWK_TUNE_WORD_TILES 10 /* word sweep (4-byte, fused and wide formats): tiles per workgroup, 1..16
                                   (exactly), or 0 (default: 8 fused, 4 otherwise, but at least 5 workgroups
                                   per CU) */
-/* 16: retired in round 6 (the folded hand-back, superseded by fused steps at the shard size) */
 #define KWK_TUNE_FUSE_STEPS 17 /* kwk_step_n / _pair on 1-byte engines with <= 4 stages and no delayed stage: up to
                                   4 (default) or 2 steps per sweep launch (each id read once, stepped in LDS,
                                   written once; each step's fired records and hand-back kept apart), or 0 / 1 (one step
@@ -509,6 +512,11 @@ kwk_status kwk_metrics_inputs(kwk_engine* pods, const int64_t* pod_created_ns, c
  * *n_out = values written (synchronises) */
 kwk_status kwk_metrics_eval(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out,
                             uint64_t cap, uint64_t* n_out);
+/* the same values left on the device (enqueue only): *out = the engine's device buffer of *n_out
+ * doubles, valid until the next kwk_metrics_eval* call — for an in-process consumer (an exposition
+ * writer on the GPU, an all-reduce) and for timing the evaluation without the copy */
+kwk_status kwk_metrics_eval_device(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes,
+                                   const double** out, uint64_t* n_out);
 
 /* Histogram Metric CRs (kind: histogram; pkg/kwok/metrics/metrics.go:133-160,356-462,
  * histogram.go:81-164): per series every bucket's value program runs (a lowered CEL value, as
@@ -537,6 +545,8 @@ kwk_status kwk_histograms_load(kwk_engine* pods, uint32_t n_hist, const kwk_hist
                                const kwk_metric_bucket* buckets, uint32_t n_ops, const kwk_metric_op* ops);
 kwk_status kwk_histograms_eval(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, uint64_t* out,
                                uint64_t cap, uint64_t* n_out);
+kwk_status kwk_histograms_eval_device(kwk_engine* pods, int64_t now_ns, uint32_t node_first, uint32_t n_nodes,
+                                      const uint64_t** out, uint64_t* n_out);
 
 /* ------------------------------------------------------------------ node leases */
 /* NodeLeaseController (pkg/kwok/controllers/node_lease_controller.go) on a NODE engine: one

@@ -189,3 +189,198 @@ def run(config: str, steps: int, warmup: int, seed: int) -> dict:
         pods.close()
         return out
     raise ValueError(config)
+
+
+# ------------------------------------------------------------------ Metric CR evaluation at scale
+METRIC_CR = os.path.join(W.METRICS_DIR, "metrics-resource.yaml")
+
+
+def c4_pod_workload(n_nodes: int, n_pods: int, seed: int):
+    """The C4 pod shape (workload._usage_workload: 1-4 containers, half annotated with the usage
+    values) for any size, vectorised: (variants, per-pod variant index, node_ptr)."""
+    rng = np.random.default_rng(seed)
+    ncont = rng.integers(1, 5, n_pods)
+    ann = rng.random(n_pods) < 0.5
+    cpu = np.where(ann, rng.integers(0, len(W.CPU_VALUES), n_pods), -1)
+    mem = np.where(ann, rng.integers(0, len(W.MEM_VALUES), n_pods), -1)
+    code = ((ncont - 1) * 17 + (cpu + 1)) * 17 + (mem + 1)
+    del ncont, ann, cpu, mem
+    present = np.bincount(code, minlength=4 * 17 * 17) > 0  # the codes that occur, in order: the variants
+    uniq = np.nonzero(present)[0]
+    remap = (np.cumsum(present) - 1).astype(np.int32)
+    idx = remap[code]
+    variants = []
+    for c in uniq.tolist():
+        m, c = c % 17 - 1, c // 17
+        cp, k = c % 17 - 1, c // 17 + 1
+        a = None if cp < 0 else {"kwok.x-k8s.io/usage-cpu": W.CPU_VALUES[cp], "kwok.x-k8s.io/usage-memory": W.MEM_VALUES[m]}
+        variants.append(W.pod_object("p", "n", containers=k, annotations=a))
+    node_ptr = np.zeros(n_nodes + 1, dtype=np.int64)
+    ppn = np.full(n_nodes, n_pods // n_nodes, dtype=np.int64)
+    ppn[: n_pods % n_nodes] += 1
+    np.cumsum(ppn, out=node_ptr[1:])
+    return variants, idx.astype(np.int32), node_ptr
+
+
+def _metric_series_bytes(programs, n_nodes, n_pods, n_containers):
+    """Algorithmic bytes of one scrape's metric kernels: per series its output (8 B) and its own
+    inputs — for pod / container series the pod's state id (1 B; 4 B of cptr for a container),
+    per load of a per-pod / per-container input 8 B (usage values from the key: the 4-byte key;
+    node inputs are shared by ~100 pods: not counted per series)."""
+    from .host import cel
+    total = 0
+    for dim, ops in programs:
+        n = {"node": n_nodes, "pod": n_pods, "container": n_containers}[dim]
+        per = 8 + (0 if dim == "node" else 1) + (4 if dim == "container" else 0)
+        for op, x in ops:
+            if op != cel.OP_LOAD:
+                continue
+            x = int(x)
+            if x in (cel.IN_CONTAINER_CPU, cel.IN_CONTAINER_MEM):
+                per += 4
+            elif cel.IN_CONTAINER_CUM_CPU <= x <= cel.IN_POD_CUM_MEM or x in (cel.IN_POD_SINCE, cel.IN_POD_CREATED):
+                per += 8
+            elif dim == "node" and x != cel.IN_NOW_S:
+                per += 8
+        total += n * per
+    return total
+
+
+def run_metrics(n_nodes: int, n_pods: int, scrapes: int, warmup: int, seed: int, sample_every: int = 97,
+                copy: bool = True, device: int = 0) -> dict:
+    """kwok_amd/metrics/metrics-resource.yaml (kwok's shipped Metric CR: node / pod / container
+    gauges and counters of Usage, CumulativeUsage and SinceSecond) evaluated for every series of
+    the cluster per scrape (pkg/kwok/metrics/metrics.go:168-462: the per-node endpoint, all nodes'
+    scrapes in one batch): kwk_usage (the usage-from-annotation ClusterResourceUsage, per-pod
+    outputs) + kwk_metrics_eval_device, timed by HIP events on the engine's stream; with `copy`
+    also the rate with every value copied to the host (kwk_metrics_eval).  Every `sample_every`-th
+    node's series are checked against oracle/metrics_ref.py (the shipped CR's values restated)
+    within 1e-6 relative over two scrapes."""
+    import copy as _copy
+    import math
+    from .host import cel
+    from .host.metrics import MetricsProgram, load_metric_yaml
+    from .host.usage import UsageProgram, load_usage_yaml, usage_columns
+    t_setup = time.perf_counter()
+    pvars, pidx, node_ptr = c4_pod_workload(n_nodes, n_pods, seed)
+    prog = KindProgram(load_stage_files(*W.stage_paths(W.POD_FAST)))
+    prog.explore(pvars)
+    ing = Ingest(prog)
+    hot, dels, rec, cls = ing.variant_columns(pvars, pidx)
+    pods = Engine(prog, capacity=n_pods, device=device, max_records=max(1, len(ing.records)) + 16)
+    pods.load_stages()
+    pods.load(hot, dels, rec, cls, ing.record_array())
+    del hot, dels, rec, cls
+    up = UsageProgram(*load_usage_yaml(open(USAGE_YAML).read()))
+    vkeys, cv, mv, mx, ck = usage_columns(up, pvars)
+    keys = vkeys[pidx]
+    pods.usage_config(node_ptr, keys, cv, mv, mx, ck)
+    n_containers = int((keys >> 28).astype(np.int64).sum())
+    del keys
+    pods.usage_pods(True)
+    text = open(METRIC_CR).read()
+    mp = MetricsProgram.from_native(text)
+    mp.load(pods)
+    # creation times: a day's spread of whole seconds, some pods without one (the Go zero time)
+    slots = np.arange(n_pods, dtype=np.int64)
+    created = NOW0 - ((slots * 7919) % 86400) * 10**9 - 3600 * 10**9
+    created[slots % 101 == 0] = np.iinfo(np.int64).min
+    zero_unix = float(cel.wrap_int64(cel.GO_ZERO_TIME.ns)) / 1e9
+    pods.metrics_inputs(created, np.full(n_nodes, np.iinfo(np.int64).min, dtype=np.int64), np.zeros(n_nodes), zero_unix)
+    setup_s = time.perf_counter() - t_setup
+    programs = MetricsProgram(load_metric_yaml(text)[1]).programs
+    mbytes = _metric_series_bytes(programs, n_nodes, n_pods, n_containers)
+    ubytes = n_pods * (1 + 1 + 56) + n_nodes * (4 + 32 + 24)  # id, usage key, per-pod outputs; per node
+    t = NOW0
+    dt = 10 * 10**9  # kwok's resource-metrics scrape interval is tens of seconds
+    n_series = 0
+    for k in range(warmup):
+        pods.usage(t)
+        n_series = pods.metrics_eval_device(t, 0, n_nodes)
+        t += dt
+    pods.sync()
+    ev_u, ev_m = [], []
+    t0 = time.perf_counter()
+    for k in range(scrapes):
+        pods.event_record(3 * k)
+        pods.usage(t)
+        pods.event_record(3 * k + 1)
+        pods.metrics_eval_device(t, 0, n_nodes)
+        pods.event_record(3 * k + 2)
+        t += dt
+    pods.sync()
+    wall = (time.perf_counter() - t0) / scrapes
+    for k in range(scrapes):
+        ev_u.append(pods.event_elapsed_ms(3 * k, 3 * k + 1) / 1e3)
+        ev_m.append(pods.event_elapsed_ms(3 * k + 1, 3 * k + 2) / 1e3)
+    us_s, m_s = float(np.median(ev_u)), float(np.median(ev_m))
+    out = {"metric": "metric series evaluations/sec (all nodes' scrapes per interval)",
+           "value": n_series / (us_s + m_s), "series_per_scrape": n_series, "containers": n_containers,
+           "device_us_per_scrape": round((us_s + m_s) * 1e6, 1), "usage_us": round(us_s * 1e6, 1),
+           "metrics_us": round(m_s * 1e6, 1), "wall_ms_per_scrape": round(wall * 1e3, 3),
+           "roofline": {"bound": "hbm", "achieved": round(mbytes / m_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(mbytes / m_s / 1e9 / 8000.0, 4), "traffic": None,
+                        "kernel": "metrics_kernel (8 launches: one per metric of the CR)",
+                        "bytes_per_scrape": int(mbytes)},
+           "usage_roofline_frac": round(ubytes / us_s / 1e9 / 8000.0, 4), "usage_bytes_per_scrape": int(ubytes),
+           "setup_s": round(setup_s, 1),
+           "workload": f"{n_nodes} nodes / {n_pods} pods (C4 shape: 1-4 containers, 50 % annotated), "
+                       f"{n_containers} containers; metrics-resource.yaml, {n_series} series per scrape"}
+    if copy:
+        from .host.engine import PinnedBuffer
+        buf = PinnedBuffer(8 * n_series)
+        L = abi.lib()
+        import ctypes as C
+        cnt = C.c_uint64()
+        t1 = time.perf_counter()
+        for k in range(scrapes):
+            pods.usage(t)
+            pods._check(L.kwk_metrics_eval(pods.h, t, 0, n_nodes, C.c_void_p(buf.p), n_series, C.byref(cnt)),
+                        "kwk_metrics_eval")
+            t += dt
+        out["with_host_copy_ms_per_scrape"] = round((time.perf_counter() - t1) / scrapes * 1e3, 3)
+        out["with_host_copy_series_per_s"] = n_series / ((time.perf_counter() - t1) / scrapes)
+        buf.close()
+    # sampled oracle check: every sample_every-th node over two more scrapes
+    from oracle.metrics_ref import MetricsOracle
+    docs = [d for d in __import__("yaml").safe_load_all(open(USAGE_YAML).read()) if d]
+    oracle = MetricsOracle(docs)
+    sample = list(range(3, n_nodes, sample_every))
+    objs = {}
+    for j in sample:
+        lo, hi = int(node_ptr[j]), int(node_ptr[j + 1])
+        lst = []
+        for i in range(lo, hi):
+            o = _copy.deepcopy(pvars[int(pidx[i])])
+            o["metadata"]["name"] = f"pod-{i}"
+            lst.append(o)
+        objs[j] = lst
+    bad, checked = 0, 0
+    nodes = {j: {"metadata": {"name": f"node-{j}"}} for j in sample}
+    rel = 1e-6
+    for k in range(2):
+        t_k = t + k * dt
+        # the oracle's integrators start at the first checked scrape: the device's too (fresh engine)
+        pods.usage(t_k)
+        for j in sample:
+            lo = int(node_ptr[j])
+            name_to_slot = {o["metadata"]["name"]: lo + q for q, o in enumerate(objs[j])}
+            dev = mp.scrape(pods, t_k, j, [nodes[j]], objs[j], node_ptr)
+            exp = oracle.scrape(t_k, nodes[j], objs[j],
+                                lambda p: None if created[name_to_slot[p["metadata"]["name"]]] == np.iinfo(np.int64).min
+                                else int(created[name_to_slot[p["metadata"]["name"]]]))
+            for name, series in exp.items():
+                if k == 0 and "cpu_usage_seconds_total" in name:
+                    continue  # cumulative counters: the device integrated the timed scrapes before
+                d = dict(dev[name])
+                for lab, v in series:
+                    checked += 1
+                    got = d.get(lab)
+                    if got is None or not (got == v or abs(got - v) <= rel * max(abs(v), 1e-300) or
+                                           (math.isnan(got) and math.isnan(v))):
+                        bad += 1
+    out["sampled_oracle"] = {"nodes": len(sample), "series_checked": checked, "mismatches": bad,
+                             "note": "every %d-th node's series against oracle/metrics_ref.py (1e-6 rel); the "
+                                     "cumulative counters from the second checked scrape on" % sample_every}
+    pods.close()
+    return out

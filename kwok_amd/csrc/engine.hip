@@ -3702,6 +3702,46 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(MetricArgs a) {
   a.out[s] = run_metric_program(a, a.ops, a.n_ops, node, pod, j);
 }
 
+// Pod-major evaluation of every pod / container metric of a scrape in one launch: one thread per
+// pod of [p0, p1) finds its node once (a guess from the pods' mean per node, then a local walk:
+// no binary search over 100M entries per series), reads its state once and writes its series of
+// each metric at the metric's offset (metric-major output, as metrics_kernel: pod series at
+// pod - p0, container series at cptr[pod] - c0 + j; NaN for a dead pod).  Adjacent lanes write
+// adjacent pods' / containers' values, so the stores coalesce.  The node metrics keep
+// metrics_kernel (one thread per node).
+constexpr uint32_t kMaxPodMetrics = 16;
+struct PodMetric {
+  uint32_t dim, first_op, n_ops, pad;
+  uint64_t off;  // the metric's first value in the scrape's output
+};
+struct PodMetricList {
+  uint32_t n;
+  PodMetric m[kMaxPodMetrics];
+};
+__global__ __launch_bounds__(kBlock) void metrics_pod_kernel(MetricArgs a, PodMetricList L, double* __restrict__ out) {
+  const uint32_t pod = a.p0 + blockIdx.x * kBlock + threadIdx.x;
+  if (pod >= a.p1) return;
+  // node: the guess node_ptr would give for equal-sized nodes, corrected by walking (nodes of the
+  // scrape are consecutive; equal-sized nodes need no step)
+  uint32_t node = a.n0 + (uint32_t)((uint64_t)(pod - a.p0) * (a.n1 - a.n0) / (uint64_t)(a.p1 - a.p0));
+  if (node >= a.n1) node = a.n1 - 1;
+  while (node > a.n0 && a.node_ptr[node] > pod) --node;
+  while (node + 1 < a.n1 && a.node_ptr[node + 1] <= pod) ++node;
+  const bool alive = (load_state(a.st, pod, a.fmt).y & KWK_F_ALIVE) != 0;
+  const uint32_t cl = a.cptr[pod], ch = a.cptr[pod + 1];
+  for (uint32_t k = 0; k < L.n; ++k) {
+    const PodMetric m = L.m[k];
+    const kwk_metric_op* ops = a.ops + m.first_op;
+    if (m.dim == KWK_METRIC_DIM_POD) {
+      out[m.off + (pod - a.p0)] = alive ? run_metric_program(a, ops, m.n_ops, node, pod, 0) : __builtin_nan("");
+    } else {
+      double* o = out + m.off + (cl - a.c0);
+      for (uint32_t j = 0; j < ch - cl; ++j)
+        o[j] = alive ? run_metric_program(a, ops, m.n_ops, node, pod, j) : __builtin_nan("");
+    }
+  }
+}
+
 // Go's uint64(float64) on amd64 (the compiler's float64ToUint64 lowering): x < 2^63 ->
 // CVTTSD2SQ (truncation; -Inf, NaN-free values <= -2^63 give the "integer indefinite"
 // 0x8000000000000000), else CVTTSD2SQ(x - 2^63) | 1 << 63 (NaN and x >= 2^64: 1 << 63)
@@ -4351,14 +4391,14 @@ struct kwk_engine {
   bool persist16 = true;      // 2-byte sweep: persistent grid for large engines
   bool use_fsm = true;        // 2-byte sweep: transition table
   bool usage_key8 = true;     // usage fast path: the 1-byte key column when it exists
-  bool agg_fused = true;      // KWK_TUNE_AGG_FUSED: kwk_aggregate's mask counts inside the usage kernel
+  bool agg_fused = true;      // KWK_TUNE_USAGE & KWK_USAGE_AGG_FUSED: kwk_aggregate's mask counts inside the usage kernel
   int n_cus = 256;
   std::vector<std::pair<const void*, int>> occupancy;  // blocks per CU per kernel (this engine's device)
   uint32_t* d_fsm = nullptr;  // transition table of the 2-byte format (fsm_build_kernel)
   int64_t* d_fsm_due = nullptr;
   uint32_t fsm_bits = 0;
   int fsm_harness = -1;       // harness enable the table was built for (-1: no table)
-  uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_FSM_KERNEL: 0 never, else its prefetch depth
+  uint32_t fsm_kernel = kFsmKernelDefault;  // KWK_TUNE_SWEEP16 kernel: 0 never, else its prefetch depth
   // the 1-byte format (StateFmt.byte): a dictionary of the half words that can occur
   bool allow_byte = true;     // KWK_ENGINE_STATE16 clears it
   bool allow_dw = true;       // KWK_ENGINE_SPLIT_DUE clears it: never the fused record
@@ -5071,35 +5111,29 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (kwk_status st = set_dev(e)) return st;
   switch (key) {
-    case KWK_TUNE_FSM:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_FSM: 0 or 1");
-      e->use_fsm = value != 0;
-      HIP_TRY(hipStreamSynchronize(e->stream));
-      if (kwk_status st = build_fsm(e)) return st;
+    case KWK_TUNE_SWEEP16: {  // KWK_SWEEP16_SHAPE(q, persistent, kernel, table)
+      const uint32_t q = value & 0xFu, persist = (value >> 4) & 0xFu, kernel = (value >> 8) & 0xFu,
+                     table = (value >> 12) & 0xFu;
+      if ((q != 1 && q != 2 && q != 4) || persist > 1 || kernel > 2 || table > 1 || (value >> 16))
+        return fail(KWK_EINVAL, "KWK_TUNE_SWEEP16: KWK_SWEEP16_SHAPE(q 1|2|4, persistent 0|1, kernel 0|1|2, table 0|1)");
+      e->q16 = q;
+      e->persist16 = persist != 0;
+      e->fsm_kernel = kernel;
+      if ((table != 0) != e->use_fsm) {
+        e->use_fsm = table != 0;
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (kwk_status st = build_fsm(e)) return st;
+      }
       return refresh_format(e);
+    }
     case KWK_TUNE_BYTE_STATE:
       if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_BYTE_STATE: 0 or 1");
       e->byte_tune = value != 0;
       return refresh_format(e);
-    case KWK_TUNE_Q16:
-      if (value != 1 && value != 2 && value != 4) return fail(KWK_EINVAL, "KWK_TUNE_Q16: 1, 2 or 4");
-      e->q16 = value;
-      return KWK_OK;
-    case KWK_TUNE_PERSIST16:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_PERSIST16: 0 or 1");
-      e->persist16 = value != 0;
-      return KWK_OK;
-    case KWK_TUNE_FSM_KERNEL:
-      if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_FSM_KERNEL: 0, 1 or 2");
-      e->fsm_kernel = value;
-      return refresh_format(e);
-    case KWK_TUNE_USAGE_KEY8:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_USAGE_KEY8: 0 or 1");
-      e->usage_key8 = value != 0;
-      return KWK_OK;
-    case KWK_TUNE_AGG_FUSED:
-      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_AGG_FUSED: 0 or 1");
-      e->agg_fused = value != 0;
+    case KWK_TUNE_USAGE:
+      if (value > 3) return fail(KWK_EINVAL, "KWK_TUNE_USAGE: KWK_USAGE_KEY8 | KWK_USAGE_AGG_FUSED bits");
+      e->usage_key8 = (value & KWK_USAGE_KEY8) != 0;
+      e->agg_fused = (value & KWK_USAGE_AGG_FUSED) != 0;
       return KWK_OK;
     case KWK_TUNE_STREAM_PRIORITY: {  // the engine's stream re-created at the HIP priority asked for
       if (value > 2) return fail(KWK_EINVAL, "KWK_TUNE_STREAM_PRIORITY: 0 (default), 1 (greatest) or 2 (least)");
@@ -6620,10 +6654,9 @@ kwk_status kwk_metrics_inputs(kwk_engine* e, const int64_t* pod_created, const i
   return KWK_OK;
 }
 
-kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out, uint64_t cap,
-                            uint64_t* n_out) {
-  ErrScope es_(e);
-  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+// the metric kernels of a scrape into d_mout (enqueue only); *n_out = the values
+static kwk_status enqueue_metrics(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, bool run,
+                                  uint64_t* n_out) {
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
   if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
@@ -6638,8 +6671,7 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
   for (const auto& m : e->metrics)
     total += m.dimension == KWK_METRIC_DIM_NODE ? n_nodes : m.dimension == KWK_METRIC_DIM_POD ? (p1 - p0) : (c1 - c0);
   *n_out = total;
-  if (!out || total == 0) return KWK_OK;
-  if (total > cap) return fail(KWK_ECAP, "metric buffer too small: need " + std::to_string(total));
+  if (!run || total == 0) return KWK_OK;
   if (total > e->mout_cap) {
     if (e->d_mout) HIP_TRY(hipFree(e->d_mout));
     e->d_mout = nullptr;
@@ -6647,18 +6679,53 @@ kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, 
     e->mout_cap = total;
   }
   uint64_t off = 0;
+  PodMetricList pl{};
   for (const auto& m : e->metrics) {
     MetricArgs a = metric_args(e, m.dimension, now_ns, n0, n1, p0, p1, c0, n_nodes);
-    a.ops = e->d_mops + m.first_op;
-    a.n_ops = m.n_ops;
-    a.out = e->d_mout + off;
-    if (a.n_series)
-      hipLaunchKernelGGL(metrics_kernel, dim3((a.n_series + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
-    HIP_TRY(hipGetLastError());
+    if (m.dimension != KWK_METRIC_DIM_NODE && pl.n < kMaxPodMetrics) {  // pod-major launch below
+      pl.m[pl.n++] = PodMetric{m.dimension, m.first_op, m.n_ops, 0u, off};
+    } else {
+      a.ops = e->d_mops + m.first_op;
+      a.n_ops = m.n_ops;
+      a.out = e->d_mout + off;
+      if (a.n_series)
+        hipLaunchKernelGGL(metrics_kernel, dim3((a.n_series + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a);
+      HIP_TRY(hipGetLastError());
+    }
     off += a.n_series;
   }
+  if (pl.n && p1 > p0) {
+    MetricArgs a = metric_args(e, KWK_METRIC_DIM_POD, now_ns, n0, n1, p0, p1, c0, n_nodes);
+    a.ops = e->d_mops;
+    hipLaunchKernelGGL(metrics_pod_kernel, dim3((p1 - p0 + kBlock - 1) / kBlock), dim3(kBlock), 0, e->stream, a, pl,
+                       e->d_mout);
+    HIP_TRY(hipGetLastError());
+  }
+  return KWK_OK;
+}
+
+kwk_status kwk_metrics_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, double* out, uint64_t cap,
+                            uint64_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  uint64_t total = 0;
+  if (kwk_status st = enqueue_metrics(e, now_ns, node_first, n_nodes, false, &total)) return st;
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "metric buffer too small: need " + std::to_string(total));
+  if (kwk_status st = enqueue_metrics(e, now_ns, node_first, n_nodes, true, &total)) return st;
   HIP_TRY(hipMemcpyAsync(out, e->d_mout, 8 * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_metrics_eval_device(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes,
+                                   const double** out, uint64_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !out || !n_out) return fail(KWK_EINVAL, "null argument");
+  *out = nullptr;
+  if (kwk_status st = enqueue_metrics(e, now_ns, node_first, n_nodes, true, n_out)) return st;
+  *out = e->d_mout;
   return KWK_OK;
 }
 
@@ -6732,10 +6799,8 @@ kwk_status kwk_histograms_load(kwk_engine* e, uint32_t n_hist, const kwk_histogr
   return KWK_OK;
 }
 
-kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, uint64_t* out,
-                               uint64_t cap, uint64_t* n_out) {
-  ErrScope es_(e);
-  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+static kwk_status enqueue_histograms(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, bool run,
+                                     uint64_t* n_out) {
   if (!e->d_node_ptr) return fail(KWK_ESTATE, "kwk_usage_config must be called first");
   if (!e->d_pod_out) return fail(KWK_ESTATE, "kwk_usage_pods(eng, 1) must be called first");
   if (e->has_mixed_keys && !e->d_mixed) return fail(KWK_ESTATE, "kwk_usage_mixed must be called first");
@@ -6750,8 +6815,7 @@ kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_firs
   for (const auto& h : e->hists)
     total += (uint64_t)metric_args(e, h.dim, now_ns, n0, n1, p0, p1, c0, n_nodes).n_series * h.out_words;
   *n_out = total;
-  if (!out || total == 0) return KWK_OK;
-  if (total > cap) return fail(KWK_ECAP, "histogram buffer too small: need " + std::to_string(total));
+  if (!run || total == 0) return KWK_OK;
   if (total > e->hout_cap) {
     if (e->d_hout) HIP_TRY(hipFree(e->d_hout));
     e->d_hout = nullptr;
@@ -6769,8 +6833,31 @@ kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_firs
     HIP_TRY(hipGetLastError());
     off += (uint64_t)a.n_series * h.out_words;
   }
+  return KWK_OK;
+}
+
+kwk_status kwk_histograms_eval(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes, uint64_t* out,
+                               uint64_t cap, uint64_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !n_out) return fail(KWK_EINVAL, "null argument");
+  uint64_t total = 0;
+  if (kwk_status st = enqueue_histograms(e, now_ns, node_first, n_nodes, false, &total)) return st;
+  *n_out = total;
+  if (!out || total == 0) return KWK_OK;
+  if (total > cap) return fail(KWK_ECAP, "histogram buffer too small: need " + std::to_string(total));
+  if (kwk_status st = enqueue_histograms(e, now_ns, node_first, n_nodes, true, &total)) return st;
   HIP_TRY(hipMemcpyAsync(out, e->d_hout, 8 * total, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return KWK_OK;
+}
+
+kwk_status kwk_histograms_eval_device(kwk_engine* e, int64_t now_ns, uint32_t node_first, uint32_t n_nodes,
+                                      const uint64_t** out, uint64_t* n_out) {
+  ErrScope es_(e);
+  if (!e || !out || !n_out) return fail(KWK_EINVAL, "null argument");
+  *out = nullptr;
+  if (kwk_status st = enqueue_histograms(e, now_ns, node_first, n_nodes, true, n_out)) return st;
+  *out = e->d_hout;
   return KWK_OK;
 }
 

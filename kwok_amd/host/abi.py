@@ -100,13 +100,19 @@ ENGINE_WIDE_STATE = 1
 ENGINE_STATE32 = 2
 ENGINE_STATE16 = 4   # never the 1-byte dictionary format
 ENGINE_SPLIT_DUE = 8  # never the fused 8-byte record {packed word, relative due}
-TUNE_FSM, TUNE_Q16, TUNE_PERSIST16, TUNE_FSM_KERNEL, TUNE_USAGE_KEY8 = 1, 2, 3, 5, 6
+TUNE_SWEEP16 = 18  # KWK_SWEEP16_SHAPE(q, persistent, kernel, table): sweep16_shape()
+TUNE_USAGE = 19    # USAGE_KEY8 | USAGE_AGG_FUSED
+USAGE_KEY8, USAGE_AGG_FUSED = 1, 2
 TUNE_COMPACT_SMALL = 8
 TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
-TUNE_AGG_FUSED = 13
 TUNE_STREAM_PRIORITY = 15
 TUNE_FUSE_STEPS = 17
+
+
+def sweep16_shape(q: int = 4, persistent: int = 1, kernel: int = 2, table: int = 1) -> int:
+    """KWK_SWEEP16_SHAPE: the value of KWK_TUNE_SWEEP16 (defaults = KWK_SWEEP16_DEFAULT)."""
+    return q | persistent << 4 | kernel << 8 | table << 12
 
 
 class Lease(C.Structure):
@@ -182,6 +188,7 @@ EXPORTS = [
     "kwk_fired_compact_packed", "kwk_fired_packed", "kwk_fired_packed_device", "kwk_fired_compact_packed16",
     "kwk_fired_packed16", "kwk_fired_fetch_async", "kwk_fired_fetch_wait",
     "kwk_fired_compact_bits", "kwk_fired_bits", "kwk_fired_keep", "kwk_fired_fetch_step",
+    "kwk_metrics_eval_device", "kwk_histograms_eval_device",
 ]
 ABI_VERSION = 2  # KWK_ABI_VERSION of include/kwok_engine.h: the library must match the structs above
 TICK_COMPACT = 1 << 0  # KWK_TICK_COMPACT
@@ -226,6 +233,10 @@ def lib():
     L.kwk_metrics_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_metrics_inputs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double]
     L.kwk_metrics_eval.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _p(C.c_uint64)]
+    L.kwk_metrics_eval_device.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, _p(C.c_void_p),
+                                          _p(C.c_uint64)]
+    L.kwk_histograms_eval_device.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, _p(C.c_void_p),
+                                             _p(C.c_uint64)]
     L.kwk_histograms_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
     L.kwk_histograms_eval.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
                                       _p(C.c_uint64)]

@@ -498,6 +498,19 @@ class Engine:
                       "kwk_metrics_eval")
         return out
 
+    def metrics_eval_device(self, now_ns: int, node_first: int, n_nodes: int) -> int:
+        """kwk_metrics_eval_device: the scrape's values left on the device (enqueue only) -> their count."""
+        p, cnt = C.c_void_p(), C.c_uint64()
+        self._check(abi.lib().kwk_metrics_eval_device(self.h, now_ns, node_first, n_nodes, C.byref(p), C.byref(cnt)),
+                    "kwk_metrics_eval_device")
+        return int(cnt.value)
+
+    def histograms_eval_device(self, now_ns: int, node_first: int, n_nodes: int) -> int:
+        p, cnt = C.c_void_p(), C.c_uint64()
+        self._check(abi.lib().kwk_histograms_eval_device(self.h, now_ns, node_first, n_nodes, C.byref(p),
+                                                          C.byref(cnt)), "kwk_histograms_eval_device")
+        return int(cnt.value)
+
     def usage(self, now_ns: int):
         self._check(abi.lib().kwk_usage(self.h, now_ns), "kwk_usage")
 

@@ -33,6 +33,8 @@ def lib():
         L.rc_last_error.restype = C.c_char_p
         L.rc_query.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
         L.rc_requirement.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p]
+        L.rc_feature.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p]
+        L.rc_feature.restype = C.c_int64
         L.rc_int_from.argtypes = [C.c_int, C.c_int64, C.c_char_p, C.c_char_p, C.POINTER(C.c_int64)]
         L.rc_duration_from.argtypes = [C.c_int, C.c_int64, C.c_char_p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
         L.rc_parse_int.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
@@ -88,6 +90,14 @@ def dumps(obj) -> bytes:
 def query(src: str, obj):
     """Query.Execute: list of outputs, or None for the nil result."""
     return json.loads(_call_str(lib().rc_query, _s(src), dumps(obj)))
+
+
+def feature(src: str, obj, literals) -> int:
+    """bit 0: the query has an output; bit 1 + i: some output hasValue literal i (selector.go:101-111)."""
+    r = lib().rc_feature(_s(src), dumps(obj), dumps(list(literals)))
+    if r < 0:
+        raise ValueError(lib().rc_last_error().decode())
+    return int(r)
 
 
 def requirement(key: str, op: str, values, obj) -> bool:

@@ -479,6 +479,26 @@ extern "C" {
 
 const char* rc_last_error() { return g_err.c_str(); }
 
+// One compiled feature of a selector key: bit 0 = the query has an output (Exists), bit 1 + i =
+// hasValue(output, literal i) for some output (selector.go:65-120: strings, bools, gojq ints).
+// -1 on a query the oracle cannot parse.
+int64_t rc_feature(const char* src, const char* obj_json, const char* lits_json) {
+  try {
+    Query q(src);
+    std::vector<JVP> res;
+    q.execute(parse_json(obj_json), res);
+    JVP lits = parse_json(lits_json);
+    int64_t m = res.empty() ? 0 : 1;
+    for (size_t i = 0; i < lits->a.size() && i < 62; ++i)
+      for (auto& d : res)
+        if (Requirement::has_value(d, {lits->a[i]->s})) { m |= (int64_t)1 << (i + 1); break; }
+    return m;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
 // Query.Execute: writes JSON array of outputs, or "null" for the nil result.
 int rc_query(const char* src, const char* obj_json, char* out, int cap) {
   try {

@@ -140,14 +140,14 @@ def oracle_pred(desc: dict, obj: dict) -> int:
     feature)."""
     pred = 0
     for f in desc["features"]:
-        out = refcpu.query(f["query"], obj) or []
-        if not out:
+        lits = list(f["literals"].items())
+        m = refcpu.feature(f["query"], obj, [v for v, _ in lits])  # hasValue: strings, bools, gojq ints
+        if not m & 1:
             continue
         if f["present_bit"] is not None:
             pred |= 1 << f["present_bit"]
-        for v, b in f["literals"].items():
-            if any((isinstance(d, str) and d == v) or (isinstance(d, bool) and ("true" if d else "false") == v)
-                   for d in out):
+        for i, (_, b) in enumerate(lits):
+            if m >> (i + 1) & 1:
                 pred |= 1 << b
     if desc["finalizer_other_bit"] is not None:
         for x in (obj.get("metadata") or {}).get("finalizers") or []:

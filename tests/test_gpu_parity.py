@@ -28,9 +28,9 @@ def test_pod_fast_c1_mini(state):
     tuning, kernel = {}, {"auto": abi.SWEEP_8, "u16": abi.SWEEP_16_FSM, "u32": abi.SWEEP_W4, "dw": abi.SWEEP_WD,
                           "wide": abi.SWEEP_W8}.get(state)
     if state == "auto-nofsm":
-        tuning, kernel, state = {abi.TUNE_FSM: 0}, abi.SWEEP_16, "auto"
+        tuning, kernel, state = {abi.TUNE_SWEEP16: abi.sweep16_shape(table=0)}, abi.SWEEP_16, "auto"
     elif state == "auto-gen":
-        tuning, kernel, state = {abi.TUNE_FSM_KERNEL: 0}, abi.SWEEP_16, "auto"
+        tuning, kernel, state = {abi.TUNE_SWEEP16: abi.sweep16_shape(kernel=0)}, abi.SWEEP_16, "auto"
     elif state == "auto-pair":
         tuning, kernel, state = {abi.TUNE_COMPACT_SMALL: 0}, abi.SWEEP_8, "auto"
     elif state == "u16-pair":
@@ -93,7 +93,7 @@ def test_fused_due_epoch(clock):
 def test_node_fast_heartbeat(state):
     tuning = {}
     if state == "auto-nofsm":
-        tuning = {abi.TUNE_FSM: 0}
+        tuning = {abi.TUNE_SWEEP16: abi.sweep16_shape(table=0)}
         state = "auto"
     cl = W.make_cluster("C1", 64, 64, seed=13)
     objs = cl.nodes.materialize()

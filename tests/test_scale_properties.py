@@ -73,14 +73,14 @@ def test_three_sweeps_agree_at_4m_pods():
 def test_sweep16_tile_shapes_agree_at_17m_pods():
     """The 2-byte sweep's kernels and tile shapes: the table-only sweep (pod-fast has no general
     table entry) with the next 2 or 1 tiles in flight and the general sweep16_kernel
-    (KWK_TUNE_FSM_KERNEL 0), at Q = 4 (8192-word tiles, persistent grid: at 17M pods the tiles
+    (KWK_TUNE_SWEEP16 kernel 0), at Q = 4 (8192-word tiles, persistent grid: at 17M pods the tiles
     outnumber twice the resident blocks), Q = 2 and Q = 1 (one block per tile) must fire the
     same sets, leave the same words and count the same statistics."""
     from kwok_amd.host import abi
-    shapes = {"4": {abi.TUNE_Q16: 4}, "4-d1": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 1},
-              "4-gen": {abi.TUNE_Q16: 4, abi.TUNE_FSM_KERNEL: 0}, "2": {abi.TUNE_Q16: 2},
-              "1": {abi.TUNE_Q16: 1}, "1-gen": {abi.TUNE_Q16: 1, abi.TUNE_FSM_KERNEL: 0}}
-    byte_shapes = {"id8": {}, "id8-d1": {abi.TUNE_FSM_KERNEL: 1}}  # the 1-byte id sweep, 2 / 1 tiles in flight
+    sh = lambda **k: {abi.TUNE_SWEEP16: abi.sweep16_shape(**k)}  # noqa: E731
+    shapes = {"4": sh(q=4), "4-d1": sh(q=4, kernel=1), "4-gen": sh(q=4, kernel=0), "2": sh(q=2), "1": sh(q=1),
+              "1-gen": sh(q=1, kernel=0)}
+    byte_shapes = {"id8": {}, "id8-d1": sh(kernel=1)}  # the 1-byte id sweep, 2 / 1 tiles in flight
     engines = {}
     try:
         for q, tuning in shapes.items():

@@ -294,7 +294,7 @@ def test_gpu_usage_fast_path_irregular_nodes(state, n_pods):
 def test_gpu_usage_key8_column_matches_4byte_keys(state):
     """kwk_usage_config builds a 1-byte usage-key column when at most 256 distinct keys occur
     (the C5 pods have 2): usage_fast_kernel<WB, true> must give node sums and integrators
-    bit-identical to the 4-byte-key kernel (KWK_TUNE_USAGE_KEY8 0), and equal to numpy."""
+    bit-identical to the 4-byte-key kernel (KWK_TUNE_USAGE without KWK_USAGE_KEY8), and equal to numpy."""
     from kwok_amd.host import abi
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.engine import Engine, Ingest
@@ -320,7 +320,7 @@ def test_gpu_usage_key8_column_matches_4byte_keys(state):
     for key8 in (1, 0):
         eng = Engine(kp, capacity=len(pods), state=state)
         try:
-            eng.set_tuning(abi.TUNE_USAGE_KEY8, key8)
+            eng.set_tuning(abi.TUNE_USAGE, key8 * abi.USAGE_KEY8 | abi.USAGE_AGG_FUSED)
             eng.load_stages()
             eng.load(*cols, ing.record_array())
             eng.usage_config(ptr, keys, cv, mv)
@@ -347,7 +347,7 @@ def test_gpu_usage_one_key_runs_match_per_pod_sums(pods_per_node):
     key (< 16 keys, the C5 case) a lane's sums are read from the in-order sums of 0..16 pods of
     that key, and a lane's first node is found from the chunk's mean node size.  Both must give
     node sums and integrators bit-identical to the per-pod loop of the 4-byte-key kernel
-    (KWK_TUNE_USAGE_KEY8 0): one column with waves of one-key runs, a mixed stretch, keys >= 16,
+    (KWK_TUNE_USAGE without KWK_USAGE_KEY8): one column with waves of one-key runs, a mixed stretch, keys >= 16,
     dead pods and churned ids, 100 pods per node (the C5 shape) and 37 (irregular last node)."""
     import bench
     from kwok_amd.host import abi
@@ -371,7 +371,7 @@ def test_gpu_usage_one_key_runs_match_per_pod_sums(pods_per_node):
         pods, nodes, _ = bench.build_engines(0, n_nodes, pods_per_node, 0, 0x6B776F6B, 0.1)
         try:
             assert pods.stats()["state_bytes"] == 1
-            pods.set_tuning(abi.TUNE_USAGE_KEY8, key8)
+            pods.set_tuning(abi.TUNE_USAGE, key8 * abi.USAGE_KEY8 | abi.USAGE_AGG_FUSED)
             pods.usage_config(ptr, keys, cv, mv)
             for k in range(3):  # churned ids (pods deleted by the harness read as dead)
                 pods.step(bench.NOW0 + k * 10**9, 1, k)
@@ -392,7 +392,7 @@ def test_gpu_usage_one_key_runs_match_per_pod_sums(pods_per_node):
 @pytest.mark.parametrize("pods_per_node", [100, 7])
 def test_gpu_aggregate_counts_in_usage_pass(pods_per_node):
     """kwk_aggregate on 1-byte ids with usage: the mask counts taken inside the usage kernel's pass
-    (KWK_TUNE_AGG_FUSED 1, the default) equal a count pass of their own (0) and kwk_count, and the
+    (KWK_USAGE_AGG_FUSED, the default) equal a count pass of their own (0) and kwk_count, and the
     usage sums are unchanged — 2M pods of the C5 shape after churn steps; 100 pods per node (the
     branch-free rows) and 7 (runs crossing several node boundaries: the per-pod loop)."""
     import bench
@@ -410,10 +410,10 @@ def test_gpu_aggregate_counts_in_usage_pass(pods_per_node):
         now = bench.NOW0 + 10 * 10**9
         outs = []
         for fused in (1, 0):
-            pods.set_tuning(abi.TUNE_AGG_FUSED, fused)
+            pods.set_tuning(abi.TUNE_USAGE, abi.USAGE_KEY8 | fused * abi.USAGE_AGG_FUSED)
             n = pods.aggregate(pm, now, usage=True)
             outs.append(pods.aggregate_read(n))
-        pods.set_tuning(abi.TUNE_AGG_FUSED, 1)
+        pods.set_tuning(abi.TUNE_USAGE, abi.USAGE_KEY8 | abi.USAGE_AGG_FUSED)
         assert np.array_equal(outs[0], outs[1])
         counts = pods.count(pm)
         n_st = len(outs[0]) - len(pm) - 2

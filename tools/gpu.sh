@@ -72,6 +72,20 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
         timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 5 >> $O/configs_C1_C4.jsonl 2> $O/config_$c.err || { tail -30 $O/config_$c.err; exit 1; }
         tail -1 $O/configs_C1_C4.jsonl | cut -c1-300
       done ;;
+    metrics)
+      # the Metric CR at C4 size (bench --config C4's metric_cr) and at 100M pods (--metrics-pods), plus a
+      # kernel trace of the 100M leg
+      timeout -k 10 400 python -u bench.py --config C4 --steps 20 --warmup 5 > $O/c4_metrics.json 2> $O/c4_metrics.err \
+        || { tail -30 $O/c4_metrics.err; exit 1; }
+      python -c "import json,sys; d=json.load(open('$O/c4_metrics.json'))['detail']['metric_cr']; print(json.dumps(d)[:900])"
+      timeout -k 10 600 python -u bench.py --metrics-pods ${arg:-100000000} > $O/metrics_100m.json 2> $O/metrics_100m.err \
+        || { tail -30 $O/metrics_100m.err; exit 1; }
+      cut -c1-900 $O/metrics_100m.json
+      TRACE
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/metrics_prof -o run -- python -u $R/bench.py \
+        --metrics-pods ${arg:-100000000} > $O/metrics_prof.log 2>&1 || { tail -30 $O/metrics_prof.log; exit 1; }
+      cd $R && python tools/rocpd_summary.py stats $(find $O/metrics_prof -name '*.db' | head -1) $O/metrics_kernel_stats.csv \
+        && cut -c1-150 $O/metrics_kernel_stats.csv | head -12 ;;
     c2prof)
       TRACE
       H="$R/bench.py --hbm-only --hbm-steps 4 --hbm-warmup 12"
