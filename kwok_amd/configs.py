@@ -320,7 +320,7 @@ def run_metrics(n_nodes: int, n_pods: int, scrapes: int, warmup: int, seed: int,
            "metrics_us": round(m_s * 1e6, 1), "wall_ms_per_scrape": round(wall * 1e3, 3),
            "roofline": {"bound": "hbm", "achieved": round(mbytes / m_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                         "frac": round(mbytes / m_s / 1e9 / 8000.0, 4), "traffic": None,
-                        "kernel": "metrics_kernel (8 launches: one per metric of the CR)",
+                        "kernel": "metrics_kernel (node series) + metrics_pod_kernel (every pod / container metric in one launch)",
                         "bytes_per_scrape": int(mbytes)},
            "usage_roofline_frac": round(ubytes / us_s / 1e9 / 8000.0, 4), "usage_bytes_per_scrape": int(ubytes),
            "setup_s": round(setup_s, 1),
@@ -335,7 +335,7 @@ def run_metrics(n_nodes: int, n_pods: int, scrapes: int, warmup: int, seed: int,
         t1 = time.perf_counter()
         for k in range(scrapes):
             pods.usage(t)
-            pods._check(L.kwk_metrics_eval(pods.h, t, 0, n_nodes, C.c_void_p(buf.p), n_series, C.byref(cnt)),
+            pods._check(L.kwk_metrics_eval(pods.h, t, 0, n_nodes, buf.p, n_series, C.byref(cnt)),
                         "kwk_metrics_eval")
             t += dt
         out["with_host_copy_ms_per_scrape"] = round((time.perf_counter() - t1) / scrapes * 1e3, 3)

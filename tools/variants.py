@@ -185,7 +185,7 @@ def build(names):
         return so
 
     with ThreadPoolExecutor(8) as ex:
-        for so in ex.map(one, names):
+        for so in ex.map(one, list(dict.fromkeys(names))):  # "run a b a b" alternates; each is built once
             print(so, flush=True)
 
 
