@@ -604,6 +604,8 @@ def main():
                          "launch, 0 / 1 one step per launch")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
                     help="diagnostic: KWK_TUNE_COMPACT_SMALL for the pod engine (-1: default)")
+    ap.add_argument("--tail-handback", type=int, default=-1, choices=(-1, 0, 1),
+                    help="diagnostic: KWK_TUNE_TAIL_HANDBACK for both engines (-1: default, 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI); gloo to rehearse ranks sharing a GPU")
     ap.add_argument("--pcie-handback", choices=("bits", "packed16", "packed", "rec"), default="bits",
                     help="the PCIe-inclusive leg's hand-back format (default: the fewest bytes per transition)")
@@ -705,6 +707,9 @@ def main():
     if args.tune_compact_small >= 0:
         from kwok_amd.host import abi
         pods.set_tuning(abi.TUNE_COMPACT_SMALL, args.tune_compact_small)
+    if args.tail_handback >= 0:
+        for e in (pods, nodes):
+            e.set_tuning(abi.TUNE_TAIL_HANDBACK, args.tail_handback)
     dt = args.dt_ms * 10**6
     reporter = Reporter(pods, nodes, dist, f"cuda:{local_rank}" if dist is not None else None, args.collective, local_rank)
     report_every = 0 if args.pmc_child else args.report_every

@@ -227,6 +227,12 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
 #define KWK_TUNE_COMPACT_SMALL 8 /* fired hand-back: the most segments compacted in one launch (each block sums
                                    the counts before its own), 0..8192 (default 8192); more use the scan +
                                    expansion pair; 0 = always the pair */
+#define KWK_TUNE_TAIL_HANDBACK 20 /* kwk_step_n / _pair / kwk_tick on 2-byte table-only engines swept one tile per
+                                     workgroup (node kinds, the strong-scaling shards' node engines) within
+                                     KWK_TUNE_COMPACT_SMALL segments: 1 (default) = the sweep writes the step's
+                                     list itself (each workgroup adds the counts of the ones before it, then copies
+                                     its records: no compaction launch), 0 = a compaction launch after the sweep.
+                                     The lists are identical */
 #define KWK_TUNE_BYTE_STATE 9 /* the 1-byte dictionary format for table-only programs, 1 (default) or 0 (the
                                  2-byte words): DESIGN.md §3 */
 #define KWK_TUNE_STREAM_PRIORITY 15 /* the engine's stream: 0 (default priority), 1 (the device's greatest) or 2 (its

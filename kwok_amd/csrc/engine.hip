@@ -316,6 +316,15 @@ struct SweepArgs {
   kwk_fired_rec* __restrict__ firedx[kMaxFuseSteps - 1];
   uint32_t* __restrict__ countsx[kMaxFuseSteps - 1];
   int64_t nowx[kMaxFuseSteps - 1];
+  // the hand-back inside a one-tile-per-block 2-byte sweep (tail_handback; out == null: none)
+  struct TailHb {
+    void* out;                     // the ring slot's list: kwk_fired_rec, or packed 4-byte records
+    uint32_t* offsets;             // [0] <- the list length
+    uint32_t* host_len;            // kwk_fired_keep's pinned length word, or null
+    unsigned long long* status;    // per block: seq << 32 | the block's records
+    uint32_t seq;                  // this launch's tag (never 0)
+    uint32_t packed;
+  } tail;
 };
 
 __host__ __device__ __forceinline__ bool stage_matches(const kwk_stage_desc& s, uint32_t pred) {
@@ -1005,6 +1014,68 @@ __device__ __forceinline__ uint2 general16(uint32_t i, uint32_t raw) {
   return make_uint2(e, f.bytes);
 }
 
+// The hand-back inside a one-tile-per-block sweep (small sweeps: the node kinds, the strong-scaling
+// shards' node engines; the bench's N = 8 shard step was bound by the node engine's chain of two
+// launches per step): each block publishes its fired count tagged with the launch's sequence
+// number, sums the counts of the blocks before it — blocks are dispatched in index order, so every
+// one of them has started, and none waits on a later block — and copies its waves' records to the
+// dense list at that offset.  The list (order, slots, record layout) is compact_small_kernel's:
+// segments in order, each segment's records in order.
+template <uint32_t kWaveSlots, uint32_t kSegWords>
+__device__ __forceinline__ void tail_handback(const SweepArgs& a, uint32_t wave_n, uint32_t lane, uint32_t wave) {
+  __shared__ uint32_t s_wn[kWavesPerBlock];
+  __shared__ uint32_t s_pre;
+  const SweepArgs::TailHb& t = a.tail;
+  // the block's segments (buffer stores) complete before its waves read them back below (a
+  // workgroup-scope fence: an agent-scope one writes the XCD's L2 back, r6h: the node step 7.6 ->
+  // 18.4 us).  The status words need none: agent-scope atomics are coherent across the XCDs' L2s
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) s_wn[wave] = wave_n;
+  __syncthreads();
+  const uint32_t bt = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&t.status[blockIdx.x], (unsigned long long)t.seq << 32 | bt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0) {
+    uint32_t pre = 0;
+    for (uint32_t j0 = 0; j0 < blockIdx.x; j0 += 64u) {
+      const uint32_t j = j0 + lane;
+      if (j < blockIdx.x) {
+        unsigned long long v;
+        v = __hip_atomic_load(&t.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((uint32_t)(v >> 32) != t.seq) {  // a block before this one still sweeping: back off
+          __builtin_amdgcn_s_sleep(2);
+          v = __hip_atomic_load(&t.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        pre += (uint32_t)v;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    if (lane == 0) s_pre = pre;
+  }
+  __syncthreads();
+  uint32_t off = s_pre;
+  for (uint32_t w = 0; w < wave; ++w) off += s_wn[w];
+  const uint64_t seg_id = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint32_t* __restrict__ sp = reinterpret_cast<const uint32_t*>(a.fired) + seg_id * kSegWords;
+  const uint32_t base = (uint32_t)seg_id * kWaveSlots;
+  for (uint32_t j = lane; j < wave_n; j += 64u) {
+    const uint32_t x = sp[1u + j];
+    const uint32_t slot = base + (x & 0x1FFFu);
+    if (t.packed) {
+      __builtin_nontemporal_store(((x >> 13) & 31u) << 27 | slot, reinterpret_cast<uint32_t*>(t.out) + off + j);
+    } else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(u32x2{slot, ((x >> 13) & 31u) | ((x >> 18) & 7u) << 16},
+                                  reinterpret_cast<u32x2*>(reinterpret_cast<kwk_fired_rec*>(t.out) + off + j));
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    t.offsets[0] = s_pre + bt;
+    if (t.host_len) t.host_len[0] = s_pre + bt;
+  }
+}
+
 constexpr int kFsmBatch = 4;  // passes (64 work items each) whose lookups are in flight together
 constexpr uint32_t kFsmKernelDefault = 2;  // table-only sweep with its prefetch depth (0: never)
 template <bool kHarness, int Q, bool kPersist, int kDepth>
@@ -1304,6 +1375,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Q >= 4 ?
   if (threadIdx.x < 3 + n_stages || threadIdx.x == kStatLine) {
     const unsigned int val = s_stat[threadIdx.x];
     if (val) atomicAdd(&a.cum[(uint64_t)blockIdx.x * kStatWords + threadIdx.x], (unsigned long long)val);
+  }
+  if constexpr (!kPersist) {
+    if (a.tail.out) tail_handback<kWave, kSeg16>(a, tile < n_tiles ? wave_fired : 0u, lane, wave);
   }
 }
 
@@ -2381,12 +2455,21 @@ __global__ __launch_bounds__(kBlock) void compact16_multi_kernel(CompactArgs4 m)
   compact16_block<kSpw>(m.a[blockIdx.y], blockIdx.x);
 }
 
-// the 2-byte hand-back in one launch for small sweeps (as compact_small_kernel below)
+// the 2-byte hand-back in one launch for small sweeps (as compact_small_kernel below), kSpw
+// segments per wave: each block sums the counts of every segment before its first (16-byte loads),
+// then each wave copies its segments' records, the first 256 of all kSpw segments loaded together.
+// (One segment per wave made the 125k-node shard's group of four steps 6104 blocks re-reading the
+// counts: 15-19 us per group, r6j.)
+constexpr uint32_t kSmall16Spw = 4;
+constexpr uint32_t kSmall16Spb = kSmall16Spw * kWavesPerBlock;  // segments per block
+template <uint32_t kSpw>
 __device__ __forceinline__ void compact16_small_block(const CompactArgs& a, const uint32_t block) {
+  constexpr uint32_t kSpb = kSpw * kWavesPerBlock;
+  static_assert(kSpb % 4 == 0, "prefix loads assume whole uint4s before the block");
   __shared__ uint32_t s_part[kWavesPerBlock];
-  __shared__ uint32_t s_seg[kWavesPerBlock];
+  __shared__ uint32_t s_seg[kSpb];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t first = block * kSegsPerBlock;
+  const uint32_t first = block * kSpb;
   const uint4* __restrict__ c4 = reinterpret_cast<const uint4*>(a.counts);
   uint32_t sum = 0;
 #pragma unroll 8
@@ -2396,28 +2479,48 @@ __device__ __forceinline__ void compact16_small_block(const CompactArgs& a, cons
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
   if (lane == 0) s_part[wave] = sum;
-  if (threadIdx.x < kSegsPerBlock) {
+  if (threadIdx.x < kSpb) {
     const uint32_t c = first + threadIdx.x < a.n_segs ? a.counts[first + threadIdx.x] : 0u;
     s_seg[threadIdx.x] = c;
     if (a.counts_out && first + threadIdx.x < a.n_segs) a.counts_out[first + threadIdx.x] = c;
   }
   __syncthreads();
-  const uint32_t seg = first + wave;
-  if (seg >= a.n_segs) return;
+  const uint32_t seg0 = first + wave * kSpw;
+  if (seg0 >= a.n_segs) return;
   uint32_t off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-  for (uint32_t w = 0; w < wave; ++w) off += s_seg[w];
-  const uint32_t c = s_seg[wave];
-  if (seg == a.n_segs - 1 && lane == 0) {
-    a.offsets[0] = off + c;
-    if (a.host_len) a.host_len[0] = off + c;
+  for (uint32_t w = 0; w < wave * kSpw; ++w) off += s_seg[w];
+  uint32_t c[kSpw];
+  uint16_t r[kSpw][4];
+#pragma unroll
+  for (uint32_t s = 0; s < kSpw; ++s) {  // (a segment holds room for >= 256 records: in bounds)
+    const uint32_t seg = seg0 + s < a.n_segs ? seg0 + s : seg0;
+    const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) r[s][k] = sp[lane + 64u * k];
+    c[s] = seg0 + s < a.n_segs ? s_seg[wave * kSpw + s] : 0u;
   }
-  const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
-  for (uint32_t j = lane; j < c; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
+#pragma unroll
+  for (uint32_t s = 0; s < kSpw; ++s) {
+    const uint32_t seg = seg0 + s;
+    if (seg >= a.n_segs) break;
+    if (seg == a.n_segs - 1 && lane == 0) {
+      a.offsets[0] = off + c[s];
+      if (a.host_len) a.host_len[0] = off + c[s];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (lane + 64u * k < c[s]) __builtin_nontemporal_store(r[s][k], out + off + lane + 64u * k);
+    const uint16_t* sp = reinterpret_cast<const uint16_t*>(a.fired32 + (uint64_t)seg * a.stride + kRec16Header / 4u);
+    for (uint32_t j = lane + 256u; j < c[s]; j += 64) __builtin_nontemporal_store(sp[j], out + off + j);
+    off += c[s];
+  }
 }
-__global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) { compact16_small_block(a, blockIdx.x); }
+__global__ __launch_bounds__(kBlock) void compact16_small_kernel(CompactArgs a) {
+  compact16_small_block<kSmall16Spw>(a, blockIdx.x);
+}
 __global__ __launch_bounds__(kBlock) void compact16_small_multi_kernel(CompactArgs4 m) {
-  compact16_small_block(m.a[blockIdx.y], blockIdx.x);
+  compact16_small_block<kSmall16Spw>(m.a[blockIdx.y], blockIdx.x);
 }
 
 // The bitmap hand-back (kwk_fired_compact_bits): the 1-byte sweep's <= 4-stage records as one
@@ -4430,6 +4533,11 @@ struct kwk_engine {
   kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
   uint32_t* d_countsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
   uint32_t* d_wave_counts = nullptr;
+  // the hand-back inside one-tile-per-block 2-byte sweeps (tail_handback, KWK_TUNE_TAIL_HANDBACK):
+  // per block the launch's tag and fired count; the tag of the last such launch
+  unsigned long long* d_tail_status = nullptr;
+  uint32_t tail_seq = 0;
+  bool tail_hb = true;
   uint32_t* d_bits_wc = nullptr;      // ... its words per segment
   uint32_t* d_bits_bsum = nullptr;    // ... its records per workgroup of bits_size_kernel
   unsigned long long* d_cum = nullptr;
@@ -4942,6 +5050,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   ALLOC(e->d_fired, sizeof(kwk_fired_rec) * ((size_t)e->n_blocks_cap * kBlock * kMinObjPerThread +
                                               (size_t)kBlock * kMaxObjPerThread));
   ALLOC(e->d_wave_counts, sizeof(uint32_t) * (n_waves + 1));
+  ALLOC(e->d_tail_status, sizeof(unsigned long long) * ((size_t)e->n_blocks_cap + 1));
   ALLOC(e->d_bits_wc, sizeof(uint32_t) * (n_waves + 4));
   ALLOC(e->d_bits_bsum, sizeof(uint32_t) * (n_waves / kSegsPerBlock + 4));
   ALLOC(e->d_cum, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords);
@@ -4956,6 +5065,7 @@ kwk_status kwk_engine_create(const kwk_engine_desc* d, kwk_engine** out) {
   hipMemsetAsync(e->d_due, 0, sizeof(int64_t) * (size_t)e->capacity, e->stream);
   hipMemsetAsync(e->d_cum, 0, sizeof(unsigned long long) * (size_t)e->n_blocks_cap * kStatWords, e->stream);
   hipMemsetAsync(e->d_wave_counts, 0, sizeof(uint32_t) * (n_waves + 1), e->stream);
+  hipMemsetAsync(e->d_tail_status, 0, sizeof(unsigned long long) * ((size_t)e->n_blocks_cap + 1), e->stream);
 #undef ALLOC
   er = hipStreamSynchronize(e->stream);
   if (er != hipSuccess) { kwk_engine_destroy(e); return fail(KWK_EHIP, hipGetErrorString(er)); }
@@ -4985,7 +5095,7 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   for (kwk_engine::HbSlot& h : e->hb) hb_free(h);
   void* ptrs[] = {e->d_firedx[0], e->d_firedx[1], e->d_firedx[2], e->d_countsx[0], e->d_countsx[1], e->d_countsx[2],
                   e->d_bits_wc, e->d_bits_bsum, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
-                  e->d_wave_counts, e->d_cum, e->d_stats,
+                  e->d_wave_counts, e->d_tail_status, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
                   e->d_lease, e->d_lease_op, e->d_lease_ops, e->d_fsm, e->d_fsm_due, e->d_mixed, e->d_ckeys, e->d_ccum,
@@ -5156,6 +5266,10 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       // prefix reads grow with the square of the segments, so the knob stops at 8192 (32 KB of counts)
       if (value > 8192) return fail(KWK_EINVAL, "KWK_TUNE_COMPACT_SMALL: 0..8192");
       e->compact_small = value;
+      return KWK_OK;
+    case KWK_TUNE_TAIL_HANDBACK:
+      if (value > 1) return fail(KWK_EINVAL, "KWK_TUNE_TAIL_HANDBACK: 0 or 1");
+      e->tail_hb = value != 0;
       return KWK_OK;
     case KWK_TUNE_FUSE_STEPS:
       if (value > kMaxFuseSteps || value == 3) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2 or 4");
@@ -5414,6 +5528,7 @@ static SweepArgs sweep_args(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64
   a.fsm_bits = 0;
   a.dw_epoch_old = e->fmt.epoch;
   a.dw_rebase = 0;
+  a.tail = SweepArgs::TailHb{nullptr, nullptr, nullptr, nullptr, 0u, 0u};
   return a;
 }
 
@@ -5454,10 +5569,20 @@ static kwk_status build_fsm(kwk_engine* e) {
   return KWK_OK;
 }
 
+// a hand-back the sweep may do itself (tail_handback): ring slot `slot` in `mode` (0 / 1); `done`
+// tells the caller whether it did (a one-tile-per-block 2-byte table-only sweep) or the caller
+// still has to compact
+struct TailReq {
+  uint32_t slot;
+  int mode;
+  bool done;
+};
+static void hb_tail_args(kwk_engine* e, const TailReq& t, SweepArgs& a);
+
 // steps > 1: the 1-byte sweep takes that many steps (now_ns + s * dt_ns) in one launch (step_group;
 // step s's segments and counts go to d_firedx / d_countsx[s - 1])
 static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uint64_t step, bool fire,
-                               uint32_t steps = 1, int64_t dt_ns = 0) {
+                               uint32_t steps = 1, int64_t dt_ns = 0, TailReq* tail = nullptr) {
   const bool fuse = steps > 1;
   if (!e) return fail(KWK_EINVAL, "null engine");
   if (!e->loaded_table) return fail(KWK_ESTATE, "kwk_load_stages must be called before kwk_step");
@@ -5543,6 +5668,10 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     e->last_sweep = kwk_sweep_info{lean ? (uint32_t)KWK_SWEEP_16_FSM : (uint32_t)KWK_SWEEP_16, QV, 0, 1, tiles,    \
                                    tiles, HV ? 1u : 0u, 0};                                                     \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
+      if (lean && tail && tiles * kWavesPerBlock <= e->compact_small) {                                         \
+        hb_tail_args(e, *tail, a);                                                                              \
+        tail->done = true;                                                                                      \
+      }                                                                                                         \
       if (lean)                                                                                                 \
         hipLaunchKernelGGL((sweep16_fsm_kernel<HV, QV, false, 1>), dim3(blocks), dim3(kBlock), 0, e->stream, a); \
       else                                                                                                      \
@@ -5716,6 +5845,13 @@ static void hb_args(const kwk_engine* e, uint32_t i, int mode, CompactArgs& a) {
   a.stride = 64u * e->last_objs + 32u;
 }
 
+static void hb_tail_args(kwk_engine* e, const TailReq& t, SweepArgs& a) {
+  const kwk_engine::HbSlot& h = e->hb[t.slot];
+  if (++e->tail_seq == 0) e->tail_seq = 1;  // 0 never tags a launch (the status words start at 0)
+  a.tail = SweepArgs::TailHb{h.list, h.offsets, e->hb_track ? e->h_len_dev + 2u * t.slot : nullptr, e->d_tail_status,
+                             e->tail_seq, t.mode == 1 ? 1u : 0u};
+}
+
 static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t stream = nullptr) {
   if (!stream) stream = e->stream;
   const uint32_t n_waves = e->last_blocks * kWavesPerBlock;
@@ -5743,7 +5879,7 @@ static kwk_status enqueue_compact(kwk_engine* e, int mode = 0, hipStream_t strea
   void* args[] = {&a};
   const uint32_t groups = (n_waves + kScanGroup - 1) / kScanGroup;
   if (mode == 2 && n_waves <= e->compact_small) {
-    hipLaunchKernelGGL(compact16_small_kernel, dim3(blocks), dim3(kBlock), 0, stream, a);
+    hipLaunchKernelGGL(compact16_small_kernel, dim3((n_waves + kSmall16Spb - 1) / kSmall16Spb), dim3(kBlock), 0, stream, a);
   } else if (mode == 3 && n_waves <= e->compact_small) {
     hipLaunchKernelGGL(bits_size_kernel, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum);
     hipLaunchKernelGGL(bits_write_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, a, e->d_bits_wc, e->d_bits_bsum,
@@ -5920,14 +6056,35 @@ kwk_status kwk_fired_packed16(kwk_engine* e, uint16_t* out, uint32_t cap, uint32
 // 78.4-78.7 us per C5 step, the persistent sweep holding the CUs the two latency-bound launches
 // then wait for; r5p / r5r.  Round 5's folded hand-back — the next sweep copying a step's 2-byte
 // list — is superseded by fused steps at the shard size and was removed in round 6.)
-static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1) {
+// the sweep of one step and its hand-back in `mode` (< 0: none) into the next ring slot — inside
+// the sweep (tail_handback) when it is a one-tile-per-block 2-byte table-only sweep, else by
+// enqueue_compact.  ev_a >= 0: events ev_a, ev_a + 1 bracket the sweep launch
+static kwk_status sweep_compact(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, int mode, int ev_a = -1) {
+  TailReq tr{0u, mode == 0 ? 0 : 1, false};  // a 2-byte sweep's records: the 2-byte / bitmap modes fall to packed
+  const bool try_tail = mode >= 0 && e->tail_hb && e->fmt.half && !e->fmt.byte && e->loaded_table;
+  if (try_tail) {
+    tr.slot = hb_next(e);
+    if (kwk_status st = hb_prepare(e, tr.slot, tr.mode, e->stream)) return st;
+  }
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a)) return st;
-  if (kwk_status st = launch_sweep(e, now, seed, step, true)) return st;
+  if (kwk_status st = launch_sweep(e, now, seed, step, true, 1, 0, try_tail ? &tr : nullptr)) return st;
   if (ev_a >= 0)
     if (kwk_status st = kwk_event_record(e, (uint32_t)ev_a + 1u)) return st;
-  if (!compact) return KWK_OK;
-  return enqueue_compact(e, compact_mode(compact));
+  if (mode < 0) return KWK_OK;
+  if (tr.done) {
+    e->compacted = true;
+    e->compacted_packed = tr.mode == 1;
+    e->compacted_16 = false;
+    e->compacted_bits = false;
+    return hb_commit(e, tr.slot, e->last_step_no, tr.mode, e->last_blocks * kWavesPerBlock, (int)tr.slot, e->stream,
+                     true);
+  }
+  return enqueue_compact(e, mode);
+}
+
+static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t step, uint32_t compact, int ev_a = -1) {
+  return sweep_compact(e, now, seed, step, compact ? compact_mode(compact) : -1, ev_a);
 }
 
 // several steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no
@@ -5978,7 +6135,8 @@ static kwk_status step_group(kwk_engine* e, uint32_t m, int64_t now, int64_t dt,
     }
     const uint32_t blocks = (n_waves + kSegsPerBlock - 1) / kSegsPerBlock;
     if (n_waves <= e->compact_small) {
-      hipLaunchKernelGGL(compact16_small_multi_kernel, dim3(blocks, m), dim3(kBlock), 0, e->stream, c4);
+      hipLaunchKernelGGL(compact16_small_multi_kernel, dim3((n_waves + kSmall16Spb - 1) / kSmall16Spb, m), dim3(kBlock), 0,
+                         e->stream, c4);
     } else {
       constexpr uint32_t W16 = kCompact16Spw;
       hipLaunchKernelGGL(seg_scan_multi_kernel, dim3((n_waves + kScanGroup - 1) / kScanGroup, m), dim3(kBlock), 0,
@@ -7310,14 +7468,9 @@ static kwk_status enqueue_tick(kwk_engine* nodes, kwk_engine* pods, int64_t now_
     HIP_TRY(hipEventRecord(pods->ev_podsync, pods->stream));
     pods->tick_pending = true;
   }
-  if (kwk_status st = launch_sweep(nodes, now_ns, seed, step, true)) return st;
-  if (compact)
-    if (kwk_status st = enqueue_compact(nodes, packed)) return st;
-  if (pods) {
-    if (kwk_status st = launch_sweep(pods, now_ns, seed, step, true)) return st;
-    if (compact)
-      if (kwk_status st = enqueue_compact(pods, packed)) return st;
-  }
+  if (kwk_status st = sweep_compact(nodes, now_ns, seed, step, compact ? (packed ? 1 : 0) : -1)) return st;
+  if (pods)
+    if (kwk_status st = sweep_compact(pods, now_ns, seed, step, compact ? (packed ? 1 : 0) : -1)) return st;
   return KWK_OK;
 }
 

@@ -108,6 +108,7 @@ TUNE_BYTE_STATE = 9
 TUNE_WORD_TILES = 10
 TUNE_STREAM_PRIORITY = 15
 TUNE_FUSE_STEPS = 17
+TUNE_TAIL_HANDBACK = 20  # the 2-byte one-tile-per-workgroup sweep writes its step's list itself (1) or not (0)
 
 
 def sweep16_shape(q: int = 4, persistent: int = 1, kernel: int = 2, table: int = 1) -> int:

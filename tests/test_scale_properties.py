@@ -610,6 +610,61 @@ def test_fused_call_every_step_list_equals_per_step_calls(n_nodes, mode):
                 p.close()
 
 
+@pytest.mark.parametrize("n_nodes", [125_000, 1_500])
+def test_tail_handback_equals_compaction_launch(n_nodes):
+    """KWK_TUNE_TAIL_HANDBACK (round 6): a 2-byte table-only node engine swept one tile per
+    workgroup (the N = 8 shard's node engine at 125k nodes: 62 workgroups; 1.5k nodes: one) writes
+    each step's list inside the sweep — every workgroup adds the counts of the workgroups before
+    it, then copies its records.  Against a twin with the compaction launch: every step's list of
+    a 10-step kwk_step_n (4-byte packed, then 8-byte records, fetched from the ring by step) is
+    identical in content and order, the states and counts equal, and kwk_tick's node lists too."""
+    import bench
+    from kwok_amd.host import abi
+    from kwok_amd.host.engine import PinnedBuffer
+    now0, dt, seed = 1_700_000_000 * 10**9, 5 * 10**9, 0x6B776F6B  # 5 s steps: heartbeats fire in both calls
+    engs = {}
+    for tail in (1, 0):
+        pods, nodes, _ = bench.build_engines(0, n_nodes, 1, 0, seed, 0.1)
+        pods.close()
+        nodes.set_tuning(abi.TUNE_TAIL_HANDBACK, tail)
+        engs[tail] = nodes
+    cap = engs[1].capacity
+    bufs = [PinnedBuffer(8 * cap + 64) for _ in range(10)]
+    try:
+        assert engs[1].stats()["state_bytes"] == 2
+        for e in engs.values():
+            e.fired_keep(16)
+        t = 0
+        for compact, rec in (("packed", np.uint32), (True, abi.FIRED_DTYPE)):
+            lists = {}
+            for tail, e in engs.items():
+                e.step_n(10, now0 + t * dt, dt, seed, t, compact)
+                assert e.last_sweep()["kernel"] == abi.SWEEP_16_FSM and not e.last_sweep()["persistent"]
+                infos = [e.fetch_step(t + k, bufs[k]) for k in range(10)]
+                e.fetch_wait()
+                lists[tail] = [bufs[k].array(rec, infos[k]["n_records"]).copy() for k in range(10)]
+            total = 0
+            for k in range(10):
+                assert np.array_equal(lists[1][k], lists[0][k]), (compact, k)
+                total += len(lists[1][k])
+            assert total > 0, "no node transition in 10 steps"
+            t += 10
+        a, b = engs[1], engs[0]
+        for col in ("pred", "sched"):
+            assert np.array_equal(a.read()[0][col], b.read()[0][col]), col
+        for key in ("fired", "matched", "fired_per_stage"):
+            assert a.stats()[key] == b.stats()[key], key
+        # kwk_tick (nodes alone): lease step + node sweep + hand-back
+        for tail, e in engs.items():
+            e.tick(None, now0 + t * dt, seed, t, "packed")
+        assert np.array_equal(a.fired_packed(), b.fired_packed())
+    finally:
+        for e in engs.values():
+            e.close()
+        for x in bufs:
+            x.close()
+
+
 def test_fused_records_load_read_step_at_4m_pods():
     """The fused records' due times at scale: 4M C2 pods loaded with a queued stage on every third
     pod, its due time inside the 68.7 s window of the first step's epoch, years before it, or

@@ -149,6 +149,10 @@ VARIANTS = {
                  "  uint32_t touch_sink = 0;\n"),
                 ("  for (int o = 32; o > 0; o >>= 1) {\n    n_matched += __shfl_xor(n_matched, o);\n    n_bytes += __shfl_xor(n_bytes, o);\n    n_line += __shfl_xor(n_line, o);\n  }\n  if (lane == 0) {\n    atomicAdd(&s_stat[0], n_matched);",
                  "  for (int o = 32; o > 0; o >>= 1) {\n    n_matched += __shfl_xor(n_matched, o);\n    n_bytes += __shfl_xor(n_bytes, o);\n    n_line += __shfl_xor(n_line, o);\n  }\n  if (touch_sink == 0x9E3779B9u && a.n == 1u) n_line += 1u;\n  if (lane == 0) {\n    atomicAdd(&s_stat[0], n_matched);")],
+    # the one-launch 2-byte hand-back with one segment per wave (round 5's) instead of four
+    "c16spw1": [("constexpr uint32_t kSmall16Spw = 4;", "constexpr uint32_t kSmall16Spw = 1;")],
+    # no hand-back inside the one-tile 2-byte sweep (KWK_TUNE_TAIL_HANDBACK 0 by default)
+    "notail": [("  bool tail_hb = true;", "  bool tail_hb = false;")],
     # the word sweep's phase 3 stores no state lines
     "w_nophase3": [("        store_chunk_nt(&gq[(wbase + (uint32_t)q * 64u * kC + lane * kC) / kC], nv);\n",
                     "        (void)gq;\n")],
