@@ -1014,12 +1014,48 @@ __device__ __forceinline__ uint2 general16(uint32_t i, uint32_t raw) {
   return make_uint2(e, f.bytes);
 }
 
+// The prefix of a block's count over the blocks of one launch (status word per block, `stride`
+// words apart: seq << 32 | count).  One wave: publishes the block's count, then loads the words of
+// every block before it — 16 per lane in flight at once, so one memory round trip up to 1024
+// blocks — re-reading (with back-off) only those not published yet: blocks are dispatched in index
+// order, so each of them has started, and none waits on a later one.  Returns the exclusive
+// prefix.
+__device__ __forceinline__ uint32_t block_prefix(unsigned long long* status, uint32_t stride, uint32_t b, uint32_t bt,
+                                                 uint32_t seq, uint32_t lane) {
+  if (lane == 0)
+    __hip_atomic_store(&status[(uint64_t)b * stride], (unsigned long long)seq << 32 | bt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  constexpr uint32_t kIn = 16;  // loads in flight per lane
+  uint32_t pre = 0;
+  for (uint32_t j0 = lane; j0 < b; j0 += 64u * kIn) {  // wave-uniform trip count: ceil(b / 1024)
+    unsigned long long v[kIn];
+#pragma unroll
+    for (uint32_t k = 0; k < kIn; ++k) {
+      const uint32_t j = j0 + 64u * k;
+      v[k] = j < b ? __hip_atomic_load(&status[(uint64_t)j * stride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : (unsigned long long)seq << 32;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kIn; ++k) {
+      const uint32_t j = j0 + 64u * k;
+      while ((uint32_t)(v[k] >> 32) != seq) {  // a block before this one still sweeping: back off
+        __builtin_amdgcn_s_sleep(2);
+        v[k] = __hip_atomic_load(&status[(uint64_t)j * stride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pre += (uint32_t)v[k];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+  return pre;
+}
+
 // The hand-back inside a one-tile-per-block sweep (small sweeps: the node kinds, the strong-scaling
 // shards' node engines; the bench's N = 8 shard step was bound by the node engine's chain of two
-// launches per step): each block publishes its fired count tagged with the launch's sequence
-// number, sums the counts of the blocks before it — blocks are dispatched in index order, so every
-// one of them has started, and none waits on a later block — and copies its waves' records to the
-// dense list at that offset.  The list (order, slots, record layout) is compact_small_kernel's:
+// launches per step): each block finds its offset by block_prefix above and copies its waves'
+// records to the dense list.  Only for grids resident in one dispatch round: no block exits before
+// every block before it has finished its tile, so a second round would start only after the whole
+// first one (the same hand-back inside the N = 8 shard's 1526-block pod sweep, more workgroups
+// than its CUs hold at once: 51-59 vs 23 us per 4-step launch, r6q-r6t; not kept).  The list (order, slots, record layout) is compact_small_kernel's:
 // segments in order, each segment's records in order.
 template <uint32_t kWaveSlots, uint32_t kSegWords>
 __device__ __forceinline__ void tail_handback(const SweepArgs& a, uint32_t wave_n, uint32_t lane, uint32_t wave) {
@@ -1033,24 +1069,8 @@ __device__ __forceinline__ void tail_handback(const SweepArgs& a, uint32_t wave_
   if (lane == 0) s_wn[wave] = wave_n;
   __syncthreads();
   const uint32_t bt = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&t.status[blockIdx.x], (unsigned long long)t.seq << 32 | bt, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
   if (wave == 0) {
-    uint32_t pre = 0;
-    for (uint32_t j0 = 0; j0 < blockIdx.x; j0 += 64u) {
-      const uint32_t j = j0 + lane;
-      if (j < blockIdx.x) {
-        unsigned long long v;
-        v = __hip_atomic_load(&t.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((uint32_t)(v >> 32) != t.seq) {  // a block before this one still sweeping: back off
-          __builtin_amdgcn_s_sleep(2);
-          v = __hip_atomic_load(&t.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        pre += (uint32_t)v;
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    const uint32_t pre = block_prefix(t.status, 1u, blockIdx.x, bt, t.seq, lane);
     if (lane == 0) s_pre = pre;
   }
   __syncthreads();
@@ -5668,7 +5688,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     e->last_sweep = kwk_sweep_info{lean ? (uint32_t)KWK_SWEEP_16_FSM : (uint32_t)KWK_SWEEP_16, QV, 0, 1, tiles,    \
                                    tiles, HV ? 1u : 0u, 0};                                                     \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
-      if (lean && tail && tiles * kWavesPerBlock <= e->compact_small) {                                         \
+      if (lean && tail && tiles <= pg && tiles * kWavesPerBlock <= e->compact_small) {                          \
         hb_tail_args(e, *tail, a);                                                                              \
         tail->done = true;                                                                                      \
       }                                                                                                         \
