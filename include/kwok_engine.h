@@ -228,8 +228,8 @@ kwk_status kwk_engine_destroy(kwk_engine* eng);
                                    the counts before its own), 0..8192 (default 8192); more use the scan +
                                    expansion pair; 0 = always the pair */
 #define KWK_TUNE_TAIL_HANDBACK 20 /* kwk_step_n / _pair / kwk_tick on 2-byte table-only engines swept one tile per
-                                     workgroup (node kinds, the strong-scaling shards' node engines) within
-                                     KWK_TUNE_COMPACT_SMALL segments: 1 (default) = the sweep writes the step's
+                                     workgroup (node kinds, the strong-scaling shards' node engines), at most a
+                                     quarter as many workgroups as the device has CUs: 1 (default) = the sweep writes the step's
                                      list itself (each workgroup adds the counts of the ones before it, then copies
                                      its records: no compaction launch), 0 = a compaction launch after the sweep.
                                      The lists are identical */

@@ -1055,7 +1055,9 @@ __device__ __forceinline__ uint32_t block_prefix(unsigned long long* status, uin
 // records to the dense list.  Only for grids resident in one dispatch round: no block exits before
 // every block before it has finished its tile, so a second round would start only after the whole
 // first one (the same hand-back inside the N = 8 shard's 1526-block pod sweep, more workgroups
-// than its CUs hold at once: 51-59 vs 23 us per 4-step launch, r6q-r6t; not kept).  The list (order, slots, record layout) is compact_small_kernel's:
+// than its CUs hold at once: 51-59 vs 23 us per 4-step launch, r6q-r6t; not kept).  Taken for
+// grids of at most a quarter as many workgroups as CUs: at the 125k-node shard (62) it shortens
+// the node chain, at 250k / 500k (123 / 245) the step was 0.7-1.3 us slower with it (r6v)  The list (order, slots, record layout) is compact_small_kernel's:
 // segments in order, each segment's records in order.
 template <uint32_t kWaveSlots, uint32_t kSegWords>
 __device__ __forceinline__ void tail_handback(const SweepArgs& a, uint32_t wave_n, uint32_t lane, uint32_t wave) {
@@ -5688,7 +5690,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     e->last_sweep = kwk_sweep_info{lean ? (uint32_t)KWK_SWEEP_16_FSM : (uint32_t)KWK_SWEEP_16, QV, 0, 1, tiles,    \
                                    tiles, HV ? 1u : 0u, 0};                                                     \
     if (2 * pg > tiles) { /* the persistent loop would run about once: one block per tile */                   \
-      if (lean && tail && tiles <= pg && tiles * kWavesPerBlock <= e->compact_small) {                          \
+      if (lean && tail && tiles * 4u <= (uint32_t)e->n_cus && tiles * kWavesPerBlock <= e->compact_small) {    \
         hb_tail_args(e, *tail, a);                                                                              \
         tail->done = true;                                                                                      \
       }                                                                                                         \
