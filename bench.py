@@ -599,7 +599,7 @@ def main():
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
-    ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4),
+    ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4, 8),
                     help="KWK_TUNE_FUSE_STEPS for the pod engine: up to 4 (default) or 2 steps per 1-byte sweep "
                          "launch, 0 / 1 one step per launch")
     ap.add_argument("--tune-compact-small", type=int, default=-1,

@@ -279,8 +279,8 @@ struct RawTest {
   uint32_t term, del;  // harness: terminal phase bits / deletionTimestamp bit (pred)
 };
 
-constexpr uint32_t kMaxFuseSteps = 4;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS)
-constexpr uint32_t kHbMin = 4;         // hand-back ring slots: at least a fused launch's steps (kwk_fired_keep)
+constexpr uint32_t kMaxFuseSteps = 8;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS)
+constexpr uint32_t kHbMin = kMaxFuseSteps;  // hand-back ring slots: at least a fused launch's steps (kwk_fired_keep)
 constexpr uint32_t kHbMax = 64;
 struct SweepArgs {
   void* __restrict__ st;         // per object state word (StateFmt: uint2 {pred, sched} or packed u32)
@@ -1795,6 +1795,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPersist
         if (real) {
           w_line += n_chunks * 16u - seg_n * 2u + kRec16Header - 4u;  // padding and header: line bytes only
           w_bytes += 2u * seg_n + 4u;
+        }
+        if constexpr (kSteps > 4) {  // a lane's byte counters hold <= 255 fires: fold them per step
+          stc[1] += stc[0] & 0x00FF00FFu;
+          stc[2] += (stc[0] >> 8) & 0x00FF00FFu;
+          stc[0] = 0u;
         }
       } else if (real) {
         const uint32_t used = 1u + seg_n, end = (used + 31u) & ~31u;
@@ -4551,9 +4556,9 @@ struct kwk_engine {
   kwk_fired_rec* d_fired = nullptr;
   // up to fuse_steps steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kSteps>):
   // steps 1.. segments and counts, rotated with d_fired / d_wave_counts by the steps' hand-backs
-  uint32_t fuse_steps = kMaxFuseSteps;
-  kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
-  uint32_t* d_countsx[kMaxFuseSteps - 1] = {nullptr, nullptr, nullptr};
+  uint32_t fuse_steps = 4;  // KWK_TUNE_FUSE_STEPS default (8 allowed)
+  kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {};
+  uint32_t* d_countsx[kMaxFuseSteps - 1] = {};
   uint32_t* d_wave_counts = nullptr;
   // the hand-back inside one-tile-per-block 2-byte sweeps (tail_handback, KWK_TUNE_TAIL_HANDBACK):
   // per block the launch's tag and fired count; the tag of the last such launch
@@ -5115,8 +5120,11 @@ kwk_status kwk_engine_destroy(kwk_engine* e) {
   if (e->stream) hipStreamSynchronize(e->stream);
   if (e->copy_stream) hipStreamSynchronize(e->copy_stream);
   for (kwk_engine::HbSlot& h : e->hb) hb_free(h);
-  void* ptrs[] = {e->d_firedx[0], e->d_firedx[1], e->d_firedx[2], e->d_countsx[0], e->d_countsx[1], e->d_countsx[2],
-                  e->d_bits_wc, e->d_bits_bsum, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
+  for (uint32_t i = 0; i + 1 < kMaxFuseSteps; ++i) {
+    if (e->d_firedx[i]) hipFree(e->d_firedx[i]);
+    if (e->d_countsx[i]) hipFree(e->d_countsx[i]);
+  }
+  void* ptrs[] = {                  e->d_bits_wc, e->d_bits_bsum, e->d_st, e->d_due, e->d_del, e->d_rec, e->d_values, e->d_table, e->d_lut, e->d_deltas, e->d_fired,
                   e->d_wave_counts, e->d_tail_status, e->d_cum, e->d_stats,
                   e->d_node_ptr, e->d_ukey, e->d_cpu, e->d_mem, e->d_node_out, e->d_node_cum, e->d_node_last,
                   e->d_usage_part, e->d_cluster, e->d_uchunk, e->d_podv, e->d_agg, e->d_agg_counts, e->d_agg_masks, e->d_count_part, e->d_stage_buf, e->d_pod_out, e->d_pod_cum, e->d_pod_last,
@@ -5294,7 +5302,8 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       e->tail_hb = value != 0;
       return KWK_OK;
     case KWK_TUNE_FUSE_STEPS:
-      if (value > kMaxFuseSteps || value == 3) return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2 or 4");
+      if (value > kMaxFuseSteps || (value > 2 && (value & (value - 1u))))
+        return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2, 4 or 8");
       e->fuse_steps = value < 2 ? 1u : value;
       return KWK_OK;
     default:
@@ -5633,7 +5642,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
 
     if (fuse) {
-      if (!s4 || (steps != 2 && steps != 4)) return fail(KWK_ESTATE, "fused steps: 2 or 4, 1-byte sweep with <= 4 stages");
+      if (!s4 || (steps != 2 && steps != 4 && steps != 8))
+        return fail(KWK_ESTATE, "fused steps: 2, 4 or 8, 1-byte sweep with <= 4 stages");
       for (uint32_t i = 0; i + 1 < steps; ++i) {
         if (!e->d_firedx[i]) return fail(KWK_ESTATE, "fused steps: buffers not allocated");
         a.firedx[i] = e->d_firedx[i];
@@ -5642,7 +5652,8 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
       }
     }
 #define K8(P, D)                                                                                        \
-  (steps == 4   ? (const void*)sweep8_kernel<P, D, true, 4>                                            \
+  (steps == 8   ? (const void*)sweep8_kernel<P, D, true, 8>                                            \
+   : steps == 4 ? (const void*)sweep8_kernel<P, D, true, 4>                                            \
    : steps == 2 ? (const void*)sweep8_kernel<P, D, true, 2>                                            \
    : s4         ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
@@ -6112,13 +6123,13 @@ static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t s
 // several steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no
 // due time (objects then step independently of the clock except through due times already
 // queued, which each step tests at its own now) and whose records are the 2-byte ones.  The steps
-// a launch takes: 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
+// a launch takes: 8, 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
 // sample per launch (ev_every 2 or 3: pairs; 1: none fused)
 static uint32_t fuse_group(const kwk_engine* e, uint32_t left, uint32_t ev_every) {
   if (e->fuse_steps < 2 || !e->fmt.byte || e->n_stages > 4 || e->fsm8_due_any || !e->loaded_table || ev_every == 1)
     return 1;
   uint32_t m = e->fuse_steps;
-  if (ev_every && ev_every < 4) m = 2;
+  while (ev_every && m > 2 && m > ev_every) m >>= 1;  // at most one event sample per launch
   while (m > left) m >>= 1;
   return m ? m : 1;
 }
