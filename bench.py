@@ -599,7 +599,7 @@ def main():
     ap.add_argument("--tune-priority", type=int, default=1,
                     help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
                          "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg); 0: both default")
-    ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4, 8),
+    ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4),
                     help="KWK_TUNE_FUSE_STEPS for the pod engine: up to 4 (default) or 2 steps per 1-byte sweep "
                          "launch, 0 / 1 one step per launch")
     ap.add_argument("--tune-compact-small", type=int, default=-1,
@@ -774,6 +774,21 @@ def main():
         nodes.close()
         return
 
+    # the bytes of one sampled launch (the first of a reporting interval: fused_first steps): one more
+    # such launch after the timed region, alone between two stats reads (the timed launches share the
+    # stats counters; their average over the 4-, 2- and 1-step launches would understate it)
+    fused_first = 1
+    if pod_kernel["kernel"] == abi.SWEEP_8:
+        fused_first = args.fuse_steps if args.fuse_steps >= 2 and len(pods.p.stages) <= 4 else 1
+        while fused_first > max(1, report_every or args.steps):
+            fused_first >>= 1
+    k0 = args.warmup + args.steps
+    sa = pods.stats()
+    pods.step_n_pair(nodes, fused_first, NOW0 + k0 * dt, dt, args.seed, k0, HANDBACK[args.handback])
+    pods.sync()
+    nodes.sync()
+    first_bytes, first_lines = sweep_bytes(sa, pods.stats())
+
     # PCIe-inclusive rate: the same steps with every fired record copied to pinned host memory
     pcie = None
     if args.pcie_steps > 0 and world == 1:
@@ -844,7 +859,7 @@ def main():
                     else 1)
         launches = sweep_launches(args.steps, report_every, fuse_max)
         spl = args.steps / launches  # steps per pod sweep launch (mean)
-        achieved = (pbytes / launches) / pod_kernel_s / 1e9
+        achieved = first_bytes / pod_kernel_s / 1e9  # the sampled launches' bytes / their duration
         sb = int(s1p["state_bytes"])
         tr = None if traffic is None else traffic["read"] + traffic["write"]
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -854,15 +869,17 @@ def main():
                                  "per launch" if traffic else f"null: {pmc_err}"),
                 "kernel": SWEEP_NAMES.get(pod_kernel["kernel"], "?") + (" persistent" if pod_kernel["persistent"] else "")
                           + " (pods)",
-                "bytes_per_launch": int(pbytes / launches), "state_bytes_per_object": sb,
-                "steps_per_launch": round(spl, 3), "launches": launches,
-                "launch_note": "bytes per launch = the timed region's pod sweep bytes / its launches (fused launches of "
-                               "4 and 2 steps averaged); avg_launch_us = the sampled launches (the first of each "
-                               "reporting interval: 4 steps when fused), so `achieved` understates a 4-step launch's",
+                "bytes_per_launch": int(first_bytes), "state_bytes_per_object": sb,
+                "steps_per_launch": fused_first, "launches": launches,
+                "mean_bytes_per_launch": int(pbytes / launches), "mean_steps_per_launch": round(spl, 3),
+                "launch_note": "avg_launch_us = the sampled launches (the first of each reporting interval: "
+                               f"{fused_first} step(s)); bytes_per_launch = the bytes of one such launch, counted "
+                               "alone after the timed region (mean_bytes_per_launch: the timed region's bytes over "
+                               "all its launches of every size)",
                 "avg_launch_us": round(pod_kernel_s * 1e6, 2),
                 # the same count with state writes as the whole 128-byte lines the sweep stores
-                "line_bytes_per_launch": int(plines / launches),
-                "line_frac": round(plines / launches / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
+                "line_bytes_per_launch": int(first_lines),
+                "line_frac": round(first_lines / pod_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
         if tr:
             roof["traffic_GBps"] = round(tr / pod_kernel_s / 1e9, 1)
         cpu = None

@@ -409,7 +409,7 @@ kwk_status kwk_fired_fetch_wait(kwk_engine* eng);
 
 /* Every step's hand-back to the host, fused steps included (the playStage workers' input for each
  * step, pod_controller.go:257-290).  kwk_fired_keep(eng, depth) keeps the lists of the last `depth`
- * compactions (1..64, at least 8: a fused launch's steps; 0 = the default: the last 8, no per-step
+ * compactions (1..64, at least 4: a fused launch's steps; 0 = the default: the last 4, no per-step
  * completion signal) in the device
  * ring and makes every compaction signal its own completion and write its length to pinned host
  * memory.  kwk_fired_fetch_step(eng, step, ...) is kwk_fired_fetch_async for the list of step

@@ -279,7 +279,7 @@ struct RawTest {
   uint32_t term, del;  // harness: terminal phase bits / deletionTimestamp bit (pred)
 };
 
-constexpr uint32_t kMaxFuseSteps = 8;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS)
+constexpr uint32_t kMaxFuseSteps = 4;  // steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS; 8 measured slower: r6x)
 constexpr uint32_t kHbMin = kMaxFuseSteps;  // hand-back ring slots: at least a fused launch's steps (kwk_fired_keep)
 constexpr uint32_t kHbMax = 64;
 struct SweepArgs {
@@ -4556,7 +4556,7 @@ struct kwk_engine {
   kwk_fired_rec* d_fired = nullptr;
   // up to fuse_steps steps per 1-byte sweep launch (KWK_TUNE_FUSE_STEPS, sweep8_kernel<..., kSteps>):
   // steps 1.. segments and counts, rotated with d_fired / d_wave_counts by the steps' hand-backs
-  uint32_t fuse_steps = 4;  // KWK_TUNE_FUSE_STEPS default (8 allowed)
+  uint32_t fuse_steps = kMaxFuseSteps;
   kwk_fired_rec* d_firedx[kMaxFuseSteps - 1] = {};
   uint32_t* d_countsx[kMaxFuseSteps - 1] = {};
   uint32_t* d_wave_counts = nullptr;
@@ -5303,7 +5303,7 @@ kwk_status kwk_set_tuning(kwk_engine* e, uint32_t key, uint32_t value) {
       return KWK_OK;
     case KWK_TUNE_FUSE_STEPS:
       if (value > kMaxFuseSteps || (value > 2 && (value & (value - 1u))))
-        return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2, 4 or 8");
+        return fail(KWK_EINVAL, "KWK_TUNE_FUSE_STEPS: 0 / 1 (off), 2 or 4");
       e->fuse_steps = value < 2 ? 1u : value;
       return KWK_OK;
     default:
@@ -5642,8 +5642,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
     const bool s4 = e->n_stages <= 4;  // per-stage counts in scalar registers
 
     if (fuse) {
-      if (!s4 || (steps != 2 && steps != 4 && steps != 8))
-        return fail(KWK_ESTATE, "fused steps: 2, 4 or 8, 1-byte sweep with <= 4 stages");
+      if (!s4 || (steps != 2 && steps != 4)) return fail(KWK_ESTATE, "fused steps: 2 or 4, 1-byte sweep with <= 4 stages");
       for (uint32_t i = 0; i + 1 < steps; ++i) {
         if (!e->d_firedx[i]) return fail(KWK_ESTATE, "fused steps: buffers not allocated");
         a.firedx[i] = e->d_firedx[i];
@@ -5652,8 +5651,7 @@ static kwk_status launch_sweep(kwk_engine* e, int64_t now_ns, uint64_t seed, uin
       }
     }
 #define K8(P, D)                                                                                        \
-  (steps == 8   ? (const void*)sweep8_kernel<P, D, true, 8>                                            \
-   : steps == 4 ? (const void*)sweep8_kernel<P, D, true, 4>                                            \
+  (steps == 4   ? (const void*)sweep8_kernel<P, D, true, 4>                                            \
    : steps == 2 ? (const void*)sweep8_kernel<P, D, true, 2>                                            \
    : s4         ? (const void*)sweep8_kernel<P, D, true> : (const void*)sweep8_kernel<P, D, false>)
     const void* pk = e->fsm_kernel == 2 ? K8(true, 2) : K8(true, 1);
@@ -6123,7 +6121,7 @@ static kwk_status step_one(kwk_engine* e, int64_t now, uint64_t seed, uint64_t s
 // several steps in one sweep launch (KWK_TUNE_FUSE_STEPS): a 1-byte engine whose table writes no
 // due time (objects then step independently of the clock except through due times already
 // queued, which each step tests at its own now) and whose records are the 2-byte ones.  The steps
-// a launch takes: 8, 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
+// a launch takes: 4, 2 or 1, at most the tuning's and the call's steps left, and at most one event
 // sample per launch (ev_every 2 or 3: pairs; 1: none fused)
 static uint32_t fuse_group(const kwk_engine* e, uint32_t left, uint32_t ev_every) {
   if (e->fuse_steps < 2 || !e->fmt.byte || e->n_stages > 4 || e->fsm8_due_any || !e->loaded_table || ev_every == 1)

@@ -401,30 +401,30 @@ def test_step_n_equals_per_step_calls():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_nodes", [20_000, 250_000])
 def test_fused_step_pairs_equal_per_step_calls(n_nodes):
-    """KWK_TUNE_FUSE_STEPS (8 here; default 4): kwk_step_n sweeps the 1-byte ids up to eight steps per launch
+    """KWK_TUNE_FUSE_STEPS (default 4): kwk_step_n sweeps the 1-byte ids up to four steps per launch
     (sweep8_kernel<..., kSteps>: each id read once, stepped in LDS, written once; each step's
     records to its own segments, each hand-back in turn).  States, the last fired list, the fired /
     matched / per-stage counts and the step count must equal the per-step kwk_step +
     kwk_fired_compact calls — one-tile grid (2M pods) and persistent grid (25M pods); groups of
-    eight, pairs (event samples every 2nd step cap a launch at two steps) and single steps; the
+    four, pairs (event samples every 2nd step cap a launch at two steps) and single steps; the
     fused launches read and write the ids once."""
     from kwok_amd.host import abi
     engines = {"calls": _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 0})[1]}
-    engines["fused"] = _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 8})[1]
-    engines["fused_ev"] = _pods("auto", n_nodes=n_nodes, tuning={abi.TUNE_FUSE_STEPS: 8})[1]
+    engines["fused"] = _pods("auto", n_nodes=n_nodes)[1]
+    engines["fused_ev"] = _pods("auto", n_nodes=n_nodes)[1]
     try:
         now0, dt, seed = 1_700_000_000 * 10**9, 10**9, 0x6B776F6B
         ref = engines["calls"]
-        for k in range(11):
+        for k in range(7):
             ref.step(now0 + k * dt, seed, k)
             ref.fired_compact()
         assert ref.last_sweep()["kernel"] == abi.SWEEP_8
         f = engines["fused"]
         f.step_n(3, now0, dt, seed, 0)
-        f.step_n(8, now0 + 3 * dt, dt, seed, 3)
-        assert f.last_sweep()["steps"] == 8  # the second call's eight steps: one launch
-        engines["fused_ev"].step_n(11, now0, dt, seed, 0, True, 2, 0)
-        assert engines["fused_ev"].last_sweep()["steps"] == 1  # samples every 2nd step: 5 pairs, then step 10
+        f.step_n(4, now0 + 3 * dt, dt, seed, 3)
+        assert f.last_sweep()["steps"] == 4  # the second call's four steps: one launch
+        engines["fused_ev"].step_n(7, now0, dt, seed, 0, True, 2, 0)
+        assert engines["fused_ev"].last_sweep()["steps"] == 1  # samples every 2nd step: 3 pairs, then step 6
         r_hot, _ = ref.read()
         r_fired = _fired_key(ref.fired())
         r_st = ref.stats()
@@ -594,14 +594,14 @@ def test_fused_call_every_step_list_equals_per_step_calls(n_nodes, mode):
         assert f.stats()["fired"] == ref.stats()["fired"]
         if mode == "16":
             assert np.array_equal(f.fired_packed16()[0], exp[9][0])
-        # the smallest ring (a fused launch's 8 steps; kwk_fired_keep(4) keeps 8) holds the last 8 compactions only
+        # a 4-deep ring holds the last 4 compactions only
         f.fired_keep(4)
         f.step_n(10, now0 + 10 * dt, dt, seed, 10, compact)
-        for k in range(12, 20):
-            f.fetch_step(k, *bufs[k - 12])
+        for k in (16, 17, 18, 19):
+            f.fetch_step(k, *bufs[k - 16])
         f.fetch_wait()
-        with pytest.raises(abi.EngineError, match="no kept list of step 11"):
-            f.fetch_step(11, *bufs[8])
+        with pytest.raises(abi.EngineError, match="no kept list of step 15"):
+            f.fetch_step(15, *bufs[4])
     finally:
         for e in (ref, f):
             e.close()
