@@ -4228,51 +4228,121 @@ static void launch_count(uint32_t n_masks, dim3 g, hipStream_t s, const void* st
 }
 
 // kwk_aggregate's tail in one launch (was count_total + usage_total + agg_pack: two launch gaps
-// fewer per report): the mask counts' partial rows summed (n_cblocks = 0: counts already final),
-// the usage kernel's block partials summed into cluster (usage), then the packed output
+// fewer per report): the sweeps' per-stage statistics rows, the mask counts' partial rows
+// (n_cblocks = 0: counts already final) and the usage kernel's block partials (usage 1; 2: no usage
+// kernel ran, the cluster sums are packed as they stand), then the packed output.  The three sums
+// run side by side on their own waves (0-3 statistics, 4-11 counts, 12-15 usage), each with its
+// loads in flight together, then one barrier (round 6: the three one after the other, each a load
+// round trip and a barrier tree, took 10.1 us per launch at the 125k-node shard, r6ab — on the
+// pod chain once per report)
 __global__ __launch_bounds__(1024) void agg_final_kernel(const uint32_t* __restrict__ cpart, uint32_t n_cblocks,
                                                          uint32_t n_masks, unsigned long long* __restrict__ counts,
                                                          const double* __restrict__ upart, uint32_t n_ublocks,
                                                          double* __restrict__ cluster, uint32_t usage,
                                                          const unsigned long long* __restrict__ cum, uint32_t cum_rows,
                                                          uint32_t n_stages, double* __restrict__ out) {
-  __shared__ unsigned long long s[1024];
-  __shared__ double s_clu[2];
+  constexpr uint32_t kCW = 8, kUW = 4;   // count / usage waves
+  constexpr uint32_t kRows = kCW * 64 / kMaxCountMasks;  // count rows summed in parallel
   __shared__ unsigned long long s_st[KWK_MAX_STAGES];
-  const uint32_t t = threadIdx.x;
-  // per-stage transitions: the sweeps' statistics rows summed here (reduce_stats_kernel's words
-  // 3 + stage, without its launch)
+  __shared__ unsigned long long s_cnt[kCW][kMaxCountMasks];
+  __shared__ double s_u[kUW][2];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   if (t < KWK_MAX_STAGES) s_st[t] = 0;
   __syncthreads();
-  for (uint32_t s0 = 0; s0 < n_stages; s0 += 8) {  // uniform: up to 8 stages' words of a row in one pass
-    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t r = t; r < cum_rows; r += blockDim.x) {
-      const unsigned long long* __restrict__ row = cum + (uint64_t)r * kStatWords + 3 + s0;
+  if (wave < 4) {
+    // per-stage transitions: rows u, u + 256, ... of 8 stage words at a time, 4 rows in flight
+    const uint32_t u = t;
+    for (uint32_t s0 = 0; s0 < n_stages; s0 += 8) {  // uniform
+      unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t r0 = u; r0 < cum_rows; r0 += 4 * 256u) {
+        unsigned long long x[4][8];
 #pragma unroll
-      for (uint32_t j = 0; j < 8; ++j)
-        if (s0 + j < n_stages) v[j] += row[j];
-    }
+        for (uint32_t q = 0; q < 4; ++q) {
+          const uint32_t r = r0 + q * 256u;
+          const unsigned long long* __restrict__ row = cum + (uint64_t)r * kStatWords + 3 + s0;
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-      if (s0 + j >= n_stages) break;
-      for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
-      if ((t & 63) == 0 && v[j]) atomicAdd(&s_st[s0 + j], v[j]);
+          for (uint32_t j = 0; j < 8; ++j) x[q][j] = (r < cum_rows && s0 + j < n_stages) ? row[j] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) v[j] += x[q][j];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        if (s0 + j >= n_stages) break;
+        for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
+        if (lane == 0 && v[j]) atomicAdd(&s_st[s0 + j], v[j]);
+      }
     }
-  }
-  if (n_cblocks) count_total_block(cpart, n_cblocks, n_masks, counts, s);
-  // usage: 1 = sum the usage kernel's partials, 2 = no usage kernel ran (no nodes): pack the
-  // cluster sums as they stand
-  if (usage == 1 && usage_total_block(upart, n_ublocks, cluster)) {
-    s_clu[0] = cluster[0];
-    s_clu[1] = cluster[1];
-  } else if (usage == 2 && t == 0) {
-    s_clu[0] = cluster[0];
-    s_clu[1] = cluster[1];
+  } else if (wave < 4 + kCW) {
+    // the mask counts' partial rows: lane m = mask, 16 rows in flight per thread
+    const uint32_t u = t - 256u, m = u & (kMaxCountMasks - 1u), cr = u / kMaxCountMasks;
+    unsigned long long c = 0;
+    for (uint32_t b = cr; b < n_cblocks; b += 16 * kRows) {
+      uint32_t cv[16];
+#pragma unroll
+      for (uint32_t q = 0; q < 16; ++q) {
+        const uint32_t bb = b + q * kRows;
+        cv[q] = bb < n_cblocks ? cpart[(uint64_t)bb * kMaxCountMasks + m] : 0u;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 16; ++q) c += cv[q];
+    }
+    c += __shfl_xor(c, 16);  // lanes 16 apart hold the same mask
+    c += __shfl_xor(c, 32);
+    if (lane < kMaxCountMasks) s_cnt[wave - 4][lane] = c;
+  } else if (usage == 1) {
+    // the usage kernel's block partials, 8 in flight per thread
+    const uint32_t u = t - 768u;
+    double uc = 0, um = 0;
+    for (uint32_t b0 = u; b0 < n_ublocks; b0 += 8 * 256u) {
+      double2 x[8];
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t b = b0 + q * 256u;
+        x[q] = b < n_ublocks ? make_double2(upart[b * 2], upart[b * 2 + 1]) : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
+        uc += x[q].x;
+        um += x[q].y;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      uc += __shfl_xor(uc, o);
+      um += __shfl_xor(um, o);
+    }
+    if (lane == 0) {
+      s_u[wave - 12][0] = uc;
+      s_u[wave - 12][1] = um;
+    }
   }
   __syncthreads();
-  if (t < n_stages) out[t] = (double)s_st[t];
-  else if (t < n_stages + n_masks) out[t] = (double)(n_cblocks ? s[t - n_stages] : counts[t - n_stages]);
-  else if (usage && t < n_stages + n_masks + 2) out[t] = s_clu[t - n_stages - n_masks];
+  if (t < n_stages) {
+    out[t] = (double)s_st[t];
+  } else if (t < n_stages + n_masks) {
+    const uint32_t k = t - n_stages;
+    if (n_cblocks) {
+      unsigned long long sum = 0;
+      for (uint32_t w = 0; w < kCW; ++w) sum += s_cnt[w][k];
+      counts[k] = sum;
+      out[t] = (double)sum;
+    } else {
+      out[t] = (double)counts[k];
+    }
+  } else if (usage && t < n_stages + n_masks + 2) {
+    const uint32_t k = t - n_stages - n_masks;
+    double x;
+    if (usage == 1) {
+      x = 0;
+      for (uint32_t w = 0; w < kUW; ++w) x += s_u[w][k];
+      cluster[k] = x;
+    } else {
+      x = cluster[k];
+    }
+    out[t] = x;
+  }
 }
 
 // ------------------------------------------------------------------ node leases
