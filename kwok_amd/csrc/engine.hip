@@ -2383,7 +2383,7 @@ __device__ __forceinline__ void store_out(const CompactArgs& a, uint32_t at, uin
 // dispatch rounds of a ~3.5 us load chain (21 us); four per wave keep every wave resident.
 // kPacked: 4-byte records (kwk_fired_packed) instead of kwk_fired_rec — half the bytes written
 constexpr uint32_t kCompactSpw = 4;
-constexpr uint32_t kCompact16Spw = 4;  // segments per wave of the 2-byte compaction
+constexpr uint32_t kCompact16Spw = 8;  // segments per wave of the 2-byte compaction (4 before round 6: C5 1.83 -> 1.90-1.92e11, r6af)
 template <int kRec, bool kPacked = false, uint32_t kSpw = 1>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   constexpr int kPre = 4;
