@@ -615,8 +615,21 @@ struct SegIter {
   }
 };
 
+// merge16 with the byte masks from two LDS tables: bytes >= lo (mlo[lo]) and bytes < hi (mhi[hi])
+__device__ __forceinline__ void merge16_lut(uint32_t (&x)[4], const uint32_t (&y)[4], uint32_t lo, uint32_t hi,
+                                            uint32_t mlo, uint32_t mhi) {
+  const u32x4 a = *(const __attribute__((address_space(3))) u32x4*)(size_t)(mlo + 16u * lo);
+  const u32x4 b = *(const __attribute__((address_space(3))) u32x4*)(size_t)(mhi + 16u * hi);
+  const uint32_t m0 = a.x & b.x, m1 = a.y & b.y, m2 = a.z & b.z, m3 = a.w & b.w;
+  x[0] = __builtin_amdgcn_bitop3_b32(y[0], x[0], m0, 0xe4);  // m ? y : x, bit by bit
+  x[1] = __builtin_amdgcn_bitop3_b32(y[1], x[1], m1, 0xe4);
+  x[2] = __builtin_amdgcn_bitop3_b32(y[2], x[2], m2, 0xe4);
+  x[3] = __builtin_amdgcn_bitop3_b32(y[3], x[3], m3, 0xe4);
+}
+
 // the 16-byte chunks of the line at L, gathered from the segments overlapping them
-__device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (&buf)[kLineChunks][4]) {
+__device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (&buf)[kLineChunks][4], uint32_t mlo,
+                                             uint32_t mhi) {
 #pragma unroll
   for (uint32_t i = 0; i < kLineChunks; ++i) {
     const uint32_t P = L + 16u * i;
@@ -625,7 +638,7 @@ __device__ __forceinline__ void produce_line(SegIter& it, uint32_t L, uint32_t (
       if (it.sb > P) {
         uint32_t y[4], x[4] = {x0, x1, x2, x3};
         lds_load16(it.src + P - it.sa, y);  // (bytes before the segment are masked out)
-        merge16(x, y, it.sa > P ? it.sa - P : 0u, min(it.sb - P, 16u));
+        merge16_lut(x, y, it.sa > P ? it.sa - P : 0u, min(it.sb - P, 16u), mlo, mhi);
         x0 = x[0];
         x1 = x[1];
         x2 = x[2];
@@ -669,6 +682,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kChunk ?
   __shared__ uint32_t s_wi[kWaves];
   __shared__ unsigned long long s_wb[kWaves];
   __shared__ uint32_t s_now[kNowWords];
+  __shared__ uint4 s_mlo[kChunk ? 17 : 1], s_mhi[kChunk ? 17 : 1];  // merge16_lut's byte masks
   const uint32_t n = min(*a.count, a.max_recs), n_tiles = (n + kTile - 1) / kTile;
   const unsigned long long tot_i = a.totals[0], tot_b = a.totals[1];
   if (tot_i > a.cap_items || tot_b > a.cap_bytes || a.totals[2]) return;  // KWK_ECAP: nothing is written
@@ -682,6 +696,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kChunk ?
   const Tables T = stage_tables<kLds, !kChunk>(a, s_pieces, s_lits, s_sksz);
   __syncthreads();  // s_skels, s_now
   const kwk_emit_skel* skels = kLds ? s_skels : a.p.skels;
+  if constexpr (kChunk) {
+    if (threadIdx.x < 34u) {  // mlo[t]: bytes >= t; mhi[t]: bytes < t
+      const uint32_t t = threadIdx.x % 17u;
+      uint32_t m[4];
+      for (uint32_t k = 0; k < 4u; ++k) {
+        m[k] = 0;
+        for (uint32_t b = 0; b < 4u; ++b) {
+          const uint32_t byte = 4u * k + b;
+          if (threadIdx.x < 17u ? byte >= t : byte < t) m[k] |= 0xFFu << (8u * b);
+        }
+      }
+      (threadIdx.x < 17u ? s_mlo : s_mhi)[t] = make_uint4(m[0], m[1], m[2], m[3]);
+    }
+  }
   if constexpr (kChunk) {  // render every skeleton into its template (Now filled in) and its segment list
     const uint32_t ns = a.p.n_skels;
     for (uint32_t q = threadIdx.x; q < a.p.n_pieces; q += kBlock) s_pofs[q] = 0xFFFFu;  // pieces of no skeleton
@@ -824,17 +852,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kChunk ?
         if (head || L1 < g1) it.next();  // (a lane with no line to write never walks the records after it)
         uint32_t buf[kLineChunks][4];
         if (head) {
-          produce_line(it, L0, buf);
+          produce_line(it, L0, buf, lds_addr(s_mlo), lds_addr(s_mhi));
           store_line_part(rs, L0, buf, g0 - L0, min(tend - L0, kLine), true);
         }
         for (uint32_t L = L1; L < g1; L += kLine) {
-          produce_line(it, L, buf);
+          produce_line(it, L, buf, lds_addr(s_mlo), lds_addr(s_mhi));
           const bool whole = L + kLine <= tend;
 #pragma unroll
           for (uint32_t i = 0; i < kLineChunks; ++i)
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{buf[i][0], buf[i][1], buf[i][2], buf[i][3]}, rs,
                                                    whole ? L + 16u * i : kOOB, 0, 0);
-          store_line_part(rs, L, buf, 0u, min(tend - L, kLine), !whole);
+          if (!whole) store_line_part(rs, L, buf, 0u, min(tend - L, kLine), true);  // the tile's last line
         }
       }
     }

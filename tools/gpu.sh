@@ -196,15 +196,34 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
           echo "$v $i $(cat $O/usage_${v}_$i.json)"
         done
       done ;;
-    abemit)  # same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>, alternating x2
+    abemit)  # same-box A/B of the patch emitter: in-tree libkwok_emit.so vs tools/ab/<so>[,<so>...], each
+             # variant first checked by tests/test_gpu_emit.py, then alternating x2
       L=kwok_amd/lib/libkwok_emit.so; cp $L $O/cur_emit.so
+      for v in ${arg//,/ }; do
+        cp tools/ab/$v $L
+        timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_emit.py \
+          > $O/emit_test_$v.log 2>&1 || { cp $O/cur_emit.so $L; tail -30 $O/emit_test_$v.log; exit 1; }
+        echo "$v: $(tail -1 $O/emit_test_$v.log)"
+      done
       for i in 1 2; do
-        for v in cur other; do
-          if [ $v = other ]; then cp tools/ab/$arg $L; else cp $O/cur_emit.so $L; fi
+        for v in cur ${arg//,/ }; do
+          if [ $v = cur ]; then cp $O/cur_emit.so $L; else cp tools/ab/$v $L; fi
           timeout -k 10 200 python -u bench.py --gpus 1 --steps 5 --warmup 3 --no-pmc --no-cpu-baseline --hbm-nodes 0 --pcie-steps 0 \
             --emit-steps 8 > $O/emit_${v}_$i.json 2> $O/emit_${v}_$i.err || { cp $O/cur_emit.so $L; tail -20 $O/emit_${v}_$i.err; exit 1; }
-          python -c "import json; e=json.load(open('$O/emit_${v}_$i.json'))['patch_emit']; print('$v', $i, e['patches_per_s'], 'us', e['avg_emit_us'])"
+          python -c "import json; e=json.load(open('$O/emit_${v}_$i.json'))['patch_emit']; print('$v', $i, e['patches_per_s'], 'us', e['avg_emit_us'], 'GBps', e['written_GBps'])"
         done
+      done
+      cp $O/cur_emit.so $L && rm -f $O/cur_emit.so ;;
+    emittrace)  # kernel trace of the emitter per variant: in-tree libkwok_emit.so and tools/ab/<so>[,<so>...]
+      TRACE
+      L=$R/kwok_amd/lib/libkwok_emit.so; cp $L $O/cur_emit.so
+      E="$R/bench.py --gpus 1 --steps 2 --warmup 2 --no-pmc --no-cpu-baseline --hbm-nodes 0 --pcie-steps 0 --emit-steps 3"
+      for v in cur ${arg//,/ }; do
+        if [ $v = cur ]; then cp $O/cur_emit.so $L; else cp $R/tools/ab/$v $L; fi
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/et_$v -o run -- python3 $E > $O/et_$v.json 2> $O/et_$v.err \
+          || { cp $O/cur_emit.so $L; tail -20 $O/et_$v.err; exit 1; }
+        (cd $R && python tools/rocpd_summary.py stats $(find $O/et_$v -name '*.db' | head -1) $O/et_${v}_stats.csv) > /dev/null \
+          && echo "== $v" && grep -i emit $O/et_${v}_stats.csv | cut -c1-160
       done
       cp $O/cur_emit.so $L && rm -f $O/cur_emit.so ;;
     variants)
