@@ -20,7 +20,7 @@ from kwok_amd import workload as W
 pytestmark = pytest.mark.gpu
 
 
-def _run(cl, steps, dt_ns, seed):
+def _run(cl, steps, dt_ns, seed, room=0):
     from kwok_amd.host import emit
     from kwok_amd.host.compiler import KindProgram
     from kwok_amd.host.controller import KindController
@@ -43,6 +43,8 @@ def _run(cl, steps, dt_ns, seed):
     ep = emit.EmitProgram(prog.stages, ctl.patcher, reps, len(prog.class_ids))
     em = emit.Emitter(eng, len(objs), ep)
     counts = collections.Counter()
+    if room:  # reserved up front for every record's worst case (no re-emit after KWK_ECAP)
+        em.reserve(len(objs) * 16, len(objs) * room)
     try:
         words, cols = ep.rows(ctl.objs, classes)
         em.set_rows(0, words, cols)
@@ -97,7 +99,7 @@ def _run(cl, steps, dt_ns, seed):
         eng.close()
 
 
-def _big_stage_run(steps):
+def _big_stage_run(steps, room=0):
     """Patches longer than the emitter's per-wave LDS window (6 KiB): the staged writer sends such a
     record straight to global memory; a short second stage keeps the windows in use around it."""
     from kwok_amd.host import emit
@@ -133,6 +135,8 @@ def _big_stage_run(steps):
     ep = emit.EmitProgram(prog.stages, ctl.patcher, {classes[0]: ctl.objs[0]}, len(prog.class_ids))
     em = emit.Emitter(eng, len(objs), ep)
     n_dev = 0
+    if room:
+        em.reserve(len(objs) * 16, len(objs) * room)
     try:
         w, cc = ep.rows(ctl.objs, classes)
         em.set_rows(0, w, cc)
@@ -160,6 +164,19 @@ def _big_stage_run(steps):
 
 def test_gpu_emit_records_larger_than_the_window():
     assert _big_stage_run(steps=4) >= 6000
+
+
+def test_gpu_emit_reserved_records_larger_than_the_window():
+    assert _big_stage_run(steps=4, room=16384) >= 6000
+
+
+def test_gpu_emit_reserved_c2_pod_general_equals_native_render():
+    """Room reserved up front for every record's worst case (the first kwk_emit of each step
+    succeeds): the same bytes, items, offsets and guard words.  C2 at 40k pods: a list of many
+    tiles, records of mixed lengths, items left to the host."""
+    cl = W.make_cluster("C2", 300, 40000, seed=94)
+    c = _run(cl, steps=6, dt_ns=500 * 10**6, seed=0x94, room=8192)
+    assert c["device"] >= 10000, c
 
 
 def test_gpu_emit_c2_pod_general_equals_native_render():
