@@ -226,6 +226,14 @@ h=d.get('hbm_working_set') or {};print('hbm',h.get('kernel'),h.get('avg_launch_u
           && echo "== $v" && grep -i emit $O/et_${v}_stats.csv | cut -c1-160
       done
       cp $O/cur_emit.so $L && rm -f $O/cur_emit.so ;;
+    abagg)  # same-box A/B of the reporting kernels alone (tools/agg_bench.py): in-tree engine vs tools/ab/<so>, x2
+      for i in 1 2; do
+        for v in cur $arg; do
+          L=""; [ $v != cur ] && L="--lib tools/ab/$v"
+          timeout -k 10 300 python -u tools/agg_bench.py $L > $O/agg_${v}_$i.json 2> $O/agg_${v}_$i.err || { tail -20 $O/agg_${v}_$i.err; exit 1; }
+          echo "$v $i $(tail -1 $O/agg_${v}_$i.json | cut -c1-400)"
+        done
+      done ;;
     variants)
       V=$(echo $arg | tr ',' ' ')
       timeout -k 10 600 python -u tools/variants.py build ${V//--*/} > $O/variants_build.log 2>&1 || { tail -30 $O/variants_build.log; exit 1; }
