@@ -67,7 +67,8 @@ typedef struct {
                                    (length 0xFF = unusable) */
 } kwk_emit_program;
 
-/* per slot: bits 0-15 class, 16-23 guard bits, 32-63 template accepted (bit tid) */
+/* per slot: bits 0-15 class, 16-23 guard bits, 32-63 template accepted (bit tid); bits 24-31 are
+ * reserved (the device caches the slot's value lengths there: kwk_emit_get_words returns them 0) */
 #define KWK_EMIT_WORD(cls, guards, accepted) \
   ((uint64_t)(uint16_t)(cls) | (uint64_t)(uint8_t)(guards) << 16 | (uint64_t)(uint32_t)(accepted) << 32)
 

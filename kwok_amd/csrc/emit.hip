@@ -88,6 +88,7 @@ struct EmitArgs {
   unsigned long long cap_items, cap_bytes;
   uint32_t now_len;
   char now[40];
+  uint32_t lencache;                 // words' bits 24-31 cache the value lengths (emit_lens_kernel)
 };
 
 // per skeleton (LDS, built per block for this call's Now length): x = its fixed bytes (literal runs
@@ -167,11 +168,31 @@ constexpr uint32_t kLdsCols = 2;
 struct Vals {
   const uint8_t* lds;  // [kLdsCols][kTile][16] or null
   uint32_t lr;         // the record's index in the tile
+  uint32_t lens = 0xFFu;  // the word's cached value lengths (kLenCache): column 0 | column 1 << 4; 0xFF: none
   __device__ __forceinline__ const uint8_t* row(const EmitArgs& a, uint32_t c, uint32_t slot) const {
     if (lds) return lds + ((uint64_t)c * kTile + lr) * 16u;
     return a.p.cols[c] + (uint64_t)slot * a.p.stride[c];
   }
+  // a value's length byte (0xFF: unusable), from the cache when the word holds it
+  __device__ __forceinline__ uint32_t len(const EmitArgs& a, uint32_t c, uint32_t slot) const {
+    if (lens != 0xFFu && c < 2u) return c ? lens >> 4 : lens & 15u;
+    return row(a, c, slot)[0];
+  }
 };
+
+// Cached value lengths: with at most two value columns of 16-byte rows, a slot's word keeps both
+// rows' text lengths in bits 24-31 (column 0 | column 1 << 4; 0xFF when either is unusable or both
+// are 15, i.e. "read the rows"), refreshed by the host entry points that write words or rows, so
+// that the size kernel gathers one word per record instead of the word and two rows
+__global__ void emit_lens_kernel(uint64_t* __restrict__ words, uint8_t* const* __restrict__ cols, uint32_t n_cols,
+                                 uint32_t first, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t s = (uint64_t)first + i;
+    const uint32_t l0 = n_cols > 0 ? cols[0][s * 16u] : 0u, l1 = n_cols > 1 ? cols[1][s * 16u] : 0u;
+    const uint32_t code = (l0 <= 15u && l1 <= 15u) ? (l0 | l1 << 4) : 0xFFu;
+    words[s] = (words[s] & ~(0xFFull << 24)) | (uint64_t)code << 24;
+  }
+}
 
 // bytes of skeleton k for this slot, or -1 when a value is unusable
 __device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables& T, uint32_t k, uint32_t slot,
@@ -182,7 +203,7 @@ __device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables&
     if (nv != kSkszPieces) {
       long long b = z.x & 0xFFFFFFu;
       for (uint32_t i = 0; i < nv; ++i) {
-        const uint32_t len = V.row(a, (z.y >> (8u * i)) & 0xFFu, slot)[0];
+        const uint32_t len = V.len(a, (z.y >> (8u * i)) & 0xFFu, slot);
         if (len == 0xFFu) return -1;
         b += len;
       }
@@ -197,7 +218,7 @@ __device__ __forceinline__ long long skel_bytes(const EmitArgs& a, const Tables&
     if (P.slot == 0) {
       b += a.now_len;
     } else if (P.slot != KWK_EMIT_NO_SLOT) {
-      const uint32_t len = V.row(a, P.slot - 1u, slot)[0];
+      const uint32_t len = V.len(a, P.slot - 1u, slot);
       if (len == 0xFFu) return -1;
       b += len;
     }
@@ -365,7 +386,8 @@ __global__ __launch_bounds__(kBlock) void emit_size_kernel(EmitArgs a) {
     const uint32_t r = t * kTile + threadIdx.x;
     if (r < n) {
       const Rec x = fetch(a, r);
-      const Size s = rec_size(a, T, x, x.valid ? a.words[x.slot] : 0ull);
+      const uint64_t w = x.valid ? a.words[x.slot] : 0ull;
+      const Size s = rec_size(a, T, x, w, Vals{nullptr, 0u, a.lencache ? (uint32_t)(w >> 24) & 0xFFu : 0xFFu});
       it = s.items;
       by = s.bytes;
     }
@@ -907,6 +929,7 @@ struct kwk_emitter {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool emitted = false;
   bool chunk_ok = false;          // skeletons own consecutive, disjoint piece ranges (the chunk writer's templates)
+  bool lencache = false;          // words' bits 24-31 cache the value lengths (emit_lens_kernel)
   uint64_t tpl_lits = 0;          // literal bytes of every skeleton's pieces
   uint32_t tpl_now_slots = 0;     // Now slots of every skeleton's pieces
 
@@ -1002,6 +1025,16 @@ kwk_status check_program(const kwk_emit_program* g) {
   return KWK_OK;
 }
 
+// the words' cached value lengths for slots [first, first + n) (after any write of words or rows)
+kwk_status refresh_lens(kwk_emitter* em, uint32_t first, uint32_t n) {
+  if (!em->lencache || !n) return KWK_OK;
+  const uint32_t blocks = std::min<uint32_t>((n + 255u) / 256u, em->cus * 16u);
+  hipLaunchKernelGGL(emit_lens_kernel, dim3(blocks), dim3(256), 0, em->stream, em->d_words, em->p.cols, em->n_columns,
+                     first, n);
+  HIP_TRY(hipGetLastError());
+  return KWK_OK;
+}
+
 kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->p.n_classes = g->n_classes;
   em->p.n_templates = g->n_templates;
@@ -1055,6 +1088,8 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   em->allocs.push_back(d);
   if (kwk_status st = fill(em, d, 0, (size_t)std::max(1u, em->capacity) * 8)) return st;  // class 0, nothing accepted: all to the host
   em->d_words = static_cast<uint64_t*>(d);
+  em->lencache = g->n_columns <= 2;
+  for (uint32_t c = 0; c < g->n_columns; ++c) em->lencache = em->lencache && g->column_stride[c] == 16u;
   em->max_tiles = (em->capacity + kTile - 1) / kTile + 1;
   HIP_TRY(hipMalloc(&d, (size_t)em->max_tiles * 4));
   em->allocs.push_back(d);
@@ -1070,6 +1105,7 @@ kwk_status emitter_init(kwk_emitter* em, const kwk_emit_program* g) {
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, em->device));
   em->grid = std::max(1u, std::min(em->max_tiles, (uint32_t)std::max(1, cus) * 8u));
   em->cus = (uint32_t)std::max(1, cus);
+  if (kwk_status st = refresh_lens(em, 0, em->capacity)) return st;
   HIP_TRY(hipEventCreate(&em->ev0));
   HIP_TRY(hipEventCreate(&em->ev1));
   return KWK_OK;
@@ -1117,7 +1153,8 @@ kwk_status kwk_emit_set_words(kwk_emitter* em, uint32_t first, uint32_t n, const
   if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
   if (kwk_status st = bind(em)) return st;
-  return copy_in(em, em->d_words + first, words, (size_t)n * 8);
+  if (kwk_status st = copy_in(em, em->d_words + first, words, (size_t)n * 8)) return st;
+  return refresh_lens(em, first, n);
 }
 
 kwk_status kwk_emit_get_words(kwk_emitter* em, uint32_t first, uint32_t n, uint64_t* words) {
@@ -1125,7 +1162,9 @@ kwk_status kwk_emit_get_words(kwk_emitter* em, uint32_t first, uint32_t n, uint6
   if (!em || (n && !words)) return fail(KWK_EINVAL, "null argument");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
   if (kwk_status st = bind(em)) return st;
-  return copy_out(em, words, em->d_words + first, (size_t)n * 8);
+  if (kwk_status st = copy_out(em, words, em->d_words + first, (size_t)n * 8)) return st;
+  for (uint32_t i = 0; i < n; ++i) words[i] &= ~(0xFFull << 24);  // (the device's length cache)
+  return KWK_OK;
 }
 
 kwk_status kwk_emit_set_column(kwk_emitter* em, uint32_t c, uint32_t first, uint32_t n, const uint8_t* data) {
@@ -1134,7 +1173,8 @@ kwk_status kwk_emit_set_column(kwk_emitter* em, uint32_t c, uint32_t first, uint
   if (c >= em->n_columns) return fail(KWK_EINVAL, "column out of range");
   if ((uint64_t)first + n > em->capacity) return fail(KWK_EINVAL, "rows beyond the capacity");
   if (kwk_status st = bind(em)) return st;
-  return copy_in(em, em->cols[c] + (size_t)first * em->stride[c], data, (size_t)n * em->stride[c]);
+  if (kwk_status st = copy_in(em, em->cols[c] + (size_t)first * em->stride[c], data, (size_t)n * em->stride[c])) return st;
+  return refresh_lens(em, first, n);
 }
 
 kwk_status kwk_emit_reserve(kwk_emitter* em, uint32_t max_items, uint64_t max_bytes) {
@@ -1192,6 +1232,7 @@ kwk_status kwk_emit(kwk_emitter* em, int64_t now_ns, uint32_t source) {
   a.out = em->d_out;
   a.cap_items = em->cap_items;
   a.cap_bytes = em->cap_bytes;
+  a.lencache = em->lencache ? 1u : 0u;
   const std::string now = kwkfmt::rfc3339nano(now_ns);
   if (now.size() >= sizeof a.now) return fail(KWK_EINVAL, "Now() text too long");
   memcpy(a.now, now.data(), now.size());
