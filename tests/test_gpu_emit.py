@@ -88,6 +88,8 @@ def _run(cl, steps, dt_ns, seed, room=0):
                 w, cc = ep.rows([ctl.objs[s] for s in live], [classes[s] for s in live])
                 em.set_slots(np.asarray(live), w, cc)
             dev = em.words(0, len(objs))
+            # the device's value-length cache in bits 24-31 stays internal (kwk_emit_get_words: 0)
+            assert not np.any((dev >> np.uint64(24)) & np.uint64(0xFF)), k
             for s, o in enumerate(ctl.objs):
                 if o is not None:
                     assert (int(dev[s]) >> 16) & 0xFF == ep.guard_bits(o), (k, s)
