@@ -158,6 +158,8 @@ VARIANTS = {
     # the bitmap hand-back would need its codes ranked; C5 cost isolation only)
     "s8_kmajor": [('          if (rdy) {\n            while (m) {\n              const uint32_t k = (uint32_t)__builtin_ctz(m);\n              m &= m - 1u;\n              *wp++ = (uint16_t)((ent0 ^ ((k & 7u) * 0x104u | k >> 3)) | ((ready >> k) & 1u) << 15);\n            }\n          } else {\n            while (m) {\n              const uint32_t k = (uint32_t)__builtin_ctz(m);\n              m &= m - 1u;\n              *wp++ = (uint16_t)(ent0 ^ ((k & 7u) * 0x104u | k >> 3));\n            }\n          }', "          (void)m; (void)wp;\n          uint32_t kbase = 0;\n#pragma unroll\n          for (uint32_t k = 0; k < 32u; ++k) {  // k-major: a pass's items are one k of many lanes\n            const bool b = (need >> k) & 1u;\n            const unsigned long long bal = ballot(b);\n            const uint32_t p = kbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));\n            if (b) wl[p] = (uint16_t)((ent0 ^ ((k & 7u) * 0x104u | k >> 3)) | ((ready >> k) & 1u) << 15);\n            kbase += (uint32_t)__popcll(bal);\n          }")],
     # the 2-byte scan + expansion hand-back (C5) with 4 (round 5) / 16 segments per wave instead of 8
+    "dwmb4": [("constexpr int kDwMinBlocks = 5; ", "constexpr int kDwMinBlocks = 4; ")],
+    "dwmb6": [("constexpr int kDwMinBlocks = 5; ", "constexpr int kDwMinBlocks = 6; ")],
     "ur2": [("constexpr uint32_t kUChunkRows = 4; ", "constexpr uint32_t kUChunkRows = 2; ")],
     "ur1": [("constexpr uint32_t kUChunkRows = 4; ", "constexpr uint32_t kUChunkRows = 1; ")],
     "c16s8": [("constexpr uint32_t kSmall16Spw = 4;", "constexpr uint32_t kSmall16Spw = 8;")],
