@@ -160,6 +160,8 @@ VARIANTS = {
     # the 2-byte scan + expansion hand-back (C5) with 4 (round 5) / 16 segments per wave instead of 8
     "dwmb4": [("constexpr int kDwMinBlocks = 5; ", "constexpr int kDwMinBlocks = 4; ")],
     "dwmb6": [("constexpr int kDwMinBlocks = 5; ", "constexpr int kDwMinBlocks = 6; ")],
+    "ucu16": [("    const uint32_t per_cu = 8u;", "    const uint32_t per_cu = 16u;")],
+    "ucu32": [("    const uint32_t per_cu = 8u;", "    const uint32_t per_cu = 32u;")],
     "ur2": [("constexpr uint32_t kUChunkRows = 4; ", "constexpr uint32_t kUChunkRows = 2; ")],
     "ur1": [("constexpr uint32_t kUChunkRows = 4; ", "constexpr uint32_t kUChunkRows = 1; ")],
     "c16s8": [("constexpr uint32_t kSmall16Spw = 4;", "constexpr uint32_t kSmall16Spw = 8;")],
