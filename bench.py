@@ -596,11 +596,10 @@ def main():
                     "pod engine (0: default)")
     ap.add_argument("--tune-fsm-kernel", type=int, default=-1,
                     help="diagnostic: the table-only kernel field of KWK_TUNE_SWEEP16 for the pod engine (-1: default)")
-    ap.add_argument("--tune-priority", type=int, default=0,
-                    help="0 (default): both engines' streams at the default priority; 1: the pod engine's stream at the "
-                         "device's greatest priority, the node engine's at the least (round 4, before fused pod steps: "
-                         "sweep 49.1-49.6 -> 48.3-48.5 us, r4zg; round 6 with fused steps: 1.92 vs 1.94e11 mean over six "
-                         "same-box runs each, the sampled 4-step launch 125 vs 117 us, profiles/r6/r6bg_r6bh_priority_ab.txt)")
+    ap.add_argument("--tune-priority", type=int, default=1,
+                    help="1 (default): the pod engine's stream at the device's greatest priority, the node engine's at "
+                         "the least (the node step fills in around the pod path: sweep 49.1-49.6 -> 48.3-48.5 us, r4zg; round 6: the PCIe-inclusive leg 3.9-4.0e10 vs 2.1-2.7e10 with 0, "
+                         "profiles/r6/r6bg_r6bh_priority_ab.txt); 0: both default")
     ap.add_argument("--fuse-steps", type=int, default=4, choices=(0, 1, 2, 4),
                     help="KWK_TUNE_FUSE_STEPS for the pod engine: up to 4 (default) or 2 steps per 1-byte sweep "
                          "launch, 0 / 1 one step per launch")
